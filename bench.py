@@ -1,0 +1,229 @@
+"""Benchmark: two-tower DSSM training samples/sec on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--batch 4096]
+    torchrun --nproc-per-node N bench.py --gpus N ...       (one process per GPU, RCCL)
+
+Workload (BASELINE.json configs[1]): MovieLens-1M-schema DSSM + Transformer sequence encoder,
+seq_len 50, d_model 64, per-GPU batch 4096, dropout as configured, temperature from the config,
+Adam + clip_grad_norm_(1.0). Synthetic MovieLens-shaped batches (synth.py), resident in HBM
+before timing. A "step" = zero_grad + forward + in-batch loss + backward + [RCCL all-reduce]
++ clip + Adam, captured as two hipGraphs (fwd/bwd, optimizer) and replayed.
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import yaml
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from recommendsystemproject_amd import dist as rdist  # noqa: E402
+from recommendsystemproject_amd import synth  # noqa: E402
+from recommendsystemproject_amd.flat import ensure_flat  # noqa: E402
+from recommendsystemproject_amd.optim import Adam  # noqa: E402
+from recommendsystemproject_amd.profiling import KernelTimer  # noqa: E402
+from recommendsystemproject_amd.project.models.TwoTower.GenericTower import GenericTower  # noqa: E402
+from recommendsystemproject_amd.project.models.TwoTower.TwoTowerModel import TwoTowerModel  # noqa: E402
+from recommendsystemproject_amd.project.utils.training_utils import extract_item_id  # noqa: E402
+
+PEAK_F32_TFLOPS = 157.3   # MI355X f32 (vector = f32-input MFMA) peak, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0     # HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--config', default='c2')
+    ap.add_argument('--batch', type=int, default=None, help='per-GPU batch (default: config)')
+    ap.add_argument('--dropout', default='config', choices=['config', '0'])
+    ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--cpu-baseline-seconds', type=float, default=15.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, seconds):
+    """The oracle (CPU restatement of the reference step, fp32) on a bounded sample."""
+    from oracle.twotower_oracle import OracleTrainer, model_state_shapes
+    maps = {'user': synth.tower_layout(cfg['two_tower']['user_tower']),
+            'item': synth.tower_layout(cfg['two_tower']['item_tower'])}
+    shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
+    tr = OracleTrainer(cfg, synth.make_state(shapes, seed=1), lr=cfg['train']['learning_rate'], dropout=None)
+    B = 256
+    batches = [synth.batch_to_torch(synth.make_batch(cfg, B, seed=900 + i)) for i in range(2)]
+    T = cfg['train']['temperature']
+    tr.step(batches[0], maps, temperature=T)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        tr.step(batches[n % 2], maps, temperature=T)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 200:
+            break
+    return {'value': round(n * B / el, 1), 'unit': 'samples/s', 'cores': torch.get_num_threads(),
+            'kind': 'port', 'sample': f'{n} steps x batch {B} of the same config (oracle, fp32, '
+                                      f'dropout as configured), {el:.1f} s'}
+
+
+def main():
+    args = parse()
+    rdist.init_from_env()
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dev = torch.device(f'cuda:{local}')
+    torch.cuda.set_device(dev)
+
+    cfg = yaml.safe_load(open(os.path.join(ROOT, 'configs', f'{args.config}.yaml')))
+    if args.dropout == '0':
+        for t in cfg['two_tower'].values():
+            t['dropout'] = 0.0
+            t.get('transformer_parameters', {})['dropout'] = 0.0
+    B = args.batch or int(cfg['train']['batch_size'])
+    T = float(cfg['train']['temperature'])
+    maps = {'user': synth.tower_layout(cfg['two_tower']['user_tower']),
+            'item': synth.tower_layout(cfg['two_tower']['item_tower'])}
+
+    torch.manual_seed(0)
+    model = TwoTowerModel(GenericTower(cfg, 'user_tower'), GenericTower(cfg, 'item_tower'),
+                          maps['user'], maps['item']).to(dev)
+    model.train()
+    ensure_flat(model)
+    rdist.broadcast_model(model)
+    opt = Adam(model.parameters(), lr=float(cfg['train']['learning_rate']))
+    opt.grad_scale = 1.0 / world
+    batch = synth.batch_to_torch(synth.make_batch(cfg, B, seed=1000 + rank), dev)  # resident in HBM
+    ids = extract_item_id(batch['item_tower'])
+
+    def fwd_bwd():
+        opt.zero_grad()
+        U, I, H = model(batch)
+        loss = model.compute_loss(U, I, item_ids=ids, hard_neg_emb=H, temperature=T)
+        loss.backward()
+        return loss
+
+    def opt_step():
+        opt.step(clip_max_norm=1.0)
+
+    def allreduce():
+        if world > 1:
+            rdist.allreduce_gradients(model, opt)
+
+    # eager warm-up (also allocates Adam state), then capture
+    for _ in range(max(2, min(args.warmup, 3))):
+        fwd_bwd()
+        allreduce()
+        opt_step()
+    torch.cuda.synchronize()
+    graphs = None
+    if not args.no_graph:
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                fwd_bwd()
+                allreduce()
+                opt_step()
+            torch.cuda.current_stream().wait_stream(s)
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                loss_static = fwd_bwd()
+            with torch.cuda.graph(g2):
+                opt_step()
+            graphs = (g1, g2, loss_static)
+        except Exception as e:  # eager fallback keeps the same kernels
+            print(f'[bench] graph capture failed ({e!r}); running eagerly', file=sys.stderr)
+            graphs = None
+
+    def step():
+        if graphs is not None:
+            graphs[0].replay()
+            allreduce()
+            graphs[1].replay()
+            return graphs[2]
+        loss = fwd_bwd()
+        allreduce()
+        opt_step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    el_t = torch.tensor([el], device=dev)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t.item())
+    final_loss = float(loss.item())
+
+    # roofline of the dominant kernel: HIP events on the launch stream, eager instrumented steps
+    with KernelTimer() as kt:
+        for _ in range(3):
+            fwd_bwd()
+            allreduce()
+            opt_step()
+    summ = kt.summary()
+    dom_name, dom = max(summ.items(), key=lambda kv: kv[1]['ms'])
+    flop_bound = dom['flops'] / max(dom['bytes'], 1.0) > PEAK_F32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+    avg_ms = dom['ms'] / dom['launches']
+    if flop_bound:
+        achieved = dom['flops'] / dom['launches'] / (avg_ms * 1e-3) / 1e12
+        roof = {'bound': 'mfma', 'achieved': round(achieved, 3), 'peak': PEAK_F32_TFLOPS, 'unit': 'TFLOP/s'}
+    else:
+        achieved = dom['bytes'] / dom['launches'] / (avg_ms * 1e-3) / 1e9
+        roof = {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s'}
+    roof['frac'] = round(roof['achieved'] / roof['peak'], 4)
+    roof['traffic'] = None
+    roof['kernel'] = dom_name
+    roof['avg_launch_ms'] = round(avg_ms, 4)
+    roof['share_of_step'] = round(dom['ms'] / sum(v['ms'] for v in summ.values()), 3)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, args.cpu_baseline_seconds)
+
+    if rank == 0:
+        samples = world * B * args.steps
+        tp = cfg['two_tower']['user_tower'].get('transformer_parameters', {})
+        has_seq = bool(cfg['two_tower']['user_tower'].get('sequence_features'))
+        out = {
+            'metric': 'training samples/sec (user-item pairs) at batch 4096; 1/2/4/8 MI355X',
+            'value': round(samples / el, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 3),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
+            'data': 'synthetic (MovieLens-1M-shaped ids, seeded numpy PCG64, resident in HBM)',
+            'config': {'workload': f'{args.config}: MovieLens-1M DSSM' +
+                       (f' + Transformer seq encoder (seq_len {tp.get("max_seq_len")}, d={cfg["two_tower"]["user_tower"]["embedding_dim"]})' if has_seq else ''),
+                       'global_batch': world * B, 'per_gpu_batch': B,
+                       'seq_len': tp.get('max_seq_len') if has_seq else None,
+                       'dropout': args.dropout, 'parallelism': f'dp{world}',
+                       'hip_graph': graphs is not None, 'final_loss': round(final_loss, 5)},
+            'roofline': roof,
+            'cpu_baseline': cpu,
+            'kernel_ms_per_step': {k: round(v['ms'] / 3, 4) for k, v in sorted(summ.items(), key=lambda kv: -kv[1]['ms'])},
+        }
+        print(json.dumps(out))
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

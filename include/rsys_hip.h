@@ -1,0 +1,210 @@
+/*
+ * rsys_hip.h — C ABI of librsys_hip.so, the MI355X (gfx950) hot path of the two-tower DSSM
+ * training step (feature gather, Transformer encoder, MLP towers, in-batch softmax loss,
+ * clip + Adam). Every entry point replaces an ATen op the reference reaches through the
+ * nn.Module API in project/models/TwoTower/ (file:line cited per function).
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; every pointer is DEVICE memory unless stated otherwise.
+ *     The caller owns all memory (tensors and workspaces); the library never allocates or frees.
+ *   - `stream` is a hipStream_t passed as void*; all work is enqueued on it, no implicit sync.
+ *     Every entry point is graph-capturable (no alloc/sync/memcpy inside).
+ *   - Return 0 on success, <0 for a bad argument (message in rs_last_error()), >0 a hipError_t.
+ *   - fp32 data, int64 ids (the reference's torch.long batches, DataLoader.py:259,287).
+ */
+#ifndef RSYS_HIP_H
+#define RSYS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- library */
+int rs_version(void);                 /* ABI version (integer, bumps on signature change) */
+const char* rs_last_error(void);      /* thread-local message of the last failing call */
+int rs_device_check(void);            /* 0 if a gfx950 device is current, else hipError / -1 */
+
+/* ---------------------------------------------------------------- GEMM (fp32 MFMA)
+ * C = epi(alpha * op(A) @ op(B))  with op(A)[m,k] = transA ? A[k*lda+m] : A[m*lda+k],
+ * op(B)[k,n] = transB ? B[n*ldb+k] : B[k*ldb+n]. Epilogue flags (bitwise):
+ *   RS_EPI_BIAS    v += bias[n]
+ *   RS_EPI_AUX_ADD v += aux[(m % aux_mod)*ld_aux + n]      (residual / positional rows)
+ *   RS_EPI_AUX_MASK v = aux[m*ld_aux+n] > 0 ? v : 0         (ReLU backward)
+ *   RS_EPI_RELU    v = max(v, 0)   (applied last)
+ *   beta != 0      v += beta * C_old   (applied before RELU)
+ * split_k > 1 needs ws of split_k*M*N floats (rs_gemm_ws_bytes).
+ * Replaces nn.Linear / addmm / matmul / bmm on the hot path: Tower.py:16-25,
+ * SequenceFeatureProcessor.py:77, TransformerEncoderLayer in/out_proj + linear1/2
+ * (SequenceEncoder.py:17-23), TwoTowerModel.py:95 (U @ I^T) and all their backwards. */
+#define RS_EPI_BIAS 1
+#define RS_EPI_RELU 2
+#define RS_EPI_AUX_ADD 4
+#define RS_EPI_AUX_MASK 8
+int rs_gemm_auto_split(int M, int N, int K);   /* split_k that fills the chip for long K */
+int64_t rs_gemm_ws_bytes(int M, int N, int K, int split_k);
+int rs_gemm_f32(int transA, int transB, int M, int N, int K, float alpha,
+                const float* A, int lda, const float* B, int ldb, float beta, float* C, int ldc,
+                int epilogue, const float* bias, const float* aux, int ld_aux, int aux_mod,
+                int split_k, float* ws, void* stream);
+
+/* ---------------------------------------------------------------- column reductions
+ * out[n] = beta*out[n] + scale * sum_{m<M} X[m*ldx + n]   (bias / pos-emb / LN grads)
+ * ws: rs_colsum_ws_bytes(M, N) bytes. */
+int64_t rs_colsum_ws_bytes(int M, int N);
+int rs_colsum(const float* X, int M, int N, int ldx, float scale, float beta, float* out,
+              float* ws, void* stream);
+
+/* ---------------------------------------------------------------- feature gather
+ * Descriptor-driven multi-table gather into a row-major concat buffer out[rows, ldo].
+ * One segment per feature (kind: 0 single sparse id, 1 pooled bag, 2 dense Linear(1,D),
+ * 3 last-valid row of a [rows*L, D] sequence, 4 plain [rows, D] slice copy). Segments are
+ * passed by value into the kernel arguments (at most 24 per call). Replaces GenericTower.forward feature loop (GenericTower.py:133-233,
+ * K1/K2/K11 + torch.cat), SequenceFeatureProcessor.forward gather/tag-pool/cat
+ * (SequenceFeatureProcessor.py:57-76, K3) and SequenceEncoder._gather_last_valid
+ * (SequenceEncoder.py:58-74, K10). Segment layout: rs_feature_seg_t below. */
+#define RS_SEG_SPARSE 0
+#define RS_SEG_POOL 1
+#define RS_SEG_DENSE 2
+#define RS_SEG_LASTVALID 3
+#define RS_SEG_COPY 4
+#define RS_POOL_MEAN 0
+#define RS_POOL_SUM 1
+#define RS_POOL_MAX 2
+typedef struct rs_feature_seg {
+  int kind;               /* RS_SEG_* */
+  int dim;                /* D: output columns of this segment */
+  int out_col;            /* first column in the concat buffer */
+  int pool_mode;          /* RS_POOL_* (kind 1) */
+  int bag;                /* kind 1: ids per row; kind 3: L (rows per sample in src) */
+  int pad_idx;            /* row whose gradient is dropped (padding_idx); -1 none */
+  int64_t vocab;          /* table rows (bounds check) */
+  int64_t idx_stride;     /* elements between consecutive rows' ids (kind 0/1), x (kind 2) */
+  const int64_t* idx;     /* kind 0/1 ids; kind 3: int64 last-valid index per row */
+  const float* table;     /* kind 0/1 [vocab, dim]; kind 2 weight [dim]; kind 3 src [rows*bag, dim];
+                             kind 4 src [rows, dim] */
+  const float* bias;      /* kind 2 bias [dim] */
+  const float* x;         /* kind 2 input column */
+  float* grad;            /* backward destination: kind 0/1 table grad [vocab, dim];
+                             kind 2 weight grad [dim]; kind 3 src grad [rows*bag, dim] (+=);
+                             kind 4 src grad [rows, dim] (=) */
+  float* grad_bias;       /* kind 2 bias grad [dim] */
+} rs_feature_seg_t;
+
+int rs_gather_fwd(const rs_feature_seg_t* segs, int nseg, int rows, float* out, int ldo,
+                  int* err_flag, void* stream);
+/* Backward: table grads by scatter-add (padding row skipped), dense grads via column
+ * reductions (ws: rs_gather_ws_bytes), last-valid rows copied into a pre-zeroed src grad. */
+int64_t rs_gather_ws_bytes(const rs_feature_seg_t* segs_host, int nseg, int rows);
+int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, const float* dout, int ldo,
+                  float* ws, void* stream);
+
+/* ---------------------------------------------------------------- sequence mask
+ * padding mask from the first sequence feature (== pad_value) with the all-padding-row fix,
+ * and last-valid index (SequenceEncoder.py:36-46, :66-70; traps T6/T7).
+ * key_pad[b*L+l] = 1 if masked; last[b] = clamp(sum(valid)-1, 0). */
+int rs_seq_mask(const int64_t* seq, int64_t ld_seq, int B, int L, int64_t pad_value,
+                uint8_t* key_pad, int64_t* last, void* stream);
+
+/* ---------------------------------------------------------------- attention
+ * Masked multi-head self-attention core on packed qkv [B*L, 3d] (in_proj output), heads of
+ * hd = d/H columns; out [B*L, d]; lse [B*H*L] saved for backward. Replaces the SDPA math path
+ * inside nn.MultiheadAttention (SequenceEncoder.py:17-29 via TransformerEncoderLayer, K6).
+ * p > 0: dropout on the attention probabilities with the rs_dropout mask of (key, site). */
+int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out, float* lse,
+                int B, int L, int d, int H, float scale, float p, const int64_t* key, int site,
+                void* stream);
+int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float* out, const float* dout,
+                const float* lse, float* dqkv, int B, int L, int d, int H, float scale, float p,
+                const int64_t* key, int site, void* stream);
+
+/* ---------------------------------------------------------------- layer norm (post-LN)
+ * h = dropout(a) + b (written back into a), y = LN(h)*gamma + beta; mean/rstd [M] saved.
+ * Replaces norm1/norm2(x + dropout1/2(sublayer)) of TransformerEncoderLayer (K8). */
+int rs_add_layernorm_fwd(float* a, const float* b, const float* gamma, const float* beta,
+                         float* y, float* mean, float* rstd, int M, int N, float eps, float p,
+                         const int64_t* key, int site, void* stream);
+/* dh = LN backward (written to dh, may alias dy); dgamma/dbeta accumulated (+=); if da != NULL
+ * da = dropout-backward(dh) (the sublayer-branch gradient). ws: rs_layernorm_ws_bytes(M, N). */
+int64_t rs_layernorm_ws_bytes(int M, int N);
+int rs_layernorm_bwd(const float* h, const float* dy, const float* gamma, const float* mean,
+                     const float* rstd, float* dh, float* dgamma, float* dbeta, int M, int N,
+                     float* da, float p, const int64_t* key, int site, float* ws, void* stream);
+
+/* ---------------------------------------------------------------- batch norm (training)
+ * x [G*Bg, C] in G independent groups of Bg rows (hard-negative slots, T13), batch statistics,
+ * running stats updated group by group (momentum), num_batches_tracked += G, optional ReLU.
+ * mean/rstd [G*C] saved. training == 0 normalises with the running statistics (eval mode).
+ * Replaces BatchNorm1d (GenericTower.py:234, Tower.py:17; K12/K13). */
+int64_t rs_batchnorm_ws_bytes(int G, int Bg, int C);
+int rs_batchnorm_fwd(const float* x, float* y, const float* w, const float* b,
+                     float* running_mean, float* running_var, int64_t* num_batches,
+                     float* mean, float* rstd, int G, int Bg, int C, float momentum, float eps,
+                     int relu, int training, float* ws, void* stream);
+int rs_batchnorm_bwd(const float* x, const float* y, const float* dy, const float* w,
+                     const float* mean, const float* rstd, float* dx, float* dw, float* db,
+                     int G, int Bg, int C, int relu, float* ws, void* stream);
+
+/* ---------------------------------------------------------------- misc elementwise */
+/* y = x / max(||x||_2, eps) per row (F.normalize, Tower.py:41; K14); norm [M] saved */
+int rs_l2norm_fwd(const float* x, float* y, float* norm, int M, int N, float eps, void* stream);
+int rs_l2norm_bwd(const float* y, const float* norm, const float* dy, float* dx, int M, int N,
+                  float eps, void* stream);
+
+/* ---------------------------------------------------------------- in-batch softmax loss
+ * logits = S/T (S = U I^T, [B, ld_s]), off-diagonal equal-item-id collisions -> -1e9, hard
+ * negative logits U_i.H_in/T appended un-masked, cross-entropy with labels arange(B), mean.
+ * item_ids may be NULL (compute_loss(item_ids=None): no collision mask).
+ * TwoTowerModel.compute_loss (TwoTowerModel.py:81-140; trap T12; K15-K17).
+ * fwd: per-row lse [B] and the mean loss (scalar) ; bwd: S <- dlogits (in place, scaled by
+ * *grad_out / B / T so the next GEMMs need alpha 1), dhl [B, N] likewise. */
+int rs_inbatch_ce_fwd(const float* S, int ld_s, const float* U, const float* Hn,
+                      const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T,
+                      float* lse, float* row_loss, float* loss, void* stream);
+int rs_inbatch_ce_bwd(float* S, int ld_s, const float* U, const float* Hn,
+                      const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T,
+                      const float* lse, const float* grad_out, float* dhl, void* stream);
+/* dU[i] += sum_n dhl[i,n] H[i,n];  dH[i,n] = dhl[i,n] U[i]   (hard-negative bmm backward) */
+int rs_hardneg_bwd(const float* U, const float* Hn, const float* dhl, float* dU, float* dH,
+                   int B, int N, int D, void* stream);
+
+/* ---------------------------------------------------------------- clip + Adam
+ * Flat multi-tensor path over a contiguous fp32 range (all parameters packed in one buffer).
+ * rs_grad_sqnorm: partial sums of (scale*g)^2 into ws; rs_clip_coef: total norm and
+ * coef = min(1, max_norm/(norm+1e-6)) written to device scalars (clip_grad_norm_,
+ * training_utils.py:53-54; K18). rs_adam_step: torch.optim.Adam (default betas/eps, L2
+ * weight decay) on p, m, v with g*scale*(*coef) (train_twotower.py:111; K19); when
+ * write_grad != 0 the clipped gradient is stored back into g. With step_dev != NULL the bias
+ * corrections use the device step count *step_dev instead of `step`. */
+int64_t rs_sqnorm_ws_bytes(int64_t n);
+int rs_grad_sqnorm(const float* g, int64_t n, float scale, double* ws, void* stream);
+int rs_clip_coef(const double* ws, int64_t n, float max_norm, float* total_norm, float* coef,
+                 void* stream);
+int rs_scale_inplace(float* g, int64_t n, float scale, const float* coef, void* stream);
+int rs_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                 float beta2, float eps, float weight_decay, int step, const int64_t* step_dev,
+                 float scale, const float* coef, int write_grad, void* stream);
+/* *counter += delta on the stream (device-side Adam step count: replayable in a hipGraph) */
+int rs_counter_add(int64_t* counter, int64_t delta, void* stream);
+
+/* ---------------------------------------------------------------- dropout
+ * Counter-based masks: element i of site `site` is kept iff hash(key[0], key[1], site, i) >= p,
+ * kept values scaled by 1/(1-p) (nn.Dropout semantics). key = {seed, counter} in device memory;
+ * rs_rng_next copies the state into a fresh key and advances the counter (graph-replay safe).
+ * rs_dropout_fwd: x = dropout(x + aux[(i/N % aux_mod)*ld_aux + i%N])  (aux optional: the
+ * positional embedding between the two input dropouts, SequenceFeatureProcessor.py:77-83).
+ * rs_dropout_bwd: dx *= mask/(1-p). */
+int rs_rng_next(int64_t* state, int64_t* key, void* stream);
+int rs_dropout_fwd(float* x, int64_t n, int N, const float* aux, int ld_aux, int aux_mod, float p,
+                   const int64_t* key, int site, void* stream);
+int rs_dropout_bwd(float* dx, int64_t n, float p, const int64_t* key, int site, void* stream);
+
+/* ---------------------------------------------------------------- reductions */
+/* out = scale * sum(x[0..n)) (deterministic; mean loss) */
+int rs_sum(const float* x, int n, float scale, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSYS_HIP_H */

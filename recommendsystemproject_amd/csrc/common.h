@@ -1,0 +1,60 @@
+// Shared device/host helpers for librsys_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/rsys_hip.h"
+
+namespace rs {
+
+void set_error(const char* fmt, ...);
+
+// Argument check: sets the thread-local message and returns -1 from the entry point.
+#define RS_CHECK_ARG(cond, ...)        \
+  do {                                 \
+    if (!(cond)) {                     \
+      ::rs::set_error(__VA_ARGS__);    \
+      return -1;                       \
+    }                                  \
+  } while (0)
+
+// Launch-status check after a kernel launch.
+#define RS_CHECK_LAUNCH(name)                                                       \
+  do {                                                                              \
+    hipError_t e__ = hipGetLastError();                                             \
+    if (e__ != hipSuccess) {                                                        \
+      ::rs::set_error("%s: launch failed: %s", name, hipGetErrorString(e__));       \
+      return (int)e__;                                                              \
+    }                                                                               \
+  } while (0)
+
+#define RS_RET_IF(x)        \
+  do {                      \
+    int r__ = (x);          \
+    if (r__ != 0) return r__; \
+  } while (0)
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace rs

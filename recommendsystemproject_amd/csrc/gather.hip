@@ -1,0 +1,328 @@
+// Multi-table feature gather / scatter-add for the tower inputs and the per-token sequence
+// features (K1, K2, K3, K10, K11 of SURVEY.md §2.2).
+//
+// One launch covers every feature of a tower: the host turns the config into a list of
+// segments (rs_feature_seg_t) and each workgroup owns one segment x a tile of rows, so the
+// concat buffer [rows, ldo] is written directly (no torch.cat). A row of D floats is read by
+// D/4 consecutive lanes with 16-byte loads (a 128-wide row = 32 lanes = one 512 B burst), a
+// bag (pooled feature) is accumulated in registers by the same lanes, so the index and the
+// row reads stay coalesced and the HBM traffic is exactly ids + rows + output.
+//
+// Backward: dense [V, D] table gradients (the reference uses sparse=False embeddings, T16) by
+// float atomics, skipping the padding row as embedding_dense_backward does; Linear(1, D) dense
+// features by a deterministic column reduction; last-valid rows by a plain copy-add.
+#include "common.h"
+
+namespace rs {
+namespace {
+
+constexpr int kMaxSeg = 24;  // segments travel by value in the kernel arguments (~2.6 KB)
+
+struct SegLaunch {
+  rs_feature_seg_t segs[kMaxSeg];
+  int nseg;
+  int rows;
+  float* out;  // fwd: concat out; bwd: unused
+  const float* dout;
+  int ldo;
+  int* err;
+  int block_start[kMaxSeg + 1];
+  int rpb[kMaxSeg];   // rows per block
+  int chunks[kMaxSeg];  // lanes per row
+  int vec[kMaxSeg];
+};
+
+__device__ __forceinline__ int find_seg(const SegLaunch& a, int bid) {
+  int s = 0;
+  while (s + 1 < a.nseg && bid >= a.block_start[s + 1]) ++s;
+  return s;
+}
+
+__device__ __forceinline__ bool id_ok(int64_t id, int64_t vocab, int* err) {
+  if (id < 0 || id >= vocab) {
+    if (err) atomicOr(err, 1);
+    return false;
+  }
+  return true;
+}
+
+template <bool VEC>
+__device__ __forceinline__ void load_row(const float* p, float* v) {
+  if (VEC) {
+    float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+    v[0] = p[0];
+  }
+}
+
+template <bool VEC>
+__device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int row, int chunk) {
+  constexpr int W = VEC ? 4 : 1;
+  const int c = chunk * W;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float* o = a.out + (int64_t)row * a.ldo + sg.out_col + c;
+  if (sg.kind == RS_SEG_SPARSE) {
+    const int64_t id = sg.idx[(int64_t)row * sg.idx_stride];
+    if (id_ok(id, sg.vocab, a.err)) load_row<VEC>(sg.table + id * sg.dim + c, acc);
+  } else if (sg.kind == RS_SEG_POOL) {
+    const int64_t* ids = sg.idx + (int64_t)row * sg.idx_stride;
+    if (sg.pool_mode == RS_POOL_MAX) {
+#pragma unroll
+      for (int j = 0; j < W; ++j) acc[j] = -INFINITY;
+    }
+    for (int l = 0; l < sg.bag; ++l) {
+      const int64_t id = ids[l];
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (id_ok(id, sg.vocab, a.err)) load_row<VEC>(sg.table + id * sg.dim + c, v);
+      if (sg.pool_mode == RS_POOL_MAX) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) acc[j] = fmaxf(acc[j], v[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < W; ++j) acc[j] += v[j];
+      }
+    }
+    if (sg.pool_mode == RS_POOL_MEAN) {
+      const float n = (float)sg.bag;
+#pragma unroll
+      for (int j = 0; j < W; ++j) acc[j] = acc[j] / n;
+    }
+  } else if (sg.kind == RS_SEG_DENSE) {
+    const float x = sg.x[(int64_t)row * sg.idx_stride];
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc[j] = sg.bias[c + j] + x * sg.table[c + j];
+  } else if (sg.kind == RS_SEG_LASTVALID) {
+    const int64_t l = sg.idx[row];
+    load_row<VEC>(sg.table + ((int64_t)row * sg.bag + l) * sg.dim + c, acc);
+  } else {  // RS_SEG_COPY
+    load_row<VEC>(sg.table + (int64_t)row * sg.dim + c, acc);
+  }
+  if (VEC) {
+    *reinterpret_cast<float4*>(o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  } else {
+    o[0] = acc[0];
+  }
+}
+
+__global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
+  const int s = find_seg(a, blockIdx.x);
+  const rs_feature_seg_t& sg = a.segs[s];
+  const int lb = blockIdx.x - a.block_start[s];
+  const int C = a.chunks[s];
+  const int r = threadIdx.x / C, chunk = threadIdx.x % C;
+  if (r >= a.rpb[s]) return;
+  const int row = lb * a.rpb[s] + r;
+  if (row >= a.rows) return;
+  if (a.vec[s]) gather_seg<true>(a, sg, row, chunk);
+  else gather_seg<false>(a, sg, row, chunk);
+}
+
+template <bool VEC>
+__device__ void scatter_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int row, int chunk) {
+  constexpr int W = VEC ? 4 : 1;
+  const int c = chunk * W;
+  float g[4] = {0.f, 0.f, 0.f, 0.f};
+  load_row<VEC>(a.dout + (int64_t)row * a.ldo + sg.out_col + c, g);
+  if (sg.kind == RS_SEG_SPARSE) {
+    const int64_t id = sg.idx[(int64_t)row * sg.idx_stride];
+    if (id == sg.pad_idx || id < 0 || id >= sg.vocab) return;
+    float* d = sg.grad + id * sg.dim + c;
+#pragma unroll
+    for (int j = 0; j < W; ++j) atomicAdd(d + j, g[j]);
+  } else if (sg.kind == RS_SEG_POOL) {
+    const int64_t* ids = sg.idx + (int64_t)row * sg.idx_stride;
+    if (sg.pool_mode == RS_POOL_MAX) {
+      // gradient goes to the (first) arg-max row of each column (torch.max(dim) backward)
+      float best[4];
+      int64_t arg[4];
+#pragma unroll
+      for (int j = 0; j < W; ++j) { best[j] = -INFINITY; arg[j] = -1; }
+      for (int l = 0; l < sg.bag; ++l) {
+        const int64_t id = ids[l];
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (id >= 0 && id < sg.vocab) load_row<VEC>(sg.table + id * sg.dim + c, v);
+#pragma unroll
+        for (int j = 0; j < W; ++j)
+          if (v[j] > best[j] || arg[j] < 0) { best[j] = v[j]; arg[j] = id; }
+      }
+#pragma unroll
+      for (int j = 0; j < W; ++j)
+        if (arg[j] >= 0 && arg[j] != sg.pad_idx && arg[j] < sg.vocab)
+          atomicAdd(sg.grad + arg[j] * sg.dim + c + j, g[j]);
+      return;
+    }
+    if (sg.pool_mode == RS_POOL_MEAN) {
+      const float n = (float)sg.bag;
+#pragma unroll
+      for (int j = 0; j < W; ++j) g[j] = g[j] / n;
+    }
+    for (int l = 0; l < sg.bag; ++l) {
+      const int64_t id = ids[l];
+      if (id == sg.pad_idx || id < 0 || id >= sg.vocab) continue;
+      float* d = sg.grad + id * sg.dim + c;
+#pragma unroll
+      for (int j = 0; j < W; ++j) atomicAdd(d + j, g[j]);
+    }
+  } else if (sg.kind == RS_SEG_LASTVALID) {
+    const int64_t l = sg.idx[row];
+    float* d = sg.grad + ((int64_t)row * sg.bag + l) * sg.dim + c;
+#pragma unroll
+    for (int j = 0; j < W; ++j) d[j] += g[j];
+  } else {  // RS_SEG_COPY: plain store of the slice gradient
+    float* d = sg.grad + (int64_t)row * sg.dim + c;
+#pragma unroll
+    for (int j = 0; j < W; ++j) d[j] = g[j];
+  }
+}
+
+__global__ __launch_bounds__(256) void gather_bwd_kernel(SegLaunch a) {
+  const int s = find_seg(a, blockIdx.x);
+  const rs_feature_seg_t& sg = a.segs[s];
+  if (sg.kind == RS_SEG_DENSE) return;
+  const int lb = blockIdx.x - a.block_start[s];
+  const int C = a.chunks[s];
+  const int r = threadIdx.x / C, chunk = threadIdx.x % C;
+  if (r >= a.rpb[s]) return;
+  const int row = lb * a.rpb[s] + r;
+  if (row >= a.rows) return;
+  if (a.vec[s]) scatter_seg<true>(a, sg, row, chunk);
+  else scatter_seg<false>(a, sg, row, chunk);
+}
+
+// Linear(1, D) backward: dW[c] += sum_b dout[b,c]*x[b]; db[c] += sum_b dout[b,c].
+// One workgroup per dense segment, fixed summation order.
+__global__ __launch_bounds__(256) void dense_bwd_kernel(SegLaunch a) {
+  const int s = blockIdx.x;
+  const rs_feature_seg_t& sg = a.segs[s];
+  if (sg.kind != RS_SEG_DENSE) return;
+  __shared__ float red_w[256], red_b[256];
+  const int D = sg.dim;
+  const int lanes = 256 / D;  // D <= 256
+  const int c = threadIdx.x % D, rl = threadIdx.x / D;
+  float aw = 0.f, ab = 0.f;
+  if (rl < lanes) {
+    for (int row = rl; row < a.rows; row += lanes) {
+      const float g = a.dout[(int64_t)row * a.ldo + sg.out_col + c];
+      aw += g * sg.x[(int64_t)row * sg.idx_stride];
+      ab += g;
+    }
+  }
+  red_w[threadIdx.x] = aw;
+  red_b[threadIdx.x] = ab;
+  __syncthreads();
+  if (threadIdx.x < D) {
+    float w = 0.f, b = 0.f;
+    for (int i = 0; i < lanes; ++i) { w += red_w[i * D + c]; b += red_b[i * D + c]; }
+    sg.grad[c] += w;
+    sg.grad_bias[c] += b;
+  }
+}
+
+int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, int ldo,
+         const float* out_ptr_for_align) {
+  RS_CHECK_ARG(nseg >= 1 && nseg <= kMaxSeg, "gather: nseg %d out of [1,%d]", nseg, kMaxSeg);
+  int blocks = 0;
+  for (int s = 0; s < nseg; ++s) {
+    const rs_feature_seg_t& g = segs_host[s];
+    RS_CHECK_ARG(g.dim >= 1 && g.dim <= 1024, "gather: seg %d dim %d", s, g.dim);
+    RS_CHECK_ARG(g.out_col >= 0 && g.out_col + g.dim <= ldo, "gather: seg %d columns exceed ldo", s);
+    RS_CHECK_ARG(g.kind >= 0 && g.kind <= 4, "gather: seg %d bad kind %d", s, g.kind);
+    RS_CHECK_ARG(g.kind != RS_SEG_POOL || g.bag >= 1, "gather: seg %d empty bag", s);
+    RS_CHECK_ARG(g.kind != RS_SEG_DENSE || g.dim <= 256, "gather: dense seg %d dim > 256", s);
+    bool vec = (g.dim % 4 == 0) && (g.out_col % 4 == 0) && (ldo % 4 == 0) &&
+               aligned16(out_ptr_for_align) && aligned16(g.table) && g.kind != RS_SEG_DENSE;
+    int C = vec ? g.dim / 4 : g.dim;
+    if (C > 256) { vec = false; C = g.dim; }
+    RS_CHECK_ARG(C <= 256, "gather: seg %d too wide", s);
+    a.vec[s] = vec;
+    a.chunks[s] = C;
+    a.rpb[s] = 256 / C;
+    a.block_start[s] = blocks;
+    blocks += cdiv(rows, a.rpb[s]);
+  }
+  a.block_start[nseg] = blocks;
+  a.nseg = nseg;
+  a.rows = rows;
+  a.ldo = ldo;
+  return 0;
+}
+
+__global__ void seq_mask_kernel(const int64_t* __restrict__ seq, int64_t ld, int B, int L,
+                                int64_t pad, uint8_t* __restrict__ key_pad,
+                                int64_t* __restrict__ last) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  int valid = 0;
+  for (int l = 0; l < L; ++l) {
+    const bool m = seq[(int64_t)b * ld + l] == pad;
+    valid += m ? 0 : 1;
+    key_pad[(int64_t)b * L + l] = m ? 1 : 0;
+  }
+  if (valid == 0 && L > 0) {  // all padding: unmask the last position (T6)
+    key_pad[(int64_t)b * L + L - 1] = 0;
+    valid = 1;
+  }
+  last[b] = valid - 1 > 0 ? valid - 1 : 0;  // clamp(sum(valid) - 1, 0)  (T7)
+}
+
+}  // namespace
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int rs_gather_fwd(const rs_feature_seg_t* segs, int nseg, int rows, float* out, int ldo,
+                             int* err_flag, void* stream) {
+  RS_CHECK_ARG(segs && out, "rs_gather_fwd: null pointer");
+  const rs_feature_seg_t* segs_host = segs;
+  if (rows == 0) return 0;
+  SegLaunch a;
+  RS_RET_IF(plan(a, segs_host, nseg, rows, ldo, out));
+  for (int i = 0; i < nseg; ++i) a.segs[i] = segs[i];
+  a.out = out; a.dout = nullptr; a.err = err_flag;
+  gather_fwd_kernel<<<a.block_start[nseg], 256, 0, as_stream(stream)>>>(a);
+  RS_CHECK_LAUNCH("rs_gather_fwd");
+  return 0;
+}
+
+extern "C" int64_t rs_gather_ws_bytes(const rs_feature_seg_t* segs_host, int nseg, int rows) {
+  (void)segs_host; (void)nseg; (void)rows;
+  return 0;
+}
+
+extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, const float* dout,
+                             int ldo, float* ws, void* stream) {
+  (void)ws;
+  RS_CHECK_ARG(segs && dout, "rs_gather_bwd: null pointer");
+  const rs_feature_seg_t* segs_host = segs;
+  if (rows == 0) return 0;
+  SegLaunch a;
+  RS_RET_IF(plan(a, segs_host, nseg, rows, ldo, dout));
+  for (int s = 0; s < nseg; ++s) {
+    const rs_feature_seg_t& g = segs_host[s];
+    RS_CHECK_ARG(g.grad, "rs_gather_bwd: seg %d has no grad destination", s);
+    RS_CHECK_ARG(g.kind != RS_SEG_DENSE || g.grad_bias, "rs_gather_bwd: seg %d has no bias grad", s);
+  }
+  for (int i = 0; i < nseg; ++i) a.segs[i] = segs[i];
+  a.out = nullptr; a.dout = dout; a.err = nullptr;
+  hipStream_t st = as_stream(stream);
+  gather_bwd_kernel<<<a.block_start[nseg], 256, 0, st>>>(a);
+  RS_CHECK_LAUNCH("rs_gather_bwd");
+  bool any_dense = false;
+  for (int s = 0; s < nseg; ++s) any_dense |= segs_host[s].kind == RS_SEG_DENSE;
+  if (any_dense) {
+    dense_bwd_kernel<<<nseg, 256, 0, st>>>(a);
+    RS_CHECK_LAUNCH("rs_gather_bwd dense");
+  }
+  return 0;
+}
+
+extern "C" int rs_seq_mask(const int64_t* seq, int64_t ld_seq, int B, int L, int64_t pad_value,
+                           uint8_t* key_pad, int64_t* last, void* stream) {
+  RS_CHECK_ARG(seq && key_pad && last && B >= 0 && L >= 1 && ld_seq >= L, "rs_seq_mask: bad args");
+  if (B == 0) return 0;
+  seq_mask_kernel<<<cdiv(B, 256), 256, 0, as_stream(stream)>>>(seq, ld_seq, B, L, pad_value,
+                                                                key_pad, last);
+  RS_CHECK_LAUNCH("rs_seq_mask");
+  return 0;
+}

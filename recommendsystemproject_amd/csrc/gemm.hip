@@ -1,0 +1,291 @@
+// fp32 GEMM on the gfx950 f32-input MFMA (v_mfma_f32_32x32x2_f32: exact f32 products, one
+// rounding per fma, 64 FLOP/clk/SIMD = the f32 vector peak; there is no xf32 on gfx950).
+//
+// Used for every dense contraction of the training step (nn.Linear forward/backward in the
+// towers and the encoder, U @ I^T of the in-batch loss). Shapes on the hot path are skinny
+// (K, N <= 256, M up to B*L = 204800) so the kernel is built for streaming A: 256-thread
+// workgroups, 2x2 waves, each wave a (BM/2)x(BN/2) block of 32x32 MFMA tiles, BK = 16,
+// global->register prefetch of tile t+1 under the MFMAs of tile t, double-buffered LDS (one
+// barrier per k-tile). Transposed operands are written k-major into LDS so every MFMA operand
+// read is a conflict-free ds_read_b32 across 32 consecutive lanes.
+// Split-K (reductions over M = B*L for weight gradients) writes f32 partial slabs that a second
+// kernel sums in a fixed order (bitwise reproducible) and finishes with the epilogue.
+#include "common.h"
+
+namespace rs {
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 16;
+constexpr int PAD = 4;
+
+struct GemmArgs {
+  int M, N, K;
+  float alpha, beta;
+  const float* A;
+  int lda;
+  const float* B;
+  int ldb;
+  float* C;
+  int ldc;
+  int epi;
+  const float* bias;
+  const float* aux;
+  int ld_aux, aux_mod;
+  int split_k, kchunk;
+  float* ws;
+  int vecA, vecB;
+};
+
+__device__ __forceinline__ float epilogue(const GemmArgs& a, int m, int n, float v) {
+  if (a.epi & RS_EPI_BIAS) v += a.bias[n];
+  if (a.epi & RS_EPI_AUX_ADD) v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
+  if (a.epi & RS_EPI_AUX_MASK) v = a.aux[(int64_t)m * a.ld_aux + n] > 0.f ? v : 0.f;
+  if (a.beta != 0.f) v += a.beta * a.C[(int64_t)m * a.ldc + n];
+  if (a.epi & RS_EPI_RELU) v = fmaxf(v, 0.f);
+  return v;
+}
+
+// Loads of one operand tile (ROWS = M or N extent of the tile) into registers.
+// T == false: element (r, k) at P[r*ld + k] (contiguous in k) -> slots of 4 consecutive k.
+// T == true : element (r, k) at P[k*ld + r] (contiguous in r) -> slots of 4 consecutive r.
+template <int ROWS, bool T>
+struct TileLoader {
+  static constexpr int kSlots = ROWS * BK / 4;           // float4 slots per tile
+  static constexpr int kPer = (kSlots + 255) / 256;      // slots per thread
+  float4 reg[kPer];
+
+  __device__ __forceinline__ void load(const float* __restrict__ P, int ld, int r0, int rmax,
+                                       int k0, int kend, bool vec, int tid) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      int s = tid + i * 256;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (s < kSlots) {
+        int r, k;
+        if (!T) { r = s / (BK / 4); k = (s % (BK / 4)) * 4; }
+        else    { k = s / (ROWS / 4); r = (s % (ROWS / 4)) * 4; }
+        int gr = r0 + r, gk = k0 + k;
+        if (!T) {
+          if (gr < rmax) {
+            const float* p = P + (int64_t)gr * ld + gk;
+            if (vec && gk + 3 < kend) v = *reinterpret_cast<const float4*>(p);
+            else {
+              if (gk + 0 < kend) v.x = p[0];
+              if (gk + 1 < kend) v.y = p[1];
+              if (gk + 2 < kend) v.z = p[2];
+              if (gk + 3 < kend) v.w = p[3];
+            }
+          }
+        } else {
+          if (gk < kend) {
+            const float* p = P + (int64_t)gk * ld + gr;
+            if (vec && gr + 3 < rmax) v = *reinterpret_cast<const float4*>(p);
+            else {
+              if (gr + 0 < rmax) v.x = p[0];
+              if (gr + 1 < rmax) v.y = p[1];
+              if (gr + 2 < rmax) v.z = p[2];
+              if (gr + 3 < rmax) v.w = p[3];
+            }
+          }
+        }
+      }
+      reg[i] = v;
+    }
+  }
+
+  // LDS image is k-major: S[k][r], pitch ROWS + PAD.
+  __device__ __forceinline__ void store(float* S, int tid) const {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      int s = tid + i * 256;
+      if (s >= kSlots) break;
+      if (!T) {
+        int r = s / (BK / 4), k = (s % (BK / 4)) * 4;
+        S[(k + 0) * (ROWS + PAD) + r] = reg[i].x;
+        S[(k + 1) * (ROWS + PAD) + r] = reg[i].y;
+        S[(k + 2) * (ROWS + PAD) + r] = reg[i].z;
+        S[(k + 3) * (ROWS + PAD) + r] = reg[i].w;
+      } else {
+        int k = s / (ROWS / 4), r = (s % (ROWS / 4)) * 4;
+        *reinterpret_cast<float4*>(&S[k * (ROWS + PAD) + r]) = reg[i];
+      }
+    }
+  }
+};
+
+template <int BM, int BN, bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
+  constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave in m / n
+  __shared__ __attribute__((aligned(16))) float As[2][BK * (BM + PAD)];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK * (BN + PAD)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int z = blockIdx.z;
+  const int kbeg = z * a.kchunk;
+  const int kend = min(a.K, kbeg + a.kchunk);
+  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  TileLoader<BM, TA> la;
+  TileLoader<BN, !TB> lb;  // B(k, n): !TB is contiguous in n  ->  "T" layout of the loader
+  const bool vecA = a.vecA, vecB = a.vecB;
+
+  int buf = 0;
+  if (kbeg < kend) {
+    la.load(a.A, a.lda, m0, a.M, kbeg, kend, vecA, tid);
+    lb.load(a.B, a.ldb, n0, a.N, kbeg, kend, vecB, tid);
+    la.store(As[0], tid);
+    lb.store(Bs[0], tid);
+  }
+  __syncthreads();
+
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    const bool more = k0 + BK < kend;
+    if (more) {
+      la.load(a.A, a.lda, m0, a.M, k0 + BK, kend, vecA, tid);
+      lb.load(a.B, a.ldb, n0, a.N, k0 + BK, kend, vecB, tid);
+    }
+    const float* Asb = As[buf];
+    const float* Bsb = Bs[buf];
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      const int kr = kk + (lane >> 5);
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = Asb[kr * (BM + PAD) + wm + i * 32 + (lane & 31)];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = Bsb[kr * (BN + PAD) + wn + j * 32 + (lane & 31)];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      la.store(As[buf ^ 1], tid);
+      lb.store(Bs[buf ^ 1], tid);
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // epilogue: C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn + j * 32 + (lane & 31);
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m >= a.M) continue;
+        float v = a.alpha * acc[i][j][r];
+        if (a.split_k > 1) {
+          a.ws[((int64_t)z * a.M + m) * a.N + n] = v;
+        } else {
+          a.C[(int64_t)m * a.ldc + n] = epilogue(a, m, n, v);
+        }
+      }
+    }
+}
+
+__global__ void splitk_reduce_kernel(GemmArgs a) {
+  const int64_t total = (int64_t)a.M * a.N;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int z = 0; z < a.split_k; ++z) v += a.ws[z * total + idx];
+    const int m = (int)(idx / a.N), n = (int)(idx % a.N);
+    a.C[(int64_t)m * a.ldc + n] = epilogue(a, m, n, v);
+  }
+}
+
+template <int BM, int BN>
+void launch_tile(const GemmArgs& g, int ta, int tb, hipStream_t st) {
+  dim3 grid(cdiv(g.M, BM), cdiv(g.N, BN), g.split_k);
+  if (!ta && !tb) gemm_f32_kernel<BM, BN, false, false><<<grid, 256, 0, st>>>(g);
+  else if (!ta && tb) gemm_f32_kernel<BM, BN, false, true><<<grid, 256, 0, st>>>(g);
+  else if (ta && !tb) gemm_f32_kernel<BM, BN, true, false><<<grid, 256, 0, st>>>(g);
+  else gemm_f32_kernel<BM, BN, true, true><<<grid, 256, 0, st>>>(g);
+}
+
+}  // namespace
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int rs_gemm_auto_split(int M, int N, int K) {
+  // Fill the chip (>= ~512 workgroups) when the output is small and K is long.
+  const int BMt = M >= 2048 ? 128 : 64, BNt = N > 64 ? 128 : 64;
+  int64_t tiles = (int64_t)cdiv(M, BMt) * cdiv(N, BNt);
+  if (tiles >= 256 || K < 1024) return 1;
+  int s = (int)((512 + tiles - 1) / tiles);
+  int maxs = K / (BK * 16);  // each split keeps >= 16 k-tiles
+  if (s > maxs) s = maxs;
+  if (s > 256) s = 256;
+  return s < 1 ? 1 : s;
+}
+
+extern "C" int64_t rs_gemm_ws_bytes(int M, int N, int K, int split_k) {
+  (void)K;
+  return split_k > 1 ? (int64_t)split_k * M * N * (int64_t)sizeof(float) : 0;
+}
+
+extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float alpha,
+                           const float* A, int lda, const float* B, int ldb, float beta, float* C,
+                           int ldc, int epilogue, const float* bias, const float* aux, int ld_aux,
+                           int aux_mod, int split_k, float* ws, void* stream) {
+  RS_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "rs_gemm_f32: negative size M=%d N=%d K=%d", M, N, K);
+  if (M == 0 || N == 0) return 0;
+  RS_CHECK_ARG(A && B && C, "rs_gemm_f32: null operand");
+  RS_CHECK_ARG(ldc >= N, "rs_gemm_f32: ldc %d < N %d", ldc, N);
+  RS_CHECK_ARG(transA ? lda >= M : lda >= K, "rs_gemm_f32: bad lda %d", lda);
+  RS_CHECK_ARG(transB ? ldb >= K : ldb >= N, "rs_gemm_f32: bad ldb %d", ldb);
+  RS_CHECK_ARG(!(epilogue & RS_EPI_BIAS) || bias, "rs_gemm_f32: bias epilogue without bias");
+  RS_CHECK_ARG(!(epilogue & (RS_EPI_AUX_ADD | RS_EPI_AUX_MASK)) || (aux && ld_aux > 0),
+               "rs_gemm_f32: aux epilogue without aux");
+  RS_CHECK_ARG(!((epilogue & RS_EPI_AUX_ADD) && (epilogue & RS_EPI_AUX_MASK)),
+               "rs_gemm_f32: AUX_ADD and AUX_MASK are exclusive");
+  if (split_k < 1) split_k = 1;
+  RS_CHECK_ARG(split_k == 1 || ws, "rs_gemm_f32: split_k %d needs a workspace", split_k);
+  GemmArgs g;
+  g.M = M; g.N = N; g.K = K; g.alpha = alpha; g.beta = beta;
+  g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
+  g.epi = epilogue; g.bias = bias; g.aux = aux; g.ld_aux = ld_aux;
+  g.aux_mod = (epilogue & RS_EPI_AUX_ADD) ? (aux_mod > 0 ? aux_mod : M) : 1;
+  int kt = cdiv(K, BK);
+  int per = cdiv(kt, split_k);
+  g.kchunk = per * BK;
+  g.split_k = cdiv(K, g.kchunk);
+  if (K == 0) { g.split_k = 1; g.kchunk = BK; }
+  g.ws = ws;
+  g.vecA = (lda % 4 == 0) && aligned16(A);
+  g.vecB = (ldb % 4 == 0) && aligned16(B);
+  hipStream_t st = as_stream(stream);
+  const bool bigM = M >= 2048;
+  const bool wideN = N > 64;
+  if (bigM && wideN) launch_tile<128, 128>(g, transA, transB, st);
+  else if (bigM) launch_tile<128, 64>(g, transA, transB, st);
+  else if (wideN) launch_tile<64, 128>(g, transA, transB, st);
+  else launch_tile<64, 64>(g, transA, transB, st);
+  RS_CHECK_LAUNCH("rs_gemm_f32");
+  if (g.split_k > 1) {
+    int64_t total = (int64_t)M * N;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    splitk_reduce_kernel<<<blocks, 256, 0, st>>>(g);
+    RS_CHECK_LAUNCH("rs_gemm_f32 splitk");
+  }
+  return 0;
+}

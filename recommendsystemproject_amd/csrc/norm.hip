@@ -1,0 +1,512 @@
+// Normalisation kernels of the training step.
+//  * add + LayerNorm (post-LN residual of nn.TransformerEncoderLayer, K8): one wave per row,
+//    the row lives in registers (d = 64 -> one float per lane), wave-shuffle reductions.
+//  * BatchNorm1d in training mode (feature_bn and the MLP BNs, K12/K13): batch statistics
+//    need the whole column, so the forward is partial column sums (fp64) -> per-column finalise
+//    (mean, rstd, running-stat update in group order) -> normalise (+ fused ReLU). G row groups
+//    keep independent statistics (one item-tower pass per hard-negative slot, trap T13).
+//  * row L2 normalisation (F.normalize, K14).
+#include "common.h"
+#include "rng.h"
+
+namespace rs {
+namespace {
+
+// ------------------------------------------------------------------------------ LayerNorm
+template <int NPL, bool DROP>
+__global__ __launch_bounds__(256) void add_ln_fwd_kernel(float* __restrict__ a,
+                                                         const float* __restrict__ b,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta,
+                                                         float* __restrict__ y,
+                                                         float* __restrict__ mean,
+                                                         float* __restrict__ rstd, int M, int N,
+                                                         float eps, float pdrop,
+                                                         const int64_t* __restrict__ key,
+                                                         int site) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  DropKey dk;
+  if (DROP) dk = make_key(key, site, pdrop);
+  float h[NPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = lane + i * 64;
+    h[i] = 0.f;
+    if (c < N) {
+      const int64_t o = (int64_t)row * N + c;
+      const float av = DROP ? a[o] * keep_mult(dk, (uint64_t)o) : a[o];  // x + dropout(sublayer)
+      h[i] = av + b[o];
+      a[o] = h[i];
+    }
+    s += h[i];
+  }
+  const float mu = wave_sum(s) / (float)N;
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = lane + i * 64;
+    const float t = c < N ? h[i] - mu : 0.f;
+    v += t * t;
+  }
+  const float var = wave_sum(v) / (float)N;
+  const float rs_ = 1.f / sqrtf(var + eps);
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = lane + i * 64;
+    if (c < N) y[(int64_t)row * N + c] = (h[i] - mu) * rs_ * gamma[c] + beta[c];
+  }
+  if (lane == 0) { mean[row] = mu; rstd[row] = rs_; }
+}
+
+template <int NPL, bool DROP>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ h,
+                                                     const float* dy,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, float* dh,
+                                                     int M, int N, float* __restrict__ ws,
+                                                     float* __restrict__ da, float pdrop,
+                                                     const int64_t* __restrict__ key, int site) {
+  DropKey dk;
+  if (DROP) dk = make_key(key, site, pdrop);
+  __shared__ float red[2][4][NPL * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float pg[NPL], pb[NPL];
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
+  for (int row = blockIdx.x * 4 + wave; row < M; row += gridDim.x * 4) {
+    const float mu = mean[row], r = rstd[row];
+    float xh[NPL], g[NPL], dyv[NPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int c = lane + i * 64;
+      xh[i] = 0.f; g[i] = 0.f; dyv[i] = 0.f;
+      if (c < N) {
+        const int64_t o = (int64_t)row * N + c;
+        xh[i] = (h[o] - mu) * r;
+        dyv[i] = dy[o];
+        g[i] = dyv[i] * gamma[c];
+      }
+      s1 += g[i];
+      s2 += g[i] * xh[i];
+      pg[i] += dyv[i] * xh[i];
+      pb[i] += dyv[i];
+    }
+    const float m1 = wave_sum(s1) / (float)N, m2 = wave_sum(s2) / (float)N;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int c = lane + i * 64;
+      if (c < N) {
+        const int64_t o = (int64_t)row * N + c;
+        const float v = r * (g[i] - m1 - xh[i] * m2);
+        dh[o] = v;
+        if (da) da[o] = DROP ? v * keep_mult(dk, (uint64_t)o) : v;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    red[0][wave][lane + i * 64] = pg[i];
+    red[1][wave][lane + i * 64] = pb[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += 256) {
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { sg += red[0][w][c]; sb += red[1][w][c]; }
+    ws[(int64_t)blockIdx.x * 2 * N + c] = sg;
+    ws[(int64_t)blockIdx.x * 2 * N + N + c] = sb;
+  }
+}
+
+__global__ void ln_bwd_final_kernel(const float* __restrict__ ws, int nb, int N,
+                                    float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float sg = 0.f, sb = 0.f;
+  for (int b = 0; b < nb; ++b) { sg += ws[(int64_t)b * 2 * N + c]; sb += ws[(int64_t)b * 2 * N + N + c]; }
+  dgamma[c] += sg;
+  dbeta[c] += sb;
+}
+
+int ln_blocks(int M) {
+  int nb = cdiv(M, 4 * 8);  // >= 8 rows per wave
+  if (nb > 1024) nb = 1024;
+  if (nb < 1) nb = 1;
+  return nb;
+}
+
+// ------------------------------------------------------------------------------ BatchNorm
+int bn_chunks(int Bg) {
+  int s = cdiv(Bg, 256);
+  if (s > 64) s = 64;
+  if (s < 1) s = 1;
+  return s;
+}
+
+// partial (sum a, sum b) per column over a row chunk of one group.
+// MODE 0: a = x, b = x*x.   MODE 1: a = dy', b = dy' * xhat  (dy' = relu-masked dy)
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_partial_kernel(const float* __restrict__ x,
+                                                         const float* __restrict__ y,
+                                                         const float* __restrict__ dy,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, int Bg,
+                                                         int C, int S, int relu,
+                                                         double* __restrict__ ws) {
+  __shared__ double red[2][256];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const int g = blockIdx.y, s = blockIdx.z;
+  const int rpc = (Bg + S - 1) / S;
+  const int r0 = s * rpc, r1 = min(Bg, r0 + rpc);
+  double sa = 0.0, sb = 0.0;
+  if (c < C) {
+    float mu = 0.f, r = 0.f;
+    if (MODE == 1) { mu = mean[g * C + c]; r = rstd[g * C + c]; }
+    for (int i = r0 + rl; i < r1; i += 4) {
+      const int64_t o = ((int64_t)g * Bg + i) * C + c;
+      const float xv = x[o];
+      if (MODE == 0) {
+        sa += (double)xv;
+        sb += (double)xv * (double)xv;
+      } else {
+        float d = dy[o];
+        if (relu && !(y[o] > 0.f)) d = 0.f;
+        const float xh = (xv - mu) * r;
+        sa += (double)d;
+        sb += (double)d * (double)xh;
+      }
+    }
+  }
+  red[0][threadIdx.x] = sa;
+  red[1][threadIdx.x] = sb;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    double ta = 0.0, tb = 0.0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { ta += red[0][w * 64 + threadIdx.x]; tb += red[1][w * 64 + threadIdx.x]; }
+    const int64_t base = ((int64_t)g * S + s) * 2 * C;
+    ws[base + c] = ta;
+    ws[base + C + c] = tb;
+  }
+}
+
+__global__ void bn_fwd_final_kernel(const double* __restrict__ ws, int G, int S, int Bg, int C,
+                                    float momentum, float eps, float* __restrict__ mean,
+                                    float* __restrict__ rstd, float* running_mean,
+                                    float* running_var, int64_t* num_batches) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && num_batches) *num_batches += G;
+  if (c >= C) return;
+  for (int g = 0; g < G; ++g) {
+    double sa = 0.0, sb = 0.0;
+    for (int s = 0; s < S; ++s) {
+      const int64_t base = ((int64_t)g * S + s) * 2 * C;
+      sa += ws[base + c];
+      sb += ws[base + C + c];
+    }
+    const double n = (double)Bg;
+    const double mu = sa / n;
+    double var = sb / n - mu * mu;
+    if (var < 0.0) var = 0.0;
+    mean[g * C + c] = (float)mu;
+    rstd[g * C + c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (running_mean) {
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mu;
+      const double unb = Bg > 1 ? var * n / (n - 1.0) : var;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+    }
+  }
+}
+
+__global__ void bn_eval_stats_kernel(const float* __restrict__ rm, const float* __restrict__ rv,
+                                     int G, int C, float eps, float* __restrict__ mean,
+                                     float* __restrict__ rstd) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= G * C) return;
+  const int c = i % C;
+  mean[i] = rm[c];
+  rstd[i] = 1.f / sqrtf(rv[c] + eps);
+}
+
+__global__ void bn_norm_kernel(const float* __restrict__ x, float* __restrict__ y,
+                               const float* __restrict__ w, const float* __restrict__ b,
+                               const float* __restrict__ mean, const float* __restrict__ rstd,
+                               int Bg, int C, int64_t total, int relu) {
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(idx % C);
+    const int g = (int)(idx / ((int64_t)Bg * C));
+    float v = (x[idx] - mean[g * C + c]) * rstd[g * C + c] * w[c] + b[c];
+    if (relu) v = fmaxf(v, 0.f);
+    y[idx] = v;
+  }
+}
+
+__global__ void bn_bwd_final_kernel(const double* __restrict__ ws, int G, int S, int Bg, int C,
+                                    float* __restrict__ stats, float* dw, float* db) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double tw = 0.0, tb = 0.0;
+  for (int g = 0; g < G; ++g) {
+    double sa = 0.0, sb = 0.0;
+    for (int s = 0; s < S; ++s) {
+      const int64_t base = ((int64_t)g * S + s) * 2 * C;
+      sa += ws[base + c];
+      sb += ws[base + C + c];
+    }
+    stats[(int64_t)g * 2 * C + c] = (float)(sa / Bg);
+    stats[(int64_t)g * 2 * C + C + c] = (float)(sb / Bg);
+    tb += sa;
+    tw += sb;
+  }
+  dw[c] += (float)tw;
+  db[c] += (float)tb;
+}
+
+__global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                             const float* __restrict__ dy, const float* __restrict__ w,
+                             const float* __restrict__ mean, const float* __restrict__ rstd,
+                             const float* __restrict__ stats, float* __restrict__ dx, int Bg,
+                             int C, int64_t total, int relu) {
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(idx % C);
+    const int g = (int)(idx / ((int64_t)Bg * C));
+    float d = dy[idx];
+    if (relu && !(y[idx] > 0.f)) d = 0.f;
+    const float r = rstd[g * C + c];
+    const float xh = (x[idx] - mean[g * C + c]) * r;
+    const float mdy = stats[(int64_t)g * 2 * C + c], mdyx = stats[(int64_t)g * 2 * C + C + c];
+    dx[idx] = w[c] * r * (d - mdy - xh * mdyx);
+  }
+}
+
+// ------------------------------------------------------------------------------ L2 norm
+template <int NPL>
+__global__ __launch_bounds__(256) void l2_fwd_kernel(const float* __restrict__ x,
+                                                     float* __restrict__ y,
+                                                     float* __restrict__ norm, int M, int N,
+                                                     float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[NPL], s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = lane + i * 64;
+    v[i] = c < N ? x[(int64_t)row * N + c] : 0.f;
+    s += v[i] * v[i];
+  }
+  const float n = sqrtf(wave_sum(s));
+  const float den = fmaxf(n, eps);
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = lane + i * 64;
+    if (c < N) y[(int64_t)row * N + c] = v[i] / den;
+  }
+  if (lane == 0) norm[row] = n;
+}
+
+template <int NPL>
+__global__ __launch_bounds__(256) void l2_bwd_kernel(const float* __restrict__ y,
+                                                     const float* __restrict__ norm,
+                                                     const float* __restrict__ dy,
+                                                     float* __restrict__ dx, int M, int N,
+                                                     float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float yv[NPL], g[NPL], s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = lane + i * 64;
+    yv[i] = 0.f; g[i] = 0.f;
+    if (c < N) { yv[i] = y[(int64_t)row * N + c]; g[i] = dy[(int64_t)row * N + c]; }
+    s += yv[i] * g[i];
+  }
+  const float dot = wave_sum(s);
+  const float n = norm[row];
+  const bool clamped = !(n > eps);
+  const float den = fmaxf(n, eps);
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = lane + i * 64;
+    if (c < N) dx[(int64_t)row * N + c] = clamped ? g[i] / den : (g[i] - yv[i] * dot) / den;
+  }
+}
+
+int npl_for(int N) {
+  int k = cdiv(N, 64);
+  if (k <= 1) return 1;
+  if (k <= 2) return 2;
+  if (k <= 4) return 4;
+  if (k <= 8) return 8;
+  if (k <= 16) return 16;
+  return -1;
+}
+
+}  // namespace
+}  // namespace rs
+
+using namespace rs;
+
+#define RS_NPL_DISPATCH(NPLV, KERNEL, GRID, ...)                               \
+  switch (NPLV) {                                                              \
+    case 1: KERNEL<1><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;               \
+    case 2: KERNEL<2><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;               \
+    case 4: KERNEL<4><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;               \
+    case 8: KERNEL<8><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;               \
+    default: KERNEL<16><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;             \
+  }
+
+#define RS_NPL_DROP_DISPATCH(NPLV, DROPV, KERNEL, GRID, ...)                              \
+  if (DROPV) {                                                                            \
+    switch (NPLV) {                                                                       \
+      case 1: KERNEL<1, true><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                  \
+      case 2: KERNEL<2, true><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                  \
+      case 4: KERNEL<4, true><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                  \
+      case 8: KERNEL<8, true><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                  \
+      default: KERNEL<16, true><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                \
+    }                                                                                     \
+  } else {                                                                                \
+    switch (NPLV) {                                                                       \
+      case 1: KERNEL<1, false><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                 \
+      case 2: KERNEL<2, false><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                 \
+      case 4: KERNEL<4, false><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                 \
+      case 8: KERNEL<8, false><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                 \
+      default: KERNEL<16, false><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;               \
+    }                                                                                     \
+  }
+
+extern "C" int rs_add_layernorm_fwd(float* a, const float* b, const float* gamma,
+                                    const float* beta, float* y, float* mean, float* rstd, int M,
+                                    int N, float eps, float p, const int64_t* key, int site,
+                                    void* stream) {
+  RS_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || key), "rs_add_layernorm_fwd: bad dropout p");
+  RS_CHECK_ARG(a && b && gamma && beta && y && mean && rstd, "rs_add_layernorm_fwd: null pointer");
+  const int npl = npl_for(N);
+  RS_CHECK_ARG(M >= 0 && N >= 1 && npl > 0, "rs_add_layernorm_fwd: bad shape M=%d N=%d", M, N);
+  if (M == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  RS_NPL_DROP_DISPATCH(npl, p > 0.f, add_ln_fwd_kernel, cdiv(M, 4), a, b, gamma, beta, y, mean, rstd,
+                       M, N, eps, p, key, site);
+  RS_CHECK_LAUNCH("rs_add_layernorm_fwd");
+  return 0;
+}
+
+extern "C" int64_t rs_layernorm_ws_bytes(int M, int N) {
+  return (int64_t)ln_blocks(M) * 2 * N * (int64_t)sizeof(float);
+}
+
+extern "C" int rs_layernorm_bwd(const float* h, const float* dy, const float* gamma,
+                                const float* mean, const float* rstd, float* dh, float* dgamma,
+                                float* dbeta, int M, int N, float* da, float p, const int64_t* key,
+                                int site, float* ws, void* stream) {
+  RS_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || (key && da)), "rs_layernorm_bwd: bad dropout p");
+  RS_CHECK_ARG(h && dy && gamma && mean && rstd && dh && dgamma && dbeta && ws,
+               "rs_layernorm_bwd: null pointer");
+  const int npl = npl_for(N);
+  RS_CHECK_ARG(M >= 0 && N >= 1 && npl > 0, "rs_layernorm_bwd: bad shape");
+  if (M == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  const int nb = ln_blocks(M);
+  RS_NPL_DROP_DISPATCH(npl, p > 0.f, ln_bwd_kernel, nb, h, dy, gamma, mean, rstd, dh, M, N, ws, da, p,
+                       key, site);
+  RS_CHECK_LAUNCH("rs_layernorm_bwd");
+  ln_bwd_final_kernel<<<cdiv(N, 256), 256, 0, st>>>(ws, nb, N, dgamma, dbeta);
+  RS_CHECK_LAUNCH("rs_layernorm_bwd final");
+  return 0;
+}
+
+extern "C" int64_t rs_batchnorm_ws_bytes(int G, int Bg, int C) {
+  const int S = bn_chunks(Bg);
+  return (int64_t)G * S * 2 * C * (int64_t)sizeof(double) + (int64_t)G * 2 * C * sizeof(float);
+}
+
+extern "C" int rs_batchnorm_fwd(const float* x, float* y, const float* w, const float* b,
+                                float* running_mean, float* running_var, int64_t* num_batches,
+                                float* mean, float* rstd, int G, int Bg, int C, float momentum,
+                                float eps, int relu, int training, float* ws, void* stream) {
+  RS_CHECK_ARG(x && y && w && b && mean && rstd && ws, "rs_batchnorm_fwd: null pointer");
+  RS_CHECK_ARG(G >= 1 && Bg >= 1 && C >= 1, "rs_batchnorm_fwd: bad shape G=%d Bg=%d C=%d", G, Bg, C);
+  RS_CHECK_ARG(!running_mean == !running_var, "rs_batchnorm_fwd: running stats must come together");
+  hipStream_t st = as_stream(stream);
+  const int S = bn_chunks(Bg);
+  double* wsd = reinterpret_cast<double*>(ws);
+  const int64_t total = (int64_t)G * Bg * C;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  if (!training) {
+    RS_CHECK_ARG(running_mean, "rs_batchnorm_fwd: eval mode needs running stats");
+    bn_eval_stats_kernel<<<cdiv((int64_t)G * C, 256), 256, 0, st>>>(running_mean, running_var, G, C,
+                                                                     eps, mean, rstd);
+    RS_CHECK_LAUNCH("rs_batchnorm_fwd eval stats");
+    bn_norm_kernel<<<blocks, 256, 0, st>>>(x, y, w, b, mean, rstd, Bg, C, total, relu);
+    RS_CHECK_LAUNCH("rs_batchnorm_fwd norm");
+    return 0;
+  }
+  bn_partial_kernel<0><<<dim3(cdiv(C, 64), G, S), 256, 0, st>>>(x, nullptr, nullptr, nullptr,
+                                                                 nullptr, Bg, C, S, 0, wsd);
+  RS_CHECK_LAUNCH("rs_batchnorm_fwd partial");
+  bn_fwd_final_kernel<<<cdiv(C, 256), 256, 0, st>>>(wsd, G, S, Bg, C, momentum, eps, mean, rstd,
+                                                    running_mean, running_var, num_batches);
+  RS_CHECK_LAUNCH("rs_batchnorm_fwd final");
+  bn_norm_kernel<<<blocks, 256, 0, st>>>(x, y, w, b, mean, rstd, Bg, C, total, relu);
+  RS_CHECK_LAUNCH("rs_batchnorm_fwd norm");
+  return 0;
+}
+
+extern "C" int rs_batchnorm_bwd(const float* x, const float* y, const float* dy, const float* w,
+                                const float* mean, const float* rstd, float* dx, float* dw,
+                                float* db, int G, int Bg, int C, int relu, float* ws,
+                                void* stream) {
+  RS_CHECK_ARG(x && dy && w && mean && rstd && dx && dw && db && ws,
+               "rs_batchnorm_bwd: null pointer");
+  RS_CHECK_ARG(!relu || y, "rs_batchnorm_bwd: relu needs y");
+  RS_CHECK_ARG(G >= 1 && Bg >= 1 && C >= 1, "rs_batchnorm_bwd: bad shape");
+  hipStream_t st = as_stream(stream);
+  const int S = bn_chunks(Bg);
+  double* wsd = reinterpret_cast<double*>(ws);
+  float* stats = reinterpret_cast<float*>(wsd + (int64_t)G * S * 2 * C);
+  bn_partial_kernel<1><<<dim3(cdiv(C, 64), G, S), 256, 0, st>>>(x, y, dy, mean, rstd, Bg, C, S,
+                                                                 relu, wsd);
+  RS_CHECK_LAUNCH("rs_batchnorm_bwd partial");
+  bn_bwd_final_kernel<<<cdiv(C, 256), 256, 0, st>>>(wsd, G, S, Bg, C, stats, dw, db);
+  RS_CHECK_LAUNCH("rs_batchnorm_bwd final");
+  const int64_t total = (int64_t)G * Bg * C;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  bn_dx_kernel<<<blocks, 256, 0, st>>>(x, y, dy, w, mean, rstd, stats, dx, Bg, C, total, relu);
+  RS_CHECK_LAUNCH("rs_batchnorm_bwd dx");
+  return 0;
+}
+
+extern "C" int rs_l2norm_fwd(const float* x, float* y, float* norm, int M, int N, float eps,
+                             void* stream) {
+  RS_CHECK_ARG(x && y && norm, "rs_l2norm_fwd: null pointer");
+  const int npl = npl_for(N);
+  RS_CHECK_ARG(M >= 0 && N >= 1 && npl > 0, "rs_l2norm_fwd: bad shape");
+  if (M == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  RS_NPL_DISPATCH(npl, l2_fwd_kernel, cdiv(M, 4), x, y, norm, M, N, eps);
+  RS_CHECK_LAUNCH("rs_l2norm_fwd");
+  return 0;
+}
+
+extern "C" int rs_l2norm_bwd(const float* y, const float* norm, const float* dy, float* dx, int M,
+                             int N, float eps, void* stream) {
+  RS_CHECK_ARG(y && norm && dy && dx, "rs_l2norm_bwd: null pointer");
+  const int npl = npl_for(N);
+  RS_CHECK_ARG(M >= 0 && N >= 1 && npl > 0, "rs_l2norm_bwd: bad shape");
+  if (M == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  RS_NPL_DISPATCH(npl, l2_bwd_kernel, cdiv(M, 4), y, norm, dy, dx, M, N, eps);
+  RS_CHECK_LAUNCH("rs_l2norm_bwd");
+  return 0;
+}

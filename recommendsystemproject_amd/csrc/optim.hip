@@ -1,0 +1,189 @@
+// Gradient clipping and Adam over the flat parameter buffer (K18, K19).
+// All parameters of a model live in ONE contiguous fp32 buffer (and grads / exp_avg /
+// exp_avg_sq in three more), so clip_grad_norm_ is one streaming reduction and the optimizer
+// step is one streaming kernel (28 B/param: read p, g, m, v; write p, m, v) regardless of how
+// many tensors the model has. The clip coefficient stays on the device: no host sync.
+#include "common.h"
+
+namespace rs {
+namespace {
+
+int sq_blocks(int64_t n) {
+  int64_t b = (n + 256 * 16 - 1) / (256 * 16);
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+__global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g, int64_t n,
+                                                     float scale, double* __restrict__ ws) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t n4 = n / 4;
+  const bool vec = (reinterpret_cast<uintptr_t>(g) & 15) == 0;
+  if (vec) {
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+      const float4 v = g4[i];
+      const float a = v.x * scale, b = v.y * scale, c = v.z * scale, d = v.w * scale;
+      acc += (double)(a * a) + (double)(b * b) + (double)(c * c) + (double)(d * d);
+    }
+    for (int64_t i = n4 * 4 + blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+      const float a = g[i] * scale;
+      acc += (double)(a * a);
+    }
+  } else {
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+      const float a = g[i] * scale;
+      acc += (double)(a * a);
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) ws[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void clip_coef_kernel(const double* __restrict__ ws, int nb, float max_norm,
+                                 float* total_norm, float* coef) {
+  if (threadIdx.x != 0) return;
+  double t = 0.0;
+  for (int i = 0; i < nb; ++i) t += ws[i];
+  const float norm = (float)sqrt(t);
+  if (total_norm) *total_norm = norm;
+  float c = max_norm / (norm + 1e-6f);
+  *coef = c < 1.f ? c : 1.f;
+}
+
+__global__ void scale_kernel(float* __restrict__ g, int64_t n, float scale,
+                             const float* __restrict__ coef) {
+  const float s = scale * (coef ? *coef : 1.f);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    g[i] *= s;
+}
+
+struct AdamArgs {
+  float* p; float* g; float* m; float* v;
+  int64_t n;
+  float lr, step_size, b1, b2, one_m_b1, one_m_b2, eps, wd, bc2_sqrt, scale;
+  const float* coef;
+  const int64_t* step_dev;  // when set, bias corrections come from *step_dev (graph replay)
+  int write_grad;
+};
+
+__device__ __forceinline__ void adam_elem(const AdamArgs& a, float s, float& p, float& g, float& m,
+                                          float& v) {
+  float gs = g * s;
+  if (a.write_grad) g = gs;
+  if (a.wd != 0.f) gs = gs + a.wd * p;
+  m = m + a.one_m_b1 * (gs - m);                // exp_avg.lerp_(grad, 1 - beta1)
+  v = v * a.b2 + a.one_m_b2 * gs * gs;          // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+  p = p - a.step_size * (m / denom);            // param.addcdiv_(exp_avg, denom, -step_size)
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  const float s = a.scale * (a.coef ? *a.coef : 1.f);
+  if (a.step_dev) {
+    const double t = (double)*a.step_dev;
+    const double bc1 = 1.0 - pow((double)a.b1, t), bc2 = 1.0 - pow((double)a.b2, t);
+    a.step_size = (float)((double)a.lr / bc1);
+    a.bc2_sqrt = (float)sqrt(bc2);
+  }
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const bool vec = ((reinterpret_cast<uintptr_t>(a.p) | reinterpret_cast<uintptr_t>(a.g) |
+                     reinterpret_cast<uintptr_t>(a.m) | reinterpret_cast<uintptr_t>(a.v)) & 15) == 0;
+  int64_t done = 0;
+  if (vec) {
+    const int64_t n4 = a.n / 4;
+    float4* p4 = reinterpret_cast<float4*>(a.p);
+    float4* g4 = reinterpret_cast<float4*>(a.g);
+    float4* m4 = reinterpret_cast<float4*>(a.m);
+    float4* v4 = reinterpret_cast<float4*>(a.v);
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+      float4 p = p4[i], g = g4[i], m = m4[i], v = v4[i];
+      adam_elem(a, s, p.x, g.x, m.x, v.x);
+      adam_elem(a, s, p.y, g.y, m.y, v.y);
+      adam_elem(a, s, p.z, g.z, m.z, v.z);
+      adam_elem(a, s, p.w, g.w, m.w, v.w);
+      p4[i] = p; m4[i] = m; v4[i] = v;
+      if (a.write_grad) g4[i] = g;
+    }
+    done = n4 * 4;
+  }
+  for (int64_t i = done + blockIdx.x * 256 + threadIdx.x; i < a.n; i += stride) {
+    float p = a.p[i], g = a.g[i], m = a.m[i], v = a.v[i];
+    adam_elem(a, s, p, g, m, v);
+    a.p[i] = p; a.m[i] = m; a.v[i] = v;
+    if (a.write_grad) a.g[i] = g;
+  }
+}
+
+__global__ void counter_add_kernel(int64_t* c, int64_t delta) { *c += delta; }
+
+}  // namespace
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int64_t rs_sqnorm_ws_bytes(int64_t n) { return (int64_t)sq_blocks(n) * sizeof(double); }
+
+extern "C" int rs_grad_sqnorm(const float* g, int64_t n, float scale, double* ws, void* stream) {
+  RS_CHECK_ARG(g && ws && n >= 0, "rs_grad_sqnorm: bad args");
+  sqnorm_kernel<<<sq_blocks(n), 256, 0, as_stream(stream)>>>(g, n, scale, ws);
+  RS_CHECK_LAUNCH("rs_grad_sqnorm");
+  return 0;
+}
+
+extern "C" int rs_clip_coef(const double* ws, int64_t n, float max_norm, float* total_norm,
+                            float* coef, void* stream) {
+  RS_CHECK_ARG(ws && coef, "rs_clip_coef: null pointer");
+  clip_coef_kernel<<<1, 64, 0, as_stream(stream)>>>(ws, sq_blocks(n), max_norm, total_norm, coef);
+  RS_CHECK_LAUNCH("rs_clip_coef");
+  return 0;
+}
+
+extern "C" int rs_scale_inplace(float* g, int64_t n, float scale, const float* coef, void* stream) {
+  RS_CHECK_ARG(g && n >= 0, "rs_scale_inplace: bad args");
+  if (n == 0) return 0;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  scale_kernel<<<(int)blocks, 256, 0, as_stream(stream)>>>(g, n, scale, coef);
+  RS_CHECK_LAUNCH("rs_scale_inplace");
+  return 0;
+}
+
+extern "C" int rs_counter_add(int64_t* counter, int64_t delta, void* stream) {
+  RS_CHECK_ARG(counter, "rs_counter_add: null pointer");
+  counter_add_kernel<<<1, 1, 0, as_stream(stream)>>>(counter, delta);
+  RS_CHECK_LAUNCH("rs_counter_add");
+  return 0;
+}
+
+extern "C" int rs_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr,
+                            float beta1, float beta2, float eps, float weight_decay, int step,
+                            const int64_t* step_dev, float scale, const float* coef, int write_grad,
+                            void* stream) {
+  RS_CHECK_ARG(p && g && m && v && n >= 0 && (step >= 1 || step_dev), "rs_adam_step: bad args");
+  if (n == 0) return 0;
+  AdamArgs a;
+  a.p = p; a.g = g; a.m = m; a.v = v; a.n = n;
+  const double t = step >= 1 ? (double)step : 1.0;
+  const double bc1 = 1.0 - pow((double)beta1, t);
+  const double bc2 = 1.0 - pow((double)beta2, t);
+  a.lr = lr;
+  a.step_dev = step_dev;
+  a.step_size = (float)((double)lr / bc1);
+  a.bc2_sqrt = (float)sqrt(bc2);
+  a.b1 = beta1; a.b2 = beta2;
+  a.one_m_b1 = 1.f - beta1; a.one_m_b2 = 1.f - beta2;
+  a.eps = eps; a.wd = weight_decay; a.scale = scale; a.coef = coef; a.write_grad = write_grad;
+  int64_t blocks = (n / 4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  adam_kernel<<<(int)blocks, 256, 0, as_stream(stream)>>>(a);
+  RS_CHECK_LAUNCH("rs_adam_step");
+  return 0;
+}

@@ -1,0 +1,498 @@
+"""Autograd functions of the two-tower training step, one per reference module.
+
+Each function runs its whole module (forward and backward) as a sequence of librsys_hip kernels;
+autograd only connects the modules (SequenceEncoder -> tower features -> feature_bn -> MLP ->
+loss), so the graph has a handful of nodes per tower instead of hundreds of ATen ops. Weight
+gradients are accumulated by the kernels directly into the flat gradient buffer (flat.py); the
+functions return None for parameters (they are inputs only so autograd records the dependency).
+
+Dropout uses counter-based masks (csrc/rng.h): each forward draws a fresh (seed, counter) key
+on the device (graph-replay safe) and the backward re-derives the same masks from it. Sites:
+  sequence input: 0 projection dropout, 1 dropout after + pos_emb      (T5)
+  encoder layer i: 16+8i attention probs, +1 dropout1, +2 FFN inner, +3 dropout2
+  MLP hidden layer j: 256+j
+With p = 0 (the parity setting) nothing is hashed.
+
+`need` (first argument of every forward) is torch.is_grad_enabled() at the call site: inside
+Function.forward grad mode is always off, so the modules decide whether to keep activations.
+"""
+from __future__ import annotations
+
+import torch
+from torch.autograd.function import once_differentiable
+
+from . import _hip, ops
+from .flat import grad_of
+
+
+def _seg(**kw):
+    s = _hip.FeatureSeg()
+    s.pad_idx = -1
+    for k, v in kw.items():
+        setattr(s, k, v)
+    return s
+
+
+def _pad(v):
+    return -1 if v is None else int(v)
+
+
+# ================================================================================ sequence input
+def seq_feature_segments(proc, seqd, B, L):
+    """Per-token gather plan of SequenceFeatureProcessor.forward (SequenceFeatureProcessor.py:57-76):
+    2-D [B, L] features give one id per token, 3-D [B, L, T] tag lists are pooled by mean/sum (T4),
+    widths concatenated in config order. Returns (segments, tables, width, kept id tensors)."""
+    segs, tables, keep, col = [], [], [], 0
+    for f in proc.feature_config_list:
+        name = f['name']
+        if name not in seqd:
+            print(f'Configuration Error: Unable to find {name} in the input dictionary, {name} has skipped')
+            continue
+        x = seqd[name]
+        x = (x if x.dtype == torch.int64 else x.long()).contiguous()
+        keep.append(x)
+        emb = proc.embeddings[name]
+        D = emb.embedding_dim
+        pad = _pad(emb.padding_idx)
+        if x.dim() == 2:
+            if tuple(x.shape) != (B, L):
+                raise RuntimeError(f'sequence feature {name}: shape {tuple(x.shape)}, expected {(B, L)}')
+            segs.append(_seg(kind=_hip.RS_SEG_SPARSE, dim=D, out_col=col, vocab=emb.num_embeddings,
+                             idx_stride=1, idx=x.data_ptr(), table=emb.weight.data_ptr(), pad_idx=pad))
+        elif x.dim() == 3:
+            mode = f.get('pooling', None)
+            if mode not in ('mean', 'sum'):
+                raise RuntimeError(f'Tensors must have same number of dimensions: 3-D sequence feature '
+                                   f"{name} needs pooling 'mean' or 'sum' (got {mode!r})")
+            T = int(x.shape[2])
+            segs.append(_seg(kind=_hip.RS_SEG_POOL, dim=D, out_col=col, pool_mode=_hip.RS_POOL[mode],
+                             bag=T, vocab=emb.num_embeddings, idx_stride=T, idx=x.data_ptr(),
+                             table=emb.weight.data_ptr(), pad_idx=pad))
+        else:
+            raise RuntimeError(f'sequence feature {name}: unsupported rank {x.dim()}')
+        tables.append(emb.weight)
+        col += D
+    if not segs:
+        raise ValueError('Configuration Error: No valid features were processed!')
+    return segs, tables, col, keep
+
+
+def seq_input_fwd(proc, seqd, B, L, p, key, err):
+    """gather -> Linear(sum dims -> d) -> Dropout -> + pos_emb -> F.dropout (T5). Returns x [B*L, d]."""
+    segs, tables, dcat, keep = seq_feature_segments(proc, seqd, B, L)
+    if dcat != proc.feature_projection[0].in_features:
+        raise RuntimeError(f'mat1 and mat2 shapes cannot be multiplied ({B * L}x{dcat} and '
+                           f'{proc.feature_projection[0].in_features}x{proc.target_dim})')
+    M = B * L
+    dev = proc.pos_emb.weight.device
+    cat = torch.empty(M, dcat, device=dev, dtype=torch.float32)
+    ops.gather_fwd(segs, M, cat, err)
+    lin = proc.feature_projection[0]
+    pos = proc.pos_emb.weight
+    if p > 0:
+        x = ops.linear_fwd(cat, lin.weight, lin.bias)
+        ops.dropout_fwd(x, p, key, 0)
+        ops.dropout_fwd(x, p, key, 1, aux=pos, aux_mod=L)
+    else:
+        x = ops.linear_fwd(cat, lin.weight, lin.bias, aux=pos, aux_mod=L)
+    return x, (segs, tables, cat, keep)
+
+
+def seq_input_bwd(proc, saved, dx, B, L, p, key):
+    """Backward of seq_input_fwd; dx [B*L, d] is consumed (modified in place)."""
+    segs, tables, cat, _ = saved
+    d = proc.target_dim
+    if p > 0:
+        ops.dropout_bwd(dx, p, key, 1)
+    pos_g = grad_of(proc.pos_emb.weight)
+    ops.colsum(dx, pos_g, M=B, N=L * d, ldx=L * d)  # d pos_emb[l] = sum_b dx[b, l]
+    if p > 0:
+        ops.dropout_bwd(dx, p, key, 0)
+    lin = proc.feature_projection[0]
+    ops.linear_bwd_weight(dx, cat, grad_of(lin.weight))
+    ops.colsum(dx, grad_of(lin.bias))
+    dcat = ops.linear_bwd_input(dx, lin.weight)
+    for s, t in zip(segs, tables):
+        s.grad = grad_of(t).data_ptr()
+    ops.gather_bwd(segs, B * L, dcat)
+
+
+# ================================================================================ encoder layer
+def layer_fwd(lyr, x, key_pad, B, L, d, H, p, key, site):
+    """nn.TransformerEncoderLayer (norm_first=False, relu) forward on x [B*L, d]."""
+    sa_mod = lyr.self_attn
+    qkv = ops.linear_fwd(x, sa_mod.in_proj_weight, sa_mod.in_proj_bias)
+    att, lse = ops.attn_fwd(qkv, key_pad, B, L, d, H, p, key, site)
+    h1 = ops.linear_fwd(att, sa_mod.out_proj.weight, sa_mod.out_proj.bias)
+    x1, m1, r1 = ops.add_layernorm_fwd(h1, x, lyr.norm1.weight, lyr.norm1.bias, lyr.norm1.eps,
+                                       p, key, site + 1)  # h1 <- x + dropout1(sa)
+    f1 = ops.linear_fwd(x1, lyr.linear1.weight, lyr.linear1.bias, relu=True)
+    if p > 0:
+        ops.dropout_fwd(f1, p, key, site + 2)
+    h2 = ops.linear_fwd(f1, lyr.linear2.weight, lyr.linear2.bias)
+    x2, m2, r2 = ops.add_layernorm_fwd(h2, x1, lyr.norm2.weight, lyr.norm2.bias, lyr.norm2.eps,
+                                       p, key, site + 3)  # h2 <- x1 + dropout2(ff)
+    return x2, (x, qkv, att, lse, h1, x1, m1, r1, f1, h2, m2, r2)
+
+
+def layer_bwd(lyr, saved, dx2, key_pad, B, L, d, H, p, key, site):
+    """Backward of layer_fwd. dx2 is consumed; returns dx [B*L, d]."""
+    x, qkv, att, lse, h1, x1, m1, r1, f1, h2, m2, r2 = saved
+    g = grad_of
+    sa_mod = lyr.self_attn
+    # x2 = LN2(x1 + drop2(ff))
+    dff = torch.empty_like(dx2) if p > 0 else None
+    dh2 = ops.layernorm_bwd(h2, dx2, lyr.norm2.weight, m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias),
+                            da=dff, p=p, key=key, site=site + 3)
+    dff = dh2 if dff is None else dff
+    ops.linear_bwd_weight(dff, f1, g(lyr.linear2.weight))
+    ops.colsum(dff, g(lyr.linear2.bias))
+    # f1 holds relu(.) after dropout: (f1 > 0) == kept & positive, kept scale 1/(1-p)
+    df1 = ops.linear_bwd_input(dff, lyr.linear2.weight, relu_mask_of=f1,
+                               alpha=(1.0 / (1.0 - p)) if p > 0 else 1.0)
+    ops.linear_bwd_weight(df1, x1, g(lyr.linear1.weight))
+    ops.colsum(df1, g(lyr.linear1.bias))
+    ops.linear_bwd_input(df1, lyr.linear1.weight, out=dh2, beta=1.0)  # dx1 = dh2 + df1 W1
+    # x1 = LN1(x + drop1(sa))
+    dsa = torch.empty_like(dh2) if p > 0 else None
+    dh1 = ops.layernorm_bwd(h1, dh2, lyr.norm1.weight, m1, r1, g(lyr.norm1.weight), g(lyr.norm1.bias),
+                            da=dsa, p=p, key=key, site=site + 1)
+    dsa = dh1 if dsa is None else dsa
+    ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight))
+    ops.colsum(dsa, g(sa_mod.out_proj.bias))
+    datt = ops.linear_bwd_input(dsa, sa_mod.out_proj.weight)
+    dqkv = ops.attn_bwd(qkv, key_pad, att, datt, lse, B, L, d, H, p, key, site)
+    ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight))
+    ops.colsum(dqkv, g(sa_mod.in_proj_bias))
+    ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight, out=dh1, beta=1.0)  # dx = dh1 + dqkv Win
+    return dh1
+
+
+def _layer_site(i):
+    return 16 + 8 * i
+
+
+class SeqEncoderFn(torch.autograd.Function):
+    """SequenceEncoder.forward (SequenceEncoder.py:32-56): padding mask from the first feature
+    with the all-padding fix (T6), feature embedding + projection + positional embedding (T5),
+    n post-LN encoder layers (T8), last-valid gather (T7). Returns [B, d]."""
+
+    @staticmethod
+    def forward(ctx, need, enc, seqd, *params):
+        proc = enc.feature_embedder
+        first = proc.feature_config_list[0]
+        main = seqd[first['name']]
+        if main.dim() < 2:
+            raise RuntimeError('the first sequence feature must be [B, L]')
+        main = main if main.dtype == torch.int64 else main.long()
+        B, L = int(main.shape[0]), int(main.shape[1])
+        d, H = proc.target_dim, enc.n_head
+        if L > proc.pos_emb.num_embeddings:
+            raise IndexError(f'index out of range in self (sequence length {L} > max_seq_len '
+                             f'{proc.pos_emb.num_embeddings})')
+        key_pad, last = ops.seq_mask(main, first.get('padding_index', 0))
+        p = enc.dropout_p if enc.training else 0.0
+        key = ops.rng_next(enc.rng_state) if p > 0 else None
+        err = enc.err_flag
+        x, in_saved = seq_input_fwd(proc, seqd, B, L, p, key, err)
+        layers = list(enc.transformer_backbone.layers)
+        saved = []
+        for i, lyr in enumerate(layers):
+            x, s = layer_fwd(lyr, x, key_pad, B, L, d, H, p, key, _layer_site(i))
+            saved.append(s)
+        if enc.transformer_backbone.norm is not None:
+            raise NotImplementedError('TransformerEncoder(norm=...) is not used by the reference')
+        out = torch.empty(B, d, device=x.device, dtype=torch.float32)
+        seg = _seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=last.data_ptr(),
+                   table=x.data_ptr())
+        ops.gather_fwd([seg], B, out)
+        if need:
+            ctx.enc, ctx.B, ctx.L, ctx.p = enc, B, L, p
+            ctx.key, ctx.key_pad, ctx.last = key, key_pad, last
+            ctx.in_saved, ctx.layer_saved, ctx.layers = in_saved, saved, layers
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dout):
+        enc, B, L, p, key = ctx.enc, ctx.B, ctx.L, ctx.p, ctx.key
+        proc = enc.feature_embedder
+        d, H = proc.target_dim, enc.n_head
+        dout = dout.contiguous()
+        dx = torch.zeros(B * L, d, device=dout.device, dtype=torch.float32)
+        seg = _seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=ctx.last.data_ptr(),
+                   grad=dx.data_ptr())
+        ops.gather_bwd([seg], B, dout)
+        for i in reversed(range(len(ctx.layers))):
+            dx = layer_bwd(ctx.layers[i], ctx.layer_saved[i], dx, ctx.key_pad, B, L, d, H, p, key,
+                           _layer_site(i))
+        seq_input_bwd(proc, ctx.in_saved, dx, B, L, p, key)
+        ctx.layer_saved = ctx.in_saved = None
+        return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
+
+
+# ================================================================================ tower features
+def tower_segments(tower, input_dict, mapping):
+    """GenericTower.forward feature loop (GenericTower.py:133-222): config order, pooled sparse
+    features in place (T9), dense Linear(1, D) on one column (T11). Returns (segs, params, keep,
+    width, seq_col)."""
+    segs, params, keep, col = [], [], [], 0
+    sparse_cfg = tower.sparse_features or []
+    dense_cfg = tower.dense_features or []
+    if sparse_cfg and 'sparse' in input_dict:
+        sparse = input_dict['sparse']
+        seqd = input_dict.get('sequence', {}) or {}
+        non_pooled = [f['name'] for f in sparse_cfg if 'pooling' not in f]
+        for f in sparse_cfg:
+            name = f['name']
+            emb = tower.embeddings[name]
+            if 'pooling' in f:
+                if name not in seqd:
+                    print(f'Warning: Pooled feature {name} missing from sequence dict')
+                    continue
+                x = seqd[name]
+                x = (x if x.dtype == torch.int64 else x.long())
+                if x.dim() == 1:
+                    x = x.unsqueeze(1)
+                x = x.contiguous()
+                keep.append(x)
+                mode = tower.pooling_config[name]
+                if mode not in _hip.RS_POOL:
+                    raise ValueError(f'unsupported pooling {mode!r} for {name}')
+                segs.append(_seg(kind=_hip.RS_SEG_POOL, dim=emb.embedding_dim, out_col=col,
+                                 pool_mode=_hip.RS_POOL[mode], bag=int(x.shape[1]),
+                                 vocab=emb.num_embeddings, idx_stride=int(x.stride(0)),
+                                 idx=x.data_ptr(), table=emb.weight.data_ptr(), pad_idx=_pad(emb.padding_idx)))
+            else:
+                if sparse is None:
+                    continue
+                if mapping and 'sparse' in mapping:
+                    c = mapping['sparse'].get(name)
+                    if c is None:
+                        raise ValueError(f"Feature '{name}' not found in column mapping")
+                else:
+                    c = non_pooled.index(name)
+                sp = sparse if sparse.dtype == torch.int64 else sparse.long()
+                keep.append(sp)
+                segs.append(_seg(kind=_hip.RS_SEG_SPARSE, dim=emb.embedding_dim, out_col=col,
+                                 vocab=emb.num_embeddings, idx_stride=int(sp.stride(0)),
+                                 idx=sp.data_ptr() + 8 * c * int(sp.stride(1)),
+                                 table=emb.weight.data_ptr(), pad_idx=_pad(emb.padding_idx)))
+            params.append((emb.weight, None))
+            col += emb.embedding_dim
+    if dense_cfg and 'dense' in input_dict:
+        dense = input_dict['dense']
+        names = [f['name'] for f in dense_cfg]
+        dn = dense if dense.dtype == torch.float32 else dense.float()
+        keep.append(dn)
+        for f in dense_cfg:
+            name = f['name']
+            if mapping and 'dense' in mapping:
+                c = mapping['dense'].get(name)
+                if c is None:
+                    raise ValueError(f"Dense feature '{name}' not found in column mapping")
+            else:
+                c = names.index(name)
+            lin = tower.embeddings[name][0]
+            if lin.in_features != 1:
+                raise RuntimeError(f'mat1 and mat2 shapes cannot be multiplied: dense feature {name} '
+                                   f'feeds one column into Linear({lin.in_features}, {lin.out_features})')
+            segs.append(_seg(kind=_hip.RS_SEG_DENSE, dim=lin.out_features, out_col=col,
+                             idx_stride=int(dn.stride(0)), x=dn.data_ptr() + 4 * c * int(dn.stride(1)),
+                             table=lin.weight.data_ptr(), bias=lin.bias.data_ptr()))
+            params.append((lin.weight, lin.bias))
+            col += lin.out_features
+    return segs, params, keep, col
+
+
+class TowerFeatureFn(torch.autograd.Function):
+    """Concat of all tower features [B, total_embed_dim] (GenericTower.py:133-233), with the
+    sequence-encoder vector copied into the last slot."""
+
+    @staticmethod
+    def forward(ctx, need, tower, input_dict, mapping, seq_vec, *params):
+        segs, pp, keep, col = tower_segments(tower, input_dict, mapping)
+        B = None
+        for t in keep:
+            B = int(t.shape[0])
+            break
+        if seq_vec is not None:
+            B = int(seq_vec.shape[0]) if B is None else B
+            seq_vec = seq_vec.contiguous()
+            segs.append(_seg(kind=_hip.RS_SEG_COPY, dim=int(seq_vec.shape[1]), out_col=col,
+                             table=seq_vec.data_ptr()))
+            col += int(seq_vec.shape[1])
+        if not segs:
+            raise RuntimeError('Tower received no valid features. Check if input_dict matches config')
+        if col != tower.total_embed_dim:
+            raise RuntimeError(f'running_mean should contain {col} elements not {tower.total_embed_dim}')
+        if len(segs) > _hip.MAX_SEGMENTS:
+            raise RuntimeError(f'too many features in one tower ({len(segs)} > {_hip.MAX_SEGMENTS})')
+        dev = tower.feature_bn.weight.device
+        out = torch.empty(B, col, device=dev, dtype=torch.float32)
+        ops.gather_fwd(segs, B, out, tower.err_flag)
+        if need:
+            ctx.segs, ctx.pp, ctx.keep, ctx.B = segs, pp, keep, B
+            ctx.has_seq = seq_vec is not None
+            ctx.seq_shape = tuple(seq_vec.shape) if seq_vec is not None else None
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dout):
+        dout = dout.contiguous()
+        segs = ctx.segs
+        dseq = None
+        n_feat = len(ctx.pp)
+        for s, (w, b) in zip(segs[:n_feat], ctx.pp):
+            s.grad = grad_of(w).data_ptr()
+            if b is not None:
+                s.grad_bias = grad_of(b).data_ptr()
+        if ctx.has_seq:
+            dseq = torch.empty(ctx.seq_shape, device=dout.device, dtype=torch.float32)
+            segs[-1].grad = dseq.data_ptr()
+        ops.gather_bwd(segs, ctx.B, dout)
+        ctx.segs = ctx.keep = None
+        return (None, None, None, None, dseq) + (None,) * (len(ctx.needs_input_grad) - 5)
+
+
+# ================================================================================ batch norm
+class BatchNormFn(torch.autograd.Function):
+    """nn.BatchNorm1d (training: batch statistics, running-stat update; eval: running stats),
+    G independent row groups (hard-negative slots). GenericTower.py:234 (feature_bn)."""
+
+    @staticmethod
+    def forward(ctx, need, bn, x, G, *params):
+        x = x.contiguous()
+        y, mean, rstd = ops.batchnorm_fwd(x, bn, G, relu=False, training=bn.training)
+        if need:
+            ctx.bn, ctx.G, ctx.x, ctx.mean, ctx.rstd = bn, G, x, mean, rstd
+            ctx.training = bn.training
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        if not ctx.training:
+            raise NotImplementedError('backward through BatchNorm1d in eval mode')
+        bn = ctx.bn
+        dx = ops.batchnorm_bwd(ctx.x, None, dy.contiguous(), bn.weight, ctx.mean, ctx.rstd,
+                               grad_of(bn.weight), grad_of(bn.bias), ctx.G, relu=False)
+        return (None, None, dx, None) + (None,) * (len(ctx.needs_input_grad) - 4)
+
+
+# ================================================================================ MLP tower
+class MLPFn(torch.autograd.Function):
+    """MLP_Tower.forward (Tower.py:16-41): [Linear -> BatchNorm1d -> ReLU -> Dropout] x n,
+    Linear, F.normalize(p=2, dim=1)."""
+
+    @staticmethod
+    def forward(ctx, need, mlp, x, G, *params):
+        seq = mlp.mlp
+        n_hidden = (len(seq) - 1) // 4
+        p = mlp.dropout_p if mlp.training else 0.0
+        key = ops.rng_next(mlp.rng_state) if p > 0 else None
+        h = x.contiguous()
+        saved = []
+        for j in range(n_hidden):
+            lin, bn = seq[4 * j], seq[4 * j + 1]
+            z = ops.linear_fwd(h, lin.weight, lin.bias)
+            y, mean, rstd = ops.batchnorm_fwd(z, bn, G, relu=True, training=mlp.training)
+            if p > 0:
+                ops.dropout_fwd(y, p, key, 256 + j)
+            saved.append((h, z, y, mean, rstd))
+            h = y
+        last = seq[len(seq) - 1]
+        z = ops.linear_fwd(h, last.weight, last.bias)
+        out, norm = ops.l2norm_fwd(z)
+        if need:
+            ctx.mlp, ctx.G, ctx.p, ctx.key = mlp, G, p, key
+            ctx.saved, ctx.h_last, ctx.out, ctx.norm = saved, h, out, norm
+            ctx.training = mlp.training
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dout):
+        if not ctx.training:
+            raise NotImplementedError('backward through MLP_Tower in eval mode (BatchNorm running stats)')
+        seq = ctx.mlp.mlp
+        g = grad_of
+        last = seq[len(seq) - 1]
+        dz = ops.l2norm_bwd(ctx.out, ctx.norm, dout.contiguous())
+        ops.linear_bwd_weight(dz, ctx.h_last, g(last.weight))
+        ops.colsum(dz, g(last.bias))
+        dh = ops.linear_bwd_input(dz, last.weight)
+        for j in reversed(range(len(ctx.saved))):
+            h, z, y, mean, rstd = ctx.saved[j]
+            lin, bn = seq[4 * j], seq[4 * j + 1]
+            if ctx.p > 0:
+                ops.dropout_bwd(dh, ctx.p, ctx.key, 256 + j)
+            # y is post-ReLU (post-dropout): y > 0 <=> kept and positive
+            dz = ops.batchnorm_bwd(z, y, dh, bn.weight, mean, rstd, g(bn.weight), g(bn.bias), ctx.G,
+                                   relu=True)
+            ops.linear_bwd_weight(dz, h, g(lin.weight))
+            ops.colsum(dz, g(lin.bias))
+            dh = ops.linear_bwd_input(dz, lin.weight)
+        ctx.saved = None
+        return (None, None, dh, None) + (None,) * (len(ctx.needs_input_grad) - 4)
+
+
+# ================================================================================ loss
+class InBatchLossFn(torch.autograd.Function):
+    """TwoTowerModel.compute_loss (TwoTowerModel.py:81-140, T12): logits = U I^T / T with
+    off-diagonal equal-id collisions at -1e9, hard-negative logits appended un-masked,
+    cross_entropy(labels = arange(B)), mean."""
+
+    @staticmethod
+    def forward(ctx, U, I, item_ids, H, temperature):
+        U = U.contiguous()
+        I = I.contiguous()
+        B, D = int(U.shape[0]), int(U.shape[1])
+        dev = U.device
+        S = torch.empty(B, B, device=dev, dtype=torch.float32)
+        ops.gemm(U, I, S, B, B, D, transA=0, transB=1, lda=D, ldb=D, ldc=B)
+        N = 0
+        Hc = None
+        if H is not None:
+            Hc = H.contiguous()
+            N = int(Hc.shape[1])
+        ids = None
+        st = 0
+        if item_ids is not None:
+            ids = item_ids.reshape(-1)
+            if ids.dtype != torch.int64:
+                ids = ids.long()
+            st = int(ids.stride(0))
+        lse = torch.empty(B, device=dev, dtype=torch.float32)
+        row_loss = torch.empty(B, device=dev, dtype=torch.float32)
+        loss = torch.empty((), device=dev, dtype=torch.float32)
+        _hip.call('rs_inbatch_ce_fwd', S.data_ptr(), B, U.data_ptr(), ops.P(Hc), ops.P(ids), st, B, N, D,
+                  float(temperature), lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(), ops.stream())
+        ctx.save_for_backward(U, I, Hc if Hc is not None else U)
+        ctx.S, ctx.ids, ctx.st, ctx.N, ctx.T, ctx.lse = S, ids, st, N, float(temperature), lse
+        return loss
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gout):
+        U, I, Hc = ctx.saved_tensors
+        B, D = int(U.shape[0]), int(U.shape[1])
+        N = ctx.N
+        S = ctx.S
+        gout = gout.contiguous()
+        dhl = torch.empty(B, max(N, 1), device=U.device, dtype=torch.float32) if N else None
+        _hip.call('rs_inbatch_ce_bwd', S.data_ptr(), B, U.data_ptr(), ops.P(Hc) if N else None,
+                  ops.P(ctx.ids), ctx.st, B, N, D, ctx.T, ctx.lse.data_ptr(), gout.data_ptr(),
+                  ops.P(dhl), ops.stream())
+        dU = torch.empty_like(U)
+        ops.gemm(S, I, dU, B, D, B, transA=0, transB=0, lda=B, ldb=D, ldc=D)       # dS @ I
+        dI = torch.empty_like(I)
+        ops.gemm(S, U, dI, B, D, B, transA=1, transB=0, lda=B, ldb=D, ldc=D)       # dS^T @ U
+        dH = None
+        if N:
+            dH = torch.empty_like(Hc)
+            _hip.call('rs_hardneg_bwd', U.data_ptr(), Hc.data_ptr(), dhl.data_ptr(), dU.data_ptr(),
+                      dH.data_ptr(), B, N, D, ops.stream())
+        ctx.S = None
+        return dU, dI, None, dH, None

@@ -1,0 +1,212 @@
+"""Thin tensor-level wrappers over the C ABI (pointers, strides, current HIP stream).
+
+Only torch is used here for device memory (torch.empty on the caching allocator) and for the
+current stream handle; all arithmetic runs in librsys_hip.so.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _hip
+from ._hip import call
+
+_ZERO = {}
+
+
+def P(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ws(nbytes: int, device) -> torch.Tensor:
+    """Workspace from the caching allocator (capture-safe)."""
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+def gemm(A, B, C, M, N, K, *, transA, transB, lda, ldb, ldc, alpha=1.0, beta=0.0, epi=0,
+         bias=None, aux=None, ld_aux=0, aux_mod=0, split=None):
+    L = _hip.lib()
+    if split is None:
+        split = L.rs_gemm_auto_split(M, N, K)
+    w = None
+    if split > 1:
+        w = ws(L.rs_gemm_ws_bytes(M, N, K, split), C.device)
+    call('rs_gemm_f32', int(transA), int(transB), M, N, K, float(alpha), P(A), lda, P(B), ldb,
+         float(beta), P(C), ldc, epi, P(bias), P(aux), ld_aux, aux_mod, split, P(w), stream())
+    return C
+
+
+def linear_fwd(x, W, b=None, out=None, *, relu=False, aux=None, aux_mod=0, beta=0.0):
+    """out[M,N] = x[M,K] @ W[N,K]^T (+ b) (+ aux[m % aux_mod]) (relu)."""
+    M, K = x.shape
+    N = W.shape[0]
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=torch.float32)
+    epi = (_hip.RS_EPI_BIAS if b is not None else 0) | (_hip.RS_EPI_RELU if relu else 0) | \
+        (_hip.RS_EPI_AUX_ADD if aux is not None else 0)
+    return gemm(x, W, out, M, N, K, transA=0, transB=1, lda=x.stride(0), ldb=W.stride(0),
+                ldc=out.stride(0), beta=beta, epi=epi, bias=b, aux=aux,
+                ld_aux=(aux.stride(0) if aux is not None else 0), aux_mod=aux_mod)
+
+
+def linear_bwd_input(dy, W, out=None, *, beta=0.0, relu_mask_of=None, alpha=1.0):
+    """out[M,K] = (dy[M,N] @ W[N,K]) (* (relu_mask_of > 0)) (+ beta*out)."""
+    M, N = dy.shape
+    K = W.shape[1]
+    if out is None:
+        out = torch.empty(M, K, device=dy.device, dtype=torch.float32)
+    epi = _hip.RS_EPI_AUX_MASK if relu_mask_of is not None else 0
+    return gemm(dy, W, out, M, K, N, transA=0, transB=0, lda=dy.stride(0), ldb=W.stride(0),
+                ldc=out.stride(0), alpha=alpha, beta=beta, epi=epi, aux=relu_mask_of,
+                ld_aux=(relu_mask_of.stride(0) if relu_mask_of is not None else 0))
+
+
+def linear_bwd_weight(dy, x, dW, *, beta=1.0):
+    """dW[N,K] (+)= dy[M,N]^T @ x[M,K] (reduction over M, split-K)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    return gemm(dy, x, dW, N, K, M, transA=1, transB=0, lda=dy.stride(0), ldb=x.stride(0),
+                ldc=dW.stride(0), beta=beta)
+
+
+def colsum(X, out, *, scale=1.0, beta=1.0, M=None, N=None, ldx=None):
+    """out[n] = beta*out[n] + scale*sum_m X[m, n]."""
+    if M is None:
+        M, N = X.shape
+        ldx = X.stride(0)
+    w = ws(_hip.lib().rs_colsum_ws_bytes(M, N), X.device)
+    call('rs_colsum', P(X), M, N, ldx, float(scale), float(beta), P(out), P(w), stream())
+    return out
+
+
+def seq_mask(seq, pad_value=0):
+    B, L = seq.shape[0], seq.shape[1]
+    key_pad = torch.empty(B, L, dtype=torch.uint8, device=seq.device)
+    last = torch.empty(B, dtype=torch.int64, device=seq.device)
+    call('rs_seq_mask', P(seq), seq.stride(0), B, L, int(pad_value), P(key_pad), P(last), stream())
+    return key_pad, last
+
+
+def segments_array(segs):
+    arr = (_hip.FeatureSeg * len(segs))(*segs)
+    return arr
+
+
+def gather_fwd(segs, rows, out, err_flag=None):
+    arr = segments_array(segs)
+    call('rs_gather_fwd', arr, len(segs), rows, P(out), out.stride(0), P(err_flag), stream())
+    return out
+
+
+def gather_bwd(segs, rows, dout):
+    arr = segments_array(segs)
+    call('rs_gather_bwd', arr, len(segs), rows, P(dout), dout.stride(0), None, stream())
+
+
+def attn_fwd(qkv, key_pad, B, L, d, H, p=0.0, key=None, site=0):
+    out = torch.empty(B * L, d, device=qkv.device, dtype=torch.float32)
+    lse = torch.empty(B * H * L, device=qkv.device, dtype=torch.float32)
+    call('rs_attn_fwd', P(qkv), P(key_pad), P(out), P(lse), B, L, d, H,
+         float((d // H) ** -0.5), float(p), P(key), site, stream())
+    return out, lse
+
+
+def attn_bwd(qkv, key_pad, out, dout, lse, B, L, d, H, p=0.0, key=None, site=0):
+    dqkv = torch.empty(B * L, 3 * d, device=qkv.device, dtype=torch.float32)
+    call('rs_attn_bwd', P(qkv), P(key_pad), P(out), P(dout), P(lse), P(dqkv), B, L, d, H,
+         float((d // H) ** -0.5), float(p), P(key), site, stream())
+    return dqkv
+
+
+def add_layernorm_fwd(a, b, gamma, beta, eps=1e-5, p=0.0, key=None, site=0):
+    """h = dropout(a) + b (into a); returns y, mean, rstd."""
+    M, N = a.shape
+    y = torch.empty_like(a)
+    mean = torch.empty(M, device=a.device, dtype=torch.float32)
+    rstd = torch.empty(M, device=a.device, dtype=torch.float32)
+    call('rs_add_layernorm_fwd', P(a), P(b), P(gamma), P(beta), P(y), P(mean), P(rstd), M, N,
+         float(eps), float(p), P(key), site, stream())
+    return y, mean, rstd
+
+
+def layernorm_bwd(h, dy, gamma, mean, rstd, dgamma, dbeta, dh=None, da=None, p=0.0, key=None,
+                  site=0):
+    """dh = LN backward (in place over dy by default); da = dropout-backward(dh) if given."""
+    M, N = h.shape
+    if dh is None:
+        dh = dy
+    w = ws(_hip.lib().rs_layernorm_ws_bytes(M, N), h.device)
+    call('rs_layernorm_bwd', P(h), P(dy), P(gamma), P(mean), P(rstd), P(dh), P(dgamma), P(dbeta),
+         M, N, P(da), float(p), P(key), site, P(w), stream())
+    return dh
+
+
+def rng_next(state):
+    key = torch.empty(2, dtype=torch.int64, device=state.device)
+    call('rs_rng_next', P(state), P(key), stream())
+    return key
+
+
+def dropout_fwd(x, p, key, site, aux=None, aux_mod=0):
+    """x = dropout(x (+ aux[row % aux_mod])) in place; x is [M, N] contiguous."""
+    N = x.shape[-1]
+    call('rs_dropout_fwd', P(x), x.numel(), N, P(aux), aux.stride(0) if aux is not None else 0,
+         aux_mod, float(p), P(key), site, stream())
+    return x
+
+
+def dropout_bwd(dx, p, key, site):
+    call('rs_dropout_bwd', P(dx), dx.numel(), float(p), P(key), site, stream())
+    return dx
+
+
+def batchnorm_fwd(x, bn, G, relu, training, momentum=None, eps=None):
+    """x [G*Bg, C]; bn: nn.BatchNorm1d-like (weight, bias, running_*, num_batches_tracked)."""
+    M, Cc = x.shape
+    Bg = M // G
+    y = torch.empty_like(x)
+    mean = torch.empty(G * Cc, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(G * Cc, device=x.device, dtype=torch.float32)
+    mom = bn.momentum if momentum is None else momentum
+    if mom is None:
+        raise NotImplementedError('BatchNorm1d(momentum=None) (cumulative average) is not supported')
+    track = bn.track_running_stats and bn.running_mean is not None
+    batch_stats = training or not track          # nn.BatchNorm1d: eval uses running stats
+    update = training and track
+    run = update or not batch_stats
+    w = ws(_hip.lib().rs_batchnorm_ws_bytes(G, Bg, Cc), x.device)
+    call('rs_batchnorm_fwd', P(x), P(y), P(bn.weight), P(bn.bias),
+         P(bn.running_mean) if run else None, P(bn.running_var) if run else None,
+         P(bn.num_batches_tracked) if update else None,
+         P(mean), P(rstd), G, Bg, Cc, float(mom), float(bn.eps if eps is None else eps), int(relu),
+         int(batch_stats), P(w), stream())
+    return y, mean, rstd
+
+
+def batchnorm_bwd(x, y, dy, weight, mean, rstd, dw, db, G, relu, dx=None):
+    M, Cc = x.shape
+    Bg = M // G
+    if dx is None:
+        dx = torch.empty_like(x)
+    w = ws(_hip.lib().rs_batchnorm_ws_bytes(G, Bg, Cc), x.device)
+    call('rs_batchnorm_bwd', P(x), P(y), P(dy), P(weight), P(mean), P(rstd), P(dx), P(dw), P(db),
+         G, Bg, Cc, int(relu), P(w), stream())
+    return dx
+
+
+def l2norm_fwd(x, eps=1e-12):
+    M, N = x.shape
+    y = torch.empty_like(x)
+    norm = torch.empty(M, device=x.device, dtype=torch.float32)
+    call('rs_l2norm_fwd', P(x), P(y), P(norm), M, N, float(eps), stream())
+    return y, norm
+
+
+def l2norm_bwd(y, norm, dy, eps=1e-12):
+    M, N = y.shape
+    dx = torch.empty_like(y)
+    call('rs_l2norm_bwd', P(y), P(norm), P(dy), P(dx), M, N, float(eps), stream())
+    return dx

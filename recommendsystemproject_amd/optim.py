@@ -1,0 +1,174 @@
+"""Adam and clip_grad_norm_ over the flat parameter buffer (HIP kernels, no host sync).
+
+`Adam` takes the same arguments as torch.optim.Adam (train_twotower.py:111) and keeps a
+torch-compatible state_dict (state[p] = {step, exp_avg, exp_avg_sq}); when a param group is
+exactly one flat buffer (flat.py) the whole update is one streaming kernel over it.
+`clip_grad_norm_` mirrors torch.nn.utils.clip_grad_norm_ (training_utils.py:53-54) with the
+total norm and the clip coefficient kept on the device.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _hip, ops
+from .flat import flat_of
+
+
+def _flat_cover(params):
+    """The FlatParams that `params` is exactly (same objects, same order), else None."""
+    if not params:
+        return None
+    f = flat_of(params[0])
+    if f is not None and f.covers(params):
+        base = f.data.data_ptr()
+        if all(p.data_ptr() == base + 4 * p._rs_offset for p in params):
+            return f
+    return None
+
+
+class _DeviceClip:
+    """sqnorm partials -> (total_norm, coef) device scalars."""
+
+    def __init__(self, device):
+        self.norm = torch.zeros((), device=device, dtype=torch.float32)
+        self.coef = torch.ones((), device=device, dtype=torch.float32)
+
+    def compute(self, g, n, max_norm, scale=1.0):
+        ws = torch.empty(max(int(_hip.lib().rs_sqnorm_ws_bytes(n)), 16), dtype=torch.uint8, device=g.device)
+        _hip.call('rs_grad_sqnorm', g.data_ptr(), n, float(scale), ws.data_ptr(), ops.stream())
+        _hip.call('rs_clip_coef', ws.data_ptr(), n, float(max_norm), self.norm.data_ptr(),
+                  self.coef.data_ptr(), ops.stream())
+
+
+def clip_grad_norm_(parameters, max_norm, norm_type=2.0, error_if_nonfinite=False, foreach=None):
+    """torch.nn.utils.clip_grad_norm_ semantics (2-norm): grads scaled in place by
+    min(1, max_norm / (total + 1e-6)); returns the total norm as a device scalar."""
+    if float(norm_type) != 2.0:
+        raise NotImplementedError('only the 2-norm (the reference default) is implemented')
+    if isinstance(parameters, torch.Tensor):
+        parameters = [parameters]
+    params = [p for p in parameters if p.grad is not None]
+    if not params:
+        return torch.tensor(0.0)
+    _hip.require_device(params[0])
+    f = _flat_cover(list(parameters))
+    clip = _DeviceClip(params[0].device)
+    if f is not None:
+        clip.compute(f.grad, f.numel, max_norm)
+        _hip.call('rs_scale_inplace', f.grad.data_ptr(), f.numel, 1.0, clip.coef.data_ptr(), ops.stream())
+    else:
+        # per-tensor partial sums into one workspace would need a multi-tensor kernel; gather
+        # the squares through a temporary flat copy instead (rare path: non-flattened params)
+        flat = torch.cat([p.grad.reshape(-1) for p in params])
+        clip.compute(flat, flat.numel(), max_norm)
+        for p in params:
+            _hip.call('rs_scale_inplace', p.grad.data_ptr(), p.grad.numel(), 1.0, clip.coef.data_ptr(),
+                      ops.stream())
+    if error_if_nonfinite and not torch.isfinite(clip.norm):
+        raise RuntimeError(f'The total norm of order {norm_type} for gradients is non-finite')
+    return clip.norm
+
+
+class Adam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 amsgrad=False, *, foreach=None, maximize=False, capturable=False,
+                 differentiable=False, fused=None):
+        if amsgrad or maximize or differentiable:
+            raise NotImplementedError('amsgrad / maximize / differentiable are not supported')
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
+                        maximize=False, foreach=foreach, capturable=capturable,
+                        differentiable=False, fused=fused)
+        super().__init__(params, defaults)
+        self.grad_scale = 1.0   # 1/world_size under data parallelism (sum all-reduce)
+        self._flat_state = {}   # id(FlatParams) -> dict(m, v, step)
+        self._clip = None
+
+    # -------------------------------------------------------------- helpers
+    def _group_flat(self, group):
+        return _flat_cover(group['params'])
+
+    def _state_for_flat(self, f):
+        st = self._flat_state.get(id(f))
+        if st is None or st['f'] is not f:
+            st = dict(f=f, m=torch.zeros_like(f.data), v=torch.zeros_like(f.data), step=0,
+                      step_dev=torch.zeros((), dtype=torch.int64, device=f.data.device))
+            self._flat_state[id(f)] = st
+            for p, o in zip(f.params, f.offsets):
+                self.state[p] = {'step': torch.tensor(0.0),
+                                 'exp_avg': st['m'][o:o + p.numel()].view(p.shape),
+                                 'exp_avg_sq': st['v'][o:o + p.numel()].view(p.shape)}
+        return st
+
+    def zero_grad(self, set_to_none: bool = True):
+        """Flat gradients are zeroed in place (one memset per flat buffer) and stay attached."""
+        done = set()
+        for group in self.param_groups:
+            for p in group['params']:
+                f = flat_of(p)
+                if f is not None:
+                    if id(f) not in done:
+                        done.add(id(f))
+                        if not f.grads_attached():
+                            f.attach_grads(zero=False)
+                        f.zero_grad()
+                elif p.grad is not None:
+                    if set_to_none:
+                        p.grad = None
+                    else:
+                        p.grad.zero_()
+
+    # -------------------------------------------------------------- step
+    @torch.no_grad()
+    def step(self, closure=None, *, clip_max_norm=None):
+        """One Adam step. With clip_max_norm the global grad-norm clip (clip_grad_norm_) is fused:
+        the coefficient is computed on the device and applied inside the Adam kernel."""
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            b1, b2 = group['betas']
+            f = self._group_flat(group)
+            if f is not None:
+                _hip.require_device(f.data)
+                st = self._state_for_flat(f)
+                st['step'] += 1
+                coef = None
+                if clip_max_norm is not None and clip_max_norm > 0:
+                    if self._clip is None:
+                        self._clip = _DeviceClip(f.data.device)
+                    self._clip.compute(f.grad, f.numel, clip_max_norm, self.grad_scale)
+                    coef = self._clip.coef.data_ptr()
+                # device-side step count: the same launch replays correctly inside a hipGraph
+                _hip.call('rs_counter_add', st['step_dev'].data_ptr(), 1, ops.stream())
+                _hip.call('rs_adam_step', f.data.data_ptr(), f.grad.data_ptr(), st['m'].data_ptr(),
+                          st['v'].data_ptr(), f.numel, float(group['lr']), float(b1), float(b2),
+                          float(group['eps']), float(group['weight_decay']), 0,
+                          st['step_dev'].data_ptr(), float(self.grad_scale), coef, 0, ops.stream())
+                continue
+            if clip_max_norm is not None and clip_max_norm > 0:
+                clip_grad_norm_(group['params'], clip_max_norm)
+            for p in group['params']:
+                if p.grad is None:
+                    continue
+                _hip.require_device(p)
+                state = self.state[p]
+                if not state:
+                    state['step'] = torch.tensor(0.0)
+                    state['exp_avg'] = torch.zeros_like(p)
+                    state['exp_avg_sq'] = torch.zeros_like(p)
+                state['step'] += 1
+                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                _hip.call('rs_adam_step', p.data_ptr(), g.data_ptr(), state['exp_avg'].data_ptr(),
+                          state['exp_avg_sq'].data_ptr(), p.numel(), float(group['lr']), float(b1),
+                          float(b2), float(group['eps']), float(group['weight_decay']),
+                          int(state['step'].item()), None, float(self.grad_scale), None, 0, ops.stream())
+        return loss
+
+    def state_dict(self):
+        for st in self._flat_state.values():
+            step = float(st['step_dev'].item())  # authoritative (graph replays advance it)
+            for p in st['f'].params:
+                if p in self.state:
+                    self.state[p]['step'] = torch.tensor(step)
+        return super().state_dict()

@@ -1,0 +1,131 @@
+"""Per-entry-point kernel timing with HIP events on the launch stream, plus the algorithmic
+work (FLOPs / HBM bytes) of every rs_* call, for the bench's roofline line.
+
+Usage:
+    with KernelTimer() as kt:
+        step()
+    kt.summary()  -> {name: {'ms': total, 'launches': n, 'flops': F, 'bytes': B}}
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _hip
+
+
+def _gemm_work(a):
+    M, N, K = a[2], a[3], a[4]
+    beta = a[10]
+    return 2.0 * M * N * K, 4.0 * (M * K + K * N + M * N * (2 if beta != 0 else 1))
+
+
+def _attn_fwd_work(a):
+    B, L, d, H = a[4], a[5], a[6], a[7]
+    hd = d // H
+    # QK^T twice (max pass + sum pass) and PV
+    return 2.0 * B * H * L * L * hd * 3, 4.0 * (B * L * 3 * d + B * L * d + B * H * L)
+
+
+def _attn_bwd_work(a):
+    B, L, d, H = a[6], a[7], a[8], a[9]
+    hd = d // H
+    # pass 1 (lane/query): s, dp, dq; pass 2 (lane/key): s, dp, dk, dv
+    return 2.0 * B * H * L * L * hd * 7, 4.0 * (B * L * 3 * d * 2 + 2 * B * L * d + B * H * L)
+
+
+def _gather_work(a, bwd=False):
+    segs, nseg, rows = a[0], a[1], a[2]
+    byts = 0.0
+    for i in range(nseg):
+        s = segs[i]
+        if s.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL):
+            bag = s.bag if s.kind == _hip.RS_SEG_POOL else 1
+            byts += rows * bag * (s.dim * 4 + 8)  # rows + int64 ids
+        elif s.kind == _hip.RS_SEG_DENSE:
+            byts += rows * 4
+        else:
+            byts += rows * s.dim * 4
+        byts += rows * s.dim * 4  # concat slice written (fwd) / read (bwd)
+    return 0.0, byts
+
+
+def _ln_fwd_work(a):
+    M, N = a[7], a[8]
+    return 8.0 * M * N, 4.0 * M * N * 4
+
+
+def _ln_bwd_work(a):
+    M, N = a[8], a[9]
+    return 12.0 * M * N, 4.0 * M * N * 3
+
+
+def _bn_work(a, bwd=False):
+    G, Bg, C = (a[9], a[10], a[11])
+    n = G * Bg * C
+    return 6.0 * n, 4.0 * n * (4 if bwd else 3)
+
+
+def _adam_work(a):
+    n = a[4]
+    return 12.0 * n, 28.0 * n
+
+
+WORK = {
+    'rs_gemm_f32': _gemm_work,
+    'rs_attn_fwd': _attn_fwd_work,
+    'rs_attn_bwd': _attn_bwd_work,
+    'rs_gather_fwd': _gather_work,
+    'rs_gather_bwd': lambda a: _gather_work(a, True),
+    'rs_add_layernorm_fwd': _ln_fwd_work,
+    'rs_layernorm_bwd': _ln_bwd_work,
+    'rs_batchnorm_fwd': _bn_work,
+    'rs_batchnorm_bwd': lambda a: _bn_work(a, True),
+    'rs_adam_step': _adam_work,
+}
+
+
+class KernelTimer:
+    """Wraps _hip.call: an event pair on the current (launch) stream around every rs_* call."""
+
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        self._orig = _hip.call
+
+        def timed(name, *args):
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record(torch.cuda.current_stream())
+            rc = self._orig(name, *args)
+            e.record(torch.cuda.current_stream())
+            fl, by = WORK[name](args) if name in WORK else (0.0, 0.0)
+            self.records.append((name, s, e, fl, by))
+            return rc
+
+        _hip.call = timed
+        # modules imported `call` by name: patch those bindings too
+        from . import ops, functions, optim
+        self._patched = []
+        for mod in (ops, functions, optim):
+            if getattr(mod, 'call', None) is self._orig:
+                self._patched.append(mod)
+                mod.call = timed
+        return self
+
+    def __exit__(self, *exc):
+        _hip.call = self._orig
+        for mod in self._patched:
+            mod.call = self._orig
+        return False
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, s, e, fl, by in self.records:
+            d = out.setdefault(name, {'ms': 0.0, 'launches': 0, 'flops': 0.0, 'bytes': 0.0})
+            d['ms'] += s.elapsed_time(e)
+            d['launches'] += 1
+            d['flops'] += fl
+            d['bytes'] += by
+        return out

@@ -1,0 +1,290 @@
+"""Per-kernel numerics on the GPU against plain PyTorch fp32 references of the same op
+(index work bit-exact)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from recommendsystemproject_amd import _hip, ops
+from recommendsystemproject_amd.functions import _seg
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+
+
+def rnd(*shape, seed=0):
+    g = torch.Generator(device='cpu').manual_seed(seed)
+    return torch.randn(*shape, generator=g).to(DEV)
+
+
+@pytest.mark.parametrize('M,N,K', [(1, 1, 1), (5, 7, 3), (64, 64, 64), (130, 70, 40), (4096, 128, 128),
+                                   (3000, 192, 64), (192, 64, 20000)])
+@pytest.mark.parametrize('ta,tb', [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_transposes(M, N, K, ta, tb):
+    A = rnd(K, M, seed=1) if ta else rnd(M, K, seed=1)
+    B = rnd(N, K, seed=2) if tb else rnd(K, N, seed=2)
+    C = torch.empty(M, N, device=DEV)
+    ops.gemm(A, B, C, M, N, K, transA=ta, transB=tb, lda=A.stride(0), ldb=B.stride(0), ldc=N)
+    ref = (A.t() if ta else A).double() @ (B.t() if tb else B).double()
+    err = (C.double() - ref).abs().max().item()
+    assert err <= 1e-5 * math.sqrt(K) * max(1.0, ref.abs().max().item()), err
+
+
+def test_gemm_epilogues_and_split():
+    M, N, K = 777, 96, 64
+    x, W, b = rnd(M, K, seed=3), rnd(N, K, seed=4), rnd(N, seed=5)
+    pos = rnd(13, N, seed=6)
+    y = ops.linear_fwd(x, W, b, aux=pos, aux_mod=13)
+    ref = x @ W.t() + b + pos[torch.arange(M, device=DEV) % 13]
+    assert torch.allclose(y, ref, atol=1e-4, rtol=1e-5)
+    y = ops.linear_fwd(x, W, b, relu=True)
+    assert torch.allclose(y, torch.relu(x @ W.t() + b), atol=1e-4, rtol=1e-5)
+    dy = rnd(M, N, seed=7)
+    dx = ops.linear_bwd_input(dy, W, relu_mask_of=y, alpha=2.0)
+    assert torch.allclose(dx, 2.0 * (dy @ W) * (y > 0), atol=1e-4, rtol=1e-5)
+    dW = rnd(N, K, seed=8)
+    ref = dW + dy.t() @ x
+    ops.linear_bwd_weight(dy, x, dW, beta=1.0)
+    assert torch.allclose(dW, ref, atol=1e-3, rtol=1e-5)
+    for split in (1, 3, 16):
+        C = torch.zeros(N, K, device=DEV)
+        ops.gemm(dy, x, C, N, K, M, transA=1, transB=0, lda=N, ldb=K, ldc=K, split=split)
+        assert torch.allclose(C, dy.t() @ x, atol=1e-3, rtol=1e-5), split
+
+
+def test_colsum_deterministic():
+    X = rnd(20000, 70, seed=9)
+    out = torch.full((70,), 2.0, device=DEV)
+    ops.colsum(X, out, scale=0.5, beta=1.0)
+    assert torch.allclose(out, 2.0 + 0.5 * X.sum(0), atol=1e-3)
+    o1 = torch.zeros(70, device=DEV)
+    o2 = torch.zeros(70, device=DEV)
+    ops.colsum(X, o1)
+    ops.colsum(X, o2)
+    assert torch.equal(o1, o2)
+
+
+def test_gather_bit_exact_all_kinds():
+    B = 257
+    V1, D1 = 1000, 64
+    V2, D2, Lb = 30, 8, 3
+    t1, t2 = rnd(V1, D1, seed=1), rnd(V2, D2, seed=2)
+    t3 = rnd(11, 6, seed=3)  # odd width -> scalar path
+    ids = torch.randint(0, V1, (B, 2), device=DEV)
+    bag = torch.randint(0, V2, (B, Lb), device=DEV)
+    ids3 = torch.randint(0, 11, (B,), device=DEV)
+    w, bb, x = rnd(4, seed=4), rnd(4, seed=5), rnd(B, 1, seed=6)
+    src = rnd(B * 5, 8, seed=7)
+    last = torch.randint(0, 5, (B,), device=DEV)
+    outs = {}
+    for mode, red in (('mean', lambda e: e.mean(1)), ('sum', lambda e: e.sum(1)), ('max', lambda e: e.max(1)[0])):
+        segs = [
+            _seg(kind=_hip.RS_SEG_SPARSE, dim=D1, out_col=0, vocab=V1, idx_stride=2, idx=ids.data_ptr() + 8,
+                 table=t1.data_ptr()),
+            _seg(kind=_hip.RS_SEG_POOL, dim=D2, out_col=64, pool_mode=_hip.RS_POOL[mode], bag=Lb, vocab=V2,
+                 idx_stride=Lb, idx=bag.data_ptr(), table=t2.data_ptr()),
+            _seg(kind=_hip.RS_SEG_SPARSE, dim=6, out_col=72, vocab=11, idx_stride=1, idx=ids3.data_ptr(),
+                 table=t3.data_ptr()),
+            _seg(kind=_hip.RS_SEG_DENSE, dim=4, out_col=78, idx_stride=1, x=x.data_ptr(), table=w.data_ptr(),
+                 bias=bb.data_ptr()),
+            _seg(kind=_hip.RS_SEG_LASTVALID, dim=8, out_col=82, bag=5, idx=last.data_ptr(), table=src.data_ptr()),
+        ]
+        out = torch.empty(B, 90, device=DEV)
+        err = torch.zeros(1, dtype=torch.int32, device=DEV)
+        ops.gather_fwd(segs, B, out, err)
+        assert torch.equal(out[:, :64], t1[ids[:, 1]])
+        assert torch.allclose(out[:, 64:72], red(t2[bag]), atol=1e-6)
+        if mode == 'max':
+            assert torch.equal(out[:, 64:72], red(t2[bag]))
+        assert torch.equal(out[:, 72:78], t3[ids3])
+        assert torch.allclose(out[:, 78:82], x * w + bb, atol=1e-6)
+        assert torch.equal(out[:, 82:90], src.view(B, 5, 8)[torch.arange(B), last])
+        assert err.item() == 0
+        outs[mode] = out
+    bad = ids.clone()
+    bad[3, 1] = V1 + 5
+    segs = [_seg(kind=_hip.RS_SEG_SPARSE, dim=D1, out_col=0, vocab=V1, idx_stride=2, idx=bad.data_ptr() + 8,
+                 table=t1.data_ptr())]
+    out = torch.empty(B, 64, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ops.gather_fwd(segs, B, out, err)
+    assert err.item() == 1
+
+
+def test_gather_backward_matches_embedding_backward():
+    B, V, D, Lb = 500, 50, 16, 4
+    t = rnd(V, D, seed=1).requires_grad_(True)
+    bag = torch.randint(0, V, (B, Lb), device=DEV)
+    bag[:, 3] = 0  # padding slot
+    ids = torch.randint(0, V, (B,), device=DEV)
+    dout = rnd(B, 2 * D, seed=2)
+    ref_out = torch.cat([F.embedding(ids, t, padding_idx=0), F.embedding(bag, t, padding_idx=0).mean(1)], 1)
+    ref_out.backward(dout)
+    g = torch.zeros(V, D, device=DEV)
+    segs = [_seg(kind=_hip.RS_SEG_SPARSE, dim=D, out_col=0, vocab=V, idx_stride=1, idx=ids.data_ptr(),
+                 table=t.data_ptr(), grad=g.data_ptr(), pad_idx=0),
+            _seg(kind=_hip.RS_SEG_POOL, dim=D, out_col=D, pool_mode=0, bag=Lb, vocab=V, idx_stride=Lb,
+                 idx=bag.data_ptr(), table=t.data_ptr(), grad=g.data_ptr(), pad_idx=0)]
+    ops.gather_bwd(segs, B, dout)
+    assert torch.allclose(g, t.grad, atol=1e-5)
+    assert (g[0] == 0).all()
+
+
+def test_seq_mask_quirks():
+    seq = torch.tensor([[5, 3, 0, 0], [0, 0, 0, 0], [1, 2, 3, 4], [0, 7, 0, 0]], device=DEV)
+    key_pad, last = ops.seq_mask(seq, 0)
+    assert key_pad.tolist() == [[0, 0, 1, 1], [1, 1, 1, 0], [0, 0, 0, 0], [1, 0, 1, 1]]  # T6
+    assert last.tolist() == [1, 0, 3, 0]  # T7: count-based, all-pad row -> 0
+
+
+def ref_attention(qkv, key_pad, B, L, d, H):
+    hd = d // H
+    q, k, v = qkv.view(B, L, 3, H, hd).permute(2, 0, 3, 1, 4)
+    s = q @ k.transpose(-1, -2) / math.sqrt(hd)
+    s = s.masked_fill(key_pad.bool()[:, None, None, :], float('-inf'))
+    return (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * L, d)
+
+
+@pytest.mark.parametrize('B,L,d,H', [(3, 50, 64, 4), (2, 7, 64, 2), (5, 200, 64, 4), (4, 20, 32, 4)])
+def test_attention_fwd_bwd(B, L, d, H):
+    qkv = rnd(B * L, 3 * d, seed=1).requires_grad_(True)
+    lens = torch.randint(0, L + 1, (B,))
+    seq = (torch.arange(L)[None, :] < lens[:, None]).long().to(DEV)
+    key_pad, _ = ops.seq_mask(seq, 0)
+    ref = ref_attention(qkv, key_pad, B, L, d, H)
+    out, lse = ops.attn_fwd(qkv.detach(), key_pad, B, L, d, H)
+    assert torch.allclose(out, ref, atol=2e-5, rtol=1e-4)
+    dout = rnd(B * L, d, seed=2)
+    ref.backward(dout)
+    dqkv = ops.attn_bwd(qkv.detach(), key_pad, out, dout, lse, B, L, d, H)
+    assert torch.allclose(dqkv, qkv.grad, atol=5e-5, rtol=1e-4)
+
+
+def test_attention_dropout_consistent():
+    """Dropout on attention probabilities: fwd/bwd use the same mask (finite-difference check
+    of <dout, out> along a random direction) and the keep rate is ~1-p."""
+    B, L, d, H, p = 4, 30, 64, 4, 0.25
+    qkv = rnd(B * L, 3 * d, seed=3).double().float()
+    key_pad = torch.zeros(B, L, dtype=torch.uint8, device=DEV)
+    key = torch.tensor([1234, 7], dtype=torch.int64, device=DEV)
+    out, lse = ops.attn_fwd(qkv, key_pad, B, L, d, H, p, key, 3)
+    out0, _ = ops.attn_fwd(qkv, key_pad, B, L, d, H, 0.0)
+    assert not torch.allclose(out, out0)
+    dout = rnd(B * L, d, seed=4)
+    dq = ops.attn_bwd(qkv, key_pad, out, dout, lse, B, L, d, H, p, key, 3)
+    direc = rnd(B * L, 3 * d, seed=5)
+    eps = 1e-3
+    fp, _ = ops.attn_fwd(qkv + eps * direc, key_pad, B, L, d, H, p, key, 3)
+    fm, _ = ops.attn_fwd(qkv - eps * direc, key_pad, B, L, d, H, p, key, 3)
+    fd = ((fp - fm) * dout).sum().item() / (2 * eps)
+    an = (dq * direc).sum().item()
+    assert abs(fd - an) < 2e-2 * max(1.0, abs(an)), (fd, an)
+
+
+def test_layernorm_fwd_bwd():
+    M, N = 1000, 64
+    a, b = rnd(M, N, seed=1), rnd(M, N, seed=2)
+    g, be = rnd(N, seed=3), rnd(N, seed=4)
+    h_ref = (a + b).requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), be.clone().requires_grad_(True)
+    y_ref = F.layer_norm(h_ref, (N,), gr, br, 1e-5)
+    a2 = a.clone()
+    y, mean, rstd = ops.add_layernorm_fwd(a2, b, g, be)
+    assert torch.allclose(y, y_ref, atol=1e-5)
+    assert torch.allclose(a2, a + b)
+    dy = rnd(M, N, seed=5)
+    y_ref.backward(dy)
+    dg, db = torch.zeros(N, device=DEV), torch.zeros(N, device=DEV)
+    dh = ops.layernorm_bwd(a2, dy.clone(), g, mean, rstd, dg, db)
+    assert torch.allclose(dh, h_ref.grad, atol=1e-4)
+    assert torch.allclose(dg, gr.grad, atol=1e-3) and torch.allclose(db, br.grad, atol=1e-3)
+
+
+@pytest.mark.parametrize('G', [1, 3])
+@pytest.mark.parametrize('relu', [False, True])
+def test_batchnorm_train_fwd_bwd(G, relu):
+    Bg, C = 300, 172
+    bn = torch.nn.BatchNorm1d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.1 * rnd(C, seed=1))
+        bn.bias.copy_(0.1 * rnd(C, seed=2))
+    ref_bn = torch.nn.BatchNorm1d(C).to(DEV)
+    ref_bn.load_state_dict(bn.state_dict())
+    x = (rnd(G * Bg, C, seed=3) * 3 + 1)
+    y, mean, rstd = ops.batchnorm_fwd(x, bn, G, relu, training=True)
+    xr = x.clone().requires_grad_(True)
+    outs = [ref_bn(xr[g * Bg:(g + 1) * Bg]) for g in range(G)]
+    yr = torch.cat(outs)
+    if relu:
+        yr = torch.relu(yr)
+    assert torch.allclose(y, yr, atol=1e-5)
+    assert torch.allclose(bn.running_mean, ref_bn.running_mean, atol=1e-6)
+    assert torch.allclose(bn.running_var, ref_bn.running_var, atol=1e-5)
+    assert bn.num_batches_tracked.item() == ref_bn.num_batches_tracked.item() == G
+    dy = rnd(G * Bg, C, seed=4)
+    yr.backward(dy)
+    dw, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dx = ops.batchnorm_bwd(x, y, dy, bn.weight, mean, rstd, dw, db, G, relu)
+    assert torch.allclose(dx, xr.grad, atol=2e-5)
+    assert torch.allclose(dw, ref_bn.weight.grad, atol=1e-3) and torch.allclose(db, ref_bn.bias.grad, atol=1e-3)
+    bn.eval()
+    ref_bn.eval()
+    ye, _, _ = ops.batchnorm_fwd(x, bn, 1, False, training=False)
+    assert torch.allclose(ye, ref_bn(x), atol=1e-5)
+
+
+def test_l2norm():
+    x = rnd(500, 128, seed=1).requires_grad_(True)
+    x.data[3] = 0.0
+    yr = F.normalize(x, p=2, dim=1)
+    y, norm = ops.l2norm_fwd(x.detach())
+    assert torch.allclose(y, yr, atol=1e-6)
+    dy = rnd(500, 128, seed=2)
+    yr.backward(dy)
+    dx = ops.l2norm_bwd(y, norm, dy)
+    assert torch.allclose(dx, x.grad, atol=1e-4)
+
+
+def test_dropout_statistics_and_mask_reuse():
+    n, p = 1 << 20, 0.3
+    x = torch.ones(n // 64, 64, device=DEV)
+    key = torch.tensor([99, 5], dtype=torch.int64, device=DEV)
+    ops.dropout_fwd(x, p, key, 2)
+    kept = (x != 0).float().mean().item()
+    assert abs(kept - (1 - p)) < 3e-3
+    assert torch.allclose(x[x != 0], torch.full_like(x[x != 0], 1 / (1 - p)))
+    g = torch.ones_like(x)
+    ops.dropout_bwd(g, p, key, 2)
+    assert torch.equal(g, x)
+    state = torch.tensor([5, 0], dtype=torch.int64, device=DEV)
+    k1, k2 = ops.rng_next(state), ops.rng_next(state)
+    assert k1.tolist() == [5, 0] and k2.tolist() == [5, 1] and state.tolist() == [5, 2]
+
+
+def test_adam_matches_torch():
+    n = 10007
+    p0 = rnd(n, seed=1)
+    ours = p0.clone()
+    m, v = torch.zeros_like(p0), torch.zeros_like(p0)
+    tp = p0.clone().cpu().requires_grad_(True)
+    opt = torch.optim.Adam([tp], lr=1e-3, weight_decay=0.01)
+    for step in range(1, 4):
+        g = rnd(n, seed=10 + step)
+        tp.grad = g.cpu().clone()
+        opt.step()
+        _hip.call('rs_adam_step', ours.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9,
+                  0.999, 1e-8, 0.01, step, None, 1.0, None, 0, ops.stream())
+    assert torch.allclose(ours.cpu(), tp.detach(), atol=1e-6)
+
+
+def test_clip_coefficient():
+    g = rnd(100000, seed=1) * 0.01
+    ws = torch.empty(int(_hip.lib().rs_sqnorm_ws_bytes(g.numel())), dtype=torch.uint8, device=DEV)
+    norm = torch.zeros((), device=DEV)
+    coef = torch.zeros((), device=DEV)
+    _hip.call('rs_grad_sqnorm', g.data_ptr(), g.numel(), 0.5, ws.data_ptr(), ops.stream())
+    _hip.call('rs_clip_coef', ws.data_ptr(), g.numel(), 1.0, norm.data_ptr(), coef.data_ptr(), ops.stream())
+    tn = (0.5 * g).norm().item()
+    assert abs(norm.item() - tn) < 1e-5 * tn
+    assert abs(coef.item() - min(1.0, 1.0 / (tn + 1e-6))) < 1e-6
