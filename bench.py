@@ -220,6 +220,11 @@ def main():
             'cpu_baseline': cpu,
             'kernel_ms_per_step': {k: round(v['ms'] / 3, 4) for k, v in sorted(summ.items(), key=lambda kv: -kv[1]['ms'])},
         }
+        if os.environ.get('RSYS_BENCH_DETAIL'):
+            shp = sorted(kt.gemm_shapes().items(), key=lambda kv: -kv[1][0])
+            print(json.dumps({'gemm_shapes_ms_per_step': [
+                [list(k), round(v[0] / 3, 4), round(v[2] / (v[0] * 1e-3) / 1e12, 2) if v[0] else 0]
+                for k, v in shp[:24]]}), file=sys.stderr)
         print(json.dumps(out))
     if dist.is_initialized():
         dist.destroy_process_group()

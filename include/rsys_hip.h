@@ -34,7 +34,9 @@ int rs_device_check(void);            /* 0 if a gfx950 device is current, else h
  *   RS_EPI_AUX_MASK v = aux[m*ld_aux+n] > 0 ? v : 0         (ReLU backward)
  *   RS_EPI_RELU    v = max(v, 0)   (applied last)
  *   beta != 0      v += beta * C_old   (applied before RELU)
- * split_k > 1 needs ws of split_k*M*N floats (rs_gemm_ws_bytes).
+ * rowsum != NULL: rowsum[m] += alpha * sum_k op(A)[m, k] — fused into the staged A tiles; with
+ *   transA this is the bias gradient of a weight-gradient GEMM (dW = dY^T X, db = colsum dY).
+ * split_k > 1 needs the workspace rs_gemm_ws_bytes(M, N, K, split_k).
  * Replaces nn.Linear / addmm / matmul / bmm on the hot path: Tower.py:16-25,
  * SequenceFeatureProcessor.py:77, TransformerEncoderLayer in/out_proj + linear1/2
  * (SequenceEncoder.py:17-23), TwoTowerModel.py:95 (U @ I^T) and all their backwards. */
@@ -47,7 +49,7 @@ int64_t rs_gemm_ws_bytes(int M, int N, int K, int split_k);
 int rs_gemm_f32(int transA, int transB, int M, int N, int K, float alpha,
                 const float* A, int lda, const float* B, int ldb, float beta, float* C, int ldc,
                 int epilogue, const float* bias, const float* aux, int ld_aux, int aux_mod,
-                int split_k, float* ws, void* stream);
+                float* rowsum, int split_k, float* ws, void* stream);
 
 /* ---------------------------------------------------------------- column reductions
  * out[n] = beta*out[n] + scale * sum_{m<M} X[m*ldx + n]   (bias / pos-emb / LN grads)

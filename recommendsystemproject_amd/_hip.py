@@ -35,7 +35,7 @@ SIGNATURES = {
     'rs_gemm_auto_split': (i32, [i32, i32, i32]),
     'rs_gemm_ws_bytes': (i64, [i32, i32, i32, i32]),
     'rs_gemm_f32': (i32, [i32, i32, i32, i32, i32, f32, vp, i32, vp, i32, f32, vp, i32, i32, vp, vp,
-                          i32, i32, i32, vp, vp]),
+                          i32, i32, vp, i32, vp, vp]),
     'rs_colsum_ws_bytes': (i64, [i32, i32]),
     'rs_colsum': (i32, [vp, i32, i32, i32, f32, f32, vp, vp, vp]),
     'rs_gather_fwd': (i32, [vp, i32, i32, vp, i32, vp, vp]),

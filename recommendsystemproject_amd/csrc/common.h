@@ -53,6 +53,10 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// out[n] = beta*out[n] + scale * sum_{p<P} ws[p*N + n], fixed order (reduce.hip)
+int partials_reduce(const float* ws, int P, int N, float scale, float beta, float* out,
+                    hipStream_t st);
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }

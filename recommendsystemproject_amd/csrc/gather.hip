@@ -17,6 +17,10 @@ namespace rs {
 namespace {
 
 constexpr int kMaxSeg = 24;  // segments travel by value in the kernel arguments (~2.6 KB)
+// tables up to this size get their gradient accumulated in LDS first (privatised per workgroup,
+// then one global atomic per touched element): a 30-row genre table hit 600k times per step
+// would otherwise serialise on a few hundred addresses
+constexpr int64_t kSmallTableBytes = 48 * 1024;
 
 struct SegLaunch {
   rs_feature_seg_t segs[kMaxSeg];
@@ -30,6 +34,10 @@ struct SegLaunch {
   int rpb[kMaxSeg];   // rows per block
   int chunks[kMaxSeg];  // lanes per row
   int vec[kMaxSeg];
+  int small[kMaxSeg];   // bwd: table gradient accumulated in LDS (kernel gather_bwd_small)
+  int sblock_start[kMaxSeg + 1];
+  int sblocks[kMaxSeg];
+  int small_lds;        // bytes of dynamic LDS for the small-table kernel
 };
 
 __device__ __forceinline__ int find_seg(const SegLaunch& a, int bid) {
@@ -118,8 +126,10 @@ __global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
   else gather_seg<false>(a, sg, row, chunk);
 }
 
-template <bool VEC>
-__device__ void scatter_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int row, int chunk) {
+// LDS_ACC: accumulate into the workgroup-private LDS copy `lds` of the table gradient
+template <bool VEC, bool LDS_ACC = false>
+__device__ void scatter_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int row, int chunk,
+                            float* lds = nullptr) {
   constexpr int W = VEC ? 4 : 1;
   const int c = chunk * W;
   float g[4] = {0.f, 0.f, 0.f, 0.f};
@@ -127,7 +137,7 @@ __device__ void scatter_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int 
   if (sg.kind == RS_SEG_SPARSE) {
     const int64_t id = sg.idx[(int64_t)row * sg.idx_stride];
     if (id == sg.pad_idx || id < 0 || id >= sg.vocab) return;
-    float* d = sg.grad + id * sg.dim + c;
+    float* d = (LDS_ACC ? lds : sg.grad) + id * sg.dim + c;
 #pragma unroll
     for (int j = 0; j < W; ++j) atomicAdd(d + j, g[j]);
   } else if (sg.kind == RS_SEG_POOL) {
@@ -149,7 +159,7 @@ __device__ void scatter_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int 
 #pragma unroll
       for (int j = 0; j < W; ++j)
         if (arg[j] >= 0 && arg[j] != sg.pad_idx && arg[j] < sg.vocab)
-          atomicAdd(sg.grad + arg[j] * sg.dim + c + j, g[j]);
+          atomicAdd((LDS_ACC ? lds : sg.grad) + arg[j] * sg.dim + c + j, g[j]);
       return;
     }
     if (sg.pool_mode == RS_POOL_MEAN) {
@@ -160,7 +170,7 @@ __device__ void scatter_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int 
     for (int l = 0; l < sg.bag; ++l) {
       const int64_t id = ids[l];
       if (id == sg.pad_idx || id < 0 || id >= sg.vocab) continue;
-      float* d = sg.grad + id * sg.dim + c;
+      float* d = (LDS_ACC ? lds : sg.grad) + id * sg.dim + c;
 #pragma unroll
       for (int j = 0; j < W; ++j) atomicAdd(d + j, g[j]);
     }
@@ -179,7 +189,7 @@ __device__ void scatter_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int 
 __global__ __launch_bounds__(256) void gather_bwd_kernel(SegLaunch a) {
   const int s = find_seg(a, blockIdx.x);
   const rs_feature_seg_t& sg = a.segs[s];
-  if (sg.kind == RS_SEG_DENSE) return;
+  if (sg.kind == RS_SEG_DENSE || a.small[s]) return;
   const int lb = blockIdx.x - a.block_start[s];
   const int C = a.chunks[s];
   const int r = threadIdx.x / C, chunk = threadIdx.x % C;
@@ -188,6 +198,31 @@ __global__ __launch_bounds__(256) void gather_bwd_kernel(SegLaunch a) {
   if (row >= a.rows) return;
   if (a.vec[s]) scatter_seg<true>(a, sg, row, chunk);
   else scatter_seg<false>(a, sg, row, chunk);
+}
+
+__global__ __launch_bounds__(256) void gather_bwd_small_kernel(SegLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  int s = 0;
+  while (s + 1 < a.nseg && (int)blockIdx.x >= a.sblock_start[s + 1]) ++s;
+  const rs_feature_seg_t& sg = a.segs[s];
+  const int lb = blockIdx.x - a.sblock_start[s];
+  const int nblk = a.sblocks[s];
+  const int n = (int)(sg.vocab * sg.dim);
+  for (int e = threadIdx.x; e < n; e += 256) lds[e] = 0.f;
+  __syncthreads();
+  const int C = a.chunks[s];
+  const int r = threadIdx.x / C, chunk = threadIdx.x % C;
+  if (r < a.rpb[s]) {
+    for (int row = lb * a.rpb[s] + r; row < a.rows; row += nblk * a.rpb[s]) {
+      if (a.vec[s]) scatter_seg<true, true>(a, sg, row, chunk, lds);
+      else scatter_seg<false, true>(a, sg, row, chunk, lds);
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < n; e += 256) {
+    const float v = lds[e];
+    if (v != 0.f) atomicAdd(sg.grad + e, v);
+  }
 }
 
 // Linear(1, D) backward: dW[c] += sum_b dout[b,c]*x[b]; db[c] += sum_b dout[b,c].
@@ -220,7 +255,7 @@ __global__ __launch_bounds__(256) void dense_bwd_kernel(SegLaunch a) {
 }
 
 int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, int ldo,
-         const float* out_ptr_for_align) {
+         const float* out_ptr_for_align, bool bwd = false) {
   RS_CHECK_ARG(nseg >= 1 && nseg <= kMaxSeg, "gather: nseg %d out of [1,%d]", nseg, kMaxSeg);
   int blocks = 0;
   for (int s = 0; s < nseg; ++s) {
@@ -238,10 +273,29 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.vec[s] = vec;
     a.chunks[s] = C;
     a.rpb[s] = 256 / C;
+    const bool table_kind = g.kind == RS_SEG_SPARSE || g.kind == RS_SEG_POOL;
+    a.small[s] = bwd && table_kind && g.vocab * g.dim * 4 <= kSmallTableBytes;
     a.block_start[s] = blocks;
-    blocks += cdiv(rows, a.rpb[s]);
+    if (!a.small[s]) blocks += cdiv(rows, a.rpb[s]);
   }
   a.block_start[nseg] = blocks;
+  int sb = 0;
+  a.small_lds = 0;
+  for (int s = 0; s < nseg; ++s) {
+    a.sblock_start[s] = sb;
+    a.sblocks[s] = 0;
+    if (a.small[s]) {
+      const int64_t work = (int64_t)rows * (segs_host[s].kind == RS_SEG_POOL ? segs_host[s].bag : 1);
+      int nb = (int)(work / 2048);
+      nb = nb < 1 ? 1 : (nb > 256 ? 256 : nb);
+      const int maxnb = cdiv(rows, a.rpb[s]);
+      a.sblocks[s] = nb < maxnb ? nb : maxnb;
+      sb += a.sblocks[s];
+      const int bytes = (int)(segs_host[s].vocab * segs_host[s].dim * 4);
+      if (bytes > a.small_lds) a.small_lds = bytes;
+    }
+  }
+  a.sblock_start[nseg] = sb;
   a.nseg = nseg;
   a.rows = rows;
   a.ldo = ldo;
@@ -297,7 +351,7 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
   const rs_feature_seg_t* segs_host = segs;
   if (rows == 0) return 0;
   SegLaunch a;
-  RS_RET_IF(plan(a, segs_host, nseg, rows, ldo, dout));
+  RS_RET_IF(plan(a, segs_host, nseg, rows, ldo, dout, true));
   for (int s = 0; s < nseg; ++s) {
     const rs_feature_seg_t& g = segs_host[s];
     RS_CHECK_ARG(g.grad, "rs_gather_bwd: seg %d has no grad destination", s);
@@ -306,8 +360,14 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
   for (int i = 0; i < nseg; ++i) a.segs[i] = segs[i];
   a.out = nullptr; a.dout = dout; a.err = nullptr;
   hipStream_t st = as_stream(stream);
-  gather_bwd_kernel<<<a.block_start[nseg], 256, 0, st>>>(a);
-  RS_CHECK_LAUNCH("rs_gather_bwd");
+  if (a.block_start[nseg] > 0) {
+    gather_bwd_kernel<<<a.block_start[nseg], 256, 0, st>>>(a);
+    RS_CHECK_LAUNCH("rs_gather_bwd");
+  }
+  if (a.sblock_start[nseg] > 0) {
+    gather_bwd_small_kernel<<<a.sblock_start[nseg], 256, a.small_lds, st>>>(a);
+    RS_CHECK_LAUNCH("rs_gather_bwd small");
+  }
   bool any_dense = false;
   for (int s = 0; s < nseg; ++s) any_dense |= segs_host[s].kind == RS_SEG_DENSE;
   if (any_dense) {

@@ -35,6 +35,7 @@ struct GemmArgs {
   int ld_aux, aux_mod;
   int split_k, kchunk;
   float* ws;
+  float* rowsum;  // RS_EPI_ROWSUM_A: rowsum[m] += alpha * sum_k op(A)[m, k]
   int vecA, vecB;
 };
 
@@ -135,6 +136,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // fused row sums of op(A) (bias gradient of a weight-gradient GEMM): one n-tile column of
+  // workgroups, thread t < BM owns row m0 + t and reads its k-column of the staged A tile
+  const bool do_rowsum = a.rowsum != nullptr && blockIdx.y == 0 && tid < BM;
+  float rsum = 0.f;
 
   TileLoader<BM, TA> la;
   TileLoader<BN, !TB> lb;  // B(k, n): !TB is contiguous in n  ->  "T" layout of the loader
@@ -157,6 +162,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
     }
     const float* Asb = As[buf];
     const float* Bsb = Bs[buf];
+    if (do_rowsum) {
+#pragma unroll
+      for (int kk = 0; kk < BK; ++kk) rsum += Asb[kk * (BM + PAD) + tid];
+    }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       const int kr = kk + (lane >> 5);
@@ -179,6 +188,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
     buf ^= 1;
   }
 
+  if (do_rowsum && m0 + tid < a.M) {
+    if (a.split_k > 1) a.ws[(int64_t)a.split_k * a.M * a.N + (int64_t)z * a.M + m0 + tid] = a.alpha * rsum;
+    else a.rowsum[m0 + tid] += a.alpha * rsum;
+  }
   // epilogue: C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -204,10 +217,25 @@ __global__ void splitk_reduce_kernel(GemmArgs a) {
   const int64_t total = (int64_t)a.M * a.N;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    float v = 0.f;
-    for (int z = 0; z < a.split_k; ++z) v += a.ws[z * total + idx];
+    float v[8];
+    int z = 0;
+    float acc = 0.f;
+    // fixed order, 8 independent loads in flight
+    for (; z + 8 <= a.split_k; z += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = a.ws[(int64_t)(z + u) * total + idx];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; z < a.split_k; ++z) acc += a.ws[(int64_t)z * total + idx];
     const int m = (int)(idx / a.N), n = (int)(idx % a.N);
-    a.C[(int64_t)m * a.ldc + n] = epilogue(a, m, n, v);
+    a.C[(int64_t)m * a.ldc + n] = epilogue(a, m, n, acc);
+    if (a.rowsum && idx < a.M) {
+      const float* rs = a.ws + (int64_t)a.split_k * total;
+      float r = 0.f;
+      for (int zz = 0; zz < a.split_k; ++zz) r += rs[(int64_t)zz * a.M + idx];
+      a.rowsum[idx] += r;
+    }
   }
 }
 
@@ -239,13 +267,13 @@ extern "C" int rs_gemm_auto_split(int M, int N, int K) {
 
 extern "C" int64_t rs_gemm_ws_bytes(int M, int N, int K, int split_k) {
   (void)K;
-  return split_k > 1 ? (int64_t)split_k * M * N * (int64_t)sizeof(float) : 0;
+  return split_k > 1 ? (int64_t)split_k * ((int64_t)M * N + M) * (int64_t)sizeof(float) : 0;
 }
 
 extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float alpha,
                            const float* A, int lda, const float* B, int ldb, float beta, float* C,
                            int ldc, int epilogue, const float* bias, const float* aux, int ld_aux,
-                           int aux_mod, int split_k, float* ws, void* stream) {
+                           int aux_mod, float* rowsum, int split_k, float* ws, void* stream) {
   RS_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "rs_gemm_f32: negative size M=%d N=%d K=%d", M, N, K);
   if (M == 0 || N == 0) return 0;
   RS_CHECK_ARG(A && B && C, "rs_gemm_f32: null operand");
@@ -270,6 +298,7 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
   g.split_k = cdiv(K, g.kchunk);
   if (K == 0) { g.split_k = 1; g.kchunk = BK; }
   g.ws = ws;
+  g.rowsum = rowsum;
   g.vecA = (lda % 4 == 0) && aligned16(A);
   g.vecB = (ldb % 4 == 0) && aligned16(B);
   hipStream_t st = as_stream(stream);
@@ -282,6 +311,7 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
   RS_CHECK_LAUNCH("rs_gemm_f32");
   if (g.split_k > 1) {
     int64_t total = (int64_t)M * N;
+    if (total < M) total = M;
     int blocks = (int)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;
     splitk_reduce_kernel<<<blocks, 256, 0, st>>>(g);

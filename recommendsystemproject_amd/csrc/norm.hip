@@ -61,6 +61,9 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(float* __restrict__ a,
   if (lane == 0) { mean[row] = mu; rstd[row] = rs_; }
 }
 
+// LN backward: each wave owns groups of R = 4 rows (4x the loads in flight of a row-per-wave
+// loop), a grid-strided sweep over the rows, per-lane dgamma/dbeta partials in registers, one
+// fixed-order partial per workgroup -> partials_reduce (deterministic).
 template <int NPL, bool DROP>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ h,
                                                      const float* dy,
@@ -70,41 +73,65 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ h
                                                      int M, int N, float* __restrict__ ws,
                                                      float* __restrict__ da, float pdrop,
                                                      const int64_t* __restrict__ key, int site) {
+  constexpr int R = 4;
   DropKey dk;
   if (DROP) dk = make_key(key, site, pdrop);
   __shared__ float red[2][4][NPL * 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float pg[NPL], pb[NPL];
+  float gm[NPL], pg[NPL], pb[NPL];
 #pragma unroll
-  for (int i = 0; i < NPL; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
-  for (int row = blockIdx.x * 4 + wave; row < M; row += gridDim.x * 4) {
-    const float mu = mean[row], r = rstd[row];
-    float xh[NPL], g[NPL], dyv[NPL];
-    float s1 = 0.f, s2 = 0.f;
+  for (int i = 0; i < NPL; ++i) {
+    const int c = lane + i * 64;
+    gm[i] = c < N ? gamma[c] : 0.f;
+    pg[i] = 0.f;
+    pb[i] = 0.f;
+  }
+  const int waves = gridDim.x * 4;
+  for (int base = (blockIdx.x * 4 + wave) * R; base < M; base += waves * R) {
+    float xh[R][NPL], g[R][NPL], s1[R], s2[R];
 #pragma unroll
-    for (int i = 0; i < NPL; ++i) {
-      const int c = lane + i * 64;
-      xh[i] = 0.f; g[i] = 0.f; dyv[i] = 0.f;
-      if (c < N) {
-        const int64_t o = (int64_t)row * N + c;
-        xh[i] = (h[o] - mu) * r;
-        dyv[i] = dy[o];
-        g[i] = dyv[i] * gamma[c];
+    for (int r = 0; r < R; ++r) {
+      const int row = base + r;
+      const bool ok = row < M;
+      const float mu = ok ? mean[row] : 0.f, rr = ok ? rstd[row] : 0.f;
+      s1[r] = 0.f;
+      s2[r] = 0.f;
+#pragma unroll
+      for (int i = 0; i < NPL; ++i) {
+        const int c = lane + i * 64;
+        float hv = 0.f, d = 0.f;
+        if (ok && c < N) {
+          const int64_t o = (int64_t)row * N + c;
+          hv = h[o];
+          d = dy[o];
+        }
+        xh[r][i] = (hv - mu) * rr;
+        pg[i] += d * xh[r][i];
+        pb[i] += d;
+        g[r][i] = d * gm[i];
+        s1[r] += g[r][i];
+        s2[r] += g[r][i] * xh[r][i];
       }
-      s1 += g[i];
-      s2 += g[i] * xh[i];
-      pg[i] += dyv[i] * xh[i];
-      pb[i] += dyv[i];
     }
-    const float m1 = wave_sum(s1) / (float)N, m2 = wave_sum(s2) / (float)N;
 #pragma unroll
-    for (int i = 0; i < NPL; ++i) {
-      const int c = lane + i * 64;
-      if (c < N) {
-        const int64_t o = (int64_t)row * N + c;
-        const float v = r * (g[i] - m1 - xh[i] * m2);
-        dh[o] = v;
-        if (da) da[o] = DROP ? v * keep_mult(dk, (uint64_t)o) : v;
+    for (int r = 0; r < R; ++r) {
+      s1[r] = wave_sum(s1[r]) / (float)N;
+      s2[r] = wave_sum(s2[r]) / (float)N;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int row = base + r;
+      if (row >= M) break;
+      const float rr = rstd[row];
+#pragma unroll
+      for (int i = 0; i < NPL; ++i) {
+        const int c = lane + i * 64;
+        if (c < N) {
+          const int64_t o = (int64_t)row * N + c;
+          const float v = rr * (g[r][i] - s1[r] - xh[r][i] * s2[r]);
+          dh[o] = v;
+          if (da) da[o] = DROP ? v * keep_mult(dk, (uint64_t)o) : v;
+        }
       }
     }
   }
@@ -118,24 +145,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ h
     float sg = 0.f, sb = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) { sg += red[0][w][c]; sb += red[1][w][c]; }
-    ws[(int64_t)blockIdx.x * 2 * N + c] = sg;
-    ws[(int64_t)blockIdx.x * 2 * N + N + c] = sb;
+    ws[(int64_t)blockIdx.x * N + c] = sg;                          // dgamma partials [nb][N]
+    ws[(int64_t)gridDim.x * N + (int64_t)blockIdx.x * N + c] = sb; // dbeta partials  [nb][N]
   }
 }
 
-__global__ void ln_bwd_final_kernel(const float* __restrict__ ws, int nb, int N,
-                                    float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  float sg = 0.f, sb = 0.f;
-  for (int b = 0; b < nb; ++b) { sg += ws[(int64_t)b * 2 * N + c]; sb += ws[(int64_t)b * 2 * N + N + c]; }
-  dgamma[c] += sg;
-  dbeta[c] += sb;
-}
-
 int ln_blocks(int M) {
-  int nb = cdiv(M, 4 * 8);  // >= 8 rows per wave
-  if (nb > 1024) nb = 1024;
+  int nb = cdiv(M, 4 * 4 * 4);  // >= 4 row groups per wave
+  if (nb > 2048) nb = 2048;
   if (nb < 1) nb = 1;
   return nb;
 }
@@ -419,9 +436,8 @@ extern "C" int rs_layernorm_bwd(const float* h, const float* dy, const float* ga
   RS_NPL_DROP_DISPATCH(npl, p > 0.f, ln_bwd_kernel, nb, h, dy, gamma, mean, rstd, dh, M, N, ws, da, p,
                        key, site);
   RS_CHECK_LAUNCH("rs_layernorm_bwd");
-  ln_bwd_final_kernel<<<cdiv(N, 256), 256, 0, st>>>(ws, nb, N, dgamma, dbeta);
-  RS_CHECK_LAUNCH("rs_layernorm_bwd final");
-  return 0;
+  RS_RET_IF(partials_reduce(ws, nb, N, 1.f, 1.f, dgamma, st));
+  return partials_reduce(ws + (int64_t)nb * N, nb, N, 1.f, 1.f, dbeta, st);
 }
 
 extern "C" int64_t rs_batchnorm_ws_bytes(int G, int Bg, int C) {

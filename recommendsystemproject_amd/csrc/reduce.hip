@@ -5,45 +5,79 @@
 
 namespace rs {
 
+// Partial-sum geometry: a chunk of rows per workgroup; 64 columns x 4 row lanes per workgroup.
 int colsum_chunks(int M) {
-  int s = cdiv(M, 256);
+  int s = cdiv(M, 128);
+  if (s > 1024) s = 1024;
   if (s < 1) s = 1;
-  if (s > 512) s = 512;
   return s;
+}
+
+// out[n] = beta*out[n] + scale * sum_p ws[p*N + n] — 64 columns x 16 lanes per workgroup, each
+// lane sums every 16th partial with 8 loads in flight, then a fixed-order LDS tree: bitwise
+// reproducible and not latency-bound for thousands of partials.
+__global__ __launch_bounds__(1024) void partials_reduce_kernel(const float* __restrict__ ws, int P,
+                                                               int N, float scale, float beta,
+                                                               float* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int l = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (c < N) {
+    int p = l;
+    for (; p + 16 * 7 < P; p += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ws[(int64_t)(p + 16 * u) * N + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; p < P; p += 16) acc += ws[(int64_t)p * N + c];
+  }
+  red[l][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (l == 0 && c < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
+    out[c] = (beta != 0.f ? beta * out[c] : 0.f) + scale * t;
+  }
+}
+
+int partials_reduce(const float* ws, int P, int N, float scale, float beta, float* out,
+                    hipStream_t st) {
+  partials_reduce_kernel<<<cdiv(N, 64), 1024, 0, st>>>(ws, P, N, scale, beta, out);
+  RS_CHECK_LAUNCH("partials_reduce");
+  return 0;
 }
 
 namespace {
 
-template <int TPR>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ X, int M,
                                                              int N, int ldx, int rows_per_chunk,
                                                              float* __restrict__ ws) {
-  constexpr int RL = 256 / TPR;
-  __shared__ float red[256];
-  const int c = blockIdx.x * TPR + (threadIdx.x % TPR);
-  const int rl = threadIdx.x / TPR;
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
   const int s = blockIdx.y;
   const int r0 = s * rows_per_chunk, r1 = min(M, r0 + rows_per_chunk);
   float acc = 0.f;
-  if (c < N)
-    for (int m = r0 + rl; m < r1; m += RL) acc += X[(int64_t)m * ldx + c];
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  if (rl == 0 && c < N) {
-    float v = 0.f;
+  if (c < N) {
+    int m = r0 + rl;
+    for (; m + 4 * 7 < r1; m += 4 * 8) {
+      float v[8];
 #pragma unroll
-    for (int i = 0; i < RL; ++i) v += red[i * TPR + (threadIdx.x % TPR)];
-    ws[(int64_t)s * N + c] = v;
+      for (int u = 0; u < 8; ++u) v[u] = X[(int64_t)(m + 4 * u) * ldx + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; m < r1; m += 4) acc += X[(int64_t)m * ldx + c];
   }
-}
-
-__global__ void colsum_final_kernel(const float* __restrict__ ws, int S, int N, float scale,
-                                    float beta, float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  float v = 0.f;
-  for (int s = 0; s < S; ++s) v += ws[(int64_t)s * N + c];
-  out[c] = (beta != 0.f ? beta * out[c] : 0.f) + scale * v;
+  red[rl][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rl == 0 && c < N)
+    ws[(int64_t)s * N + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                             red[3][threadIdx.x];
 }
 
 __global__ __launch_bounds__(1024) void sum_kernel(const float* __restrict__ x, int n, float scale,
@@ -67,17 +101,9 @@ int colsum_launch(const float* X, int M, int N, int ldx, float scale, float beta
                   float* ws, hipStream_t st) {
   const int S = colsum_chunks(M);
   const int rpc = cdiv(M, S);
-  if (N <= 64) {
-    colsum_partial_kernel<64><<<dim3(cdiv(N, 64), S), 256, 0, st>>>(X, M, N, ldx, rpc, ws);
-  } else if (N <= 128) {
-    colsum_partial_kernel<128><<<dim3(cdiv(N, 128), S), 256, 0, st>>>(X, M, N, ldx, rpc, ws);
-  } else {
-    colsum_partial_kernel<256><<<dim3(cdiv(N, 256), S), 256, 0, st>>>(X, M, N, ldx, rpc, ws);
-  }
+  colsum_partial_kernel<<<dim3(cdiv(N, 64), S), 256, 0, st>>>(X, M, N, ldx, rpc, ws);
   RS_CHECK_LAUNCH("colsum partial");
-  colsum_final_kernel<<<cdiv(N, 256), 256, 0, st>>>(ws, S, N, scale, beta, out);
-  RS_CHECK_LAUNCH("colsum final");
-  return 0;
+  return partials_reduce(ws, S, N, scale, beta, out, st);
 }
 
 }  // namespace rs

@@ -109,8 +109,7 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key):
     if p > 0:
         ops.dropout_bwd(dx, p, key, 0)
     lin = proc.feature_projection[0]
-    ops.linear_bwd_weight(dx, cat, grad_of(lin.weight))
-    ops.colsum(dx, grad_of(lin.bias))
+    ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
     dcat = ops.linear_bwd_input(dx, lin.weight)
     for s, t in zip(segs, tables):
         s.grad = grad_of(t).data_ptr()
@@ -145,25 +144,21 @@ def layer_bwd(lyr, saved, dx2, key_pad, B, L, d, H, p, key, site):
     dh2 = ops.layernorm_bwd(h2, dx2, lyr.norm2.weight, m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias),
                             da=dff, p=p, key=key, site=site + 3)
     dff = dh2 if dff is None else dff
-    ops.linear_bwd_weight(dff, f1, g(lyr.linear2.weight))
-    ops.colsum(dff, g(lyr.linear2.bias))
+    ops.linear_bwd_weight(dff, f1, g(lyr.linear2.weight), db=g(lyr.linear2.bias))
     # f1 holds relu(.) after dropout: (f1 > 0) == kept & positive, kept scale 1/(1-p)
     df1 = ops.linear_bwd_input(dff, lyr.linear2.weight, relu_mask_of=f1,
                                alpha=(1.0 / (1.0 - p)) if p > 0 else 1.0)
-    ops.linear_bwd_weight(df1, x1, g(lyr.linear1.weight))
-    ops.colsum(df1, g(lyr.linear1.bias))
+    ops.linear_bwd_weight(df1, x1, g(lyr.linear1.weight), db=g(lyr.linear1.bias))
     ops.linear_bwd_input(df1, lyr.linear1.weight, out=dh2, beta=1.0)  # dx1 = dh2 + df1 W1
     # x1 = LN1(x + drop1(sa))
     dsa = torch.empty_like(dh2) if p > 0 else None
     dh1 = ops.layernorm_bwd(h1, dh2, lyr.norm1.weight, m1, r1, g(lyr.norm1.weight), g(lyr.norm1.bias),
                             da=dsa, p=p, key=key, site=site + 1)
     dsa = dh1 if dsa is None else dsa
-    ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight))
-    ops.colsum(dsa, g(sa_mod.out_proj.bias))
+    ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
     datt = ops.linear_bwd_input(dsa, sa_mod.out_proj.weight)
     dqkv = ops.attn_bwd(qkv, key_pad, att, datt, lse, B, L, d, H, p, key, site)
-    ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight))
-    ops.colsum(dqkv, g(sa_mod.in_proj_bias))
+    ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
     ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight, out=dh1, beta=1.0)  # dx = dh1 + dqkv Win
     return dh1
 
@@ -420,8 +415,7 @@ class MLPFn(torch.autograd.Function):
         g = grad_of
         last = seq[len(seq) - 1]
         dz = ops.l2norm_bwd(ctx.out, ctx.norm, dout.contiguous())
-        ops.linear_bwd_weight(dz, ctx.h_last, g(last.weight))
-        ops.colsum(dz, g(last.bias))
+        ops.linear_bwd_weight(dz, ctx.h_last, g(last.weight), db=g(last.bias))
         dh = ops.linear_bwd_input(dz, last.weight)
         for j in reversed(range(len(ctx.saved))):
             h, z, y, mean, rstd = ctx.saved[j]
@@ -431,8 +425,7 @@ class MLPFn(torch.autograd.Function):
             # y is post-ReLU (post-dropout): y > 0 <=> kept and positive
             dz = ops.batchnorm_bwd(z, y, dh, bn.weight, mean, rstd, g(bn.weight), g(bn.bias), ctx.G,
                                    relu=True)
-            ops.linear_bwd_weight(dz, h, g(lin.weight))
-            ops.colsum(dz, g(lin.bias))
+            ops.linear_bwd_weight(dz, h, g(lin.weight), db=g(lin.bias))
             dh = ops.linear_bwd_input(dz, lin.weight)
         ctx.saved = None
         return (None, None, dh, None) + (None,) * (len(ctx.needs_input_grad) - 4)

@@ -27,7 +27,7 @@ def ws(nbytes: int, device) -> torch.Tensor:
 
 
 def gemm(A, B, C, M, N, K, *, transA, transB, lda, ldb, ldc, alpha=1.0, beta=0.0, epi=0,
-         bias=None, aux=None, ld_aux=0, aux_mod=0, split=None):
+         bias=None, aux=None, ld_aux=0, aux_mod=0, split=None, rowsum=None):
     L = _hip.lib()
     if split is None:
         split = L.rs_gemm_auto_split(M, N, K)
@@ -35,7 +35,7 @@ def gemm(A, B, C, M, N, K, *, transA, transB, lda, ldb, ldc, alpha=1.0, beta=0.0
     if split > 1:
         w = ws(L.rs_gemm_ws_bytes(M, N, K, split), C.device)
     call('rs_gemm_f32', int(transA), int(transB), M, N, K, float(alpha), P(A), lda, P(B), ldb,
-         float(beta), P(C), ldc, epi, P(bias), P(aux), ld_aux, aux_mod, split, P(w), stream())
+         float(beta), P(C), ldc, epi, P(bias), P(aux), ld_aux, aux_mod, P(rowsum), split, P(w), stream())
     return C
 
 
@@ -64,12 +64,12 @@ def linear_bwd_input(dy, W, out=None, *, beta=0.0, relu_mask_of=None, alpha=1.0)
                 ld_aux=(relu_mask_of.stride(0) if relu_mask_of is not None else 0))
 
 
-def linear_bwd_weight(dy, x, dW, *, beta=1.0):
-    """dW[N,K] (+)= dy[M,N]^T @ x[M,K] (reduction over M, split-K)."""
+def linear_bwd_weight(dy, x, dW, *, beta=1.0, db=None):
+    """dW[N,K] (+)= dy[M,N]^T @ x[M,K] (reduction over M, split-K); db[N] += colsum(dy) fused."""
     M, N = dy.shape
     K = x.shape[1]
     return gemm(dy, x, dW, N, K, M, transA=1, transB=0, lda=dy.stride(0), ldb=x.stride(0),
-                ldc=dW.stride(0), beta=beta)
+                ldc=dW.stride(0), beta=beta, rowsum=db)
 
 
 def colsum(X, out, *, scale=1.0, beta=1.0, M=None, N=None, ldx=None):

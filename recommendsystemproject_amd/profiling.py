@@ -100,7 +100,8 @@ class KernelTimer:
             rc = self._orig(name, *args)
             e.record(torch.cuda.current_stream())
             fl, by = WORK[name](args) if name in WORK else (0.0, 0.0)
-            self.records.append((name, s, e, fl, by))
+            shape = tuple(args[:5]) if name == 'rs_gemm_f32' else None
+            self.records.append((name, s, e, fl, by, shape))
             return rc
 
         _hip.call = timed
@@ -119,10 +120,23 @@ class KernelTimer:
             mod.call = self._orig
         return False
 
+    def gemm_shapes(self):
+        """{(transA, transB, M, N, K): [ms, launches, flops]} for rs_gemm_f32."""
+        torch.cuda.synchronize()
+        out = {}
+        for name, s, e, fl, by, shape in self.records:
+            if shape is None:
+                continue
+            d = out.setdefault(shape, [0.0, 0, 0.0])
+            d[0] += s.elapsed_time(e)
+            d[1] += 1
+            d[2] += fl
+        return out
+
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for name, s, e, fl, by in self.records:
+        for name, s, e, fl, by, _ in self.records:
             d = out.setdefault(name, {'ms': 0.0, 'launches': 0, 'flops': 0.0, 'bytes': 0.0})
             d['ms'] += s.elapsed_time(e)
             d['launches'] += 1

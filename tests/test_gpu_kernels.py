@@ -41,16 +41,21 @@ def test_gemm_epilogues_and_split():
     y = ops.linear_fwd(x, W, b, relu=True)
     assert torch.allclose(y, torch.relu(x @ W.t() + b), atol=1e-4, rtol=1e-5)
     dy = rnd(M, N, seed=7)
-    dx = ops.linear_bwd_input(dy, W, relu_mask_of=y, alpha=2.0)
-    assert torch.allclose(dx, 2.0 * (dy @ W) * (y > 0), atol=1e-4, rtol=1e-5)
+    mask_src = rnd(M, K, seed=11)
+    dx = ops.linear_bwd_input(dy, W, relu_mask_of=mask_src, alpha=2.0)
+    assert torch.allclose(dx, 2.0 * (dy @ W) * (mask_src > 0), atol=1e-4, rtol=1e-5)
     dW = rnd(N, K, seed=8)
-    ref = dW + dy.t() @ x
-    ops.linear_bwd_weight(dy, x, dW, beta=1.0)
+    db = rnd(N, seed=12)
+    ref, refb = dW + dy.t() @ x, db + dy.sum(0)
+    ops.linear_bwd_weight(dy, x, dW, beta=1.0, db=db)
     assert torch.allclose(dW, ref, atol=1e-3, rtol=1e-5)
+    assert torch.allclose(db, refb, atol=1e-3, rtol=1e-5)
     for split in (1, 3, 16):
         C = torch.zeros(N, K, device=DEV)
-        ops.gemm(dy, x, C, N, K, M, transA=1, transB=0, lda=N, ldb=K, ldc=K, split=split)
+        rs = torch.zeros(N, device=DEV)
+        ops.gemm(dy, x, C, N, K, M, transA=1, transB=0, lda=N, ldb=K, ldc=K, split=split, rowsum=rs)
         assert torch.allclose(C, dy.t() @ x, atol=1e-3, rtol=1e-5), split
+        assert torch.allclose(rs, dy.sum(0), atol=1e-3, rtol=1e-5), split
 
 
 def test_colsum_deterministic():
@@ -112,8 +117,9 @@ def test_gather_bit_exact_all_kinds():
     assert err.item() == 1
 
 
-def test_gather_backward_matches_embedding_backward():
-    B, V, D, Lb = 500, 50, 16, 4
+@pytest.mark.parametrize('V', [50, 5000])  # LDS-privatised small table / global atomics
+def test_gather_backward_matches_embedding_backward(V):
+    B, D, Lb = 3000, 16, 4
     t = rnd(V, D, seed=1).requires_grad_(True)
     bag = torch.randint(0, V, (B, Lb), device=DEV)
     bag[:, 3] = 0  # padding slot
