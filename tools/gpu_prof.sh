@@ -1,0 +1,16 @@
+#!/bin/bash
+# rocprofv3 kernel-trace stats + separate PMC passes (FETCH_SIZE, WRITE_SIZE) of a short bench.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+mkdir -p gpurun_out/prof
+export TMPDIR=/tmp
+B="bench.py --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline ${BENCH_ARGS}"
+( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $ROOT/gpurun_out/prof/trace -o run --output-format csv -- python3 $ROOT/$B ) > gpurun_out/prof/trace.log 2>&1
+rc=$?; echo "trace rc=$rc"; tail -3 gpurun_out/prof/trace.log; [ $rc -eq 0 ] || exit $rc
+if [ -n "$PMC" ]; then
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  ( cd /tmp && timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace -d $ROOT/gpurun_out/prof/pmc_$ctr -o run --output-format csv -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-graph ${BENCH_ARGS} ) > gpurun_out/prof/pmc_$ctr.log 2>&1
+  rc=$?; echo "pmc $ctr rc=$rc"; tail -2 gpurun_out/prof/pmc_$ctr.log; [ $rc -eq 0 ] || exit $rc
+done
+fi
+find gpurun_out/prof -name '*.csv' | head -20
