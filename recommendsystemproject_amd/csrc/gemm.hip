@@ -249,6 +249,28 @@ void launch_tile(const GemmArgs& g, int ta, int tb, hipStream_t st) {
 }
 
 }  // namespace
+
+// gemm_stream.hip
+struct StreamArgs {
+  int M, N, K;
+  float alpha, beta;
+  const float* A; int lda;
+  const float* B; int ldb;
+  float* C; int ldc;
+  int epi;
+  const float* bias;
+  const float* aux; int ld_aux, aux_mod;
+  float* rowsum;
+  float* ws;
+  int transB;
+};
+bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda);
+int rowgemm_launch(const StreamArgs& s, hipStream_t st);
+bool wgrad_supported(int transA, int transB, int M, int N, int K, const float* A, int lda,
+                     const float* B, int ldb, int ldc, int epi);
+int64_t wgrad_ws_bytes(int M, int N, int K);
+int wgrad_launch(const StreamArgs& s, hipStream_t st);
+
 }  // namespace rs
 
 using namespace rs;
@@ -266,8 +288,12 @@ extern "C" int rs_gemm_auto_split(int M, int N, int K) {
 }
 
 extern "C" int64_t rs_gemm_ws_bytes(int M, int N, int K, int split_k) {
-  (void)K;
-  return split_k > 1 ? (int64_t)split_k * ((int64_t)M * N + M) * (int64_t)sizeof(float) : 0;
+  int64_t b = split_k > 1 ? (int64_t)split_k * ((int64_t)M * N + M) * (int64_t)sizeof(float) : 0;
+  if (K >= 8192) {  // the weight-gradient streaming kernel may be chosen (gemm_stream.hip)
+    const int64_t w = wgrad_ws_bytes(M, N, K);
+    if (w > b) b = w;
+  }
+  return b;
 }
 
 extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float alpha,
@@ -302,6 +328,16 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
   g.vecA = (lda % 4 == 0) && aligned16(A);
   g.vecB = (ldb % 4 == 0) && aligned16(B);
   hipStream_t st = as_stream(stream);
+  {
+    StreamArgs sa;
+    sa.M = M; sa.N = N; sa.K = K; sa.alpha = alpha; sa.beta = beta; sa.A = A; sa.lda = lda;
+    sa.B = B; sa.ldb = ldb; sa.C = C; sa.ldc = ldc; sa.epi = epilogue; sa.bias = bias;
+    sa.aux = aux; sa.ld_aux = ld_aux; sa.aux_mod = g.aux_mod; sa.rowsum = rowsum; sa.ws = ws;
+    sa.transB = transB;
+    if (!rowsum && rowgemm_supported(transA, M, N, K, A, lda)) return rowgemm_launch(sa, st);
+    if (ws && wgrad_supported(transA, transB, M, N, K, A, lda, B, ldb, ldc, epilogue))
+      return wgrad_launch(sa, st);
+  }
   const bool bigM = M >= 2048;
   const bool wideN = N > 64;
   if (bigM && wideN) launch_tile<128, 128>(g, transA, transB, st);

@@ -1,0 +1,366 @@
+// Streaming fp32 GEMMs for the encoder's big-M shapes (M = B*L = 204,800 tokens, K, N <= 256),
+// selected automatically by rs_gemm_f32.
+//
+// rowgemm: C[M,N] = A[M,K] @ op(B)  (A row-major; B = W[N][K] (nn.Linear forward) or W[K][N]
+//   (input gradient)). The whole op(B) (<= 256 x 256 fp32) is staged ONCE per persistent
+//   workgroup into LDS as Bs[n][k]; each wave streams 16-row groups of A straight from HBM into
+//   registers with 16-byte loads and keeps all N columns of its 16 rows in accumulators.
+//   v_mfma_f32_16x16x4_f32 with a permuted k order: lane (r = l&15, q = l>>4) loads
+//   A[r][16t+4q .. +3] as one float4 and feeds element s to the s-th MFMA of chunk t, whose k slot
+//   q then stands for k = 16t + 4q + s; the B fragment for the same lane is the float4
+//   Bs[n][16t+4q .. +3] (one ds_read_b128). Sums over k are order-free, so every A byte is read
+//   once, coalesced, with no LDS round trip; the next row group is prefetched under the MFMAs.
+// wgrad: dW[Mo,No] = dY^T X over a long M (weight gradients). One workgroup owns the whole dW
+//   tile (Mo*No <= 16K floats in accumulators) for a chunk of rows; dY and X chunks are staged
+//   k-major exactly as they lie in memory (no transposition), partial tiles are summed by a
+//   fixed-order reduce (deterministic), and the bias gradient colsum(dY) is fused.
+#include "common.h"
+
+namespace rs {
+
+struct StreamArgs {
+  int M, N, K;
+  float alpha, beta;
+  const float* A; int lda;
+  const float* B; int ldb;
+  float* C; int ldc;
+  int epi;
+  const float* bias;
+  const float* aux; int ld_aux, aux_mod;
+  float* rowsum;
+  float* ws;
+  int transB;
+};
+
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float epi_apply(const StreamArgs& a, int m, int n, float v) {
+  if (a.epi & RS_EPI_BIAS) v += a.bias[n];
+  if (a.epi & RS_EPI_AUX_ADD) v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
+  if (a.epi & RS_EPI_AUX_MASK) v = a.aux[(int64_t)m * a.ld_aux + n] > 0.f ? v : 0.f;
+  if (a.beta != 0.f) v += a.beta * a.C[(int64_t)m * a.ldc + n];
+  if (a.epi & RS_EPI_RELU) v = fmaxf(v, 0.f);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------- rowgemm
+template <int NT, int KT>
+__global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
+  constexpr int KP = KT * 16 + 4;  // LDS pitch (floats): conflict-free ds_read_b128 per 16 lanes
+  constexpr bool PREFETCH = KT <= 8;
+  extern __shared__ __attribute__((aligned(16))) float Bs[];  // [NT*16][KP]
+  const int tid = threadIdx.x;
+  // stage op(B) as Bs[n][k], zero padded to NT*16 x KT*16
+  if (a.transB) {  // B[n*ldb + k]: consecutive threads -> consecutive k
+    for (int idx = tid; idx < NT * 16 * KT * 16; idx += 512) {
+      const int n = idx / (KT * 16), k = idx % (KT * 16);
+      Bs[n * KP + k] = (n < a.N && k < a.K) ? a.B[(int64_t)n * a.ldb + k] : 0.f;
+    }
+  } else {  // B[k*ldb + n]: consecutive threads -> consecutive n
+    for (int idx = tid; idx < NT * 16 * KT * 16; idx += 512) {
+      const int k = idx / (NT * 16), n = idx % (NT * 16);
+      Bs[n * KP + k] = (n < a.N && k < a.K) ? a.B[(int64_t)k * a.ldb + n] : 0.f;
+    }
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int groups = (a.M + 15) / 16;
+  const int stride = gridDim.x * 8;
+  int g = blockIdx.x * 8 + wave;
+  floatx4 areg[KT];
+  auto load_group = [&](int gg, floatx4* dst) {
+    const int m = gg * 16 + r;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      const int k = 16 * t + 4 * q;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (m < a.M && k < a.K) v = *reinterpret_cast<const floatx4*>(a.A + (int64_t)m * a.lda + k);
+      dst[t] = v;
+    }
+  };
+  if (g < groups) load_group(g, areg);
+  for (; g < groups; g += stride) {
+    floatx4 anext[PREFETCH ? KT : 1];
+    if (PREFETCH && g + stride < groups) load_group(g + stride, anext);
+    // N tiles in pairs: two independent accumulator chains hide the 40-cycle dependent MFMA
+    // latency; each pair is stored right away so only 8 accumulators are ever live
+#pragma unroll
+    for (int j0 = 0; j0 < NT; j0 += 2) {
+      // keep the scheduler from hoisting every pair's B reads / accumulators (register spills)
+      __builtin_amdgcn_sched_barrier(0);
+      const bool two = j0 + 1 < NT;
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const floatx4 b0 = *reinterpret_cast<const floatx4*>(&Bs[(j0 * 16 + r) * KP + 16 * t + 4 * q]);
+        floatx4 b1 = b0;
+        if (two) b1 = *reinterpret_cast<const floatx4*>(&Bs[((j0 + 1) * 16 + r) * KP + 16 * t + 4 * q]);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(areg[t][s4], b0[s4], acc0, 0, 0, 0);
+          if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(areg[t][s4], b1[s4], acc1, 0, 0, 0);
+        }
+      }
+      // C/D map of 16x16: col = lane&15, row = 4*(lane>>4) + i
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
+        const int n = (j0 + h) * 16 + r;
+        if (n >= a.N) continue;
+        const floatx4 acc = h ? acc1 : acc0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = g * 16 + 4 * q + i;
+          if (m < a.M) a.C[(int64_t)m * a.ldc + n] = epi_apply(a, m, n, a.alpha * acc[i]);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (PREFETCH) {
+#pragma unroll
+      for (int t = 0; t < KT; ++t) areg[t] = anext[t];
+    } else if (g + stride < groups) {
+      load_group(g + stride, areg);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------- wgrad
+constexpr int WG_BK = 16;
+
+// op(A) = A^T with A = dY [Kr rows][lda] (GEMM M = Mo = dY columns), B = X [Kr][ldb] (N = No)
+template <int MO_PAD, int NO_PAD>
+__global__ __launch_bounds__(256) void wgrad_kernel(StreamArgs a, int rows_per_block) {
+  constexpr int mo_pad = MO_PAD, no_pad = NO_PAD;
+  constexpr int TPW = ((MO_PAD / 32) * (NO_PAD / 32) + 3) / 4;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* Ys = sm;                                // [2][WG_BK][mo_pad]
+  float* Xs = Ys + 2 * WG_BK * mo_pad;           // [2][WG_BK][no_pad]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Mo = a.M, No = a.N;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(a.K, r0 + rows_per_block);
+  constexpr int tiles_n = no_pad / 32;
+  constexpr int ntiles = (mo_pad / 32) * tiles_n;
+  // register staging of one chunk: WG_BK rows x (mo_pad + no_pad) floats, float4 per slot
+  constexpr int ysl = WG_BK * mo_pad / 4, xsl = WG_BK * no_pad / 4;
+  constexpr int MAXS = (ysl + xsl + 255) / 256;
+  floatx4 st[MAXS];
+  auto load_chunk = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < MAXS; ++i) {
+      const int s = tid + i * 256;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (s < ysl) {
+        const int kk = s / (mo_pad / 4), c = (s % (mo_pad / 4)) * 4, m = c0 + kk;
+        if (m < r1 && c < Mo) v = *reinterpret_cast<const floatx4*>(a.A + (int64_t)m * a.lda + c);
+      } else if (s < ysl + xsl) {
+        const int s2 = s - ysl;
+        const int kk = s2 / (no_pad / 4), c = (s2 % (no_pad / 4)) * 4, m = c0 + kk;
+        if (m < r1 && c < No) v = *reinterpret_cast<const floatx4*>(a.B + (int64_t)m * a.ldb + c);
+      }
+      st[i] = v;
+    }
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < MAXS; ++i) {
+      const int s = tid + i * 256;
+      if (s < ysl) {
+        *reinterpret_cast<floatx4*>(&Ys[buf * WG_BK * mo_pad + s * 4]) = st[i];
+      } else if (s < ysl + xsl) {
+        *reinterpret_cast<floatx4*>(&Xs[buf * WG_BK * no_pad + (s - ysl) * 4]) = st[i];
+      }
+    }
+  };
+  floatx16 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+  float rsum = 0.f;
+  const bool do_rs = a.rowsum != nullptr && tid < Mo;
+
+  int buf = 0;
+  if (r0 < r1) {
+    load_chunk(r0);
+    store_chunk(0);
+  }
+  __syncthreads();
+  for (int c0 = r0; c0 < r1; c0 += WG_BK) {
+    const bool more = c0 + WG_BK < r1;
+    if (more) load_chunk(c0 + WG_BK);
+    const float* Y = Ys + buf * WG_BK * mo_pad;
+    const float* X = Xs + buf * WG_BK * no_pad;
+    if (do_rs) {
+#pragma unroll
+      for (int kk = 0; kk < WG_BK; ++kk) rsum += Y[kk * mo_pad + tid];
+    }
+#pragma unroll
+    for (int kk = 0; kk < WG_BK; kk += 2) {
+      const int kr = kk + (lane >> 5);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        const int tile = wave + 4 * t;
+        if (tile < ntiles) {
+          const int ti = tile / tiles_n, tj = tile % tiles_n;
+          const float av = Y[kr * mo_pad + ti * 32 + (lane & 31)];
+          const float bv = X[kr * no_pad + tj * 32 + (lane & 31)];
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
+        }
+      }
+    }
+    if (more) store_chunk(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // partial tile -> ws[block][Mo][No] (fixed-order reduce later); rowsum partial after the tiles
+  float* out = a.ws + (int64_t)blockIdx.x * Mo * No;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int tile = wave + 4 * t;
+    if (tile >= ntiles) continue;
+    const int ti = tile / tiles_n, tj = tile % tiles_n;
+    const int n = tj * 32 + (lane & 31);
+    if (n >= No) continue;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int m = ti * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      if (m < Mo) out[(int64_t)m * No + n] = acc[t][e];
+    }
+  }
+  if (do_rs) a.ws[(int64_t)gridDim.x * Mo * No + (int64_t)blockIdx.x * Mo + tid] = rsum;
+}
+
+// C[m][n] = beta*C + alpha*sum_p ws[p][m*No+n];  rowsum[m] += alpha*sum_p wsr[p][m]
+__global__ __launch_bounds__(1024) void wgrad_reduce_kernel(StreamArgs a, int P) {
+  __shared__ float red[16][64];
+  const int total = a.M * a.N;
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int l = threadIdx.x >> 6;
+  const bool is_rs = e >= total;
+  const int rs_idx = e - total;
+  float acc = 0.f;
+  if (!is_rs || (a.rowsum && rs_idx < a.M)) {
+    const float* base = is_rs ? a.ws + (int64_t)P * total + rs_idx : a.ws + e;
+    const int64_t stride = is_rs ? a.M : total;
+    int p = l;
+    for (; p + 16 * 7 < P; p += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = base[(int64_t)(p + 16 * u) * stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; p < P; p += 16) acc += base[(int64_t)p * stride];
+  }
+  red[l][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (l != 0) return;
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
+  if (!is_rs) {
+    if (e < total) {
+      const int m = e / a.N, n = e % a.N;
+      float v = a.alpha * t;
+      if (a.beta != 0.f) v += a.beta * a.C[(int64_t)m * a.ldc + n];
+      a.C[(int64_t)m * a.ldc + n] = v;
+    }
+  } else if (a.rowsum && rs_idx < a.M) {
+    a.rowsum[rs_idx] += a.alpha * t;
+  }
+}
+
+int wgrad_blocks(int Kr) {
+  int nb = Kr / 512;
+  if (nb > 512) nb = 512;
+  if (nb < 1) nb = 1;
+  return nb;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ dispatch
+bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda) {
+  if (transA || M < 2048 || K < 4 || K > 256 || N < 1 || N > 256) return false;
+  if (K % 4 != 0 || lda % 4 != 0 || !aligned16(A)) return false;
+  const int nt = (N + 15) / 16, kt = (K + 15) / 16;
+  // instantiated (NT, KT) pairs: the encoder/projection shapes
+  switch (nt * 100 + kt) {
+    case 403: case 404: case 412: case 416: case 1204: case 1604: case 304: case 1216:
+    case 204: case 804: case 408: case 808: case 1608: return true;
+    default: return false;
+  }
+}
+
+int rowgemm_launch(const StreamArgs& s, hipStream_t st) {
+  const int nt = (s.N + 15) / 16, kt = (s.K + 15) / 16;
+  const size_t lds = (size_t)nt * 16 * (kt * 16 + 4) * sizeof(float);
+  const int groups = (s.M + 15) / 16;
+  int blocks = cdiv(groups, 8 * 2);  // >= 2 row groups per wave
+  const int per_cu = lds > 80 * 1024 ? 1 : (lds > 53 * 1024 ? 2 : (lds > 40 * 1024 ? 3 : 4));
+  if (blocks > 256 * per_cu) blocks = 256 * per_cu;
+  if (blocks < 1) blocks = 1;
+#define RS_RG(NTV, KTV)                                                            \
+  case NTV * 100 + KTV:                                                            \
+    rowgemm_kernel<NTV, KTV><<<blocks, 512, lds, st>>>(s);                          \
+    break;
+  switch (nt * 100 + kt) {
+    RS_RG(4, 3) RS_RG(4, 4) RS_RG(4, 12) RS_RG(4, 16) RS_RG(12, 4) RS_RG(16, 4) RS_RG(3, 4)
+    RS_RG(12, 16) RS_RG(2, 4) RS_RG(8, 4) RS_RG(4, 8) RS_RG(8, 8) RS_RG(16, 8)
+    default: set_error("rowgemm: no instance for N=%d K=%d", s.N, s.K); return -1;
+  }
+#undef RS_RG
+  RS_CHECK_LAUNCH("rowgemm");
+  return 0;
+}
+
+bool wgrad_supported(int transA, int transB, int M, int N, int K, const float* A, int lda,
+                     const float* B, int ldb, int ldc, int epi) {
+  if (!transA || transB || epi != 0 || K < 8192) return false;
+  const int mo_pad = (M + 31) / 32 * 32, no_pad = (N + 31) / 32 * 32;
+  switch (mo_pad * 1000 + no_pad) {
+    case 64064: case 64256: case 256064: case 192064: case 64192: case 128128: case 128064:
+    case 64128: case 32064: case 64032: break;
+    default: return false;
+  }
+  if (M % 4 != 0 || N % 4 != 0 || lda % 4 != 0 || ldb % 4 != 0 || !aligned16(A) || !aligned16(B))
+    return false;
+  (void)ldc;
+  return true;
+}
+
+int64_t wgrad_ws_bytes(int M, int N, int K) {
+  return (int64_t)wgrad_blocks(K) * ((int64_t)M * N + M) * (int64_t)sizeof(float);
+}
+
+int wgrad_launch(const StreamArgs& s, hipStream_t st) {
+  const int mo_pad = (s.M + 31) / 32 * 32, no_pad = (s.N + 31) / 32 * 32;
+  const int nb = wgrad_blocks(s.K);
+  const int rpb = cdiv(cdiv(s.K, nb), WG_BK) * WG_BK;
+  const int nblk = cdiv(s.K, rpb);
+  const size_t lds = (size_t)2 * WG_BK * (mo_pad + no_pad) * sizeof(float);
+#define RS_WG(MOV, NOV)                                                   \
+  case MOV * 1000 + NOV:                                                  \
+    wgrad_kernel<MOV, NOV><<<nblk, 256, lds, st>>>(s, rpb);               \
+    break;
+  switch (mo_pad * 1000 + no_pad) {
+    RS_WG(64, 64) RS_WG(64, 256) RS_WG(256, 64) RS_WG(192, 64) RS_WG(64, 192) RS_WG(128, 128)
+    RS_WG(128, 64) RS_WG(64, 128) RS_WG(32, 64) RS_WG(64, 32)
+    default: set_error("wgrad: no instance for %dx%d", s.M, s.N); return -1;
+  }
+#undef RS_WG
+  RS_CHECK_LAUNCH("wgrad");
+  const int total = s.M * s.N + (s.rowsum ? s.M : 0);
+  wgrad_reduce_kernel<<<cdiv(total, 64), 1024, 0, st>>>(s, nblk);
+  RS_CHECK_LAUNCH("wgrad reduce");
+  return 0;
+}
+
+}  // namespace rs
