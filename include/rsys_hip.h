@@ -28,12 +28,15 @@ int rs_device_check(void);            /* 0 if a gfx950 device is current, else h
 
 /* ---------------------------------------------------------------- GEMM (fp32 MFMA)
  * C = epi(alpha * op(A) @ op(B))  with op(A)[m,k] = transA ? A[k*lda+m] : A[m*lda+k],
- * op(B)[k,n] = transB ? B[n*ldb+k] : B[k*ldb+n]. Epilogue flags (bitwise):
- *   RS_EPI_BIAS    v += bias[n]
- *   RS_EPI_AUX_ADD v += aux[(m % aux_mod)*ld_aux + n]      (residual / positional rows)
- *   RS_EPI_AUX_MASK v = aux[m*ld_aux+n] > 0 ? v : 0         (ReLU backward)
- *   RS_EPI_RELU    v = max(v, 0)   (applied last)
- *   beta != 0      v += beta * C_old   (applied before RELU)
+ * op(B)[k,n] = transB ? B[n*ldb+k] : B[k*ldb+n]. Epilogue, in this order (flags bitwise):
+ *   v = alpha * acc
+ *   RS_EPI_BIAS     v += bias[n]
+ *   RS_EPI_AUX_MASK v = aux[m*ld_aux+n] > 0 ? v : 0        (ReLU backward)
+ *   RS_EPI_RELU     v = max(v, 0)
+ *   RS_EPI_DROP_A   v *= dropout mask of (drop_key, site_a) at element m*N+n  (rs_dropout_fwd)
+ *   RS_EPI_AUX_ADD  v += aux[(m % aux_mod)*ld_aux + n]     (residual / positional rows)
+ *   RS_EPI_DROP_B   v *= dropout mask of (drop_key, site_b) at element m*N+n
+ *   beta != 0       v += beta * C_old
  * rowsum != NULL: rowsum[m] += alpha * sum_k op(A)[m, k] — fused into the staged A tiles; with
  *   transA this is the bias gradient of a weight-gradient GEMM (dW = dY^T X, db = colsum dY).
  * split_k > 1 needs the workspace rs_gemm_ws_bytes(M, N, K, split_k).
@@ -44,11 +47,14 @@ int rs_device_check(void);            /* 0 if a gfx950 device is current, else h
 #define RS_EPI_RELU 2
 #define RS_EPI_AUX_ADD 4
 #define RS_EPI_AUX_MASK 8
+#define RS_EPI_DROP_A 16
+#define RS_EPI_DROP_B 32
 int rs_gemm_auto_split(int M, int N, int K);   /* split_k that fills the chip for long K */
 int64_t rs_gemm_ws_bytes(int M, int N, int K, int split_k);
 int rs_gemm_f32(int transA, int transB, int M, int N, int K, float alpha,
                 const float* A, int lda, const float* B, int ldb, float beta, float* C, int ldc,
                 int epilogue, const float* bias, const float* aux, int ld_aux, int aux_mod,
+                float drop_p, const int64_t* drop_key, int site_a, int site_b,
                 float* rowsum, int split_k, float* ws, void* stream);
 
 /* ---------------------------------------------------------------- column reductions

@@ -11,6 +11,7 @@
 // Split-K (reductions over M = B*L for weight gradients) writes f32 partial slabs that a second
 // kernel sums in a fixed order (bitwise reproducible) and finishes with the epilogue.
 #include "common.h"
+#include "rng.h"
 
 namespace rs {
 namespace {
@@ -35,16 +36,27 @@ struct GemmArgs {
   int ld_aux, aux_mod;
   int split_k, kchunk;
   float* ws;
-  float* rowsum;  // RS_EPI_ROWSUM_A: rowsum[m] += alpha * sum_k op(A)[m, k]
+  float* rowsum;  // rowsum[m] += alpha * sum_k op(A)[m, k]
   int vecA, vecB;
+  float drop_p;
+  const int64_t* drop_key;
+  int site_a, site_b;
 };
 
-__device__ __forceinline__ float epilogue(const GemmArgs& a, int m, int n, float v) {
+template <class Args>
+__device__ __forceinline__ float epilogue(const Args& a, int m, int n, float v) {
   if (a.epi & RS_EPI_BIAS) v += a.bias[n];
-  if (a.epi & RS_EPI_AUX_ADD) v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
   if (a.epi & RS_EPI_AUX_MASK) v = a.aux[(int64_t)m * a.ld_aux + n] > 0.f ? v : 0.f;
-  if (a.beta != 0.f) v += a.beta * a.C[(int64_t)m * a.ldc + n];
   if (a.epi & RS_EPI_RELU) v = fmaxf(v, 0.f);
+  if (a.epi & (RS_EPI_DROP_A | RS_EPI_DROP_B)) {
+    const uint64_t e = (uint64_t)m * a.N + n;
+    if (a.epi & RS_EPI_DROP_A) v *= keep_mult(make_key(a.drop_key, a.site_a, a.drop_p), e);
+    if (a.epi & RS_EPI_AUX_ADD) v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
+    if (a.epi & RS_EPI_DROP_B) v *= keep_mult(make_key(a.drop_key, a.site_b, a.drop_p), e);
+  } else if (a.epi & RS_EPI_AUX_ADD) {
+    v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
+  }
+  if (a.beta != 0.f) v += a.beta * a.C[(int64_t)m * a.ldc + n];
   return v;
 }
 
@@ -263,6 +275,9 @@ struct StreamArgs {
   float* rowsum;
   float* ws;
   int transB;
+  float drop_p;
+  const int64_t* drop_key;
+  int site_a, site_b;
 };
 bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda);
 int rowgemm_launch(const StreamArgs& s, hipStream_t st);
@@ -280,6 +295,7 @@ extern "C" int rs_gemm_auto_split(int M, int N, int K) {
   const int BMt = M >= 2048 ? 128 : 64, BNt = N > 64 ? 128 : 64;
   int64_t tiles = (int64_t)cdiv(M, BMt) * cdiv(N, BNt);
   if (tiles >= 256 || K < 1024) return 1;
+  if (K >= 2048 && (int64_t)M * N <= 16384) return 2;  // wgrad path: needs a workspace only
   int s = (int)((512 + tiles - 1) / tiles);
   int maxs = K / (BK * 16);  // each split keeps >= 16 k-tiles
   if (s > maxs) s = maxs;
@@ -289,7 +305,7 @@ extern "C" int rs_gemm_auto_split(int M, int N, int K) {
 
 extern "C" int64_t rs_gemm_ws_bytes(int M, int N, int K, int split_k) {
   int64_t b = split_k > 1 ? (int64_t)split_k * ((int64_t)M * N + M) * (int64_t)sizeof(float) : 0;
-  if (K >= 8192) {  // the weight-gradient streaming kernel may be chosen (gemm_stream.hip)
+  if (K >= 2048) {  // the weight-gradient streaming kernel may be chosen (gemm_stream.hip)
     const int64_t w = wgrad_ws_bytes(M, N, K);
     if (w > b) b = w;
   }
@@ -299,7 +315,8 @@ extern "C" int64_t rs_gemm_ws_bytes(int M, int N, int K, int split_k) {
 extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float alpha,
                            const float* A, int lda, const float* B, int ldb, float beta, float* C,
                            int ldc, int epilogue, const float* bias, const float* aux, int ld_aux,
-                           int aux_mod, float* rowsum, int split_k, float* ws, void* stream) {
+                           int aux_mod, float drop_p, const int64_t* drop_key, int site_a,
+                           int site_b, float* rowsum, int split_k, float* ws, void* stream) {
   RS_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "rs_gemm_f32: negative size M=%d N=%d K=%d", M, N, K);
   if (M == 0 || N == 0) return 0;
   RS_CHECK_ARG(A && B && C, "rs_gemm_f32: null operand");
@@ -311,6 +328,9 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
                "rs_gemm_f32: aux epilogue without aux");
   RS_CHECK_ARG(!((epilogue & RS_EPI_AUX_ADD) && (epilogue & RS_EPI_AUX_MASK)),
                "rs_gemm_f32: AUX_ADD and AUX_MASK are exclusive");
+  RS_CHECK_ARG(!(epilogue & (RS_EPI_DROP_A | RS_EPI_DROP_B)) ||
+                   (drop_key && drop_p >= 0.f && drop_p < 1.f),
+               "rs_gemm_f32: dropout epilogue needs a key and 0 <= p < 1");
   if (split_k < 1) split_k = 1;
   RS_CHECK_ARG(split_k == 1 || ws, "rs_gemm_f32: split_k %d needs a workspace", split_k);
   GemmArgs g;
@@ -325,6 +345,7 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
   if (K == 0) { g.split_k = 1; g.kchunk = BK; }
   g.ws = ws;
   g.rowsum = rowsum;
+  g.drop_p = drop_p; g.drop_key = drop_key; g.site_a = site_a; g.site_b = site_b;
   g.vecA = (lda % 4 == 0) && aligned16(A);
   g.vecB = (ldb % 4 == 0) && aligned16(B);
   hipStream_t st = as_stream(stream);
@@ -334,6 +355,7 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
     sa.B = B; sa.ldb = ldb; sa.C = C; sa.ldc = ldc; sa.epi = epilogue; sa.bias = bias;
     sa.aux = aux; sa.ld_aux = ld_aux; sa.aux_mod = g.aux_mod; sa.rowsum = rowsum; sa.ws = ws;
     sa.transB = transB;
+    sa.drop_p = drop_p; sa.drop_key = drop_key; sa.site_a = site_a; sa.site_b = site_b;
     if (!rowsum && rowgemm_supported(transA, M, N, K, A, lda)) return rowgemm_launch(sa, st);
     if (ws && wgrad_supported(transA, transB, M, N, K, A, lda, B, ldb, ldc, epilogue))
       return wgrad_launch(sa, st);

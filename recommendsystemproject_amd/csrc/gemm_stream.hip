@@ -15,6 +15,7 @@
 //   k-major exactly as they lie in memory (no transposition), partial tiles are summed by a
 //   fixed-order reduce (deterministic), and the bias gradient colsum(dY) is fused.
 #include "common.h"
+#include "rng.h"
 
 namespace rs {
 
@@ -30,6 +31,9 @@ struct StreamArgs {
   float* rowsum;
   float* ws;
   int transB;
+  float drop_p;
+  const int64_t* drop_key;
+  int site_a, site_b;
 };
 
 namespace {
@@ -37,12 +41,20 @@ namespace {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+// same epilogue order as gemm.hip (see rsys_hip.h)
 __device__ __forceinline__ float epi_apply(const StreamArgs& a, int m, int n, float v) {
   if (a.epi & RS_EPI_BIAS) v += a.bias[n];
-  if (a.epi & RS_EPI_AUX_ADD) v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
   if (a.epi & RS_EPI_AUX_MASK) v = a.aux[(int64_t)m * a.ld_aux + n] > 0.f ? v : 0.f;
-  if (a.beta != 0.f) v += a.beta * a.C[(int64_t)m * a.ldc + n];
   if (a.epi & RS_EPI_RELU) v = fmaxf(v, 0.f);
+  if (a.epi & (RS_EPI_DROP_A | RS_EPI_DROP_B)) {
+    const uint64_t e = (uint64_t)m * a.N + n;
+    if (a.epi & RS_EPI_DROP_A) v *= keep_mult(make_key(a.drop_key, a.site_a, a.drop_p), e);
+    if (a.epi & RS_EPI_AUX_ADD) v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
+    if (a.epi & RS_EPI_DROP_B) v *= keep_mult(make_key(a.drop_key, a.site_b, a.drop_p), e);
+  } else if (a.epi & RS_EPI_AUX_ADD) {
+    v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
+  }
+  if (a.beta != 0.f) v += a.beta * a.C[(int64_t)m * a.ldc + n];
   return v;
 }
 
@@ -53,16 +65,17 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
   constexpr bool PREFETCH = KT <= 8;
   extern __shared__ __attribute__((aligned(16))) float Bs[];  // [NT*16][KP]
   const int tid = threadIdx.x;
-  // stage op(B) as Bs[n][k], zero padded to NT*16 x KT*16
+  const int nb0 = blockIdx.y * NT * 16;  // this workgroup's column slice (small-M N split)
+  // stage op(B)[:, nb0 : nb0 + NT*16] as Bs[n][k], zero padded to NT*16 x KT*16
   if (a.transB) {  // B[n*ldb + k]: consecutive threads -> consecutive k
     for (int idx = tid; idx < NT * 16 * KT * 16; idx += 512) {
       const int n = idx / (KT * 16), k = idx % (KT * 16);
-      Bs[n * KP + k] = (n < a.N && k < a.K) ? a.B[(int64_t)n * a.ldb + k] : 0.f;
+      Bs[n * KP + k] = (nb0 + n < a.N && k < a.K) ? a.B[(int64_t)(nb0 + n) * a.ldb + k] : 0.f;
     }
   } else {  // B[k*ldb + n]: consecutive threads -> consecutive n
     for (int idx = tid; idx < NT * 16 * KT * 16; idx += 512) {
       const int k = idx / (NT * 16), n = idx % (NT * 16);
-      Bs[n * KP + k] = (n < a.N && k < a.K) ? a.B[(int64_t)k * a.ldb + n] : 0.f;
+      Bs[n * KP + k] = (nb0 + n < a.N && k < a.K) ? a.B[(int64_t)k * a.ldb + nb0 + n] : 0.f;
     }
   }
   __syncthreads();
@@ -110,7 +123,7 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         if (h == 1 && !two) break;
-        const int n = (j0 + h) * 16 + r;
+        const int n = nb0 + (j0 + h) * 16 + r;
         if (n >= a.N) continue;
         const floatx4 acc = h ? acc1 : acc0;
 #pragma unroll
@@ -278,7 +291,7 @@ __global__ __launch_bounds__(1024) void wgrad_reduce_kernel(StreamArgs a, int P)
 }
 
 int wgrad_blocks(int Kr) {
-  int nb = Kr / 512;
+  int nb = Kr / 256;
   if (nb > 512) nb = 512;
   if (nb < 1) nb = 1;
   return nb;
@@ -287,10 +300,13 @@ int wgrad_blocks(int Kr) {
 }  // namespace
 
 // ------------------------------------------------------------------------------ dispatch
+// Small M: split N over workgroups (NT = 4 column tiles each) so the grid still fills the chip.
+constexpr int kSmallM = 32768;
+
 bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda) {
-  if (transA || M < 2048 || K < 4 || K > 256 || N < 1 || N > 256) return false;
+  if (transA || M < 1024 || K < 4 || K > 256 || N < 1 || N > 256) return false;
   if (K % 4 != 0 || lda % 4 != 0 || !aligned16(A)) return false;
-  const int nt = (N + 15) / 16, kt = (K + 15) / 16;
+  const int nt = M < kSmallM ? 4 : (N + 15) / 16, kt = (K + 15) / 16;
   // instantiated (NT, KT) pairs: the encoder/projection shapes
   switch (nt * 100 + kt) {
     case 403: case 404: case 412: case 416: case 1204: case 1604: case 304: case 1216:
@@ -300,13 +316,16 @@ bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda)
 }
 
 int rowgemm_launch(const StreamArgs& s, hipStream_t st) {
-  const int nt = (s.N + 15) / 16, kt = (s.K + 15) / 16;
+  const bool small = s.M < kSmallM;
+  const int nt = small ? 4 : (s.N + 15) / 16, kt = (s.K + 15) / 16;
+  const int nsplit = small ? cdiv(s.N, 64) : 1;
   const size_t lds = (size_t)nt * 16 * (kt * 16 + 4) * sizeof(float);
   const int groups = (s.M + 15) / 16;
-  int blocks = cdiv(groups, 8 * 2);  // >= 2 row groups per wave
+  int bx = cdiv(groups, small ? 8 : 8 * 2);  // small M: one row group per wave
   const int per_cu = lds > 80 * 1024 ? 1 : (lds > 53 * 1024 ? 2 : (lds > 40 * 1024 ? 3 : 4));
-  if (blocks > 256 * per_cu) blocks = 256 * per_cu;
-  if (blocks < 1) blocks = 1;
+  if (bx > 256 * per_cu) bx = 256 * per_cu;
+  if (bx < 1) bx = 1;
+  const dim3 blocks(bx, nsplit);
 #define RS_RG(NTV, KTV)                                                            \
   case NTV * 100 + KTV:                                                            \
     rowgemm_kernel<NTV, KTV><<<blocks, 512, lds, st>>>(s);                          \
@@ -323,7 +342,7 @@ int rowgemm_launch(const StreamArgs& s, hipStream_t st) {
 
 bool wgrad_supported(int transA, int transB, int M, int N, int K, const float* A, int lda,
                      const float* B, int ldb, int ldc, int epi) {
-  if (!transA || transB || epi != 0 || K < 8192) return false;
+  if (!transA || transB || epi != 0 || K < 2048) return false;
   const int mo_pad = (M + 31) / 32 * 32, no_pad = (N + 31) / 32 * 32;
   switch (mo_pad * 1000 + no_pad) {
     case 64064: case 64256: case 256064: case 192064: case 64192: case 128128: case 128064:

@@ -89,12 +89,9 @@ def seq_input_fwd(proc, seqd, B, L, p, key, err):
     ops.gather_fwd(segs, M, cat, err)
     lin = proc.feature_projection[0]
     pos = proc.pos_emb.weight
-    if p > 0:
-        x = ops.linear_fwd(cat, lin.weight, lin.bias)
-        ops.dropout_fwd(x, p, key, 0)
-        ops.dropout_fwd(x, p, key, 1, aux=pos, aux_mod=L)
-    else:
-        x = ops.linear_fwd(cat, lin.weight, lin.bias, aux=pos, aux_mod=L)
+    # drop_b(drop_a(cat W^T + b) + pos[l]) in the GEMM epilogue (sites 0, 1 = rs_dropout masks)
+    x = ops.linear_fwd(cat, lin.weight, lin.bias, aux=pos, aux_mod=L, drop_p=p, drop_key=key,
+                       site_a=0, site_b=1)
     return x, (segs, tables, cat, keep)
 
 
@@ -125,9 +122,8 @@ def layer_fwd(lyr, x, key_pad, B, L, d, H, p, key, site):
     h1 = ops.linear_fwd(att, sa_mod.out_proj.weight, sa_mod.out_proj.bias)
     x1, m1, r1 = ops.add_layernorm_fwd(h1, x, lyr.norm1.weight, lyr.norm1.bias, lyr.norm1.eps,
                                        p, key, site + 1)  # h1 <- x + dropout1(sa)
-    f1 = ops.linear_fwd(x1, lyr.linear1.weight, lyr.linear1.bias, relu=True)
-    if p > 0:
-        ops.dropout_fwd(f1, p, key, site + 2)
+    f1 = ops.linear_fwd(x1, lyr.linear1.weight, lyr.linear1.bias, relu=True, drop_p=p, drop_key=key,
+                        site_a=site + 2)  # dropout(relu(.)) fused
     h2 = ops.linear_fwd(f1, lyr.linear2.weight, lyr.linear2.bias)
     x2, m2, r2 = ops.add_layernorm_fwd(h2, x1, lyr.norm2.weight, lyr.norm2.bias, lyr.norm2.eps,
                                        p, key, site + 3)  # h2 <- x1 + dropout2(ff)

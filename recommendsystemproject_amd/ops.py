@@ -27,7 +27,8 @@ def ws(nbytes: int, device) -> torch.Tensor:
 
 
 def gemm(A, B, C, M, N, K, *, transA, transB, lda, ldb, ldc, alpha=1.0, beta=0.0, epi=0,
-         bias=None, aux=None, ld_aux=0, aux_mod=0, split=None, rowsum=None):
+         bias=None, aux=None, ld_aux=0, aux_mod=0, split=None, rowsum=None, drop_p=0.0,
+         drop_key=None, site_a=0, site_b=0):
     L = _hip.lib()
     if split is None:
         split = L.rs_gemm_auto_split(M, N, K)
@@ -35,21 +36,27 @@ def gemm(A, B, C, M, N, K, *, transA, transB, lda, ldb, ldc, alpha=1.0, beta=0.0
     if split > 1:
         w = ws(L.rs_gemm_ws_bytes(M, N, K, split), C.device)
     call('rs_gemm_f32', int(transA), int(transB), M, N, K, float(alpha), P(A), lda, P(B), ldb,
-         float(beta), P(C), ldc, epi, P(bias), P(aux), ld_aux, aux_mod, P(rowsum), split, P(w), stream())
+         float(beta), P(C), ldc, epi, P(bias), P(aux), ld_aux, aux_mod, float(drop_p), P(drop_key),
+         site_a, site_b, P(rowsum), split, P(w), stream())
     return C
 
 
-def linear_fwd(x, W, b=None, out=None, *, relu=False, aux=None, aux_mod=0, beta=0.0):
-    """out[M,N] = x[M,K] @ W[N,K]^T (+ b) (+ aux[m % aux_mod]) (relu)."""
+def linear_fwd(x, W, b=None, out=None, *, relu=False, aux=None, aux_mod=0, beta=0.0,
+               drop_p=0.0, drop_key=None, site_a=None, site_b=None):
+    """out[M,N] = drop_b(drop_a(relu(x[M,K] @ W[N,K]^T + b)) + aux[m % aux_mod]) (+ beta*out);
+    dropout stages are active when drop_p > 0 and their site is given."""
     M, K = x.shape
     N = W.shape[0]
     if out is None:
         out = torch.empty(M, N, device=x.device, dtype=torch.float32)
     epi = (_hip.RS_EPI_BIAS if b is not None else 0) | (_hip.RS_EPI_RELU if relu else 0) | \
         (_hip.RS_EPI_AUX_ADD if aux is not None else 0)
+    if drop_p > 0:
+        epi |= (_hip.RS_EPI_DROP_A if site_a is not None else 0) | (_hip.RS_EPI_DROP_B if site_b is not None else 0)
     return gemm(x, W, out, M, N, K, transA=0, transB=1, lda=x.stride(0), ldb=W.stride(0),
                 ldc=out.stride(0), beta=beta, epi=epi, bias=b, aux=aux,
-                ld_aux=(aux.stride(0) if aux is not None else 0), aux_mod=aux_mod)
+                ld_aux=(aux.stride(0) if aux is not None else 0), aux_mod=aux_mod, drop_p=drop_p,
+                drop_key=drop_key, site_a=site_a or 0, site_b=site_b or 0)
 
 
 def linear_bwd_input(dy, W, out=None, *, beta=0.0, relu_mask_of=None, alpha=1.0):

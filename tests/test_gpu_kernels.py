@@ -275,6 +275,24 @@ def test_l2norm():
     assert torch.allclose(dx, x.grad, atol=1e-4)
 
 
+@pytest.mark.parametrize('M', [300, 5000])
+def test_gemm_dropout_epilogue_matches_dropout_kernel(M):
+    """GEMM epilogue dropout == rs_dropout_fwd with the same (key, site) (masks are shared by
+    the fused forward and the unfused backward)."""
+    K, N, L, p = 40, 64, 25, 0.2
+    x, W, b, pos = rnd(M, K, seed=1), rnd(N, K, seed=2), rnd(N, seed=3), rnd(L, N, seed=4)
+    key = torch.tensor([77, 3], dtype=torch.int64, device=DEV)
+    fused = ops.linear_fwd(x, W, b, aux=pos, aux_mod=L, drop_p=p, drop_key=key, site_a=0, site_b=1)
+    ref = ops.linear_fwd(x, W, b)
+    ops.dropout_fwd(ref, p, key, 0)
+    ops.dropout_fwd(ref, p, key, 1, aux=pos, aux_mod=L)
+    assert torch.allclose(fused, ref, atol=1e-5)
+    f1 = ops.linear_fwd(x, W, b, relu=True, drop_p=p, drop_key=key, site_a=9)
+    r1 = ops.linear_fwd(x, W, b, relu=True)
+    ops.dropout_fwd(r1, p, key, 9)
+    assert torch.allclose(f1, r1, atol=1e-5)
+
+
 def test_dropout_statistics_and_mask_reuse():
     n, p = 1 << 20, 0.3
     x = torch.ones(n // 64, 64, device=DEV)
