@@ -44,15 +44,16 @@ struct GemmArgs {
 };
 
 template <class Args>
-__device__ __forceinline__ float epilogue(const Args& a, int m, int n, float v) {
+__device__ __forceinline__ float epilogue(const Args& a, int m, int n, float v, const DropKey& ka,
+                                          const DropKey& kb) {
   if (a.epi & RS_EPI_BIAS) v += a.bias[n];
   if (a.epi & RS_EPI_AUX_MASK) v = a.aux[(int64_t)m * a.ld_aux + n] > 0.f ? v : 0.f;
   if (a.epi & RS_EPI_RELU) v = fmaxf(v, 0.f);
   if (a.epi & (RS_EPI_DROP_A | RS_EPI_DROP_B)) {
     const uint64_t e = (uint64_t)m * a.N + n;
-    if (a.epi & RS_EPI_DROP_A) v *= keep_mult(make_key(a.drop_key, a.site_a, a.drop_p), e);
+    if (a.epi & RS_EPI_DROP_A) v *= keep_mult(ka, e);
     if (a.epi & RS_EPI_AUX_ADD) v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
-    if (a.epi & RS_EPI_DROP_B) v *= keep_mult(make_key(a.drop_key, a.site_b, a.drop_p), e);
+    if (a.epi & RS_EPI_DROP_B) v *= keep_mult(kb, e);
   } else if (a.epi & RS_EPI_AUX_ADD) {
     v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
   }
@@ -204,6 +205,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
     if (a.split_k > 1) a.ws[(int64_t)a.split_k * a.M * a.N + (int64_t)z * a.M + m0 + tid] = a.alpha * rsum;
     else a.rowsum[m0 + tid] += a.alpha * rsum;
   }
+  DropKey ka{}, kb{};
+  if (a.epi & RS_EPI_DROP_A) ka = make_key(a.drop_key, a.site_a, a.drop_p);
+  if (a.epi & RS_EPI_DROP_B) kb = make_key(a.drop_key, a.site_b, a.drop_p);
   // epilogue: C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -219,7 +223,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
         if (a.split_k > 1) {
           a.ws[((int64_t)z * a.M + m) * a.N + n] = v;
         } else {
-          a.C[(int64_t)m * a.ldc + n] = epilogue(a, m, n, v);
+          a.C[(int64_t)m * a.ldc + n] = epilogue(a, m, n, v, ka, kb);
         }
       }
     }
@@ -227,6 +231,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
 
 __global__ void splitk_reduce_kernel(GemmArgs a) {
   const int64_t total = (int64_t)a.M * a.N;
+  DropKey ka{}, kb{};
+  if (a.epi & RS_EPI_DROP_A) ka = make_key(a.drop_key, a.site_a, a.drop_p);
+  if (a.epi & RS_EPI_DROP_B) kb = make_key(a.drop_key, a.site_b, a.drop_p);
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     float v[8];
@@ -241,7 +248,7 @@ __global__ void splitk_reduce_kernel(GemmArgs a) {
     }
     for (; z < a.split_k; ++z) acc += a.ws[(int64_t)z * total + idx];
     const int m = (int)(idx / a.N), n = (int)(idx % a.N);
-    a.C[(int64_t)m * a.ldc + n] = epilogue(a, m, n, acc);
+    a.C[(int64_t)m * a.ldc + n] = epilogue(a, m, n, acc, ka, kb);
     if (a.rowsum && idx < a.M) {
       const float* rs = a.ws + (int64_t)a.split_k * total;
       float r = 0.f;

@@ -42,15 +42,16 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // same epilogue order as gemm.hip (see rsys_hip.h)
-__device__ __forceinline__ float epi_apply(const StreamArgs& a, int m, int n, float v) {
+__device__ __forceinline__ float epi_apply(const StreamArgs& a, int m, int n, float v,
+                                           const DropKey& ka, const DropKey& kb) {
   if (a.epi & RS_EPI_BIAS) v += a.bias[n];
   if (a.epi & RS_EPI_AUX_MASK) v = a.aux[(int64_t)m * a.ld_aux + n] > 0.f ? v : 0.f;
   if (a.epi & RS_EPI_RELU) v = fmaxf(v, 0.f);
   if (a.epi & (RS_EPI_DROP_A | RS_EPI_DROP_B)) {
     const uint64_t e = (uint64_t)m * a.N + n;
-    if (a.epi & RS_EPI_DROP_A) v *= keep_mult(make_key(a.drop_key, a.site_a, a.drop_p), e);
+    if (a.epi & RS_EPI_DROP_A) v *= keep_mult(ka, e);
     if (a.epi & RS_EPI_AUX_ADD) v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
-    if (a.epi & RS_EPI_DROP_B) v *= keep_mult(make_key(a.drop_key, a.site_b, a.drop_p), e);
+    if (a.epi & RS_EPI_DROP_B) v *= keep_mult(kb, e);
   } else if (a.epi & RS_EPI_AUX_ADD) {
     v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
   }
@@ -83,6 +84,9 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
   const int groups = (a.M + 15) / 16;
+  DropKey ka{}, kb{};
+  if (a.epi & RS_EPI_DROP_A) ka = make_key(a.drop_key, a.site_a, a.drop_p);
+  if (a.epi & RS_EPI_DROP_B) kb = make_key(a.drop_key, a.site_b, a.drop_p);
   const int stride = gridDim.x * 8;
   int g = blockIdx.x * 8 + wave;
   floatx4 areg[KT];
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int m = g * 16 + 4 * q + i;
-          if (m < a.M) a.C[(int64_t)m * a.ldc + n] = epi_apply(a, m, n, a.alpha * acc[i]);
+          if (m < a.M) a.C[(int64_t)m * a.ldc + n] = epi_apply(a, m, n, a.alpha * acc[i], ka, kb);
         }
       }
     }

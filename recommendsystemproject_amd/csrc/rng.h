@@ -14,24 +14,37 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 }
 
 struct DropKey {
-  uint64_t base;
-  float p, scale;  // scale = 1/(1-p)
+  uint32_t k0, k1;  // per (seed, counter, site) stream keys
+  uint32_t thresh;  // keep iff hash >= thresh, thresh = p * 2^32
+  float scale;      // 1 / (1 - p)
 };
 
 __device__ __forceinline__ DropKey make_key(const int64_t* key, int site, float p) {
   DropKey k;
-  k.base = mix64((uint64_t)key[0] ^ mix64((uint64_t)key[1] * 0x9e3779b97f4a7c15ULL +
-                                          (uint64_t)site * 0xd1b54a32d192ed03ULL));
-  k.p = p;
+  const uint64_t b = mix64((uint64_t)key[0] ^ mix64((uint64_t)key[1] * 0x9e3779b97f4a7c15ULL +
+                                                    (uint64_t)site * 0xd1b54a32d192ed03ULL));
+  k.k0 = (uint32_t)b;
+  k.k1 = (uint32_t)(b >> 32);
+  const double t = (double)p * 4294967296.0;
+  k.thresh = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
   k.scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   return k;
 }
 
-// multiplier for element idx: 0 (dropped) or 1/(1-p) (kept)
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+
+// multiplier for element idx: 0 (dropped) or 1/(1-p) (kept); two 32-bit finalisers (cheap on
+// the VALU: no 64-bit multiplies) keyed by the 64-bit stream key
 __device__ __forceinline__ float keep_mult(const DropKey& k, uint64_t idx) {
-  const uint64_t h = mix64(k.base + idx * 0x9e3779b97f4a7c15ULL);
-  const float u = (float)(h >> 40) * (1.0f / 16777216.0f);  // [0, 1), 24 bits
-  return u >= k.p ? k.scale : 0.f;
+  const uint32_t h = fmix32(fmix32((uint32_t)idx ^ k.k0) + k.k1 + (uint32_t)(idx >> 32));
+  return h >= k.thresh ? k.scale : 0.f;
 }
 
 }  // namespace rs
