@@ -186,8 +186,10 @@ int rs_hardneg_bwd(const float* U, const float* Hn, const float* dhl, float* dU,
  * write_grad != 0 the clipped gradient is stored back into g. With step_dev != NULL the bias
  * corrections use the device step count *step_dev instead of `step`. */
 int64_t rs_sqnorm_ws_bytes(int64_t n);
+int rs_sqnorm_parts(int64_t n);          /* number of double partials rs_grad_sqnorm writes */
 int rs_grad_sqnorm(const float* g, int64_t n, float scale, double* ws, void* stream);
-int rs_clip_coef(const double* ws, int64_t n, float max_norm, float* total_norm, float* coef,
+/* sums nparts double partials (dense + sparse-table contributions) into norm and coef */
+int rs_clip_coef(const double* ws, int nparts, float max_norm, float* total_norm, float* coef,
                  void* stream);
 int rs_scale_inplace(float* g, int64_t n, float scale, const float* coef, void* stream);
 int rs_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, float beta1,
@@ -195,6 +197,47 @@ int rs_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, fl
                  float scale, const float* coef, int write_grad, void* stream);
 /* *counter += delta on the stream (device-side Adam step count: replayable in a hipGraph) */
 int rs_counter_add(int64_t* counter, int64_t delta, void* stream);
+
+/* ---------------------------------------------------------------- lazy-exact Adam (large tables)
+ * Dense-gradient Adam semantics (every row moves every step, T16) without sweeping the table:
+ * rows carry last[] = the optimizer step they were last brought to; consts[s] =
+ * {lr/bc1(s), sqrt(bc2(s))} is written once per step by rs_adam_prepare (which also advances
+ * the device step count). Per step: rs_sparse_touch (dedup the batch's ids into list/count via
+ * flag) -> rs_sparse_catchup (replay skipped zero-gradient steps for listed rows, bitwise equal
+ * to dense Adam, before the gather reads them) -> backward scatter-add -> rs_sparse_sqnorm
+ * (clip norm partials, rs_sparse_sqnorm_parts of them) -> rs_sparse_adam (step t for listed rows,
+ * zero their gradient, clear flags and count). rs_sparse_flush brings every row to the current
+ * step (checkpoint / state_dict). rs_sparse_zero_grad zeroes the listed gradient rows.
+ * Replaces torch.optim.Adam on sparse=False embeddings (GenericTower.py:45-49; train_twotower.py:111). */
+int rs_adam_prepare(int64_t* step, float* consts, int cap, float lr, float beta1, float beta2,
+                    void* stream);
+int rs_sparse_touch(const int64_t* ids, int rows, int bag, int64_t row_stride, int64_t vocab,
+                    int64_t pad, int* flag, int* list, int* count, void* stream);
+int rs_sparse_catchup(float* p, float* m, float* v, int* last, const int* list, const int* count,
+                      int D, const int64_t* step, const float* consts, float beta1, float beta2,
+                      float eps, float weight_decay, void* stream);
+int rs_sparse_adam(float* p, float* g, float* m, float* v, int* last, int* flag, const int* list,
+                   int* count, int D, const int64_t* step, const float* consts, float beta1,
+                   float beta2, float eps, float weight_decay, float scale, const float* coef,
+                   void* stream);
+int rs_sparse_sqnorm_parts(void);
+int rs_sparse_sqnorm(const float* g, const int* list, const int* count, int D, float scale,
+                     double* ws, void* stream);
+int rs_sparse_flush(float* p, float* m, float* v, int* last, int64_t V, int D, const int64_t* step,
+                    const float* consts, float beta1, float beta2, float eps, float weight_decay,
+                    void* stream);
+int rs_sparse_zero_grad(float* g, const int* list, const int* count, int D, void* stream);
+/* Data-parallel row-sparse gradient exchange (replicated tables; replaces the dense
+ * all-reduce of [V, D] embedding gradients the reference's DDP-style scaling would need).
+ * rs_sparse_pack writes [cap int32 ids (-1 = unused)][cap x D rows] from the local list (flags
+ * err_flag |= 2 on overflow); after an all-gather each rank rs_sparse_unpack_add's every rank's
+ * buffer in rank order (ids unique within a buffer; sets flags) and rs_sparse_compact rebuilds
+ * list/count in ascending row order, so every rank holds bitwise-identical gradients and lists. */
+int64_t rs_sparse_compact_ws_bytes(int64_t V);
+int rs_sparse_compact(const int* flag, int64_t V, int* list, int* count, int* ws, void* stream);
+int rs_sparse_pack(const float* g, const int* list, const int* count, int D, int cap, float* buf,
+                   int* err_flag, void* stream);
+int rs_sparse_unpack_add(float* g, int* flag, const float* buf, int D, int cap, void* stream);
 
 /* ---------------------------------------------------------------- dropout
  * Counter-based masks: element i of site `site` is kept iff hash(key[0], key[1], site, i) >= p,

@@ -59,12 +59,25 @@ SIGNATURES = {
     'rs_hardneg_bwd': (i32, [vp, vp, vp, vp, vp, i32, i32, i32, vp]),
     'rs_sqnorm_ws_bytes': (i64, [i64]),
     'rs_grad_sqnorm': (i32, [vp, i64, f32, vp, vp]),
-    'rs_clip_coef': (i32, [vp, i64, f32, vp, vp, vp]),
+    'rs_sqnorm_parts': (i32, [i64]),
+    'rs_clip_coef': (i32, [vp, i32, f32, vp, vp, vp]),
     'rs_scale_inplace': (i32, [vp, i64, f32, vp, vp]),
     'rs_adam_step': (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, vp, f32, vp, i32, vp]),
     'rs_counter_add': (i32, [vp, i64, vp]),
     'rs_sum': (i32, [vp, i32, f32, vp, vp]),
     'rs_rng_next': (i32, [vp, vp, vp]),
+    'rs_adam_prepare': (i32, [vp, vp, i32, f32, f32, f32, vp]),
+    'rs_sparse_touch': (i32, [vp, i32, i32, i64, i64, i64, vp, vp, vp, vp]),
+    'rs_sparse_catchup': (i32, [vp, vp, vp, vp, vp, vp, i32, vp, vp, f32, f32, f32, f32, vp]),
+    'rs_sparse_adam': (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, f32, f32, f32, f32, f32, vp, vp]),
+    'rs_sparse_sqnorm_parts': (i32, []),
+    'rs_sparse_sqnorm': (i32, [vp, vp, vp, i32, f32, vp, vp]),
+    'rs_sparse_flush': (i32, [vp, vp, vp, vp, i64, i32, vp, vp, f32, f32, f32, f32, vp]),
+    'rs_sparse_zero_grad': (i32, [vp, vp, vp, i32, vp]),
+    'rs_sparse_compact_ws_bytes': (i64, [i64]),
+    'rs_sparse_compact': (i32, [vp, i64, vp, vp, vp, vp]),
+    'rs_sparse_pack': (i32, [vp, vp, vp, i32, i32, vp, vp, vp]),
+    'rs_sparse_unpack_add': (i32, [vp, vp, vp, i32, i32, vp]),
     'rs_dropout_fwd': (i32, [vp, i64, i32, vp, i32, i32, f32, vp, i32, vp]),
     'rs_dropout_bwd': (i32, [vp, i64, f32, vp, i32, vp]),
 }

@@ -5,6 +5,9 @@
 // many tensors the model has. The clip coefficient stays on the device: no host sync.
 #include "common.h"
 
+// no fma contraction: the dense and the lazy (sparse.hip) Adam must round identically
+#pragma clang fp contract(off)
+
 namespace rs {
 namespace {
 
@@ -130,6 +133,20 @@ using namespace rs;
 
 extern "C" int64_t rs_sqnorm_ws_bytes(int64_t n) { return (int64_t)sq_blocks(n) * sizeof(double); }
 
+__global__ void zero_rows_kernel(float* __restrict__ g, const int* __restrict__ list,
+                                 const int* __restrict__ count, int D) {
+  const int n = *count;
+  for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4)
+    for (int c = threadIdx.x & 63; c < D; c += 64) g[(int64_t)list[i] * D + c] = 0.f;
+}
+
+extern "C" int rs_sparse_zero_grad(float* g, const int* list, const int* count, int D, void* stream) {
+  RS_CHECK_ARG(g && list && count && D >= 1, "rs_sparse_zero_grad: bad args");
+  zero_rows_kernel<<<1024, 256, 0, as_stream(stream)>>>(g, list, count, D);
+  RS_CHECK_LAUNCH("rs_sparse_zero_grad");
+  return 0;
+}
+
 extern "C" int rs_grad_sqnorm(const float* g, int64_t n, float scale, double* ws, void* stream) {
   RS_CHECK_ARG(g && ws && n >= 0, "rs_grad_sqnorm: bad args");
   sqnorm_kernel<<<sq_blocks(n), 256, 0, as_stream(stream)>>>(g, n, scale, ws);
@@ -137,10 +154,12 @@ extern "C" int rs_grad_sqnorm(const float* g, int64_t n, float scale, double* ws
   return 0;
 }
 
-extern "C" int rs_clip_coef(const double* ws, int64_t n, float max_norm, float* total_norm,
+extern "C" int rs_sqnorm_parts(int64_t n) { return sq_blocks(n); }
+
+extern "C" int rs_clip_coef(const double* ws, int nparts, float max_norm, float* total_norm,
                             float* coef, void* stream) {
-  RS_CHECK_ARG(ws && coef, "rs_clip_coef: null pointer");
-  clip_coef_kernel<<<1, 64, 0, as_stream(stream)>>>(ws, sq_blocks(n), max_norm, total_norm, coef);
+  RS_CHECK_ARG(ws && coef && nparts >= 1, "rs_clip_coef: bad args");
+  clip_coef_kernel<<<1, 64, 0, as_stream(stream)>>>(ws, nparts, max_norm, total_norm, coef);
   RS_CHECK_LAUNCH("rs_clip_coef");
   return 0;
 }

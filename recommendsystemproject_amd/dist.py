@@ -3,6 +3,13 @@ per GPU. The batch is sharded: each rank runs the full training
 B samples (own in-batch negatives, own BatchNorm statistics, as DDP applied to the reference),
 then ONE all-reduce of the flat gradient buffer (all parameters, ~3.5 MB for the demo schema)
 and an identical clip + Adam on every rank. Parameters are broadcast from rank 0 at start.
+
+Large tables trained by lazy-exact Adam (flat.py) stay replicated (a 10M x 128 table with its
+Adam state is ~20 GB: it fits 288 GB of HBM many times over) but their gradient is NOT
+all-reduced densely (5 GB per table per step): each rank packs only the rows its batch touched,
+one all-gather moves [ids | rows] of every rank, and every rank adds the W buffers in rank order
+and rebuilds the touched-row list in ascending order, so all ranks hold bitwise-identical
+gradients and lists (csrc/sparse.hip rs_sparse_pack / rs_sparse_unpack_add / rs_sparse_compact).
 """
 from __future__ import annotations
 
@@ -11,6 +18,7 @@ import os
 import torch
 import torch.distributed as dist
 
+from . import _hip
 from .flat import ensure_flat, flat_of
 
 
@@ -55,6 +63,48 @@ def allreduce_gradients(model: torch.nn.Module, optimizer=None):
     f = flat_of(params[0])
     if f is None:
         raise RuntimeError('model is not flattened')
-    allreduce_flat_grad(f.grad)
+    if f.lazy:
+        allreduce_flat_grad(f.grad[:f.dense_numel])
+        exchange_lazy_grads(f)
+    else:
+        allreduce_flat_grad(f.grad)
     if optimizer is not None:
         optimizer.grad_scale = 1.0 / dist.get_world_size()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def exchange_lazy_grads(f):
+    """Row-sparse gradient exchange of every lazy table of flat buffer f (see module doc)."""
+    world = dist.get_world_size()
+    dev = f.data.device
+    # ids looked up since the last exchange (host count; a replayed hipGraph does not re-run the
+    # host side, so the last non-zero count stands in for the replayed forward)
+    for t in f.lazy:
+        if t.cap > 0:
+            t.cap_used, t.cap = t.cap, 0
+    caps = torch.tensor([max(1, min(t.cap_used, t.V)) for t in f.lazy], dtype=torch.int64, device=dev)
+    dist.all_reduce(caps, op=dist.ReduceOp.MAX)
+    caps = caps.tolist()
+    nccl = dist.get_backend() == 'nccl'
+    for t, cap in zip(f.lazy, caps):
+        n = cap * (t.D + 1)
+        buf = torch.empty(n, dtype=torch.float32, device=dev)
+        _hip.call('rs_sparse_pack', t.ptr(f.grad), t.list.data_ptr(), t.count.data_ptr(), t.D, cap,
+                  buf.data_ptr(), None, _stream())
+        allbuf = torch.empty(world * n, dtype=torch.float32, device=dev)
+        if nccl:
+            dist.all_gather_into_tensor(allbuf, buf)
+        else:
+            dist.all_gather(list(allbuf.split(n)), buf)
+        _hip.call('rs_sparse_zero_grad', t.ptr(f.grad), t.list.data_ptr(), t.count.data_ptr(), t.D,
+                  _stream())
+        for r in range(world):  # fixed summation order: identical rows on every rank
+            _hip.call('rs_sparse_unpack_add', t.ptr(f.grad), t.flag.data_ptr(),
+                      allbuf.data_ptr() + 4 * r * n, t.D, cap, _stream())
+        ws = torch.empty(int(_hip.lib().rs_sparse_compact_ws_bytes(t.V)) // 4 + 1, dtype=torch.int32,
+                         device=dev)
+        _hip.call('rs_sparse_compact', t.flag.data_ptr(), t.V, t.list.data_ptr(), t.count.data_ptr(),
+                  ws.data_ptr(), _stream())

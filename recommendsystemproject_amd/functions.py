@@ -22,7 +22,7 @@ import torch
 from torch.autograd.function import once_differentiable
 
 from . import _hip, ops
-from .flat import grad_of
+from .flat import grad_of, touch_table
 
 
 def _seg(**kw):
@@ -35,6 +35,15 @@ def _seg(**kw):
 
 def _pad(v):
     return -1 if v is None else int(v)
+
+
+def _touch_lazy(segs, tables, rows):
+    """Lazy-exact Adam tables (flat.py): list the rows this lookup reads and bring them to the
+    current optimizer step before the gather (no-op for ordinary tables)."""
+    for s, t in zip(segs, tables):
+        if s.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL) and hasattr(t, '_rs_lazy'):
+            bag = s.bag if s.kind == _hip.RS_SEG_POOL else 1
+            touch_table(t, s.idx, rows, bag, s.idx_stride, s.pad_idx)
 
 
 # ================================================================================ sequence input
@@ -86,6 +95,7 @@ def seq_input_fwd(proc, seqd, B, L, p, key, err):
     M = B * L
     dev = proc.pos_emb.weight.device
     cat = torch.empty(M, dcat, device=dev, dtype=torch.float32)
+    _touch_lazy(segs, tables, M)
     ops.gather_fwd(segs, M, cat, err)
     lin = proc.feature_projection[0]
     pos = proc.pos_emb.weight
@@ -321,6 +331,7 @@ class TowerFeatureFn(torch.autograd.Function):
             raise RuntimeError(f'too many features in one tower ({len(segs)} > {_hip.MAX_SEGMENTS})')
         dev = tower.feature_bn.weight.device
         out = torch.empty(B, col, device=dev, dtype=torch.float32)
+        _touch_lazy(segs, [w for w, _ in pp], B)
         ops.gather_fwd(segs, B, out, tower.err_flag)
         if need:
             ctx.segs, ctx.pp, ctx.keep, ctx.B = segs, pp, keep, B

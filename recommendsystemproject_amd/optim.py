@@ -13,6 +13,8 @@ import torch
 from . import _hip, ops
 from .flat import flat_of
 
+CONSTS_CAP = 1 << 22  # max optimizer steps with lazy tables (32 MB of per-step constants)
+
 
 def _flat_cover(params):
     """The FlatParams that `params` is exactly (same objects, same order), else None."""
@@ -33,11 +35,19 @@ class _DeviceClip:
         self.norm = torch.zeros((), device=device, dtype=torch.float32)
         self.coef = torch.ones((), device=device, dtype=torch.float32)
 
-    def compute(self, g, n, max_norm, scale=1.0):
-        ws = torch.empty(max(int(_hip.lib().rs_sqnorm_ws_bytes(n)), 16), dtype=torch.uint8, device=g.device)
+    def compute(self, g, n, max_norm, scale=1.0, lazy=()):
+        """2-norm of g[:n] plus the listed rows of every lazy table (their other rows hold no
+        gradient), one double partial per block, summed in one fixed order."""
+        L = _hip.lib()
+        nd = int(L.rs_sqnorm_parts(n))
+        ns = int(L.rs_sparse_sqnorm_parts())
+        ws = torch.empty(nd + ns * len(lazy) + 2, dtype=torch.float64, device=g.device)
         _hip.call('rs_grad_sqnorm', g.data_ptr(), n, float(scale), ws.data_ptr(), ops.stream())
-        _hip.call('rs_clip_coef', ws.data_ptr(), n, float(max_norm), self.norm.data_ptr(),
-                  self.coef.data_ptr(), ops.stream())
+        for k, t in enumerate(lazy):
+            _hip.call('rs_sparse_sqnorm', t.ptr(g), t.list.data_ptr(), t.count.data_ptr(), t.D,
+                      float(scale), ws.data_ptr() + 8 * (nd + k * ns), ops.stream())
+        _hip.call('rs_clip_coef', ws.data_ptr(), nd + ns * len(lazy), float(max_norm),
+                  self.norm.data_ptr(), self.coef.data_ptr(), ops.stream())
 
 
 def clip_grad_norm_(parameters, max_norm, norm_type=2.0, error_if_nonfinite=False, foreach=None):
@@ -54,7 +64,9 @@ def clip_grad_norm_(parameters, max_norm, norm_type=2.0, error_if_nonfinite=Fals
     f = _flat_cover(list(parameters))
     clip = _DeviceClip(params[0].device)
     if f is not None:
-        clip.compute(f.grad, f.numel, max_norm)
+        # lazy tables: their unlisted gradient rows are zero, so scaling the whole region is
+        # correct (one sweep of the table gradient: the fused Adam clip avoids it)
+        clip.compute(f.grad, f.dense_numel, max_norm, lazy=f.lazy)
         _hip.call('rs_scale_inplace', f.grad.data_ptr(), f.numel, 1.0, clip.coef.data_ptr(), ops.stream())
     else:
         # per-tensor partial sums into one workspace would need a multi-tensor kernel; gather
@@ -92,6 +104,9 @@ class Adam(torch.optim.Optimizer):
         if st is None or st['f'] is not f:
             st = dict(f=f, m=torch.zeros_like(f.data), v=torch.zeros_like(f.data), step=0,
                       step_dev=torch.zeros((), dtype=torch.int64, device=f.data.device))
+            if f.lazy:
+                # consts[s] = {lr/bc1(s), sqrt(bc2(s))} for every step s, replayed by catch-up
+                st['consts'] = torch.zeros(CONSTS_CAP, 2, dtype=torch.float32, device=f.data.device)
             self._flat_state[id(f)] = st
             for p, o in zip(f.params, f.offsets):
                 self.state[p] = {'step': torch.tensor(0.0),
@@ -133,18 +148,34 @@ class Adam(torch.optim.Optimizer):
                 _hip.require_device(f.data)
                 st = self._state_for_flat(f)
                 st['step'] += 1
+                lr, eps, wd = float(group['lr']), float(group['eps']), float(group['weight_decay'])
                 coef = None
                 if clip_max_norm is not None and clip_max_norm > 0:
                     if self._clip is None:
                         self._clip = _DeviceClip(f.data.device)
-                    self._clip.compute(f.grad, f.numel, clip_max_norm, self.grad_scale)
+                    self._clip.compute(f.grad, f.dense_numel, clip_max_norm, self.grad_scale, f.lazy)
                     coef = self._clip.coef.data_ptr()
                 # device-side step count: the same launch replays correctly inside a hipGraph
-                _hip.call('rs_counter_add', st['step_dev'].data_ptr(), 1, ops.stream())
+                if f.lazy:
+                    if st['step'] >= CONSTS_CAP - 1:
+                        raise RuntimeError(f'lazy Adam: more than {CONSTS_CAP - 2} steps; raise optim.CONSTS_CAP')
+                    _hip.call('rs_adam_prepare', st['step_dev'].data_ptr(), st['consts'].data_ptr(),
+                              CONSTS_CAP, lr, float(b1), float(b2), ops.stream())
+                else:
+                    _hip.call('rs_counter_add', st['step_dev'].data_ptr(), 1, ops.stream())
                 _hip.call('rs_adam_step', f.data.data_ptr(), f.grad.data_ptr(), st['m'].data_ptr(),
-                          st['v'].data_ptr(), f.numel, float(group['lr']), float(b1), float(b2),
-                          float(group['eps']), float(group['weight_decay']), 0,
+                          st['v'].data_ptr(), f.dense_numel, lr, float(b1), float(b2), eps, wd, 0,
                           st['step_dev'].data_ptr(), float(self.grad_scale), coef, 0, ops.stream())
+                if f.lazy:
+                    hyper = (float(b1), float(b2), eps, wd)
+                    f.lazy_opt = dict(m=st['m'], v=st['v'], step_dev=st['step_dev'],
+                                      consts=st['consts'], hyper=hyper)
+                    for t in f.lazy:
+                        _hip.call('rs_sparse_adam', t.ptr(f.data), t.ptr(f.grad), t.ptr(st['m']),
+                                  t.ptr(st['v']), t.last.data_ptr(), t.flag.data_ptr(),
+                                  t.list.data_ptr(), t.count.data_ptr(), t.D,
+                                  st['step_dev'].data_ptr(), st['consts'].data_ptr(), *hyper,
+                                  float(self.grad_scale), coef, ops.stream())
                 continue
             if clip_max_norm is not None and clip_max_norm > 0:
                 clip_grad_norm_(group['params'], clip_max_norm)
@@ -167,6 +198,7 @@ class Adam(torch.optim.Optimizer):
 
     def state_dict(self):
         for st in self._flat_state.values():
+            st['f'].flush()  # lazy tables: exp_avg / exp_avg_sq rows current
             step = float(st['step_dev'].item())  # authoritative (graph replays advance it)
             for p in st['f'].params:
                 if p in self.state:

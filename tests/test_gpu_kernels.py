@@ -331,7 +331,8 @@ def test_clip_coefficient():
     norm = torch.zeros((), device=DEV)
     coef = torch.zeros((), device=DEV)
     _hip.call('rs_grad_sqnorm', g.data_ptr(), g.numel(), 0.5, ws.data_ptr(), ops.stream())
-    _hip.call('rs_clip_coef', ws.data_ptr(), g.numel(), 1.0, norm.data_ptr(), coef.data_ptr(), ops.stream())
+    nparts = int(_hip.lib().rs_sqnorm_parts(g.numel()))
+    _hip.call('rs_clip_coef', ws.data_ptr(), nparts, 1.0, norm.data_ptr(), coef.data_ptr(), ops.stream())
     tn = (0.5 * g).norm().item()
     assert abs(norm.item() - tn) < 1e-5 * tn
     assert abs(coef.item() - min(1.0, 1.0 / (tn + 1e-6))) < 1e-6
