@@ -98,6 +98,9 @@ typedef struct rs_feature_seg {
                              kind 2 weight grad [dim]; kind 3 src grad [rows*bag, dim] (+=);
                              kind 4 src grad [rows, dim] (=) */
   float* grad_bias;       /* kind 2 bias grad [dim] */
+  const int* touch_count; /* kind 0/1, nullable: per-row lookup count of this optimizer step
+                             (rs_sparse_touch); a row looked up once gets its gradient by a
+                             plain store instead of an atomic add */
 } rs_feature_seg_t;
 
 int rs_gather_fwd(const rs_feature_seg_t* segs, int nseg, int rows, float* out, int ldo,

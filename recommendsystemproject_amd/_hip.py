@@ -25,7 +25,7 @@ class FeatureSeg(C.Structure):
     """Mirror of rs_feature_seg_t."""
     _fields_ = [('kind', i32), ('dim', i32), ('out_col', i32), ('pool_mode', i32), ('bag', i32),
                 ('pad_idx', i32), ('vocab', i64), ('idx_stride', i64), ('idx', vp), ('table', vp),
-                ('bias', vp), ('x', vp), ('grad', vp), ('grad_bias', vp)]
+                ('bias', vp), ('x', vp), ('grad', vp), ('grad_bias', vp), ('touch_count', vp)]
 
 
 # name -> (restype, argtypes). Every symbol declared in include/rsys_hip.h.

@@ -22,6 +22,8 @@ constexpr int kMaxSeg = 24;  // segments travel by value in the kernel arguments
 // would otherwise serialise on a few hundred addresses
 constexpr int64_t kSmallTableBytes = 48 * 1024;
 
+constexpr int kBagBatch = 8;               // bag ids (and rows) loaded per batch
+
 struct SegLaunch {
   rs_feature_seg_t segs[kMaxSeg];
   int nseg;
@@ -39,6 +41,7 @@ struct SegLaunch {
   int sblocks[kMaxSeg];
   int small_lds;        // bytes of dynamic LDS for the small-table kernel
 };
+static_assert(sizeof(SegLaunch) <= 4096, "SegLaunch must fit the kernel-argument segment");
 
 __device__ __forceinline__ int find_seg(const SegLaunch& a, int bid) {
   int s = 0;
@@ -65,6 +68,12 @@ __device__ __forceinline__ void load_row(const float* p, float* v) {
 }
 
 template <bool VEC>
+__device__ __forceinline__ void store_row(float* p, const float* v) {
+  if (VEC) *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  else p[0] = v[0];
+}
+
+template <bool VEC>
 __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int row, int chunk) {
   constexpr int W = VEC ? 4 : 1;
   const int c = chunk * W;
@@ -79,16 +88,29 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
 #pragma unroll
       for (int j = 0; j < W; ++j) acc[j] = -INFINITY;
     }
-    for (int l = 0; l < sg.bag; ++l) {
-      const int64_t id = ids[l];
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (id_ok(id, sg.vocab, a.err)) load_row<VEC>(sg.table + id * sg.dim + c, v);
-      if (sg.pool_mode == RS_POOL_MAX) {
+    // kBagBatch ids, then their kBagBatch rows, in flight at once (the row loads depend on the
+    // id loads: a one-at-a-time loop is latency-bound); summation order stays l = 0, 1, ...
+    for (int l0 = 0; l0 < sg.bag; l0 += kBagBatch) {
+      const int nb = sg.bag - l0 < kBagBatch ? sg.bag - l0 : kBagBatch;
+      int64_t id[kBagBatch];
 #pragma unroll
-        for (int j = 0; j < W; ++j) acc[j] = fmaxf(acc[j], v[j]);
-      } else {
+      for (int u = 0; u < kBagBatch; ++u) id[u] = u < nb ? ids[l0 + u] : 0;
+      float v[kBagBatch][4];
 #pragma unroll
-        for (int j = 0; j < W; ++j) acc[j] += v[j];
+      for (int u = 0; u < kBagBatch; ++u) {
+        v[u][0] = v[u][1] = v[u][2] = v[u][3] = 0.f;
+        if (u < nb && id_ok(id[u], sg.vocab, a.err)) load_row<VEC>(sg.table + id[u] * sg.dim + c, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kBagBatch; ++u) {
+        if (u >= nb) break;
+        if (sg.pool_mode == RS_POOL_MAX) {
+#pragma unroll
+          for (int j = 0; j < W; ++j) acc[j] = fmaxf(acc[j], v[u][j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < W; ++j) acc[j] += v[u][j];
+        }
       }
     }
     if (sg.pool_mode == RS_POOL_MEAN) {
@@ -138,6 +160,10 @@ __device__ void scatter_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int 
     const int64_t id = sg.idx[(int64_t)row * sg.idx_stride];
     if (id == sg.pad_idx || id < 0 || id >= sg.vocab) return;
     float* d = (LDS_ACC ? lds : sg.grad) + id * sg.dim + c;
+    if (!LDS_ACC && sg.touch_count && sg.touch_count[id] == 1) {
+      store_row<VEC>(d, g);  // the row's only lookup this step: its gradient row is still zero
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < W; ++j) atomicAdd(d + j, g[j]);
   } else if (sg.kind == RS_SEG_POOL) {
@@ -167,12 +193,30 @@ __device__ void scatter_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int 
 #pragma unroll
       for (int j = 0; j < W; ++j) g[j] = g[j] / n;
     }
-    for (int l = 0; l < sg.bag; ++l) {
-      const int64_t id = ids[l];
-      if (id == sg.pad_idx || id < 0 || id >= sg.vocab) continue;
-      float* d = (LDS_ACC ? lds : sg.grad) + id * sg.dim + c;
+    for (int l0 = 0; l0 < sg.bag; l0 += kBagBatch) {
+      const int nb = sg.bag - l0 < kBagBatch ? sg.bag - l0 : kBagBatch;
+      int64_t id[kBagBatch];
+      bool use[kBagBatch];
 #pragma unroll
-      for (int j = 0; j < W; ++j) atomicAdd(d + j, g[j]);
+      for (int u = 0; u < kBagBatch; ++u) {
+        id[u] = u < nb ? ids[l0 + u] : 0;
+        use[u] = u < nb && id[u] != sg.pad_idx && id[u] >= 0 && id[u] < sg.vocab;
+      }
+      int once[kBagBatch];
+#pragma unroll
+      for (int u = 0; u < kBagBatch; ++u)
+        once[u] = (!LDS_ACC && sg.touch_count && use[u]) ? sg.touch_count[id[u]] == 1 : 0;
+#pragma unroll
+      for (int u = 0; u < kBagBatch; ++u) {
+        if (!use[u]) continue;
+        float* d = (LDS_ACC ? lds : sg.grad) + id[u] * sg.dim + c;
+        if (once[u]) {
+          store_row<VEC>(d, g);
+        } else {
+#pragma unroll
+          for (int j = 0; j < W; ++j) atomicAdd(d + j, g[j]);
+        }
+      }
     }
   } else if (sg.kind == RS_SEG_LASTVALID) {
     const int64_t l = sg.idx[row];

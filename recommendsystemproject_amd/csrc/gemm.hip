@@ -11,6 +11,7 @@
 // Split-K (reductions over M = B*L for weight gradients) writes f32 partial slabs that a second
 // kernel sums in a fixed order (bitwise reproducible) and finishes with the epilogue.
 #include "common.h"
+#include "gemm_stream.h"
 #include "rng.h"
 
 namespace rs {
@@ -268,31 +269,6 @@ void launch_tile(const GemmArgs& g, int ta, int tb, hipStream_t st) {
 }
 
 }  // namespace
-
-// gemm_stream.hip
-struct StreamArgs {
-  int M, N, K;
-  float alpha, beta;
-  const float* A; int lda;
-  const float* B; int ldb;
-  float* C; int ldc;
-  int epi;
-  const float* bias;
-  const float* aux; int ld_aux, aux_mod;
-  float* rowsum;
-  float* ws;
-  int transB;
-  float drop_p;
-  const int64_t* drop_key;
-  int site_a, site_b;
-};
-bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda);
-int rowgemm_launch(const StreamArgs& s, hipStream_t st);
-bool wgrad_supported(int transA, int transB, int M, int N, int K, const float* A, int lda,
-                     const float* B, int ldb, int ldc, int epi);
-int64_t wgrad_ws_bytes(int M, int N, int K);
-int wgrad_launch(const StreamArgs& s, hipStream_t st);
-
 }  // namespace rs
 
 using namespace rs;

@@ -15,26 +15,12 @@
 //   k-major exactly as they lie in memory (no transposition), partial tiles are summed by a
 //   fixed-order reduce (deterministic), and the bias gradient colsum(dY) is fused.
 #include "common.h"
+#include "gemm_stream.h"
 #include "rng.h"
 
 namespace rs {
 
-struct StreamArgs {
-  int M, N, K;
-  float alpha, beta;
-  const float* A; int lda;
-  const float* B; int ldb;
-  float* C; int ldc;
-  int epi;
-  const float* bias;
-  const float* aux; int ld_aux, aux_mod;
-  float* rowsum;
-  float* ws;
-  int transB;
-  float drop_p;
-  const int64_t* drop_key;
-  int site_a, site_b;
-};
+
 
 namespace {
 
@@ -56,6 +42,34 @@ __device__ __forceinline__ float epi_apply(const StreamArgs& a, int m, int n, fl
     v += a.aux[(int64_t)(m % a.aux_mod) * a.ld_aux + n];
   }
   if (a.beta != 0.f) v += a.beta * a.C[(int64_t)m * a.ldc + n];
+  return v;
+}
+
+// four consecutive columns n0..n0+3 of row m (same order of operations as epi_apply)
+__device__ __forceinline__ floatx4 epi_apply4(const StreamArgs& a, int m, int n0, floatx4 v,
+                                              const DropKey& ka, const DropKey& kb) {
+  if (a.epi & RS_EPI_BIAS) v += *reinterpret_cast<const floatx4*>(a.bias + n0);
+  if (a.epi & RS_EPI_AUX_MASK) {
+    const floatx4 mk = *reinterpret_cast<const floatx4*>(a.aux + (int64_t)m * a.ld_aux + n0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = mk[i] > 0.f ? v[i] : 0.f;
+  }
+  if (a.epi & RS_EPI_RELU) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], 0.f);
+  }
+  const uint64_t e0 = (uint64_t)m * a.N + n0;
+  if (a.epi & RS_EPI_DROP_A) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] *= keep_mult(ka, e0 + i);
+  }
+  if (a.epi & RS_EPI_AUX_ADD)
+    v += *reinterpret_cast<const floatx4*>(a.aux + (int64_t)(m % a.aux_mod) * a.ld_aux + n0);
+  if (a.epi & RS_EPI_DROP_B) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] *= keep_mult(kb, e0 + i);
+  }
+  if (a.beta != 0.f) v += a.beta * *reinterpret_cast<const floatx4*>(a.C + (int64_t)m * a.ldc + n0);
   return v;
 }
 
@@ -119,21 +133,27 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
         if (two) b1 = *reinterpret_cast<const floatx4*>(&Bs[((j0 + 1) * 16 + r) * KP + 16 * t + 4 * q]);
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(areg[t][s4], b0[s4], acc0, 0, 0, 0);
-          if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(areg[t][s4], b1[s4], acc1, 0, 0, 0);
+          // W rows on the MFMA row side, the 16 A rows on the column side: each lane ends up
+          // holding 4 consecutive output columns of one row (float4 epilogue loads / stores)
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(b0[s4], areg[t][s4], acc0, 0, 0, 0);
+          if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(b1[s4], areg[t][s4], acc1, 0, 0, 0);
         }
       }
-      // C/D map of 16x16: col = lane&15, row = 4*(lane>>4) + i
+      // C/D map of 16x16: col = lane&15 -> row m of A, row = 4*(lane>>4) + i -> column n of C
+      const int m = g * 16 + r;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         if (h == 1 && !two) break;
-        const int n = nb0 + (j0 + h) * 16 + r;
-        if (n >= a.N) continue;
-        const floatx4 acc = h ? acc1 : acc0;
+        const int n0 = nb0 + (j0 + h) * 16 + 4 * q;
+        if (m >= a.M || n0 >= a.N) continue;
+        const floatx4 acc = (h ? acc1 : acc0) * a.alpha;
+        float* crow = a.C + (int64_t)m * a.ldc;
+        if (a.vec_epi && n0 + 3 < a.N) {
+          *reinterpret_cast<floatx4*>(crow + n0) = epi_apply4(a, m, n0, acc, ka, kb);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = g * 16 + 4 * q + i;
-          if (m < a.M) a.C[(int64_t)m * a.ldc + n] = epi_apply(a, m, n, a.alpha * acc[i], ka, kb);
+          for (int i = 0; i < 4; ++i)
+            if (n0 + i < a.N) crow[n0 + i] = epi_apply(a, m, n0 + i, acc[i], ka, kb);
         }
       }
     }
@@ -319,7 +339,11 @@ bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda)
   }
 }
 
-int rowgemm_launch(const StreamArgs& s, hipStream_t st) {
+int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
+  StreamArgs s = s_in;
+  s.vec_epi = s.N % 4 == 0 && s.ldc % 4 == 0 && aligned16(s.C) &&
+              (!(s.epi & RS_EPI_BIAS) || aligned16(s.bias)) &&
+              (!(s.epi & (RS_EPI_AUX_ADD | RS_EPI_AUX_MASK)) || (s.ld_aux % 4 == 0 && aligned16(s.aux)));
   const bool small = s.M < kSmallM;
   const int nt = small ? 4 : (s.N + 15) / 16, kt = (s.K + 15) / 16;
   const int nsplit = small ? cdiv(s.N, 64) : 1;

@@ -159,8 +159,8 @@ int ln_blocks(int M) {
 
 // ------------------------------------------------------------------------------ BatchNorm
 int bn_chunks(int Bg) {
-  int s = cdiv(Bg, 256);
-  if (s > 64) s = 64;
+  int s = cdiv(Bg, 64);  // 64-row chunks: 16 rows per thread in the partial kernel
+  if (s > 512) s = 512;
   if (s < 1) s = 1;
   return s;
 }
@@ -213,31 +213,114 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const float* __restrict
   }
 }
 
-__global__ void bn_fwd_final_kernel(const double* __restrict__ ws, int G, int S, int Bg, int C,
-                                    float momentum, float eps, float* __restrict__ mean,
-                                    float* __restrict__ rstd, float* running_mean,
-                                    float* running_var, int64_t* num_batches) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && num_batches) *num_batches += G;
-  if (c >= C) return;
-  for (int g = 0; g < G; ++g) {
-    double sa = 0.0, sb = 0.0;
-    for (int s = 0; s < S; ++s) {
+// column statistics of group g from the S chunk partials, summed in a fixed order (4 row lanes
+// strided over the chunks, then lane 0..3): every block of the column group gets the same bits
+__device__ __forceinline__ void bn_col_sums(const double* __restrict__ ws, int g, int S, int C,
+                                            int c, int rl, double (*red)[2][64], double& A,
+                                            double& Bv) {
+  const int cl = threadIdx.x & 63;
+  double sa = 0.0, sb = 0.0;
+  if (c < C)
+    for (int s = rl; s < S; s += 4) {
       const int64_t base = ((int64_t)g * S + s) * 2 * C;
       sa += ws[base + c];
       sb += ws[base + C + c];
     }
-    const double n = (double)Bg;
-    const double mu = sa / n;
-    double var = sb / n - mu * mu;
-    if (var < 0.0) var = 0.0;
-    mean[g * C + c] = (float)mu;
-    rstd[g * C + c] = (float)(1.0 / sqrt(var + (double)eps));
-    if (running_mean) {
-      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mu;
-      const double unb = Bg > 1 ? var * n / (n - 1.0) : var;
-      running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  red[rl][0][cl] = sa;
+  red[rl][1][cl] = sb;
+  __syncthreads();
+  A = red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl];
+  Bv = red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl];
+  __syncthreads();
+}
+
+// training forward, second kernel: stats from the partials + normalise this block's row chunk.
+// Block (column group, g, chunk); chunk-0 blocks publish mean/rstd, block (cg, 0, 0) updates the
+// running statistics for g = 0..G-1 in order.
+__global__ __launch_bounds__(256) void bn_fwd_norm_kernel(
+    const double* __restrict__ ws, const float* __restrict__ x, float* __restrict__ y,
+    const float* __restrict__ w, const float* __restrict__ b, float* running_mean,
+    float* running_var, int64_t* num_batches, float* __restrict__ mean, float* __restrict__ rstd,
+    int G, int Bg, int C, int S, float momentum, float eps, int relu) {
+  __shared__ double red[4][2][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int g = blockIdx.y, s = blockIdx.z;
+  const double n = (double)Bg;
+  double A, Bv;
+  if (g == 0 && s == 0 && running_mean) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && num_batches) *num_batches += G;
+    for (int gg = 0; gg < G; ++gg) {
+      bn_col_sums(ws, gg, S, C, c, rl, red, A, Bv);
+      if (rl == 0 && c < C) {
+        const double mu = A / n;
+        double var = Bv / n - mu * mu;
+        if (var < 0.0) var = 0.0;
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mu;
+        const double unb = Bg > 1 ? var * n / (n - 1.0) : var;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+      }
     }
+  } else if (blockIdx.x == 0 && g == 0 && s == 0 && threadIdx.x == 0 && num_batches) {
+    *num_batches += G;
+  }
+  bn_col_sums(ws, g, S, C, c, rl, red, A, Bv);
+  if (c >= C) return;
+  const double mu = A / n;
+  double var = Bv / n - mu * mu;
+  if (var < 0.0) var = 0.0;
+  const float muf = (float)mu, r = (float)(1.0 / sqrt(var + (double)eps));
+  if (s == 0 && rl == 0) {
+    mean[g * C + c] = muf;
+    rstd[g * C + c] = r;
+  }
+  const float wc = w[c], bc = b[c];
+  const int rpc = (Bg + S - 1) / S;
+  const int r1 = min(Bg, (s + 1) * rpc);
+  for (int i = s * rpc + rl; i < r1; i += 4) {
+    const int64_t o = ((int64_t)g * Bg + i) * C + c;
+    float v = (x[o] - muf) * r * wc + bc;
+    if (relu) v = fmaxf(v, 0.f);
+    y[o] = v;
+  }
+}
+
+// backward, second kernel: mean(dy'), mean(dy' * xhat) from the partials + dx for this block's
+// row chunk; block (cg, 0, 0) accumulates dW = sum dy' xhat and dB = sum dy' over all groups.
+__global__ __launch_bounds__(256) void bn_bwd_dx_kernel(
+    const double* __restrict__ ws, const float* __restrict__ x, const float* __restrict__ y,
+    const float* __restrict__ dy, const float* __restrict__ w, const float* __restrict__ mean,
+    const float* __restrict__ rstd, float* __restrict__ dx, float* dw, float* db, int G, int Bg,
+    int C, int S, int relu) {
+  __shared__ double red[4][2][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int g = blockIdx.y, s = blockIdx.z;
+  double A, Bv;
+  if (g == 0 && s == 0) {
+    double tw = 0.0, tb = 0.0;
+    for (int gg = 0; gg < G; ++gg) {
+      bn_col_sums(ws, gg, S, C, c, rl, red, A, Bv);
+      tb += A;
+      tw += Bv;
+    }
+    if (rl == 0 && c < C) {
+      dw[c] += (float)tw;
+      db[c] += (float)tb;
+    }
+  }
+  bn_col_sums(ws, g, S, C, c, rl, red, A, Bv);
+  if (c >= C) return;
+  const float mdy = (float)(A / Bg), mdyx = (float)(Bv / Bg);
+  const float mu = mean[g * C + c], r = rstd[g * C + c], wr = w[c] * r;
+  const int rpc = (Bg + S - 1) / S;
+  const int r1 = min(Bg, (s + 1) * rpc);
+  for (int i = s * rpc + rl; i < r1; i += 4) {
+    const int64_t o = ((int64_t)g * Bg + i) * C + c;
+    float d = dy[o];
+    if (relu && !(y[o] > 0.f)) d = 0.f;
+    const float xh = (x[o] - mu) * r;
+    dx[o] = wr * (d - mdy - xh * mdyx);
   }
 }
 
@@ -262,45 +345,6 @@ __global__ void bn_norm_kernel(const float* __restrict__ x, float* __restrict__ 
     float v = (x[idx] - mean[g * C + c]) * rstd[g * C + c] * w[c] + b[c];
     if (relu) v = fmaxf(v, 0.f);
     y[idx] = v;
-  }
-}
-
-__global__ void bn_bwd_final_kernel(const double* __restrict__ ws, int G, int S, int Bg, int C,
-                                    float* __restrict__ stats, float* dw, float* db) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double tw = 0.0, tb = 0.0;
-  for (int g = 0; g < G; ++g) {
-    double sa = 0.0, sb = 0.0;
-    for (int s = 0; s < S; ++s) {
-      const int64_t base = ((int64_t)g * S + s) * 2 * C;
-      sa += ws[base + c];
-      sb += ws[base + C + c];
-    }
-    stats[(int64_t)g * 2 * C + c] = (float)(sa / Bg);
-    stats[(int64_t)g * 2 * C + C + c] = (float)(sb / Bg);
-    tb += sa;
-    tw += sb;
-  }
-  dw[c] += (float)tw;
-  db[c] += (float)tb;
-}
-
-__global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restrict__ y,
-                             const float* __restrict__ dy, const float* __restrict__ w,
-                             const float* __restrict__ mean, const float* __restrict__ rstd,
-                             const float* __restrict__ stats, float* __restrict__ dx, int Bg,
-                             int C, int64_t total, int relu) {
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(idx % C);
-    const int g = (int)(idx / ((int64_t)Bg * C));
-    float d = dy[idx];
-    if (relu && !(y[idx] > 0.f)) d = 0.f;
-    const float r = rstd[g * C + c];
-    const float xh = (x[idx] - mean[g * C + c]) * r;
-    const float mdy = stats[(int64_t)g * 2 * C + c], mdyx = stats[(int64_t)g * 2 * C + C + c];
-    dx[idx] = w[c] * r * (d - mdy - xh * mdyx);
   }
 }
 
@@ -470,10 +514,9 @@ extern "C" int rs_batchnorm_fwd(const float* x, float* y, const float* w, const 
   bn_partial_kernel<0><<<dim3(cdiv(C, 64), G, S), 256, 0, st>>>(x, nullptr, nullptr, nullptr,
                                                                  nullptr, Bg, C, S, 0, wsd);
   RS_CHECK_LAUNCH("rs_batchnorm_fwd partial");
-  bn_fwd_final_kernel<<<cdiv(C, 256), 256, 0, st>>>(wsd, G, S, Bg, C, momentum, eps, mean, rstd,
-                                                    running_mean, running_var, num_batches);
-  RS_CHECK_LAUNCH("rs_batchnorm_fwd final");
-  bn_norm_kernel<<<blocks, 256, 0, st>>>(x, y, w, b, mean, rstd, Bg, C, total, relu);
+  bn_fwd_norm_kernel<<<dim3(cdiv(C, 64), G, S), 256, 0, st>>>(wsd, x, y, w, b, running_mean,
+                                                              running_var, num_batches, mean, rstd,
+                                                              G, Bg, C, S, momentum, eps, relu);
   RS_CHECK_LAUNCH("rs_batchnorm_fwd norm");
   return 0;
 }
@@ -489,16 +532,11 @@ extern "C" int rs_batchnorm_bwd(const float* x, const float* y, const float* dy,
   hipStream_t st = as_stream(stream);
   const int S = bn_chunks(Bg);
   double* wsd = reinterpret_cast<double*>(ws);
-  float* stats = reinterpret_cast<float*>(wsd + (int64_t)G * S * 2 * C);
   bn_partial_kernel<1><<<dim3(cdiv(C, 64), G, S), 256, 0, st>>>(x, y, dy, mean, rstd, Bg, C, S,
                                                                  relu, wsd);
   RS_CHECK_LAUNCH("rs_batchnorm_bwd partial");
-  bn_bwd_final_kernel<<<cdiv(C, 256), 256, 0, st>>>(wsd, G, S, Bg, C, stats, dw, db);
-  RS_CHECK_LAUNCH("rs_batchnorm_bwd final");
-  const int64_t total = (int64_t)G * Bg * C;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 8192) blocks = 8192;
-  bn_dx_kernel<<<blocks, 256, 0, st>>>(x, y, dy, w, mean, rstd, stats, dx, Bg, C, total, relu);
+  bn_bwd_dx_kernel<<<dim3(cdiv(C, 64), G, S), 256, 0, st>>>(wsd, x, y, dy, w, mean, rstd, dx, dw,
+                                                            db, G, Bg, C, S, relu);
   RS_CHECK_LAUNCH("rs_batchnorm_bwd dx");
   return 0;
 }

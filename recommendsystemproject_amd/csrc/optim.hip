@@ -48,11 +48,19 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g
   if (threadIdx.x == 0) ws[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ void clip_coef_kernel(const double* __restrict__ ws, int nb, float max_norm,
-                                 float* total_norm, float* coef) {
-  if (threadIdx.x != 0) return;
+// fixed-order (deterministic) sum of nb partials: strided per-thread sums, then a fixed tree
+__global__ __launch_bounds__(1024) void clip_coef_kernel(const double* __restrict__ ws, int nb,
+                                                         float max_norm, float* total_norm,
+                                                         float* coef) {
+  __shared__ double red[16];
   double t = 0.0;
-  for (int i = 0; i < nb; ++i) t += ws[i];
+  for (int i = threadIdx.x; i < nb; i += 1024) t += ws[i];
+  t = wave_sum(t);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  t = 0.0;
+  for (int w = 0; w < 16; ++w) t += red[w];
   const float norm = (float)sqrt(t);
   if (total_norm) *total_norm = norm;
   float c = max_norm / (norm + 1e-6f);
@@ -159,7 +167,7 @@ extern "C" int rs_sqnorm_parts(int64_t n) { return sq_blocks(n); }
 extern "C" int rs_clip_coef(const double* ws, int nparts, float max_norm, float* total_norm,
                             float* coef, void* stream) {
   RS_CHECK_ARG(ws && coef && nparts >= 1, "rs_clip_coef: bad args");
-  clip_coef_kernel<<<1, 64, 0, as_stream(stream)>>>(ws, nparts, max_norm, total_norm, coef);
+  clip_coef_kernel<<<1, 1024, 0, as_stream(stream)>>>(ws, nparts, max_norm, total_norm, coef);
   RS_CHECK_LAUNCH("rs_clip_coef");
   return 0;
 }

@@ -67,7 +67,8 @@ __global__ void touch_kernel(const int64_t* __restrict__ ids, int rows, int bag,
     const int64_t r = e / bag, l = e - r * bag;
     const int64_t id = ids[r * stride + l];
     if (id < 0 || id >= vocab || id == pad) continue;
-    if (atomicExch(&flag[id], 1) == 0) list[atomicAdd(count, 1)] = (int)id;
+    // flag = lookups of the row this step (the gradient scatter stores instead of adding when 1)
+    if (atomicAdd(&flag[id], 1) == 0) list[atomicAdd(count, 1)] = (int)id;
   }
 }
 

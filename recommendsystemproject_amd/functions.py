@@ -44,6 +44,7 @@ def _touch_lazy(segs, tables, rows):
         if s.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL) and hasattr(t, '_rs_lazy'):
             bag = s.bag if s.kind == _hip.RS_SEG_POOL else 1
             touch_table(t, s.idx, rows, bag, s.idx_stride, s.pad_idx)
+            s.touch_count = t._rs_lazy.flag.data_ptr()
 
 
 # ================================================================================ sequence input

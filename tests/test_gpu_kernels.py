@@ -230,10 +230,11 @@ def test_layernorm_fwd_bwd():
     assert torch.allclose(dg, gr.grad, atol=1e-3) and torch.allclose(db, br.grad, atol=1e-3)
 
 
+@pytest.mark.parametrize('Bg', [300, 6000])  # single-kernel path / partials path (G*Bg > 16384)
 @pytest.mark.parametrize('G', [1, 3])
 @pytest.mark.parametrize('relu', [False, True])
-def test_batchnorm_train_fwd_bwd(G, relu):
-    Bg, C = 300, 172
+def test_batchnorm_train_fwd_bwd(G, relu, Bg):
+    C = 172
     bn = torch.nn.BatchNorm1d(C).to(DEV)
     with torch.no_grad():
         bn.weight.copy_(1 + 0.1 * rnd(C, seed=1))
