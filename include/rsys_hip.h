@@ -111,6 +111,17 @@ int64_t rs_gather_ws_bytes(const rs_feature_seg_t* segs_host, int nseg, int rows
 int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, const float* dout, int ldo,
                   float* ws, void* stream);
 
+/* h = dropout(A W^T + bias) + resid; y = LayerNorm(h)*gamma + beta; per-row mean / rstd.
+ * The post-LN residual block of nn.TransformerEncoderLayer (x + dropout(sublayer(x)) -> norm,
+ * SequenceEncoder.py:17-29) with the sublayer's closing Linear fused in: one streaming kernel
+ * for the encoder width (N = 64; K = 64 or 256), otherwise rs_gemm_f32 + rs_add_layernorm_fwd.
+ * A [M, lda], W [N, ldw] (nn.Linear weight), resid / h / y [M, N]; bias nullable. Dropout mask
+ * of element (m, n): site `site`, index m*N + n (the same draw as rs_add_layernorm_fwd). */
+int rs_gemm_add_layernorm(int M, int N, int K, const float* A, int lda, const float* W, int ldw,
+                          const float* bias, const float* resid, float* h, float* y,
+                          const float* gamma, const float* beta, float* mean, float* rstd, float eps,
+                          float p, const int64_t* key, int site, void* stream);
+
 /* ---------------------------------------------------------------- sequence mask
  * padding mask from the first sequence feature (== pad_value) with the all-padding-row fix,
  * and last-valid index (SequenceEncoder.py:36-46, :66-70; traps T6/T7).

@@ -37,6 +37,8 @@ SIGNATURES = {
     'rs_gemm_ws_bytes': (i64, [i32, i32, i32, i32]),
     'rs_gemm_f32': (i32, [i32, i32, i32, i32, i32, f32, vp, i32, vp, i32, f32, vp, i32, i32, vp, vp,
                           i32, i32, f32, vp, i32, i32, vp, i32, vp, vp]),
+    'rs_gemm_add_layernorm': (i32, [i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp,
+                                    f32, f32, vp, i32, vp]),
     'rs_colsum_ws_bytes': (i64, [i32, i32]),
     'rs_colsum': (i32, [vp, i32, i32, i32, f32, f32, vp, vp, vp]),
     'rs_gather_fwd': (i32, [vp, i32, i32, vp, i32, vp, vp]),

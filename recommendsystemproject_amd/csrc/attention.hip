@@ -187,6 +187,253 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const float* __restrict__
   }
 }
 
+// ============================================================================ MFMA path
+// head_dim 16, L <= 64 (the C2/C3 encoder: d = 64, H = 4, L = 50): one wave per (sample, head),
+// f32 MFMA 16x16x4 (exact f32 products, same rate as the VALU but a quarter of the issue slots
+// and the VALU left free for exp / masks / dropout hashes). NT = ceil(L/16) tiles of 16.
+//
+// Score tiles are computed transposed, S^T[key][query] = K Q^T: with the K fragment on the MFMA
+// row side each lane ends up owning ONE query (lane & 15) and 4 consecutive keys per tile
+// (4 * (lane >> 4) + e), so a query's softmax statistics reduce over the lane's own 4 NT values
+// plus two cross-lane xor shuffles (16, 32), and the lane's probabilities are directly the A
+// fragment of P V (k = key index), no data movement. Fragment loads are float4 rows of qkv:
+// lane (r = lane & 15, q = lane >> 4) holds X[row 16 t + r][4q .. 4q + 3], and MFMA s of a
+// 4-step k chain consumes component s (k = 4q + s), the permuted-k order used by rowgemm.
+typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float xsum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+__device__ __forceinline__ float xmax(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+
+// one wave per (b, h); 4 waves per workgroup = 4 consecutive (b, h) (the heads of one sample)
+template <int NT, bool DROP>
+__global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(
+    const float* __restrict__ qkv, const uint8_t* __restrict__ key_pad, float* __restrict__ out,
+    float* __restrict__ lse, int B, int L, int d, int H, float scale, float pdrop,
+    const int64_t* __restrict__ key, int site) {
+  constexpr int LP = NT * 16;
+  __shared__ __attribute__((aligned(16))) float Vsm[4][LP][16];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int bh = blockIdx.x * 4 + wave;
+  if (bh >= B * H) return;  // whole wave exits together (no block barrier below)
+  const int b = bh / H, h = bh % H;
+  const int ld = 3 * d;
+  const float* base = qkv + (int64_t)b * L * ld + h * 16;
+  float(*Vs)[16] = Vsm[wave];
+  f4 qf[NT], kf[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int row = t * 16 + r;
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    qf[t] = row < L ? ld4(base + (int64_t)row * ld + 4 * q) : z;
+    kf[t] = row < L ? ld4(base + (int64_t)row * ld + d + 4 * q) : z;
+    *reinterpret_cast<f4*>(&Vs[row][4 * q]) = row < L ? ld4(base + (int64_t)row * ld + 2 * d + 4 * q) : z;
+  }
+  // key validity for this lane's keys 16 t + 4 q + e
+  bool kok[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = t * 16 + 4 * q + e;
+      kok[t][e] = j < L && key_pad[(int64_t)b * L + j] == 0;
+    }
+  DropKey dk;
+  if (DROP) dk = make_key(key, site, pdrop);
+  const float scale2 = scale * kLog2e;
+  __builtin_amdgcn_wave_barrier();  // Vs written by this wave only
+#pragma unroll
+  for (int tq = 0; tq < NT; ++tq) {
+    f4 sv[NT];
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) {
+      f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) acc = mfma4(kf[tk][s4], qf[tq][s4], acc);
+      sv[tk] = acc;
+    }
+    // softmax over keys for query i = 16 tq + r (same op order as the VALU kernel:
+    // max of scale*s, then exp(scale*s - max))
+    // exp(x) = exp2(x * log2 e): one v_exp_f32 per probability (the softmax is VALU-bound)
+    float m = -INFINITY;
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (kok[tk][e]) m = fmaxf(m, sv[tk][e] * scale2);
+    m = xmax(m);
+    float l = 0.f;
+    const int i = tq * 16 + r;
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = kok[tk][e] ? exp2f(sv[tk][e] * scale2 - m) : 0.f;
+        l += pv;
+        sv[tk][e] = DROP ? pv * keep_mult(dk, ((uint64_t)bh * L + i) * L + tk * 16 + 4 * q + e) : pv;
+      }
+    l = xsum(l);
+    // O[i][c] = sum_j pz[i][j] V[j][c]: A = this lane's probabilities (row i = lane & 15,
+    // k = key), B = V[key][c = lane & 15]
+    f4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) o = mfma4(sv[tk][s4], Vs[tk * 16 + 4 * q + s4][r], o);
+    // o[e] = O[16 tq + 4 q + e][c = r]; its 1/l lives in lanes with (lane & 15) == 4 q + e
+    if (q == 0 && i < L) lse[(int64_t)bh * L + i] = (m + log2f(l)) * kLn2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float le = __shfl(l, 4 * q + e, 64);
+      const int row = tq * 16 + 4 * q + e;
+      if (row < L) out[((int64_t)b * L + row) * d + h * 16 + r] = o[e] * (1.f / le);
+    }
+  }
+}
+
+template <int NT, bool DROP>
+__global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(
+    const float* __restrict__ qkv, const uint8_t* __restrict__ key_pad,
+    const float* __restrict__ out, const float* __restrict__ dout, const float* __restrict__ lse,
+    float* __restrict__ dqkv, int B, int L, int d, int H, float scale, float pdrop,
+    const int64_t* __restrict__ key, int site) {
+  constexpr int LP = NT * 16;
+  constexpr int TP = 20;  // transpose buffer [LP keys][16 queries of the current tile], pitch 20
+  __shared__ __attribute__((aligned(16))) float Qsm[4][LP][16];
+  __shared__ __attribute__((aligned(16))) float Ksm[4][LP][16];
+  __shared__ __attribute__((aligned(16))) float Gsm[4][LP][16];
+  __shared__ __attribute__((aligned(16))) float Tsm[4][LP * TP];  // 5 KB per wave
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int bh = blockIdx.x * 4 + wave;
+  if (bh >= B * H) return;
+  const int b = bh / H, h = bh % H;
+  const int ld = 3 * d;
+  const float* base = qkv + (int64_t)b * L * ld + h * 16;
+  const float* gbase = dout + (int64_t)b * L * d + h * 16;
+  const float* obase = out + (int64_t)b * L * d + h * 16;
+  float(*Qs)[16] = Qsm[wave];
+  float(*Ks)[16] = Ksm[wave];
+  float(*Gs)[16] = Gsm[wave];
+  float* T = Tsm[wave];
+  f4 qf[NT], kf[NT], vf[NT], gf[NT];
+  float Di[NT], lsei[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int row = t * 16 + r;
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    const bool ok = row < L;
+    qf[t] = ok ? ld4(base + (int64_t)row * ld + 4 * q) : z;
+    kf[t] = ok ? ld4(base + (int64_t)row * ld + d + 4 * q) : z;
+    vf[t] = ok ? ld4(base + (int64_t)row * ld + 2 * d + 4 * q) : z;
+    gf[t] = ok ? ld4(gbase + (int64_t)row * d + 4 * q) : z;
+    const f4 of = ok ? ld4(obase + (int64_t)row * d + 4 * q) : z;
+    *reinterpret_cast<f4*>(&Qs[row][4 * q]) = qf[t];
+    *reinterpret_cast<f4*>(&Ks[row][4 * q]) = kf[t];
+    *reinterpret_cast<f4*>(&Gs[row][4 * q]) = gf[t];
+    // D_i = sum_c dO[i][c] O[i][c] (query i = row, this lane's 4 columns, then across q)
+    Di[t] = xsum(gf[t][0] * of[0] + gf[t][1] * of[1] + gf[t][2] * of[2] + gf[t][3] * of[3]);
+    lsei[t] = ok ? lse[(int64_t)bh * L + row] * kLog2e : 0.f;  // base-2 log-sum-exp
+  }
+  bool kok[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = t * 16 + 4 * q + e;
+      kok[t][e] = j < L && key_pad[(int64_t)b * L + j] == 0;
+    }
+  DropKey dk;
+  if (DROP) dk = make_key(key, site, pdrop);
+  const float scale2 = scale * kLog2e;
+  __builtin_amdgcn_wave_barrier();
+  float* dbase = dqkv + (int64_t)b * L * ld + h * 16;
+  // per query tile: P^T, dS^T (keys x queries), dQ; P∘Z and dS go to T for dV / dK
+  f4 dv_acc[NT], dk_acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) dv_acc[t] = dk_acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int tq = 0; tq < NT; ++tq) {
+    const int i = tq * 16 + r;
+    f4 ps[NT], ds[NT];
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) {
+      f4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        sacc = mfma4(kf[tk][s4], qf[tq][s4], sacc);   // S^T[key][query]
+        pacc = mfma4(vf[tk][s4], gf[tq][s4], pacc);   // dP^T[key][query] = V dO^T
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = (kok[tk][e] && i < L) ? exp2f(sacc[e] * scale2 - lsei[tq]) : 0.f;
+        const float z = DROP ? keep_mult(dk, ((uint64_t)bh * L + i) * L + tk * 16 + 4 * q + e) : 1.f;
+        ds[tk][e] = pv * (z * pacc[e] - Di[tq]);
+        ps[tk][e] = pv * z;
+      }
+    }
+    // dQ[i][c] = scale * sum_j dS[i][j] K[j][c]
+    f4 dq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) dq = mfma4(ds[tk][s4], Ks[tk * 16 + 4 * q + s4][r], dq);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = tq * 16 + 4 * q + e;
+      if (row < L) dbase[(int64_t)row * ld + r] = dq[e] * scale;
+    }
+    // dV[j][c] += sum_i PZ[i][j] dO[i][c]: A must be indexed (key = lane & 15, k = query):
+    // transpose this query tile's PZ^T through T (T[key][query])
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) T[(tk * 16 + 4 * q + e) * TP + r] = ps[tk][e];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) {
+      const f4 a = ld4(&T[(tk * 16 + r) * TP + 4 * q]);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) dv_acc[tk] = mfma4(a[s4], Gs[tq * 16 + 4 * q + s4][r], dv_acc[tk]);
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) T[(tk * 16 + 4 * q + e) * TP + r] = ds[tk][e];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) {
+      const f4 a = ld4(&T[(tk * 16 + r) * TP + 4 * q]);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) dk_acc[tk] = mfma4(a[s4], Qs[tq * 16 + 4 * q + s4][r], dk_acc[tk]);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // dK / dV rows: acc[e] = X[key 16 tk + 4 q + e][c = r]
+#pragma unroll
+  for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = tk * 16 + 4 * q + e;
+      if (row < L) {
+        dbase[(int64_t)row * ld + d + r] = dk_acc[tk][e] * scale;
+        dbase[(int64_t)row * ld + 2 * d + r] = dv_acc[tk][e];
+      }
+    }
+}
+
 int threads_for(int L) {
   int t = ((L + 63) / 64) * 64;
   return t > 256 ? 256 : t;
@@ -222,9 +469,22 @@ extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out,
   const size_t lds = (size_t)(2 * L * hd + L) * sizeof(float);
   RS_CHECK_ARG(lds <= 64 * 1024, "rs_attn_fwd: L=%d hd=%d exceeds LDS", L, hd);
   RS_CHECK_ARG(d % 4 == 0 && aligned16(qkv) && aligned16(out), "rs_attn_fwd: needs 16-byte aligned rows");
+  hipStream_t st = as_stream(stream);
+  if (hd == 16 && L <= 64 && !getenv_flag("RSYS_ATTN_VALU")) {
+    const int nt = (L + 15) / 16;
+    const dim3 g4(cdiv((int64_t)B * H, 4));
+#define RS_AF(NTV)                                                                                  \
+  if (nt == NTV) {                                                                                  \
+    if (p > 0.f) attn_fwd_mfma_kernel<NTV, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    else attn_fwd_mfma_kernel<NTV, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+  }
+    RS_AF(1) RS_AF(2) RS_AF(3) RS_AF(4)
+#undef RS_AF
+    RS_CHECK_LAUNCH("rs_attn_fwd mfma");
+    return 0;
+  }
   dim3 grid(bh_grid(B, H));
   int thr = threads_for(L);
-  hipStream_t st = as_stream(stream);
   RS_ATTN_DISPATCH(hd, p > 0.f, attn_fwd_kernel, qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site);
   RS_CHECK_LAUNCH("rs_attn_fwd");
   return 0;
@@ -243,9 +503,23 @@ extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float
   const size_t lds = (size_t)(4 * L * hd + 3 * L) * sizeof(float);
   RS_CHECK_ARG(lds <= 64 * 1024, "rs_attn_bwd: L=%d hd=%d exceeds LDS", L, hd);
   RS_CHECK_ARG(d % 4 == 0 && aligned16(qkv) && aligned16(dout), "rs_attn_bwd: needs 16-byte aligned rows");
+  hipStream_t st = as_stream(stream);
+  if (hd == 16 && L <= 64 && !getenv_flag("RSYS_ATTN_VALU")) {
+    RS_CHECK_ARG(aligned16(out), "rs_attn_bwd: needs 16-byte aligned rows");
+    const int nt = (L + 15) / 16;
+    const dim3 g4(cdiv((int64_t)B * H, 4));
+#define RS_AB(NTV)                                                                                  \
+  if (nt == NTV) {                                                                                  \
+    if (p > 0.f) attn_bwd_mfma_kernel<NTV, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    else attn_bwd_mfma_kernel<NTV, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+  }
+    RS_AB(1) RS_AB(2) RS_AB(3) RS_AB(4)
+#undef RS_AB
+    RS_CHECK_LAUNCH("rs_attn_bwd mfma");
+    return 0;
+  }
   dim3 grid(bh_grid(B, H));
   int thr = threads_for(L);
-  hipStream_t st = as_stream(stream);
   RS_ATTN_DISPATCH(hd, p > 0.f, attn_bwd_kernel, qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale,
                    p, key, site);
   RS_CHECK_LAUNCH("rs_attn_bwd");

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "../../include/rsys_hip.h"
 
@@ -58,6 +59,12 @@ int partials_reduce(const float* ws, int P, int N, float scale, float beta, floa
                     hipStream_t st);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+// debug / A-B switches read at launch time (host only): set and not "0"
+inline bool getenv_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] && !(v[0] == '0' && v[1] == 0);
+}
+
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 

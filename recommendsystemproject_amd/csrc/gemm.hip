@@ -280,7 +280,7 @@ extern "C" int rs_gemm_auto_split(int M, int N, int K) {
   if (tiles >= 256 || K < 1024) return 1;
   if (K >= 2048 && (int64_t)M * N <= 16384) return 2;  // wgrad path: needs a workspace only
   int s = (int)((512 + tiles - 1) / tiles);
-  int maxs = K / (BK * 16);  // each split keeps >= 16 k-tiles
+  int maxs = K / (BK * 4);  // each split keeps >= 4 k-tiles
   if (s > maxs) s = maxs;
   if (s > 256) s = 256;
   return s < 1 ? 1 : s;
@@ -333,7 +333,7 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
   g.vecB = (ldb % 4 == 0) && aligned16(B);
   hipStream_t st = as_stream(stream);
   {
-    StreamArgs sa;
+    StreamArgs sa{};
     sa.M = M; sa.N = N; sa.K = K; sa.alpha = alpha; sa.beta = beta; sa.A = A; sa.lda = lda;
     sa.B = B; sa.ldb = ldb; sa.C = C; sa.ldc = ldc; sa.epi = epilogue; sa.bias = bias;
     sa.aux = aux; sa.ld_aux = ld_aux; sa.aux_mod = g.aux_mod; sa.rowsum = rowsum; sa.ws = ws;
@@ -343,8 +343,9 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
     if (ws && wgrad_supported(transA, transB, M, N, K, A, lda, B, ldb, ldc, epilogue))
       return wgrad_launch(sa, st);
   }
-  const bool bigM = M >= 2048;
-  const bool wideN = N > 64;
+  // 128-wide tiles only when they still give >= 256 workgroups
+  const bool bigM = M >= 2048 && (int64_t)cdiv(M, 128) * cdiv(N, N > 64 ? 128 : 64) * g.split_k >= 256;
+  const bool wideN = N > 64 && (int64_t)cdiv(M, bigM ? 128 : 64) * cdiv(N, 128) * g.split_k >= 256;
   if (bigM && wideN) launch_tile<128, 128>(g, transA, transB, st);
   else if (bigM) launch_tile<128, 64>(g, transA, transB, st);
   else if (wideN) launch_tile<64, 128>(g, transA, transB, st);
@@ -359,4 +360,34 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
     RS_CHECK_LAUNCH("rs_gemm_f32 splitk");
   }
   return 0;
+}
+
+// h = dropout(A W^T + bias) + resid; y = LayerNorm(h) (TransformerEncoderLayer's
+// norm(x + dropout(sublayer(x))) with the sublayer's last Linear). One streaming kernel for the
+// encoder shape (N = d_model = 64); otherwise the GEMM followed by rs_add_layernorm_fwd.
+extern "C" int rs_gemm_add_layernorm(int M, int N, int K, const float* A, int lda, const float* W,
+                                     int ldw, const float* bias, const float* resid, float* h,
+                                     float* y, const float* gamma, const float* beta, float* mean,
+                                     float* rstd, float eps, float p, const int64_t* key, int site,
+                                     void* stream) {
+  RS_CHECK_ARG(M >= 0 && N >= 1 && K >= 1, "rs_gemm_add_layernorm: bad shape");
+  RS_CHECK_ARG(A && W && resid && h && y && gamma && beta && mean && rstd,
+               "rs_gemm_add_layernorm: null pointer");
+  RS_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || key), "rs_gemm_add_layernorm: bad dropout p");
+  if (M == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  if (rowgemm_ln_supported(M, N, K, A, lda) && !getenv_flag("RSYS_UNFUSED_LN")) {
+    StreamArgs sa{};
+    sa.M = M; sa.N = N; sa.K = K; sa.alpha = 1.f; sa.beta = 0.f; sa.A = A; sa.lda = lda;
+    sa.B = W; sa.ldb = ldw; sa.transB = 1; sa.C = h; sa.ldc = N;
+    sa.epi = RS_EPI_AUX_ADD | (bias ? RS_EPI_BIAS : 0) | (p > 0.f ? RS_EPI_DROP_A : 0);
+    sa.bias = bias; sa.aux = resid; sa.ld_aux = N; sa.aux_mod = M;
+    sa.drop_p = p; sa.drop_key = key; sa.site_a = site;
+    sa.ln_gamma = gamma; sa.ln_beta = beta; sa.ln_y = y; sa.ln_mean = mean; sa.ln_rstd = rstd;
+    sa.ln_eps = eps;
+    return rowgemm_ln_launch(sa, st);
+  }
+  RS_RET_IF(rs_gemm_f32(0, 1, M, N, K, 1.f, A, lda, W, ldw, 0.f, h, N, bias ? RS_EPI_BIAS : 0, bias,
+                        nullptr, 0, 0, 0.f, nullptr, 0, 0, nullptr, 1, nullptr, stream));
+  return rs_add_layernorm_fwd(h, resid, gamma, beta, y, mean, rstd, M, N, eps, p, key, site, stream);
 }

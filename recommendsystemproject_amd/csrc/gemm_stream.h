@@ -21,10 +21,20 @@ struct StreamArgs {
   float drop_p;
   const int64_t* drop_key;
   int site_a, site_b;
+  // fused residual + LayerNorm epilogue (rowgemm LN instances, N == 64):
+  //   h = drop_a(alpha*acc + bias) + aux  -> C;   y = LN(h) * gamma + beta -> ln_y
+  const float* ln_gamma;
+  const float* ln_beta;
+  float* ln_y;
+  float* ln_mean;
+  float* ln_rstd;
+  float ln_eps;
 };
 
 bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda);
 int rowgemm_launch(const StreamArgs& s, hipStream_t st);
+bool rowgemm_ln_supported(int M, int N, int K, const float* A, int lda);
+int rowgemm_ln_launch(const StreamArgs& s, hipStream_t st);
 bool wgrad_supported(int transA, int transB, int M, int N, int K, const float* A, int lda,
                      const float* B, int ldb, int ldc, int epi);
 int64_t wgrad_ws_bytes(int M, int N, int K);

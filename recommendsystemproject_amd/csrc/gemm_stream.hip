@@ -73,8 +73,70 @@ __device__ __forceinline__ floatx4 epi_apply4(const StreamArgs& a, int m, int n0
   return v;
 }
 
+// residual + LayerNorm over a full row of N = NT*16 columns. Lane (r, q) holds, for row m, the
+// columns t*16 + 4q + e (t < NT, e < 4); the row's other columns are in the lanes q' != q with
+// the same r: two xor shuffles (16, 32) complete the row sums. Same operation order per element
+// as the unfused pair (GEMM epilogue: alpha*acc + bias; add_ln: drop(.) + resid, mean, centred
+// variance, 1/sqrtf).
+template <int NT>
+__device__ __forceinline__ void ln_epilogue(const StreamArgs& a, int m, int q, const floatx4* acc,
+                                            const DropKey& ka) {
+  constexpr int N = NT * 16;
+  float hv[NT][4];
+  float s = 0.f;
+  const bool ok = m < a.M;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int n0 = t * 16 + 4 * q;
+    floatx4 v = acc[t] * a.alpha;
+    if (a.epi & RS_EPI_BIAS) v += *reinterpret_cast<const floatx4*>(a.bias + n0);
+    floatx4 res = {0.f, 0.f, 0.f, 0.f};
+    if (ok) res = *reinterpret_cast<const floatx4*>(a.aux + (int64_t)m * a.ld_aux + n0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = v[e];
+      if (a.epi & RS_EPI_DROP_A) x *= keep_mult(ka, (uint64_t)m * N + n0 + e);
+      hv[t][e] = x + res[e];
+      s += hv[t][e];
+    }
+  }
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  const float mu = s / (float)N;
+  float vs = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = hv[t][e] - mu;
+      vs += d * d;
+    }
+  vs += __shfl_xor(vs, 16, 64);
+  vs += __shfl_xor(vs, 32, 64);
+  const float rs = 1.f / sqrtf(vs / (float)N + a.ln_eps);
+  if (!ok) return;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int n0 = t * 16 + 4 * q;
+    const floatx4 gm = *reinterpret_cast<const floatx4*>(a.ln_gamma + n0);
+    const floatx4 bt = *reinterpret_cast<const floatx4*>(a.ln_beta + n0);
+    floatx4 h4, y4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      h4[e] = hv[t][e];
+      y4[e] = (hv[t][e] - mu) * rs * gm[e] + bt[e];
+    }
+    *reinterpret_cast<floatx4*>(a.C + (int64_t)m * a.ldc + n0) = h4;
+    *reinterpret_cast<floatx4*>(a.ln_y + (int64_t)m * N + n0) = y4;
+  }
+  if (q == 0) {
+    a.ln_mean[m] = mu;
+    a.ln_rstd[m] = rs;
+  }
+}
+
 // ---------------------------------------------------------------------------------- rowgemm
-template <int NT, int KT>
+template <int NT, int KT, bool LN = false>
 __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
   constexpr int KP = KT * 16 + 4;  // LDS pitch (floats): conflict-free ds_read_b128 per 16 lanes
   constexpr bool PREFETCH = KT <= 8;
@@ -115,6 +177,7 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
     }
   };
   if (g < groups) load_group(g, areg);
+  floatx4 lnacc[LN ? NT : 1];
   for (; g < groups; g += stride) {
     floatx4 anext[PREFETCH ? KT : 1];
     if (PREFETCH && g + stride < groups) load_group(g + stride, anext);
@@ -141,6 +204,11 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
       }
       // C/D map of 16x16: col = lane&15 -> row m of A, row = 4*(lane>>4) + i -> column n of C
       const int m = g * 16 + r;
+      if constexpr (LN) {
+        lnacc[j0] = acc0;
+        if (two) lnacc[j0 + 1] = acc1;
+        continue;
+      }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         if (h == 1 && !two) break;
@@ -157,6 +225,7 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
         }
       }
     }
+    if constexpr (LN) ln_epilogue<NT>(a, g * 16 + r, q, lnacc, ka);
     __builtin_amdgcn_sched_barrier(0);
     if (PREFETCH) {
 #pragma unroll
@@ -315,7 +384,7 @@ __global__ __launch_bounds__(1024) void wgrad_reduce_kernel(StreamArgs a, int P)
 }
 
 int wgrad_blocks(int Kr) {
-  int nb = Kr / 256;
+  int nb = Kr / 64;  // >= 64 rows per workgroup; short K (the MLP's B = 4096) still fills 64 CUs
   if (nb > 512) nb = 512;
   if (nb < 1) nb = 1;
   return nb;
@@ -368,13 +437,36 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   return 0;
 }
 
+bool rowgemm_ln_supported(int M, int N, int K, const float* A, int lda) {
+  if (N != 64 || M < kSmallM || K % 4 != 0 || lda % 4 != 0 || !aligned16(A)) return false;
+  const int kt = (K + 15) / 16;
+  return kt == 4 || kt == 16;
+}
+
+int rowgemm_ln_launch(const StreamArgs& s, hipStream_t st) {
+  const int kt = (s.K + 15) / 16;
+  RS_CHECK_ARG(s.ldc % 4 == 0 && s.ld_aux % 4 == 0 && aligned16(s.C) && aligned16(s.aux) &&
+                   aligned16(s.ln_y) && aligned16(s.ln_gamma) && aligned16(s.ln_beta) &&
+                   (!(s.epi & RS_EPI_BIAS) || aligned16(s.bias)),
+               "rowgemm_ln: operands must be 16-byte aligned");
+  const size_t lds = (size_t)4 * 16 * (kt * 16 + 4) * sizeof(float);
+  const int groups = (s.M + 15) / 16;
+  int bx = cdiv(groups, 16);
+  const int per_cu = lds > 80 * 1024 ? 1 : (lds > 53 * 1024 ? 2 : (lds > 40 * 1024 ? 3 : 4));
+  if (bx > 256 * per_cu) bx = 256 * per_cu;
+  if (kt == 4) rowgemm_kernel<4, 4, true><<<bx, 512, lds, st>>>(s);
+  else rowgemm_kernel<4, 16, true><<<bx, 512, lds, st>>>(s);
+  RS_CHECK_LAUNCH("rowgemm_ln");
+  return 0;
+}
+
 bool wgrad_supported(int transA, int transB, int M, int N, int K, const float* A, int lda,
                      const float* B, int ldb, int ldc, int epi) {
   if (!transA || transB || epi != 0 || K < 2048) return false;
   const int mo_pad = (M + 31) / 32 * 32, no_pad = (N + 31) / 32 * 32;
   switch (mo_pad * 1000 + no_pad) {
     case 64064: case 64256: case 256064: case 192064: case 64192: case 128128: case 128064:
-    case 64128: case 32064: case 64032: break;
+    case 64128: case 32064: case 64032: case 128256: case 256128: break;
     default: return false;
   }
   if (M % 4 != 0 || N % 4 != 0 || lda % 4 != 0 || ldb % 4 != 0 || !aligned16(A) || !aligned16(B))
@@ -399,7 +491,7 @@ int wgrad_launch(const StreamArgs& s, hipStream_t st) {
     break;
   switch (mo_pad * 1000 + no_pad) {
     RS_WG(64, 64) RS_WG(64, 256) RS_WG(256, 64) RS_WG(192, 64) RS_WG(64, 192) RS_WG(128, 128)
-    RS_WG(128, 64) RS_WG(64, 128) RS_WG(32, 64) RS_WG(64, 32)
+    RS_WG(128, 64) RS_WG(64, 128) RS_WG(32, 64) RS_WG(64, 32) RS_WG(128, 256) RS_WG(256, 128)
     default: set_error("wgrad: no instance for %dx%d", s.M, s.N); return -1;
   }
 #undef RS_WG

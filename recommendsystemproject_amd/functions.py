@@ -130,14 +130,15 @@ def layer_fwd(lyr, x, key_pad, B, L, d, H, p, key, site):
     sa_mod = lyr.self_attn
     qkv = ops.linear_fwd(x, sa_mod.in_proj_weight, sa_mod.in_proj_bias)
     att, lse = ops.attn_fwd(qkv, key_pad, B, L, d, H, p, key, site)
-    h1 = ops.linear_fwd(att, sa_mod.out_proj.weight, sa_mod.out_proj.bias)
-    x1, m1, r1 = ops.add_layernorm_fwd(h1, x, lyr.norm1.weight, lyr.norm1.bias, lyr.norm1.eps,
-                                       p, key, site + 1)  # h1 <- x + dropout1(sa)
+    # h1 = x + dropout1(out_proj(att)), x1 = norm1(h1): GEMM + residual + LayerNorm in one kernel
+    h1, x1, m1, r1 = ops.linear_add_layernorm(att, sa_mod.out_proj.weight, sa_mod.out_proj.bias, x,
+                                              lyr.norm1.weight, lyr.norm1.bias, lyr.norm1.eps, p, key,
+                                              site + 1)
     f1 = ops.linear_fwd(x1, lyr.linear1.weight, lyr.linear1.bias, relu=True, drop_p=p, drop_key=key,
                         site_a=site + 2)  # dropout(relu(.)) fused
-    h2 = ops.linear_fwd(f1, lyr.linear2.weight, lyr.linear2.bias)
-    x2, m2, r2 = ops.add_layernorm_fwd(h2, x1, lyr.norm2.weight, lyr.norm2.bias, lyr.norm2.eps,
-                                       p, key, site + 3)  # h2 <- x1 + dropout2(ff)
+    h2, x2, m2, r2 = ops.linear_add_layernorm(f1, lyr.linear2.weight, lyr.linear2.bias, x1,
+                                              lyr.norm2.weight, lyr.norm2.bias, lyr.norm2.eps, p, key,
+                                              site + 3)  # h2 = x1 + dropout2(ff), x2 = norm2(h2)
     return x2, (x, qkv, att, lse, h1, x1, m1, r1, f1, h2, m2, r2)
 
 

@@ -128,6 +128,23 @@ def attn_bwd(qkv, key_pad, out, dout, lse, B, L, d, H, p=0.0, key=None, site=0):
     return dqkv
 
 
+def linear_add_layernorm(x, W, bias, resid, gamma, beta, eps=1e-5, p=0.0, key=None, site=0):
+    """h = dropout(x W^T + bias) + resid, y = LayerNorm(h): one fused kernel at the encoder
+    width. Returns h (kept for the backward), y, mean, rstd."""
+    M, K = x.shape
+    N = W.shape[0]
+    if tuple(resid.shape) != (M, N) or not resid.is_contiguous():
+        raise RuntimeError('linear_add_layernorm: resid must be a contiguous [M, N] tensor')
+    dev = x.device
+    h = torch.empty(M, N, device=dev, dtype=torch.float32)
+    y = torch.empty(M, N, device=dev, dtype=torch.float32)
+    mean = torch.empty(M, device=dev, dtype=torch.float32)
+    rstd = torch.empty(M, device=dev, dtype=torch.float32)
+    call('rs_gemm_add_layernorm', M, N, K, P(x), x.stride(0), P(W), W.stride(0), P(bias), P(resid),
+         P(h), P(y), P(gamma), P(beta), P(mean), P(rstd), float(eps), float(p), P(key), site, stream())
+    return h, y, mean, rstd
+
+
 def add_layernorm_fwd(a, b, gamma, beta, eps=1e-5, p=0.0, key=None, site=0):
     """h = dropout(a) + b (into a); returns y, mean, rstd."""
     M, N = a.shape

@@ -175,7 +175,10 @@ def ref_attention(qkv, key_pad, B, L, d, H):
     return (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * L, d)
 
 
-@pytest.mark.parametrize('B,L,d,H', [(3, 50, 64, 4), (2, 7, 64, 2), (5, 200, 64, 4), (4, 20, 32, 4)])
+# head_dim 16 with L <= 64 takes the MFMA kernels (NT = ceil(L/16) tiles); the rest the VALU ones
+@pytest.mark.parametrize('B,L,d,H', [(3, 50, 64, 4), (2, 7, 64, 2), (5, 200, 64, 4), (4, 20, 32, 4),
+                                     (6, 33, 64, 4), (5, 16, 64, 4), (3, 64, 64, 4), (5, 16, 48, 3),
+                                     (3, 50, 32, 2), (2, 1, 64, 4)])
 def test_attention_fwd_bwd(B, L, d, H):
     qkv = rnd(B * L, 3 * d, seed=1).requires_grad_(True)
     lens = torch.randint(0, L + 1, (B,))
@@ -209,6 +212,26 @@ def test_attention_dropout_consistent():
     fd = ((fp - fm) * dout).sum().item() / (2 * eps)
     an = (dq * direc).sum().item()
     assert abs(fd - an) < 2e-2 * max(1.0, abs(an)), (fd, an)
+
+
+@pytest.mark.parametrize('L', [30, 50])
+def test_attention_mfma_matches_valu_kernel(L, monkeypatch):
+    """The MFMA and VALU attention kernels draw the same dropout masks and agree numerically."""
+    B, d, H, p = 5, 64, 4, 0.2
+    qkv = rnd(B * L, 3 * d, seed=8)
+    lens = torch.tensor([L, 1, L // 2, 3, L - 1])
+    seq = (torch.arange(L)[None, :] < lens[:, None]).long().to(DEV)
+    key_pad, _ = ops.seq_mask(seq, 0)
+    key = torch.tensor([99, 5], dtype=torch.int64, device=DEV)
+    dout = rnd(B * L, d, seed=9)
+    res = []
+    for valu in ('0', '1'):
+        monkeypatch.setenv('RSYS_ATTN_VALU', valu)
+        out, lse = ops.attn_fwd(qkv, key_pad, B, L, d, H, p, key, 4)
+        dq = ops.attn_bwd(qkv, key_pad, out, dout, lse, B, L, d, H, p, key, 4)
+        res.append((out, lse, dq))
+    for a, b in zip(*res):
+        assert torch.allclose(a, b, atol=2e-5, rtol=1e-4)
 
 
 def test_layernorm_fwd_bwd():
@@ -274,6 +297,29 @@ def test_l2norm():
     yr.backward(dy)
     dx = ops.l2norm_bwd(y, norm, dy)
     assert torch.allclose(dx, x.grad, atol=1e-4)
+
+
+@pytest.mark.parametrize('K', [64, 256, 40])
+@pytest.mark.parametrize('p', [0.0, 0.1])
+def test_linear_add_layernorm_fused(K, p, monkeypatch):
+    """rs_gemm_add_layernorm: the fused streaming kernel (M >= 32768, N = 64, K in {64, 256})
+    equals the GEMM + rs_add_layernorm_fwd pair it replaces, and torch at p = 0."""
+    M, N = 40000, 64
+    x, W, b = rnd(M, K, seed=1), rnd(N, K, seed=2) * 0.2, rnd(N, seed=3)
+    res, g, be = rnd(M, N, seed=4), 1 + 0.1 * rnd(N, seed=5), 0.1 * rnd(N, seed=6)
+    key = torch.tensor([17, 4], dtype=torch.int64, device=DEV)
+    outs = []
+    for unfused in ('0', '1'):
+        monkeypatch.setenv('RSYS_UNFUSED_LN', unfused)
+        outs.append(ops.linear_add_layernorm(x, W, b, res, g, be, 1e-5, p, key, 9))
+    (h, y, mu, rs), (h2, y2, mu2, rs2) = outs
+    assert torch.equal(h, h2)
+    assert torch.allclose(y, y2, atol=1e-5) and torch.allclose(mu, mu2, atol=1e-6)
+    assert torch.allclose(rs, rs2, rtol=1e-5)
+    if p == 0.0:
+        href = x @ W.t() + b + res
+        assert torch.allclose(h, href, atol=1e-4)
+        assert torch.allclose(y, F.layer_norm(href, (N,), g, be, 1e-5), atol=1e-4)
 
 
 @pytest.mark.parametrize('M', [300, 5000])
