@@ -46,11 +46,19 @@ __device__ __forceinline__ float epi_apply(const StreamArgs& a, int m, int n, fl
 }
 
 // four consecutive columns n0..n0+3 of row m (same order of operations as epi_apply)
+// aux row element of (m, n0..n0+3) for AUX_MASK (row m) / AUX_ADD (row m % aux_mod)
+__device__ __forceinline__ const float* aux_ptr(const StreamArgs& a, int m, int n0) {
+  const int row = (a.epi & RS_EPI_AUX_ADD) ? m % a.aux_mod : m;
+  return a.aux + (int64_t)row * a.ld_aux + n0;
+}
+
+// auxv: the prefetched aux values of (m, n0..n0+3) when the epilogue has AUX_MASK / AUX_ADD
 __device__ __forceinline__ floatx4 epi_apply4(const StreamArgs& a, int m, int n0, floatx4 v,
-                                              const DropKey& ka, const DropKey& kb) {
+                                              const DropKey& ka, const DropKey& kb,
+                                              const floatx4& auxv) {
   if (a.epi & RS_EPI_BIAS) v += *reinterpret_cast<const floatx4*>(a.bias + n0);
   if (a.epi & RS_EPI_AUX_MASK) {
-    const floatx4 mk = *reinterpret_cast<const floatx4*>(a.aux + (int64_t)m * a.ld_aux + n0);
+    const floatx4 mk = auxv;
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = mk[i] > 0.f ? v[i] : 0.f;
   }
@@ -63,8 +71,7 @@ __device__ __forceinline__ floatx4 epi_apply4(const StreamArgs& a, int m, int n0
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] *= keep_mult(ka, e0 + i);
   }
-  if (a.epi & RS_EPI_AUX_ADD)
-    v += *reinterpret_cast<const floatx4*>(a.aux + (int64_t)(m % a.aux_mod) * a.ld_aux + n0);
+  if (a.epi & RS_EPI_AUX_ADD) v += auxv;
   if (a.epi & RS_EPI_DROP_B) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] *= keep_mult(kb, e0 + i);
@@ -80,7 +87,7 @@ __device__ __forceinline__ floatx4 epi_apply4(const StreamArgs& a, int m, int n0
 // variance, 1/sqrtf).
 template <int NT>
 __device__ __forceinline__ void ln_epilogue(const StreamArgs& a, int m, int q, const floatx4* acc,
-                                            const DropKey& ka) {
+                                            const floatx4* resv, const DropKey& ka) {
   constexpr int N = NT * 16;
   float hv[NT][4];
   float s = 0.f;
@@ -90,8 +97,7 @@ __device__ __forceinline__ void ln_epilogue(const StreamArgs& a, int m, int q, c
     const int n0 = t * 16 + 4 * q;
     floatx4 v = acc[t] * a.alpha;
     if (a.epi & RS_EPI_BIAS) v += *reinterpret_cast<const floatx4*>(a.bias + n0);
-    floatx4 res = {0.f, 0.f, 0.f, 0.f};
-    if (ok) res = *reinterpret_cast<const floatx4*>(a.aux + (int64_t)m * a.ld_aux + n0);
+    const floatx4 res = resv[t];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float x = v[e];
@@ -178,9 +184,32 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
   };
   if (g < groups) load_group(g, areg);
   floatx4 lnacc[LN ? NT : 1];
+  // aux prefetch costs 16 VGPRs: skipped for the widest instances (they would spill)
+  constexpr bool AUXPF = !(NT >= 12 && KT >= 8);
+  const bool has_aux = (a.epi & (RS_EPI_AUX_ADD | RS_EPI_AUX_MASK)) && a.vec_epi;
   for (; g < groups; g += stride) {
     floatx4 anext[PREFETCH ? KT : 1];
     if (PREFETCH && g + stride < groups) load_group(g + stride, anext);
+    const int m = g * 16 + r;
+    // epilogue operands read ahead of the MFMAs so their latency hides under them:
+    // LN: the residual row slice; otherwise one pair of tiles ahead
+    floatx4 lnres[LN ? NT : 1];
+    floatx4 auxc[2], auxn[2];
+    const floatx4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    auto load_aux = [&](int j, floatx4& dst) {
+      const int n0 = nb0 + j * 16 + 4 * q;
+      dst = (j < NT && m < a.M && n0 + 3 < a.N) ? *reinterpret_cast<const floatx4*>(aux_ptr(a, m, n0))
+                                                  : zero4;
+    };
+    if constexpr (LN) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        lnres[t] = m < a.M ? *reinterpret_cast<const floatx4*>(a.aux + (int64_t)m * a.ld_aux + t * 16 + 4 * q)
+                           : zero4;
+    } else if (AUXPF && has_aux) {
+      load_aux(0, auxc[0]);
+      load_aux(1, auxc[1]);
+    }
     // N tiles in pairs: two independent accumulator chains hide the 40-cycle dependent MFMA
     // latency; each pair is stored right away so only 8 accumulators are ever live
 #pragma unroll
@@ -188,6 +217,10 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
       // keep the scheduler from hoisting every pair's B reads / accumulators (register spills)
       __builtin_amdgcn_sched_barrier(0);
       const bool two = j0 + 1 < NT;
+      if (!LN && AUXPF && has_aux && j0 + 2 < NT) {
+        load_aux(j0 + 2, auxn[0]);
+        load_aux(j0 + 3, auxn[1]);
+      }
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
@@ -203,7 +236,6 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
         }
       }
       // C/D map of 16x16: col = lane&15 -> row m of A, row = 4*(lane>>4) + i -> column n of C
-      const int m = g * 16 + r;
       if constexpr (LN) {
         lnacc[j0] = acc0;
         if (two) lnacc[j0 + 1] = acc1;
@@ -217,15 +249,18 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
         const floatx4 acc = (h ? acc1 : acc0) * a.alpha;
         float* crow = a.C + (int64_t)m * a.ldc;
         if (a.vec_epi && n0 + 3 < a.N) {
-          *reinterpret_cast<floatx4*>(crow + n0) = epi_apply4(a, m, n0, acc, ka, kb);
+          if (!AUXPF && has_aux) load_aux(j0 + h, auxc[h]);
+          *reinterpret_cast<floatx4*>(crow + n0) = epi_apply4(a, m, n0, acc, ka, kb, auxc[h]);
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             if (n0 + i < a.N) crow[n0 + i] = epi_apply(a, m, n0 + i, acc[i], ka, kb);
         }
       }
+      auxc[0] = auxn[0];
+      auxc[1] = auxn[1];
     }
-    if constexpr (LN) ln_epilogue<NT>(a, g * 16 + r, q, lnacc, ka);
+    if constexpr (LN) ln_epilogue<NT>(a, m, q, lnacc, lnres, ka);
     __builtin_amdgcn_sched_barrier(0);
     if (PREFETCH) {
 #pragma unroll

@@ -313,7 +313,8 @@ def test_linear_add_layernorm_fused(K, p, monkeypatch):
         monkeypatch.setenv('RSYS_UNFUSED_LN', unfused)
         outs.append(ops.linear_add_layernorm(x, W, b, res, g, be, 1e-5, p, key, 9))
     (h, y, mu, rs), (h2, y2, mu2, rs2) = outs
-    assert torch.equal(h, h2)
+    # same products and masks; fma contraction of drop(.) + resid may differ by an ulp
+    assert torch.allclose(h, h2, rtol=1e-6, atol=1e-6)
     assert torch.allclose(y, y2, atol=1e-5) and torch.allclose(mu, mu2, atol=1e-6)
     assert torch.allclose(rs, rs2, rtol=1e-5)
     if p == 0.0:
