@@ -47,6 +47,7 @@ def parse():
     ap.add_argument('--batch', type=int, default=None, help='per-GPU batch (default: config)')
     ap.add_argument('--dropout', default='config', choices=['config', '0'])
     ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--zipf', type=float, default=None, help='Zipf(alpha) ids instead of uniform (C3 variant)')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     return ap.parse_args()
@@ -70,9 +71,18 @@ def cpu_baseline(cfg, seconds):
         el = time.perf_counter() - t0
         if el >= seconds or n >= 200:
             break
+    model = None
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                model = line.split(':', 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {'value': round(n * B / el, 1), 'unit': 'samples/s', 'cores': torch.get_num_threads(),
             'kind': 'port', 'sample': f'{n} steps x batch {B} of the same config (oracle, fp32, '
-                                      f'dropout as configured), {el:.1f} s'}
+                                      f'dropout as configured), {el:.1f} s',
+            'nproc': os.cpu_count(), 'cpu_model': model}
 
 
 def main():
@@ -89,6 +99,8 @@ def main():
         for t in cfg['two_tower'].values():
             t['dropout'] = 0.0
             t.get('transformer_parameters', {})['dropout'] = 0.0
+    if args.zipf:
+        cfg.setdefault('synthetic', {})['zipf'] = args.zipf
     B = args.batch or int(cfg['train']['batch_size'])
     T = float(cfg['train']['temperature'])
     maps = {'user': synth.tower_layout(cfg['two_tower']['user_tower']),
@@ -195,6 +207,13 @@ def main():
     roof['kernel'] = dom_name
     roof['avg_launch_ms'] = round(avg_ms, 4)
     roof['share_of_step'] = round(dom['ms'] / sum(v['ms'] for v in summ.values()), 3)
+    # whole-step roofline: max(sum bytes / HBM peak, sum flops / f32 MFMA peak) of the
+    # instrumented entry points' algorithmic work, over the measured step time
+    step_flops = sum(v['flops'] for v in summ.values()) / 3
+    step_bytes = sum(v['bytes'] for v in summ.values()) / 3
+    bound_ms = max(step_bytes / (PEAK_HBM_GBS * 1e9), step_flops / (PEAK_F32_TFLOPS * 1e12)) * 1e3
+    step_roof = {'flops_per_step': round(step_flops), 'bytes_per_step': round(step_bytes),
+                 'bound_ms': round(bound_ms, 4), 'frac': round(bound_ms / (el / args.steps * 1e3), 4)}
     # the embedding gather against the HBM roofline (north_star: >= 70 % on the gather)
     gather_roof = {}
     for k in ('rs_gather_fwd', 'rs_gather_bwd'):
@@ -225,9 +244,11 @@ def main():
                        'global_batch': world * B, 'per_gpu_batch': B,
                        'seq_len': tp.get('max_seq_len') if has_seq else None,
                        'dropout': args.dropout, 'parallelism': f'dp{world}',
-                       'hip_graph': graphs is not None, 'final_loss': round(final_loss, 5)},
+                       'hip_graph': graphs is not None, 'final_loss': round(final_loss, 5),
+                       'ids': f'zipf({args.zipf})' if args.zipf else 'uniform'},
             'roofline': roof,
             'gather_roofline': gather_roof,
+            'step_roofline': step_roof,
             'cpu_baseline': cpu,
             'kernel_ms_per_step': {k: round(v['ms'] / 3, 4) for k, v in sorted(summ.items(), key=lambda kv: -kv[1]['ms'])},
         }

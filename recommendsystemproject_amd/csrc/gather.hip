@@ -270,21 +270,36 @@ __global__ __launch_bounds__(256) void gather_bwd_small_kernel(SegLaunch a) {
 }
 
 // Linear(1, D) backward: dW[c] += sum_b dout[b,c]*x[b]; db[c] += sum_b dout[b,c].
-// One workgroup per dense segment, fixed summation order.
-__global__ __launch_bounds__(256) void dense_bwd_kernel(SegLaunch a) {
+// One 1024-thread workgroup per dense segment: 1024/D row lanes, 8 rows in flight per lane,
+// then a fixed-order LDS reduction (deterministic).
+__global__ __launch_bounds__(1024) void dense_bwd_kernel(SegLaunch a) {
   const int s = blockIdx.x;
   const rs_feature_seg_t& sg = a.segs[s];
   if (sg.kind != RS_SEG_DENSE) return;
-  __shared__ float red_w[256], red_b[256];
+  __shared__ float red_w[1024], red_b[1024];
   const int D = sg.dim;
-  const int lanes = 256 / D;  // D <= 256
+  const int lanes = 1024 / D;  // D <= 256
   const int c = threadIdx.x % D, rl = threadIdx.x / D;
   float aw = 0.f, ab = 0.f;
   if (rl < lanes) {
-    for (int row = rl; row < a.rows; row += lanes) {
-      const float g = a.dout[(int64_t)row * a.ldo + sg.out_col + c];
-      aw += g * sg.x[(int64_t)row * sg.idx_stride];
-      ab += g;
+    int row = rl;
+    for (; row + 7 * lanes < a.rows; row += 8 * lanes) {
+      float gv[8], xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        gv[u] = a.dout[(int64_t)(row + u * lanes) * a.ldo + sg.out_col + c];
+        xv[u] = sg.x[(int64_t)(row + u * lanes) * sg.idx_stride];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        aw += gv[u] * xv[u];
+        ab += gv[u];
+      }
+    }
+    for (; row < a.rows; row += lanes) {
+      const float gv = a.dout[(int64_t)row * a.ldo + sg.out_col + c];
+      aw += gv * sg.x[(int64_t)row * sg.idx_stride];
+      ab += gv;
     }
   }
   red_w[threadIdx.x] = aw;
@@ -330,8 +345,10 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.sblocks[s] = 0;
     if (a.small[s]) {
       const int64_t work = (int64_t)rows * (segs_host[s].kind == RS_SEG_POOL ? segs_host[s].bag : 1);
-      int nb = (int)(work / 2048);
-      nb = nb < 1 ? 1 : (nb > 256 ? 256 : nb);
+      // ~256 lookups per workgroup: enough workgroups that the LDS accumulation is not one
+      // long serial chain; each flushes only its non-zero table entries
+      int nb = (int)(work / 256);
+      nb = nb < 1 ? 1 : (nb > 512 ? 512 : nb);
       const int maxnb = cdiv(rows, a.rpb[s]);
       a.sblocks[s] = nb < maxnb ? nb : maxnb;
       sb += a.sblocks[s];
@@ -415,7 +432,7 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
   bool any_dense = false;
   for (int s = 0; s < nseg; ++s) any_dense |= segs_host[s].kind == RS_SEG_DENSE;
   if (any_dense) {
-    dense_bwd_kernel<<<nseg, 256, 0, st>>>(a);
+    dense_bwd_kernel<<<nseg, 1024, 0, st>>>(a);
     RS_CHECK_LAUNCH("rs_gather_bwd dense");
   }
   return 0;

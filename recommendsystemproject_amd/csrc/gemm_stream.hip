@@ -142,10 +142,12 @@ __device__ __forceinline__ void ln_epilogue(const StreamArgs& a, int m, int q, c
 }
 
 // ---------------------------------------------------------------------------------- rowgemm
-template <int NT, int KT, bool LN = false>
+// RG row groups of 16 per wave step: every B fragment read from LDS feeds RG MFMA chains (the
+// LDS reads, not the MFMAs, bounded the one-group loop at K = 64: 45 % MFMA-busy measured).
+template <int NT, int KT, bool LN = false, int RG = 1>
 __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
   constexpr int KP = KT * 16 + 4;  // LDS pitch (floats): conflict-free ds_read_b128 per 16 lanes
-  constexpr bool PREFETCH = KT <= 8;
+  constexpr bool PREFETCH = KT * RG <= 8;
   extern __shared__ __attribute__((aligned(16))) float Bs[];  // [NT*16][KP]
   const int tid = threadIdx.x;
   const int nb0 = blockIdx.y * NT * 16;  // this workgroup's column slice (small-M N split)
@@ -165,63 +167,55 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
 
   const int lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
-  const int groups = (a.M + 15) / 16;
+  const int groups = (a.M + 16 * RG - 1) / (16 * RG);
   DropKey ka{}, kb{};
   if (a.epi & RS_EPI_DROP_A) ka = make_key(a.drop_key, a.site_a, a.drop_p);
   if (a.epi & RS_EPI_DROP_B) kb = make_key(a.drop_key, a.site_b, a.drop_p);
   const int stride = gridDim.x * 8;
   int g = blockIdx.x * 8 + wave;
-  floatx4 areg[KT];
-  auto load_group = [&](int gg, floatx4* dst) {
-    const int m = gg * 16 + r;
+  floatx4 areg[RG][KT];
+  auto load_group = [&](int gg, floatx4 (*dst)[KT]) {
 #pragma unroll
-    for (int t = 0; t < KT; ++t) {
-      const int k = 16 * t + 4 * q;
-      floatx4 v = {0.f, 0.f, 0.f, 0.f};
-      if (m < a.M && k < a.K) v = *reinterpret_cast<const floatx4*>(a.A + (int64_t)m * a.lda + k);
-      dst[t] = v;
+    for (int rg = 0; rg < RG; ++rg) {
+      const int m = (gg * RG + rg) * 16 + r;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const int k = 16 * t + 4 * q;
+        floatx4 v = {0.f, 0.f, 0.f, 0.f};
+        if (m < a.M && k < a.K) v = *reinterpret_cast<const floatx4*>(a.A + (int64_t)m * a.lda + k);
+        dst[rg][t] = v;
+      }
     }
   };
   if (g < groups) load_group(g, areg);
-  floatx4 lnacc[LN ? NT : 1];
-  // aux prefetch costs 16 VGPRs: skipped for the widest instances (they would spill)
-  constexpr bool AUXPF = !(NT >= 12 && KT >= 8);
-  const bool has_aux = (a.epi & (RS_EPI_AUX_ADD | RS_EPI_AUX_MASK)) && a.vec_epi;
+  floatx4 lnacc[LN ? RG : 1][LN ? NT : 1];
   for (; g < groups; g += stride) {
-    floatx4 anext[PREFETCH ? KT : 1];
-    if (PREFETCH && g + stride < groups) load_group(g + stride, anext);
-    const int m = g * 16 + r;
-    // epilogue operands read ahead of the MFMAs so their latency hides under them:
-    // LN: the residual row slice; otherwise one pair of tiles ahead
-    floatx4 lnres[LN ? NT : 1];
-    floatx4 auxc[2], auxn[2];
-    const floatx4 zero4 = {0.f, 0.f, 0.f, 0.f};
-    auto load_aux = [&](int j, floatx4& dst) {
-      const int n0 = nb0 + j * 16 + 4 * q;
-      dst = (j < NT && m < a.M && n0 + 3 < a.N) ? *reinterpret_cast<const floatx4*>(aux_ptr(a, m, n0))
-                                                  : zero4;
-    };
-    if constexpr (LN) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-        lnres[t] = m < a.M ? *reinterpret_cast<const floatx4*>(a.aux + (int64_t)m * a.ld_aux + t * 16 + 4 * q)
-                           : zero4;
-    } else if (AUXPF && has_aux) {
-      load_aux(0, auxc[0]);
-      load_aux(1, auxc[1]);
+    floatx4 anext[RG][KT];  // dead (eliminated) without PREFETCH
+    if constexpr (PREFETCH) {
+      if (g + stride < groups) load_group(g + stride, anext);
     }
-    // N tiles in pairs: two independent accumulator chains hide the 40-cycle dependent MFMA
-    // latency; each pair is stored right away so only 8 accumulators are ever live
+    floatx4 lnres[LN ? RG : 1][LN ? NT : 1];
+    if constexpr (LN) {  // residual rows, read ahead of the MFMAs
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) {
+        const int m = (g * RG + rg) * 16 + r;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+          lnres[rg][t] = m < a.M ? *reinterpret_cast<const floatx4*>(a.aux + (int64_t)m * a.ld_aux + t * 16 + 4 * q) : z;
+        }
+      }
+    }
+    // N tiles in pairs: independent accumulator chains hide the 40-cycle dependent MFMA
+    // latency; each pair is stored right away so only 8*RG accumulators are ever live
 #pragma unroll
     for (int j0 = 0; j0 < NT; j0 += 2) {
       // keep the scheduler from hoisting every pair's B reads / accumulators (register spills)
       __builtin_amdgcn_sched_barrier(0);
       const bool two = j0 + 1 < NT;
-      if (!LN && AUXPF && has_aux && j0 + 2 < NT) {
-        load_aux(j0 + 2, auxn[0]);
-        load_aux(j0 + 3, auxn[1]);
-      }
-      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      floatx4 acc[RG][2];
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) acc[rg][0] = acc[rg][1] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
         const floatx4 b0 = *reinterpret_cast<const floatx4*>(&Bs[(j0 * 16 + r) * KP + 16 * t + 4 * q]);
@@ -231,40 +225,53 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
         for (int s4 = 0; s4 < 4; ++s4) {
           // W rows on the MFMA row side, the 16 A rows on the column side: each lane ends up
           // holding 4 consecutive output columns of one row (float4 epilogue loads / stores)
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(b0[s4], areg[t][s4], acc0, 0, 0, 0);
-          if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(b1[s4], areg[t][s4], acc1, 0, 0, 0);
+#pragma unroll
+          for (int rg = 0; rg < RG; ++rg) {
+            acc[rg][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(b0[s4], areg[rg][t][s4], acc[rg][0], 0, 0, 0);
+            if (two)
+              acc[rg][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(b1[s4], areg[rg][t][s4], acc[rg][1], 0, 0, 0);
+          }
         }
       }
       // C/D map of 16x16: col = lane&15 -> row m of A, row = 4*(lane>>4) + i -> column n of C
-      if constexpr (LN) {
-        lnacc[j0] = acc0;
-        if (two) lnacc[j0 + 1] = acc1;
-        continue;
-      }
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && !two) break;
-        const int n0 = nb0 + (j0 + h) * 16 + 4 * q;
-        if (m >= a.M || n0 >= a.N) continue;
-        const floatx4 acc = (h ? acc1 : acc0) * a.alpha;
-        float* crow = a.C + (int64_t)m * a.ldc;
-        if (a.vec_epi && n0 + 3 < a.N) {
-          if (!AUXPF && has_aux) load_aux(j0 + h, auxc[h]);
-          *reinterpret_cast<floatx4*>(crow + n0) = epi_apply4(a, m, n0, acc, ka, kb, auxc[h]);
-        } else {
+      for (int rg = 0; rg < RG; ++rg) {
+        if constexpr (LN) {
+          lnacc[rg][j0] = acc[rg][0];
+          if (two) lnacc[rg][j0 + 1] = acc[rg][1];
+          continue;
+        }
+        const int m = (g * RG + rg) * 16 + r;
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (n0 + i < a.N) crow[n0 + i] = epi_apply(a, m, n0 + i, acc[i], ka, kb);
+        for (int h = 0; h < 2; ++h) {
+          if (h == 1 && !two) break;
+          const int n0 = nb0 + (j0 + h) * 16 + 4 * q;
+          if (m >= a.M || n0 >= a.N) continue;
+          const floatx4 v = acc[rg][h] * a.alpha;
+          float* crow = a.C + (int64_t)m * a.ldc;
+          if (a.vec_epi && n0 + 3 < a.N) {
+            floatx4 auxv = {0.f, 0.f, 0.f, 0.f};
+            if (a.epi & (RS_EPI_AUX_ADD | RS_EPI_AUX_MASK))
+              auxv = *reinterpret_cast<const floatx4*>(aux_ptr(a, m, n0));
+            *reinterpret_cast<floatx4*>(crow + n0) = epi_apply4(a, m, n0, v, ka, kb, auxv);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (n0 + i < a.N) crow[n0 + i] = epi_apply(a, m, n0 + i, v[i], ka, kb);
+          }
         }
       }
-      auxc[0] = auxn[0];
-      auxc[1] = auxn[1];
     }
-    if constexpr (LN) ln_epilogue<NT>(a, m, q, lnacc, lnres, ka);
-    __builtin_amdgcn_sched_barrier(0);
-    if (PREFETCH) {
+    if constexpr (LN) {
 #pragma unroll
-      for (int t = 0; t < KT; ++t) areg[t] = anext[t];
+      for (int rg = 0; rg < RG; ++rg) ln_epilogue<NT>(a, (g * RG + rg) * 16 + r, q, lnacc[rg], lnres[rg], ka);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PREFETCH) {
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+        for (int t = 0; t < KT; ++t) areg[rg][t] = anext[rg][t];
     } else if (g + stride < groups) {
       load_group(g + stride, areg);
     }
@@ -452,7 +459,10 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   const int nt = small ? 4 : (s.N + 15) / 16, kt = (s.K + 15) / 16;
   const int nsplit = small ? cdiv(s.N, 64) : 1;
   const size_t lds = (size_t)nt * 16 * (kt * 16 + 4) * sizeof(float);
-  const int groups = (s.M + 15) / 16;
+  // RG = 2: two 16-row groups per wave step (B fragments reused across both)
+  // measured slower than one group per step on every K = 64 shape (kept for experiments)
+  const int rg = (!small && kt <= 4 && getenv_flag("RSYS_ROWGEMM_RG2")) ? 2 : 1;
+  const int groups = (s.M + 16 * rg - 1) / (16 * rg);
   int bx = cdiv(groups, small ? 8 : 8 * 2);  // small M: one row group per wave
   const int per_cu = lds > 80 * 1024 ? 1 : (lds > 53 * 1024 ? 2 : (lds > 40 * 1024 ? 3 : 4));
   if (bx > 256 * per_cu) bx = 256 * per_cu;
@@ -460,7 +470,8 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   const dim3 blocks(bx, nsplit);
 #define RS_RG(NTV, KTV)                                                            \
   case NTV * 100 + KTV:                                                            \
-    rowgemm_kernel<NTV, KTV><<<blocks, 512, lds, st>>>(s);                          \
+    if (rg == 2 && KTV <= 4) rowgemm_kernel<NTV, KTV, false, (KTV <= 4 ? 2 : 1)><<<blocks, 512, lds, st>>>(s); \
+    else rowgemm_kernel<NTV, KTV><<<blocks, 512, lds, st>>>(s);                     \
     break;
   switch (nt * 100 + kt) {
     RS_RG(4, 3) RS_RG(4, 4) RS_RG(4, 12) RS_RG(4, 16) RS_RG(12, 4) RS_RG(16, 4) RS_RG(3, 4)

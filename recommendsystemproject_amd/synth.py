@@ -56,6 +56,15 @@ def _tags_for(rng, valid: np.ndarray, vocab: int) -> np.ndarray:
     return np.where(keep, tags, 0).astype(np.int64)
 
 
+def _ids(rng, V: int, size, zipf: float | None) -> np.ndarray:
+    """Ids in [1, V-1]: uniform, or Zipf(alpha) ranks scattered over the table by a
+    multiplicative hash (SURVEY §8d's skewed variant: a few hot rows, a long cold tail)."""
+    if not zipf:
+        return rng.integers(1, V, size=size)
+    z = rng.zipf(zipf, size=size).astype(np.uint64) - np.uint64(1)
+    return ((z * np.uint64(2654435761)) % np.uint64(max(V - 1, 1))).astype(np.int64) + 1
+
+
 def make_tower_batch(tower_cfg: dict, B: int, rng: np.random.Generator,
                      synth_cfg: dict | None = None, seq_len: int | None = None,
                      seq_valid: np.ndarray | None = None, ids_override: dict | None = None) -> dict:
@@ -63,6 +72,7 @@ def make_tower_batch(tower_cfg: dict, B: int, rng: np.random.Generator,
     `ids_override` {feature name: int64 [B]} forces single-value ids (e.g. collisions)."""
     synth_cfg = synth_cfg or {}
     bags = synth_cfg.get('bags', {})
+    zipf = synth_cfg.get('zipf')
     out: dict = {}
     sparse_cols = []
     seq: dict = {}
@@ -75,10 +85,10 @@ def make_tower_batch(tower_cfg: dict, B: int, rng: np.random.Generator,
             else:  # long bag (C3 hist_item_ids): k ~ U{min_valid..length}, right-padded with 0
                 Lb = int(spec['length'])
                 k = rng.integers(int(spec.get('min_valid', 0)), Lb + 1, size=B)
-                ids = rng.integers(1, V, size=(B, Lb))
+                ids = _ids(rng, V, (B, Lb), zipf)
                 seq[name] = np.where(np.arange(Lb)[None, :] < k[:, None], ids, 0).astype(np.int64)
         else:
-            col = rng.integers(1, V, size=B).astype(np.int64)
+            col = (_ids(rng, V, B, zipf) if V >= 1000 else rng.integers(1, V, size=B)).astype(np.int64)
             if ids_override and name in ids_override:
                 col = np.asarray(ids_override[name], dtype=np.int64)
             sparse_cols.append(col)
@@ -98,7 +108,7 @@ def make_tower_batch(tower_cfg: dict, B: int, rng: np.random.Generator,
             if 'pooling' in feat:
                 seq[name] = _tags_for(rng, valid, V)
             else:
-                ids = rng.integers(1, V, size=(B, L))
+                ids = _ids(rng, V, (B, L), zipf)
                 seq[name] = np.where(valid, ids, 0).astype(np.int64)
     if seq:
         out['sequence'] = seq

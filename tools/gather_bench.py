@@ -1,0 +1,87 @@
+"""Standalone embedding-gather benchmark against the HBM roofline (the >= 70 %
+target is reported on a launch of >= 100 MB).
+
+    python tools/gather_bench.py [--vocab 10000000] [--dim 128] [--rows 65536] [--bag 50]
+
+Pooled-mean bags (the C3 history feature) and single-id lookups, forward gather and backward
+scatter (touch counts on, as for a lazy-Adam table). Algorithmic bytes per launch:
+  fwd: lookups * D * 4 (rows read) + rows * D * 4 (written) + lookups * 8 (int64 ids)
+  bwd: the same rows written (first lookup: plain store) + dout read + ids
+Prints one JSON line per case.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from recommendsystemproject_amd import _hip, ops  # noqa: E402
+from recommendsystemproject_amd.functions import _seg  # noqa: E402
+
+PEAK = 8000.0  # GB/s, MI355X HBM3E spec
+
+
+def timed(fn, it):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--vocab', type=int, default=10_000_000)
+    ap.add_argument('--dim', type=int, default=128)
+    ap.add_argument('--rows', type=int, default=65536)
+    ap.add_argument('--bag', type=int, default=50)
+    ap.add_argument('--iters', type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device('cuda:0')
+    V, D, B, L = args.vocab, args.dim, args.rows, args.bag
+    g = torch.Generator(device=dev).manual_seed(0)
+    table = torch.randn(V, D, device=dev, generator=g)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    for kind, bag in (('pooled_mean', L), ('single_id', 1)):
+        ids = torch.randint(1, V, (B, bag), device=dev, generator=g)
+        out = torch.empty(B, D, device=dev)
+        if bag > 1:
+            seg = _seg(kind=_hip.RS_SEG_POOL, dim=D, out_col=0, pool_mode=_hip.RS_POOL['mean'], bag=bag,
+                       vocab=V, idx_stride=bag, idx=ids.data_ptr(), table=table.data_ptr(), pad_idx=0)
+        else:
+            seg = _seg(kind=_hip.RS_SEG_SPARSE, dim=D, out_col=0, vocab=V, idx_stride=1, idx=ids.data_ptr(),
+                       table=table.data_ptr(), pad_idx=0)
+        ms = timed(lambda: ops.gather_fwd([seg], B, out, err), args.iters)
+        lookups = B * bag
+        byts = lookups * D * 4 + B * D * 4 + lookups * 8
+        print(json.dumps({'case': f'gather_fwd {kind}', 'vocab': V, 'dim': D, 'rows': B, 'bag': bag,
+                          'MB_per_launch': round(byts / 1e6, 1), 'us': round(ms * 1e3, 1),
+                          'GBps': round(byts / ms / 1e6, 1), 'frac_of_8TBps': round(byts / ms / 1e6 / PEAK, 3)}))
+        # backward scatter into a table gradient with touch counts (lazy-Adam tables)
+        grad = torch.zeros(V, D, device=dev)
+        flag = torch.zeros(V, dtype=torch.int32, device=dev)
+        lst = torch.zeros(V, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        _hip.call('rs_sparse_touch', ids.data_ptr(), B, bag, bag, V, 0, flag.data_ptr(), lst.data_ptr(),
+                  cnt.data_ptr(), ops.stream())
+        seg.grad = grad.data_ptr()
+        seg.touch_count = flag.data_ptr()
+        dout = torch.randn(B, D, device=dev)
+        ms = timed(lambda: ops.gather_bwd([seg], B, dout), args.iters)
+        byts = lookups * D * 4 + B * D * 4 + lookups * (8 + 4)
+        print(json.dumps({'case': f'gather_bwd {kind} (touch counts)', 'MB_per_launch': round(byts / 1e6, 1),
+                          'us': round(ms * 1e3, 1), 'GBps': round(byts / ms / 1e6, 1),
+                          'frac_of_8TBps': round(byts / ms / 1e6 / PEAK, 3)}))
+        del grad, flag, lst
+    assert err.item() == 0
+
+
+if __name__ == '__main__':
+    main()
