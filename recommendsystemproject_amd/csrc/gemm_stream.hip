@@ -85,23 +85,27 @@ __device__ __forceinline__ floatx4 epi_apply4(const StreamArgs& a, int m, int n0
 // the same r: two xor shuffles (16, 32) complete the row sums. Same operation order per element
 // as the unfused pair (GEMM epilogue: alpha*acc + bias; add_ln: drop(.) + resid, mean, centred
 // variance, 1/sqrtf).
-template <int NT>
+template <int NT, int EPI>
 __device__ __forceinline__ void ln_epilogue(const StreamArgs& a, int m, int q, const floatx4* acc,
-                                            const floatx4* resv, const DropKey& ka) {
+                                            const floatx4* resv, const DropKey& ka,
+                                            const float* sbias, const float* sgamma,
+                                            const float* sbeta) {
+  constexpr bool kBias = EPI >= 0 ? (EPI & RS_EPI_BIAS) != 0 : false;
+  constexpr bool kDrop = EPI >= 0 ? (EPI & RS_EPI_DROP_A) != 0 : false;
   constexpr int N = NT * 16;
   float hv[NT][4];
   float s = 0.f;
-  const bool ok = m < a.M;
+  const bool ok = EPI >= 0 || m < a.M;  // specialised instances: M % 16 == 0
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int n0 = t * 16 + 4 * q;
     floatx4 v = acc[t] * a.alpha;
-    if (a.epi & RS_EPI_BIAS) v += *reinterpret_cast<const floatx4*>(a.bias + n0);
+    if (EPI >= 0 ? kBias : (a.epi & RS_EPI_BIAS) != 0) v += *reinterpret_cast<const floatx4*>(sbias + n0);
     const floatx4 res = resv[t];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float x = v[e];
-      if (a.epi & RS_EPI_DROP_A) x *= keep_mult(ka, (uint64_t)m * N + n0 + e);
+      if (EPI >= 0 ? kDrop : (a.epi & RS_EPI_DROP_A) != 0) x *= keep_mult(ka, (uint64_t)m * N + n0 + e);
       hv[t][e] = x + res[e];
       s += hv[t][e];
     }
@@ -124,8 +128,8 @@ __device__ __forceinline__ void ln_epilogue(const StreamArgs& a, int m, int q, c
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int n0 = t * 16 + 4 * q;
-    const floatx4 gm = *reinterpret_cast<const floatx4*>(a.ln_gamma + n0);
-    const floatx4 bt = *reinterpret_cast<const floatx4*>(a.ln_beta + n0);
+    const floatx4 gm = *reinterpret_cast<const floatx4*>(sgamma + n0);
+    const floatx4 bt = *reinterpret_cast<const floatx4*>(sbeta + n0);
     floatx4 h4, y4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -141,13 +145,47 @@ __device__ __forceinline__ void ln_epilogue(const StreamArgs& a, int m, int q, c
   }
 }
 
+// compile-time epilogue (EPI = RS_EPI_* bits | kEpiBeta): no uniform branches in the store
+// loop, so the compiler can count outstanding stores exactly instead of draining vmcnt(0) (which
+// also waited for the next row group's prefetched A) after every epilogue load. bias and the
+// AUX_ADD table (aux_mod rows: the positional embedding) come from LDS.
+constexpr int kEpiBeta = 64;
+template <int EPI>
+__device__ __forceinline__ floatx4 epi4_ct(const StreamArgs& a, int m, int n0, floatx4 v,
+                                           const DropKey& ka, const DropKey& kb,
+                                           const floatx4& biasv, const floatx4& auxv,
+                                           const floatx4& cv) {
+  if constexpr ((EPI & RS_EPI_BIAS) != 0) v += biasv;
+  if constexpr ((EPI & RS_EPI_AUX_MASK) != 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = auxv[i] > 0.f ? v[i] : 0.f;
+  }
+  if constexpr ((EPI & RS_EPI_RELU) != 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], 0.f);
+  }
+  const uint64_t e0 = (uint64_t)m * a.N + n0;
+  if constexpr ((EPI & RS_EPI_DROP_A) != 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] *= keep_mult(ka, e0 + i);
+  }
+  if constexpr ((EPI & RS_EPI_AUX_ADD) != 0) v += auxv;
+  if constexpr ((EPI & RS_EPI_DROP_B) != 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] *= keep_mult(kb, e0 + i);
+  }
+  if constexpr ((EPI & kEpiBeta) != 0) v += a.beta * cv;
+  return v;
+}
+
 // ---------------------------------------------------------------------------------- rowgemm
 // RG row groups of 16 per wave step: every B fragment read from LDS feeds RG MFMA chains (the
 // LDS reads, not the MFMAs, bounded the one-group loop at K = 64: 45 % MFMA-busy measured).
-template <int NT, int KT, bool LN = false, int RG = 1>
+template <int NT, int KT, bool LN = false, int RG = 1, int EPI = -1>
 __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
   constexpr int KP = KT * 16 + 4;  // LDS pitch (floats): conflict-free ds_read_b128 per 16 lanes
-  constexpr bool PREFETCH = KT * RG <= 8;
+  // specialised instances are lean enough (~100 VGPRs) to prefetch K = 256 rows too
+  constexpr bool PREFETCH = KT * RG <= 8 || (EPI >= 0 && RG == 1 && KT <= 16);
   extern __shared__ __attribute__((aligned(16))) float Bs[];  // [NT*16][KP]
   const int tid = threadIdx.x;
   const int nb0 = blockIdx.y * NT * 16;  // this workgroup's column slice (small-M N split)
@@ -163,6 +201,28 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
       Bs[n * KP + k] = (nb0 + n < a.N && k < a.K) ? a.B[(int64_t)k * a.ldb + nb0 + n] : 0.f;
     }
   }
+  // specialised epilogues: bias [NT*16] and the AUX_ADD table [aux_mod][NT*16] in LDS
+  constexpr int NTN = NT * 16;
+  float* sbias = Bs + NTN * KP;
+  float* saux = sbias + NTN;
+  if constexpr ((EPI >= 0 && (EPI & RS_EPI_BIAS) != 0) || LN) {
+    if (EPI >= 0 ? (EPI & RS_EPI_BIAS) != 0 : (a.epi & RS_EPI_BIAS) != 0)
+      for (int n = tid; n < NTN; n += 512) sbias[n] = a.bias[nb0 + n];
+  }
+  float* sgamma = saux;  // LN: gamma, beta after the bias (LN kernels have no AUX table in LDS)
+  float* sbeta = saux + NTN;
+  if constexpr (LN) {
+    for (int n = tid; n < NTN; n += 512) {
+      sgamma[n] = a.ln_gamma[n];
+      sbeta[n] = a.ln_beta[n];
+    }
+  }
+  if constexpr (!LN && EPI >= 0 && (EPI & RS_EPI_AUX_ADD) != 0) {
+    for (int idx = tid; idx < a.aux_mod * NTN; idx += 512) {
+      const int rr = idx / NTN, n = idx % NTN;
+      saux[idx] = a.aux[(int64_t)rr * a.ld_aux + nb0 + n];
+    }
+  }
   __syncthreads();
 
   const int lane = tid & 63, wave = tid >> 6;
@@ -174,6 +234,10 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
   const int stride = gridDim.x * 8;
   int g = blockIdx.x * 8 + wave;
   floatx4 areg[RG][KT];
+  // FULL (specialised instances): M % 16 == 0 and K == KT*16, so no row / k guards and no
+  // uniform branches in the loop body -- the waitcnt pass can then count the outstanding
+  // stores exactly instead of draining vmcnt(0) (which also waited for the prefetch)
+  constexpr bool FULL = EPI >= 0;
   auto load_group = [&](int gg, floatx4 (*dst)[KT]) {
 #pragma unroll
     for (int rg = 0; rg < RG; ++rg) {
@@ -182,7 +246,9 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
       for (int t = 0; t < KT; ++t) {
         const int k = 16 * t + 4 * q;
         floatx4 v = {0.f, 0.f, 0.f, 0.f};
-        if (m < a.M && k < a.K) v = *reinterpret_cast<const floatx4*>(a.A + (int64_t)m * a.lda + k);
+        // explicit global address space: a flat load would also count against lgkmcnt
+        if (FULL || (m < a.M && k < a.K))
+          v = *(const __attribute__((address_space(1))) floatx4*)(a.A + (int64_t)m * a.lda + k);
         dst[rg][t] = v;
       }
     }
@@ -190,61 +256,107 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
   if (g < groups) load_group(g, areg);
   floatx4 lnacc[LN ? RG : 1][LN ? NT : 1];
   for (; g < groups; g += stride) {
-    floatx4 anext[RG][KT];  // dead (eliminated) without PREFETCH
-    if constexpr (PREFETCH) {
-      if (g + stride < groups) load_group(g + stride, anext);
-    }
     floatx4 lnres[LN ? RG : 1][LN ? NT : 1];
-    if constexpr (LN) {  // residual rows, read ahead of the MFMAs
+    if constexpr (LN) {  // residual rows, issued BEFORE the next group's A prefetch (vmcnt is in order)
 #pragma unroll
       for (int rg = 0; rg < RG; ++rg) {
         const int m = (g * RG + rg) * 16 + r;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const floatx4 z = {0.f, 0.f, 0.f, 0.f};
-          lnres[rg][t] = m < a.M ? *reinterpret_cast<const floatx4*>(a.aux + (int64_t)m * a.ld_aux + t * 16 + 4 * q) : z;
+          lnres[rg][t] = (FULL || m < a.M) ? *reinterpret_cast<const floatx4*>(a.aux + (int64_t)m * a.ld_aux + t * 16 + 4 * q) : z;
         }
       }
     }
-    // N tiles in pairs: independent accumulator chains hide the 40-cycle dependent MFMA
-    // latency; each pair is stored right away so only 8*RG accumulators are ever live
+    // specialised epilogues' global operands (AUX_MASK rows / C for beta), also issued before
+    // the A prefetch so that waiting for them does not wait for the prefetch
+    constexpr bool EPRE = EPI >= 0 && (EPI & (RS_EPI_AUX_MASK | kEpiBeta)) != 0;
+    static_assert(EPI < 0 || (EPI & RS_EPI_AUX_MASK) == 0 || (EPI & kEpiBeta) == 0,
+                  "AUX_MASK and beta cannot both be preloaded");
+    floatx4 epre[EPRE ? RG : 1][EPRE ? NT : 1];
+    if constexpr (EPRE) {
 #pragma unroll
-    for (int j0 = 0; j0 < NT; j0 += 2) {
-      // keep the scheduler from hoisting every pair's B reads / accumulators (register spills)
+      for (int rg = 0; rg < RG; ++rg) {
+        const int m = (g * RG + rg) * 16 + r;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int n0 = nb0 + t * 16 + 4 * q;
+          if constexpr ((EPI & RS_EPI_AUX_MASK) != 0)
+            epre[rg][t] = *reinterpret_cast<const floatx4*>(a.aux + (int64_t)m * a.ld_aux + n0);
+          else
+            epre[rg][t] = *reinterpret_cast<const floatx4*>(a.C + (int64_t)m * a.ldc + n0);
+        }
+      }
+    }
+    floatx4 anext[RG][KT];  // dead (eliminated) without PREFETCH
+    if constexpr (PREFETCH) {
+      if constexpr (FULL) load_group(g + stride < groups ? g + stride : g, anext);  // no branch
+      else if (g + stride < groups) load_group(g + stride, anext);
+    }
+    // N tiles in groups of TG: TG independent accumulator chains hide the 40-cycle dependent
+    // MFMA latency; each group is stored right away so only 4*TG*RG accumulators are live.
+    // Specialised instances use TG = 4 (more MFMAs between the B-fragment LDS reads).
+    constexpr int TG = (EPI >= 0 && NT % 4 == 0 && RG == 1) ? 4 : 2;
+#pragma unroll
+    for (int j0 = 0; j0 < NT; j0 += TG) {
+      // keep the scheduler from hoisting every group's B reads / accumulators (register spills)
       __builtin_amdgcn_sched_barrier(0);
-      const bool two = j0 + 1 < NT;
-      floatx4 acc[RG][2];
+      floatx4 acc[RG][TG];
 #pragma unroll
-      for (int rg = 0; rg < RG; ++rg) acc[rg][0] = acc[rg][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+        for (int h = 0; h < TG; ++h) acc[rg][h] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
-        const floatx4 b0 = *reinterpret_cast<const floatx4*>(&Bs[(j0 * 16 + r) * KP + 16 * t + 4 * q]);
-        floatx4 b1 = b0;
-        if (two) b1 = *reinterpret_cast<const floatx4*>(&Bs[((j0 + 1) * 16 + r) * KP + 16 * t + 4 * q]);
+        floatx4 b[TG];
+#pragma unroll
+        for (int h = 0; h < TG; ++h)
+          b[h] = (j0 + h < NT) ? *reinterpret_cast<const floatx4*>(&Bs[((j0 + h) * 16 + r) * KP + 16 * t + 4 * q])
+                               : b[0];
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
           // W rows on the MFMA row side, the 16 A rows on the column side: each lane ends up
           // holding 4 consecutive output columns of one row (float4 epilogue loads / stores)
 #pragma unroll
-          for (int rg = 0; rg < RG; ++rg) {
-            acc[rg][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(b0[s4], areg[rg][t][s4], acc[rg][0], 0, 0, 0);
-            if (two)
-              acc[rg][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(b1[s4], areg[rg][t][s4], acc[rg][1], 0, 0, 0);
-          }
+          for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+            for (int h = 0; h < TG; ++h)
+              if (j0 + h < NT)
+                acc[rg][h] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[h][s4], areg[rg][t][s4], acc[rg][h], 0, 0, 0);
         }
       }
       // C/D map of 16x16: col = lane&15 -> row m of A, row = 4*(lane>>4) + i -> column n of C
 #pragma unroll
       for (int rg = 0; rg < RG; ++rg) {
         if constexpr (LN) {
-          lnacc[rg][j0] = acc[rg][0];
-          if (two) lnacc[rg][j0 + 1] = acc[rg][1];
+#pragma unroll
+          for (int h = 0; h < TG; ++h)
+            if (j0 + h < NT) lnacc[rg][j0 + h] = acc[rg][h];
           continue;
         }
         const int m = (g * RG + rg) * 16 + r;
+        if constexpr (EPI >= 0) {  // N % (NT*16) == 0 and 16-byte rows guaranteed by the dispatch
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          if (h == 1 && !two) break;
+          for (int h = 0; h < TG; ++h) {
+            if (j0 + h >= NT) break;
+            const int nl = (j0 + h) * 16 + 4 * q, n0 = nb0 + nl;
+            {  // FULL: every row valid
+              const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+              floatx4 biasv = z, auxv = z, cv = z;
+              if constexpr ((EPI & RS_EPI_BIAS) != 0) biasv = *reinterpret_cast<const floatx4*>(sbias + nl);
+              if constexpr ((EPI & RS_EPI_AUX_ADD) != 0)
+                auxv = *reinterpret_cast<const floatx4*>(saux + (m % a.aux_mod) * NTN + nl);
+              if constexpr ((EPI & RS_EPI_AUX_MASK) != 0) auxv = epre[rg][j0 + h];
+              if constexpr ((EPI & kEpiBeta) != 0) cv = epre[rg][j0 + h];
+              *reinterpret_cast<floatx4*>(a.C + (int64_t)m * a.ldc + n0) =
+                  epi4_ct<EPI>(a, m, n0, acc[rg][h] * a.alpha, ka, kb, biasv, auxv, cv);
+            }
+          }
+          continue;
+        }
+#pragma unroll
+        for (int h = 0; h < TG; ++h) {
+          if (j0 + h >= NT) break;
           const int n0 = nb0 + (j0 + h) * 16 + 4 * q;
           if (m >= a.M || n0 >= a.N) continue;
           const floatx4 v = acc[rg][h] * a.alpha;
@@ -264,7 +376,8 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
     }
     if constexpr (LN) {
 #pragma unroll
-      for (int rg = 0; rg < RG; ++rg) ln_epilogue<NT>(a, (g * RG + rg) * 16 + r, q, lnacc[rg], lnres[rg], ka);
+      for (int rg = 0; rg < RG; ++rg)
+        ln_epilogue<NT, EPI>(a, (g * RG + rg) * 16 + r, q, lnacc[rg], lnres[rg], ka, sbias, sgamma, sbeta);
     }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (PREFETCH) {
@@ -468,6 +581,28 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   if (bx > 256 * per_cu) bx = 256 * per_cu;
   if (bx < 1) bx = 1;
   const dim3 blocks(bx, nsplit);
+  // specialised (compile-time epilogue) instances for the encoder's GEMMs
+  const int ekey = s.epi | (s.beta != 0.f ? kEpiBeta : 0);
+  const bool aux_small = !(s.epi & RS_EPI_AUX_ADD) || (int64_t)s.aux_mod * nt * 16 * 4 <= 48 * 1024;
+  if (!small && rg == 1 && s.vec_epi && s.N % (nt * 16) == 0 && aux_small && s.M % 16 == 0 &&
+      s.K == kt * 16 &&
+      !getenv_flag("RSYS_ROWGEMM_GENERIC")) {
+    const size_t lds2 = lds + (size_t)(nt * 16 + ((s.epi & RS_EPI_AUX_ADD) ? s.aux_mod * nt * 16 : 0)) * sizeof(float);
+    const int per_cu2 = lds2 > 80 * 1024 ? 1 : (lds2 > 53 * 1024 ? 2 : (lds2 > 40 * 1024 ? 3 : 4));
+    int bx2 = cdiv(groups, 16);
+    if (bx2 > 256 * per_cu2) bx2 = 256 * per_cu2;
+    if (bx2 < 1) bx2 = 1;
+#define RS_RGE(NTV, KTV, EV)                                                                     \
+    if (nt == NTV && kt == KTV && ekey == EV) {                                                  \
+      rowgemm_kernel<NTV, KTV, false, 1, EV><<<dim3(bx2, 1), 512, lds2, st>>>(s);               \
+      RS_CHECK_LAUNCH("rowgemm (specialised)");                                                  \
+      return 0;                                                                                  \
+    }
+    RS_RGE(16, 4, 19) RS_RGE(16, 4, 3) RS_RGE(16, 4, 8) RS_RGE(16, 4, 0) RS_RGE(12, 4, 1)
+    RS_RGE(4, 12, 64) RS_RGE(4, 16, 64) RS_RGE(4, 4, 0) RS_RGE(4, 4, 64) RS_RGE(4, 3, 53)
+    RS_RGE(4, 3, 5) RS_RGE(4, 16, 0) RS_RGE(4, 12, 0)
+#undef RS_RGE
+  }
 #define RS_RG(NTV, KTV)                                                            \
   case NTV * 100 + KTV:                                                            \
     if (rg == 2 && KTV <= 4) rowgemm_kernel<NTV, KTV, false, (KTV <= 4 ? 2 : 1)><<<blocks, 512, lds, st>>>(s); \
@@ -495,13 +630,22 @@ int rowgemm_ln_launch(const StreamArgs& s, hipStream_t st) {
                    aligned16(s.ln_y) && aligned16(s.ln_gamma) && aligned16(s.ln_beta) &&
                    (!(s.epi & RS_EPI_BIAS) || aligned16(s.bias)),
                "rowgemm_ln: operands must be 16-byte aligned");
-  const size_t lds = (size_t)4 * 16 * (kt * 16 + 4) * sizeof(float);
+  const size_t lds = (size_t)4 * 16 * (kt * 16 + 4 + 3) * sizeof(float);  // + bias, gamma, beta
   const int groups = (s.M + 15) / 16;
   int bx = cdiv(groups, 16);
   const int per_cu = lds > 80 * 1024 ? 1 : (lds > 53 * 1024 ? 2 : (lds > 40 * 1024 ? 3 : 4));
   if (bx > 256 * per_cu) bx = 256 * per_cu;
-  if (kt == 4) rowgemm_kernel<4, 4, true><<<bx, 512, lds, st>>>(s);
-  else rowgemm_kernel<4, 16, true><<<bx, 512, lds, st>>>(s);
+  const int ekey = s.epi & (RS_EPI_BIAS | RS_EPI_DROP_A);
+  if (s.M % 16 != 0 || s.K != kt * 16) {  // guarded generic instances
+    if (kt == 4) rowgemm_kernel<4, 4, true><<<bx, 512, lds, st>>>(s);
+    else rowgemm_kernel<4, 16, true><<<bx, 512, lds, st>>>(s);
+  } else {
+#define RS_LN(KTV, EV) \
+  if (kt == KTV && ekey == EV) rowgemm_kernel<4, KTV, true, 1, EV><<<bx, 512, lds, st>>>(s);
+    RS_LN(4, 0) else RS_LN(4, 1) else RS_LN(4, 16) else RS_LN(4, 17)
+    else RS_LN(16, 0) else RS_LN(16, 1) else RS_LN(16, 16) else RS_LN(16, 17)
+#undef RS_LN
+  }
   RS_CHECK_LAUNCH("rowgemm_ln");
   return 0;
 }
