@@ -550,15 +550,17 @@ int wgrad_blocks(int Kr) {
 // ------------------------------------------------------------------------------ dispatch
 // Small M: split N over workgroups (NT = 4 column tiles each) so the grid still fills the chip.
 constexpr int kSmallM = 32768;
+constexpr int kSmallNT = 2;  // small M (the MLP at B = 4096): 32 columns per workgroup
 
 bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda) {
   if (transA || M < 1024 || K < 4 || K > 256 || N < 1 || N > 256) return false;
   if (K % 4 != 0 || lda % 4 != 0 || !aligned16(A)) return false;
-  const int nt = M < kSmallM ? 4 : (N + 15) / 16, kt = (K + 15) / 16;
-  // instantiated (NT, KT) pairs: the encoder/projection shapes
+  const int nt = M < kSmallM ? kSmallNT : (N + 15) / 16, kt = (K + 15) / 16;
+  // instantiated (NT, KT) pairs: the encoder/projection shapes and the small-M MLP shapes
   switch (nt * 100 + kt) {
     case 403: case 404: case 412: case 416: case 1204: case 1604: case 304: case 1216:
-    case 204: case 804: case 408: case 808: case 1608: return true;
+    case 204: case 804: case 408: case 808: case 1608:
+    case 203: case 208: case 211: case 212: case 216: return true;
     default: return false;
   }
 }
@@ -569,8 +571,8 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
               (!(s.epi & RS_EPI_BIAS) || aligned16(s.bias)) &&
               (!(s.epi & (RS_EPI_AUX_ADD | RS_EPI_AUX_MASK)) || (s.ld_aux % 4 == 0 && aligned16(s.aux)));
   const bool small = s.M < kSmallM;
-  const int nt = small ? 4 : (s.N + 15) / 16, kt = (s.K + 15) / 16;
-  const int nsplit = small ? cdiv(s.N, 64) : 1;
+  const int nt = small ? kSmallNT : (s.N + 15) / 16, kt = (s.K + 15) / 16;
+  const int nsplit = small ? cdiv(s.N, kSmallNT * 16) : 1;
   const size_t lds = (size_t)nt * 16 * (kt * 16 + 4) * sizeof(float);
   // RG = 2: two 16-row groups per wave step (B fragments reused across both)
   // measured slower than one group per step on every K = 64 shape (kept for experiments)
@@ -611,6 +613,7 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   switch (nt * 100 + kt) {
     RS_RG(4, 3) RS_RG(4, 4) RS_RG(4, 12) RS_RG(4, 16) RS_RG(12, 4) RS_RG(16, 4) RS_RG(3, 4)
     RS_RG(12, 16) RS_RG(2, 4) RS_RG(8, 4) RS_RG(4, 8) RS_RG(8, 8) RS_RG(16, 8)
+    RS_RG(2, 3) RS_RG(2, 8) RS_RG(2, 11) RS_RG(2, 12) RS_RG(2, 16)
     default: set_error("rowgemm: no instance for N=%d K=%d", s.N, s.K); return -1;
   }
 #undef RS_RG
