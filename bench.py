@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 from recommendsystemproject_amd import dist as rdist  # noqa: E402
 from recommendsystemproject_amd import synth  # noqa: E402
+from recommendsystemproject_amd import precision  # noqa: E402
 from recommendsystemproject_amd.flat import ensure_flat  # noqa: E402
 from recommendsystemproject_amd.optim import Adam  # noqa: E402
 from recommendsystemproject_amd.profiling import KernelTimer  # noqa: E402
@@ -47,6 +48,8 @@ def parse():
     ap.add_argument('--batch', type=int, default=None, help='per-GPU batch (default: config)')
     ap.add_argument('--dropout', default='config', choices=['config', '0'])
     ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'],
+                    help='compute dtype of the encoder GEMMs (bf16: bf16 MFMA, fp32 accumulate / master weights)')
     ap.add_argument('--zipf', type=float, default=None, help='Zipf(alpha) ids instead of uniform (C3 variant)')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -101,6 +104,7 @@ def main():
             t.get('transformer_parameters', {})['dropout'] = 0.0
     if args.zipf:
         cfg.setdefault('synthetic', {})['zipf'] = args.zipf
+    precision.set_compute_dtype(args.dtype)
     B = args.batch or int(cfg['train']['batch_size'])
     T = float(cfg['train']['temperature'])
     maps = {'user': synth.tower_layout(cfg['two_tower']['user_tower']),
@@ -237,7 +241,7 @@ def main():
             'metric': 'training samples/sec (user-item pairs) at batch 4096; 1/2/4/8 MI355X',
             'value': round(samples / el, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 3),
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
             'data': 'synthetic (MovieLens-1M-shaped ids, seeded numpy PCG64, resident in HBM)',
             'config': {'workload': f'{args.config}: ' + ('synthetic 10M-item vocab DSSM (emb 128, pooled 50-long history, lazy-exact Adam tables)' if args.config == 'c3' else 'MovieLens-1M DSSM') +
                        (f' + Transformer seq encoder (seq_len {tp.get("max_seq_len")}, d={cfg["two_tower"]["user_tower"]["embedding_dim"]})' if has_seq else ''),

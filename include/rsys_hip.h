@@ -49,6 +49,10 @@ int rs_device_check(void);            /* 0 if a gfx950 device is current, else h
 #define RS_EPI_AUX_MASK 8
 #define RS_EPI_DROP_A 16
 #define RS_EPI_DROP_B 32
+/* Flag in the same word: the caller allows bf16 operands (bf16 compute mode). Where a bf16-MFMA
+ * instance exists (the encoder's streaming shapes) A and B are rounded to bf16 (RNE) and the
+ * products accumulate in fp32; every other shape runs the fp32 kernels unchanged. */
+#define RS_GEMM_BF16 256
 int rs_gemm_auto_split(int M, int N, int K);   /* split_k that fills the chip for long K */
 int64_t rs_gemm_ws_bytes(int M, int N, int K, int split_k);
 int rs_gemm_f32(int transA, int transB, int M, int N, int K, float alpha,
@@ -120,7 +124,8 @@ int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, const float*
 int rs_gemm_add_layernorm(int M, int N, int K, const float* A, int lda, const float* W, int ldw,
                           const float* bias, const float* resid, float* h, float* y,
                           const float* gamma, const float* beta, float* mean, float* rstd, float eps,
-                          float p, const int64_t* key, int site, void* stream);
+                          float p, const int64_t* key, int site, int flags, void* stream);
+/* flags: RS_GEMM_BF16 (bf16 operands for the GEMM part; LayerNorm stays fp32) or 0. */
 
 /* ---------------------------------------------------------------- sequence mask
  * padding mask from the first sequence feature (== pad_value) with the all-padding-row fix,

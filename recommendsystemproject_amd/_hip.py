@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, '_lib', 'librsys_hip.so')
 
 RS_EPI_BIAS, RS_EPI_RELU, RS_EPI_AUX_ADD, RS_EPI_AUX_MASK = 1, 2, 4, 8
+RS_GEMM_BF16 = 256
 RS_EPI_DROP_A, RS_EPI_DROP_B = 16, 32
 RS_SEG_SPARSE, RS_SEG_POOL, RS_SEG_DENSE, RS_SEG_LASTVALID, RS_SEG_COPY = 0, 1, 2, 3, 4
 RS_POOL = {'mean': 0, 'sum': 1, 'max': 2}
@@ -38,7 +39,7 @@ SIGNATURES = {
     'rs_gemm_f32': (i32, [i32, i32, i32, i32, i32, f32, vp, i32, vp, i32, f32, vp, i32, i32, vp, vp,
                           i32, i32, f32, vp, i32, i32, vp, i32, vp, vp]),
     'rs_gemm_add_layernorm': (i32, [i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp,
-                                    f32, f32, vp, i32, vp]),
+                                    f32, f32, vp, i32, i32, vp]),
     'rs_colsum_ws_bytes': (i64, [i32, i32]),
     'rs_colsum': (i32, [vp, i32, i32, i32, f32, f32, vp, vp, vp]),
     'rs_gather_fwd': (i32, [vp, i32, i32, vp, i32, vp, vp]),

@@ -302,6 +302,8 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
                            int site_b, float* rowsum, int split_k, float* ws, void* stream) {
   RS_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "rs_gemm_f32: negative size M=%d N=%d K=%d", M, N, K);
   if (M == 0 || N == 0) return 0;
+  const int mode = epilogue & RS_GEMM_BF16;  // a compute-mode flag, not an epilogue stage
+  epilogue &= ~RS_GEMM_BF16;
   RS_CHECK_ARG(A && B && C, "rs_gemm_f32: null operand");
   RS_CHECK_ARG(ldc >= N, "rs_gemm_f32: ldc %d < N %d", ldc, N);
   RS_CHECK_ARG(transA ? lda >= M : lda >= K, "rs_gemm_f32: bad lda %d", lda);
@@ -335,7 +337,7 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
   {
     StreamArgs sa{};
     sa.M = M; sa.N = N; sa.K = K; sa.alpha = alpha; sa.beta = beta; sa.A = A; sa.lda = lda;
-    sa.B = B; sa.ldb = ldb; sa.C = C; sa.ldc = ldc; sa.epi = epilogue; sa.bias = bias;
+    sa.B = B; sa.ldb = ldb; sa.C = C; sa.ldc = ldc; sa.epi = epilogue | mode; sa.bias = bias;
     sa.aux = aux; sa.ld_aux = ld_aux; sa.aux_mod = g.aux_mod; sa.rowsum = rowsum; sa.ws = ws;
     sa.transB = transB;
     sa.drop_p = drop_p; sa.drop_key = drop_key; sa.site_a = site_a; sa.site_b = site_b;
@@ -369,7 +371,7 @@ extern "C" int rs_gemm_add_layernorm(int M, int N, int K, const float* A, int ld
                                      int ldw, const float* bias, const float* resid, float* h,
                                      float* y, const float* gamma, const float* beta, float* mean,
                                      float* rstd, float eps, float p, const int64_t* key, int site,
-                                     void* stream) {
+                                     int flags, void* stream) {
   RS_CHECK_ARG(M >= 0 && N >= 1 && K >= 1, "rs_gemm_add_layernorm: bad shape");
   RS_CHECK_ARG(A && W && resid && h && y && gamma && beta && mean && rstd,
                "rs_gemm_add_layernorm: null pointer");
@@ -380,14 +382,16 @@ extern "C" int rs_gemm_add_layernorm(int M, int N, int K, const float* A, int ld
     StreamArgs sa{};
     sa.M = M; sa.N = N; sa.K = K; sa.alpha = 1.f; sa.beta = 0.f; sa.A = A; sa.lda = lda;
     sa.B = W; sa.ldb = ldw; sa.transB = 1; sa.C = h; sa.ldc = N;
-    sa.epi = RS_EPI_AUX_ADD | (bias ? RS_EPI_BIAS : 0) | (p > 0.f ? RS_EPI_DROP_A : 0);
+    sa.epi = RS_EPI_AUX_ADD | (bias ? RS_EPI_BIAS : 0) | (p > 0.f ? RS_EPI_DROP_A : 0) |
+             (flags & RS_GEMM_BF16);
     sa.bias = bias; sa.aux = resid; sa.ld_aux = N; sa.aux_mod = M;
     sa.drop_p = p; sa.drop_key = key; sa.site_a = site;
     sa.ln_gamma = gamma; sa.ln_beta = beta; sa.ln_y = y; sa.ln_mean = mean; sa.ln_rstd = rstd;
     sa.ln_eps = eps;
     return rowgemm_ln_launch(sa, st);
   }
-  RS_RET_IF(rs_gemm_f32(0, 1, M, N, K, 1.f, A, lda, W, ldw, 0.f, h, N, bias ? RS_EPI_BIAS : 0, bias,
+  RS_RET_IF(rs_gemm_f32(0, 1, M, N, K, 1.f, A, lda, W, ldw, 0.f, h, N,
+                        (bias ? RS_EPI_BIAS : 0) | (flags & RS_GEMM_BF16), bias,
                         nullptr, 0, 0, 0.f, nullptr, 0, 0, nullptr, 1, nullptr, stream));
   return rs_add_layernorm_fwd(h, resid, gamma, beta, y, mean, rstd, M, N, eps, p, key, site, stream);
 }

@@ -545,6 +545,148 @@ int wgrad_blocks(int Kr) {
   return nb;
 }
 
+
+// ------------------------------------------------------------------------ rowgemm, bf16 MFMA
+// Same streaming structure as rowgemm (persistent waves, op(B) staged once in LDS, one 16-row
+// group of A per wave step, float4 epilogue via the swapped operand order), computing on
+// v_mfma_f32_16x16x32_bf16: op(B) is rounded to bf16 once while staging, A rows are rounded in
+// registers; products are exact in fp32 and accumulate in fp32. 16x the f32 MFMA rate, so these
+// shapes (K <= 256) become purely HBM-bound. Used when the caller sets RS_GEMM_BF16 (bf16
+// compute mode; SURVEY §8d: C2 is quoted in bf16 with fp32 master weights).
+// k map of a 64-wide chunk c: lane (r, q) holds k = 64c + 16q + (0..15); MFMA 2c uses its first
+// 8, MFMA 2c+1 the next 8 -- the same permutation for both operands, so the sum is unchanged.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ bf16x8 cvt8(const floatx4& lo, const floatx4& hi) {
+  bf16x8 r;
+  r[0] = (__bf16)lo[0]; r[1] = (__bf16)lo[1]; r[2] = (__bf16)lo[2]; r[3] = (__bf16)lo[3];
+  r[4] = (__bf16)hi[0]; r[5] = (__bf16)hi[1]; r[6] = (__bf16)hi[2]; r[7] = (__bf16)hi[3];
+  return r;
+}
+
+template <int NT, int KC, bool LN, int EPI>
+__global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
+  constexpr int KK = KC * 64;
+  constexpr int KPH = KK + 8;  // LDS pitch in bf16 (16-byte pad: conflict-free b128 reads)
+  constexpr int NTN = NT * 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  __bf16* Bs = reinterpret_cast<__bf16*>(smem_raw);
+  float* sbias = reinterpret_cast<float*>(smem_raw + (size_t)NTN * KPH * 2);
+  float* saux = sbias + NTN;  // AUX_ADD table, or LN gamma / beta
+  const int tid = threadIdx.x;
+  if (a.transB) {
+    for (int idx = tid; idx < NTN * KK; idx += 512) {
+      const int n = idx / KK, k = idx % KK;
+      Bs[n * KPH + k] = (__bf16)a.B[(int64_t)n * a.ldb + k];
+    }
+  } else {
+    for (int idx = tid; idx < NTN * KK; idx += 512) {
+      const int k = idx / NTN, n = idx % NTN;
+      Bs[n * KPH + k] = (__bf16)a.B[(int64_t)k * a.ldb + n];
+    }
+  }
+  if constexpr ((EPI & RS_EPI_BIAS) != 0)
+    for (int n = tid; n < NTN; n += 512) sbias[n] = a.bias[n];
+  if constexpr (LN) {
+    for (int n = tid; n < NTN; n += 512) {
+      saux[n] = a.ln_gamma[n];
+      saux[NTN + n] = a.ln_beta[n];
+    }
+  } else if constexpr ((EPI & RS_EPI_AUX_ADD) != 0) {
+    for (int idx = tid; idx < a.aux_mod * NTN; idx += 512) {
+      const int rr = idx / NTN, n = idx % NTN;
+      saux[idx] = a.aux[(int64_t)rr * a.ld_aux + n];
+    }
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int groups = a.M / 16;  // dispatch: M % 16 == 0
+  DropKey ka{}, kb{};
+  if constexpr ((EPI & RS_EPI_DROP_A) != 0) ka = make_key(a.drop_key, a.site_a, a.drop_p);
+  if constexpr ((EPI & RS_EPI_DROP_B) != 0) kb = make_key(a.drop_key, a.site_b, a.drop_p);
+  const int stride = gridDim.x * 8;
+  int g = blockIdx.x * 8 + wave;
+  typedef const __attribute__((address_space(1))) floatx4* gptr4;
+  floatx4 araw[KC][4];
+  auto load_raw = [&](int gg, floatx4 (*dst)[4]) {
+    const float* row = a.A + (int64_t)(gg * 16 + r) * a.lda + 16 * q;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) dst[c][u] = *(gptr4)(row + 64 * c + 4 * u);
+  };
+  if (g < groups) load_raw(g, araw);
+  constexpr bool EPRE = !LN && (EPI & (RS_EPI_AUX_MASK | kEpiBeta)) != 0;
+  for (; g < groups; g += stride) {
+    const int m = g * 16 + r;
+    floatx4 lnres[LN ? NT : 1];
+    floatx4 epre[EPRE ? NT : 1];
+    if constexpr (LN) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) lnres[t] = *(gptr4)(a.aux + (int64_t)m * a.ld_aux + t * 16 + 4 * q);
+    }
+    if constexpr (EPRE) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n0 = t * 16 + 4 * q;
+        if constexpr ((EPI & RS_EPI_AUX_MASK) != 0) epre[t] = *(gptr4)(a.aux + (int64_t)m * a.ld_aux + n0);
+        else epre[t] = *(gptr4)(a.C + (int64_t)m * a.ldc + n0);
+      }
+    }
+    bf16x8 af[KC][2];
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      af[c][0] = cvt8(araw[c][0], araw[c][1]);
+      af[c][1] = cvt8(araw[c][2], araw[c][3]);
+    }
+    load_raw(g + stride < groups ? g + stride : g, araw);  // next group, no branch
+    floatx4 lnacc[LN ? NT : 1];
+    constexpr int TG = NT % 4 == 0 ? 4 : (NT % 2 == 0 ? 2 : 1);
+#pragma unroll
+    for (int j0 = 0; j0 < NT; j0 += TG) {
+      __builtin_amdgcn_sched_barrier(0);
+      floatx4 acc[TG];
+#pragma unroll
+      for (int h = 0; h < TG; ++h) acc[h] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        bf16x8 b[TG][2];
+#pragma unroll
+        for (int h = 0; h < TG; ++h) {
+          const __bf16* bp = Bs + ((j0 + h) * 16 + r) * KPH + 64 * c + 16 * q;
+          b[h][0] = *reinterpret_cast<const bf16x8*>(bp);
+          b[h][1] = *reinterpret_cast<const bf16x8*>(bp + 8);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int h = 0; h < TG; ++h)
+            acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[h][u], af[c][u], acc[h], 0, 0, 0);
+      }
+#pragma unroll
+      for (int h = 0; h < TG; ++h) {
+        if constexpr (LN) {
+          lnacc[j0 + h] = acc[h];
+        } else {
+          const int nl = (j0 + h) * 16 + 4 * q;
+          const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+          floatx4 biasv = z, auxv = z, cv = z;
+          if constexpr ((EPI & RS_EPI_BIAS) != 0) biasv = *reinterpret_cast<const floatx4*>(sbias + nl);
+          if constexpr ((EPI & RS_EPI_AUX_ADD) != 0)
+            auxv = *reinterpret_cast<const floatx4*>(saux + (m % a.aux_mod) * NTN + nl);
+          if constexpr ((EPI & RS_EPI_AUX_MASK) != 0) auxv = epre[j0 + h];
+          if constexpr ((EPI & kEpiBeta) != 0) cv = epre[j0 + h];
+          *reinterpret_cast<floatx4*>(a.C + (int64_t)m * a.ldc + nl) =
+              epi4_ct<EPI>(a, m, nl, acc[h] * a.alpha, ka, kb, biasv, auxv, cv);
+        }
+      }
+    }
+    if constexpr (LN) ln_epilogue<NT, EPI>(a, m, q, lnacc, lnres, ka, sbias, saux, saux + NTN);
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------ dispatch
@@ -583,8 +725,26 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   if (bx > 256 * per_cu) bx = 256 * per_cu;
   if (bx < 1) bx = 1;
   const dim3 blocks(bx, nsplit);
+  // bf16 compute mode: the bf16-MFMA instances (fp32 kernels below for anything else)
+  const int ekey = (s.epi & ~RS_GEMM_BF16) | (s.beta != 0.f ? kEpiBeta : 0);
+  if ((s.epi & RS_GEMM_BF16) && !small && s.vec_epi && s.M % 16 == 0 && s.K % 64 == 0 &&
+      s.N == nt * 16 && s.lda % 4 == 0 && (!(s.epi & RS_EPI_AUX_ADD) || (int64_t)s.aux_mod * nt * 16 * 4 <= 48 * 1024)) {
+    const int kc = s.K / 64;
+    const size_t ldsb = (size_t)nt * 16 * (s.K + 8) * 2 + (size_t)(nt * 16 + ((s.epi & RS_EPI_AUX_ADD) ? s.aux_mod * nt * 16 : 0)) * 4;
+    const int per_cub = ldsb > 80 * 1024 ? 1 : (ldsb > 53 * 1024 ? 2 : (ldsb > 40 * 1024 ? 3 : 4));
+    int bxb = cdiv(s.M / 16, 16);
+    if (bxb > 256 * per_cub) bxb = 256 * per_cub;
+#define RS_RGB(NTV, KCV, EV)                                                                      \
+    if (nt == NTV && kc == KCV && ekey == EV) {                                                   \
+      rowgemm_bf16_kernel<NTV, KCV, false, EV><<<bxb, 512, ldsb, st>>>(s);                        \
+      RS_CHECK_LAUNCH("rowgemm bf16");                                                            \
+      return 0;                                                                                   \
+    }
+    RS_RGB(16, 1, 19) RS_RGB(16, 1, 3) RS_RGB(16, 1, 8) RS_RGB(16, 1, 0) RS_RGB(12, 1, 1)
+    RS_RGB(4, 3, 64) RS_RGB(4, 4, 64) RS_RGB(4, 1, 0) RS_RGB(4, 1, 64) RS_RGB(4, 4, 0) RS_RGB(4, 3, 0)
+#undef RS_RGB
+  }
   // specialised (compile-time epilogue) instances for the encoder's GEMMs
-  const int ekey = s.epi | (s.beta != 0.f ? kEpiBeta : 0);
   const bool aux_small = !(s.epi & RS_EPI_AUX_ADD) || (int64_t)s.aux_mod * nt * 16 * 4 <= 48 * 1024;
   if (!small && rg == 1 && s.vec_epi && s.N % (nt * 16) == 0 && aux_small && s.M % 16 == 0 &&
       s.K == kt * 16 &&
@@ -639,6 +799,17 @@ int rowgemm_ln_launch(const StreamArgs& s, hipStream_t st) {
   const int per_cu = lds > 80 * 1024 ? 1 : (lds > 53 * 1024 ? 2 : (lds > 40 * 1024 ? 3 : 4));
   if (bx > 256 * per_cu) bx = 256 * per_cu;
   const int ekey = s.epi & (RS_EPI_BIAS | RS_EPI_DROP_A);
+  if ((s.epi & RS_GEMM_BF16) && s.M % 16 == 0 && s.K % 64 == 0 && s.lda % 4 == 0) {
+    const int kc = s.K / 64;
+    const size_t ldsb = (size_t)64 * (s.K + 8) * 2 + (size_t)3 * 64 * 4;
+    const int per_cub = ldsb > 80 * 1024 ? 1 : (ldsb > 53 * 1024 ? 2 : (ldsb > 40 * 1024 ? 3 : 4));
+    int bxb = cdiv(s.M / 16, 16);
+    if (bxb > 256 * per_cub) bxb = 256 * per_cub;
+#define RS_LNB(KCV, EV) \
+  if (kc == KCV && ekey == EV) { rowgemm_bf16_kernel<4, KCV, true, EV><<<bxb, 512, ldsb, st>>>(s); RS_CHECK_LAUNCH("rowgemm_ln bf16"); return 0; }
+    RS_LNB(1, 0) RS_LNB(1, 1) RS_LNB(1, 16) RS_LNB(1, 17) RS_LNB(4, 0) RS_LNB(4, 1) RS_LNB(4, 16) RS_LNB(4, 17)
+#undef RS_LNB
+  }
   if (s.M % 16 != 0 || s.K != kt * 16) {  // guarded generic instances
     if (kt == 4) rowgemm_kernel<4, 4, true><<<bx, 512, lds, st>>>(s);
     else rowgemm_kernel<4, 16, true><<<bx, 512, lds, st>>>(s);

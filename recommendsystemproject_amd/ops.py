@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _hip
+from . import _hip, precision
 from ._hip import call
 
 _ZERO = {}
@@ -36,7 +36,8 @@ def gemm(A, B, C, M, N, K, *, transA, transB, lda, ldb, ldc, alpha=1.0, beta=0.0
     if split > 1:
         w = ws(L.rs_gemm_ws_bytes(M, N, K, split), C.device)
     call('rs_gemm_f32', int(transA), int(transB), M, N, K, float(alpha), P(A), lda, P(B), ldb,
-         float(beta), P(C), ldc, epi, P(bias), P(aux), ld_aux, aux_mod, float(drop_p), P(drop_key),
+         float(beta), P(C), ldc, epi | precision.gemm_flags(), P(bias), P(aux), ld_aux, aux_mod,
+         float(drop_p), P(drop_key),
          site_a, site_b, P(rowsum), split, P(w), stream())
     return C
 
@@ -141,7 +142,8 @@ def linear_add_layernorm(x, W, bias, resid, gamma, beta, eps=1e-5, p=0.0, key=No
     mean = torch.empty(M, device=dev, dtype=torch.float32)
     rstd = torch.empty(M, device=dev, dtype=torch.float32)
     call('rs_gemm_add_layernorm', M, N, K, P(x), x.stride(0), P(W), W.stride(0), P(bias), P(resid),
-         P(h), P(y), P(gamma), P(beta), P(mean), P(rstd), float(eps), float(p), P(key), site, stream())
+         P(h), P(y), P(gamma), P(beta), P(mean), P(rstd), float(eps), float(p), P(key), site,
+         precision.gemm_flags(), stream())
     return h, y, mean, rstd
 
 
