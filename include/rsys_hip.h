@@ -185,16 +185,32 @@ int rs_l2norm_bwd(const float* y, const float* norm, const float* dy, float* dx,
  * item_ids may be NULL (compute_loss(item_ids=None): no collision mask).
  * TwoTowerModel.compute_loss (TwoTowerModel.py:81-140; trap T12; K15-K17).
  * fwd: per-row lse [B] and the mean loss (scalar) ; bwd: S <- dlogits (in place, scaled by
- * *grad_out / B / T so the next GEMMs need alpha 1), dhl [B, N] likewise. */
+ * *grad_out / B / T so the next GEMMs need alpha 1), dhl [B, N] likewise.
+ * Hard negatives: element (i, n, c) of H at Hn[i*h_row_stride + n*h_slot_stride + c] (0, 0 =
+ * contiguous [B, N, D]; the grouped item-tower pass hands over [N, B, D] as row D, slot B*D). */
 int rs_inbatch_ce_fwd(const float* S, int ld_s, const float* U, const float* Hn,
+                      int64_t h_row_stride, int64_t h_slot_stride,
                       const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T,
                       float* lse, float* row_loss, float* loss, void* stream);
 int rs_inbatch_ce_bwd(float* S, int ld_s, const float* U, const float* Hn,
+                      int64_t h_row_stride, int64_t h_slot_stride,
                       const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T,
                       const float* lse, const float* grad_out, float* dhl, void* stream);
-/* dU[i] += sum_n dhl[i,n] H[i,n];  dH[i,n] = dhl[i,n] U[i]   (hard-negative bmm backward) */
-int rs_hardneg_bwd(const float* U, const float* Hn, const float* dhl, float* dU, float* dH,
-                   int B, int N, int D, void* stream);
+/* dU[i] += sum_n dhl[i,n] H[i,n];  dH[i,n] = dhl[i,n] U[i]   (hard-negative bmm backward; dH in
+ * the layout of H) */
+int rs_hardneg_bwd(const float* U, const float* Hn, int64_t h_row_stride, int64_t h_slot_stride,
+                   const float* dhl, float* dU, float* dH, int B, int N, int D, void* stream);
+
+/* ---------------------------------------------------------------- hard-negative catalog
+ * Materialise N item-tower feature rows per sample from an on-device item catalog (SURVEY §8f.2;
+ * the reference leaves `hard_negatives` as a TODO in CombineTwoTower.py:86-90 and samples the
+ * ids in parsing.py:215-250): out[(n*B + b)*ld_out + f] = cat[ids[b*ld_ids + n]*ld_cat + f] for
+ * f < F, i.e. the N slots stacked along the batch ([N*B, F], one grouped tower pass). elem = 4
+ * or 8 bytes (copied as is); widen = 1 reads int32 and writes int64 (id columns). An id outside
+ * [0, V) writes zeros (the padding row) and sets *err_flag |= 1. */
+int rs_catalog_gather(const void* cat, int elem, int widen, int64_t V, int F, int64_t ld_cat,
+                      const int64_t* ids, int B, int N, int64_t ld_ids, void* out, int64_t ld_out,
+                      int* err_flag, void* stream);
 
 /* ---------------------------------------------------------------- clip + Adam
  * Flat multi-tensor path over a contiguous fp32 range (all parameters packed in one buffer).

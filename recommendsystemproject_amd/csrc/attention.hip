@@ -201,6 +201,16 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const float* __restrict__
 // 4-step k chain consumes component s (k = 4q + s), the permuted-k order used by rowgemm.
 typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+// LDS row pitch of the per-wave [L][16] tiles: lanes (c, q) read rows 4q + s, so a pitch of 20
+// words puts the four q groups on disjoint bank quarters (16 words would be a 4-way conflict)
+constexpr int kRowP = 20;
+
+// dropout index ((b*H + h)*L + i)*L + j in 32 bits (the host checks B*H*L*L < 2^32): the same
+// draw as keep_mult on the 64-bit index, without 64-bit multiplies per probability
+__device__ __forceinline__ float keep_mult32(const DropKey& k, uint32_t idx) {
+  const uint32_t h = fmix32(fmix32(idx ^ k.k0) + k.k1);
+  return h >= k.thresh ? k.scale : 0.f;
+}
 
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
@@ -222,7 +232,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(
     float* __restrict__ lse, int B, int L, int d, int H, float scale, float pdrop,
     const int64_t* __restrict__ key, int site) {
   constexpr int LP = NT * 16;
-  __shared__ __attribute__((aligned(16))) float Vsm[4][LP][16];
+  __shared__ __attribute__((aligned(16))) float Vsm[4][LP][kRowP];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
   const int bh = blockIdx.x * 4 + wave;
@@ -230,7 +240,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(
   const int b = bh / H, h = bh % H;
   const int ld = 3 * d;
   const float* base = qkv + (int64_t)b * L * ld + h * 16;
-  float(*Vs)[16] = Vsm[wave];
+  float(*Vs)[kRowP] = Vsm[wave];
   f4 qf[NT], kf[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -275,13 +285,14 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(
     m = xmax(m);
     float l = 0.f;
     const int i = tq * 16 + r;
+    const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float pv = kok[tk][e] ? exp2f(sv[tk][e] * scale2 - m) : 0.f;
         l += pv;
-        sv[tk][e] = DROP ? pv * keep_mult(dk, ((uint64_t)bh * L + i) * L + tk * 16 + 4 * q + e) : pv;
+        sv[tk][e] = DROP ? pv * keep_mult32(dk, rowbase + tk * 16 + 4 * q + e) : pv;
       }
     l = xsum(l);
     // O[i][c] = sum_j pz[i][j] V[j][c]: A = this lane's probabilities (row i = lane & 15,
@@ -310,9 +321,9 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(
     const int64_t* __restrict__ key, int site) {
   constexpr int LP = NT * 16;
   constexpr int TP = 20;  // transpose buffer [LP keys][16 queries of the current tile], pitch 20
-  __shared__ __attribute__((aligned(16))) float Qsm[4][LP][16];
-  __shared__ __attribute__((aligned(16))) float Ksm[4][LP][16];
-  __shared__ __attribute__((aligned(16))) float Gsm[4][LP][16];
+  __shared__ __attribute__((aligned(16))) float Qsm[4][LP][kRowP];
+  __shared__ __attribute__((aligned(16))) float Ksm[4][LP][kRowP];
+  __shared__ __attribute__((aligned(16))) float Gsm[4][LP][kRowP];
   __shared__ __attribute__((aligned(16))) float Tsm[4][LP * TP];  // 5 KB per wave
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
@@ -323,9 +334,9 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(
   const float* base = qkv + (int64_t)b * L * ld + h * 16;
   const float* gbase = dout + (int64_t)b * L * d + h * 16;
   const float* obase = out + (int64_t)b * L * d + h * 16;
-  float(*Qs)[16] = Qsm[wave];
-  float(*Ks)[16] = Ksm[wave];
-  float(*Gs)[16] = Gsm[wave];
+  float(*Qs)[kRowP] = Qsm[wave];
+  float(*Ks)[kRowP] = Ksm[wave];
+  float(*Gs)[kRowP] = Gsm[wave];
   float* T = Tsm[wave];
   f4 qf[NT], kf[NT], vf[NT], gf[NT];
   float Di[NT], lsei[NT];
@@ -366,6 +377,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(
 #pragma unroll
   for (int tq = 0; tq < NT; ++tq) {
     const int i = tq * 16 + r;
+    const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
     f4 ps[NT], ds[NT];
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk) {
@@ -378,7 +390,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float pv = (kok[tk][e] && i < L) ? exp2f(sacc[e] * scale2 - lsei[tq]) : 0.f;
-        const float z = DROP ? keep_mult(dk, ((uint64_t)bh * L + i) * L + tk * 16 + 4 * q + e) : 1.f;
+        const float z = DROP ? keep_mult32(dk, rowbase + tk * 16 + 4 * q + e) : 1.f;
         ds[tk][e] = pv * (z * pacc[e] - Di[tq]);
         ps[tk][e] = pv * z;
       }
@@ -470,7 +482,7 @@ extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out,
   RS_CHECK_ARG(lds <= 64 * 1024, "rs_attn_fwd: L=%d hd=%d exceeds LDS", L, hd);
   RS_CHECK_ARG(d % 4 == 0 && aligned16(qkv) && aligned16(out), "rs_attn_fwd: needs 16-byte aligned rows");
   hipStream_t st = as_stream(stream);
-  if (hd == 16 && L <= 64 && !getenv_flag("RSYS_ATTN_VALU")) {
+  if (hd == 16 && L <= 64 && (int64_t)B * H * L * L < ((int64_t)1 << 32) && !getenv_flag("RSYS_ATTN_VALU")) {
     const int nt = (L + 15) / 16;
     const dim3 g4(cdiv((int64_t)B * H, 4));
 #define RS_AF(NTV)                                                                                  \
@@ -504,7 +516,7 @@ extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float
   RS_CHECK_ARG(lds <= 64 * 1024, "rs_attn_bwd: L=%d hd=%d exceeds LDS", L, hd);
   RS_CHECK_ARG(d % 4 == 0 && aligned16(qkv) && aligned16(dout), "rs_attn_bwd: needs 16-byte aligned rows");
   hipStream_t st = as_stream(stream);
-  if (hd == 16 && L <= 64 && !getenv_flag("RSYS_ATTN_VALU")) {
+  if (hd == 16 && L <= 64 && (int64_t)B * H * L * L < ((int64_t)1 << 32) && !getenv_flag("RSYS_ATTN_VALU")) {
     RS_CHECK_ARG(aligned16(out), "rs_attn_bwd: needs 16-byte aligned rows");
     const int nt = (L + 15) / 16;
     const dim3 g4(cdiv((int64_t)B * H, 4));

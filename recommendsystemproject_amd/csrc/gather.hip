@@ -447,3 +447,53 @@ extern "C" int rs_seq_mask(const int64_t* seq, int64_t ld_seq, int B, int L, int
   RS_CHECK_LAUNCH("rs_seq_mask");
   return 0;
 }
+
+// ---------------------------------------------------------------- hard-negative catalog gather
+namespace rs {
+namespace {
+template <typename TI, typename TO>
+__global__ void catalog_gather_kernel(const TI* __restrict__ cat, int64_t V, int F, int64_t ld_cat,
+                                      const int64_t* __restrict__ ids, int B, int N,
+                                      int64_t ld_ids, TO* __restrict__ out, int64_t ld_out,
+                                      int* err) {
+  const int64_t total = (int64_t)N * B * F;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = e / F;  // n*B + b
+    const int f = (int)(e - row * F);
+    const int n = (int)(row / B), b = (int)(row - (int64_t)n * B);
+    const int64_t id = ids[(int64_t)b * ld_ids + n];
+    TO v = 0;
+    if (id >= 0 && id < V) v = (TO)cat[id * ld_cat + f];
+    else if (err && f == 0) atomicOr(err, 1);
+    out[row * ld_out + f] = v;
+  }
+}
+}  // namespace
+}  // namespace rs
+
+extern "C" int rs_catalog_gather(const void* cat, int elem, int widen, int64_t V, int F,
+                                 int64_t ld_cat, const int64_t* ids, int B, int N, int64_t ld_ids,
+                                 void* out, int64_t ld_out, int* err_flag, void* stream) {
+  RS_CHECK_ARG(cat && ids && out && V >= 1 && F >= 1 && B >= 0 && N >= 0 && ld_cat >= F &&
+                   ld_out >= F && ld_ids >= N,
+               "rs_catalog_gather: bad args");
+  RS_CHECK_ARG(elem == 4 || elem == 8, "rs_catalog_gather: elem must be 4 or 8 bytes");
+  RS_CHECK_ARG(!widen || elem == 4, "rs_catalog_gather: widen needs int32 input");
+  const int64_t total = (int64_t)N * B * F;
+  if (total == 0) return 0;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipStream_t st = as_stream(stream);
+  if (widen)
+    catalog_gather_kernel<int32_t, int64_t><<<blocks, 256, 0, st>>>(
+        static_cast<const int32_t*>(cat), V, F, ld_cat, ids, B, N, ld_ids, static_cast<int64_t*>(out), ld_out, err_flag);
+  else if (elem == 8)
+    catalog_gather_kernel<int64_t, int64_t><<<blocks, 256, 0, st>>>(
+        static_cast<const int64_t*>(cat), V, F, ld_cat, ids, B, N, ld_ids, static_cast<int64_t*>(out), ld_out, err_flag);
+  else
+    catalog_gather_kernel<uint32_t, uint32_t><<<blocks, 256, 0, st>>>(
+        static_cast<const uint32_t*>(cat), V, F, ld_cat, ids, B, N, ld_ids, static_cast<uint32_t*>(out), ld_out, err_flag);
+  RS_CHECK_LAUNCH("rs_catalog_gather");
+  return 0;
+}

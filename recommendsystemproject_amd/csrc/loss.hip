@@ -27,17 +27,25 @@ __device__ __forceinline__ float logit_at(const float* Srow, const int64_t* ids,
   return Srow[j] / T;
 }
 
-// hard-negative logit n of row i: dot(U_i, H_in) / T computed by one wave
-__device__ float hard_logit(const float* U, const float* Hn, int i, int n, int N, int D, float T) {
+// hard-negative logit n of row i: dot(U_i, H[i, n]) / T computed by one wave; H element
+// (i, n, c) at Hn[i*hs.row + n*hs.slot + c] ([B, N, D] contiguous, or the [N, B, D] output of one
+// grouped item-tower pass viewed as [B, N, D])
+struct HStride {
+  int64_t row, slot;
+};
+
+__device__ float hard_logit(const float* U, const float* Hn, HStride hs, int i, int n, int D,
+                            float T) {
   const int lane = threadIdx.x & 63;
+  const float* h = Hn + (int64_t)i * hs.row + (int64_t)n * hs.slot;
   float s = 0.f;
-  for (int c = lane; c < D; c += 64) s += U[(int64_t)i * D + c] * Hn[((int64_t)i * N + n) * D + c];
+  for (int c = lane; c < D; c += 64) s += U[(int64_t)i * D + c] * h[c];
   return wave_sum(s) / T;
 }
 
 __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ S, int ld,
                                                      const float* __restrict__ U,
-                                                     const float* __restrict__ Hn,
+                                                     const float* __restrict__ Hn, HStride hs,
                                                      const int64_t* __restrict__ ids, int64_t st,
                                                      int B, int N, int D, float T,
                                                      float* __restrict__ lse,
@@ -49,7 +57,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ S
   const int64_t idi = ids ? ids[(int64_t)i * st] : 0;
   const int wave = threadIdx.x >> 6;
   for (int n = wave; n < N; n += 4) {
-    const float v = hard_logit(U, Hn, i, n, N, D, T);
+    const float v = hard_logit(U, Hn, hs, i, n, D, T);
     if ((threadIdx.x & 63) == 0) hl[n] = v;
   }
   __syncthreads();
@@ -70,7 +78,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ S
 
 __global__ __launch_bounds__(256) void ce_bwd_kernel(float* __restrict__ S, int ld,
                                                      const float* __restrict__ U,
-                                                     const float* __restrict__ Hn,
+                                                     const float* __restrict__ Hn, HStride hs,
                                                      const int64_t* __restrict__ ids, int64_t st,
                                                      int B, int N, int D, float T,
                                                      const float* __restrict__ lse,
@@ -87,14 +95,16 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(float* __restrict__ S, int 
   }
   const int wave = threadIdx.x >> 6;
   for (int n = wave; n < N; n += 4) {
-    const float v = hard_logit(U, Hn, i, n, N, D, T);
+    const float v = hard_logit(U, Hn, hs, i, n, D, T);
     if ((threadIdx.x & 63) == 0) dhl[(int64_t)i * N + n] = g * expf(v - l);
   }
 }
 
+// dU += sum_n dhl[i,n] H[i,n,:]; dH[i,n,:] = dhl[i,n] U[i,:] (dH in the layout of H)
 __global__ void hardneg_bwd_kernel(const float* __restrict__ U, const float* __restrict__ Hn,
-                                   const float* __restrict__ dhl, float* __restrict__ dU,
-                                   float* __restrict__ dH, int B, int N, int D) {
+                                   HStride hs, const float* __restrict__ dhl,
+                                   float* __restrict__ dU, float* __restrict__ dH, int B, int N,
+                                   int D) {
   const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (idx >= (int64_t)B * D) return;
   const int i = (int)(idx / D), c = (int)(idx % D);
@@ -102,8 +112,9 @@ __global__ void hardneg_bwd_kernel(const float* __restrict__ U, const float* __r
   float acc = 0.f;
   for (int n = 0; n < N; ++n) {
     const float w = dhl[(int64_t)i * N + n];
-    acc += w * Hn[((int64_t)i * N + n) * D + c];
-    dH[((int64_t)i * N + n) * D + c] = w * u;
+    const int64_t o = (int64_t)i * hs.row + (int64_t)n * hs.slot + c;
+    acc += w * Hn[o];
+    dH[o] = w * u;
   }
   dU[idx] += acc;
 }
@@ -114,36 +125,42 @@ __global__ void hardneg_bwd_kernel(const float* __restrict__ U, const float* __r
 using namespace rs;
 
 extern "C" int rs_inbatch_ce_fwd(const float* S, int ld_s, const float* U, const float* Hn,
+                                 int64_t h_row_stride, int64_t h_slot_stride,
                                  const int64_t* item_ids, int64_t id_stride, int B, int N, int D,
                                  float T, float* lse, float* row_loss, float* loss, void* stream) {
   RS_CHECK_ARG(S && lse && row_loss && loss, "rs_inbatch_ce_fwd: null pointer");
   RS_CHECK_ARG(B >= 1 && ld_s >= B && N >= 0 && N <= 64, "rs_inbatch_ce_fwd: bad shape B=%d N=%d", B, N);
   RS_CHECK_ARG(N == 0 || (U && Hn && D >= 1), "rs_inbatch_ce_fwd: hard negatives need U, H, D");
   hipStream_t st = as_stream(stream);
-  ce_fwd_kernel<<<B, 256, 0, st>>>(S, ld_s, U, Hn, item_ids, id_stride, B, N, D, T, lse, row_loss);
+  const HStride hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
+  ce_fwd_kernel<<<B, 256, 0, st>>>(S, ld_s, U, Hn, hs, item_ids, id_stride, B, N, D, T, lse, row_loss);
   RS_CHECK_LAUNCH("rs_inbatch_ce_fwd");
   return rs_sum(row_loss, B, 1.f / (float)B, loss, stream);
 }
 
 extern "C" int rs_inbatch_ce_bwd(float* S, int ld_s, const float* U, const float* Hn,
+                                 int64_t h_row_stride, int64_t h_slot_stride,
                                  const int64_t* item_ids, int64_t id_stride, int B, int N, int D,
                                  float T, const float* lse, const float* grad_out, float* dhl,
                                  void* stream) {
   RS_CHECK_ARG(S && lse, "rs_inbatch_ce_bwd: null pointer");
   RS_CHECK_ARG(B >= 1 && ld_s >= B && N >= 0 && N <= 64, "rs_inbatch_ce_bwd: bad shape");
   RS_CHECK_ARG(N == 0 || (U && Hn && dhl && D >= 1), "rs_inbatch_ce_bwd: hard negatives need U, H, dhl");
-  ce_bwd_kernel<<<B, 256, 0, as_stream(stream)>>>(S, ld_s, U, Hn, item_ids, id_stride, B, N, D, T,
+  const HStride hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
+  ce_bwd_kernel<<<B, 256, 0, as_stream(stream)>>>(S, ld_s, U, Hn, hs, item_ids, id_stride, B, N, D, T,
                                                   lse, grad_out, dhl);
   RS_CHECK_LAUNCH("rs_inbatch_ce_bwd");
   return 0;
 }
 
-extern "C" int rs_hardneg_bwd(const float* U, const float* Hn, const float* dhl, float* dU,
-                              float* dH, int B, int N, int D, void* stream) {
+extern "C" int rs_hardneg_bwd(const float* U, const float* Hn, int64_t h_row_stride,
+                              int64_t h_slot_stride, const float* dhl, float* dU, float* dH, int B,
+                              int N, int D, void* stream) {
   RS_CHECK_ARG(U && Hn && dhl && dU && dH && B >= 0 && N >= 1 && D >= 1, "rs_hardneg_bwd: bad args");
   const int64_t total = (int64_t)B * D;
   if (total == 0) return 0;
-  hardneg_bwd_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(U, Hn, dhl, dU, dH, B, N, D);
+  const HStride hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
+  hardneg_bwd_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(U, Hn, hs, dhl, dU, dH, B, N, D);
   RS_CHECK_LAUNCH("rs_hardneg_bwd");
   return 0;
 }

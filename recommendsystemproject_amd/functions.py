@@ -456,9 +456,13 @@ class InBatchLossFn(torch.autograd.Function):
         ops.gemm(U, I, S, B, B, D, transA=0, transB=1, lda=D, ldb=D, ldc=B)
         N = 0
         Hc = None
+        hsr = hss = 0
         if H is not None:
-            Hc = H.contiguous()
+            # [B, N, D] with unit column stride: contiguous, or the permuted [N, B, D] output of
+            # one grouped item-tower pass (no copy either way)
+            Hc = H if H.stride(2) == 1 else H.contiguous()
             N = int(Hc.shape[1])
+            hsr, hss = int(Hc.stride(0)), int(Hc.stride(1))
         ids = None
         st = 0
         if item_ids is not None:
@@ -469,10 +473,12 @@ class InBatchLossFn(torch.autograd.Function):
         lse = torch.empty(B, device=dev, dtype=torch.float32)
         row_loss = torch.empty(B, device=dev, dtype=torch.float32)
         loss = torch.empty((), device=dev, dtype=torch.float32)
-        _hip.call('rs_inbatch_ce_fwd', S.data_ptr(), B, U.data_ptr(), ops.P(Hc), ops.P(ids), st, B, N, D,
-                  float(temperature), lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(), ops.stream())
+        _hip.call('rs_inbatch_ce_fwd', S.data_ptr(), B, U.data_ptr(), ops.P(Hc), hsr, hss, ops.P(ids), st,
+                  B, N, D, float(temperature), lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(),
+                  ops.stream())
         ctx.save_for_backward(U, I, Hc if Hc is not None else U)
         ctx.S, ctx.ids, ctx.st, ctx.N, ctx.T, ctx.lse = S, ids, st, N, float(temperature), lse
+        ctx.hs = (hsr, hss)
         return loss
 
     @staticmethod
@@ -485,16 +491,16 @@ class InBatchLossFn(torch.autograd.Function):
         gout = gout.contiguous()
         dhl = torch.empty(B, max(N, 1), device=U.device, dtype=torch.float32) if N else None
         _hip.call('rs_inbatch_ce_bwd', S.data_ptr(), B, U.data_ptr(), ops.P(Hc) if N else None,
-                  ops.P(ctx.ids), ctx.st, B, N, D, ctx.T, ctx.lse.data_ptr(), gout.data_ptr(),
-                  ops.P(dhl), ops.stream())
+                  ctx.hs[0], ctx.hs[1], ops.P(ctx.ids), ctx.st, B, N, D, ctx.T, ctx.lse.data_ptr(),
+                  gout.data_ptr(), ops.P(dhl), ops.stream())
         dU = torch.empty_like(U)
         ops.gemm(S, I, dU, B, D, B, transA=0, transB=0, lda=B, ldb=D, ldc=D)       # dS @ I
         dI = torch.empty_like(I)
         ops.gemm(S, U, dI, B, D, B, transA=1, transB=0, lda=B, ldb=D, ldc=D)       # dS^T @ U
         dH = None
         if N:
-            dH = torch.empty_like(Hc)
-            _hip.call('rs_hardneg_bwd', U.data_ptr(), Hc.data_ptr(), dhl.data_ptr(), dU.data_ptr(),
-                      dH.data_ptr(), B, N, D, ops.stream())
+            dH = torch.empty_strided(Hc.shape, Hc.stride(), device=Hc.device, dtype=Hc.dtype)
+            _hip.call('rs_hardneg_bwd', U.data_ptr(), Hc.data_ptr(), ctx.hs[0], ctx.hs[1], dhl.data_ptr(),
+                      dU.data_ptr(), dH.data_ptr(), B, N, D, ops.stream())
         ctx.S = None
         return dU, dI, None, dH, None

@@ -78,9 +78,11 @@ class GenericTower(nn.Module):
                              output_dim=output_dims, dropout=dropout_cfg)
         self.register_buffer('err_flag', torch.zeros(1, dtype=torch.int32), persistent=False)
 
-    def forward(self, input_dict, feature_column_mapping=None):
+    def forward(self, input_dict, feature_column_mapping=None, groups=1):
         """input_dict {'sparse': [B,S] long, 'dense': [B,Dn] float, 'sequence': {...}} ->
-        L2-normalised [B, output_dims] (GenericTower.py:120-237)."""
+        L2-normalised [B, output_dims] (GenericTower.py:120-237). `groups` > 1: the batch is G
+        blocks of B/G rows (e.g. the N hard-negative slots stacked) and every BatchNorm keeps
+        per-block statistics -- identical to G separate passes (T13), in one pass."""
         _hip.require_device(self.feature_bn.weight)
         ensure_flat(self)
         need = torch.is_grad_enabled()
@@ -91,8 +93,9 @@ class GenericTower(nn.Module):
                 seq_vec = self.seq_encoder(seqd)
         x = TowerFeatureFn.apply(need, self, input_dict, feature_column_mapping, seq_vec,
                                  *self.embeddings.parameters())
-        x = BatchNormFn.apply(need, self.feature_bn, x, 1, self.feature_bn.weight, self.feature_bn.bias)
-        return self.mlp(x)
+        x = BatchNormFn.apply(need, self.feature_bn, x, int(groups), self.feature_bn.weight,
+                              self.feature_bn.bias)
+        return self.mlp(x, groups=int(groups))
 
     def check_errors(self):
         """Raise IndexError if any id was outside its table since the last check (the reference

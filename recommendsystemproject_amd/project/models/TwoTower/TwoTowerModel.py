@@ -35,9 +35,19 @@ class TwoTowerModel(nn.Module):
         user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
         item_emb = self.item_tower(batch_data['item_tower'], self.item_feature_mapping)
         hard_neg_emb = None
-        if 'hard_negatives' in batch_data and batch_data['hard_negatives']:
-            hard_neg_emb = torch.stack([self.item_tower(neg, self.item_feature_mapping)
-                                        for neg in batch_data['hard_negatives']], dim=1)
+        negs = batch_data.get('hard_negatives') if isinstance(batch_data, dict) else None
+        if negs:
+            stacked = getattr(negs, 'stacked', None)
+            if stacked is not None:
+                # materialised by ItemCatalog: the N slots are already one [N*B] batch; one item-tower
+                # pass with per-slot BatchNorm statistics == N separate passes (T13)
+                N = len(negs)
+                out = self.item_tower(stacked, self.item_feature_mapping, groups=N)
+                B = out.shape[0] // N
+                hard_neg_emb = out.view(N, B, out.shape[1]).transpose(0, 1)  # [B, N, D] view
+            else:
+                hard_neg_emb = torch.stack([self.item_tower(neg, self.item_feature_mapping)
+                                            for neg in negs], dim=1)
         return user_emb, item_emb, hard_neg_emb
 
     def predict(self, batch_data):
