@@ -39,6 +39,12 @@ PEAK_F32_TFLOPS = 157.3   # MI355X f32 (vector = f32-input MFMA) peak, MI355X_MI
 PEAK_HBM_GBS = 8000.0     # HBM3E spec
 
 
+WORKLOADS = {
+    'c3': 'synthetic 10M-item vocab DSSM (emb 128, pooled 50-long history, lazy-exact Adam tables)',
+    'c5': 'synthetic 100M-item vocab DSSM (emb 64, lazy-exact Adam tables)',
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -50,6 +56,9 @@ def parse():
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'],
                     help='compute dtype of the encoder GEMMs (bf16: bf16 MFMA, fp32 accumulate / master weights)')
+    ap.add_argument('--hard-negatives', type=int, default=0,
+                    help='N sampled hard negatives per row, materialised from a device item catalog '
+                         'each step (one grouped item-tower pass)')
     ap.add_argument('--zipf', type=float, default=None, help='Zipf(alpha) ids instead of uniform (C3 variant)')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -111,8 +120,15 @@ def main():
             'item': synth.tower_layout(cfg['two_tower']['item_tower'])}
 
     torch.manual_seed(0)
-    model = TwoTowerModel(GenericTower(cfg, 'user_tower'), GenericTower(cfg, 'item_tower'),
-                          maps['user'], maps['item']).to(dev)
+    big = max(int(f.get('vocab_size', 0)) for t in cfg['two_tower'].values()
+              for f in (t.get('sparse_features') or []) + (t.get('sequence_features') or [])) >= 10 ** 7
+    if big:  # 10M-100M-row tables: initialise on the device (CPU init of 25 GB tables takes minutes)
+        with torch.device(dev):
+            model = TwoTowerModel(GenericTower(cfg, 'user_tower'), GenericTower(cfg, 'item_tower'),
+                                  maps['user'], maps['item'])
+    else:
+        model = TwoTowerModel(GenericTower(cfg, 'user_tower'), GenericTower(cfg, 'item_tower'),
+                              maps['user'], maps['item']).to(dev)
     model.train()
     ensure_flat(model)
     rdist.broadcast_model(model)
@@ -120,9 +136,27 @@ def main():
     opt.grad_scale = 1.0 / world
     batch = synth.batch_to_torch(synth.make_batch(cfg, B, seed=1000 + rank), dev)  # resident in HBM
     ids = extract_item_id(batch['item_tower'])
+    catalog = neg_ids = None
+    if args.hard_negatives:
+        # synthetic item catalog (id column = row, other features random) and uniformly sampled
+        # negative ids, resident; the N item-tower dicts are materialised inside every step
+        from recommendsystemproject_amd.project.utils.hard_negatives import ItemCatalog
+        item_cfg = cfg['two_tower']['item_tower']
+        V = int(item_cfg['sparse_features'][0]['vocab_size'])
+        g = torch.Generator(device=dev).manual_seed(7 + rank)
+        cols = [f for f in item_cfg['sparse_features'] if 'pooling' not in f]
+        sparse = torch.stack([torch.arange(V, device=dev, dtype=torch.int32) if i == 0 else
+                              torch.randint(1, int(f['vocab_size']), (V,), device=dev, generator=g, dtype=torch.int32)
+                              for i, f in enumerate(cols)], 1)
+        seqc = {f['name']: torch.randint(0, int(f['vocab_size']), (V, 3), device=dev, generator=g, dtype=torch.int32)
+                for f in item_cfg['sparse_features'] if 'pooling' in f}
+        catalog = ItemCatalog(sparse=sparse, sequence=seqc, device=dev)
+        neg_ids = torch.randint(1, V, (B, args.hard_negatives), device=dev, generator=g)
 
     def fwd_bwd():
         opt.zero_grad()
+        if catalog is not None:
+            batch['hard_negatives'] = catalog.materialize(neg_ids)
         U, I, H = model(batch)
         loss = model.compute_loss(U, I, item_ids=ids, hard_neg_emb=H, temperature=T)
         loss.backward()
@@ -243,13 +277,14 @@ def main():
             'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 3),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
             'data': 'synthetic (MovieLens-1M-shaped ids, seeded numpy PCG64, resident in HBM)',
-            'config': {'workload': f'{args.config}: ' + ('synthetic 10M-item vocab DSSM (emb 128, pooled 50-long history, lazy-exact Adam tables)' if args.config == 'c3' else 'MovieLens-1M DSSM') +
+            'config': {'workload': f'{args.config}: ' + WORKLOADS.get(args.config, 'MovieLens-1M DSSM') +
                        (f' + Transformer seq encoder (seq_len {tp.get("max_seq_len")}, d={cfg["two_tower"]["user_tower"]["embedding_dim"]})' if has_seq else ''),
                        'global_batch': world * B, 'per_gpu_batch': B,
                        'seq_len': tp.get('max_seq_len') if has_seq else None,
                        'dropout': args.dropout, 'parallelism': f'dp{world}',
                        'hip_graph': graphs is not None, 'final_loss': round(final_loss, 5),
-                       'ids': f'zipf({args.zipf})' if args.zipf else 'uniform'},
+                       'ids': f'zipf({args.zipf})' if args.zipf else 'uniform',
+                       'hard_negatives': args.hard_negatives},
             'roofline': roof,
             'gather_roofline': gather_roof,
             'step_roofline': step_roof,

@@ -278,7 +278,8 @@ extern "C" int rs_gemm_auto_split(int M, int N, int K) {
   const int BMt = M >= 2048 ? 128 : 64, BNt = N > 64 ? 128 : 64;
   int64_t tiles = (int64_t)cdiv(M, BMt) * cdiv(N, BNt);
   if (tiles >= 256 || K < 1024) return 1;
-  if (K >= 2048 && (int64_t)M * N <= 16384) return 2;  // wgrad path: needs a workspace only
+  // weight-gradient streaming kernel (gemm_stream.hip): needs a workspace only
+  if (K >= 2048 && (int64_t)M * N <= 16384 && wgrad_instance(M, N)) return 2;
   int s = (int)((512 + tiles - 1) / tiles);
   int maxs = K / (BK * 4);  // each split keeps >= 4 k-tiles
   if (s > maxs) s = maxs;

@@ -35,6 +35,7 @@ bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda)
 int rowgemm_launch(const StreamArgs& s, hipStream_t st);
 bool rowgemm_ln_supported(int M, int N, int K, const float* A, int lda);
 int rowgemm_ln_launch(const StreamArgs& s, hipStream_t st);
+bool wgrad_instance(int M, int N);  // an instance exists for this (padded) dW tile
 bool wgrad_supported(int transA, int transB, int M, int N, int K, const float* A, int lda,
                      const float* B, int ldb, int ldc, int epi);
 int64_t wgrad_ws_bytes(int M, int N, int K);

@@ -824,15 +824,20 @@ int rowgemm_ln_launch(const StreamArgs& s, hipStream_t st) {
   return 0;
 }
 
-bool wgrad_supported(int transA, int transB, int M, int N, int K, const float* A, int lda,
-                     const float* B, int ldb, int ldc, int epi) {
-  if (!transA || transB || epi != 0 || K < 2048) return false;
+bool wgrad_instance(int M, int N) {
   const int mo_pad = (M + 31) / 32 * 32, no_pad = (N + 31) / 32 * 32;
   switch (mo_pad * 1000 + no_pad) {
     case 64064: case 64256: case 256064: case 192064: case 64192: case 128128: case 128064:
-    case 64128: case 32064: case 64032: case 128256: case 256128: break;
+    case 64128: case 32064: case 64032: case 128256: case 256128: case 64096: case 96064:
+      return true;
     default: return false;
   }
+}
+
+bool wgrad_supported(int transA, int transB, int M, int N, int K, const float* A, int lda,
+                     const float* B, int ldb, int ldc, int epi) {
+  if (!transA || transB || epi != 0 || K < 2048) return false;
+  if (!wgrad_instance(M, N)) return false;
   if (M % 4 != 0 || N % 4 != 0 || lda % 4 != 0 || ldb % 4 != 0 || !aligned16(A) || !aligned16(B))
     return false;
   (void)ldc;
@@ -856,6 +861,7 @@ int wgrad_launch(const StreamArgs& s, hipStream_t st) {
   switch (mo_pad * 1000 + no_pad) {
     RS_WG(64, 64) RS_WG(64, 256) RS_WG(256, 64) RS_WG(192, 64) RS_WG(64, 192) RS_WG(128, 128)
     RS_WG(128, 64) RS_WG(64, 128) RS_WG(32, 64) RS_WG(64, 32) RS_WG(128, 256) RS_WG(256, 128)
+    RS_WG(64, 96) RS_WG(96, 64)
     default: set_error("wgrad: no instance for %dx%d", s.M, s.N); return -1;
   }
 #undef RS_WG
