@@ -212,6 +212,28 @@ int rs_catalog_gather(const void* cat, int elem, int widen, int64_t V, int F, in
                       const int64_t* ids, int B, int N, int64_t ld_ids, void* out, int64_t ld_out,
                       int* err_flag, void* stream);
 
+/* ---------------------------------------------------------------- validation / Recall@K
+ * The reference's validate() (training_utils.py:121-275) on the device: scores = U I_all^T via
+ * rs_gemm_f32, then
+ *   rs_mask_history: column c = hist_idx[j] -> -inf for j in [hist_off[u], hist_off[u+1]), u =
+ *     user_ids[b*uid_stride] (CSR of each user's training items as catalog column indices;
+ *     replaces the per-user Python loop :238-252); S holds catalog columns [col0, col0+ncols)
+ *     (one column chunk) at S[b*ld + c - col0];
+ *   rs_topk_rows: per row the K (<= 256) largest of S[b, 0:N], sorted descending, ties by the
+ *     lower column; out_idx[b*ld_out + i] = column + col_offset, or idx_in[b*ld_idx_in + column]
+ *     when idx_in is given (merging per-chunk candidates); out_val nullable (torch.topk :256);
+ *   rs_recall_hits: hits[i] += #rows whose target item is among the first ks[i] of its list
+ *     (item_ids[col] == targets[b*target_stride]; :258-262). */
+int rs_mask_history(float* S, int64_t ld, int B, int64_t col0, int64_t ncols,
+                    const int64_t* user_ids, int64_t uid_stride, const int64_t* hist_off,
+                    const int32_t* hist_idx, int64_t num_users, void* stream);
+int rs_topk_rows(const float* S, int64_t ld, int B, int N, int K, const int32_t* idx_in,
+                 int64_t ld_idx_in, int col_offset, int32_t* out_idx, float* out_val,
+                 int64_t ld_out, void* stream);
+int rs_recall_hits(const int32_t* topk_idx, int B, int K, const int64_t* item_ids,
+                   const int64_t* targets, int64_t target_stride, const int32_t* ks, int nk,
+                   int32_t* hits, void* stream);
+
 /* ---------------------------------------------------------------- clip + Adam
  * Flat multi-tensor path over a contiguous fp32 range (all parameters packed in one buffer).
  * rs_grad_sqnorm: partial sums of (scale*g)^2 into ws; rs_clip_coef: total norm and

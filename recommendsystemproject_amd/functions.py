@@ -84,6 +84,8 @@ def seq_feature_segments(proc, seqd, B, L):
         col += D
     if not segs:
         raise ValueError('Configuration Error: No valid features were processed!')
+    for t in keep:  # the kernels read these through raw pointers
+        _hip.require_device(t)
     return segs, tables, col, keep
 
 
@@ -305,6 +307,8 @@ def tower_segments(tower, input_dict, mapping):
                              table=lin.weight.data_ptr(), bias=lin.bias.data_ptr()))
             params.append((lin.weight, lin.bias))
             col += lin.out_features
+    for t in keep:
+        _hip.require_device(t)
     return segs, params, keep, col
 
 
@@ -467,6 +471,7 @@ class InBatchLossFn(torch.autograd.Function):
         st = 0
         if item_ids is not None:
             ids = item_ids.reshape(-1)
+            _hip.require_device(ids)
             if ids.dtype != torch.int64:
                 ids = ids.long()
             st = int(ids.stride(0))

@@ -109,3 +109,16 @@ def test_synthetic_batch_contract():
     maps = synth.tower_layout(cfg['two_tower']['item_tower'])
     assert maps == {'sparse': {'movie_id_enc': 0, 'release_year_enc': 1}, 'dense': {},
                     'sequence': {'genre_ids': 'genre_ids'}}
+
+
+def test_history_csr_filters_like_reference():
+    """validate()'s history mask input (training_utils.py:238-252): per user the catalog
+    columns of their items; ids above the catalog's max id or not in it are dropped."""
+    from recommendsystemproject_amd.project.utils.training_utils import _history_csr
+    item_ids = np.array([10, 11, 13, 20])  # column = position
+    hist = {0: {10, 13, 99}, 2: {12, 20, 11}, 3: set()}
+    off, idx, U = _history_csr(hist, item_ids, 'cpu')
+    assert U == 4
+    off, idx = off.numpy(), idx.numpy()
+    rows = [sorted(idx[off[u]:off[u + 1]].tolist()) for u in range(U)]
+    assert rows == [[0, 2], [], [1, 3], []]
