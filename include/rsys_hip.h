@@ -127,6 +127,35 @@ int rs_gemm_add_layernorm(int M, int N, int K, const float* A, int lda, const fl
                           float p, const int64_t* key, int site, int flags, void* stream);
 /* flags: RS_GEMM_BF16 (bf16 operands for the GEMM part; LayerNorm stays fp32) or 0. */
 
+/* ---------------------------------------------------------------- fused feed-forward block (bf16 mode)
+ * x2 = norm2(x1 + dropout2(linear2(dropout(relu(linear1(x1)))))) of nn.TransformerEncoderLayer
+ * (SequenceEncoder.py:17-29), d_model = 64, F = dim_feedforward = 256, bf16 operands / fp32
+ * accumulation (the RS_GEMM_BF16 compute mode). The [M, F] inner activation stays in registers:
+ *   rs_ffn_fwd_bf16: x [M,64] (x1; also the residual), W1 [F,64], b1, W2 [64,F], b2, gamma, beta
+ *     -> h [M,64] (pre-norm sum), y [M,64] (x2), mean/rstd [M], mask [rs_ffn_mask_words] uint64
+ *     (bit set where f1 > 0). Dropout: linear1's output site1 (element m*F + n), linear2's site2
+ *     (m*64 + n) -- the draws of the unfused rs_gemm_f32 / rs_gemm_add_layernorm calls.
+ *   rs_ffn_bwd_bf16: dff [M,64] = gradient of linear2's output (after dropout2's backward);
+ *     writes f1 and dPre1 (gradient of linear1's output) as bf16 [M,F] for the weight gradients
+ *     and dx [M,64] = dres + dPre1 W1 (dres: the residual-path gradient; dx may alias dres but
+ *     not dff). M % 16 == 0. */
+int64_t rs_ffn_mask_words(int M, int F);
+int rs_ffn_fwd_bf16(int M, int F, const float* x, const float* W1, const float* b1, const float* W2,
+                    const float* b2, const float* gamma, const float* beta, float eps, float* h,
+                    float* y, float* mean, float* rstd, uint64_t* mask, float p, const int64_t* key,
+                    int site1, int site2, void* stream);
+int rs_ffn_bwd_bf16(int M, int F, const float* x, const float* W1, const float* b1, const float* W2,
+                    const uint64_t* mask, const float* dff, const float* dres, float* dx, void* f1,
+                    void* dpre, float p, void* stream);
+/* dW[Mo,No] = beta*dW + dY^T X over `rows` rows on bf16 MFMA (fp32 accumulate, fixed-order
+ * reduction); db[Mo] += colsum(dY) (nullable). dY / X are fp32 or, with dy_bf16 / x_bf16, bf16
+ * (the fused FFN's f1 / dPre1). Replaces the weight-gradient part of autograd's Linear backward
+ * (Tower.py:16-25, TransformerEncoderLayer). ws: rs_wgrad_ws_bytes. */
+int64_t rs_wgrad_ws_bytes(int Mo, int No, int rows);
+int rs_wgrad_bf16(int rows, int Mo, int No, const void* dy, int ldy, int dy_bf16, const void* x,
+                  int ldx, int x_bf16, float beta, float* dW, int ldw, float* db, float* ws,
+                  void* stream);
+
 /* ---------------------------------------------------------------- sequence mask
  * padding mask from the first sequence feature (== pad_value) with the all-padding-row fix,
  * and last-valid index (SequenceEncoder.py:36-46, :66-70; traps T6/T7).

@@ -40,6 +40,12 @@ SIGNATURES = {
                           i32, i32, f32, vp, i32, i32, vp, i32, vp, vp]),
     'rs_gemm_add_layernorm': (i32, [i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp,
                                     f32, f32, vp, i32, i32, vp]),
+    'rs_ffn_mask_words': (i64, [i32, i32]),
+    'rs_ffn_fwd_bf16': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, f32, vp,
+                              i32, i32, vp]),
+    'rs_ffn_bwd_bf16': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, vp]),
+    'rs_wgrad_ws_bytes': (i64, [i32, i32, i32]),
+    'rs_wgrad_bf16': (i32, [i32, i32, i32, vp, i32, i32, vp, i32, i32, f32, vp, i32, vp, vp, vp]),
     'rs_colsum_ws_bytes': (i64, [i32, i32]),
     'rs_colsum': (i32, [vp, i32, i32, i32, f32, f32, vp, vp, vp]),
     'rs_gather_fwd': (i32, [vp, i32, i32, vp, i32, vp, vp]),

@@ -205,12 +205,8 @@ constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
 // words puts the four q groups on disjoint bank quarters (16 words would be a 4-way conflict)
 constexpr int kRowP = 20;
 
-// dropout index ((b*H + h)*L + i)*L + j in 32 bits (the host checks B*H*L*L < 2^32): the same
-// draw as keep_mult on the 64-bit index, without 64-bit multiplies per probability
-__device__ __forceinline__ float keep_mult32(const DropKey& k, uint32_t idx) {
-  const uint32_t h = fmix32(fmix32(idx ^ k.k0) + k.k1);
-  return h >= k.thresh ? k.scale : 0.f;
-}
+// dropout index ((b*H + h)*L + i)*L + j in 32 bits (the host checks B*H*L*L < 2^32):
+// keep_mult32 (rng.h)
 
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
@@ -287,13 +283,16 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(
     const int i = tq * 16 + r;
     const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
 #pragma unroll
-    for (int tk = 0; tk < NT; ++tk)
+    for (int tk = 0; tk < NT; ++tk) {
+      float mk[4] = {1.f, 1.f, 1.f, 1.f};
+      if (DROP) keep4_32(dk, rowbase + tk * 16 + 4 * q, mk);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float pv = kok[tk][e] ? exp2f(sv[tk][e] * scale2 - m) : 0.f;
         l += pv;
-        sv[tk][e] = DROP ? pv * keep_mult32(dk, rowbase + tk * 16 + 4 * q + e) : pv;
+        sv[tk][e] = DROP ? pv * mk[e] : pv;
       }
+    }
     l = xsum(l);
     // O[i][c] = sum_j pz[i][j] V[j][c]: A = this lane's probabilities (row i = lane & 15,
     // k = key), B = V[key][c = lane & 15]
@@ -387,10 +386,12 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(
         sacc = mfma4(kf[tk][s4], qf[tq][s4], sacc);   // S^T[key][query]
         pacc = mfma4(vf[tk][s4], gf[tq][s4], pacc);   // dP^T[key][query] = V dO^T
       }
+      float mk[4] = {1.f, 1.f, 1.f, 1.f};
+      if (DROP) keep4_32(dk, rowbase + tk * 16 + 4 * q, mk);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float pv = (kok[tk][e] && i < L) ? exp2f(sacc[e] * scale2 - lsei[tq]) : 0.f;
-        const float z = DROP ? keep_mult32(dk, rowbase + tk * 16 + 4 * q + e) : 1.f;
+        const float z = DROP ? mk[e] : 1.f;
         ds[tk][e] = pv * (z * pacc[e] - Di[tq]);
         ps[tk][e] = pv * z;
       }

@@ -1,0 +1,427 @@
+// The Transformer layer's feed-forward block fused per 16-token row group (bf16 compute mode).
+//
+// Reference: nn.TransformerEncoderLayer(norm_first=False, activation=relu) inside
+// SequenceEncoder (SequenceEncoder.py:17-29):
+//     x2 = norm2(x1 + dropout2(linear2(dropout(relu(linear1(x1))))))
+//
+// Unfused, the [tokens, F = 256] inner activation f1 is the largest tensor of the step: written
+// by linear1, read by linear2, by linear2's weight gradient and (as the ReLU mask) by its input
+// gradient, and the same again for its gradient dPre1. Here it never reaches HBM in the forward:
+//
+// rs_ffn_fwd_bf16: per wave and 16-row group, f1 = drop(relu(x1 W1^T + b1)) stays in registers as
+//   the bf16 operand of linear2 (the 16x16 accumulator tiles of the first product ARE the k-slices
+//   of the second product's operand under a fixed k permutation, applied to W2's LDS image too),
+//   followed by bias + dropout2 + residual + LayerNorm in the epilogue. Stores h2, x2, mean, rstd
+//   and one bit per f1 element (kept by dropout and positive): [M][F/64] uint64 (6.5 MB at C2).
+// rs_ffn_bwd_bf16: recomputes x1 W1^T + b1 on the MFMA (exactly the forward's operation order),
+//   rebuilds f1 from the bits (no dropout hash in the backward), writes f1 and
+//   dPre1 = (dff W2) * mask / (1 - p) as bf16 for the two weight gradients, and accumulates
+//   dx1 += dPre1 W1 -- three products per row group, f1 / dPre1 never read back.
+// Weight gradients: rs_wgrad_bf16 with the bf16 operands (gemm_stream.hip).
+//
+// Numerics are those of the bf16 compute mode (operands rounded to bf16, fp32 accumulation,
+// fp32 epilogues): identical element values to the unfused bf16 path except for the summation
+// order inside linear2 / dx1 (a different k permutation) and db1, which is summed from the bf16
+// dPre1 (as under autocast, where the gradient reaching the bias is bf16).
+#include "common.h"
+#include "gemm_stream.h"
+#include "rng.h"
+#include "stage.h"
+
+namespace rs {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) floatx4* gptr4;
+
+constexpr int D = 64;      // d_model
+constexpr int DP = D + 8;  // LDS pitch (bf16) of [*][D] images: conflict-free 16-byte reads
+
+struct FfnArgs {
+  int M;
+  const float* x;   // [M, D] FFN input x1 (also the LayerNorm residual)
+  const float* W1;  // [F, D]
+  const float* b1;  // [F]
+  const float* W2;  // [D, F]
+  const float* b2;  // [D]
+  const float* gamma;
+  const float* beta;
+  float eps;
+  float* h;      // fwd: x1 + dropout2(linear2(.))  [M, D]
+  float* y;      // fwd: LayerNorm(h)               [M, D]
+  float* mean;   // fwd: [M]
+  float* rstd;   // fwd: [M]
+  uint64_t* mask;        // fwd: out, bwd: in -- [M][F/64] (f1 > 0 bits)
+  const float* dff;      // bwd: gradient of linear2's output after dropout2's backward [M, D]
+  const float* dres;     // bwd: [M, D] gradient already reaching x1 (residual path)
+  float* dx;             // bwd: out [M, D] = dres + dPre1 W1 (may alias dres)
+  __bf16* f1;            // bwd: out [M, F]
+  __bf16* dpre;          // bwd: out [M, F]
+  float p;
+  const int64_t* key;
+  int site1, site2;
+};
+
+// k permutation of a 32-wide chunk: operand slot 8q + j (lane quad q, element j) holds column
+// kp(q, j) of the chunk -- the columns lane quad q owns in the two 16x16 output tiles 2c, 2c+1
+__host__ __device__ constexpr int kp(int q, int j) { return j < 4 ? 4 * q + j : 16 + 4 * q + (j - 4); }
+
+__device__ __forceinline__ bf16x8 cvt8(const floatx4& lo, const floatx4& hi) {
+  bf16x8 r;
+  r[0] = (__bf16)lo[0]; r[1] = (__bf16)lo[1]; r[2] = (__bf16)lo[2]; r[3] = (__bf16)lo[3];
+  r[4] = (__bf16)hi[0]; r[5] = (__bf16)hi[1]; r[6] = (__bf16)hi[2]; r[7] = (__bf16)hi[3];
+  return r;
+}
+
+__device__ __forceinline__ bf16x8 lds8(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// column k of a 32-wide chunk -> its slot in the k-permuted image (inverse of kp)
+__host__ __device__ constexpr int kslot(int k) {
+  const int kk = k & 31, c = k >> 5;
+  return 32 * c + (kk < 16 ? 8 * (kk >> 2) + (kk & 3) : 8 * ((kk - 16) >> 2) + 4 + (kk & 3));
+}
+
+__device__ __forceinline__ void put4(__bf16* p, const floatx4& v) {
+  bf16x4 h;
+  h[0] = (__bf16)v[0]; h[1] = (__bf16)v[1]; h[2] = (__bf16)v[2]; h[3] = (__bf16)v[3];
+  *reinterpret_cast<bf16x4*>(p) = h;
+}
+
+// x [M, D] row m, columns 16q .. 16q+15 (lane quad q) as the k-fragments of a K = 64 product
+__device__ __forceinline__ void load_row64(const float* base, int64_t m, int q, floatx4 (&v)[4]) {
+  const float* row = base + m * D + 16 * q;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) v[u] = *(gptr4)(row + 4 * u);
+}
+
+// acc[t] = sum over the K = 64 fragments of W-image rows 16t + r (two MFMAs)
+#define RS_MFMA2(ACC, IMG, PITCH, ROW, AF)                                                  \
+  do {                                                                                      \
+    const __bf16* bp_ = (IMG) + (ROW) * (PITCH) + 16 * q;                                   \
+    ACC = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(bp_), (AF)[0], ACC, 0, 0, 0);        \
+    ACC = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(bp_ + 8), (AF)[1], ACC, 0, 0, 0);    \
+  } while (0)
+
+template <int F, bool DROP>
+__global__ __launch_bounds__(512) void ffn_fwd_bf16_kernel(FfnArgs a) {
+  constexpr int FP = F + 8;
+  constexpr int NH = F / 16, NC = F / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  __bf16* W1s = reinterpret_cast<__bf16*>(smem_raw);  // [F][DP]
+  __bf16* W2p = W1s + F * DP;                           // [D][FP], k-permuted
+  float* sb1 = reinterpret_cast<float*>(W2p + D * FP);  // [F]
+  float* sb2 = sb1 + F;                                 // [D]
+  float* sg = sb2 + D;
+  float* sbt = sg + D;
+  // W1 [F][D] as is; W2 [D][F] with each 32-chunk's columns in kslot order (4 consecutive
+  // columns stay consecutive)
+  stage_batched<F, D, 512>(a.W1, D, [&](int n, int k, const floatx4& v) { put4(W1s + n * DP + k, v); });
+  stage_batched<D, F, 512>(a.W2, F, [&](int n, int k, const floatx4& v) { put4(W2p + n * FP + kslot(k), v); });
+  for (int i = threadIdx.x; i < F; i += blockDim.x) sb1[i] = a.b1[i];
+  for (int i = threadIdx.x; i < D; i += blockDim.x) {
+    sb2[i] = a.b2[i];
+    sg[i] = a.gamma[i];
+    sbt[i] = a.beta[i];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int groups = a.M / 16;  // host: M % 16 == 0
+  DropKey k1{}, k2{};
+  if constexpr (DROP) {
+    k1 = make_key(a.key, a.site1, a.p);
+    k2 = make_key(a.key, a.site2, a.p);
+  }
+  const int stride = gridDim.x * 8;
+  int g = blockIdx.x * 8 + wave;
+  floatx4 xr[4];
+  if (g < groups) load_row64(a.x, (int64_t)g * 16 + r, q, xr);
+  for (; g < groups; g += stride) {
+    // an opaque zero offset per iteration keeps the W fragment reads inside the loop (hoisted,
+    // the 64 fragments alone would take every VGPR and spill)
+    int zo = 0;
+    asm volatile("" : "+s"(zo));
+    const __bf16* W1i = W1s + zo;
+    const __bf16* W2i = W2p + zo;
+    const int64_t m = (int64_t)g * 16 + r;
+    floatx4 res[4];  // LayerNorm residual x1[m][16t + 4q ..]
+#pragma unroll
+    for (int t = 0; t < 4; ++t) res[t] = *(gptr4)(a.x + m * D + 16 * t + 4 * q);
+    bf16x8 af[2] = {cvt8(xr[0], xr[1]), cvt8(xr[2], xr[3])};
+    const int gn = g + stride < groups ? g + stride : g;
+    load_row64(a.x, (int64_t)gn * 16 + r, q, xr);
+    // dropout element indices m*F + n / m*D + n in 32 bits (host: M*F < 2^32)
+    const uint32_t base1 = (uint32_t)m * F + 4 * q, base2 = (uint32_t)m * D + 4 * q;
+    // linear1 + bias + relu + dropout, 4 tiles at a time, into linear2's operand fragments
+    bf16x8 a2[NC];
+    uint64_t bits = 0;
+#pragma unroll
+    for (int h0 = 0; h0 < NH; h0 += 4) {
+      floatx4 acc[4];
+#pragma unroll
+      for (int hh = 0; hh < 4; ++hh) {
+        acc[hh] = floatx4{0.f, 0.f, 0.f, 0.f};
+        RS_MFMA2(acc[hh], W1i, DP, (h0 + hh) * 16 + r, af);
+      }
+#pragma unroll
+      for (int hh = 0; hh < 4; ++hh) {
+        const int h = h0 + hh, n0 = 16 * h + 4 * q;
+        const floatx4 bv = *reinterpret_cast<const floatx4*>(sb1 + n0);
+        float mk[4];
+        if constexpr (DROP) keep4_32(k1, base1 + 16 * h, mk);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = acc[hh][i] * 1.0f + bv[i];
+          v = fmaxf(v, 0.f);
+          if constexpr (DROP) v *= mk[i];
+          if (v > 0.f) bits |= 1ull << (4 * h + i);
+          a2[h >> 1][4 * (h & 1) + i] = (__bf16)v;
+        }
+      }
+    }
+    a.mask[m * (F / 64) + q] = bits;  // F == 256: one word per lane quad
+    // linear2 over the permuted k slices
+    floatx4 acc2[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc2[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        acc2[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(W2i + (16 * t + r) * FP + 32 * c + 8 * q),
+                                                           a2[c], acc2[t], 0, 0, 0);
+    // bias + dropout2 + residual + LayerNorm (same per-element order as rs_gemm_add_layernorm)
+    float hv[4][4];
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int n0 = 16 * t + 4 * q;
+      const floatx4 bv = *reinterpret_cast<const floatx4*>(sb2 + n0);
+      float mk[4];
+      if constexpr (DROP) keep4_32(k2, base2 + 16 * t, mk);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc2[t][e] * 1.0f + bv[e];
+        if constexpr (DROP) v *= mk[e];
+        hv[t][e] = v + res[t][e];
+        s += hv[t][e];
+      }
+    }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const float mu = s / (float)D;
+    float vs = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = hv[t][e] - mu;
+        vs += d * d;
+      }
+    vs += __shfl_xor(vs, 16, 64);
+    vs += __shfl_xor(vs, 32, 64);
+    const float rs = 1.f / sqrtf(vs / (float)D + a.eps);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int n0 = 16 * t + 4 * q;
+      const floatx4 gm = *reinterpret_cast<const floatx4*>(sg + n0);
+      const floatx4 bt = *reinterpret_cast<const floatx4*>(sbt + n0);
+      floatx4 h4, y4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        h4[e] = hv[t][e];
+        y4[e] = (hv[t][e] - mu) * rs * gm[e] + bt[e];
+      }
+      *reinterpret_cast<floatx4*>(a.h + m * D + n0) = h4;
+      *reinterpret_cast<floatx4*>(a.y + m * D + n0) = y4;
+    }
+    if (q == 0) {
+      a.mean[m] = mu;
+      a.rstd[m] = rs;
+    }
+  }
+}
+
+template <int F>
+__global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
+  constexpr int FP = F + 8;
+  constexpr int NH = F / 16, NC = F / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  __bf16* W1s = reinterpret_cast<__bf16*>(smem_raw);  // [F][DP]  (x1 W1^T)
+  __bf16* W2t = W1s + F * DP;                           // [F][DP]  W2^T (dff W2)
+  __bf16* W1t = W2t + F * DP;                           // [D][FP]  W1^T, k-permuted (dPre1 W1)
+  float* sb1 = reinterpret_cast<float*>(W1t + D * FP);  // [F]
+  stage_batched<F, D, 512>(a.W1, D, [&](int n1, int k, const floatx4& v) {
+    put4(W1s + n1 * DP + k, v);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) W1t[(k + e) * FP + kslot(n1)] = (__bf16)v[e];  // W1^T, k-permuted
+  });
+  stage_batched<D, F, 512>(a.W2, F, [&](int n2, int n1, const floatx4& v) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) W2t[(n1 + e) * DP + n2] = (__bf16)v[e];  // W2^T
+  });
+  for (int i = threadIdx.x; i < F; i += blockDim.x) sb1[i] = a.b1[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int groups = a.M / 16;
+  const float scale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+  const int stride = gridDim.x * 8;
+  int g = blockIdx.x * 8 + wave;
+  floatx4 xr[4], dr[4];
+  if (g < groups) {
+    load_row64(a.x, (int64_t)g * 16 + r, q, xr);
+    load_row64(a.dff, (int64_t)g * 16 + r, q, dr);
+  }
+  for (; g < groups; g += stride) {
+    int zo = 0;
+    asm volatile("" : "+s"(zo));
+    const __bf16* W1i = W1s + zo;
+    const __bf16* W2i = W2t + zo;
+    const __bf16* W3i = W1t + zo;
+    const int64_t m = (int64_t)g * 16 + r;
+    floatx4 res[4];  // dres[m][16t + 4q ..] (accumulated into)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) res[t] = *(gptr4)(a.dres + m * D + 16 * t + 4 * q);
+    const uint64_t bits = a.mask[m * (F / 64) + q];
+    bf16x8 ax[2] = {cvt8(xr[0], xr[1]), cvt8(xr[2], xr[3])};
+    bf16x8 ad[2] = {cvt8(dr[0], dr[1]), cvt8(dr[2], dr[3])};
+    const int gn = g + stride < groups ? g + stride : g;
+    load_row64(a.x, (int64_t)gn * 16 + r, q, xr);
+    load_row64(a.dff, (int64_t)gn * 16 + r, q, dr);
+    bf16x8 a3[NC];
+#pragma unroll
+    for (int h0 = 0; h0 < NH; h0 += 4) {
+      floatx4 acc[4], accd[4];
+#pragma unroll
+      for (int hh = 0; hh < 4; ++hh) {
+        acc[hh] = floatx4{0.f, 0.f, 0.f, 0.f};
+        accd[hh] = floatx4{0.f, 0.f, 0.f, 0.f};
+        RS_MFMA2(acc[hh], W1i, DP, (h0 + hh) * 16 + r, ax);
+        RS_MFMA2(accd[hh], W2i, DP, (h0 + hh) * 16 + r, ad);
+      }
+#pragma unroll
+      for (int hh = 0; hh < 4; ++hh) {
+        const int h = h0 + hh, n0 = 16 * h + 4 * q;
+        const floatx4 bv = *reinterpret_cast<const floatx4*>(sb1 + n0);
+        bf16x4 f4, d4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool keep = (bits >> (4 * h + i)) & 1ull;
+          const float pre = acc[hh][i] * 1.0f + bv[i];
+          const float f = keep ? pre * scale : 0.f;  // == the forward's drop(relu(pre))
+          const float d = keep ? scale * accd[hh][i] : 0.f;
+          f4[i] = (__bf16)f;
+          d4[i] = (__bf16)d;
+          a3[h >> 1][4 * (h & 1) + i] = d4[i];
+        }
+        *reinterpret_cast<bf16x4*>(a.f1 + m * F + n0) = f4;
+        *reinterpret_cast<bf16x4*>(a.dpre + m * F + n0) = d4;
+      }
+    }
+    floatx4 acc3[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc3[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        acc3[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(W3i + (16 * t + r) * FP + 32 * c + 8 * q),
+                                                           a3[c], acc3[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      floatx4 v = acc3[t] * 1.0f;
+      v += 1.0f * res[t];
+      *reinterpret_cast<floatx4*>(a.dx + m * D + 16 * t + 4 * q) = v;
+    }
+  }
+}
+
+#undef RS_MFMA2
+
+size_t fwd_lds(int F) { return (size_t)F * DP * 2 + (size_t)D * (F + 8) * 2 + (size_t)(F + 3 * D) * 4; }
+size_t bwd_lds(int F) { return (size_t)2 * F * DP * 2 + (size_t)D * (F + 8) * 2 + (size_t)F * 4; }
+
+int grid_for(int M, size_t lds) {
+  const int per_cu = lds > 80 * 1024 ? 1 : 2;
+  int bx = cdiv(M / 16, 16);
+  if (bx > 256 * per_cu) bx = 256 * per_cu;
+  return bx < 1 ? 1 : bx;
+}
+
+}  // namespace
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int64_t rs_ffn_mask_words(int M, int F) { return (int64_t)M * (F / 64); }
+
+extern "C" int rs_ffn_fwd_bf16(int M, int F, const float* x, const float* W1, const float* b1,
+                               const float* W2, const float* b2, const float* gamma,
+                               const float* beta, float eps, float* h, float* y, float* mean,
+                               float* rstd, uint64_t* mask, float p, const int64_t* key,
+                               int site1, int site2, void* stream) {
+  RS_CHECK_ARG(M >= 0 && M % 16 == 0 && F == 256, "rs_ffn_fwd_bf16: need M %% 16 == 0 and F == 256 (M=%d F=%d)", M, F);
+  RS_CHECK_ARG(x && W1 && b1 && W2 && b2 && gamma && beta && h && y && mean && rstd && mask,
+               "rs_ffn_fwd_bf16: null operand");
+  RS_CHECK_ARG(aligned16(x) && aligned16(h) && aligned16(y) && aligned16(b1) && aligned16(b2) &&
+                   aligned16(gamma) && aligned16(beta),
+               "rs_ffn_fwd_bf16: operands must be 16-byte aligned");
+  RS_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || key), "rs_ffn_fwd_bf16: dropout needs a key, 0 <= p < 1");
+  RS_CHECK_ARG((int64_t)M * F < ((int64_t)1 << 32), "rs_ffn_fwd_bf16: M*F must be < 2^32");
+  if (M == 0) return 0;
+  FfnArgs a{};
+  a.M = M; a.x = x; a.W1 = W1; a.b1 = b1; a.W2 = W2; a.b2 = b2; a.gamma = gamma; a.beta = beta;
+  a.eps = eps; a.h = h; a.y = y; a.mean = mean; a.rstd = rstd; a.mask = mask; a.p = p; a.key = key;
+  a.site1 = site1; a.site2 = site2;
+  const size_t lds = fwd_lds(F);
+  const int bx = grid_for(M, lds);
+  if (p > 0.f) ffn_fwd_bf16_kernel<256, true><<<bx, 512, lds, as_stream(stream)>>>(a);
+  else ffn_fwd_bf16_kernel<256, false><<<bx, 512, lds, as_stream(stream)>>>(a);
+  RS_CHECK_LAUNCH("rs_ffn_fwd_bf16");
+  return 0;
+}
+
+extern "C" int rs_ffn_bwd_bf16(int M, int F, const float* x, const float* W1, const float* b1,
+                               const float* W2, const uint64_t* mask, const float* dff,
+                               const float* dres, float* dx, void* f1, void* dpre, float p,
+                               void* stream) {
+  RS_CHECK_ARG(M >= 0 && M % 16 == 0 && F == 256, "rs_ffn_bwd_bf16: need M %% 16 == 0 and F == 256 (M=%d F=%d)", M, F);
+  RS_CHECK_ARG(x && W1 && b1 && W2 && mask && dff && dres && dx && f1 && dpre,
+               "rs_ffn_bwd_bf16: null operand");
+  RS_CHECK_ARG(dx != dff || dx == dres, "rs_ffn_bwd_bf16: dx may alias dres only");
+  RS_CHECK_ARG(aligned16(x) && aligned16(dff) && aligned16(dres) && aligned16(dx) && aligned16(b1) &&
+                   ((uintptr_t)f1 & 7) == 0 && ((uintptr_t)dpre & 7) == 0,
+               "rs_ffn_bwd_bf16: misaligned operand");
+  RS_CHECK_ARG(p >= 0.f && p < 1.f, "rs_ffn_bwd_bf16: 0 <= p < 1");
+  if (M == 0) return 0;
+  FfnArgs a{};
+  a.M = M; a.x = x; a.W1 = W1; a.b1 = b1; a.W2 = W2; a.mask = const_cast<uint64_t*>(mask);
+  a.dff = dff; a.dres = dres; a.dx = dx; a.f1 = reinterpret_cast<__bf16*>(f1); a.dpre = reinterpret_cast<__bf16*>(dpre);
+  a.p = p;
+  const size_t lds = bwd_lds(F);
+  ffn_bwd_bf16_kernel<256><<<grid_for(M, lds), 512, lds, as_stream(stream)>>>(a);
+  RS_CHECK_LAUNCH("rs_ffn_bwd_bf16");
+  return 0;
+}
+
+extern "C" int64_t rs_wgrad_ws_bytes(int Mo, int No, int rows) { return wgrad_ws_bytes(Mo, No, rows); }
+
+extern "C" int rs_wgrad_bf16(int rows, int Mo, int No, const void* dy, int ldy, int dy_bf16,
+                             const void* x, int ldx, int x_bf16, float beta, float* dW, int ldw,
+                             float* db, float* ws, void* stream) {
+  RS_CHECK_ARG(rows >= 0 && Mo > 0 && No > 0 && dy && x && dW && ws && ldw >= No && ldy >= Mo && ldx >= No,
+               "rs_wgrad_bf16: bad arguments");
+  const int ey = dy_bf16 ? 2 : 4, ex = x_bf16 ? 2 : 4;
+  RS_CHECK_ARG(aligned16(dy) && aligned16(x) && (ldy * ey) % 16 == 0 && (ldx * ex) % 16 == 0 &&
+                   (Mo * ey) % 16 == 0 && (No * ex) % 16 == 0,
+               "rs_wgrad_bf16: rows must be 16-byte aligned and a whole number of 16-byte slots");
+  StreamArgs s{};
+  s.M = Mo; s.N = No; s.K = rows; s.alpha = 1.f; s.beta = beta;
+  s.A = reinterpret_cast<const float*>(dy); s.lda = ldy;
+  s.B = reinterpret_cast<const float*>(x); s.ldb = ldx;
+  s.C = dW; s.ldc = ldw; s.epi = RS_GEMM_BF16; s.rowsum = db; s.ws = ws; s.transB = 0;
+  return wgrad_bf16_launch(s, dy_bf16 != 0, x_bf16 != 0, as_stream(stream));
+}

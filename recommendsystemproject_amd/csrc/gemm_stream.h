@@ -40,5 +40,7 @@ bool wgrad_supported(int transA, int transB, int M, int N, int K, const float* A
                      const float* B, int ldb, int ldc, int epi);
 int64_t wgrad_ws_bytes(int M, int N, int K);
 int wgrad_launch(const StreamArgs& s, hipStream_t st);
+// bf16 MFMA weight gradient; y_bf16 / x_bf16: dY (A) / X (B) are stored as bf16
+int wgrad_bf16_launch(const StreamArgs& s, bool y_bf16, bool x_bf16, hipStream_t st);
 
 }  // namespace rs

@@ -17,6 +17,7 @@
 #include "common.h"
 #include "gemm_stream.h"
 #include "rng.h"
+#include "stage.h"
 
 namespace rs {
 
@@ -68,13 +69,17 @@ __device__ __forceinline__ floatx4 epi_apply4(const StreamArgs& a, int m, int n0
   }
   const uint64_t e0 = (uint64_t)m * a.N + n0;
   if (a.epi & RS_EPI_DROP_A) {
+    float mk[4];
+    keep4(ka, e0, mk);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] *= keep_mult(ka, e0 + i);
+    for (int i = 0; i < 4; ++i) v[i] *= mk[i];
   }
   if (a.epi & RS_EPI_AUX_ADD) v += auxv;
   if (a.epi & RS_EPI_DROP_B) {
+    float mk[4];
+    keep4(kb, e0, mk);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] *= keep_mult(kb, e0 + i);
+    for (int i = 0; i < 4; ++i) v[i] *= mk[i];
   }
   if (a.beta != 0.f) v += a.beta * *reinterpret_cast<const floatx4*>(a.C + (int64_t)m * a.ldc + n0);
   return v;
@@ -102,10 +107,12 @@ __device__ __forceinline__ void ln_epilogue(const StreamArgs& a, int m, int q, c
     floatx4 v = acc[t] * a.alpha;
     if (EPI >= 0 ? kBias : (a.epi & RS_EPI_BIAS) != 0) v += *reinterpret_cast<const floatx4*>(sbias + n0);
     const floatx4 res = resv[t];
+    float mk[4] = {1.f, 1.f, 1.f, 1.f};
+    if (EPI >= 0 ? kDrop : (a.epi & RS_EPI_DROP_A) != 0) keep4(ka, (uint64_t)m * N + n0, mk);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float x = v[e];
-      if (EPI >= 0 ? kDrop : (a.epi & RS_EPI_DROP_A) != 0) x *= keep_mult(ka, (uint64_t)m * N + n0 + e);
+      if (EPI >= 0 ? kDrop : (a.epi & RS_EPI_DROP_A) != 0) x *= mk[e];
       hv[t][e] = x + res[e];
       s += hv[t][e];
     }
@@ -166,13 +173,17 @@ __device__ __forceinline__ floatx4 epi4_ct(const StreamArgs& a, int m, int n0, f
   }
   const uint64_t e0 = (uint64_t)m * a.N + n0;
   if constexpr ((EPI & RS_EPI_DROP_A) != 0) {
+    float mk[4];
+    keep4(ka, e0, mk);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] *= keep_mult(ka, e0 + i);
+    for (int i = 0; i < 4; ++i) v[i] *= mk[i];
   }
   if constexpr ((EPI & RS_EPI_AUX_ADD) != 0) v += auxv;
   if constexpr ((EPI & RS_EPI_DROP_B) != 0) {
+    float mk[4];
+    keep4(kb, e0, mk);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] *= keep_mult(kb, e0 + i);
+    for (int i = 0; i < 4; ++i) v[i] *= mk[i];
   }
   if constexpr ((EPI & kEpiBeta) != 0) v += a.beta * cv;
   return v;
@@ -190,7 +201,23 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
   const int tid = threadIdx.x;
   const int nb0 = blockIdx.y * NT * 16;  // this workgroup's column slice (small-M N split)
   // stage op(B)[:, nb0 : nb0 + NT*16] as Bs[n][k], zero padded to NT*16 x KT*16
-  if (a.transB) {  // B[n*ldb + k]: consecutive threads -> consecutive k
+  // batched 16-byte loads (dispatch: K % 4 == 0; [K][N] weights also need N % 4 == 0)
+  if (a.ldb % 4 == 0 && ((uintptr_t)a.B & 15) == 0 && (a.transB || a.N % 4 == 0)) {
+    if (a.transB) {
+      stage_batched<NT * 16, KT * 16, 512>(
+          a.B + (int64_t)nb0 * a.ldb, a.ldb,
+          [&](int n, int k, const floatx4& v) { *reinterpret_cast<floatx4*>(Bs + n * KP + k) = v; },
+          [&](int n, int k) { return nb0 + n < a.N && k < a.K; });
+    } else {
+      stage_batched<KT * 16, NT * 16, 512>(
+          a.B + nb0, a.ldb,
+          [&](int k, int n, const floatx4& v) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Bs[(n + e) * KP + k] = v[e];
+          },
+          [&](int k, int n) { return k < a.K && nb0 + n < a.N; });
+    }
+  } else if (a.transB) {  // B[n*ldb + k]: consecutive threads -> consecutive k
     for (int idx = tid; idx < NT * 16 * KT * 16; idx += 512) {
       const int n = idx / (KT * 16), k = idx % (KT * 16);
       Bs[n * KP + k] = (nb0 + n < a.N && k < a.K) ? a.B[(int64_t)(nb0 + n) * a.ldb + k] : 0.f;
@@ -538,6 +565,210 @@ __global__ __launch_bounds__(1024) void wgrad_reduce_kernel(StreamArgs a, int P)
   }
 }
 
+// --------------------------------------------------------------------- wgrad, bf16 MFMA
+// bf16 compute mode: the same dW = dY^T X over a long row range on v_mfma_f32_32x32x16_bf16
+// (16x the f32 MFMA rate, so the kernel is HBM-bound on the fp32 operands it streams). Rows are
+// staged 32 at a time through registers (fp32, 16-byte loads) into a row-major bf16 LDS image;
+// the MFMA operands want 8 consecutive ROWS of one column per lane, which ds_read_b64_tr_b16
+// delivers from the row-major image (two transposed reads per fragment). The bias gradient
+// colsum(dY) is taken from the fp32 registers before rounding (per-thread partials, then a
+// fixed-order sum over the chunk's rows): it is exact fp32 as in the fp32 kernel.
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+typedef short shortx8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4w __attribute__((ext_vector_type(4)));
+constexpr int WB_BK = 32;
+
+// LDS row pitch (bf16 elements) for a pad-wide image: the 4 rows of one transposed read must
+// fall in distinct 64-byte windows of the 256-byte bank space -> pitch*2 mod 256 in {64, 192}
+constexpr int wb_pitch(int pad) { return (pad % 128 == 32 || pad % 128 == 96) ? pad : pad + 32; }
+
+// wave grid over the (MO/32) x (NO/32) tiles: the split of 4 waves with the fewest fragments
+constexpr int wb_gm(int tm, int tn) {
+  int best = 1, cost = 1 << 30;
+  for (int gm = 1; gm <= 4; gm *= 2) {
+    const int gn = 4 / gm;
+    const int c = (tm + gm - 1) / gm + (tn + gn - 1) / gn + 64 * ((tm < gm) + (tn < gn));
+    if (c < cost) { cost = c; best = gm; }
+  }
+  return best;
+}
+
+__device__ __forceinline__ bf16x8w tr_frag(const __bf16* lds_lo, const __bf16* lds_hi) {
+  typedef __attribute__((address_space(3))) shortx4* lptr;
+  const shortx4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lptr)(lds_lo));
+  const shortx4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lptr)(lds_hi));
+  const shortx8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8w, v);
+}
+
+// YB / XB: the operand is stored as bf16 in HBM (16-byte loads carry 8 elements and go to LDS
+// as they are); otherwise fp32 (4 elements per load, rounded to bf16 on the way to LDS)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <int MO_PAD, int NO_PAD, bool YB, bool XB>
+__global__ __launch_bounds__(256) void wgrad_bf16_kernel(StreamArgs a, int rows_per_block) {
+  constexpr int PY = wb_pitch(MO_PAD), PX = wb_pitch(NO_PAD);
+  constexpr int TMT = MO_PAD / 32, TNT = NO_PAD / 32;
+  constexpr int GM = wb_gm(TMT, TNT), GN = 4 / GM;
+  constexpr int TM = (TMT + GM - 1) / GM, TN = (TNT + GN - 1) / GN;
+  constexpr int VY = YB ? 8 : 4, VX = XB ? 8 : 4;  // elements per 16-byte slot
+  constexpr int ysl = WB_BK * MO_PAD / VY, xsl = WB_BK * NO_PAD / VX;
+  constexpr int MAXS = (ysl + xsl + 255) / 256;
+  constexpr int NYS = (ysl + 255) / 256;  // slots that can hold dY (column partials)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  __bf16* Ys = reinterpret_cast<__bf16*>(smem_raw);  // [2][WB_BK][PY]
+  __bf16* Xs = Ys + 2 * WB_BK * PY;                    // [2][WB_BK][PX]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Mo = a.M, No = a.N;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(a.K, r0 + rows_per_block);
+  const int wm = wave / GN, wn = wave % GN;
+  const unsigned char* Ag = reinterpret_cast<const unsigned char*>(a.A);
+  const unsigned char* Bg = reinterpret_cast<const unsigned char*>(a.B);
+  constexpr int EY = YB ? 2 : 4, EX = XB ? 2 : 4;  // bytes per element in HBM
+  u32x4 st[MAXS];
+  float ysum[NYS][VY];
+#pragma unroll
+  for (int i = 0; i < NYS; ++i)
+#pragma unroll
+    for (int e = 0; e < VY; ++e) ysum[i][e] = 0.f;
+  auto load_chunk = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < MAXS; ++i) {
+      const int s = tid + i * 256;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (s < ysl) {
+        const int kk = s / (MO_PAD / VY), c = (s % (MO_PAD / VY)) * VY, m = c0 + kk;
+        if (m < r1 && c < Mo) v = *reinterpret_cast<const u32x4*>(Ag + ((int64_t)m * a.lda + c) * EY);
+      } else if (s < ysl + xsl) {
+        const int s2 = s - ysl;
+        const int kk = s2 / (NO_PAD / VX), c = (s2 % (NO_PAD / VX)) * VX, m = c0 + kk;
+        if (m < r1 && c < No) v = *reinterpret_cast<const u32x4*>(Bg + ((int64_t)m * a.ldb + c) * EX);
+      }
+      st[i] = v;
+    }
+  };
+  auto put = [&](__bf16* dst, const u32x4& v, bool is_bf16) {
+    if (is_bf16) {
+      *reinterpret_cast<u32x4*>(dst) = v;
+    } else {
+      const floatx4 f = __builtin_bit_cast(floatx4, v);
+      bf16x4w h;
+      h[0] = (__bf16)f[0]; h[1] = (__bf16)f[1]; h[2] = (__bf16)f[2]; h[3] = (__bf16)f[3];
+      *reinterpret_cast<bf16x4w*>(dst) = h;
+    }
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < MAXS; ++i) {
+      const int s = tid + i * 256;
+      if (s < ysl) {
+        if constexpr (YB) {
+          const bf16x8w hv = __builtin_bit_cast(bf16x8w, st[i]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ysum[i < NYS ? i : 0][e] += (float)hv[e];
+        } else {
+          const floatx4 f = __builtin_bit_cast(floatx4, st[i]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ysum[i < NYS ? i : 0][e] += f[e];
+        }
+        const int kk = s / (MO_PAD / VY), c = (s % (MO_PAD / VY)) * VY;
+        put(&Ys[(buf * WB_BK + kk) * PY + c], st[i], YB);
+      } else if (s < ysl + xsl) {
+        const int s2 = s - ysl;
+        const int kk = s2 / (NO_PAD / VX), c = (s2 % (NO_PAD / VX)) * VX;
+        put(&Xs[(buf * WB_BK + kk) * PX + c], st[i], XB);
+      }
+    }
+  };
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  // transposed-read addresses: lane 4q+p of 16-lane group g reads row q (+4 for the second
+  // half of the fragment) of the block, columns 4p..4p+3 of the 16-column half (g & 1);
+  // rows 8h.. with h = g >> 1
+  const int g = lane >> 4, lq = (lane & 15) >> 2, lp = lane & 3;
+  const int trow = 8 * (g >> 1) + lq, tcol = 16 * (g & 1) + 4 * lp;
+
+  int buf = 0;
+  if (r0 < r1) {
+    load_chunk(r0);
+    store_chunk(0);
+  }
+  __syncthreads();
+  for (int c0 = r0; c0 < r1; c0 += WB_BK) {
+    const bool more = c0 + WB_BK < r1;
+    if (more) load_chunk(c0 + WB_BK);
+    const __bf16* Y = Ys + buf * WB_BK * PY;
+    const __bf16* X = Xs + buf * WB_BK * PX;
+#pragma unroll
+    for (int ks = 0; ks < WB_BK / 16; ++ks) {
+      bf16x8w af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int ti = wm * TM + i;
+        const __bf16* p = Y + (16 * ks + trow) * PY + 32 * (ti < TMT ? ti : 0) + tcol;
+        af[i] = tr_frag(p, p + 4 * PY);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int tj = wn * TN + j;
+        const __bf16* p = X + (16 * ks + trow) * PX + 32 * (tj < TNT ? tj : 0) + tcol;
+        bfr[j] = tr_frag(p, p + 4 * PX);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store_chunk(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // partial tile -> ws[block][Mo][No] (fixed-order reduce later)
+  float* out = a.ws + (int64_t)blockIdx.x * Mo * No;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ti = wm * TM + i;
+    if (ti >= TMT) continue;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int tj = wn * TN + j;
+      if (tj >= TNT) continue;
+      const int n = tj * 32 + (lane & 31);
+      if (n >= No) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = ti * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        if (m < Mo) out[(int64_t)m * No + n] = acc[i][j][e];
+      }
+    }
+  }
+  if (a.rowsum != nullptr) {
+    // per-thread column partials -> R[kk][c] (reusing the staging LDS), then rows summed in order
+    float* R = reinterpret_cast<float*>(smem_raw);
+#pragma unroll
+    for (int i = 0; i < NYS; ++i) {
+      const int s = tid + i * 256;
+      if (s < ysl)
+#pragma unroll
+        for (int e = 0; e < VY; ++e) R[s * VY + e] = ysum[i][e];
+    }
+    __syncthreads();
+    if (tid < Mo) {
+      float rsum = 0.f;
+#pragma unroll 8
+      for (int kk = 0; kk < WB_BK; ++kk) rsum += R[kk * MO_PAD + tid];
+      a.ws[(int64_t)gridDim.x * Mo * No + (int64_t)blockIdx.x * Mo + tid] = rsum;
+    }
+  }
+}
+
 int wgrad_blocks(int Kr) {
   int nb = Kr / 64;  // >= 64 rows per workgroup; short K (the MLP's B = 4096) still fills 64 CUs
   if (nb > 512) nb = 512;
@@ -574,16 +805,17 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
   float* sbias = reinterpret_cast<float*>(smem_raw + (size_t)NTN * KPH * 2);
   float* saux = sbias + NTN;  // AUX_ADD table, or LN gamma / beta
   const int tid = threadIdx.x;
-  if (a.transB) {
-    for (int idx = tid; idx < NTN * KK; idx += 512) {
-      const int n = idx / KK, k = idx % KK;
-      Bs[n * KPH + k] = (__bf16)a.B[(int64_t)n * a.ldb + k];
-    }
-  } else {
-    for (int idx = tid; idx < NTN * KK; idx += 512) {
-      const int k = idx / NTN, n = idx % NTN;
-      Bs[n * KPH + k] = (__bf16)a.B[(int64_t)k * a.ldb + n];
-    }
+  if (a.transB) {  // B = W[N][K]: rows n (dispatch: ldb % 4 == 0, 16-byte aligned)
+    stage_batched<NTN, KK, 512>(a.B, a.ldb, [&](int n, int k, const floatx4& v) {
+      bf16x4w h;
+      h[0] = (__bf16)v[0]; h[1] = (__bf16)v[1]; h[2] = (__bf16)v[2]; h[3] = (__bf16)v[3];
+      *reinterpret_cast<bf16x4w*>(Bs + n * KPH + k) = h;
+    });
+  } else {  // B = W[K][N]: rows k
+    stage_batched<KK, NTN, 512>(a.B, a.ldb, [&](int k, int n, const floatx4& v) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Bs[(n + e) * KPH + k] = (__bf16)v[e];
+    });
   }
   if constexpr ((EPI & RS_EPI_BIAS) != 0)
     for (int n = tid; n < NTN; n += 512) sbias[n] = a.bias[n];
@@ -728,6 +960,7 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   // bf16 compute mode: the bf16-MFMA instances (fp32 kernels below for anything else)
   const int ekey = (s.epi & ~RS_GEMM_BF16) | (s.beta != 0.f ? kEpiBeta : 0);
   if ((s.epi & RS_GEMM_BF16) && !small && s.vec_epi && s.M % 16 == 0 && s.K % 64 == 0 &&
+      s.ldb % 4 == 0 && aligned16(s.B) &&
       s.N == nt * 16 && s.lda % 4 == 0 && (!(s.epi & RS_EPI_AUX_ADD) || (int64_t)s.aux_mod * nt * 16 * 4 <= 48 * 1024)) {
     const int kc = s.K / 64;
     const size_t ldsb = (size_t)nt * 16 * (s.K + 8) * 2 + (size_t)(nt * 16 + ((s.epi & RS_EPI_AUX_ADD) ? s.aux_mod * nt * 16 : 0)) * 4;
@@ -799,7 +1032,8 @@ int rowgemm_ln_launch(const StreamArgs& s, hipStream_t st) {
   const int per_cu = lds > 80 * 1024 ? 1 : (lds > 53 * 1024 ? 2 : (lds > 40 * 1024 ? 3 : 4));
   if (bx > 256 * per_cu) bx = 256 * per_cu;
   const int ekey = s.epi & (RS_EPI_BIAS | RS_EPI_DROP_A);
-  if ((s.epi & RS_GEMM_BF16) && s.M % 16 == 0 && s.K % 64 == 0 && s.lda % 4 == 0) {
+  if ((s.epi & RS_GEMM_BF16) && s.M % 16 == 0 && s.K % 64 == 0 && s.lda % 4 == 0 && s.ldb % 4 == 0 &&
+      aligned16(s.B)) {
     const int kc = s.K / 64;
     const size_t ldsb = (size_t)64 * (s.K + 8) * 2 + (size_t)3 * 64 * 4;
     const int per_cub = ldsb > 80 * 1024 ? 1 : (ldsb > 53 * 1024 ? 2 : (ldsb > 40 * 1024 ? 3 : 4));
@@ -848,11 +1082,45 @@ int64_t wgrad_ws_bytes(int M, int N, int K) {
   return (int64_t)wgrad_blocks(K) * ((int64_t)M * N + M) * (int64_t)sizeof(float);
 }
 
+int wgrad_bf16_launch(const StreamArgs& s, bool y_bf16, bool x_bf16, hipStream_t st) {
+  const int mo_pad = (s.M + 31) / 32 * 32, no_pad = (s.N + 31) / 32 * 32;
+  const int nb = wgrad_blocks(s.K);
+  const int rpb = cdiv(cdiv(s.K, nb), WB_BK) * WB_BK;
+  const int nblk = cdiv(s.K, rpb);
+  const size_t stage = (size_t)2 * WB_BK * (wb_pitch(mo_pad) + wb_pitch(no_pad)) * 2;
+  const size_t red = (size_t)WB_BK * mo_pad * sizeof(float);
+  const size_t lds = stage > red ? stage : red;
+  const int key = (mo_pad * 1000 + no_pad) * 4 + (y_bf16 ? 2 : 0) + (x_bf16 ? 1 : 0);
+#define RS_WB(MOV, NOV, YB, XB)                                                    \
+  case (MOV * 1000 + NOV) * 4 + (YB ? 2 : 0) + (XB ? 1 : 0):                       \
+    wgrad_bf16_kernel<MOV, NOV, YB, XB><<<nblk, 256, lds, st>>>(s, rpb);           \
+    break;
+  switch (key) {
+    RS_WB(64, 64, false, false) RS_WB(64, 256, false, false) RS_WB(256, 64, false, false)
+    RS_WB(192, 64, false, false) RS_WB(64, 192, false, false) RS_WB(128, 128, false, false)
+    RS_WB(128, 64, false, false) RS_WB(64, 128, false, false) RS_WB(32, 64, false, false)
+    RS_WB(64, 32, false, false) RS_WB(128, 256, false, false) RS_WB(256, 128, false, false)
+    RS_WB(64, 96, false, false) RS_WB(96, 64, false, false)
+    RS_WB(64, 256, false, true) RS_WB(256, 64, true, false)  // the fused FFN's weight gradients
+    default:
+      set_error("wgrad bf16: no instance for %dx%d (bf16 operands %d/%d)", s.M, s.N, (int)y_bf16,
+                (int)x_bf16);
+      return -1;
+  }
+#undef RS_WB
+  RS_CHECK_LAUNCH("wgrad bf16");
+  const int total = s.M * s.N + (s.rowsum ? s.M : 0);
+  wgrad_reduce_kernel<<<cdiv(total, 64), 1024, 0, st>>>(s, nblk);
+  RS_CHECK_LAUNCH("wgrad reduce");
+  return 0;
+}
+
 int wgrad_launch(const StreamArgs& s, hipStream_t st) {
   const int mo_pad = (s.M + 31) / 32 * 32, no_pad = (s.N + 31) / 32 * 32;
   const int nb = wgrad_blocks(s.K);
   const int rpb = cdiv(cdiv(s.K, nb), WG_BK) * WG_BK;
   const int nblk = cdiv(s.K, rpb);
+  if (s.epi & RS_GEMM_BF16) return wgrad_bf16_launch(s, false, false, st);
   const size_t lds = (size_t)2 * WG_BK * (mo_pad + no_pad) * sizeof(float);
 #define RS_WG(MOV, NOV)                                                   \
   case MOV * 1000 + NOV:                                                  \

@@ -15,7 +15,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 
 struct DropKey {
   uint32_t k0, k1;  // per (seed, counter, site) stream keys
-  uint32_t thresh;  // keep iff hash >= thresh, thresh = p * 2^32
+  uint32_t thresh;  // keep iff the element's 16 hash bits >= thresh = floor(p * 2^16)
   float scale;      // 1 / (1 - p)
 };
 
@@ -25,8 +25,8 @@ __device__ __forceinline__ DropKey make_key(const int64_t* key, int site, float 
                                                     (uint64_t)site * 0xd1b54a32d192ed03ULL));
   k.k0 = (uint32_t)b;
   k.k1 = (uint32_t)(b >> 32);
-  const double t = (double)p * 4294967296.0;
-  k.thresh = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  const double t = (double)p * 65536.0;
+  k.thresh = t >= 65536.0 ? 65536u : (uint32_t)t;
   k.scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   return k;
 }
@@ -40,11 +40,62 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   return h;
 }
 
-// multiplier for element idx: 0 (dropped) or 1/(1-p) (kept); two 32-bit finalisers (cheap on
-// the VALU: no 64-bit multiplies) keyed by the 64-bit stream key
+// One 32-bit hash (two murmur3 finalisers keyed by the 64-bit stream key) per PAIR of elements
+// (2j, 2j+1): the low 16 bits decide element 2j, the high 16 bits element 2j+1. The hash's
+// integer multiplies are the expensive part on the VALU, so kernels that own consecutive
+// elements draw two masks per hash (keep_pair); keep_mult gives the same draw element by element.
+__device__ __forceinline__ uint32_t pair_hash(const DropKey& k, uint64_t pair) {
+  return fmix32(fmix32((uint32_t)pair ^ k.k0) + k.k1 + (uint32_t)(pair >> 32));
+}
+__device__ __forceinline__ uint32_t pair_hash32(const DropKey& k, uint32_t pair) {
+  return fmix32(fmix32(pair ^ k.k0) + k.k1);
+}
+
+// multiplier for element idx: 0 (dropped) or 1/(1-p) (kept)
 __device__ __forceinline__ float keep_mult(const DropKey& k, uint64_t idx) {
-  const uint32_t h = fmix32(fmix32((uint32_t)idx ^ k.k0) + k.k1 + (uint32_t)(idx >> 32));
-  return h >= k.thresh ? k.scale : 0.f;
+  const uint32_t h = pair_hash(k, idx >> 1);
+  const uint32_t bits = (idx & 1) ? (h >> 16) : (h & 0xffffu);
+  return bits >= k.thresh ? k.scale : 0.f;
+}
+
+// the same draw for an index known to be < 2^32 (callers check their index range on the host):
+// no 64-bit index arithmetic per element
+__device__ __forceinline__ float keep_mult32(const DropKey& k, uint32_t idx) {
+  const uint32_t h = pair_hash32(k, idx >> 1);
+  const uint32_t bits = (idx & 1) ? (h >> 16) : (h & 0xffffu);
+  return bits >= k.thresh ? k.scale : 0.f;
+}
+
+// multipliers of elements 2*pair and 2*pair + 1 from one hash
+__device__ __forceinline__ void keep_pair(const DropKey& k, uint64_t pair, float& m0, float& m1) {
+  const uint32_t h = pair_hash(k, pair);
+  m0 = (h & 0xffffu) >= k.thresh ? k.scale : 0.f;
+  m1 = (h >> 16) >= k.thresh ? k.scale : 0.f;
+}
+__device__ __forceinline__ void keep_pair32(const DropKey& k, uint32_t pair, float& m0, float& m1) {
+  const uint32_t h = pair_hash32(k, pair);
+  m0 = (h & 0xffffu) >= k.thresh ? k.scale : 0.f;
+  m1 = (h >> 16) >= k.thresh ? k.scale : 0.f;
+}
+
+// elements idx0 .. idx0+3 (idx0 even: two hashes)
+__device__ __forceinline__ void keep4(const DropKey& k, uint64_t idx0, float (&mk)[4]) {
+  if ((idx0 & 1) == 0) {
+    keep_pair(k, idx0 >> 1, mk[0], mk[1]);
+    keep_pair(k, (idx0 >> 1) + 1, mk[2], mk[3]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mk[i] = keep_mult(k, idx0 + i);
+  }
+}
+__device__ __forceinline__ void keep4_32(const DropKey& k, uint32_t idx0, float (&mk)[4]) {
+  if ((idx0 & 1) == 0) {
+    keep_pair32(k, idx0 >> 1, mk[0], mk[1]);
+    keep_pair32(k, (idx0 >> 1) + 1, mk[2], mk[3]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mk[i] = keep_mult32(k, idx0 + i);
+  }
 }
 
 }  // namespace rs

@@ -136,6 +136,12 @@ def layer_fwd(lyr, x, key_pad, B, L, d, H, p, key, site):
     h1, x1, m1, r1 = ops.linear_add_layernorm(att, sa_mod.out_proj.weight, sa_mod.out_proj.bias, x,
                                               lyr.norm1.weight, lyr.norm1.bias, lyr.norm1.eps, p, key,
                                               site + 1)
+    if ops.ffn_supported(x1, lyr.linear1.weight):
+        # bf16 mode: the whole feed-forward block in one kernel; f1 stays on chip (csrc/ffn.hip)
+        h2, x2, m2, r2, fmask = ops.ffn_fwd_bf16(x1, lyr.linear1.weight, lyr.linear1.bias,
+                                                 lyr.linear2.weight, lyr.linear2.bias, lyr.norm2.weight,
+                                                 lyr.norm2.bias, lyr.norm2.eps, p, key, site + 2, site + 3)
+        return x2, (x, qkv, att, lse, h1, x1, m1, r1, ('ffn', fmask), h2, m2, r2)
     f1 = ops.linear_fwd(x1, lyr.linear1.weight, lyr.linear1.bias, relu=True, drop_p=p, drop_key=key,
                         site_a=site + 2)  # dropout(relu(.)) fused
     h2, x2, m2, r2 = ops.linear_add_layernorm(f1, lyr.linear2.weight, lyr.linear2.bias, x1,
@@ -154,12 +160,19 @@ def layer_bwd(lyr, saved, dx2, key_pad, B, L, d, H, p, key, site):
     dh2 = ops.layernorm_bwd(h2, dx2, lyr.norm2.weight, m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias),
                             da=dff, p=p, key=key, site=site + 3)
     dff = dh2 if dff is None else dff
-    ops.linear_bwd_weight(dff, f1, g(lyr.linear2.weight), db=g(lyr.linear2.bias))
-    # f1 holds relu(.) after dropout: (f1 > 0) == kept & positive, kept scale 1/(1-p)
-    df1 = ops.linear_bwd_input(dff, lyr.linear2.weight, relu_mask_of=f1,
-                               alpha=(1.0 / (1.0 - p)) if p > 0 else 1.0)
-    ops.linear_bwd_weight(df1, x1, g(lyr.linear1.weight), db=g(lyr.linear1.bias))
-    ops.linear_bwd_input(df1, lyr.linear1.weight, out=dh2, beta=1.0)  # dx1 = dh2 + df1 W1
+    if isinstance(f1, tuple):  # fused feed-forward block (bf16 mode)
+        # dx1 = dh2 + dPre1 W1 (out of place: dff may be dh2 itself and is read again below)
+        dh2, f1b, dpre = ops.ffn_bwd_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight,
+                                          f1[1], dff, dh2, p)
+        ops.wgrad_bf16(dff, f1b, g(lyr.linear2.weight), db=g(lyr.linear2.bias))
+        ops.wgrad_bf16(dpre, x1, g(lyr.linear1.weight), db=g(lyr.linear1.bias))
+    else:
+        ops.linear_bwd_weight(dff, f1, g(lyr.linear2.weight), db=g(lyr.linear2.bias))
+        # f1 holds relu(.) after dropout: (f1 > 0) == kept & positive, kept scale 1/(1-p)
+        df1 = ops.linear_bwd_input(dff, lyr.linear2.weight, relu_mask_of=f1,
+                                   alpha=(1.0 / (1.0 - p)) if p > 0 else 1.0)
+        ops.linear_bwd_weight(df1, x1, g(lyr.linear1.weight), db=g(lyr.linear1.bias))
+        ops.linear_bwd_input(df1, lyr.linear1.weight, out=dh2, beta=1.0)  # dx1 = dh2 + df1 W1
     # x1 = LN1(x + drop1(sa))
     dsa = torch.empty_like(dh2) if p > 0 else None
     dh1 = ops.layernorm_bwd(h1, dh2, lyr.norm1.weight, m1, r1, g(lyr.norm1.weight), g(lyr.norm1.bias),

@@ -5,6 +5,8 @@ current stream handle; all arithmetic runs in librsys_hip.so.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _hip, precision
@@ -78,6 +80,51 @@ def linear_bwd_weight(dy, x, dW, *, beta=1.0, db=None):
     K = x.shape[1]
     return gemm(dy, x, dW, N, K, M, transA=1, transB=0, lda=dy.stride(0), ldb=x.stride(0),
                 ldc=dW.stride(0), beta=beta, rowsum=db)
+
+
+def ffn_supported(x, W1):
+    """The fused feed-forward block: bf16 compute mode, d_model 64, dim_feedforward 256."""
+    return (precision.compute_dtype() == 'bf16' and not os.environ.get('RSYS_UNFUSED_FFN') and
+            x.dim() == 2 and x.shape[1] == 64 and
+            tuple(W1.shape) == (256, 64) and x.shape[0] % 16 == 0 and x.is_contiguous())
+
+
+def ffn_fwd_bf16(x, W1, b1, W2, b2, gamma, beta, eps, p, key, site1, site2):
+    """x2 = LN(x + drop2(linear2(drop(relu(linear1(x)))))) -> (h, x2, mean, rstd, mask)."""
+    M, F = x.shape[0], W1.shape[0]
+    dev = x.device
+    h = torch.empty(M, 64, device=dev)
+    y = torch.empty(M, 64, device=dev)
+    mean = torch.empty(M, device=dev)
+    rstd = torch.empty(M, device=dev)
+    mask = torch.empty(int(_hip.lib().rs_ffn_mask_words(M, F)), dtype=torch.int64, device=dev)
+    call('rs_ffn_fwd_bf16', M, F, P(x), P(W1), P(b1), P(W2), P(b2), P(gamma), P(beta), float(eps), P(h),
+         P(y), P(mean), P(rstd), P(mask), float(p), P(key), site1, site2, stream())
+    return h, y, mean, rstd, mask
+
+
+def ffn_bwd_bf16(x, W1, b1, W2, mask, dff, dres, p, dx=None):
+    """-> (dx = dres + dPre1 W1, f1 bf16 [M,F], dPre1 bf16 [M,F])."""
+    M, F = x.shape[0], W1.shape[0]
+    dev = x.device
+    if dx is None:
+        dx = torch.empty_like(dres)
+    f1 = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    dpre = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    call('rs_ffn_bwd_bf16', M, F, P(x), P(W1), P(b1), P(W2), P(mask), P(dff), P(dres), P(dx), P(f1), P(dpre),
+         float(p), stream())
+    return dx, f1, dpre
+
+
+def wgrad_bf16(dy, x, dW, *, db=None, beta=1.0):
+    """dW[Mo,No] = beta*dW + dy[rows,Mo]^T x[rows,No] on bf16 MFMA; db += colsum(dy). dy / x may be
+    fp32 or bf16 tensors."""
+    rows, Mo = dy.shape
+    No = x.shape[1]
+    w = ws(_hip.lib().rs_wgrad_ws_bytes(Mo, No, rows), dy.device)
+    call('rs_wgrad_bf16', rows, Mo, No, P(dy), dy.stride(0), int(dy.dtype == torch.bfloat16), P(x), x.stride(0),
+         int(x.dtype == torch.bfloat16), float(beta), P(dW), dW.stride(0), P(db), P(w), stream())
+    return dW
 
 
 def colsum(X, out, *, scale=1.0, beta=1.0, M=None, N=None, ldx=None):
