@@ -241,6 +241,16 @@ int rs_catalog_gather(const void* cat, int elem, int widen, int64_t V, int F, in
                       const int64_t* ids, int B, int N, int64_t ld_ids, void* out, int64_t ld_out,
                       int* err_flag, void* stream);
 
+/* ---------------------------------------------------------------- device batch assembly
+ * The ragged part of collate_fn (DataLoader.py:250-288; per tower in CombineTwoTower.py:62-92):
+ * rows idx[0..B) of a CSR list column (values [nnz, tw] int32 (elem 4) or int64 (elem 8),
+ * offsets [rows + 1] int64) -> out [B, Lb, tw] int64, zero right-padded (np.pad(..., 0)); Lb >=
+ * the longest selected list (the caller's batch maximum, as the reference pads to it). Row index
+ * out of range: zeros, *err_flag |= 1; a list longer than Lb: truncated, *err_flag |= 2.
+ * Fixed-width columns (sparse id matrix, dense matrix) use rs_catalog_gather with N = 1. */
+int rs_collate_ragged(const void* values, int elem, int tw, const int64_t* offsets, int64_t rows,
+                      const int64_t* idx, int B, int Lb, int64_t* out, int* err_flag, void* stream);
+
 /* ---------------------------------------------------------------- validation / Recall@K
  * The reference's validate() (training_utils.py:121-275) on the device: scores = U I_all^T via
  * rs_gemm_f32, then

@@ -69,6 +69,7 @@ SIGNATURES = {
     'rs_mask_history': (i32, [vp, i64, i32, i64, i64, vp, i64, vp, vp, i64, vp]),
     'rs_topk_rows': (i32, [vp, i64, i32, i32, i32, vp, i64, i32, vp, vp, i64, vp]),
     'rs_recall_hits': (i32, [vp, i32, i32, vp, vp, i64, vp, i32, vp, vp]),
+    'rs_collate_ragged': (i32, [vp, i32, i32, vp, i64, vp, i32, i32, vp, vp, vp]),
     'rs_catalog_gather': (i32, [vp, i32, i32, i64, i32, i64, vp, i32, i32, i64, vp, i64, vp, vp]),
     'rs_sqnorm_ws_bytes': (i64, [i64]),
     'rs_grad_sqnorm': (i32, [vp, i64, f32, vp, vp]),

@@ -1,0 +1,297 @@
+"""GPU batch assembly -- drop-in for CombineTwoTower.CombinedTwoTowerDataLoader.
+
+The reference builds every batch on the host: per-sample `RecommendationDataset.__getitem__`
+(DataLoader.py:220-240), then `collate_fn` (:250-288) stacks the id / dense matrices and pads
+each list feature to the longest list of the batch with np.pad, per tower
+(CombineTwoTower.py:62-92) -- SURVEY §6 measured ~80k samples/s for that path, far below what the
+training step consumes. Here the columns live in HBM once:
+
+* `TowerColumns` -- one tower's columns in the reference's matrix layout
+  (`_build_feature_matrices`, DataLoader.py:129-205): the non-pooled sparse ids [N, S] (int32 when
+  the values fit), the dense matrix [N, Dn] fp32, and every list feature (pooled sparse features,
+  then sequence features) as CSR: values [nnz, T] (T = tags per token for lists of lists) and
+  offsets [N + 1]. `feature_column_mapping` is the reference's `get_feature_column_mapping()`.
+* `ColumnarDataset` -- the user and item towers of one interaction table; `save(dir)` / `load(dir)`
+  is the on-disk columnar format (one .npy per array + meta.json, loaded with allow_pickle=False).
+* `DeviceCombinedLoader` -- iterates batches ON THE DEVICE: the row indices of a batch go through
+  rs_catalog_gather (fixed-width matrices) and rs_collate_ragged (lists -> [B, Lb(, T)] int64,
+  zero right-padded, Lb = the batch's longest list as in the reference). The batch dicts have the
+  reference's keys, dtypes and shapes. With shuffle=True the epoch order is the one torch's
+  DataLoader(shuffle=True) draws from the default generator (`reference_shuffle_order`), so under
+  the same torch.manual_seed the batches are the reference's batches.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import torch
+
+from recommendsystemproject_amd import _hip
+
+
+def _tower_feature_lists(tower_cfg):
+    """(sparse matrix columns, dense columns, list columns) in the reference's order."""
+    sparse, lists = [], []
+    for f in tower_cfg.get('sparse_features') or []:
+        (lists if 'pooling' in f else sparse).append(f['name'])
+    dense = [f['name'] for f in tower_cfg.get('dense_features') or []]
+    lists += [f['name'] for f in tower_cfg.get('sequence_features') or []]
+    return sparse, dense, lists
+
+
+def _to_csr(cells):
+    """A column of lists (1-D) or lists of lists (2-D, equal inner width) -> (values [nnz, T],
+    offsets [N + 1] int64, ndim)."""
+    lens = np.fromiter((len(c) for c in cells), dtype=np.int64, count=len(cells))
+    offsets = np.zeros(len(cells) + 1, dtype=np.int64)
+    np.cumsum(lens, out=offsets[1:])
+    first = next((c for c in cells if len(c) > 0), None)
+    if first is None:
+        return np.zeros((0, 1), dtype=np.int32), offsets, 1
+    two_d = np.ndim(first[0]) == 1 if not isinstance(first, np.ndarray) else first.ndim == 2
+    if two_d:
+        T = len(first[0])
+        flat = [np.asarray(c, dtype=np.int64).reshape(-1, T) for c in cells if len(c) > 0]
+        values = np.concatenate(flat, axis=0)
+    else:
+        values = np.concatenate([np.asarray(c, dtype=np.int64).reshape(-1) for c in cells if len(c) > 0])
+        values = values.reshape(-1, 1)
+    if values.size and values.min() >= -2 ** 31 and values.max() < 2 ** 31:
+        values = values.astype(np.int32)
+    return np.ascontiguousarray(values), offsets, 2 if two_d else 1
+
+
+class TowerColumns:
+    """One tower's columns (see the module docstring)."""
+
+    def __init__(self, n, sparse=None, dense=None, lists=None, mapping=None):
+        self.n = int(n)
+        self.sparse = sparse          # [N, S] int32/int64 or None
+        self.dense = dense            # [N, Dn] float32 or None
+        self.lists = lists or {}      # name -> (values [nnz, T], offsets [N+1], ndim)
+        self.mapping = mapping or {'sparse': {}, 'dense': {}, 'sequence': {}}
+
+    @classmethod
+    def from_dataframe(cls, df, tower_cfg):
+        """DataLoader.py:129-205 (`_build_feature_matrices`) into the columnar layout."""
+        sparse_cols, dense_cols, list_cols = _tower_feature_lists(tower_cfg)
+        for c in sparse_cols + dense_cols + list_cols:
+            if c not in df.columns:
+                raise ValueError(f"Feature '{c}' column '{c}' not found in DataFrame. "
+                                 f"Available columns: {list(df.columns)}")
+        sparse = None
+        if sparse_cols:
+            sparse = np.stack([df[c].to_numpy() for c in sparse_cols], axis=1).astype(np.int64)
+            if sparse.size and sparse.min() >= -2 ** 31 and sparse.max() < 2 ** 31:
+                sparse = sparse.astype(np.int32)
+            sparse = np.ascontiguousarray(sparse)
+        dense = None
+        if dense_cols:
+            dense = np.ascontiguousarray(np.stack([df[c].to_numpy().astype(np.float32) for c in dense_cols],
+                                                  axis=1))
+        lists = {}
+        for c in list_cols:
+            cells = df[c].tolist()
+            if len(cells) == 0:
+                raise AttributeError(f"No data was provided in the feature: {c}")
+            lists[c] = _to_csr(cells)
+        mapping = {'sparse': {c: i for i, c in enumerate(sparse_cols)},
+                   'dense': {c: i for i, c in enumerate(dense_cols)},
+                   'sequence': {c: c for c in list_cols}}
+        return cls(len(df), sparse, dense, lists, mapping)
+
+    def save(self, path, prefix):
+        meta = {'n': self.n, 'mapping': self.mapping, 'lists': {}}
+        if self.sparse is not None:
+            np.save(os.path.join(path, f'{prefix}.sparse.npy'), self.sparse)
+        if self.dense is not None:
+            np.save(os.path.join(path, f'{prefix}.dense.npy'), self.dense)
+        for name, (vals, offs, nd) in self.lists.items():
+            np.save(os.path.join(path, f'{prefix}.{name}.values.npy'), vals)
+            np.save(os.path.join(path, f'{prefix}.{name}.offsets.npy'), offs)
+            meta['lists'][name] = nd
+        return meta
+
+    @classmethod
+    def load(cls, path, prefix, meta):
+        def get(name):
+            f = os.path.join(path, f'{prefix}.{name}.npy')
+            return np.load(f, allow_pickle=False) if os.path.exists(f) else None
+        lists = {name: (get(f'{name}.values'), get(f'{name}.offsets'), int(nd))
+                 for name, nd in meta['lists'].items()}
+        return cls(meta['n'], get('sparse'), get('dense'), lists, meta['mapping'])
+
+    def lengths(self, name):
+        offs = self.lists[name][1]
+        return offs[1:] - offs[:-1]
+
+
+class ColumnarDataset:
+    """The user / item towers of one interaction table (CombineTwoTower.py:34-46)."""
+
+    def __init__(self, user: TowerColumns, item: TowerColumns):
+        if user.n != item.n:
+            raise AssertionError('User and item datasets must have same length')
+        self.user, self.item = user, item
+
+    def __len__(self):
+        return self.user.n
+
+    @classmethod
+    def from_dataframe(cls, df, config):
+        tt = config['two_tower']
+        return cls(TowerColumns.from_dataframe(df, tt['user_tower']),
+                   TowerColumns.from_dataframe(df, tt['item_tower']))
+
+    def save(self, path):
+        os.makedirs(path, exist_ok=True)
+        meta = {'format': 'rsys-columnar-1', 'user': self.user.save(path, 'user'),
+                'item': self.item.save(path, 'item')}
+        with open(os.path.join(path, 'meta.json'), 'w') as f:
+            json.dump(meta, f)
+
+    @classmethod
+    def load(cls, path):
+        with open(os.path.join(path, 'meta.json')) as f:
+            meta = json.load(f)
+        if meta.get('format') != 'rsys-columnar-1':
+            raise ValueError(f'{path}: not a columnar dataset')
+        return cls(TowerColumns.load(path, 'user', meta['user']), TowerColumns.load(path, 'item', meta['item']))
+
+
+def reference_shuffle_order(n):
+    """The order torch.utils.data.DataLoader(shuffle=True, num_workers=0) visits n samples in,
+    drawn from the default generator the same way: the iterator first draws its base seed, then
+    RandomSampler seeds a generator from a second draw and takes randperm(n)."""
+    torch.empty((), dtype=torch.int64).random_()  # _BaseDataLoaderIter._base_seed
+    seed = int(torch.empty((), dtype=torch.int64).random_().item())
+    g = torch.Generator()
+    g.manual_seed(seed)
+    return torch.randperm(n, generator=g).numpy()
+
+
+class _DeviceTower:
+    def __init__(self, cols: TowerColumns, device):
+        self.cols = cols
+        self.device = device
+        up = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+        self.sparse = up(cols.sparse)
+        self.dense = up(cols.dense)
+        self.lists = {k: (up(v), up(o), nd) for k, (v, o, nd) in cols.lists.items()}
+        self.lens = {k: cols.lengths(k) for k in cols.lists}
+
+    def batch(self, idx, B, lb, err, stream):
+        out = {}
+        if self.sparse is not None:
+            S = int(self.sparse.shape[1])
+            t = torch.empty(B, S, dtype=torch.int64, device=self.device)
+            _hip.call('rs_catalog_gather', self.sparse.data_ptr(), self.sparse.element_size(),
+                      int(self.sparse.dtype == torch.int32), self.cols.n, S, S, idx.data_ptr(), B, 1, 1,
+                      t.data_ptr(), S, err.data_ptr(), stream)
+            out['sparse'] = t
+        if self.dense is not None:
+            Dn = int(self.dense.shape[1])
+            t = torch.empty(B, Dn, dtype=torch.float32, device=self.device)
+            _hip.call('rs_catalog_gather', self.dense.data_ptr(), 4, 0, self.cols.n, Dn, Dn, idx.data_ptr(), B, 1,
+                      1, t.data_ptr(), Dn, err.data_ptr(), stream)
+            out['dense'] = t
+        if self.lists:
+            seq = {}
+            for name, (vals, offs, nd) in self.lists.items():
+                T = int(vals.shape[1])
+                L = int(lb[name])
+                t = torch.empty((B, L, T) if nd == 2 else (B, L), dtype=torch.int64, device=self.device)
+                _hip.call('rs_collate_ragged', vals.data_ptr(), vals.element_size(), T, offs.data_ptr(), self.cols.n,
+                          idx.data_ptr(), B, L, t.data_ptr(), err.data_ptr(), stream)
+                seq[name] = t
+            out['sequence'] = seq
+        return out
+
+
+class DeviceCombinedLoader:
+    """CombinedTwoTowerDataLoader (CombineTwoTower.py:13-105) with the collate on the device.
+
+    data: a pandas DataFrame (the reference's pickle content), a ColumnarDataset, or the directory
+    of a saved ColumnarDataset. Batches are dicts {'user_tower': {...}, 'item_tower': {...}} of
+    device tensors (sparse int64 [B, S], dense float32 [B, Dn], sequence {name: int64 [B, Lb] or
+    [B, Lb, T]}); the last batch may be short (DataLoader's drop_last=False default).
+    """
+
+    def __init__(self, config, data, batch_size=512, shuffle=True, device='cuda',
+                 hard_negatives_enabled=False, drop_last=False, num_workers=0):
+        if isinstance(config, str):
+            from recommendsystemproject_amd.project.utils.config_utils import file_loader
+            config = file_loader(config)
+        if isinstance(data, str):
+            data = ColumnarDataset.load(data)
+        elif not isinstance(data, ColumnarDataset):
+            data = ColumnarDataset.from_dataframe(data, config)
+        self.data = data
+        self.batch_size = int(batch_size)
+        self.shuffle = shuffle
+        self.drop_last = drop_last
+        self.device = torch.device(device)
+        self.hard_negatives_enabled = hard_negatives_enabled
+        self.user = _DeviceTower(data.user, self.device)
+        self.item = _DeviceTower(data.item, self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        del num_workers  # the collate runs on the device; no host workers
+
+    def __len__(self):
+        n, B = len(self.data), self.batch_size
+        return n // B if self.drop_last else (n + B - 1) // B
+
+    def _batch_max(self, tower, order, nb):
+        """Per batch, per list feature: the longest list (the reference pads to it)."""
+        B, n = self.batch_size, len(order)
+        res = []
+        for k in range(nb):
+            res.append({})
+        for name, lens in tower.lens.items():
+            sel = lens[order]
+            pad = (-n) % B
+            if pad:
+                sel = np.concatenate([sel, np.zeros(pad, dtype=sel.dtype)])
+            mx = sel.reshape(-1, B).max(axis=1)
+            for k in range(nb):
+                res[k][name] = int(mx[k])
+        return res
+
+    def __iter__(self):
+        n = len(self.data)
+        order = reference_shuffle_order(n) if self.shuffle else np.arange(n, dtype=np.int64)
+        nb = len(self)
+        ulb = self._batch_max(self.user, order, nb)
+        ilb = self._batch_max(self.item, order, nb)
+        order_dev = torch.from_numpy(np.ascontiguousarray(order, dtype=np.int64)).to(self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        for k in range(nb):
+            s = k * self.batch_size
+            e = min(n, s + self.batch_size)
+            idx = order_dev[s:e]
+            B = e - s
+            yield {'user_tower': self.user.batch(idx, B, ulb[k], self.err, stream),
+                   'item_tower': self.item.batch(idx, B, ilb[k], self.err, stream)}
+
+    def check_errors(self):
+        """Raise if a gather saw an index or a list length it could not honour (host sync)."""
+        v = int(self.err.item())
+        if v:
+            self.err.zero_()
+            raise IndexError(f'device collate error flags {v:#x}')
+
+    def get_feature_mappings(self):
+        return {'user': self.data.user.mapping, 'item': self.data.item.mapping}
+
+
+def create_device_dataloader(config_path, data, batch_size=None, shuffle=True, device='cuda',
+                             hard_negatives_enabled=False):
+    """create_combined_dataloader (CombineTwoTower.py:108-140) for the device loader."""
+    from recommendsystemproject_amd.project.utils.config_utils import file_loader
+    config = file_loader(config_path) if isinstance(config_path, str) else config_path
+    if batch_size is None:
+        batch_size = config['train']['batch_size']
+    return DeviceCombinedLoader(config, data, batch_size=batch_size, shuffle=shuffle, device=device,
+                                hard_negatives_enabled=hard_negatives_enabled)
