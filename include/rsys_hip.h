@@ -167,13 +167,15 @@ int rs_seq_mask(const int64_t* seq, int64_t ld_seq, int B, int L, int64_t pad_va
  * Masked multi-head self-attention core on packed qkv [B*L, 3d] (in_proj output), heads of
  * hd = d/H columns; out [B*L, d]; lse [B*H*L] saved for backward. Replaces the SDPA math path
  * inside nn.MultiheadAttention (SequenceEncoder.py:17-29 via TransformerEncoderLayer, K6).
- * p > 0: dropout on the attention probabilities with the rs_dropout mask of (key, site). */
+ * p > 0: dropout on the attention probabilities with the rs_dropout mask of (key, site).
+ * flags: RS_GEMM_BF16 -> the products on bf16 MFMA (operands rounded to bf16; softmax, dropout
+ * and dS arithmetic in fp32) where the MFMA kernels apply (head_dim 16, L <= 64), else 0. */
 int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out, float* lse,
                 int B, int L, int d, int H, float scale, float p, const int64_t* key, int site,
-                void* stream);
+                int flags, void* stream);
 int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float* out, const float* dout,
                 const float* lse, float* dqkv, int B, int L, int d, int H, float scale, float p,
-                const int64_t* key, int site, void* stream);
+                const int64_t* key, int site, int flags, void* stream);
 
 /* ---------------------------------------------------------------- layer norm (post-LN)
  * h = dropout(a) + b (written back into a), y = LN(h)*gamma + beta; mean/rstd [M] saved.

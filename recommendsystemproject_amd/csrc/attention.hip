@@ -447,6 +447,246 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(
     }
 }
 
+// ------------------------------------------------------------------ bf16 MFMA (bf16 mode)
+// Same structure as the f32 MFMA kernels (one wave per (b, h), S^T tiles with the key on the
+// row so each lane owns one query), on v_mfma_f32_16x16x16_bf16: with head_dim 16 every 16x16
+// product is ONE instruction instead of four 16x16x4 f32 ones. Operand maps (16x16x16): lane
+// (r = l&15, q = l>>4) supplies A[r][4q + j] and B[4q + j][r], j < 4 -- the same registers the
+// f32 kernels feed one k-slice at a time, so Q/K/V/dO rows load as before and the softmax /
+// dropout / dS arithmetic (fp32) is unchanged. The B operands that need a column per lane
+// (V for P V; K, Q, dO for dQ, dK, dV) are read once per wave through LDS before the loops.
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ s4v bf4(const f4& v) {
+  bf4v h;
+  h[0] = (__bf16)v[0]; h[1] = (__bf16)v[1]; h[2] = (__bf16)v[2]; h[3] = (__bf16)v[3];
+  return __builtin_bit_cast(s4v, h);
+}
+__device__ __forceinline__ f4 mfma16(const s4v& a, const s4v& b, const f4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+// column r, rows 16t + 4q + j of a per-wave [LP][kRowP] fp32 image
+template <int NT>
+__device__ __forceinline__ void col_frags(const float (*X)[kRowP], int r, int q, s4v (&out)[NT]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    f4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = X[t * 16 + 4 * q + j][r];
+    out[t] = bf4(v);
+  }
+}
+
+template <int NT, bool DROP>
+__global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
+    const float* __restrict__ qkv, const uint8_t* __restrict__ key_pad, float* __restrict__ out,
+    float* __restrict__ lse, int B, int L, int d, int H, float scale, float pdrop,
+    const int64_t* __restrict__ key, int site) {
+  constexpr int LP = NT * 16;
+  __shared__ __attribute__((aligned(16))) float Vsm[4][LP][kRowP];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int bh = blockIdx.x * 4 + wave;
+  if (bh >= B * H) return;  // whole wave exits together (no block barrier below)
+  const int b = bh / H, h = bh % H;
+  const int ld = 3 * d;
+  const float* base = qkv + (int64_t)b * L * ld + h * 16;
+  float(*Vs)[kRowP] = Vsm[wave];
+  s4v qb[NT], kb[NT], vb[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int row = t * 16 + r;
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    qb[t] = bf4(row < L ? ld4(base + (int64_t)row * ld + 4 * q) : z);
+    kb[t] = bf4(row < L ? ld4(base + (int64_t)row * ld + d + 4 * q) : z);
+    *reinterpret_cast<f4*>(&Vs[row][4 * q]) = row < L ? ld4(base + (int64_t)row * ld + 2 * d + 4 * q) : z;
+  }
+  bool kok[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = t * 16 + 4 * q + e;
+      kok[t][e] = j < L && key_pad[(int64_t)b * L + j] == 0;
+    }
+  DropKey dk;
+  if (DROP) dk = make_key(key, site, pdrop);
+  const float scale2 = scale * kLog2e;
+  __builtin_amdgcn_wave_barrier();  // Vs written by this wave only
+  col_frags<NT>(Vs, r, q, vb);      // B of P V: V[16 tk + 4q + j][c = r]
+#pragma unroll
+  for (int tq = 0; tq < NT; ++tq) {
+    f4 sv[NT];
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) sv[tk] = mfma16(kb[tk], qb[tq], f4{0.f, 0.f, 0.f, 0.f});
+    float m = -INFINITY;
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (kok[tk][e]) m = fmaxf(m, sv[tk][e] * scale2);
+    m = xmax(m);
+    float l = 0.f;
+    const int i = tq * 16 + r;
+    const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) {
+      float mk[4] = {1.f, 1.f, 1.f, 1.f};
+      if (DROP) keep4_32(dk, rowbase + tk * 16 + 4 * q, mk);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = kok[tk][e] ? exp2f(sv[tk][e] * scale2 - m) : 0.f;
+        l += pv;
+        sv[tk][e] = DROP ? pv * mk[e] : pv;
+      }
+    }
+    l = xsum(l);
+    f4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) o = mfma16(bf4(sv[tk]), vb[tk], o);
+    if (q == 0 && i < L) lse[(int64_t)bh * L + i] = (m + log2f(l)) * kLn2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float le = __shfl(l, 4 * q + e, 64);
+      const int row = tq * 16 + 4 * q + e;
+      if (row < L) out[((int64_t)b * L + row) * d + h * 16 + r] = o[e] * (1.f / le);
+    }
+  }
+}
+
+template <int NT, bool DROP>
+__global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
+    const float* __restrict__ qkv, const uint8_t* __restrict__ key_pad,
+    const float* __restrict__ out, const float* __restrict__ dout, const float* __restrict__ lse,
+    float* __restrict__ dqkv, int B, int L, int d, int H, float scale, float pdrop,
+    const int64_t* __restrict__ key, int site) {
+  constexpr int LP = NT * 16;
+  constexpr int TP = 20;
+  // one 5 KB image per wave: Q, K and dO pass through it once (column fragments), then it is the
+  // transpose buffer of P∘Z and dS
+  __shared__ __attribute__((aligned(16))) float Xsm[4][LP][kRowP];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int bh = blockIdx.x * 4 + wave;
+  if (bh >= B * H) return;
+  const int b = bh / H, h = bh % H;
+  const int ld = 3 * d;
+  const float* base = qkv + (int64_t)b * L * ld + h * 16;
+  const float* gbase = dout + (int64_t)b * L * d + h * 16;
+  const float* obase = out + (int64_t)b * L * d + h * 16;
+  float(*X)[kRowP] = Xsm[wave];
+  float* T = &Xsm[wave][0][0];
+  f4 qf[NT], kf[NT], gf[NT];
+  s4v qb[NT], kb[NT], vb[NT], gb[NT];
+  float Di[NT], lsei[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int row = t * 16 + r;
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    const bool ok = row < L;
+    qf[t] = ok ? ld4(base + (int64_t)row * ld + 4 * q) : z;
+    kf[t] = ok ? ld4(base + (int64_t)row * ld + d + 4 * q) : z;
+    vb[t] = bf4(ok ? ld4(base + (int64_t)row * ld + 2 * d + 4 * q) : z);
+    gf[t] = ok ? ld4(gbase + (int64_t)row * d + 4 * q) : z;
+    const f4 of = ok ? ld4(obase + (int64_t)row * d + 4 * q) : z;
+    Di[t] = xsum(gf[t][0] * of[0] + gf[t][1] * of[1] + gf[t][2] * of[2] + gf[t][3] * of[3]);
+    lsei[t] = ok ? lse[(int64_t)bh * L + row] * kLog2e : 0.f;
+  }
+  // column fragments (B operands of dQ = dS K, dK = dS^T Q, dV = PZ^T dO) via the LDS image
+  s4v qc[NT], kc[NT], gc[NT];
+#pragma unroll
+  for (int pass = 0; pass < 3; ++pass) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      *reinterpret_cast<f4*>(&X[t * 16 + r][4 * q]) = pass == 0 ? qf[t] : (pass == 1 ? kf[t] : gf[t]);
+    __builtin_amdgcn_wave_barrier();
+    if (pass == 0) col_frags<NT>(X, r, q, qc);
+    else if (pass == 1) col_frags<NT>(X, r, q, kc);
+    else col_frags<NT>(X, r, q, gc);
+    __builtin_amdgcn_wave_barrier();
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    qb[t] = bf4(qf[t]);
+    kb[t] = bf4(kf[t]);
+    gb[t] = bf4(gf[t]);
+  }
+  bool kok[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = t * 16 + 4 * q + e;
+      kok[t][e] = j < L && key_pad[(int64_t)b * L + j] == 0;
+    }
+  DropKey dk;
+  if (DROP) dk = make_key(key, site, pdrop);
+  const float scale2 = scale * kLog2e;
+  float* dbase = dqkv + (int64_t)b * L * ld + h * 16;
+  f4 dv_acc[NT], dk_acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) dv_acc[t] = dk_acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int tq = 0; tq < NT; ++tq) {
+    const int i = tq * 16 + r;
+    const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
+    f4 ps[NT], ds[NT];
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) {
+      const f4 sacc = mfma16(kb[tk], qb[tq], f4{0.f, 0.f, 0.f, 0.f});  // S^T[key][query]
+      const f4 pacc = mfma16(vb[tk], gb[tq], f4{0.f, 0.f, 0.f, 0.f});  // dP^T = V dO^T
+      float mk[4] = {1.f, 1.f, 1.f, 1.f};
+      if (DROP) keep4_32(dk, rowbase + tk * 16 + 4 * q, mk);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = (kok[tk][e] && i < L) ? exp2f(sacc[e] * scale2 - lsei[tq]) : 0.f;
+        const float z = DROP ? mk[e] : 1.f;
+        ds[tk][e] = pv * (z * pacc[e] - Di[tq]);
+        ps[tk][e] = pv * z;
+      }
+    }
+    f4 dq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) dq = mfma16(bf4(ds[tk]), kc[tk], dq);  // dS[query][key] K
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = tq * 16 + 4 * q + e;
+      if (row < L) dbase[(int64_t)row * ld + r] = dq[e] * scale;
+    }
+    // dV[key][c] += PZ^T dO and dK[key][c] += dS^T Q: A = [key = lane & 15][query], i.e. the
+    // transpose of this lane's tiles, through T (T[key][query])
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) T[(tk * 16 + 4 * q + e) * TP + r] = ps[tk][e];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+      dv_acc[tk] = mfma16(bf4(ld4(&T[(tk * 16 + r) * TP + 4 * q])), gc[tq], dv_acc[tk]);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) T[(tk * 16 + 4 * q + e) * TP + r] = ds[tk][e];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+      dk_acc[tk] = mfma16(bf4(ld4(&T[(tk * 16 + r) * TP + 4 * q])), qc[tq], dk_acc[tk]);
+    __builtin_amdgcn_wave_barrier();
+  }
+#pragma unroll
+  for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = tk * 16 + 4 * q + e;
+      if (row < L) {
+        dbase[(int64_t)row * ld + d + r] = dk_acc[tk][e] * scale;
+        dbase[(int64_t)row * ld + 2 * d + r] = dv_acc[tk][e];
+      }
+    }
+}
+
 int threads_for(int L) {
   int t = ((L + 63) / 64) * 64;
   return t > 256 ? 256 : t;
@@ -472,7 +712,7 @@ using namespace rs;
 
 extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out, float* lse,
                            int B, int L, int d, int H, float scale, float p, const int64_t* key,
-                           int site, void* stream) {
+                           int site, int flags, void* stream) {
   RS_CHECK_ARG(qkv && key_pad && out && lse, "rs_attn_fwd: null pointer");
   RS_CHECK_ARG(B >= 0 && L >= 1 && H >= 1 && d % H == 0, "rs_attn_fwd: bad shape");
   RS_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || key), "rs_attn_fwd: bad dropout p=%f", p);
@@ -486,9 +726,12 @@ extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out,
   if (hd == 16 && L <= 64 && (int64_t)B * H * L * L < ((int64_t)1 << 32) && !getenv_flag("RSYS_ATTN_VALU")) {
     const int nt = (L + 15) / 16;
     const dim3 g4(cdiv((int64_t)B * H, 4));
+    const bool bf = (flags & RS_GEMM_BF16) != 0;
 #define RS_AF(NTV)                                                                                  \
   if (nt == NTV) {                                                                                  \
-    if (p > 0.f) attn_fwd_mfma_kernel<NTV, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    if (bf && p > 0.f) attn_fwd_bf16_kernel<NTV, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    else if (bf) attn_fwd_bf16_kernel<NTV, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    else if (p > 0.f) attn_fwd_mfma_kernel<NTV, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
     else attn_fwd_mfma_kernel<NTV, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
   }
     RS_AF(1) RS_AF(2) RS_AF(3) RS_AF(4)
@@ -505,7 +748,7 @@ extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out,
 
 extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float* out,
                            const float* dout, const float* lse, float* dqkv, int B, int L, int d,
-                           int H, float scale, float p, const int64_t* key, int site,
+                           int H, float scale, float p, const int64_t* key, int site, int flags,
                            void* stream) {
   RS_CHECK_ARG(qkv && key_pad && out && dout && lse && dqkv, "rs_attn_bwd: null pointer");
   RS_CHECK_ARG(B >= 0 && L >= 1 && H >= 1 && d % H == 0, "rs_attn_bwd: bad shape");
@@ -521,9 +764,12 @@ extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float
     RS_CHECK_ARG(aligned16(out), "rs_attn_bwd: needs 16-byte aligned rows");
     const int nt = (L + 15) / 16;
     const dim3 g4(cdiv((int64_t)B * H, 4));
+    const bool bf = (flags & RS_GEMM_BF16) != 0;
 #define RS_AB(NTV)                                                                                  \
   if (nt == NTV) {                                                                                  \
-    if (p > 0.f) attn_bwd_mfma_kernel<NTV, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    if (bf && p > 0.f) attn_bwd_bf16_kernel<NTV, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    else if (bf) attn_bwd_bf16_kernel<NTV, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    else if (p > 0.f) attn_bwd_mfma_kernel<NTV, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
     else attn_bwd_mfma_kernel<NTV, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
   }
     RS_AB(1) RS_AB(2) RS_AB(3) RS_AB(4)

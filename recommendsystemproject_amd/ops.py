@@ -165,14 +165,14 @@ def attn_fwd(qkv, key_pad, B, L, d, H, p=0.0, key=None, site=0):
     out = torch.empty(B * L, d, device=qkv.device, dtype=torch.float32)
     lse = torch.empty(B * H * L, device=qkv.device, dtype=torch.float32)
     call('rs_attn_fwd', P(qkv), P(key_pad), P(out), P(lse), B, L, d, H,
-         float((d // H) ** -0.5), float(p), P(key), site, stream())
+         float((d // H) ** -0.5), float(p), P(key), site, precision.gemm_flags(), stream())
     return out, lse
 
 
 def attn_bwd(qkv, key_pad, out, dout, lse, B, L, d, H, p=0.0, key=None, site=0):
     dqkv = torch.empty(B * L, 3 * d, device=qkv.device, dtype=torch.float32)
     call('rs_attn_bwd', P(qkv), P(key_pad), P(out), P(dout), P(lse), P(dqkv), B, L, d, H,
-         float((d // H) ** -0.5), float(p), P(key), site, stream())
+         float((d // H) ** -0.5), float(p), P(key), site, precision.gemm_flags(), stream())
     return dqkv
 
 

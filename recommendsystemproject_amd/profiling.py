@@ -71,7 +71,41 @@ def _adam_work(a):
     return 12.0 * n, 28.0 * n
 
 
+def _gemm_ln_work(a):
+    M, N, K = a[0], a[1], a[2]
+    # A, W read; resid read; h, y written; mean / rstd
+    return 2.0 * M * N * K, 4.0 * (M * K + N * K + 3 * M * N + 2 * M)
+
+
+def _ffn_fwd_work(a):
+    M, F = a[0], a[1]
+    # x read (GEMM operand + residual: once from HBM), h, y written, mask bits, mean / rstd
+    return 4.0 * M * F * 64, 4.0 * (3 * M * 64 + 2 * M) + M * F / 8.0
+
+
+def _ffn_bwd_work(a):
+    M, F = a[0], a[1]
+    # x, dff, dres read, dx written (fp32); f1, dPre1 written (bf16); mask bits read
+    return 6.0 * M * F * 64, 4.0 * 4 * M * 64 + 2.0 * 2 * M * F + M * F / 8.0
+
+
+def _wgrad_work(a):
+    rows, Mo, No = a[0], a[1], a[2]
+    return 2.0 * rows * Mo * No, rows * (Mo * (2 if a[5] else 4) + No * (2 if a[8] else 4))
+
+
+def _ce_work(a, bwd=False):
+    B = a[8]
+    return 0.0, 4.0 * B * B * 2  # fwd: two passes over S; bwd: S read + dS written
+
+
 WORK = {
+    'rs_gemm_add_layernorm': _gemm_ln_work,
+    'rs_ffn_fwd_bf16': _ffn_fwd_work,
+    'rs_ffn_bwd_bf16': _ffn_bwd_work,
+    'rs_wgrad_bf16': _wgrad_work,
+    'rs_inbatch_ce_fwd': _ce_work,
+    'rs_inbatch_ce_bwd': lambda a: _ce_work(a, True),
     'rs_gemm_f32': _gemm_work,
     'rs_attn_fwd': _attn_fwd_work,
     'rs_attn_bwd': _attn_bwd_work,

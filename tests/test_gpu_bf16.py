@@ -242,3 +242,78 @@ def test_bf16_step_fused_ffn_vs_unfused(monkeypatch):
     (l1, g1), (l2, g2) = res['fused'], res['unfused']
     assert abs(l1 - l2) < 1e-4 * abs(l2), (l1, l2)
     assert F.cosine_similarity(g1, g2, dim=0).item() > 0.9999
+
+
+def _bf16_attention_ref(qkv, key_pad, dout, B, L, d, H):
+    """The bf16 MFMA attention's arithmetic in float64: Q, K, V, dO rounded to bf16; the
+    unnormalised probabilities and dS rounded to bf16 where they enter a product; softmax,
+    dropout-free dS and the scale in full precision."""
+    hd = d // H
+    q, k, v = (r16(t).double() for t in qkv.view(B, L, 3, H, hd).permute(2, 0, 3, 1, 4))
+    g = r16(dout).double().view(B, L, H, hd).transpose(1, 2)
+    sc = hd ** -0.5
+    s = q @ k.transpose(-1, -2)
+    mask = key_pad.bool()[:, None, None, :]
+    s = s.masked_fill(mask, float('-inf'))
+    m = (s * sc).amax(-1, keepdim=True)
+    e = torch.exp(s * sc - m).masked_fill(mask, 0.0)
+    l = e.sum(-1, keepdim=True)
+    out = (r16(e.float()).double() @ v) / l
+    P = e / l
+    dp = g @ v.transpose(-1, -2)
+    o32 = out.transpose(1, 2).reshape(B * L, d).float()
+    D = (dout.double().view(B, L, H, hd).transpose(1, 2) * o32.double().view(B, L, H, hd).transpose(1, 2)).sum(-1, keepdim=True)
+    ds = P * (dp - D)
+    dsb, Pb = r16(ds.float()).double(), r16(P.float()).double()
+    dq = dsb @ k * sc
+    dk = dsb.transpose(-1, -2) @ q * sc
+    dv = Pb.transpose(-1, -2) @ g
+    dqkv = torch.stack([dq, dk, dv], 0).permute(1, 3, 0, 2, 4).reshape(B * L, 3 * d)
+    return o32, dqkv.float()
+
+
+@pytest.mark.parametrize('B,L', [(3, 50), (5, 16), (4, 33), (2, 64), (3, 1)])
+def test_bf16_attention(B, L, bf16_mode):
+    d, H = 64, 4
+    qkv = rnd(B * L, 3 * d, seed=11)
+    lens = torch.randint(1, L + 1, (B,))
+    seq = (torch.arange(L)[None, :] < lens[:, None]).long().to(DEV)
+    key_pad, _ = ops.seq_mask(seq, 0)
+    dout = rnd(B * L, d, seed=12)
+    out, lse = ops.attn_fwd(qkv, key_pad, B, L, d, H)
+    dqkv = ops.attn_bwd(qkv, key_pad, out, dout, lse, B, L, d, H)
+    ro, rd = _bf16_attention_ref(qkv, key_pad, dout, B, L, d, H)
+    # an fp32 value next to a bf16 rounding boundary may round the other way than in float64:
+    # single-ulp (2^-8) flips of a probability bound the worst element; the mean stays tight
+    for a, b_ in ((out, ro), (dqkv, rd)):
+        sc = b_.abs().max().item()
+        err = (a - b_).abs()
+        assert err.max().item() < 5e-3 * sc, (err.max().item(), sc)
+        assert err.mean().item() < 1e-4 * sc, (err.mean().item(), sc)
+    # and it is not the fp32 kernel
+    precision.set_compute_dtype('fp32')
+    out32, _ = ops.attn_fwd(qkv, key_pad, B, L, d, H)
+    precision.set_compute_dtype('bf16')
+    if L > 1:
+        assert not torch.equal(out, out32)
+
+
+def test_bf16_attention_dropout_matches_fp32_masks(bf16_mode):
+    """Same dropout masks as the fp32 MFMA kernel (the draw is per element): results agree to
+    bf16 precision, and differ clearly from the no-dropout output."""
+    B, L, d, H, p = 6, 50, 64, 4, 0.2
+    qkv = rnd(B * L, 3 * d, seed=13)
+    key_pad = torch.zeros(B, L, dtype=torch.uint8, device=DEV)
+    key = torch.tensor([77, 3], dtype=torch.int64, device=DEV)
+    dout = rnd(B * L, d, seed=14)
+    o16, l16 = ops.attn_fwd(qkv, key_pad, B, L, d, H, p, key, 5)
+    g16 = ops.attn_bwd(qkv, key_pad, o16, dout, l16, B, L, d, H, p, key, 5)
+    precision.set_compute_dtype('fp32')
+    o32, l32 = ops.attn_fwd(qkv, key_pad, B, L, d, H, p, key, 5)
+    g32 = ops.attn_bwd(qkv, key_pad, o32, dout, l32, B, L, d, H, p, key, 5)
+    o0, _ = ops.attn_fwd(qkv, key_pad, B, L, d, H, 0.0)
+    precision.set_compute_dtype('bf16')
+    scale = o32.abs().max().item()
+    assert (o16 - o32).abs().max().item() < 2e-2 * scale
+    assert (o0 - o32).abs().max().item() > 0.2 * scale
+    assert (g16 - g32).abs().max().item() < 3e-2 * g32.abs().max().item()
