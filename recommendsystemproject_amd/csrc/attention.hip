@@ -466,14 +466,14 @@ __device__ __forceinline__ s4v bf4(const f4& v) {
 __device__ __forceinline__ f4 mfma16(const s4v& a, const s4v& b, const f4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
-// column r, rows 16t + 4q + j of a per-wave [LP][kRowP] fp32 image
-template <int NT>
-__device__ __forceinline__ void col_frags(const float (*X)[kRowP], int r, int q, s4v (&out)[NT]) {
+// column r, rows 16t + 4q + j of a per-wave [LP][P] fp32 image
+template <int NT, int P>
+__device__ __forceinline__ void col_frags(const float* X, int r, int q, s4v (&out)[NT]) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     f4 v;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = X[t * 16 + 4 * q + j][r];
+    for (int j = 0; j < 4; ++j) v[j] = X[(t * 16 + 4 * q + j) * P + r];
     out[t] = bf4(v);
   }
 }
@@ -513,8 +513,8 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
   DropKey dk;
   if (DROP) dk = make_key(key, site, pdrop);
   const float scale2 = scale * kLog2e;
-  __builtin_amdgcn_wave_barrier();  // Vs written by this wave only
-  col_frags<NT>(Vs, r, q, vb);      // B of P V: V[16 tk + 4q + j][c = r]
+  __builtin_amdgcn_wave_barrier();            // Vs written by this wave only
+  col_frags<NT, kRowP>(&Vs[0][0], r, q, vb);  // B of P V: V[16 tk + 4q + j][c = r]
 #pragma unroll
   for (int tq = 0; tq < NT; ++tq) {
     f4 sv[NT];
@@ -562,10 +562,12 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
     float* __restrict__ dqkv, int B, int L, int d, int H, float scale, float pdrop,
     const int64_t* __restrict__ key, int site) {
   constexpr int LP = NT * 16;
-  constexpr int TP = 20;
-  // one 5 KB image per wave: Q, K and dO pass through it once (column fragments), then it is the
+  // pitch 24: the transpose's ds_read_b128 (rows r, columns 4q) is conflict-free; its b32 writes
+  // are 2-way, which costs nothing for ds_write_b32 (MI355X_MICROARCH.md §LDS)
+  constexpr int TP = 24;
+  // one 6 KB image per wave: Q, K and dO pass through it once (column fragments), then it is the
   // transpose buffer of P∘Z and dS
-  __shared__ __attribute__((aligned(16))) float Xsm[4][LP][kRowP];
+  __shared__ __attribute__((aligned(16))) float Xsm[4][LP * TP];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
   const int bh = blockIdx.x * 4 + wave;
@@ -575,8 +577,7 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
   const float* base = qkv + (int64_t)b * L * ld + h * 16;
   const float* gbase = dout + (int64_t)b * L * d + h * 16;
   const float* obase = out + (int64_t)b * L * d + h * 16;
-  float(*X)[kRowP] = Xsm[wave];
-  float* T = &Xsm[wave][0][0];
+  float* T = Xsm[wave];
   f4 qf[NT], kf[NT], gf[NT];
   s4v qb[NT], kb[NT], vb[NT], gb[NT];
   float Di[NT], lsei[NT];
@@ -599,11 +600,11 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
   for (int pass = 0; pass < 3; ++pass) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
-      *reinterpret_cast<f4*>(&X[t * 16 + r][4 * q]) = pass == 0 ? qf[t] : (pass == 1 ? kf[t] : gf[t]);
+      *reinterpret_cast<f4*>(&T[(t * 16 + r) * TP + 4 * q]) = pass == 0 ? qf[t] : (pass == 1 ? kf[t] : gf[t]);
     __builtin_amdgcn_wave_barrier();
-    if (pass == 0) col_frags<NT>(X, r, q, qc);
-    else if (pass == 1) col_frags<NT>(X, r, q, kc);
-    else col_frags<NT>(X, r, q, gc);
+    if (pass == 0) col_frags<NT, TP>(T, r, q, qc);
+    else if (pass == 1) col_frags<NT, TP>(T, r, q, kc);
+    else col_frags<NT, TP>(T, r, q, gc);
     __builtin_amdgcn_wave_barrier();
   }
 #pragma unroll

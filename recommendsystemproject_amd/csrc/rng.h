@@ -40,15 +40,18 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   return h;
 }
 
-// One 32-bit hash (two murmur3 finalisers keyed by the 64-bit stream key) per PAIR of elements
-// (2j, 2j+1): the low 16 bits decide element 2j, the high 16 bits element 2j+1. The hash's
-// integer multiplies are the expensive part on the VALU, so kernels that own consecutive
-// elements draw two masks per hash (keep_pair); keep_mult gives the same draw element by element.
-__device__ __forceinline__ uint32_t pair_hash(const DropKey& k, uint64_t pair) {
-  return fmix32(fmix32((uint32_t)pair ^ k.k0) + k.k1 + (uint32_t)(pair >> 32));
-}
+// One 32-bit hash per PAIR of elements (2j, 2j+1): the low 16 bits decide element 2j, the high
+// 16 bits element 2j+1. The hash is the murmur3 finaliser (a bijection with full avalanche) of
+// the pair index keyed by the 64-bit stream key (k0 before, k1 after); its two integer
+// multiplies are the expensive part on the VALU, so kernels that own consecutive elements draw
+// two masks per hash (keep_pair); keep_mult gives the same draw element by element.
 __device__ __forceinline__ uint32_t pair_hash32(const DropKey& k, uint32_t pair) {
-  return fmix32(fmix32(pair ^ k.k0) + k.k1);
+  return fmix32(pair ^ k.k0) ^ k.k1;
+}
+__device__ __forceinline__ uint32_t pair_hash(const DropKey& k, uint64_t pair) {
+  // indices >= 2^33 fold their high word in (an odd multiple keeps distinct pairs distinct
+  // within a 2^32 window); below 2^33 this is pair_hash32
+  return pair_hash32(k, (uint32_t)pair ^ ((uint32_t)(pair >> 32) * 0x9e3779b9u));
 }
 
 // multiplier for element idx: 0 (dropped) or 1/(1-p) (kept)

@@ -1,6 +1,6 @@
 """Run the encoder attention forward + backward a few times at the C2 shape (for rocprofv3 --pmc).
 
-    python tools/attn_one.py [B] [L] [p]
+    python tools/attn_one.py [B] [L] [p] [fp32|bf16]
 """
 import os
 import sys
@@ -8,13 +8,14 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from recommendsystemproject_amd import ops  # noqa: E402
+from recommendsystemproject_amd import ops, precision  # noqa: E402
 
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     L = int(sys.argv[2]) if len(sys.argv) > 2 else 50
     p = float(sys.argv[3]) if len(sys.argv) > 3 else 0.1
+    precision.set_compute_dtype(sys.argv[4] if len(sys.argv) > 4 else 'fp32')
     d, H = 64, 4
     dev = torch.device('cuda:0')
     qkv = torch.randn(B * L, 3 * d, device=dev)
