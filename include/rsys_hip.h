@@ -227,6 +227,22 @@ int rs_inbatch_ce_bwd(float* S, int ld_s, const float* U, const float* Hn,
                       int64_t h_row_stride, int64_t h_slot_stride,
                       const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T,
                       const float* lse, const float* grad_out, float* dhl, void* stream);
+/* The same loss with S never stored (bf16 compute mode; D = 64 or 128): the 32 x 32 tiles of
+ * U I^T are recomputed on bf16 MFMA where needed -- an online log-sum-exp per user in the
+ * forward, dU = dS I and dI = dS^T U accumulated from dS tiles held in registers in the
+ * backward (fixed-order split reduction). Same semantics as the pair above (collision mask,
+ * hard negatives, mean); the products run on bf16-rounded U, I. ws: rs_inbatch_ce_fused_ws_bytes.
+ * The backward writes dU, dI (overwrite) and dhl; rs_hardneg_bwd then adds the hard-negative
+ * terms to dU and writes dH. */
+int64_t rs_inbatch_ce_fused_ws_bytes(int B, int D);
+int rs_inbatch_ce_fused_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
+                            int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
+                            int N, int D, float T, float* lse, float* row_loss, float* loss, float* ws,
+                            void* stream);
+int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
+                            int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
+                            int N, int D, float T, const float* lse, const float* grad_out, float* dU,
+                            float* dI, float* dhl, float* ws, void* stream);
 /* dU[i] += sum_n dhl[i,n] H[i,n];  dH[i,n] = dhl[i,n] U[i]   (hard-negative bmm backward; dH in
  * the layout of H) */
 int rs_hardneg_bwd(const float* U, const float* Hn, int64_t h_row_stride, int64_t h_slot_stride,

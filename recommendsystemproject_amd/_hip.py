@@ -63,6 +63,10 @@ SIGNATURES = {
     'rs_batchnorm_bwd': (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]),
     'rs_l2norm_fwd': (i32, [vp, vp, vp, i32, i32, f32, vp]),
     'rs_l2norm_bwd': (i32, [vp, vp, vp, vp, i32, i32, f32, vp]),
+    'rs_inbatch_ce_fused_ws_bytes': (i64, [i32, i32]),
+    'rs_inbatch_ce_fused_fwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp]),
+    'rs_inbatch_ce_fused_bwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp,
+                                      vp]),
     'rs_inbatch_ce_fwd': (i32, [vp, i32, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp]),
     'rs_inbatch_ce_bwd': (i32, [vp, i32, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp]),
     'rs_hardneg_bwd': (i32, [vp, vp, i64, i64, vp, vp, vp, i32, i32, i32, vp]),

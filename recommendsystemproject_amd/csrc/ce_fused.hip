@@ -1,0 +1,402 @@
+// In-batch sampled-softmax loss with the batch similarity never stored (bf16 compute mode).
+//
+// Reference: TwoTowerModel.compute_loss (TwoTowerModel.py:81-140): logits = U I^T / T, the
+// off-diagonal entries whose item ids collide set to -1e9 (trap T12), the N hard-negative
+// logits U_i . H_in / T appended, cross_entropy(logits, arange(B)), mean over the batch.
+//
+// The unfused path writes S = U I^T ([B, B] fp32, 64 MB at B = 4096), reads it twice for the
+// log-sum-exp, rewrites it as dS and reads it twice more for dU = dS I and dI = dS^T U. Here the
+// 32 x 32 tiles of S are recomputed on v_mfma_f32_32x32x16_bf16 wherever they are needed and
+// consumed in registers:
+//   fwd : per user, an online (max, sum-exp) over its item tiles -> partials per column split;
+//   dU  : per user block, dS^T tiles (items x users) become the B operand of dU^T += I^T dS^T
+//         with no data movement (an accumulator tile summed over its ROW index is already a
+//         bf16 operand after pairwise packing); I^T comes from the staged item tile through
+//         ds_read_b64_tr_b16;
+//   dI  : the same kernel with the roles of U and I exchanged (dI^T += U^T dS).
+// One kernel template serves all three: the wave OWNS 32 rows (users for fwd / dU, items for
+// dI) whose bf16 fragments stay in registers, and streams 32-row tiles of the other matrix
+// through LDS. Column splits give >= 256 workgroups at B = 4096; their partials are reduced in
+// a fixed order (deterministic).
+#include "common.h"
+
+namespace rs {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+typedef short shortx8 __attribute__((ext_vector_type(8)));
+
+constexpr int kOwnW = 32;    // owned rows per wave
+constexpr int kWaves = 4;    // owned rows per workgroup: 128
+constexpr int kTile = 32;    // streamed rows per tile
+constexpr float kMasked = -1e9f;
+
+struct HStrideArgs {
+  int64_t row, slot;  // hard-negative H element (i, n, c) at i*row + n*slot + c
+};
+
+struct CeArgs {
+  const float* own;     // [B, D] owned rows (U for fwd / dU, I for dI)
+  const float* str;     // [B, D] streamed rows
+  int B;
+  float invT;
+  const int64_t* ids;   // nullable: item ids (collision mask)
+  int64_t id_stride;
+  int split_rows;       // streamed rows per column split (multiple of kTile)
+  const float* lse;     // bwd: [B] natural log-sum-exp per user
+  const float* grad_out;  // bwd: d loss (nullable -> 1)
+  float* part_m;        // fwd: [NS][B]
+  float* part_s;        // fwd: [NS][B]
+  float* diag;          // fwd: [B] S_ii / T
+  float* part_d;        // bwd: [NS][B][D]
+};
+
+__device__ __forceinline__ bf16x8 cvt8(const floatx4& a, const floatx4& b) {
+  bf16x8 r;
+  r[0] = (__bf16)a[0]; r[1] = (__bf16)a[1]; r[2] = (__bf16)a[2]; r[3] = (__bf16)a[3];
+  r[4] = (__bf16)b[0]; r[5] = (__bf16)b[1]; r[6] = (__bf16)b[2]; r[7] = (__bf16)b[3];
+  return r;
+}
+
+__device__ __forceinline__ bf16x8 tr_frag(const __bf16* lo, const __bf16* hi) {
+  typedef __attribute__((address_space(3))) shortx4* lptr;
+  const shortx4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lptr)(lo));
+  const shortx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lptr)(hi));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// MODE 0: forward statistics (own = U, str = I)
+// MODE 1: dU (own = U, str = I; lse of the owned user)
+// MODE 2: dI (own = I, str = U; lse of the streamed user)
+template <int D, int MODE>
+__global__ __launch_bounds__(256) void ce_tile_kernel(CeArgs a) {
+  constexpr int KS = D / 16;          // 32x32x16 k-steps over the embedding
+  constexpr int PT = D + 8;           // LDS pitch (bf16) of a streamed tile row
+  constexpr int DB = D / 32;          // 32-wide blocks of the gradient
+  __shared__ __attribute__((aligned(16))) __bf16 Ts[2][kTile * PT];
+  __shared__ int64_t sid[2][kTile];
+  __shared__ float slse[2][kTile];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int B = a.B;
+  const int o = blockIdx.x * (kOwnW * kWaves) + wave * kOwnW + c;  // this lane's owned row
+  const bool o_ok = o < B;
+  const int t_begin = blockIdx.y * a.split_rows;
+  const int t_end = min(B, t_begin + a.split_rows);
+
+  // owned fragments: B operand of the S tile, lane (c, h) holds own[o][16 s + 8 h .. +7]
+  bf16x8 ob[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    floatx4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = x0;
+    if (o_ok) {
+      const float* p = a.own + (int64_t)o * D + 16 * s + 8 * h;
+      x0 = *reinterpret_cast<const floatx4*>(p);
+      x1 = *reinterpret_cast<const floatx4*>(p + 4);
+    }
+    ob[s] = cvt8(x0, x1);
+  }
+  const int64_t id_o = (a.ids && o_ok) ? a.ids[(int64_t)o * a.id_stride] : 0;
+  float g = 0.f, lse_o = 0.f;
+  if constexpr (MODE != 0) {
+    g = (a.grad_out ? *a.grad_out : 1.f) / (float)B * a.invT;  // d loss / d S = dlogits / T
+    if constexpr (MODE == 1) lse_o = o_ok ? a.lse[o] : 0.f;
+  }
+  float run_m = -INFINITY, run_s = 0.f;  // fwd: online statistics of this lane's values
+  floatx16 gacc[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) gacc[i][e] = 0.f;
+
+  // streamed tile staging: 32 rows x D fp32 -> bf16 LDS, 256 threads, float4 each
+  constexpr int SL = kTile * D / 4 / 256;  // float4 slots per thread
+  floatx4 st[SL];
+  auto load_tile = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < SL; ++i) {
+      const int slot = tid + 256 * i;
+      const int row = slot / (D / 4), col = (slot % (D / 4)) * 4;
+      const int t = t0 + row;
+      st[i] = t < B ? *reinterpret_cast<const floatx4*>(a.str + (int64_t)t * D + col) : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store_tile = [&](int buf, int t0) {
+#pragma unroll
+    for (int i = 0; i < SL; ++i) {
+      const int slot = tid + 256 * i;
+      const int row = slot / (D / 4), col = (slot % (D / 4)) * 4;
+      bf16x4 v;
+      v[0] = (__bf16)st[i][0]; v[1] = (__bf16)st[i][1]; v[2] = (__bf16)st[i][2]; v[3] = (__bf16)st[i][3];
+      *reinterpret_cast<bf16x4*>(&Ts[buf][row * PT + col]) = v;
+    }
+    if (tid < kTile) {
+      const int t = t0 + tid;
+      sid[buf][tid] = (a.ids && t < B) ? a.ids[(int64_t)t * a.id_stride] : 0;
+      if constexpr (MODE == 2) slse[buf][tid] = t < B ? a.lse[t] : 0.f;
+    }
+  };
+
+  int buf = 0;
+  if (t_begin < t_end) {
+    load_tile(t_begin);
+    store_tile(0, t_begin);
+  }
+  __syncthreads();
+  for (int t0 = t_begin; t0 < t_end; t0 += kTile) {
+    const bool more = t0 + kTile < t_end;
+    if (more) load_tile(t0 + kTile);
+    const __bf16* T = Ts[buf];
+    // S^T tile: C[t][o] = str[t] . own[o]; A = streamed rows (lane c: row t0 + c)
+    floatx16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(&T[c * PT + 16 * s + 8 * h]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, ob[s], acc, 0, 0, 0);
+    }
+    // element e of this lane: streamed row t = t0 + 8(e>>2) + 4h + (e&3), owned column o
+    if constexpr (MODE == 0) {
+      float v[16];
+      float tm = -INFINITY;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int tl = 8 * (e >> 2) + 4 * h + (e & 3);
+        const int t = t0 + tl;
+        float x = acc[e] * a.invT;
+        if (t == o && o_ok) a.diag[o] = x;
+        if (a.ids && t != o && sid[buf][tl] == id_o) x = kMasked;
+        if (t >= B) x = -INFINITY;
+        v[e] = x;
+        tm = fmaxf(tm, x);
+      }
+      const float nm = fmaxf(run_m, tm);
+      if (nm != -INFINITY) {  // a lane may see only padding rows (t >= B) so far
+        float ss = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) ss += __expf(v[e] - nm);
+        run_s = (run_m == -INFINITY ? 0.f : run_s * __expf(run_m - nm)) + ss;
+        run_m = nm;
+      }
+    } else {
+      // dS^T tile -> bf16 operand fragments (k-step 0: registers 0..7, k-step 1: 8..15)
+      bf16x8 xf[2];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int tl = 8 * (e >> 2) + 4 * h + (e & 3);
+        const int t = t0 + tl;
+        const float x = acc[e] * a.invT;
+        const bool collide = a.ids && t != o && sid[buf][tl] == id_o;  // logit -1e9: P = 0
+        const float l = MODE == 1 ? lse_o : slse[buf][tl];
+        const float p = collide ? 0.f : __expf(x - l);
+        const float dv = (t >= B || !o_ok) ? 0.f : g * (p - (t == o ? 1.f : 0.f));
+        xf[e >> 3][e & 7] = (__bf16)dv;
+      }
+      // grad^T[d][o] += sum_t str^T[d][t] dS^T[t][o]: A = transposed streamed tile,
+      // element j of lane half h <-> tile row 16 kstep + 8 (j>>2) + 4 h + (j&3)
+      const int g16 = lane >> 4, lq = (lane & 15) >> 2, lp = lane & 3;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int r0 = 16 * k + 4 * (g16 >> 1) + lq;
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+          const __bf16* p = &T[r0 * PT + 32 * db + 16 * (g16 & 1) + 4 * lp];
+          const bf16x8 af = tr_frag(p, p + 8 * PT);
+          gacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, xf[k], gacc[db], 0, 0, 0);
+        }
+      }
+    }
+    if (more) store_tile(buf ^ 1, t0 + kTile);
+    __syncthreads();
+    buf ^= 1;
+  }
+  const int split = blockIdx.y;
+  if constexpr (MODE == 0) {
+    // merge the two lane halves (same owned row, different streamed rows)
+    const float om = __shfl_xor(run_m, 32, 64), os = __shfl_xor(run_s, 32, 64);
+    const float nm = fmaxf(run_m, om);
+    const float ns = (nm == -INFINITY) ? 0.f
+                                       : (run_m == -INFINITY ? 0.f : run_s * __expf(run_m - nm)) +
+                                             (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    if (h == 0 && o_ok) {
+      a.part_m[(int64_t)split * B + o] = nm;
+      a.part_s[(int64_t)split * B + o] = ns;
+    }
+  } else {
+    // gacc[db] element e: d = 32 db + 8(e>>2) + 4h + (e&3), owned row o = lane column
+    if (o_ok) {
+      float* out = a.part_d + ((int64_t)split * B + o) * D;
+#pragma unroll
+      for (int db = 0; db < DB; ++db)
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const floatx4 v = {gacc[db][4 * e4], gacc[db][4 * e4 + 1], gacc[db][4 * e4 + 2], gacc[db][4 * e4 + 3]};
+          *reinterpret_cast<floatx4*>(out + 32 * db + 8 * e4 + 4 * h) = v;
+        }
+    }
+  }
+}
+
+// per user row: merge the split statistics with the hard-negative logits -> lse, row loss
+__global__ __launch_bounds__(256) void ce_finish_fwd_kernel(const float* __restrict__ part_m,
+                                                            const float* __restrict__ part_s,
+                                                            const float* __restrict__ diag, int NS,
+                                                            const float* __restrict__ U,
+                                                            const float* __restrict__ Hn,
+                                                            int64_t hs_row, int64_t hs_slot, int B,
+                                                            int N, int D, float invT,
+                                                            float* __restrict__ lse,
+                                                            float* __restrict__ row_loss) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + wave;
+  if (i >= B) return;
+  float hl = -INFINITY;  // lane n < N: hard-negative logit n
+  for (int n = 0; n < N; ++n) {
+    const float* hp = Hn + (int64_t)i * hs_row + (int64_t)n * hs_slot;
+    float sacc = 0.f;
+    for (int cc = lane; cc < D; cc += 64) sacc += U[(int64_t)i * D + cc] * hp[cc];
+    sacc = wave_sum(sacc) * invT;
+    if (lane == n) hl = sacc;
+  }
+  float m = lane < NS ? part_m[(int64_t)lane * B + i] : -INFINITY;
+  m = fmaxf(m, hl);
+  m = wave_max(m);
+  float s = 0.f;
+  if (lane < NS) s += part_s[(int64_t)lane * B + i] * __expf(part_m[(int64_t)lane * B + i] - m);
+  if (lane < N) s += __expf(hl - m);
+  s = wave_sum(s);
+  if (lane == 0) {
+    const float l = m + logf(s);
+    lse[i] = l;
+    row_loss[i] = l - diag[i];
+  }
+}
+
+// hard-negative logit gradients dhl[i, n] = g * exp(l_in - lse_i) (the in-batch part is fused)
+__global__ __launch_bounds__(256) void ce_hard_bwd_kernel(const float* __restrict__ U,
+                                                          const float* __restrict__ Hn,
+                                                          int64_t hs_row, int64_t hs_slot, int B,
+                                                          int N, int D, float invT,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ grad_out,
+                                                          float* __restrict__ dhl) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + wave;
+  if (i >= B) return;
+  const float g = (grad_out ? *grad_out : 1.f) / (float)B * invT;
+  for (int n = 0; n < N; ++n) {
+    const float* hp = Hn + (int64_t)i * hs_row + (int64_t)n * hs_slot;
+    float sacc = 0.f;
+    for (int cc = lane; cc < D; cc += 64) sacc += U[(int64_t)i * D + cc] * hp[cc];
+    sacc = wave_sum(sacc) * invT;
+    if (lane == 0) dhl[(int64_t)i * N + n] = g * __expf(sacc - lse[i]);
+  }
+}
+
+// out[r][d] = sum over splits (fixed order) of part[s][r][d]
+__global__ void ce_reduce_kernel(const float* __restrict__ part, int NS, int64_t n,
+                                 float* __restrict__ out) {
+  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4;
+  if (i >= n) return;
+  floatx4 acc = *reinterpret_cast<const floatx4*>(part + i);
+  for (int s = 1; s < NS; ++s) acc += *reinterpret_cast<const floatx4*>(part + (int64_t)s * n + i);
+  *reinterpret_cast<floatx4*>(out + i) = acc;
+}
+
+int splits_for(int B) {
+  const int blocks = cdiv(B, kOwnW * kWaves);
+  int ns = cdiv(256, blocks);
+  const int max_ns = cdiv(B, kTile);
+  if (ns > max_ns) ns = max_ns;
+  if (ns > 64) ns = 64;  // ce_finish reads the partials with one lane each
+  return ns < 1 ? 1 : ns;
+}
+
+template <int MODE>
+int launch_tiles(const CeArgs& a, int D, int NS, hipStream_t st) {
+  const dim3 grid(cdiv(a.B, kOwnW * kWaves), NS);
+  if (D == 128) ce_tile_kernel<128, MODE><<<grid, 256, 0, st>>>(a);
+  else ce_tile_kernel<64, MODE><<<grid, 256, 0, st>>>(a);
+  return 0;
+}
+
+}  // namespace
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int64_t rs_inbatch_ce_fused_ws_bytes(int B, int D) {
+  const int NS = splits_for(B);
+  const int64_t fwd = (int64_t)NS * B * 2 + B;
+  const int64_t bwd = (int64_t)NS * B * D;
+  return (fwd > bwd ? fwd : bwd) * (int64_t)sizeof(float);
+}
+
+extern "C" int rs_inbatch_ce_fused_fwd(const float* U, const float* I, const float* Hn,
+                                       int64_t h_row_stride, int64_t h_slot_stride,
+                                       const int64_t* item_ids, int64_t id_stride, int B, int N,
+                                       int D, float T, float* lse, float* row_loss, float* loss,
+                                       float* ws, void* stream) {
+  RS_CHECK_ARG(U && I && lse && row_loss && loss && ws, "rs_inbatch_ce_fused_fwd: null pointer");
+  RS_CHECK_ARG(B >= 1 && (D == 64 || D == 128) && N >= 0 && N <= 64,
+               "rs_inbatch_ce_fused_fwd: needs D in {64, 128}, N <= 64 (B=%d N=%d D=%d)", B, N, D);
+  RS_CHECK_ARG(N == 0 || Hn, "rs_inbatch_ce_fused_fwd: hard negatives need H");
+  RS_CHECK_ARG(aligned16(U) && aligned16(I), "rs_inbatch_ce_fused_fwd: U, I must be 16-byte aligned");
+  hipStream_t st = as_stream(stream);
+  const int NS = splits_for(B);
+  CeArgs a{};
+  a.own = U; a.str = I; a.B = B; a.invT = 1.f / T; a.ids = item_ids; a.id_stride = id_stride;
+  a.split_rows = cdiv(cdiv(B, NS), kTile) * kTile;
+  a.part_m = ws; a.part_s = ws + (int64_t)NS * B; a.diag = ws + (int64_t)2 * NS * B;
+  const int NSr = cdiv(B, a.split_rows);
+  launch_tiles<0>(a, D, NSr, st);
+  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_fwd tiles");
+  const HStrideArgs hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
+  ce_finish_fwd_kernel<<<cdiv(B, 4), 256, 0, st>>>(a.part_m, a.part_s, a.diag, NSr, U, Hn, hs.row, hs.slot, B,
+                                                   N, D, a.invT, lse, row_loss);
+  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_fwd finish");
+  return rs_sum(row_loss, B, 1.f / (float)B, loss, stream);
+}
+
+extern "C" int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const float* Hn,
+                                       int64_t h_row_stride, int64_t h_slot_stride,
+                                       const int64_t* item_ids, int64_t id_stride, int B, int N,
+                                       int D, float T, const float* lse, const float* grad_out,
+                                       float* dU, float* dI, float* dhl, float* ws, void* stream) {
+  RS_CHECK_ARG(U && I && lse && dU && dI && ws, "rs_inbatch_ce_fused_bwd: null pointer");
+  RS_CHECK_ARG(B >= 1 && (D == 64 || D == 128) && N >= 0 && N <= 64, "rs_inbatch_ce_fused_bwd: bad shape");
+  RS_CHECK_ARG(N == 0 || (Hn && dhl), "rs_inbatch_ce_fused_bwd: hard negatives need H, dhl");
+  RS_CHECK_ARG(aligned16(U) && aligned16(I) && aligned16(dU) && aligned16(dI),
+               "rs_inbatch_ce_fused_bwd: operands must be 16-byte aligned");
+  hipStream_t st = as_stream(stream);
+  const int NS = splits_for(B);
+  CeArgs a{};
+  a.B = B; a.invT = 1.f / T; a.ids = item_ids; a.id_stride = id_stride; a.lse = lse; a.grad_out = grad_out;
+  a.split_rows = cdiv(cdiv(B, NS), kTile) * kTile;
+  a.part_d = ws;
+  const int NSr = cdiv(B, a.split_rows);
+  const int64_t n = (int64_t)B * D;
+  // dU: users owned, items streamed
+  a.own = U; a.str = I;
+  launch_tiles<1>(a, D, NSr, st);
+  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd dU");
+  ce_reduce_kernel<<<(int)cdiv(n / 4, 256), 256, 0, st>>>(ws, NSr, n, dU);
+  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd dU reduce");
+  // dI: items owned, users streamed
+  a.own = I; a.str = U;
+  launch_tiles<2>(a, D, NSr, st);
+  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd dI");
+  ce_reduce_kernel<<<(int)cdiv(n / 4, 256), 256, 0, st>>>(ws, NSr, n, dI);
+  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd dI reduce");
+  if (N) {
+    const HStrideArgs hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
+    ce_hard_bwd_kernel<<<cdiv(B, 4), 256, 0, st>>>(U, Hn, hs.row, hs.slot, B, N, D, a.invT, lse, grad_out, dhl);
+    RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd hard");
+  }
+  return 0;
+}

@@ -18,10 +18,12 @@ Function.forward grad mode is always off, so the modules decide whether to keep 
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch.autograd.function import once_differentiable
 
-from . import _hip, ops
+from . import _hip, ops, precision
 from .flat import grad_of, touch_table
 
 
@@ -469,8 +471,13 @@ class InBatchLossFn(torch.autograd.Function):
         I = I.contiguous()
         B, D = int(U.shape[0]), int(U.shape[1])
         dev = U.device
-        S = torch.empty(B, B, device=dev, dtype=torch.float32)
-        ops.gemm(U, I, S, B, B, D, transA=0, transB=1, lda=D, ldb=D, ldc=B)
+        # bf16 mode: S tiles recomputed on the MFMA, never stored (csrc/ce_fused.hip)
+        fused = (precision.compute_dtype() == 'bf16' and D in (64, 128) and
+                 not os.environ.get('RSYS_UNFUSED_CE'))
+        S = None
+        if not fused:
+            S = torch.empty(B, B, device=dev, dtype=torch.float32)
+            ops.gemm(U, I, S, B, B, D, transA=0, transB=1, lda=D, ldb=D, ldc=B)
         N = 0
         Hc = None
         hsr = hss = 0
@@ -491,11 +498,18 @@ class InBatchLossFn(torch.autograd.Function):
         lse = torch.empty(B, device=dev, dtype=torch.float32)
         row_loss = torch.empty(B, device=dev, dtype=torch.float32)
         loss = torch.empty((), device=dev, dtype=torch.float32)
-        _hip.call('rs_inbatch_ce_fwd', S.data_ptr(), B, U.data_ptr(), ops.P(Hc), hsr, hss, ops.P(ids), st,
-                  B, N, D, float(temperature), lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(),
-                  ops.stream())
+        if fused:
+            w = ops.ws(_hip.lib().rs_inbatch_ce_fused_ws_bytes(B, D), dev)
+            _hip.call('rs_inbatch_ce_fused_fwd', U.data_ptr(), I.data_ptr(), ops.P(Hc), hsr, hss, ops.P(ids), st,
+                      B, N, D, float(temperature), lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(),
+                      w.data_ptr(), ops.stream())
+        else:
+            _hip.call('rs_inbatch_ce_fwd', S.data_ptr(), B, U.data_ptr(), ops.P(Hc), hsr, hss, ops.P(ids), st,
+                      B, N, D, float(temperature), lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(),
+                      ops.stream())
         ctx.save_for_backward(U, I, Hc if Hc is not None else U)
         ctx.S, ctx.ids, ctx.st, ctx.N, ctx.T, ctx.lse = S, ids, st, N, float(temperature), lse
+        ctx.fused = fused
         ctx.hs = (hsr, hss)
         return loss
 
@@ -508,6 +522,19 @@ class InBatchLossFn(torch.autograd.Function):
         S = ctx.S
         gout = gout.contiguous()
         dhl = torch.empty(B, max(N, 1), device=U.device, dtype=torch.float32) if N else None
+        if ctx.fused:
+            dU = torch.empty_like(U)
+            dI = torch.empty_like(I)
+            w = ops.ws(_hip.lib().rs_inbatch_ce_fused_ws_bytes(B, D), U.device)
+            _hip.call('rs_inbatch_ce_fused_bwd', U.data_ptr(), I.data_ptr(), ops.P(Hc) if N else None,
+                      ctx.hs[0], ctx.hs[1], ops.P(ctx.ids), ctx.st, B, N, D, ctx.T, ctx.lse.data_ptr(),
+                      gout.data_ptr(), dU.data_ptr(), dI.data_ptr(), ops.P(dhl), w.data_ptr(), ops.stream())
+            dH = None
+            if N:
+                dH = torch.empty_strided(Hc.shape, Hc.stride(), device=Hc.device, dtype=Hc.dtype)
+                _hip.call('rs_hardneg_bwd', U.data_ptr(), Hc.data_ptr(), ctx.hs[0], ctx.hs[1], dhl.data_ptr(),
+                          dU.data_ptr(), dH.data_ptr(), B, N, D, ops.stream())
+            return dU, dI, None, dH, None
         _hip.call('rs_inbatch_ce_bwd', S.data_ptr(), B, U.data_ptr(), ops.P(Hc) if N else None,
                   ctx.hs[0], ctx.hs[1], ops.P(ctx.ids), ctx.st, B, N, D, ctx.T, ctx.lse.data_ptr(),
                   gout.data_ptr(), ops.P(dhl), ops.stream())

@@ -317,3 +317,56 @@ def test_bf16_attention_dropout_matches_fp32_masks(bf16_mode):
     assert (o16 - o32).abs().max().item() < 2e-2 * scale
     assert (o0 - o32).abs().max().item() > 0.2 * scale
     assert (g16 - g32).abs().max().item() < 3e-2 * g32.abs().max().item()
+
+
+def _ce_ref(U, I, ids, H, T, gout=1.0):
+    """compute_loss (TwoTowerModel.py:81-140) in float64 on bf16-rounded U, I (the fused kernel's
+    products); hard-negative logits from the fp32 embeddings as in the kernel."""
+    Ud = r16(U).double().requires_grad_(True)
+    Id = r16(I).double().requires_grad_(True)
+    logits = Ud @ Id.t() / T
+    if ids is not None:
+        coll = (ids[:, None] == ids[None, :]) & ~torch.eye(len(ids), dtype=torch.bool, device=U.device)
+        logits = logits.masked_fill(coll, -1e9)
+    Uh = U.double().requires_grad_(True)
+    if H is not None:
+        Hd = H.double().requires_grad_(True)
+        hl = torch.einsum('bd,bnd->bn', Uh, Hd) / T
+        logits = torch.cat([logits, hl], 1)
+    loss = F.cross_entropy(logits, torch.arange(len(U), device=U.device))
+    (loss * gout).backward()
+    dU = Ud.grad + (Uh.grad if H is not None else 0)
+    return loss.item(), dU.float(), Id.grad.float(), (Hd.grad.float() if H is not None else None)
+
+
+@pytest.mark.parametrize('B,D,N,coll', [(4096, 128, 0, True), (1000, 128, 3, True), (300, 64, 0, False),
+                                        (33, 128, 2, True)])
+def test_fused_inbatch_ce(B, D, N, coll, bf16_mode):
+    from recommendsystemproject_amd.functions import InBatchLossFn
+    U = F.normalize(rnd(B, D, seed=21), dim=1).requires_grad_(True)
+    I = F.normalize(rnd(B, D, seed=22), dim=1).requires_grad_(True)
+    ids = torch.randint(0, B // 2 if coll else 10 ** 9, (B,), device=DEV) if True else None
+    H = F.normalize(rnd(B, N, D, seed=23), dim=2).requires_grad_(True) if N else None
+    T = 0.15
+    loss = InBatchLossFn.apply(U, I, ids, H, T)
+    loss.backward(torch.tensor(0.7, device=DEV))
+    l_ref, dU, dI, dH = _ce_ref(U.detach(), I.detach(), ids, H.detach() if N else None, T, 0.7)
+    assert abs(loss.item() - l_ref) < 2e-4 * max(1.0, abs(l_ref)), (loss.item(), l_ref)
+    for a, b_ in ((U.grad, dU), (I.grad, dI)) + (((H.grad, dH),) if N else ()):
+        sc = b_.abs().max().item()
+        assert (a - b_).abs().max().item() < 2e-2 * sc, ((a - b_).abs().max().item(), sc)
+
+
+def test_fused_ce_deterministic(bf16_mode):
+    from recommendsystemproject_amd.functions import InBatchLossFn
+    B, D = 4096, 128
+    U = F.normalize(rnd(B, D, seed=31), dim=1).requires_grad_(True)
+    I = F.normalize(rnd(B, D, seed=32), dim=1).requires_grad_(True)
+    ids = torch.randint(0, 3000, (B,), device=DEV)
+    res = []
+    for _ in range(2):
+        U.grad = I.grad = None
+        loss = InBatchLossFn.apply(U, I, ids, None, 0.1)
+        loss.backward()
+        res.append((loss.item(), U.grad.clone(), I.grad.clone()))
+    assert res[0][0] == res[1][0] and torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
