@@ -73,13 +73,13 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* lo, const __bf16* hi) {
 // MODE 1: dU (own = U, str = I; lse of the owned user)
 // MODE 2: dI (own = I, str = U; lse of the streamed user)
 template <int D, int MODE>
-__global__ __launch_bounds__(256) void ce_tile_kernel(CeArgs a) {
+__global__ __launch_bounds__(64 * kWaves) void ce_tile_kernel(CeArgs a) {
   constexpr int KS = D / 16;          // 32x32x16 k-steps over the embedding
   constexpr int PT = D + 8;           // LDS pitch (bf16) of a streamed tile row
   constexpr int DB = D / 32;          // 32-wide blocks of the gradient
   __shared__ __attribute__((aligned(16))) __bf16 Ts[2][kTile * PT];
-  __shared__ int64_t sid[2][kTile];
-  __shared__ float slse[2][kTile];
+  __shared__ __attribute__((aligned(16))) int64_t sid[2][kTile];
+  __shared__ __attribute__((aligned(16))) float slse[2][kTile];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int B = a.B;
@@ -113,54 +113,83 @@ __global__ __launch_bounds__(256) void ce_tile_kernel(CeArgs a) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) gacc[i][e] = 0.f;
 
-  // streamed tile staging: 32 rows x D fp32 -> bf16 LDS, 256 threads, float4 each
-  constexpr int SL = kTile * D / 4 / 256;  // float4 slots per thread
-  floatx4 st[SL];
-  auto load_tile = [&](int t0) {
-#pragma unroll
-    for (int i = 0; i < SL; ++i) {
-      const int slot = tid + 256 * i;
-      const int row = slot / (D / 4), col = (slot % (D / 4)) * 4;
-      const int t = t0 + row;
-      st[i] = t < B ? *reinterpret_cast<const floatx4*>(a.str + (int64_t)t * D + col) : floatx4{0.f, 0.f, 0.f, 0.f};
-    }
+  // streamed tile staging: 32 rows x D fp32 -> bf16 LDS, float4 per slot. Two register sets
+  // keep the loads of tiles i+1 and i+2 in flight while tile i is consumed (the kernel is short
+  // per tile; with one set every iteration waited for an L2 round trip).
+  constexpr int NTHR = 64 * kWaves;
+  constexpr int SL = kTile * D / 4 / NTHR;  // float4 slots per thread
+  struct Stage {
+    floatx4 v[SL];
+    int64_t id;
+    float l;
   };
-  auto store_tile = [&](int buf, int t0) {
+  Stage RA, RB;
+  // loads are unconditional (row index clamped to B - 1; rows >= B are masked when consumed):
+  // a guarded load would sit in its own branch, and the waitcnt pass then drains vmcnt(0) at the
+  // join -- waiting for the prefetch it was meant to overlap
+  auto load_tile = [&](int t0, Stage& R) {
 #pragma unroll
     for (int i = 0; i < SL; ++i) {
-      const int slot = tid + 256 * i;
+      const int slot = tid + NTHR * i;
+      const int row = slot / (D / 4), col = (slot % (D / 4)) * 4;
+      const int t = min(t0 + row, B - 1);
+      R.v[i] = *reinterpret_cast<const floatx4*>(a.str + (int64_t)t * D + col);
+    }
+    const int t = min(t0 + (tid & (kTile - 1)), B - 1);
+    R.id = a.ids ? a.ids[(int64_t)t * a.id_stride] : 0;
+    if constexpr (MODE == 2) R.l = a.lse[t];
+  };
+  auto store_tile = [&](int bf, const Stage& R) {
+#pragma unroll
+    for (int i = 0; i < SL; ++i) {
+      const int slot = tid + NTHR * i;
       const int row = slot / (D / 4), col = (slot % (D / 4)) * 4;
       bf16x4 v;
-      v[0] = (__bf16)st[i][0]; v[1] = (__bf16)st[i][1]; v[2] = (__bf16)st[i][2]; v[3] = (__bf16)st[i][3];
-      *reinterpret_cast<bf16x4*>(&Ts[buf][row * PT + col]) = v;
+      v[0] = (__bf16)R.v[i][0]; v[1] = (__bf16)R.v[i][1]; v[2] = (__bf16)R.v[i][2]; v[3] = (__bf16)R.v[i][3];
+      *reinterpret_cast<bf16x4*>(&Ts[bf][row * PT + col]) = v;
     }
     if (tid < kTile) {
-      const int t = t0 + tid;
-      sid[buf][tid] = (a.ids && t < B) ? a.ids[(int64_t)t * a.id_stride] : 0;
-      if constexpr (MODE == 2) slse[buf][tid] = t < B ? a.lse[t] : 0.f;
+      sid[bf][tid] = R.id;
+      if constexpr (MODE == 2) slse[bf][tid] = R.l;
     }
   };
-
-  int buf = 0;
-  if (t_begin < t_end) {
-    load_tile(t_begin);
-    store_tile(0, t_begin);
-  }
-  __syncthreads();
-  for (int t0 = t_begin; t0 < t_end; t0 += kTile) {
-    const bool more = t0 + kTile < t_end;
-    if (more) load_tile(t0 + kTile);
+  float dg = 0.f;  // fwd: S_oo / T, captured by the lane that meets the diagonal
+  bool has_dg = false;
+  auto consume = [&](int buf, int t0) {
     const __bf16* T = Ts[buf];
     // S^T tile: C[t][o] = str[t] . own[o]; A = streamed rows (lane c: row t0 + c)
-    floatx16 acc;
+    // two accumulator chains (even / odd k-steps) halve the dependent-MFMA latency
+    floatx16 acc, acc1;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    for (int e = 0; e < 16; ++e) acc[e] = acc1[e] = 0.f;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(&T[c * PT + 16 * s + 8 * h]);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, ob[s], acc, 0, 0, 0);
+    for (int s = 0; s < KS; s += 2) {
+      const bf16x8 af0 = *reinterpret_cast<const bf16x8*>(&T[c * PT + 16 * s + 8 * h]);
+      const bf16x8 af1 = *reinterpret_cast<const bf16x8*>(&T[c * PT + 16 * s + 16 + 8 * h]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af0, ob[s], acc, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af1, ob[s + 1], acc1, 0, 0, 0);
     }
-    // element e of this lane: streamed row t = t0 + 8(e>>2) + 4h + (e&3), owned column o
+    acc += acc1;
+    // element e of this lane: streamed row t = t0 + 8(e>>2) + 4h + (e&3), owned column o.
+    // The tile's ids (and lse) are read up front as vectors and the masks are selects: a
+    // per-element `if (ids && ...) sid[...]` became a divergent branch with its own LDS
+    // round trip, 16 serialised LDS latencies per tile.
+    bool coll[16];
+    {
+      const bool have_ids = a.ids != nullptr;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+        const i64x2* sp = reinterpret_cast<const i64x2*>(&sid[buf][8 * g4 + 4 * h]);
+        const i64x2 s01 = sp[0], s23 = sp[1];
+        const int64_t sv[4] = {s01[0], s01[1], s23[0], s23[1]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int t = t0 + 8 * g4 + 4 * h + j;
+          coll[4 * g4 + j] = have_ids & (t != o) & (sv[j] == id_o);
+        }
+      }
+    }
     if constexpr (MODE == 0) {
       float v[16];
       float tm = -INFINITY;
@@ -169,9 +198,11 @@ __global__ __launch_bounds__(256) void ce_tile_kernel(CeArgs a) {
         const int tl = 8 * (e >> 2) + 4 * h + (e & 3);
         const int t = t0 + tl;
         float x = acc[e] * a.invT;
-        if (t == o && o_ok) a.diag[o] = x;
-        if (a.ids && t != o && sid[buf][tl] == id_o) x = kMasked;
-        if (t >= B) x = -INFINITY;
+        const bool diag = t == o;
+        dg = diag ? x : dg;
+        has_dg = has_dg | diag;
+        x = coll[e] ? kMasked : x;
+        x = t >= B ? -INFINITY : x;
         v[e] = x;
         tm = fmaxf(tm, x);
       }
@@ -186,14 +217,22 @@ __global__ __launch_bounds__(256) void ce_tile_kernel(CeArgs a) {
     } else {
       // dS^T tile -> bf16 operand fragments (k-step 0: registers 0..7, k-step 1: 8..15)
       bf16x8 xf[2];
+      float lt[16];
+      if constexpr (MODE == 2) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const floatx4 l4 = *reinterpret_cast<const floatx4*>(&slse[buf][8 * g4 + 4 * h]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) lt[4 * g4 + j] = l4[j];
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int tl = 8 * (e >> 2) + 4 * h + (e & 3);
         const int t = t0 + tl;
         const float x = acc[e] * a.invT;
-        const bool collide = a.ids && t != o && sid[buf][tl] == id_o;  // logit -1e9: P = 0
-        const float l = MODE == 1 ? lse_o : slse[buf][tl];
-        const float p = collide ? 0.f : __expf(x - l);
+        const float l = MODE == 1 ? lse_o : lt[e];
+        const float p = coll[e] ? 0.f : __expf(x - l);  // collision: logit -1e9, P = 0
         const float dv = (t >= B || !o_ok) ? 0.f : g * (p - (t == o ? 1.f : 0.f));
         xf[e >> 3][e & 7] = (__bf16)dv;
       }
@@ -211,9 +250,31 @@ __global__ __launch_bounds__(256) void ce_tile_kernel(CeArgs a) {
         }
       }
     }
-    if (more) store_tile(buf ^ 1, t0 + kTile);
+  };
+
+  const int ntiles = t_begin < t_end ? (t_end - t_begin + kTile - 1) / kTile : 0;
+  if (ntiles > 0) {
+    load_tile(t_begin, RA);
+    store_tile(0, RA);
+    load_tile(t_begin + kTile, RA);
+    load_tile(t_begin + 2 * kTile, RB);
+  }
+  __syncthreads();
+  // two tiles per trip so the register sets are fixed: tile it+1 waits in RA, it+2 in RB
+  for (int it = 0; it < ntiles; it += 2) {
+    const int t0 = t_begin + it * kTile;
+    consume(0, t0);
+    store_tile(1, RA);
+    load_tile(t0 + 3 * kTile, RA);
     __syncthreads();
-    buf ^= 1;
+    if (it + 1 >= ntiles) break;
+    consume(1, t0 + kTile);
+    store_tile(0, RB);
+    load_tile(t0 + 4 * kTile, RB);
+    __syncthreads();
+  }
+  if constexpr (MODE == 0) {
+    if (has_dg && o_ok) a.diag[o] = dg;
   }
   const int split = blockIdx.y;
   if constexpr (MODE == 0) {
@@ -310,7 +371,7 @@ __global__ void ce_reduce_kernel(const float* __restrict__ part, int NS, int64_t
 
 int splits_for(int B) {
   const int blocks = cdiv(B, kOwnW * kWaves);
-  int ns = cdiv(256, blocks);
+  int ns = cdiv(512, blocks);  // two workgroups per CU: the waves hide each other's latency
   const int max_ns = cdiv(B, kTile);
   if (ns > max_ns) ns = max_ns;
   if (ns > 64) ns = 64;  // ce_finish reads the partials with one lane each
@@ -320,8 +381,8 @@ int splits_for(int B) {
 template <int MODE>
 int launch_tiles(const CeArgs& a, int D, int NS, hipStream_t st) {
   const dim3 grid(cdiv(a.B, kOwnW * kWaves), NS);
-  if (D == 128) ce_tile_kernel<128, MODE><<<grid, 256, 0, st>>>(a);
-  else ce_tile_kernel<64, MODE><<<grid, 256, 0, st>>>(a);
+  if (D == 128) ce_tile_kernel<128, MODE><<<grid, 64 * kWaves, 0, st>>>(a);
+  else ce_tile_kernel<64, MODE><<<grid, 64 * kWaves, 0, st>>>(a);
   return 0;
 }
 
