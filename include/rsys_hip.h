@@ -194,15 +194,20 @@ int rs_layernorm_bwd(const float* h, const float* dy, const float* gamma, const 
  * x [G*Bg, C] in G independent groups of Bg rows (hard-negative slots, T13), batch statistics,
  * running stats updated group by group (momentum), num_batches_tracked += G, optional ReLU.
  * mean/rstd [G*C] saved. training == 0 normalises with the running statistics (eval mode).
- * Replaces BatchNorm1d (GenericTower.py:234, Tower.py:17; K12/K13). */
+ * Replaces BatchNorm1d (GenericTower.py:234, Tower.py:17; K12/K13).
+ * drop_p > 0 (with relu): the MLP block's following nn.Dropout (Tower.py:19) is applied to the
+ * output, mask of element (row*C + c) from (key, site) -- the rs_dropout_fwd draw. In the
+ * backward, drop_scale = 1/(1-p) (1 without dropout): y > 0 <=> positive and kept, so the
+ * gradient of relu-then-dropout is dy * drop_scale where y > 0. */
 int64_t rs_batchnorm_ws_bytes(int G, int Bg, int C);
 int rs_batchnorm_fwd(const float* x, float* y, const float* w, const float* b,
                      float* running_mean, float* running_var, int64_t* num_batches,
                      float* mean, float* rstd, int G, int Bg, int C, float momentum, float eps,
-                     int relu, int training, float* ws, void* stream);
+                     int relu, int training, float drop_p, const int64_t* key, int site, float* ws,
+                     void* stream);
 int rs_batchnorm_bwd(const float* x, const float* y, const float* dy, const float* w,
                      const float* mean, const float* rstd, float* dx, float* dw, float* db,
-                     int G, int Bg, int C, int relu, float* ws, void* stream);
+                     int G, int Bg, int C, int relu, float drop_scale, float* ws, void* stream);
 
 /* ---------------------------------------------------------------- misc elementwise */
 /* y = x / max(||x||_2, eps) per row (F.normalize, Tower.py:41; K14); norm [M] saved */

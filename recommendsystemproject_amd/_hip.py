@@ -59,8 +59,8 @@ SIGNATURES = {
     'rs_layernorm_bwd': (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, f32, vp, i32, vp, vp]),
     'rs_batchnorm_ws_bytes': (i64, [i32, i32, i32]),
     'rs_batchnorm_fwd': (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, i32, i32,
-                               vp, vp]),
-    'rs_batchnorm_bwd': (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]),
+                               f32, vp, i32, vp, vp]),
+    'rs_batchnorm_bwd': (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp, vp]),
     'rs_l2norm_fwd': (i32, [vp, vp, vp, i32, i32, f32, vp]),
     'rs_l2norm_bwd': (i32, [vp, vp, vp, vp, i32, i32, f32, vp]),
     'rs_inbatch_ce_fused_ws_bytes': (i64, [i32, i32]),

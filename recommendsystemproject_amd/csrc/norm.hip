@@ -174,6 +174,7 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const float* __restrict
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, int Bg,
                                                          int C, int S, int relu,
+                                                         float drop_scale,
                                                          double* __restrict__ ws) {
   __shared__ double red[2][256];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const float* __restrict
         sb += (double)xv * (double)xv;
       } else {
         float d = dy[o];
-        if (relu && !(y[o] > 0.f)) d = 0.f;
+        if (relu) d = y[o] > 0.f ? d * drop_scale : 0.f;
         const float xh = (xv - mu) * r;
         sa += (double)d;
         sb += (double)d * (double)xh;
@@ -241,7 +242,8 @@ __global__ __launch_bounds__(256) void bn_fwd_norm_kernel(
     const double* __restrict__ ws, const float* __restrict__ x, float* __restrict__ y,
     const float* __restrict__ w, const float* __restrict__ b, float* running_mean,
     float* running_var, int64_t* num_batches, float* __restrict__ mean, float* __restrict__ rstd,
-    int G, int Bg, int C, int S, float momentum, float eps, int relu) {
+    int G, int Bg, int C, int S, float momentum, float eps, int relu, float drop_p,
+    const int64_t* __restrict__ key, int site) {
   __shared__ double red[4][2][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -277,10 +279,14 @@ __global__ __launch_bounds__(256) void bn_fwd_norm_kernel(
   const float wc = w[c], bc = b[c];
   const int rpc = (Bg + S - 1) / S;
   const int r1 = min(Bg, (s + 1) * rpc);
+  DropKey dk{};
+  const bool drop = drop_p > 0.f;
+  if (drop) dk = make_key(key, site, drop_p);
   for (int i = s * rpc + rl; i < r1; i += 4) {
     const int64_t o = ((int64_t)g * Bg + i) * C + c;
     float v = (x[o] - muf) * r * wc + bc;
     if (relu) v = fmaxf(v, 0.f);
+    if (drop) v *= keep_mult(dk, (uint64_t)o);  // the block's nn.Dropout (rs_dropout_fwd draw)
     y[o] = v;
   }
 }
@@ -291,7 +297,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(
     const double* __restrict__ ws, const float* __restrict__ x, const float* __restrict__ y,
     const float* __restrict__ dy, const float* __restrict__ w, const float* __restrict__ mean,
     const float* __restrict__ rstd, float* __restrict__ dx, float* dw, float* db, int G, int Bg,
-    int C, int S, int relu) {
+    int C, int S, int relu, float drop_scale) {
   __shared__ double red[4][2][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -318,7 +324,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(
   for (int i = s * rpc + rl; i < r1; i += 4) {
     const int64_t o = ((int64_t)g * Bg + i) * C + c;
     float d = dy[o];
-    if (relu && !(y[o] > 0.f)) d = 0.f;
+    if (relu) d = y[o] > 0.f ? d * drop_scale : 0.f;
     const float xh = (x[o] - mu) * r;
     dx[o] = wr * (d - mdy - xh * mdyx);
   }
@@ -492,8 +498,11 @@ extern "C" int64_t rs_batchnorm_ws_bytes(int G, int Bg, int C) {
 extern "C" int rs_batchnorm_fwd(const float* x, float* y, const float* w, const float* b,
                                 float* running_mean, float* running_var, int64_t* num_batches,
                                 float* mean, float* rstd, int G, int Bg, int C, float momentum,
-                                float eps, int relu, int training, float* ws, void* stream) {
+                                float eps, int relu, int training, float drop_p,
+                                const int64_t* key, int site, float* ws, void* stream) {
   RS_CHECK_ARG(x && y && w && b && mean && rstd && ws, "rs_batchnorm_fwd: null pointer");
+  RS_CHECK_ARG(drop_p == 0.f || (relu && training && key && drop_p > 0.f && drop_p < 1.f),
+               "rs_batchnorm_fwd: dropout needs relu, training, a key and 0 < p < 1");
   RS_CHECK_ARG(G >= 1 && Bg >= 1 && C >= 1, "rs_batchnorm_fwd: bad shape G=%d Bg=%d C=%d", G, Bg, C);
   RS_CHECK_ARG(!running_mean == !running_var, "rs_batchnorm_fwd: running stats must come together");
   hipStream_t st = as_stream(stream);
@@ -512,19 +521,20 @@ extern "C" int rs_batchnorm_fwd(const float* x, float* y, const float* w, const 
     return 0;
   }
   bn_partial_kernel<0><<<dim3(cdiv(C, 64), G, S), 256, 0, st>>>(x, nullptr, nullptr, nullptr,
-                                                                 nullptr, Bg, C, S, 0, wsd);
+                                                                 nullptr, Bg, C, S, 0, 1.f, wsd);
   RS_CHECK_LAUNCH("rs_batchnorm_fwd partial");
   bn_fwd_norm_kernel<<<dim3(cdiv(C, 64), G, S), 256, 0, st>>>(wsd, x, y, w, b, running_mean,
                                                               running_var, num_batches, mean, rstd,
-                                                              G, Bg, C, S, momentum, eps, relu);
+                                                              G, Bg, C, S, momentum, eps, relu,
+                                                              drop_p, key, site);
   RS_CHECK_LAUNCH("rs_batchnorm_fwd norm");
   return 0;
 }
 
 extern "C" int rs_batchnorm_bwd(const float* x, const float* y, const float* dy, const float* w,
                                 const float* mean, const float* rstd, float* dx, float* dw,
-                                float* db, int G, int Bg, int C, int relu, float* ws,
-                                void* stream) {
+                                float* db, int G, int Bg, int C, int relu, float drop_scale,
+                                float* ws, void* stream) {
   RS_CHECK_ARG(x && dy && w && mean && rstd && dx && dw && db && ws,
                "rs_batchnorm_bwd: null pointer");
   RS_CHECK_ARG(!relu || y, "rs_batchnorm_bwd: relu needs y");
@@ -533,10 +543,10 @@ extern "C" int rs_batchnorm_bwd(const float* x, const float* y, const float* dy,
   const int S = bn_chunks(Bg);
   double* wsd = reinterpret_cast<double*>(ws);
   bn_partial_kernel<1><<<dim3(cdiv(C, 64), G, S), 256, 0, st>>>(x, y, dy, mean, rstd, Bg, C, S,
-                                                                 relu, wsd);
+                                                                 relu, drop_scale, wsd);
   RS_CHECK_LAUNCH("rs_batchnorm_bwd partial");
   bn_bwd_dx_kernel<<<dim3(cdiv(C, 64), G, S), 256, 0, st>>>(wsd, x, y, dy, w, mean, rstd, dx, dw,
-                                                            db, G, Bg, C, S, relu);
+                                                            db, G, Bg, C, S, relu, drop_scale);
   RS_CHECK_LAUNCH("rs_batchnorm_bwd dx");
   return 0;
 }

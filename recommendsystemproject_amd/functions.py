@@ -420,9 +420,9 @@ class MLPFn(torch.autograd.Function):
         for j in range(n_hidden):
             lin, bn = seq[4 * j], seq[4 * j + 1]
             z = ops.linear_fwd(h, lin.weight, lin.bias)
-            y, mean, rstd = ops.batchnorm_fwd(z, bn, G, relu=True, training=mlp.training)
-            if p > 0:
-                ops.dropout_fwd(y, p, key, 256 + j)
+            # Linear -> BatchNorm1d -> ReLU -> Dropout: BN, ReLU and the dropout in one pass
+            y, mean, rstd = ops.batchnorm_fwd(z, bn, G, relu=True, training=mlp.training, drop_p=p,
+                                              drop_key=key, drop_site=256 + j)
             saved.append((h, z, y, mean, rstd))
             h = y
         last = seq[len(seq) - 1]
@@ -448,11 +448,10 @@ class MLPFn(torch.autograd.Function):
         for j in reversed(range(len(ctx.saved))):
             h, z, y, mean, rstd = ctx.saved[j]
             lin, bn = seq[4 * j], seq[4 * j + 1]
-            if ctx.p > 0:
-                ops.dropout_bwd(dh, ctx.p, ctx.key, 256 + j)
-            # y is post-ReLU (post-dropout): y > 0 <=> kept and positive
+            # y is post-ReLU, post-dropout: y > 0 <=> kept and positive, so the dropout's
+            # backward is a scale on the same mask (fused into the BN backward)
             dz = ops.batchnorm_bwd(z, y, dh, bn.weight, mean, rstd, g(bn.weight), g(bn.bias), ctx.G,
-                                   relu=True)
+                                   relu=True, drop_p=ctx.p)
             ops.linear_bwd_weight(dz, h, g(lin.weight), db=g(lin.bias))
             dh = ops.linear_bwd_input(dz, lin.weight)
         ctx.saved = None

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
 import torch
 
 from . import _hip, precision
@@ -236,8 +237,10 @@ def dropout_bwd(dx, p, key, site):
     return dx
 
 
-def batchnorm_fwd(x, bn, G, relu, training, momentum=None, eps=None):
-    """x [G*Bg, C]; bn: nn.BatchNorm1d-like (weight, bias, running_*, num_batches_tracked)."""
+def batchnorm_fwd(x, bn, G, relu, training, momentum=None, eps=None, drop_p=0.0, drop_key=None,
+                  drop_site=0):
+    """x [G*Bg, C]; bn: nn.BatchNorm1d-like (weight, bias, running_*, num_batches_tracked).
+    drop_p > 0: the following nn.Dropout fused into the output (relu and training only)."""
     M, Cc = x.shape
     Bg = M // G
     y = torch.empty_like(x)
@@ -255,18 +258,20 @@ def batchnorm_fwd(x, bn, G, relu, training, momentum=None, eps=None):
          P(bn.running_mean) if run else None, P(bn.running_var) if run else None,
          P(bn.num_batches_tracked) if update else None,
          P(mean), P(rstd), G, Bg, Cc, float(mom), float(bn.eps if eps is None else eps), int(relu),
-         int(batch_stats), P(w), stream())
+         int(batch_stats), float(drop_p), P(drop_key), drop_site, P(w), stream())
     return y, mean, rstd
 
 
-def batchnorm_bwd(x, y, dy, weight, mean, rstd, dw, db, G, relu, dx=None):
+def batchnorm_bwd(x, y, dy, weight, mean, rstd, dw, db, G, relu, dx=None, drop_p=0.0):
     M, Cc = x.shape
     Bg = M // G
     if dx is None:
         dx = torch.empty_like(x)
     w = ws(_hip.lib().rs_batchnorm_ws_bytes(G, Bg, Cc), x.device)
+    # the fused dropout's scale, in the forward's fp32 arithmetic (rng.h make_key)
+    scale = float(np.float32(1.0) / (np.float32(1.0) - np.float32(drop_p))) if drop_p > 0 else 1.0
     call('rs_batchnorm_bwd', P(x), P(y), P(dy), P(weight), P(mean), P(rstd), P(dx), P(dw), P(db),
-         G, Bg, Cc, int(relu), P(w), stream())
+         G, Bg, Cc, int(relu), scale, P(w), stream())
     return dx
 
 

@@ -287,6 +287,30 @@ def test_batchnorm_train_fwd_bwd(G, relu, Bg):
     assert torch.allclose(ye, ref_bn(x), atol=1e-5)
 
 
+@pytest.mark.parametrize('G', [1, 2])
+def test_batchnorm_fused_dropout_equals_separate(G):
+    """BN -> ReLU -> Dropout in one kernel (MLP block) == BN+ReLU then the standalone dropout
+    kernel (same draw, bitwise), and its backward == dropout_bwd then the BN backward."""
+    C, Bg, p = 256, 4096, 0.3
+    bn = torch.nn.BatchNorm1d(C).to(DEV)
+    bn2 = torch.nn.BatchNorm1d(C).to(DEV)
+    x = rnd(G * Bg, C, seed=7) * 2 + 0.5
+    key = torch.tensor([42, 9], dtype=torch.int64, device=DEV)
+    y, mean, rstd = ops.batchnorm_fwd(x, bn, G, True, training=True, drop_p=p, drop_key=key, drop_site=257)
+    y2, mean2, rstd2 = ops.batchnorm_fwd(x, bn2, G, True, training=True)
+    ops.dropout_fwd(y2, p, key, 257)
+    assert torch.equal(y, y2) and torch.equal(mean, mean2)
+    assert 0.6 < (y2 != 0).float().mean().item() / max((torch.relu(x - x.mean(0)) > 0).float().mean().item(), 1e-6) < 0.8
+    dy = rnd(G * Bg, C, seed=8)
+    dw, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dx = ops.batchnorm_bwd(x, y, dy, bn.weight, mean, rstd, dw, db, G, True, drop_p=p)
+    dy2 = dy.clone()
+    ops.dropout_bwd(dy2, p, key, 257)
+    dw2, db2 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dx2 = ops.batchnorm_bwd(x, y2, dy2, bn2.weight, mean2, rstd2, dw2, db2, G, True)
+    assert torch.allclose(dx, dx2, atol=1e-6) and torch.allclose(dw, dw2, atol=1e-5) and torch.allclose(db, db2, atol=1e-5)
+
+
 def test_l2norm():
     x = rnd(500, 128, seed=1).requires_grad_(True)
     x.data[3] = 0.0
