@@ -57,6 +57,9 @@ __device__ __forceinline__ float wave_max(float v) {
 // out[n] = beta*out[n] + scale * sum_{p<P} ws[p*N + n], fixed order (reduce.hip)
 int partials_reduce(const float* ws, int P, int N, float scale, float beta, float* out,
                     hipStream_t st);
+// the same with columns [0, split) -> out0 and [split, N) -> out1
+int partials_reduce2(const float* ws, int P, int N, int split, float scale, float beta, float* out0,
+                     float* out1, hipStream_t st);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // debug / A-B switches read at launch time (host only): set and not "0"

@@ -150,6 +150,103 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ h
   }
 }
 
+// LN backward for the encoder width N = 64: lane (r, q) of a wave owns columns 16q .. 16q+15 of
+// row r of a 16-row group (16-byte loads and stores, a row = 4 lanes x 64 contiguous bytes), the
+// row sums are two xor-shuffles instead of a 64-lane reduction per row, and the sublayer's
+// dropout draws two masks per hash. dgamma/dbeta partials: [nb][128] (gamma | beta).
+template <bool DROP>
+__global__ __launch_bounds__(256) void ln_bwd64_kernel(const float* __restrict__ h,
+                                                       const float* dy,  // may alias dh
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd,
+                                                       float* dh, int M,
+                                                       float* __restrict__ ws,
+                                                       float* __restrict__ da, float pdrop,
+                                                       const int64_t* __restrict__ key, int site) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ float red[4][64][17];
+  DropKey dk{};
+  if (DROP) dk = make_key(key, site, pdrop);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  float gm[16], pg[16], pb[16];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const f4 v = *reinterpret_cast<const f4*>(gamma + 16 * q + 4 * u);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gm[4 * u + e] = v[e];
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) pg[i] = pb[i] = 0.f;
+  const int groups = (M + 15) / 16;
+  for (int gi = blockIdx.x * 4 + wave; gi < groups; gi += gridDim.x * 4) {
+    const int row = gi * 16 + r;
+    const bool ok = row < M;
+    const int64_t o = (int64_t)(ok ? row : 0) * 64 + 16 * q;
+    float hv[16], dv[16];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f4 a = *reinterpret_cast<const f4*>(h + o + 4 * u);
+      const f4 b = *reinterpret_cast<const f4*>(dy + o + 4 * u);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hv[4 * u + e] = a[e];
+        dv[4 * u + e] = ok ? b[e] : 0.f;
+      }
+    }
+    const float mu = mean[ok ? row : 0], rr = rstd[ok ? row : 0];
+    float xh[16], g[16], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      xh[i] = (hv[i] - mu) * rr;
+      pg[i] += dv[i] * xh[i];
+      pb[i] += dv[i];
+      g[i] = dv[i] * gm[i];
+      s1 += g[i];
+      s2 += g[i] * xh[i];
+    }
+    s1 += __shfl_xor(s1, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    s1 /= 64.f;
+    s2 /= 64.f;
+    if (ok) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        f4 v, w;
+        float mk[4] = {1.f, 1.f, 1.f, 1.f};
+        if (DROP) keep4(dk, (uint64_t)(o + 4 * u), mk);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * u + e;
+          v[e] = rr * (g[i] - s1 - xh[i] * s2);
+          w[e] = DROP ? v[e] * mk[e] : v[e];
+        }
+        *reinterpret_cast<f4*>(dh + o + 4 * u) = v;
+        if (da) *reinterpret_cast<f4*>(da + o + 4 * u) = w;
+      }
+    }
+  }
+  // column partials: lanes with the same q hold the same 16 columns; fixed-order sum over the
+  // 16 rows r and the 4 waves
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) red[wave][lane][i] = pass == 0 ? pg[i] : pb[i];
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int c = threadIdx.x, qq = c >> 4, i = c & 15;
+      float t = 0.f;
+      for (int w = 0; w < 4; ++w)
+        for (int rr2 = 0; rr2 < 16; ++rr2) t += red[w][16 * qq + rr2][i];
+      ws[(int64_t)blockIdx.x * 128 + pass * 64 + c] = t;
+    }
+    __syncthreads();
+  }
+}
+
 int ln_blocks(int M) {
   int nb = cdiv(M, 4 * 4 * 4);  // >= 4 row groups per wave
   if (nb > 2048) nb = 2048;
@@ -483,6 +580,13 @@ extern "C" int rs_layernorm_bwd(const float* h, const float* dy, const float* ga
   if (M == 0) return 0;
   hipStream_t st = as_stream(stream);
   const int nb = ln_blocks(M);
+  if (N == 64 && aligned16(h) && aligned16(dy) && aligned16(dh) && aligned16(gamma) &&
+      (!da || aligned16(da))) {
+    if (p > 0.f) ln_bwd64_kernel<true><<<nb, 256, 0, st>>>(h, dy, gamma, mean, rstd, dh, M, ws, da, p, key, site);
+    else ln_bwd64_kernel<false><<<nb, 256, 0, st>>>(h, dy, gamma, mean, rstd, dh, M, ws, da, p, key, site);
+    RS_CHECK_LAUNCH("rs_layernorm_bwd n64");
+    return partials_reduce2(ws, nb, 128, 64, 1.f, 1.f, dgamma, dbeta, st);
+  }
   RS_NPL_DROP_DISPATCH(npl, p > 0.f, ln_bwd_kernel, nb, h, dy, gamma, mean, rstd, dh, M, N, ws, da, p,
                        key, site);
   RS_CHECK_LAUNCH("rs_layernorm_bwd");

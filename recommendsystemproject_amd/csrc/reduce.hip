@@ -18,7 +18,9 @@ int colsum_chunks(int M) {
 // reproducible and not latency-bound for thousands of partials.
 __global__ __launch_bounds__(1024) void partials_reduce_kernel(const float* __restrict__ ws, int P,
                                                                int N, float scale, float beta,
-                                                               float* __restrict__ out) {
+                                                               float* __restrict__ out,
+                                                               float* __restrict__ out1 = nullptr,
+                                                               int split = 1 << 30) {
   __shared__ float red[16][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int l = threadIdx.x >> 6;
@@ -40,7 +42,8 @@ __global__ __launch_bounds__(1024) void partials_reduce_kernel(const float* __re
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
-    out[c] = (beta != 0.f ? beta * out[c] : 0.f) + scale * t;
+    float* o = c < split ? out + c : out1 + (c - split);
+    *o = (beta != 0.f ? beta * *o : 0.f) + scale * t;
   }
 }
 
@@ -48,6 +51,14 @@ int partials_reduce(const float* ws, int P, int N, float scale, float beta, floa
                     hipStream_t st) {
   partials_reduce_kernel<<<cdiv(N, 64), 1024, 0, st>>>(ws, P, N, scale, beta, out);
   RS_CHECK_LAUNCH("partials_reduce");
+  return 0;
+}
+
+// columns [0, split) -> out0, [split, N) -> out1 (two parameter gradients, one launch)
+int partials_reduce2(const float* ws, int P, int N, int split, float scale, float beta, float* out0,
+                     float* out1, hipStream_t st) {
+  partials_reduce_kernel<<<cdiv(N, 64), 1024, 0, st>>>(ws, P, N, scale, beta, out0, out1, split);
+  RS_CHECK_LAUNCH("partials_reduce2");
   return 0;
 }
 

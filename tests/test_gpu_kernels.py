@@ -234,8 +234,8 @@ def test_attention_mfma_matches_valu_kernel(L, monkeypatch):
         assert torch.allclose(a, b, atol=2e-5, rtol=1e-4)
 
 
-def test_layernorm_fwd_bwd():
-    M, N = 1000, 64
+@pytest.mark.parametrize('M,N', [(1000, 64), (40003, 64), (777, 48)])  # N = 64: the 16-row kernel
+def test_layernorm_fwd_bwd(M, N):
     a, b = rnd(M, N, seed=1), rnd(M, N, seed=2)
     g, be = rnd(N, seed=3), rnd(N, seed=4)
     h_ref = (a + b).requires_grad_(True)
@@ -250,7 +250,17 @@ def test_layernorm_fwd_bwd():
     dg, db = torch.zeros(N, device=DEV), torch.zeros(N, device=DEV)
     dh = ops.layernorm_bwd(a2, dy.clone(), g, mean, rstd, dg, db)
     assert torch.allclose(dh, h_ref.grad, atol=1e-4)
-    assert torch.allclose(dg, gr.grad, atol=1e-3) and torch.allclose(db, br.grad, atol=1e-3)
+    assert torch.allclose(dg, gr.grad, atol=1e-3 * max(1.0, M / 1000)) and \
+        torch.allclose(db, br.grad, atol=1e-3 * max(1.0, M / 1000))
+    # the sublayer's dropout in the same pass: da == dropout_bwd(dh) (same draw)
+    key = torch.tensor([3, 4], dtype=torch.int64, device=DEV)
+    da = torch.empty_like(dh)
+    dh2 = ops.layernorm_bwd(a2, dy.clone(), g, mean, rstd, torch.zeros_like(dg), torch.zeros_like(db), da=da,
+                            p=0.2, key=key, site=7)
+    assert torch.equal(dh2, dh)
+    ref_da = dh.clone()
+    ops.dropout_bwd(ref_da, 0.2, key, 7)
+    assert torch.equal(da, ref_da)
 
 
 @pytest.mark.parametrize('Bg', [300, 6000])  # single-kernel path / partials path (G*Bg > 16384)
