@@ -25,6 +25,10 @@ extern "C" {
 int rs_version(void);                 /* ABI version (integer, bumps on signature change) */
 const char* rs_last_error(void);      /* thread-local message of the last failing call */
 int rs_device_check(void);            /* 0 if a gfx950 device is current, else hipError / -1 */
+/* Profiling only: launches an empty one-lane kernel (prof_marker_kernel) on the stream so that
+ * a rocprofv3 --pmc pass can attribute the dispatches between two markers to one entry point
+ * (bench.py --pmc-bracket, tools/pmc_traffic.py). Not on the training path. */
+int rs_prof_marker(int tag, void* stream);
 
 /* ---------------------------------------------------------------- GEMM (fp32 MFMA)
  * C = epi(alpha * op(A) @ op(B))  with op(A)[m,k] = transA ? A[k*lda+m] : A[m*lda+k],

@@ -82,6 +82,7 @@ SIGNATURES = {
     'rs_scale_inplace': (i32, [vp, i64, f32, vp, vp]),
     'rs_adam_step': (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, vp, f32, vp, i32, vp]),
     'rs_counter_add': (i32, [vp, i64, vp]),
+    'rs_prof_marker': (i32, [i32, vp]),
     'rs_sum': (i32, [vp, i32, f32, vp, vp]),
     'rs_rng_next': (i32, [vp, vp, vp]),
     'rs_adam_prepare': (i32, [vp, vp, i32, f32, f32, f32, vp]),

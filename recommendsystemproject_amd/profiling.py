@@ -122,41 +122,79 @@ WORK = {
 }
 
 
-class KernelTimer:
-    """Wraps _hip.call: an event pair on the current (launch) stream around every rs_* call."""
+class _CallPatch:
+    """Swap `call` in _hip and in the modules that imported it by name."""
 
-    def __init__(self):
-        self.records = []
-
-    def __enter__(self):
+    def _install(self, fn):
         self._orig = _hip.call
-
-        def timed(name, *args):
-            s = torch.cuda.Event(enable_timing=True)
-            e = torch.cuda.Event(enable_timing=True)
-            s.record(torch.cuda.current_stream())
-            rc = self._orig(name, *args)
-            e.record(torch.cuda.current_stream())
-            fl, by = WORK[name](args) if name in WORK else (0.0, 0.0)
-            shape = tuple(args[:5]) if name == 'rs_gemm_f32' else None
-            self.records.append((name, s, e, fl, by, shape))
-            return rc
-
-        _hip.call = timed
-        # modules imported `call` by name: patch those bindings too
+        _hip.call = fn
         from . import ops, functions, optim
         self._patched = []
         for mod in (ops, functions, optim):
             if getattr(mod, 'call', None) is self._orig:
                 self._patched.append(mod)
-                mod.call = timed
-        return self
+                mod.call = fn
 
     def __exit__(self, *exc):
         _hip.call = self._orig
         for mod in self._patched:
             mod.call = self._orig
         return False
+
+
+class PmcBracket(_CallPatch):
+    """Brackets every call of one entry point with rs_prof_marker dispatches, so that a
+    rocprofv3 --pmc pass can sum the counters of exactly the kernels that entry point launched
+    (tools/pmc_traffic.py). Records the algorithmic bytes/flops of the bracketed calls."""
+
+    def __init__(self, target):
+        self.target = target
+        self.launches = 0
+        self.flops = 0.0
+        self.bytes = 0.0
+
+    def __enter__(self):
+        orig = _hip.call
+
+        def bracketed(name, *args):
+            if name != self.target:
+                return orig(name, *args)
+            st = torch.cuda.current_stream().cuda_stream
+            orig('rs_prof_marker', 1, st)
+            rc = orig(name, *args)
+            orig('rs_prof_marker', 2, st)
+            fl, by = WORK[name](args) if name in WORK else (0.0, 0.0)
+            self.launches += 1
+            self.flops += fl
+            self.bytes += by
+            return rc
+
+        self._install(bracketed)
+        return self
+
+
+class KernelTimer(_CallPatch):
+    """Wraps _hip.call: an event pair on the current (launch) stream around every rs_* call."""
+
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        orig = _hip.call
+
+        def timed(name, *args):
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record(torch.cuda.current_stream())
+            rc = orig(name, *args)
+            e.record(torch.cuda.current_stream())
+            fl, by = WORK[name](args) if name in WORK else (0.0, 0.0)
+            shape = tuple(args[:5]) if name == 'rs_gemm_f32' else None
+            self.records.append((name, s, e, fl, by, shape))
+            return rc
+
+        self._install(timed)
+        return self
 
     def gemm_shapes(self):
         """{(transA, transB, M, N, K): [ms, launches, flops]} for rs_gemm_f32."""

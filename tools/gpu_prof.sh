@@ -1,5 +1,6 @@
 #!/bin/bash
-# rocprofv3 kernel-trace stats + separate PMC passes (FETCH_SIZE, WRITE_SIZE) of a short bench.
+# rocprofv3 kernel-trace stats of a short bench, then (PMC=1) HBM traffic of the dominant entry
+# point: bench.py --pmc-bracket under separate FETCH_SIZE / WRITE_SIZE --pmc passes.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 mkdir -p gpurun_out/prof
@@ -9,8 +10,10 @@ B="bench.py --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline ${BENCH_ARGS}"
 rc=$?; echo "trace rc=$rc"; tail -3 gpurun_out/prof/trace.log; [ $rc -eq 0 ] || exit $rc
 if [ -n "$PMC" ]; then
 for ctr in FETCH_SIZE WRITE_SIZE; do
-  ( cd /tmp && timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace -d $ROOT/gpurun_out/prof/pmc_$ctr -o run --output-format csv -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-graph ${BENCH_ARGS} ) > gpurun_out/prof/pmc_$ctr.log 2>&1
+  ( cd /tmp && timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d $ROOT/gpurun_out/prof/pmc_$ctr -o run --output-format csv -- python3 $ROOT/bench.py --warmup 2 --pmc-bracket ${BRACKET:-auto} ${BENCH_ARGS} ) > gpurun_out/prof/pmc_$ctr.log 2>&1
   rc=$?; echo "pmc $ctr rc=$rc"; tail -2 gpurun_out/prof/pmc_$ctr.log; [ $rc -eq 0 ] || exit $rc
 done
+python3 tools/pmc_traffic.py gpurun_out/prof gpurun_out/prof/pmc_FETCH_SIZE.log > gpurun_out/prof/traffic.json
+echo "traffic rc=$?"; cat gpurun_out/prof/traffic.json | head -12
 fi
-find gpurun_out/prof -name '*.csv' | head -20
+python3 tools/prof_summary.py gpurun_out/prof > gpurun_out/prof/summary.txt; echo "summary rc=$?"
