@@ -57,6 +57,13 @@ int rs_prof_marker(int tag, void* stream);
  * instance exists (the encoder's streaming shapes) A and B are rounded to bf16 (RNE) and the
  * products accumulate in fp32; every other shape runs the fp32 kernels unchanged. */
 #define RS_GEMM_BF16 256
+/* Storage flags in the same word (bf16 compute mode only): A holds bf16 elements (lda counted in
+ * elements) / C is written as bf16 (RNE of the fp32 epilogue result). For operands that are only
+ * ever consumed as bf16 MFMA operands (the encoder's packed qkv and its gradient) this halves their
+ * HBM bytes without changing any product. Only the streaming bf16 instances accept them; a call
+ * none covers fails with a bad-argument error (never a silent conversion). */
+#define RS_GEMM_A_BF16 512
+#define RS_GEMM_C_BF16 1024
 int rs_gemm_auto_split(int M, int N, int K);   /* split_k that fills the chip for long K */
 int64_t rs_gemm_ws_bytes(int M, int N, int K, int split_k);
 int rs_gemm_f32(int transA, int transB, int M, int N, int K, float alpha,
@@ -173,7 +180,10 @@ int rs_seq_mask(const int64_t* seq, int64_t ld_seq, int B, int L, int64_t pad_va
  * inside nn.MultiheadAttention (SequenceEncoder.py:17-29 via TransformerEncoderLayer, K6).
  * p > 0: dropout on the attention probabilities with the rs_dropout mask of (key, site).
  * flags: RS_GEMM_BF16 -> the products on bf16 MFMA (operands rounded to bf16; softmax, dropout
- * and dS arithmetic in fp32) where the MFMA kernels apply (head_dim 16, L <= 64), else 0. */
+ * and dS arithmetic in fp32) where the MFMA kernels apply (head_dim 16, L <= 64), else 0.
+ * RS_ATTN_QKV_BF16 (with RS_GEMM_BF16, on that path only): qkv is bf16 storage and rs_attn_bwd
+ * writes dqkv as bf16 (RNE); Q, K, V are MFMA operands only, so the products are unchanged. */
+#define RS_ATTN_QKV_BF16 2048
 int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out, float* lse,
                 int B, int L, int d, int H, float scale, float p, const int64_t* key, int site,
                 int flags, void* stream);

@@ -14,6 +14,8 @@ LIB_PATH = os.path.join(_HERE, '_lib', 'librsys_hip.so')
 
 RS_EPI_BIAS, RS_EPI_RELU, RS_EPI_AUX_ADD, RS_EPI_AUX_MASK = 1, 2, 4, 8
 RS_GEMM_BF16 = 256
+RS_GEMM_A_BF16, RS_GEMM_C_BF16 = 512, 1024
+RS_ATTN_QKV_BF16 = 2048
 RS_EPI_DROP_A, RS_EPI_DROP_B = 16, 32
 RS_SEG_SPARSE, RS_SEG_POOL, RS_SEG_DENSE, RS_SEG_LASTVALID, RS_SEG_COPY = 0, 1, 2, 3, 4
 RS_POOL = {'mean': 0, 'sum': 1, 'max': 2}

@@ -9,6 +9,8 @@
 // saves only the per-row log-sum-exp (flash-style), the backward recomputes P from it.
 //   fwd  HBM: qkv slice in (3*L*hd*4 B) + out (L*hd*4 B) + lse
 //   bwd  two passes over the (query, key) pairs: lane-per-query for dQ, lane-per-key for dK/dV.
+#include <type_traits>
+
 #include "common.h"
 #include "rng.h"
 
@@ -478,9 +480,19 @@ __device__ __forceinline__ void col_frags(const float* X, int r, int q, s4v (&ou
   }
 }
 
-template <int NT, bool DROP>
+// qkv / dqkv storage: fp32, or bf16 (RS_ATTN_QKV_BF16). Q, K and V are only ever MFMA operands
+// here (rounded to bf16 by bf4), so bf16 storage gives the same products with half the bytes.
+__device__ __forceinline__ f4 ldq(const float* p) { return ld4(p); }
+__device__ __forceinline__ f4 ldq(const __bf16* p) {
+  const bf4v h = *reinterpret_cast<const bf4v*>(p);  // 8-byte load; bf16 -> fp32 is exact
+  return f4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+}
+__device__ __forceinline__ void stq(float* p, float v) { *p = v; }
+__device__ __forceinline__ void stq(__bf16* p, float v) { *p = (__bf16)v; }
+
+template <int NT, bool DROP, bool QB>
 __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
-    const float* __restrict__ qkv, const uint8_t* __restrict__ key_pad, float* __restrict__ out,
+    const void* __restrict__ qkv_, const uint8_t* __restrict__ key_pad, float* __restrict__ out,
     float* __restrict__ lse, int B, int L, int d, int H, float scale, float pdrop,
     const int64_t* __restrict__ key, int site) {
   constexpr int LP = NT * 16;
@@ -491,16 +503,17 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
   if (bh >= B * H) return;  // whole wave exits together (no block barrier below)
   const int b = bh / H, h = bh % H;
   const int ld = 3 * d;
-  const float* base = qkv + (int64_t)b * L * ld + h * 16;
+  typedef typename std::conditional<QB, __bf16, float>::type QT;
+  const QT* base = reinterpret_cast<const QT*>(qkv_) + (int64_t)b * L * ld + h * 16;
   float(*Vs)[kRowP] = Vsm[wave];
   s4v qb[NT], kb[NT], vb[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int row = t * 16 + r;
     const f4 z = {0.f, 0.f, 0.f, 0.f};
-    qb[t] = bf4(row < L ? ld4(base + (int64_t)row * ld + 4 * q) : z);
-    kb[t] = bf4(row < L ? ld4(base + (int64_t)row * ld + d + 4 * q) : z);
-    *reinterpret_cast<f4*>(&Vs[row][4 * q]) = row < L ? ld4(base + (int64_t)row * ld + 2 * d + 4 * q) : z;
+    qb[t] = bf4(row < L ? ldq(base + (int64_t)row * ld + 4 * q) : z);
+    kb[t] = bf4(row < L ? ldq(base + (int64_t)row * ld + d + 4 * q) : z);
+    *reinterpret_cast<f4*>(&Vs[row][4 * q]) = row < L ? ldq(base + (int64_t)row * ld + 2 * d + 4 * q) : z;
   }
   bool kok[NT][4];
 #pragma unroll
@@ -555,11 +568,11 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
   }
 }
 
-template <int NT, bool DROP>
+template <int NT, bool DROP, bool QB>
 __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
-    const float* __restrict__ qkv, const uint8_t* __restrict__ key_pad,
+    const void* __restrict__ qkv_, const uint8_t* __restrict__ key_pad,
     const float* __restrict__ out, const float* __restrict__ dout, const float* __restrict__ lse,
-    float* __restrict__ dqkv, int B, int L, int d, int H, float scale, float pdrop,
+    void* __restrict__ dqkv_, int B, int L, int d, int H, float scale, float pdrop,
     const int64_t* __restrict__ key, int site) {
   constexpr int LP = NT * 16;
   // pitch 24: the transpose's ds_read_b128 (rows r, columns 4q) is conflict-free; its b32 writes
@@ -574,7 +587,8 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
   if (bh >= B * H) return;
   const int b = bh / H, h = bh % H;
   const int ld = 3 * d;
-  const float* base = qkv + (int64_t)b * L * ld + h * 16;
+  typedef typename std::conditional<QB, __bf16, float>::type QT;
+  const QT* base = reinterpret_cast<const QT*>(qkv_) + (int64_t)b * L * ld + h * 16;
   const float* gbase = dout + (int64_t)b * L * d + h * 16;
   const float* obase = out + (int64_t)b * L * d + h * 16;
   float* T = Xsm[wave];
@@ -586,9 +600,9 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
     const int row = t * 16 + r;
     const f4 z = {0.f, 0.f, 0.f, 0.f};
     const bool ok = row < L;
-    qf[t] = ok ? ld4(base + (int64_t)row * ld + 4 * q) : z;
-    kf[t] = ok ? ld4(base + (int64_t)row * ld + d + 4 * q) : z;
-    vb[t] = bf4(ok ? ld4(base + (int64_t)row * ld + 2 * d + 4 * q) : z);
+    qf[t] = ok ? ldq(base + (int64_t)row * ld + 4 * q) : z;
+    kf[t] = ok ? ldq(base + (int64_t)row * ld + d + 4 * q) : z;
+    vb[t] = bf4(ok ? ldq(base + (int64_t)row * ld + 2 * d + 4 * q) : z);
     gf[t] = ok ? ld4(gbase + (int64_t)row * d + 4 * q) : z;
     const f4 of = ok ? ld4(obase + (int64_t)row * d + 4 * q) : z;
     Di[t] = xsum(gf[t][0] * of[0] + gf[t][1] * of[1] + gf[t][2] * of[2] + gf[t][3] * of[3]);
@@ -624,7 +638,7 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
   DropKey dk;
   if (DROP) dk = make_key(key, site, pdrop);
   const float scale2 = scale * kLog2e;
-  float* dbase = dqkv + (int64_t)b * L * ld + h * 16;
+  QT* dbase = reinterpret_cast<QT*>(dqkv_) + (int64_t)b * L * ld + h * 16;
   f4 dv_acc[NT], dk_acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) dv_acc[t] = dk_acc[t] = f4{0.f, 0.f, 0.f, 0.f};
@@ -653,7 +667,7 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int row = tq * 16 + 4 * q + e;
-      if (row < L) dbase[(int64_t)row * ld + r] = dq[e] * scale;
+      if (row < L) stq(dbase + (int64_t)row * ld + r, dq[e] * scale);
     }
     // dV[key][c] += PZ^T dO and dK[key][c] += dS^T Q: A = [key = lane & 15][query], i.e. the
     // transpose of this lane's tiles, through T (T[key][query])
@@ -682,8 +696,8 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
     for (int e = 0; e < 4; ++e) {
       const int row = tk * 16 + 4 * q + e;
       if (row < L) {
-        dbase[(int64_t)row * ld + d + r] = dk_acc[tk][e] * scale;
-        dbase[(int64_t)row * ld + 2 * d + r] = dv_acc[tk][e];
+        stq(dbase + (int64_t)row * ld + d + r, dk_acc[tk][e] * scale);
+        stq(dbase + (int64_t)row * ld + 2 * d + r, dv_acc[tk][e]);
       }
     }
 }
@@ -723,15 +737,21 @@ extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out,
   const size_t lds = (size_t)(2 * L * hd + L) * sizeof(float);
   RS_CHECK_ARG(lds <= 64 * 1024, "rs_attn_fwd: L=%d hd=%d exceeds LDS", L, hd);
   RS_CHECK_ARG(d % 4 == 0 && aligned16(qkv) && aligned16(out), "rs_attn_fwd: needs 16-byte aligned rows");
+  RS_CHECK_ARG(!(flags & RS_ATTN_QKV_BF16) || ((flags & RS_GEMM_BF16) && hd == 16 && L <= 64 &&
+                                                 !getenv_flag("RSYS_ATTN_VALU")),
+               "rs_attn_fwd: bf16 qkv storage needs the bf16 MFMA path (head_dim 16, L <= 64)");
   hipStream_t st = as_stream(stream);
   if (hd == 16 && L <= 64 && (int64_t)B * H * L * L < ((int64_t)1 << 32) && !getenv_flag("RSYS_ATTN_VALU")) {
     const int nt = (L + 15) / 16;
     const dim3 g4(cdiv((int64_t)B * H, 4));
     const bool bf = (flags & RS_GEMM_BF16) != 0;
+    const bool qb = (flags & RS_ATTN_QKV_BF16) != 0;
 #define RS_AF(NTV)                                                                                  \
   if (nt == NTV) {                                                                                  \
-    if (bf && p > 0.f) attn_fwd_bf16_kernel<NTV, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
-    else if (bf) attn_fwd_bf16_kernel<NTV, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    if (qb && p > 0.f) attn_fwd_bf16_kernel<NTV, true, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    else if (qb) attn_fwd_bf16_kernel<NTV, false, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    else if (bf && p > 0.f) attn_fwd_bf16_kernel<NTV, true, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    else if (bf) attn_fwd_bf16_kernel<NTV, false, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
     else if (p > 0.f) attn_fwd_mfma_kernel<NTV, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
     else attn_fwd_mfma_kernel<NTV, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
   }
@@ -760,16 +780,22 @@ extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float
   const size_t lds = (size_t)(4 * L * hd + 3 * L) * sizeof(float);
   RS_CHECK_ARG(lds <= 64 * 1024, "rs_attn_bwd: L=%d hd=%d exceeds LDS", L, hd);
   RS_CHECK_ARG(d % 4 == 0 && aligned16(qkv) && aligned16(dout), "rs_attn_bwd: needs 16-byte aligned rows");
+  RS_CHECK_ARG(!(flags & RS_ATTN_QKV_BF16) || ((flags & RS_GEMM_BF16) && hd == 16 && L <= 64 &&
+                                                 !getenv_flag("RSYS_ATTN_VALU")),
+               "rs_attn_bwd: bf16 qkv storage needs the bf16 MFMA path (head_dim 16, L <= 64)");
   hipStream_t st = as_stream(stream);
   if (hd == 16 && L <= 64 && (int64_t)B * H * L * L < ((int64_t)1 << 32) && !getenv_flag("RSYS_ATTN_VALU")) {
     RS_CHECK_ARG(aligned16(out), "rs_attn_bwd: needs 16-byte aligned rows");
     const int nt = (L + 15) / 16;
     const dim3 g4(cdiv((int64_t)B * H, 4));
     const bool bf = (flags & RS_GEMM_BF16) != 0;
+    const bool qb = (flags & RS_ATTN_QKV_BF16) != 0;
 #define RS_AB(NTV)                                                                                  \
   if (nt == NTV) {                                                                                  \
-    if (bf && p > 0.f) attn_bwd_bf16_kernel<NTV, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
-    else if (bf) attn_bwd_bf16_kernel<NTV, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    if (qb && p > 0.f) attn_bwd_bf16_kernel<NTV, true, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    else if (qb) attn_bwd_bf16_kernel<NTV, false, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    else if (bf && p > 0.f) attn_bwd_bf16_kernel<NTV, true, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    else if (bf) attn_bwd_bf16_kernel<NTV, false, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
     else if (p > 0.f) attn_bwd_mfma_kernel<NTV, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
     else attn_bwd_mfma_kernel<NTV, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
   }

@@ -304,7 +304,10 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
   RS_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "rs_gemm_f32: negative size M=%d N=%d K=%d", M, N, K);
   if (M == 0 || N == 0) return 0;
   const int mode = epilogue & RS_GEMM_BF16;  // a compute-mode flag, not an epilogue stage
-  epilogue &= ~RS_GEMM_BF16;
+  const int io = epilogue & (RS_GEMM_A_BF16 | RS_GEMM_C_BF16);  // bf16 storage of A / C
+  epilogue &= ~(RS_GEMM_BF16 | RS_GEMM_A_BF16 | RS_GEMM_C_BF16);
+  RS_CHECK_ARG(!io || (mode && !transA && !rowsum && split_k <= 1),
+               "rs_gemm_f32: bf16 A/C storage needs RS_GEMM_BF16, transA = 0, no rowsum/split-K");
   RS_CHECK_ARG(A && B && C, "rs_gemm_f32: null operand");
   RS_CHECK_ARG(ldc >= N, "rs_gemm_f32: ldc %d < N %d", ldc, N);
   RS_CHECK_ARG(transA ? lda >= M : lda >= K, "rs_gemm_f32: bad lda %d", lda);
@@ -338,11 +341,12 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
   {
     StreamArgs sa{};
     sa.M = M; sa.N = N; sa.K = K; sa.alpha = alpha; sa.beta = beta; sa.A = A; sa.lda = lda;
-    sa.B = B; sa.ldb = ldb; sa.C = C; sa.ldc = ldc; sa.epi = epilogue | mode; sa.bias = bias;
+    sa.B = B; sa.ldb = ldb; sa.C = C; sa.ldc = ldc; sa.epi = epilogue | mode | io; sa.bias = bias;
     sa.aux = aux; sa.ld_aux = ld_aux; sa.aux_mod = g.aux_mod; sa.rowsum = rowsum; sa.ws = ws;
     sa.transB = transB;
     sa.drop_p = drop_p; sa.drop_key = drop_key; sa.site_a = site_a; sa.site_b = site_b;
     if (!rowsum && rowgemm_supported(transA, M, N, K, A, lda)) return rowgemm_launch(sa, st);
+    RS_CHECK_ARG(!io, "rs_gemm_f32: no streaming instance for bf16 A/C storage (M=%d N=%d K=%d)", M, N, K);
     if (ws && wgrad_supported(transA, transB, M, N, K, A, lda, B, ldb, ldc, epilogue))
       return wgrad_launch(sa, st);
   }

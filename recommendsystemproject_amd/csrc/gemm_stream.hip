@@ -795,8 +795,13 @@ __device__ __forceinline__ bf16x8 cvt8(const floatx4& lo, const floatx4& hi) {
   return r;
 }
 
-template <int NT, int KC, bool LN, int EPI>
+// IO bit 0: A is bf16 storage (RS_GEMM_A_BF16; loaded as bf16x8, no conversion); bit 1: C is
+// written as bf16 (RS_GEMM_C_BF16; 8-byte stores). Either leaves every product unchanged.
+template <int NT, int KC, bool LN, int EPI, int IO = 0>
 __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
+  constexpr bool ABF = (IO & 1) != 0, CBF = (IO & 2) != 0;
+  static_assert(!(CBF && (LN || (EPI & (RS_EPI_AUX_MASK | kEpiBeta)) != 0)),
+                "bf16 C: no epilogue that reads C or aux rows");
   constexpr int KK = KC * 64;
   constexpr int KPH = KK + 8;  // LDS pitch in bf16 (16-byte pad: conflict-free b128 reads)
   constexpr int NTN = NT * 16;
@@ -841,13 +846,24 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
   const int stride = gridDim.x * 8;
   int g = blockIdx.x * 8 + wave;
   typedef const __attribute__((address_space(1))) floatx4* gptr4;
-  floatx4 araw[KC][4];
+  typedef const __attribute__((address_space(1))) bf16x8* gptrb8;
+  floatx4 araw[ABF ? 1 : KC][4];
+  bf16x8 abraw[ABF ? KC : 1][2];
   auto load_raw = [&](int gg, floatx4 (*dst)[4]) {
-    const float* row = a.A + (int64_t)(gg * 16 + r) * a.lda + 16 * q;
+    if constexpr (ABF) {
+      const __bf16* row = reinterpret_cast<const __bf16*>(a.A) + (int64_t)(gg * 16 + r) * a.lda + 16 * q;
 #pragma unroll
-    for (int c = 0; c < KC; ++c)
+      for (int c = 0; c < KC; ++c) {
+        abraw[c][0] = *(gptrb8)(row + 64 * c);
+        abraw[c][1] = *(gptrb8)(row + 64 * c + 8);
+      }
+    } else {
+      const float* row = a.A + (int64_t)(gg * 16 + r) * a.lda + 16 * q;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) dst[c][u] = *(gptr4)(row + 64 * c + 4 * u);
+      for (int c = 0; c < KC; ++c)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dst[c][u] = *(gptr4)(row + 64 * c + 4 * u);
+    }
   };
   if (g < groups) load_raw(g, araw);
   constexpr bool EPRE = !LN && (EPI & (RS_EPI_AUX_MASK | kEpiBeta)) != 0;
@@ -870,8 +886,13 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
     bf16x8 af[KC][2];
 #pragma unroll
     for (int c = 0; c < KC; ++c) {
-      af[c][0] = cvt8(araw[c][0], araw[c][1]);
-      af[c][1] = cvt8(araw[c][2], araw[c][3]);
+      if constexpr (ABF) {
+        af[c][0] = abraw[c][0];
+        af[c][1] = abraw[c][1];
+      } else {
+        af[c][0] = cvt8(araw[c][0], araw[c][1]);
+        af[c][1] = cvt8(araw[c][2], araw[c][3]);
+      }
     }
     load_raw(g + stride < groups ? g + stride : g, araw);  // next group, no branch
     floatx4 lnacc[LN ? NT : 1];
@@ -910,8 +931,14 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
             auxv = *reinterpret_cast<const floatx4*>(saux + (m % a.aux_mod) * NTN + nl);
           if constexpr ((EPI & RS_EPI_AUX_MASK) != 0) auxv = epre[j0 + h];
           if constexpr ((EPI & kEpiBeta) != 0) cv = epre[j0 + h];
-          *reinterpret_cast<floatx4*>(a.C + (int64_t)m * a.ldc + nl) =
-              epi4_ct<EPI>(a, m, nl, acc[h] * a.alpha, ka, kb, biasv, auxv, cv);
+          const floatx4 v = epi4_ct<EPI>(a, m, nl, acc[h] * a.alpha, ka, kb, biasv, auxv, cv);
+          if constexpr (CBF) {
+            bf16x4w o;
+            o[0] = (__bf16)v[0]; o[1] = (__bf16)v[1]; o[2] = (__bf16)v[2]; o[3] = (__bf16)v[3];
+            *reinterpret_cast<bf16x4w*>(reinterpret_cast<__bf16*>(a.C) + (int64_t)m * a.ldc + nl) = o;
+          } else {
+            *reinterpret_cast<floatx4*>(a.C + (int64_t)m * a.ldc + nl) = v;
+          }
         }
       }
     }
@@ -958,24 +985,33 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   if (bx < 1) bx = 1;
   const dim3 blocks(bx, nsplit);
   // bf16 compute mode: the bf16-MFMA instances (fp32 kernels below for anything else)
-  const int ekey = (s.epi & ~RS_GEMM_BF16) | (s.beta != 0.f ? kEpiBeta : 0);
+  const int io = ((s.epi & RS_GEMM_A_BF16) ? 1 : 0) | ((s.epi & RS_GEMM_C_BF16) ? 2 : 0);
+  const int ekey = (s.epi & ~(RS_GEMM_BF16 | RS_GEMM_A_BF16 | RS_GEMM_C_BF16)) | (s.beta != 0.f ? kEpiBeta : 0);
   if ((s.epi & RS_GEMM_BF16) && !small && s.vec_epi && s.M % 16 == 0 && s.K % 64 == 0 &&
       s.ldb % 4 == 0 && aligned16(s.B) &&
-      s.N == nt * 16 && s.lda % 4 == 0 && (!(s.epi & RS_EPI_AUX_ADD) || (int64_t)s.aux_mod * nt * 16 * 4 <= 48 * 1024)) {
+      s.N == nt * 16 && s.lda % ((io & 1) ? 8 : 4) == 0 && (!(io & 1) || aligned16(s.A)) &&
+      (!(s.epi & RS_EPI_AUX_ADD) || (int64_t)s.aux_mod * nt * 16 * 4 <= 48 * 1024)) {
     const int kc = s.K / 64;
     const size_t ldsb = (size_t)nt * 16 * (s.K + 8) * 2 + (size_t)(nt * 16 + ((s.epi & RS_EPI_AUX_ADD) ? s.aux_mod * nt * 16 : 0)) * 4;
     const int per_cub = ldsb > 80 * 1024 ? 1 : (ldsb > 53 * 1024 ? 2 : (ldsb > 40 * 1024 ? 3 : 4));
     int bxb = cdiv(s.M / 16, 16);
     if (bxb > 256 * per_cub) bxb = 256 * per_cub;
-#define RS_RGB(NTV, KCV, EV)                                                                      \
-    if (nt == NTV && kc == KCV && ekey == EV) {                                                   \
-      rowgemm_bf16_kernel<NTV, KCV, false, EV><<<bxb, 512, ldsb, st>>>(s);                        \
+#define RS_RGB(NTV, KCV, EV, IOV)                                                                 \
+    if (nt == NTV && kc == KCV && ekey == EV && io == IOV) {                                      \
+      rowgemm_bf16_kernel<NTV, KCV, false, EV, IOV><<<bxb, 512, ldsb, st>>>(s);                   \
       RS_CHECK_LAUNCH("rowgemm bf16");                                                            \
       return 0;                                                                                   \
     }
-    RS_RGB(16, 1, 19) RS_RGB(16, 1, 3) RS_RGB(16, 1, 8) RS_RGB(16, 1, 0) RS_RGB(12, 1, 1)
-    RS_RGB(4, 3, 64) RS_RGB(4, 4, 64) RS_RGB(4, 1, 0) RS_RGB(4, 1, 64) RS_RGB(4, 4, 0) RS_RGB(4, 3, 0)
+    RS_RGB(16, 1, 19, 0) RS_RGB(16, 1, 3, 0) RS_RGB(16, 1, 8, 0) RS_RGB(16, 1, 0, 0) RS_RGB(12, 1, 1, 0)
+    RS_RGB(4, 3, 64, 0) RS_RGB(4, 4, 64, 0) RS_RGB(4, 1, 0, 0) RS_RGB(4, 1, 64, 0) RS_RGB(4, 4, 0, 0)
+    RS_RGB(4, 3, 0, 0)
+    // bf16 storage: the qkv projection's output (C) and its input gradient's dqkv operand (A)
+    RS_RGB(12, 1, 1, 2) RS_RGB(12, 1, 0, 2) RS_RGB(4, 3, 64, 1) RS_RGB(4, 3, 0, 1)
 #undef RS_RGB
+  }
+  if (io != 0) {
+    set_error("rowgemm: no bf16-storage instance for M=%d N=%d K=%d epi=%d", s.M, s.N, s.K, s.epi);
+    return -1;
   }
   // specialised (compile-time epilogue) instances for the encoder's GEMMs
   const bool aux_small = !(s.epi & RS_EPI_AUX_ADD) || (int64_t)s.aux_mod * nt * 16 * 4 <= 48 * 1024;
@@ -1102,6 +1138,7 @@ int wgrad_bf16_launch(const StreamArgs& s, bool y_bf16, bool x_bf16, hipStream_t
     RS_WB(64, 32, false, false) RS_WB(128, 256, false, false) RS_WB(256, 128, false, false)
     RS_WB(64, 96, false, false) RS_WB(96, 64, false, false)
     RS_WB(64, 256, false, true) RS_WB(256, 64, true, false)  // the fused FFN's weight gradients
+    RS_WB(192, 64, true, false)  // in_proj from the bf16 dqkv (RS_ATTN_QKV_BF16)
     default:
       set_error("wgrad bf16: no instance for %dx%d (bf16 operands %d/%d)", s.M, s.N, (int)y_bf16,
                 (int)x_bf16);

@@ -132,7 +132,9 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key):
 def layer_fwd(lyr, x, key_pad, B, L, d, H, p, key, site):
     """nn.TransformerEncoderLayer (norm_first=False, relu) forward on x [B*L, d]."""
     sa_mod = lyr.self_attn
-    qkv = ops.linear_fwd(x, sa_mod.in_proj_weight, sa_mod.in_proj_bias)
+    # bf16 mode: qkv stored as bf16 (only ever an MFMA operand: same products, half the bytes)
+    qkv = ops.linear_fwd(x, sa_mod.in_proj_weight, sa_mod.in_proj_bias,
+                         out_dtype=torch.bfloat16 if ops.qkv_bf16_ok(L, d, H) else torch.float32)
     att, lse = ops.attn_fwd(qkv, key_pad, B, L, d, H, p, key, site)
     # h1 = x + dropout1(out_proj(att)), x1 = norm1(h1): GEMM + residual + LayerNorm in one kernel
     h1, x1, m1, r1 = ops.linear_add_layernorm(att, sa_mod.out_proj.weight, sa_mod.out_proj.bias, x,
@@ -183,7 +185,10 @@ def layer_bwd(lyr, saved, dx2, key_pad, B, L, d, H, p, key, site):
     ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
     datt = ops.linear_bwd_input(dsa, sa_mod.out_proj.weight)
     dqkv = ops.attn_bwd(qkv, key_pad, att, datt, lse, B, L, d, H, p, key, site)
-    ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
+    if dqkv.dtype == torch.bfloat16:  # bf16 dqkv (RS_ATTN_QKV_BF16): bf16-MFMA weight gradient
+        ops.wgrad_bf16(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
+    else:
+        ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
     ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight, out=dh1, beta=1.0)  # dx = dh1 + dqkv Win
     return dh1
 

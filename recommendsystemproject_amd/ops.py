@@ -45,16 +45,23 @@ def gemm(A, B, C, M, N, K, *, transA, transB, lda, ldb, ldc, alpha=1.0, beta=0.0
     return C
 
 
+def _io_flags(a, c):
+    """bf16 storage of the A operand / the output C (bf16 compute mode, streaming instances)."""
+    return (_hip.RS_GEMM_A_BF16 if a.dtype == torch.bfloat16 else 0) | \
+        (_hip.RS_GEMM_C_BF16 if c.dtype == torch.bfloat16 else 0)
+
+
 def linear_fwd(x, W, b=None, out=None, *, relu=False, aux=None, aux_mod=0, beta=0.0,
-               drop_p=0.0, drop_key=None, site_a=None, site_b=None):
+               drop_p=0.0, drop_key=None, site_a=None, site_b=None, out_dtype=torch.float32):
     """out[M,N] = drop_b(drop_a(relu(x[M,K] @ W[N,K]^T + b)) + aux[m % aux_mod]) (+ beta*out);
-    dropout stages are active when drop_p > 0 and their site is given."""
+    dropout stages are active when drop_p > 0 and their site is given. out_dtype bf16: the
+    result is stored as bf16 (only for outputs consumed as bf16 MFMA operands)."""
     M, K = x.shape
     N = W.shape[0]
     if out is None:
-        out = torch.empty(M, N, device=x.device, dtype=torch.float32)
+        out = torch.empty(M, N, device=x.device, dtype=out_dtype)
     epi = (_hip.RS_EPI_BIAS if b is not None else 0) | (_hip.RS_EPI_RELU if relu else 0) | \
-        (_hip.RS_EPI_AUX_ADD if aux is not None else 0)
+        (_hip.RS_EPI_AUX_ADD if aux is not None else 0) | _io_flags(x, out)
     if drop_p > 0:
         epi |= (_hip.RS_EPI_DROP_A if site_a is not None else 0) | (_hip.RS_EPI_DROP_B if site_b is not None else 0)
     return gemm(x, W, out, M, N, K, transA=0, transB=1, lda=x.stride(0), ldb=W.stride(0),
@@ -69,7 +76,7 @@ def linear_bwd_input(dy, W, out=None, *, beta=0.0, relu_mask_of=None, alpha=1.0)
     K = W.shape[1]
     if out is None:
         out = torch.empty(M, K, device=dy.device, dtype=torch.float32)
-    epi = _hip.RS_EPI_AUX_MASK if relu_mask_of is not None else 0
+    epi = (_hip.RS_EPI_AUX_MASK if relu_mask_of is not None else 0) | _io_flags(dy, out)
     return gemm(dy, W, out, M, K, N, transA=0, transB=0, lda=dy.stride(0), ldb=W.stride(0),
                 ldc=out.stride(0), alpha=alpha, beta=beta, epi=epi, aux=relu_mask_of,
                 ld_aux=(relu_mask_of.stride(0) if relu_mask_of is not None else 0))
@@ -162,18 +169,30 @@ def gather_bwd(segs, rows, dout):
     call('rs_gather_bwd', arr, len(segs), rows, P(dout), dout.stride(0), None, stream())
 
 
+def qkv_bf16_ok(L, d, H):
+    """Store the packed qkv (and dqkv) as bf16: bf16 compute mode on the bf16 MFMA attention
+    path (head_dim 16, L <= 64), where Q, K, V are only MFMA operands (RS_ATTN_QKV_BF16)."""
+    return (precision.compute_dtype() == 'bf16' and d // H == 16 and L <= 64 and
+            not os.environ.get('RSYS_ATTN_VALU') and not os.environ.get('RSYS_QKV_FP32'))
+
+
+def _attn_flags(qkv):
+    return precision.gemm_flags() | (_hip.RS_ATTN_QKV_BF16 if qkv.dtype == torch.bfloat16 else 0)
+
+
 def attn_fwd(qkv, key_pad, B, L, d, H, p=0.0, key=None, site=0):
     out = torch.empty(B * L, d, device=qkv.device, dtype=torch.float32)
     lse = torch.empty(B * H * L, device=qkv.device, dtype=torch.float32)
     call('rs_attn_fwd', P(qkv), P(key_pad), P(out), P(lse), B, L, d, H,
-         float((d // H) ** -0.5), float(p), P(key), site, precision.gemm_flags(), stream())
+         float((d // H) ** -0.5), float(p), P(key), site, _attn_flags(qkv), stream())
     return out, lse
 
 
 def attn_bwd(qkv, key_pad, out, dout, lse, B, L, d, H, p=0.0, key=None, site=0):
-    dqkv = torch.empty(B * L, 3 * d, device=qkv.device, dtype=torch.float32)
+    """dqkv has qkv's storage dtype (bf16 with RS_ATTN_QKV_BF16)."""
+    dqkv = torch.empty(B * L, 3 * d, device=qkv.device, dtype=qkv.dtype)
     call('rs_attn_bwd', P(qkv), P(key_pad), P(out), P(dout), P(lse), P(dqkv), B, L, d, H,
-         float((d // H) ** -0.5), float(p), P(key), site, precision.gemm_flags(), stream())
+         float((d // H) ** -0.5), float(p), P(key), site, _attn_flags(qkv), stream())
     return dqkv
 
 

@@ -15,22 +15,27 @@ from . import _hip
 
 def _gemm_work(a):
     M, N, K = a[2], a[3], a[4]
-    beta = a[10]
-    return 2.0 * M * N * K, 4.0 * (M * K + K * N + M * N * (2 if beta != 0 else 1))
+    beta, epi = a[10], a[13]
+    ea = 2.0 if epi & _hip.RS_GEMM_A_BF16 else 4.0  # bf16 storage of A / C
+    ec = 2.0 if epi & _hip.RS_GEMM_C_BF16 else 4.0
+    return 2.0 * M * N * K, ea * M * K + 4.0 * K * N + ec * M * N + (4.0 * M * N if beta != 0 else 0.0)
 
 
 def _attn_fwd_work(a):
     B, L, d, H = a[4], a[5], a[6], a[7]
     hd = d // H
-    # QK^T twice (max pass + sum pass) and PV
-    return 2.0 * B * H * L * L * hd * 3, 4.0 * (B * L * 3 * d + B * L * d + B * H * L)
+    eq = 2.0 if a[12] & _hip.RS_ATTN_QKV_BF16 else 4.0
+    # QK^T twice (max pass + sum pass) and PV; qkv read, out + lse written
+    return 2.0 * B * H * L * L * hd * 3, eq * B * L * 3 * d + 4.0 * (B * L * d + B * H * L)
 
 
 def _attn_bwd_work(a):
     B, L, d, H = a[6], a[7], a[8], a[9]
     hd = d // H
-    # pass 1 (lane/query): s, dp, dq; pass 2 (lane/key): s, dp, dk, dv
-    return 2.0 * B * H * L * L * hd * 7, 4.0 * (B * L * 3 * d * 2 + 2 * B * L * d + B * H * L)
+    eq = 2.0 if a[14] & _hip.RS_ATTN_QKV_BF16 else 4.0
+    # pass 1 (lane/query): s, dp, dq; pass 2 (lane/key): s, dp, dk, dv; qkv read, dqkv written,
+    # out and dout read, lse read
+    return 2.0 * B * H * L * L * hd * 7, eq * B * L * 3 * d * 2 + 4.0 * (2 * B * L * d + B * H * L)
 
 
 def _gather_work(a, bwd=False):

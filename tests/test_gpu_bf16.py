@@ -370,3 +370,104 @@ def test_fused_ce_deterministic(bf16_mode):
         loss.backward()
         res.append((loss.item(), U.grad.clone(), I.grad.clone()))
     assert res[0][0] == res[1][0] and torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+
+
+# ------------------------------------------------------------ bf16 storage of qkv / dqkv
+@pytest.mark.parametrize('B,L,p', [(3, 50, 0.0), (4, 33, 0.1), (3, 1, 0.0), (2, 64, 0.0)])
+def test_qkv_bf16_storage_is_lossless(B, L, p, bf16_mode):
+    """RS_ATTN_QKV_BF16: Q, K, V enter the bf16 attention only as MFMA operands, so bf16 storage
+    gives bit-identical out / lse, and dqkv stored as bf16 is the fp32 dqkv rounded (RNE)."""
+    d, H = 64, 4
+    qkv = rnd(B * L, 3 * d, seed=21)
+    lens = torch.randint(1, L + 1, (B,))
+    seq = (torch.arange(L)[None, :] < lens[:, None]).long().to(DEV)
+    key_pad, _ = ops.seq_mask(seq, 0)
+    key = torch.tensor([5, 9], dtype=torch.int64, device=DEV)
+    dout = rnd(B * L, d, seed=22)
+    q16 = qkv.to(torch.bfloat16)
+    o32, l32 = ops.attn_fwd(q16.float(), key_pad, B, L, d, H, p, key, 3)
+    o16, l16 = ops.attn_fwd(q16, key_pad, B, L, d, H, p, key, 3)
+    assert torch.equal(o32, o16) and torch.equal(l32, l16)
+    g32 = ops.attn_bwd(q16.float(), key_pad, o32, dout, l32, B, L, d, H, p, key, 3)
+    g16 = ops.attn_bwd(q16, key_pad, o16, dout, l16, B, L, d, H, p, key, 3)
+    assert g16.dtype == torch.bfloat16
+    assert torch.equal(g16, g32.to(torch.bfloat16))
+
+
+def test_qkv_bf16_storage_gemms(bf16_mode):
+    """The streaming GEMM's bf16-storage instances: bf16 C == fp32 C rounded; bf16 A == fp32 A
+    (the kernel rounds fp32 A rows to bf16 in registers); the in_proj weight gradient from bf16
+    dqkv == from fp32 dqkv (dW bit-exact, db sums the bf16 values)."""
+    M, d = 40960, 64
+    x = rnd(M, d, seed=31)
+    W, b = rnd(3 * d, d, seed=32) * 0.1, rnd(3 * d, seed=33)
+    c32 = ops.linear_fwd(x, W, b)
+    c16 = ops.linear_fwd(x, W, b, out_dtype=torch.bfloat16)
+    assert c16.dtype == torch.bfloat16 and torch.equal(c16, c32.to(torch.bfloat16))
+    dq = rnd(M, 3 * d, seed=34).to(torch.bfloat16)
+    base = rnd(M, d, seed=35)
+    r32 = ops.linear_bwd_input(dq.float(), W, out=base.clone(), beta=1.0)
+    r16_ = ops.linear_bwd_input(dq, W, out=base.clone(), beta=1.0)
+    assert torch.equal(r32, r16_)
+    dW32, db32 = torch.zeros_like(W), torch.zeros_like(b)
+    dW16, db16 = torch.zeros_like(W), torch.zeros_like(b)
+    ops.wgrad_bf16(dq.float(), x, dW32, db=db32)
+    ops.wgrad_bf16(dq, x, dW16, db=db16)
+    assert torch.equal(dW32, dW16)
+    assert torch.allclose(db16, db32, atol=1e-3 * db32.abs().max().item())
+
+
+def test_qkv_bf16_storage_rejected_off_path():
+    """bf16 storage outside the bf16 MFMA path fails loudly (no silent conversion)."""
+    precision.set_compute_dtype('fp32')
+    x = rnd(4096, 64, seed=1)
+    W = rnd(192, 64, seed=2)
+    with pytest.raises(RuntimeError):
+        ops.linear_fwd(x, W, out_dtype=torch.bfloat16)
+
+
+def test_bf16_step_qkv_storage(monkeypatch):
+    """A whole bf16 step with bf16 qkv / dqkv storage against fp32 storage: identical loss and
+    gradients except the in_proj bias gradients (column sums of the bf16-rounded dqkv)."""
+    from oracle.twotower_oracle import model_state_shapes
+    from recommendsystemproject_amd import synth
+    from recommendsystemproject_amd.flat import ensure_flat
+    from recommendsystemproject_amd.project.models.TwoTower.GenericTower import GenericTower
+    from recommendsystemproject_amd.project.models.TwoTower.TwoTowerModel import TwoTowerModel
+    from recommendsystemproject_amd.project.utils.training_utils import extract_item_id
+    cfg = yaml.safe_load(open(os.path.join(ROOT, 'configs', 'c2.yaml')))
+    for t in cfg['two_tower'].values():
+        t['dropout'] = 0.0
+        t.get('transformer_parameters', {})['dropout'] = 0.0
+    maps = {'user': synth.tower_layout(cfg['two_tower']['user_tower']),
+            'item': synth.tower_layout(cfg['two_tower']['item_tower'])}
+    shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
+    state = synth.make_state(shapes, seed=3)
+    b = synth.batch_to_torch(synth.make_batch(cfg, 1024, seed=7), DEV)
+    res = {}
+    precision.set_compute_dtype('bf16')
+    try:
+        for mode in ('bf16', 'fp32'):
+            if mode == 'fp32':
+                monkeypatch.setenv('RSYS_QKV_FP32', '1')
+            m = TwoTowerModel(GenericTower(cfg, 'user_tower'), GenericTower(cfg, 'item_tower'),
+                              maps['user'], maps['item'])
+            m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()})
+            m = m.to(DEV)
+            f = ensure_flat(m)
+            f.zero_grad()
+            U, I, H = m(b)
+            loss = m.compute_loss(U, I, item_ids=extract_item_id(b['item_tower']), temperature=0.15)
+            loss.backward()
+            res[mode] = (loss.item(), {k: p.grad.clone() for k, p in m.named_parameters()})
+    finally:
+        precision.set_compute_dtype('fp32')
+    (l1, g1), (l2, g2) = res['bf16'], res['fp32']
+    assert l1 == l2
+    for k in g1:
+        if k.endswith('in_proj_bias'):
+            assert torch.allclose(g1[k], g2[k], atol=1e-2 * g2[k].abs().max().item()), k
+        elif 'in_proj_bias' not in k:
+            # everything upstream of the first layer's in_proj bias sees the same dqkv rounding
+            sc = g2[k].abs().max().item()
+            assert (g1[k] - g2[k]).abs().max().item() <= 1e-5 * max(sc, 1e-30), k
