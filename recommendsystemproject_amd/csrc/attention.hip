@@ -490,6 +490,49 @@ __device__ __forceinline__ f4 ldq(const __bf16* p) {
 __device__ __forceinline__ void stq(float* p, float v) { *p = v; }
 __device__ __forceinline__ void stq(__bf16* p, float v) { *p = (__bf16)v; }
 
+// Per-lane key-validity bits: bit 4t + e <-> key 16t + 4q + e (the lane's keys in S^T tile t),
+// from one coalesced byte load per lane and a wave ballot (L <= 64).
+template <int NT>
+__device__ __forceinline__ uint32_t key_bits(const uint8_t* __restrict__ key_pad, int b, int L,
+                                             int lane, int q) {
+  const bool valid = lane < L && key_pad[(int64_t)b * L + lane] == 0;
+  const uint64_t vm = __ballot(valid);
+  uint32_t kb = 0;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) kb |= (uint32_t)((vm >> (16 * t + 4 * q)) & 0xFu) << (4 * t);
+  return kb;
+}
+
+// dropout multipliers of keys 16 tk + 4q .. +3 of query row i: with L even the row base
+// ((bh L + i) L) and the 4-aligned key offset are even, so two pair hashes cover the 4 keys
+// (the same draws keep4_32 makes; odd L keeps the general path)
+__device__ __forceinline__ void attn_keep4(const DropKey& dk, bool leven, uint32_t idx0, float (&mk)[4]) {
+  if (leven) {
+    keep_pair32(dk, idx0 >> 1, mk[0], mk[1]);
+    keep_pair32(dk, (idx0 >> 1) + 1, mk[2], mk[3]);
+  } else {
+    keep4_32(dk, idx0, mk);
+  }
+}
+
+// 16x16 tile held as acc[e] = X[row 4q + e][col r] -> rows of 4 consecutive columns per lane
+// through the wave's LDS image T (pitch TP): lane l gets row l >> 2, columns 4 (l & 3) .. + 3
+template <int TP>
+__device__ __forceinline__ f4 tile_rows(float* T, const f4& acc, int r, int q, int lane) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) T[(4 * q + e) * TP + r] = acc[e];
+  __builtin_amdgcn_wave_barrier();
+  const f4 v = ld4(&T[(lane >> 2) * TP + 4 * (lane & 3)]);
+  __builtin_amdgcn_wave_barrier();
+  return v;
+}
+__device__ __forceinline__ void st4q(float* p, const f4& v) { *reinterpret_cast<f4*>(p) = v; }
+__device__ __forceinline__ void st4q(__bf16* p, const f4& v) {
+  bf4v h;
+  h[0] = (__bf16)v[0]; h[1] = (__bf16)v[1]; h[2] = (__bf16)v[2]; h[3] = (__bf16)v[3];
+  *reinterpret_cast<bf4v*>(p) = h;
+}
+
 template <int NT, bool DROP, bool QB>
 __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
     const void* __restrict__ qkv_, const uint8_t* __restrict__ key_pad, float* __restrict__ out,
@@ -515,19 +558,15 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
     kb[t] = bf4(row < L ? ldq(base + (int64_t)row * ld + d + 4 * q) : z);
     *reinterpret_cast<f4*>(&Vs[row][4 * q]) = row < L ? ldq(base + (int64_t)row * ld + 2 * d + 4 * q) : z;
   }
-  bool kok[NT][4];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int j = t * 16 + 4 * q + e;
-      kok[t][e] = j < L && key_pad[(int64_t)b * L + j] == 0;
-    }
+  const uint32_t kbits = key_bits<NT>(key_pad, b, L, lane, q);
   DropKey dk;
   if (DROP) dk = make_key(key, site, pdrop);
+  const bool leven = (L & 1) == 0;
   const float scale2 = scale * kLog2e;
   __builtin_amdgcn_wave_barrier();            // Vs written by this wave only
   col_frags<NT, kRowP>(&Vs[0][0], r, q, vb);  // B of P V: V[16 tk + 4q + j][c = r]
+  __builtin_amdgcn_wave_barrier();
+  float* T = &Vs[0][0];  // V is in registers now: the image is free for the output transpose
 #pragma unroll
   for (int tq = 0; tq < NT; ++tq) {
     f4 sv[NT];
@@ -538,7 +577,7 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
     for (int tk = 0; tk < NT; ++tk)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        if (kok[tk][e]) m = fmaxf(m, sv[tk][e] * scale2);
+        if ((kbits >> (4 * tk + e)) & 1u) m = fmaxf(m, sv[tk][e] * scale2);
     m = xmax(m);
     float l = 0.f;
     const int i = tq * 16 + r;
@@ -546,10 +585,10 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk) {
       float mk[4] = {1.f, 1.f, 1.f, 1.f};
-      if (DROP) keep4_32(dk, rowbase + tk * 16 + 4 * q, mk);
+      if (DROP) attn_keep4(dk, leven, rowbase + tk * 16 + 4 * q, mk);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float pv = kok[tk][e] ? exp2f(sv[tk][e] * scale2 - m) : 0.f;
+        const float pv = ((kbits >> (4 * tk + e)) & 1u) ? __builtin_amdgcn_exp2f(sv[tk][e] * scale2 - m) : 0.f;
         l += pv;
         sv[tk][e] = DROP ? pv * mk[e] : pv;
       }
@@ -558,13 +597,14 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
     f4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk) o = mfma16(bf4(sv[tk]), vb[tk], o);
-    if (q == 0 && i < L) lse[(int64_t)bh * L + i] = (m + log2f(l)) * kLn2;
+    if (q == 0 && i < L) lse[(int64_t)bh * L + i] = (m + __builtin_amdgcn_logf(l)) * kLn2;
+    // rows 4q + e of the tile need the 1/l of query 4q + e (lane 4q + e)
+    f4 on;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float le = __shfl(l, 4 * q + e, 64);
-      const int row = tq * 16 + 4 * q + e;
-      if (row < L) out[((int64_t)b * L + row) * d + h * 16 + r] = o[e] * (1.f / le);
-    }
+    for (int e = 0; e < 4; ++e) on[e] = o[e] * __builtin_amdgcn_rcpf(__shfl(l, 4 * q + e, 64));
+    const f4 v = tile_rows<kRowP>(T, on, r, q, lane);
+    const int row = tq * 16 + (lane >> 2);
+    if (row < L) st4q(out + ((int64_t)b * L + row) * d + h * 16 + 4 * (lane & 3), v);
   }
 }
 
@@ -579,7 +619,7 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
   // are 2-way, which costs nothing for ds_write_b32 (MI355X_MICROARCH.md §LDS)
   constexpr int TP = 24;
   // one 6 KB image per wave: Q, K and dO pass through it once (column fragments), then it is the
-  // transpose buffer of P∘Z and dS
+  // transpose buffer of P∘Z, dS and the output tiles
   __shared__ __attribute__((aligned(16))) float Xsm[4][LP * TP];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
@@ -590,53 +630,46 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
   typedef typename std::conditional<QB, __bf16, float>::type QT;
   const QT* base = reinterpret_cast<const QT*>(qkv_) + (int64_t)b * L * ld + h * 16;
   const float* gbase = dout + (int64_t)b * L * d + h * 16;
-  const float* obase = out + (int64_t)b * L * d + h * 16;
   float* T = Xsm[wave];
-  f4 qf[NT], kf[NT], gf[NT];
   s4v qb[NT], kb[NT], vb[NT], gb[NT];
-  float Di[NT], lsei[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int row = t * 16 + r;
-    const f4 z = {0.f, 0.f, 0.f, 0.f};
-    const bool ok = row < L;
-    qf[t] = ok ? ldq(base + (int64_t)row * ld + 4 * q) : z;
-    kf[t] = ok ? ldq(base + (int64_t)row * ld + d + 4 * q) : z;
-    vb[t] = bf4(ok ? ldq(base + (int64_t)row * ld + 2 * d + 4 * q) : z);
-    gf[t] = ok ? ld4(gbase + (int64_t)row * d + 4 * q) : z;
-    const f4 of = ok ? ld4(obase + (int64_t)row * d + 4 * q) : z;
-    Di[t] = xsum(gf[t][0] * of[0] + gf[t][1] * of[1] + gf[t][2] * of[2] + gf[t][3] * of[3]);
-    lsei[t] = ok ? lse[(int64_t)bh * L + row] * kLog2e : 0.f;
-  }
+  float lsei[NT];
   // column fragments (B operands of dQ = dS K, dK = dS^T Q, dV = PZ^T dO) via the LDS image
   s4v qc[NT], kc[NT], gc[NT];
+  {
+    f4 qf[NT], kf[NT], gf[NT];
 #pragma unroll
-  for (int pass = 0; pass < 3; ++pass) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-      *reinterpret_cast<f4*>(&T[(t * 16 + r) * TP + 4 * q]) = pass == 0 ? qf[t] : (pass == 1 ? kf[t] : gf[t]);
-    __builtin_amdgcn_wave_barrier();
-    if (pass == 0) col_frags<NT, TP>(T, r, q, qc);
-    else if (pass == 1) col_frags<NT, TP>(T, r, q, kc);
-    else col_frags<NT, TP>(T, r, q, gc);
-    __builtin_amdgcn_wave_barrier();
-  }
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    qb[t] = bf4(qf[t]);
-    kb[t] = bf4(kf[t]);
-    gb[t] = bf4(gf[t]);
-  }
-  bool kok[NT][4];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int j = t * 16 + 4 * q + e;
-      kok[t][e] = j < L && key_pad[(int64_t)b * L + j] == 0;
+    for (int t = 0; t < NT; ++t) {
+      const int row = t * 16 + r;
+      const f4 z = {0.f, 0.f, 0.f, 0.f};
+      const bool ok = row < L;
+      qf[t] = ok ? ldq(base + (int64_t)row * ld + 4 * q) : z;
+      kf[t] = ok ? ldq(base + (int64_t)row * ld + d + 4 * q) : z;
+      vb[t] = bf4(ok ? ldq(base + (int64_t)row * ld + 2 * d + 4 * q) : z);
+      gf[t] = ok ? ld4(gbase + (int64_t)row * d + 4 * q) : z;
+      lsei[t] = ok ? lse[(int64_t)bh * L + row] * kLog2e : 0.f;
     }
+#pragma unroll
+    for (int pass = 0; pass < 3; ++pass) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        *reinterpret_cast<f4*>(&T[(t * 16 + r) * TP + 4 * q]) = pass == 0 ? qf[t] : (pass == 1 ? kf[t] : gf[t]);
+      __builtin_amdgcn_wave_barrier();
+      if (pass == 0) col_frags<NT, TP>(T, r, q, qc);
+      else if (pass == 1) col_frags<NT, TP>(T, r, q, kc);
+      else col_frags<NT, TP>(T, r, q, gc);
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      qb[t] = bf4(qf[t]);
+      kb[t] = bf4(kf[t]);
+      gb[t] = bf4(gf[t]);
+    }
+  }
+  const uint32_t kbits = key_bits<NT>(key_pad, b, L, lane, q);
   DropKey dk;
   if (DROP) dk = make_key(key, site, pdrop);
+  const bool leven = (L & 1) == 0;
   const float scale2 = scale * kLog2e;
   QT* dbase = reinterpret_cast<QT*>(dqkv_) + (int64_t)b * L * ld + h * 16;
   f4 dv_acc[NT], dk_acc[NT];
@@ -646,35 +679,47 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
   for (int tq = 0; tq < NT; ++tq) {
     const int i = tq * 16 + r;
     const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
-    f4 ps[NT], ds[NT];
+    f4 pvs[NT], ds[NT];  // ds holds z * dP^T until D is known
+    uint32_t zb = 0;      // kept-element bits (dropout), bit 4 tk + e
+    float Dp = 0.f;
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk) {
       const f4 sacc = mfma16(kb[tk], qb[tq], f4{0.f, 0.f, 0.f, 0.f});  // S^T[key][query]
       const f4 pacc = mfma16(vb[tk], gb[tq], f4{0.f, 0.f, 0.f, 0.f});  // dP^T = V dO^T
       float mk[4] = {1.f, 1.f, 1.f, 1.f};
-      if (DROP) keep4_32(dk, rowbase + tk * 16 + 4 * q, mk);
+      if (DROP) attn_keep4(dk, leven, rowbase + tk * 16 + 4 * q, mk);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float pv = (kok[tk][e] && i < L) ? exp2f(sacc[e] * scale2 - lsei[tq]) : 0.f;
-        const float z = DROP ? mk[e] : 1.f;
-        ds[tk][e] = pv * (z * pacc[e] - Di[tq]);
-        ps[tk][e] = pv * z;
+        const float pv = (((kbits >> (4 * tk + e)) & 1u) && i < L)
+                             ? __builtin_amdgcn_exp2f(sacc[e] * scale2 - lsei[tq]) : 0.f;
+        pvs[tk][e] = pv;
+        ds[tk][e] = DROP ? mk[e] * pacc[e] : pacc[e];
+        if (DROP) zb |= (mk[e] != 0.f ? 1u : 0u) << (4 * tk + e);
+        Dp += pv * ds[tk][e];
       }
     }
+    // D_i = sum_j P_ij dP_ij (= dO_i . O_i): from the register tiles, no O read
+    const float Di = xsum(Dp);
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ds[tk][e] = pvs[tk][e] * (ds[tk][e] - Di);
     f4 dq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk) dq = mfma16(bf4(ds[tk]), kc[tk], dq);  // dS[query][key] K
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = tq * 16 + 4 * q + e;
-      if (row < L) stq(dbase + (int64_t)row * ld + r, dq[e] * scale);
+    {
+      const f4 v = tile_rows<TP>(T, dq * scale, r, q, lane);
+      const int row = tq * 16 + (lane >> 2);
+      if (row < L) st4q(dbase + (int64_t)row * ld + 4 * (lane & 3), v);
     }
     // dV[key][c] += PZ^T dO and dK[key][c] += dS^T Q: A = [key = lane & 15][query], i.e. the
     // transpose of this lane's tiles, through T (T[key][query])
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) T[(tk * 16 + 4 * q + e) * TP + r] = ps[tk][e];
+      for (int e = 0; e < 4; ++e)  // P∘Z (kept: P * 1/(1-p), the forward's product)
+        T[(tk * 16 + 4 * q + e) * TP + r] =
+            DROP ? (((zb >> (4 * tk + e)) & 1u) ? pvs[tk][e] * dk.scale : 0.f) : pvs[tk][e];
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk)
@@ -690,16 +735,17 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(
       dk_acc[tk] = mfma16(bf4(ld4(&T[(tk * 16 + r) * TP + 4 * q])), qc[tq], dk_acc[tk]);
     __builtin_amdgcn_wave_barrier();
   }
+  // dK / dV rows: acc[e] = X[key 16 tk + 4 q + e][c = r]
 #pragma unroll
-  for (int tk = 0; tk < NT; ++tk)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = tk * 16 + 4 * q + e;
-      if (row < L) {
-        stq(dbase + (int64_t)row * ld + d + r, dk_acc[tk][e] * scale);
-        stq(dbase + (int64_t)row * ld + 2 * d + r, dv_acc[tk][e]);
-      }
+  for (int tk = 0; tk < NT; ++tk) {
+    const f4 vk = tile_rows<TP>(T, dk_acc[tk] * scale, r, q, lane);
+    const f4 vv = tile_rows<TP>(T, dv_acc[tk], r, q, lane);
+    const int row = tk * 16 + (lane >> 2);
+    if (row < L) {
+      st4q(dbase + (int64_t)row * ld + d + 4 * (lane & 3), vk);
+      st4q(dbase + (int64_t)row * ld + 2 * d + 4 * (lane & 3), vv);
     }
+  }
 }
 
 int threads_for(int L) {

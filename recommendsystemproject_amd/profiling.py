@@ -33,9 +33,10 @@ def _attn_bwd_work(a):
     B, L, d, H = a[6], a[7], a[8], a[9]
     hd = d // H
     eq = 2.0 if a[14] & _hip.RS_ATTN_QKV_BF16 else 4.0
-    # pass 1 (lane/query): s, dp, dq; pass 2 (lane/key): s, dp, dk, dv; qkv read, dqkv written,
-    # out and dout read, lse read
-    return 2.0 * B * H * L * L * hd * 7, eq * B * L * 3 * d * 2 + 4.0 * (2 * B * L * d + B * H * L)
+    # s, dp, dq, dk, dv; qkv read, dqkv written, dout and lse read; the bf16 path forms
+    # D = rowsum(P dP) from its own tiles, the others read out (D = dO . O)
+    bf = a[14] & _hip.RS_GEMM_BF16 and hd == 16 and L <= 64
+    return 2.0 * B * H * L * L * hd * 5, eq * B * L * 3 * d * 2 + 4.0 * ((1 if bf else 2) * B * L * d + B * H * L)
 
 
 def _gather_work(a, bwd=False):
