@@ -191,6 +191,20 @@ int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float* out, cons
                 const float* lse, float* dqkv, int B, int L, int d, int H, float scale, float p,
                 const int64_t* key, int site, int flags, void* stream);
 
+/* Attention for ONE query row per sample, i_b = last[b] (the final encoder layer: the encoder
+ * returns context[b, last[b]] only, SequenceEncoder.py:58-74 (T7), so the final layer's other
+ * query rows are dead). Keys / values: all L rows of qkv [B*L, 3d] under key_pad. out [B, d],
+ * lse [B*H]. rs_attn_rows_bwd: dout [B, d] -> dqkv [B*L, 3d], every element written (dQ is zero
+ * off the selected rows; dK / dV dense). Dropout draws are rs_attn_fwd's for (b, h, i_b, j).
+ * flags as rs_attn_fwd (RS_GEMM_BF16: bf16-rounded operands; RS_ATTN_QKV_BF16: bf16 qkv/dqkv).
+ * L <= 256, head_dim 8/16/32/64. */
+int rs_attn_rows_fwd(const float* qkv, const uint8_t* key_pad, const int64_t* last, float* out,
+                     float* lse, int B, int L, int d, int H, float scale, float p,
+                     const int64_t* key, int site, int flags, void* stream);
+int rs_attn_rows_bwd(const float* qkv, const uint8_t* key_pad, const int64_t* last,
+                     const float* dout, const float* lse, float* dqkv, int B, int L, int d, int H,
+                     float scale, float p, const int64_t* key, int site, int flags, void* stream);
+
 /* ---------------------------------------------------------------- layer norm (post-LN)
  * h = dropout(a) + b (written back into a), y = LN(h)*gamma + beta; mean/rstd [M] saved.
  * Replaces norm1/norm2(x + dropout1/2(sublayer)) of TransformerEncoderLayer (K8). */

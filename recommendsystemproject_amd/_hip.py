@@ -56,6 +56,8 @@ SIGNATURES = {
     'rs_seq_mask': (i32, [vp, i64, i32, i32, i64, vp, vp, vp]),
     'rs_attn_fwd': (i32, [vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, vp]),
     'rs_attn_bwd': (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, vp]),
+    'rs_attn_rows_fwd': (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, vp]),
+    'rs_attn_rows_bwd': (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, vp]),
     'rs_add_layernorm_fwd': (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, vp, i32, vp]),
     'rs_layernorm_ws_bytes': (i64, [i32, i32]),
     'rs_layernorm_bwd': (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, f32, vp, i32, vp, vp]),

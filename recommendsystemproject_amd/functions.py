@@ -129,6 +129,22 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key):
 
 
 # ================================================================================ encoder layer
+def _ffn_fwd(lyr, x1, p, key, site):
+    """x2 = norm2(x1 + dropout2(linear2(dropout(relu(linear1(x1)))))) on any row count."""
+    if ops.ffn_supported(x1, lyr.linear1.weight):
+        # bf16 mode: the whole feed-forward block in one kernel; f1 stays on chip (csrc/ffn.hip)
+        h2, x2, m2, r2, fmask = ops.ffn_fwd_bf16(x1, lyr.linear1.weight, lyr.linear1.bias,
+                                                 lyr.linear2.weight, lyr.linear2.bias, lyr.norm2.weight,
+                                                 lyr.norm2.bias, lyr.norm2.eps, p, key, site + 2, site + 3)
+        return x2, (('ffn', fmask), h2, m2, r2)
+    f1 = ops.linear_fwd(x1, lyr.linear1.weight, lyr.linear1.bias, relu=True, drop_p=p, drop_key=key,
+                        site_a=site + 2)  # dropout(relu(.)) fused
+    h2, x2, m2, r2 = ops.linear_add_layernorm(f1, lyr.linear2.weight, lyr.linear2.bias, x1,
+                                              lyr.norm2.weight, lyr.norm2.bias, lyr.norm2.eps, p, key,
+                                              site + 3)  # h2 = x1 + dropout2(ff), x2 = norm2(h2)
+    return x2, (f1, h2, m2, r2)
+
+
 def layer_fwd(lyr, x, key_pad, B, L, d, H, p, key, site):
     """nn.TransformerEncoderLayer (norm_first=False, relu) forward on x [B*L, d]."""
     sa_mod = lyr.self_attn
@@ -140,22 +156,38 @@ def layer_fwd(lyr, x, key_pad, B, L, d, H, p, key, site):
     h1, x1, m1, r1 = ops.linear_add_layernorm(att, sa_mod.out_proj.weight, sa_mod.out_proj.bias, x,
                                               lyr.norm1.weight, lyr.norm1.bias, lyr.norm1.eps, p, key,
                                               site + 1)
-    if ops.ffn_supported(x1, lyr.linear1.weight):
-        # bf16 mode: the whole feed-forward block in one kernel; f1 stays on chip (csrc/ffn.hip)
-        h2, x2, m2, r2, fmask = ops.ffn_fwd_bf16(x1, lyr.linear1.weight, lyr.linear1.bias,
-                                                 lyr.linear2.weight, lyr.linear2.bias, lyr.norm2.weight,
-                                                 lyr.norm2.bias, lyr.norm2.eps, p, key, site + 2, site + 3)
-        return x2, (x, qkv, att, lse, h1, x1, m1, r1, ('ffn', fmask), h2, m2, r2)
-    f1 = ops.linear_fwd(x1, lyr.linear1.weight, lyr.linear1.bias, relu=True, drop_p=p, drop_key=key,
-                        site_a=site + 2)  # dropout(relu(.)) fused
-    h2, x2, m2, r2 = ops.linear_add_layernorm(f1, lyr.linear2.weight, lyr.linear2.bias, x1,
-                                              lyr.norm2.weight, lyr.norm2.bias, lyr.norm2.eps, p, key,
-                                              site + 3)  # h2 = x1 + dropout2(ff), x2 = norm2(h2)
-    return x2, (x, qkv, att, lse, h1, x1, m1, r1, f1, h2, m2, r2)
+    x2, ff = _ffn_fwd(lyr, x1, p, key, site)
+    return x2, (x, qkv, att, lse, h1, x1, m1, r1) + ff
 
 
-def layer_bwd(lyr, saved, dx2, key_pad, B, L, d, H, p, key, site):
-    """Backward of layer_fwd. dx2 is consumed; returns dx [B*L, d]."""
+def prune_last_layer() -> bool:
+    """The final encoder layer runs its post-attention half on the B selected rows only (T7):
+    SequenceEncoder returns context[b, last[b]] (SequenceEncoder.py:58-74), so every other row of
+    that layer is dead: same loss, same gradients. RSYS_FULL_LAST_LAYER=1 computes all rows."""
+    return not os.environ.get('RSYS_FULL_LAST_LAYER')
+
+
+def layer_fwd_last(lyr, x, key_pad, last, B, L, d, H, p, key, site):
+    """The final encoder layer for the selected rows last[b] only -> x2 [B, d] (= the encoder
+    output): qkv for all rows (every key / value is live), attention of the B selected queries,
+    then out-proj + LN1 + FFN + LN2 on B rows."""
+    sa_mod = lyr.self_attn
+    qkv = ops.linear_fwd(x, sa_mod.in_proj_weight, sa_mod.in_proj_bias,
+                         out_dtype=torch.bfloat16 if ops.qkv_bf16_ok(L, d, H) else torch.float32)
+    att, lse = ops.attn_rows_fwd(qkv, key_pad, last, B, L, d, H, p, key, site)
+    xs = torch.empty(B, d, device=x.device, dtype=torch.float32)  # residual rows x[b, last[b]]
+    ops.gather_fwd([_seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=last.data_ptr(),
+                         table=x.data_ptr())], B, xs)
+    h1, x1, m1, r1 = ops.linear_add_layernorm(att, sa_mod.out_proj.weight, sa_mod.out_proj.bias, xs,
+                                              lyr.norm1.weight, lyr.norm1.bias, lyr.norm1.eps, p, key,
+                                              site + 1)
+    x2, ff = _ffn_fwd(lyr, x1, p, key, site)
+    return x2, (x, qkv, att, lse, h1, x1, m1, r1) + ff
+
+
+def _post_attn_bwd(lyr, saved, dx2, p, key, site):
+    """Backward of out-proj + LN1 + FFN + LN2 (any row count). Returns (dh1, datt): dh1 the
+    gradient of the layer input through the residual, datt the gradient of the attention output."""
     x, qkv, att, lse, h1, x1, m1, r1, f1, h2, m2, r2 = saved
     g = grad_of
     sa_mod = lyr.self_attn
@@ -184,13 +216,40 @@ def layer_bwd(lyr, saved, dx2, key_pad, B, L, d, H, p, key, site):
     dsa = dh1 if dsa is None else dsa
     ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
     datt = ops.linear_bwd_input(dsa, sa_mod.out_proj.weight)
-    dqkv = ops.attn_bwd(qkv, key_pad, att, datt, lse, B, L, d, H, p, key, site)
+    return dh1, datt
+
+
+def _in_proj_bwd(lyr, x, dqkv, dx=None):
+    """in_proj weight gradient and dx (+)= dqkv W_in."""
+    g = grad_of
+    sa_mod = lyr.self_attn
     if dqkv.dtype == torch.bfloat16:  # bf16 dqkv (RS_ATTN_QKV_BF16): bf16-MFMA weight gradient
         ops.wgrad_bf16(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
     else:
         ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
-    ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight, out=dh1, beta=1.0)  # dx = dh1 + dqkv Win
-    return dh1
+    if dx is None:
+        return ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight)
+    return ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight, out=dx, beta=1.0)  # dx = dh1 + dqkv Win
+
+
+def layer_bwd(lyr, saved, dx2, key_pad, B, L, d, H, p, key, site):
+    """Backward of layer_fwd. dx2 is consumed; returns dx [B*L, d]."""
+    x, qkv, lse = saved[0], saved[1], saved[3]
+    dh1, datt = _post_attn_bwd(lyr, saved, dx2, p, key, site)
+    dqkv = ops.attn_bwd(qkv, key_pad, saved[2], datt, lse, B, L, d, H, p, key, site)
+    return _in_proj_bwd(lyr, x, dqkv, dx=dh1)
+
+
+def layer_bwd_last(lyr, saved, dx2, key_pad, last, B, L, d, H, p, key, site):
+    """Backward of layer_fwd_last: dx2 [B, d] (the encoder output's gradient) -> dx [B*L, d]."""
+    x, qkv, lse = saved[0], saved[1], saved[3]
+    dh1, datt = _post_attn_bwd(lyr, saved, dx2, p, key, site)
+    dqkv = ops.attn_rows_bwd(qkv, key_pad, last, datt, lse, B, L, d, H, p, key, site)
+    dx = _in_proj_bwd(lyr, x, dqkv)
+    # the residual rows x[b, last[b]] got dh1: add it back at those rows
+    ops.gather_bwd([_seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=last.data_ptr(),
+                         grad=dx.data_ptr())], B, dh1)
+    return dx
 
 
 def _layer_site(i):
@@ -221,17 +280,25 @@ class SeqEncoderFn(torch.autograd.Function):
         err = enc.err_flag
         x, in_saved = seq_input_fwd(proc, seqd, B, L, p, key, err)
         layers = list(enc.transformer_backbone.layers)
-        saved = []
-        for i, lyr in enumerate(layers):
-            x, s = layer_fwd(lyr, x, key_pad, B, L, d, H, p, key, _layer_site(i))
-            saved.append(s)
         if enc.transformer_backbone.norm is not None:
             raise NotImplementedError('TransformerEncoder(norm=...) is not used by the reference')
-        out = torch.empty(B, d, device=x.device, dtype=torch.float32)
-        seg = _seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=last.data_ptr(),
-                   table=x.data_ptr())
-        ops.gather_fwd([seg], B, out)
+        prune = prune_last_layer() and len(layers) > 0 and L <= 256
+        saved = []
+        for i, lyr in enumerate(layers):
+            if prune and i == len(layers) - 1:
+                x, s = layer_fwd_last(lyr, x, key_pad, last, B, L, d, H, p, key, _layer_site(i))
+            else:
+                x, s = layer_fwd(lyr, x, key_pad, B, L, d, H, p, key, _layer_site(i))
+            saved.append(s)
+        if prune:
+            out = x  # [B, d]: the final layer produced the selected rows only
+        else:
+            out = torch.empty(B, d, device=x.device, dtype=torch.float32)
+            seg = _seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=last.data_ptr(),
+                       table=x.data_ptr())
+            ops.gather_fwd([seg], B, out)
         if need:
+            ctx.prune = prune
             ctx.enc, ctx.B, ctx.L, ctx.p = enc, B, L, p
             ctx.key, ctx.key_pad, ctx.last = key, key_pad, last
             ctx.in_saved, ctx.layer_saved, ctx.layers = in_saved, saved, layers
@@ -244,11 +311,17 @@ class SeqEncoderFn(torch.autograd.Function):
         proc = enc.feature_embedder
         d, H = proc.target_dim, enc.n_head
         dout = dout.contiguous()
-        dx = torch.zeros(B * L, d, device=dout.device, dtype=torch.float32)
-        seg = _seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=ctx.last.data_ptr(),
-                   grad=dx.data_ptr())
-        ops.gather_bwd([seg], B, dout)
-        for i in reversed(range(len(ctx.layers))):
+        n = len(ctx.layers)
+        if ctx.prune:
+            dx = layer_bwd_last(ctx.layers[n - 1], ctx.layer_saved[n - 1], dout.clone(), ctx.key_pad,
+                                ctx.last, B, L, d, H, p, key, _layer_site(n - 1))
+            n -= 1
+        else:
+            dx = torch.zeros(B * L, d, device=dout.device, dtype=torch.float32)
+            seg = _seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=ctx.last.data_ptr(),
+                       grad=dx.data_ptr())
+            ops.gather_bwd([seg], B, dout)
+        for i in reversed(range(n)):
             dx = layer_bwd(ctx.layers[i], ctx.layer_saved[i], dx, ctx.key_pad, B, L, d, H, p, key,
                            _layer_site(i))
         seq_input_bwd(proc, ctx.in_saved, dx, B, L, p, key)

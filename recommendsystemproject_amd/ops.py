@@ -196,6 +196,23 @@ def attn_bwd(qkv, key_pad, out, dout, lse, B, L, d, H, p=0.0, key=None, site=0):
     return dqkv
 
 
+def attn_rows_fwd(qkv, key_pad, last, B, L, d, H, p=0.0, key=None, site=0):
+    """Attention of the selected query row last[b] of each sample -> out [B, d], lse [B*H]."""
+    out = torch.empty(B, d, device=qkv.device, dtype=torch.float32)
+    lse = torch.empty(B * H, device=qkv.device, dtype=torch.float32)
+    call('rs_attn_rows_fwd', P(qkv), P(key_pad), P(last), P(out), P(lse), B, L, d, H,
+         float((d // H) ** -0.5), float(p), P(key), site, _attn_flags(qkv), stream())
+    return out, lse
+
+
+def attn_rows_bwd(qkv, key_pad, last, dout, lse, B, L, d, H, p=0.0, key=None, site=0):
+    """-> dqkv [B*L, 3d] (qkv's dtype), dQ zero off the selected rows."""
+    dqkv = torch.empty(B * L, 3 * d, device=qkv.device, dtype=qkv.dtype)
+    call('rs_attn_rows_bwd', P(qkv), P(key_pad), P(last), P(dout), P(lse), P(dqkv), B, L, d, H,
+         float((d // H) ** -0.5), float(p), P(key), site, _attn_flags(qkv), stream())
+    return dqkv
+
+
 def linear_add_layernorm(x, W, bias, resid, gamma, beta, eps=1e-5, p=0.0, key=None, site=0):
     """h = dropout(x W^T + bias) + resid, y = LayerNorm(h): one fused kernel at the encoder
     width. Returns h (kept for the backward), y, mean, rstd."""

@@ -222,6 +222,9 @@ def test_bf16_step_fused_ffn_vs_unfused(monkeypatch):
     state = synth.make_state(shapes, seed=3)
     b = synth.batch_to_torch(synth.make_batch(cfg, 1024, seed=7), DEV)
     res = {}
+    # the full final layer: both FFN paths then run at B*L rows, where each has its bf16 instance
+    # (the pruned layer's B-row unfused FFN would run on the fp32 kernels)
+    monkeypatch.setenv('RSYS_FULL_LAST_LAYER', '1')
     precision.set_compute_dtype('bf16')
     try:
         for mode in ('fused', 'unfused'):
