@@ -22,7 +22,7 @@ constexpr int kMaxSeg = 24;  // segments travel by value in the kernel arguments
 // would otherwise serialise on a few hundred addresses
 constexpr int64_t kSmallTableBytes = 48 * 1024;
 
-constexpr int kBagBatch = 8;               // bag ids (and rows) loaded per batch
+constexpr int kBagBatch = 16;              // bag ids (and rows) loaded per batch
 
 struct SegLaunch {
   rs_feature_seg_t segs[kMaxSeg];
@@ -40,6 +40,7 @@ struct SegLaunch {
   int sblock_start[kMaxSeg + 1];
   int sblocks[kMaxSeg];
   int small_lds;        // bytes of dynamic LDS for the small-table kernel
+  int split[kMaxSeg];   // pooled bags: row groups sharing one bag (positions split S ways)
 };
 static_assert(sizeof(SegLaunch) <= 4096, "SegLaunch must fit the kernel-argument segment");
 
@@ -73,6 +74,48 @@ __device__ __forceinline__ void store_row(float* p, const float* v) {
   else p[0] = v[0];
 }
 
+// Pooled bag: the (un-normalised) sum or max of positions [lbeg, lend) of row `row`'s bag.
+template <bool VEC>
+__device__ __forceinline__ void pool_acc(const SegLaunch& a, const rs_feature_seg_t& sg, int row,
+                                         int c, int lbeg, int lend, float* acc) {
+  constexpr int W = VEC ? 4 : 1;
+  const int64_t* ids = sg.idx + (int64_t)row * sg.idx_stride;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = sg.pool_mode == RS_POOL_MAX ? -INFINITY : 0.f;
+  // Straight-line code only (no per-row branch or error atomic inside the batch): a branch
+  // around each load makes the compiler wait for it before issuing the next.
+  const bool is_max = sg.pool_mode == RS_POOL_MAX;
+  bool bad = false;
+  int64_t raw[kBagBatch];
+#pragma unroll
+  for (int u = 0; u < kBagBatch; ++u) raw[u] = lbeg + u < lend ? ids[lbeg + u] : 0;
+  for (int l0 = lbeg; l0 < lend; l0 += kBagBatch) {
+    const int nb = lend - l0 < kBagBatch ? lend - l0 : kBagBatch;
+    bool ok[kBagBatch];
+    float v[kBagBatch][4];
+#pragma unroll
+    for (int u = 0; u < kBagBatch; ++u) {
+      const bool valid = raw[u] >= 0 && raw[u] < sg.vocab;
+      bad |= u < nb && !valid;
+      ok[u] = u < nb && valid;
+      load_row<VEC>(sg.table + (ok[u] ? raw[u] : 0) * sg.dim + c, v[u]);
+    }
+    const int n2 = l0 + kBagBatch;
+#pragma unroll
+    for (int u = 0; u < kBagBatch; ++u) raw[u] = n2 + u < lend ? ids[n2 + u] : 0;
+#pragma unroll
+    for (int u = 0; u < kBagBatch; ++u) {
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const float x = ok[u] ? v[u][j] : 0.f;
+        const float y = is_max ? fmaxf(acc[j], x) : acc[j] + x;
+        acc[j] = u < nb ? y : acc[j];
+      }
+    }
+  }
+  if (bad && a.err) atomicOr(a.err, 1);
+}
+
 template <bool VEC>
 __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int row, int chunk) {
   constexpr int W = VEC ? 4 : 1;
@@ -83,36 +126,7 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
     const int64_t id = sg.idx[(int64_t)row * sg.idx_stride];
     if (id_ok(id, sg.vocab, a.err)) load_row<VEC>(sg.table + id * sg.dim + c, acc);
   } else if (sg.kind == RS_SEG_POOL) {
-    const int64_t* ids = sg.idx + (int64_t)row * sg.idx_stride;
-    if (sg.pool_mode == RS_POOL_MAX) {
-#pragma unroll
-      for (int j = 0; j < W; ++j) acc[j] = -INFINITY;
-    }
-    // kBagBatch ids, then their kBagBatch rows, in flight at once (the row loads depend on the
-    // id loads: a one-at-a-time loop is latency-bound); summation order stays l = 0, 1, ...
-    for (int l0 = 0; l0 < sg.bag; l0 += kBagBatch) {
-      const int nb = sg.bag - l0 < kBagBatch ? sg.bag - l0 : kBagBatch;
-      int64_t id[kBagBatch];
-#pragma unroll
-      for (int u = 0; u < kBagBatch; ++u) id[u] = u < nb ? ids[l0 + u] : 0;
-      float v[kBagBatch][4];
-#pragma unroll
-      for (int u = 0; u < kBagBatch; ++u) {
-        v[u][0] = v[u][1] = v[u][2] = v[u][3] = 0.f;
-        if (u < nb && id_ok(id[u], sg.vocab, a.err)) load_row<VEC>(sg.table + id[u] * sg.dim + c, v[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < kBagBatch; ++u) {
-        if (u >= nb) break;
-        if (sg.pool_mode == RS_POOL_MAX) {
-#pragma unroll
-          for (int j = 0; j < W; ++j) acc[j] = fmaxf(acc[j], v[u][j]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < W; ++j) acc[j] += v[u][j];
-        }
-      }
-    }
+    pool_acc<VEC>(a, sg, row, c, 0, sg.bag, acc);
     if (sg.pool_mode == RS_POOL_MEAN) {
       const float n = (float)sg.bag;
 #pragma unroll
@@ -135,10 +149,48 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
   }
 }
 
+// Pooled bag split over S row groups (small batches: more loads in flight per bag). Row group
+// g = r * S + p sums positions [p * per, (p + 1) * per) of bag r; the S partial sums are added
+// in p order through LDS by group p = 0.
+template <bool VEC>
+__device__ void gather_pool_split(const SegLaunch& a, const rs_feature_seg_t& sg, int s, int lb) {
+  constexpr int W = VEC ? 4 : 1;
+  __shared__ float4 red[256];
+  const int C = a.chunks[s], S = a.split[s];
+  const int grp = threadIdx.x / C, chunk = threadIdx.x % C;
+  const int r = grp / S, p = grp % S;
+  const int row = lb * a.rpb[s] + r;
+  const bool active = r < a.rpb[s] && row < a.rows;
+  const int per = (sg.bag + S - 1) / S;
+  const int lbeg = p * per < sg.bag ? p * per : sg.bag;
+  const int lend = lbeg + per < sg.bag ? lbeg + per : sg.bag;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (active) pool_acc<VEC>(a, sg, row, chunk * W, lbeg, lend, acc);
+  red[threadIdx.x] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  __syncthreads();
+  if (!active || p != 0) return;
+  for (int q = 1; q < S; ++q) {
+    const float4 t = red[threadIdx.x + q * C];
+    acc[0] += t.x; acc[1] += t.y; acc[2] += t.z; acc[3] += t.w;
+  }
+  if (sg.pool_mode == RS_POOL_MEAN) {
+    const float n = (float)sg.bag;
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc[j] = acc[j] / n;
+  }
+  float* o = a.out + (int64_t)row * a.ldo + sg.out_col + chunk * W;
+  store_row<VEC>(o, acc);
+}
+
 __global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
   const int s = find_seg(a, blockIdx.x);
   const rs_feature_seg_t& sg = a.segs[s];
   const int lb = blockIdx.x - a.block_start[s];
+  if (a.split[s] > 1) {  // uniform per workgroup: the barrier inside is reached by every thread
+    if (a.vec[s]) gather_pool_split<true>(a, sg, s, lb);
+    else gather_pool_split<false>(a, sg, s, lb);
+    return;
+  }
   const int C = a.chunks[s];
   const int r = threadIdx.x / C, chunk = threadIdx.x % C;
   if (r >= a.rpb[s]) return;
@@ -149,9 +201,10 @@ __global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
 }
 
 // LDS_ACC: accumulate into the workgroup-private LDS copy `lds` of the table gradient
+// [lbeg, lend): the bag positions this lane scatters (a split bag, see gather_pool_split)
 template <bool VEC, bool LDS_ACC = false>
 __device__ void scatter_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int row, int chunk,
-                            float* lds = nullptr) {
+                            float* lds = nullptr, int lbeg = 0, int lend = -1) {
   constexpr int W = VEC ? 4 : 1;
   const int c = chunk * W;
   float g[4] = {0.f, 0.f, 0.f, 0.f};
@@ -193,24 +246,39 @@ __device__ void scatter_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int 
 #pragma unroll
       for (int j = 0; j < W; ++j) g[j] = g[j] / n;
     }
-    for (int l0 = 0; l0 < sg.bag; l0 += kBagBatch) {
-      const int nb = sg.bag - l0 < kBagBatch ? sg.bag - l0 : kBagBatch;
+    // per batch: the touch counts of this batch's rows are loaded together with the next
+    // batch's ids, so each batch costs one dependent round trip before its stores/atomics
+    if (lend < 0) lend = sg.bag;
+    int64_t raw[kBagBatch];
+#pragma unroll
+    for (int u = 0; u < kBagBatch; ++u) raw[u] = lbeg + u < lend ? ids[lbeg + u] : 0;
+    for (int l0 = lbeg; l0 < lend; l0 += kBagBatch) {
+      const int nb = lend - l0 < kBagBatch ? lend - l0 : kBagBatch;
       int64_t id[kBagBatch];
       bool use[kBagBatch];
 #pragma unroll
       for (int u = 0; u < kBagBatch; ++u) {
-        id[u] = u < nb ? ids[l0 + u] : 0;
+        id[u] = raw[u];
         use[u] = u < nb && id[u] != sg.pad_idx && id[u] >= 0 && id[u] < sg.vocab;
       }
-      int once[kBagBatch];
+      // the touch counts are folded into one bit mask before the first store: otherwise the
+      // compiler sinks each load into its branch and waits for them one at a time
+      unsigned once = 0;
+      if (!LDS_ACC && sg.touch_count) {
+        int t[kBagBatch];
 #pragma unroll
-      for (int u = 0; u < kBagBatch; ++u)
-        once[u] = (!LDS_ACC && sg.touch_count && use[u]) ? sg.touch_count[id[u]] == 1 : 0;
+        for (int u = 0; u < kBagBatch; ++u) t[u] = sg.touch_count[use[u] ? id[u] : 0];
+#pragma unroll
+        for (int u = 0; u < kBagBatch; ++u) once |= (unsigned)(t[u] == 1) << u;
+      }
+      const int n2 = l0 + kBagBatch;
+#pragma unroll
+      for (int u = 0; u < kBagBatch; ++u) raw[u] = n2 + u < lend ? ids[n2 + u] : 0;
 #pragma unroll
       for (int u = 0; u < kBagBatch; ++u) {
         if (!use[u]) continue;
         float* d = (LDS_ACC ? lds : sg.grad) + id[u] * sg.dim + c;
-        if (once[u]) {
+        if ((once >> u) & 1u) {
           store_row<VEC>(d, g);
         } else {
 #pragma unroll
@@ -235,13 +303,20 @@ __global__ __launch_bounds__(256) void gather_bwd_kernel(SegLaunch a) {
   const rs_feature_seg_t& sg = a.segs[s];
   if (sg.kind == RS_SEG_DENSE || a.small[s]) return;
   const int lb = blockIdx.x - a.block_start[s];
-  const int C = a.chunks[s];
-  const int r = threadIdx.x / C, chunk = threadIdx.x % C;
+  const int C = a.chunks[s], S = a.split[s];
+  const int grp = threadIdx.x / C, chunk = threadIdx.x % C;
+  const int r = grp / S, p = grp % S;
   if (r >= a.rpb[s]) return;
   const int row = lb * a.rpb[s] + r;
   if (row >= a.rows) return;
-  if (a.vec[s]) scatter_seg<true>(a, sg, row, chunk);
-  else scatter_seg<false>(a, sg, row, chunk);
+  int lbeg = 0, lend = -1;
+  if (S > 1) {
+    const int per = (sg.bag + S - 1) / S;
+    lbeg = p * per < sg.bag ? p * per : sg.bag;
+    lend = lbeg + per < sg.bag ? lbeg + per : sg.bag;
+  }
+  if (a.vec[s]) scatter_seg<true>(a, sg, row, chunk, nullptr, lbeg, lend);
+  else scatter_seg<false>(a, sg, row, chunk, nullptr, lbeg, lend);
 }
 
 __global__ __launch_bounds__(256) void gather_bwd_small_kernel(SegLaunch a) {
@@ -331,9 +406,18 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     RS_CHECK_ARG(C <= 256, "gather: seg %d too wide", s);
     a.vec[s] = vec;
     a.chunks[s] = C;
-    a.rpb[s] = 256 / C;
     const bool table_kind = g.kind == RS_SEG_SPARSE || g.kind == RS_SEG_POOL;
     a.small[s] = bwd && table_kind && g.vocab * g.dim * 4 <= kSmallTableBytes;
+    // Split long sum/mean bags over S row groups while the launch is short of ~8 waves per SIMD
+    // and every group keeps >= 8 positions (C3: B = 4096, L = 50, D = 128 -> S = 4).
+    int S = 1;
+    if (g.kind == RS_SEG_POOL && g.pool_mode != RS_POOL_MAX && !a.small[s]) {
+      while (2 * S * C <= 256 && (g.bag + 2 * S - 1) / (2 * S) >= 8 &&
+             (int64_t)rows * C * S < 8192 * 64)
+        S *= 2;
+    }
+    a.split[s] = S;
+    a.rpb[s] = 256 / (C * S);
     a.block_start[s] = blocks;
     if (!a.small[s]) blocks += cdiv(rows, a.rpb[s]);
   }

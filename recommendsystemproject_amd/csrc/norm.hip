@@ -255,6 +255,8 @@ int ln_blocks(int M) {
 }
 
 // ------------------------------------------------------------------------------ BatchNorm
+constexpr int kBnU = 16; // independent loads in flight per thread in the BatchNorm row loops
+
 int bn_chunks(int Bg) {
   int s = cdiv(Bg, 64);  // 64-row chunks: 16 rows per thread in the partial kernel
   if (s > 512) s = 512;
@@ -283,18 +285,33 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const float* __restrict
   if (c < C) {
     float mu = 0.f, r = 0.f;
     if (MODE == 1) { mu = mean[g * C + c]; r = rstd[g * C + c]; }
-    for (int i = r0 + rl; i < r1; i += 4) {
-      const int64_t o = ((int64_t)g * Bg + i) * C + c;
-      const float xv = x[o];
-      if (MODE == 0) {
-        sa += (double)xv;
-        sb += (double)xv * (double)xv;
-      } else {
-        float d = dy[o];
-        if (relu) d = y[o] > 0.f ? d * drop_scale : 0.f;
-        const float xh = (xv - mu) * r;
-        sa += (double)d;
-        sb += (double)d * (double)xh;
+    // kBnU rows per thread loaded before any is summed (rows past the chunk re-read its last
+    // row and are masked); the summation order is unchanged: i, i + 4, i + 8, ...
+    for (int i0 = r0 + rl; i0 < r1; i0 += 4 * kBnU) {
+      float xv[kBnU], dv[kBnU], yv[kBnU];
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        const int i = min(i0 + 4 * u, r1 - 1);
+        const int64_t o = ((int64_t)g * Bg + i) * C + c;
+        xv[u] = x[o];
+        if (MODE == 1) {
+          dv[u] = dy[o];
+          yv[u] = relu ? y[o] : 1.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        if (i0 + 4 * u >= r1) break;
+        if (MODE == 0) {
+          sa += (double)xv[u];
+          sb += (double)xv[u] * (double)xv[u];
+        } else {
+          float d = dv[u];
+          if (relu) d = yv[u] > 0.f ? d * drop_scale : 0.f;
+          const float xh = (xv[u] - mu) * r;
+          sa += (double)d;
+          sb += (double)d * (double)xh;
+        }
       }
     }
   }
@@ -319,10 +336,20 @@ __device__ __forceinline__ void bn_col_sums(const double* __restrict__ ws, int g
   const int cl = threadIdx.x & 63;
   double sa = 0.0, sb = 0.0;
   if (c < C)
-    for (int s = rl; s < S; s += 4) {
-      const int64_t base = ((int64_t)g * S + s) * 2 * C;
-      sa += ws[base + c];
-      sb += ws[base + C + c];
+    for (int s0 = rl; s0 < S; s0 += 4 * kBnU) {
+      double pa[kBnU], pb[kBnU];
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        const int64_t base = ((int64_t)g * S + min(s0 + 4 * u, S - 1)) * 2 * C;
+        pa[u] = ws[base + c];
+        pb[u] = ws[base + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        if (s0 + 4 * u >= S) break;
+        sa += pa[u];
+        sb += pb[u];
+      }
     }
   red[rl][0][cl] = sa;
   red[rl][1][cl] = sb;
@@ -379,12 +406,19 @@ __global__ __launch_bounds__(256) void bn_fwd_norm_kernel(
   DropKey dk{};
   const bool drop = drop_p > 0.f;
   if (drop) dk = make_key(key, site, drop_p);
-  for (int i = s * rpc + rl; i < r1; i += 4) {
-    const int64_t o = ((int64_t)g * Bg + i) * C + c;
-    float v = (x[o] - muf) * r * wc + bc;
-    if (relu) v = fmaxf(v, 0.f);
-    if (drop) v *= keep_mult(dk, (uint64_t)o);  // the block's nn.Dropout (rs_dropout_fwd draw)
-    y[o] = v;
+  for (int i0 = s * rpc + rl; i0 < r1; i0 += 4 * kBnU) {
+    float xv[kBnU];
+#pragma unroll
+    for (int u = 0; u < kBnU; ++u) xv[u] = x[((int64_t)g * Bg + min(i0 + 4 * u, r1 - 1)) * C + c];
+#pragma unroll
+    for (int u = 0; u < kBnU; ++u) {
+      if (i0 + 4 * u >= r1) break;
+      const int64_t o = ((int64_t)g * Bg + i0 + 4 * u) * C + c;
+      float v = (xv[u] - muf) * r * wc + bc;
+      if (relu) v = fmaxf(v, 0.f);
+      if (drop) v *= keep_mult(dk, (uint64_t)o);  // the block's nn.Dropout (rs_dropout_fwd draw)
+      y[o] = v;
+    }
   }
 }
 
@@ -418,12 +452,23 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(
   const float mu = mean[g * C + c], r = rstd[g * C + c], wr = w[c] * r;
   const int rpc = (Bg + S - 1) / S;
   const int r1 = min(Bg, (s + 1) * rpc);
-  for (int i = s * rpc + rl; i < r1; i += 4) {
-    const int64_t o = ((int64_t)g * Bg + i) * C + c;
-    float d = dy[o];
-    if (relu) d = y[o] > 0.f ? d * drop_scale : 0.f;
-    const float xh = (x[o] - mu) * r;
-    dx[o] = wr * (d - mdy - xh * mdyx);
+  for (int i0 = s * rpc + rl; i0 < r1; i0 += 4 * kBnU) {
+    float xv[kBnU], dv[kBnU], yv[kBnU];
+#pragma unroll
+    for (int u = 0; u < kBnU; ++u) {
+      const int64_t o = ((int64_t)g * Bg + min(i0 + 4 * u, r1 - 1)) * C + c;
+      xv[u] = x[o];
+      dv[u] = dy[o];
+      yv[u] = relu ? y[o] : 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kBnU; ++u) {
+      if (i0 + 4 * u >= r1) break;
+      float d = dv[u];
+      if (relu) d = yv[u] > 0.f ? d * drop_scale : 0.f;
+      const float xh = (xv[u] - mu) * r;
+      dx[((int64_t)g * Bg + i0 + 4 * u) * C + c] = wr * (d - mdy - xh * mdyx);
+    }
   }
 }
 

@@ -160,6 +160,42 @@ def test_gather_backward_matches_embedding_backward(V):
     assert (g[0] == 0).all()
 
 
+@pytest.mark.parametrize('B,D,Lb,mode', [(300, 128, 50, 'mean'), (300, 128, 50, 'sum'), (257, 64, 17, 'mean'),
+                                          (4096, 128, 50, 'mean'), (5, 128, 33, 'mean')])
+def test_pooled_split_bags(B, D, Lb, mode):
+    """Long sum/mean bags at small batch are split over several row groups (gather.hip
+    gather_pool_split); forward against torch, backward (with touch counts: a row looked up
+    once is a plain store) against the embedding backward, bad ids flagged."""
+    V = 20000
+    t = rnd(V, D, seed=11).requires_grad_(True)
+    bag = torch.randint(0, V, (B, Lb), device=DEV)
+    bag[:, -1] = 0  # padding slot
+    bag[1, :] = 7  # one row many times in one bag
+    red = (lambda e: e.mean(1)) if mode == 'mean' else (lambda e: e.sum(1))
+    ref = red(F.embedding(bag, t, padding_idx=0))
+    segs = [_seg(kind=_hip.RS_SEG_POOL, dim=D, out_col=0, pool_mode=_hip.RS_POOL[mode], bag=Lb, vocab=V,
+                 idx_stride=Lb, idx=bag.data_ptr(), table=t.data_ptr(), pad_idx=0)]
+    out = torch.empty(B, D, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ops.gather_fwd(segs, B, out, err)
+    assert err.item() == 0
+    # fp32 summation-order tolerance: the split bag adds S partial sums of Lb/S rows
+    assert torch.allclose(out, ref, atol=2e-6 * (Lb if mode == 'sum' else 1), rtol=1e-5)
+    dout = rnd(B, D, seed=12)
+    ref.backward(dout)
+    counts = torch.bincount(bag.flatten(), minlength=V).to(torch.int32)
+    g = torch.zeros(V, D, device=DEV)
+    segs[0].grad = g.data_ptr()
+    segs[0].touch_count = counts.data_ptr()
+    ops.gather_bwd(segs, B, dout)
+    assert torch.allclose(g, t.grad, atol=1e-5, rtol=1e-5)
+    bad = bag.clone()
+    bad[B - 1, Lb // 2] = V + 3
+    segs[0].idx = bad.data_ptr()
+    ops.gather_fwd(segs, B, out, err)
+    assert err.item() == 1
+
+
 def test_seq_mask_quirks():
     seq = torch.tensor([[5, 3, 0, 0], [0, 0, 0, 0], [1, 2, 3, 4], [0, 7, 0, 0]], device=DEV)
     key_pad, last = ops.seq_mask(seq, 0)

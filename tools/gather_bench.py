@@ -49,6 +49,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     table = torch.randn(V, D, device=dev, generator=g)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
+    copy_gbs = 6290.0  # MI355X_MICROARCH.md: measured float4 copy bandwidth
     for kind, bag in (('pooled_mean', L), ('single_id', 1)):
         ids = torch.randint(1, V, (B, bag), device=dev, generator=g)
         out = torch.empty(B, D, device=dev)
@@ -63,7 +64,8 @@ def main():
         byts = lookups * D * 4 + B * D * 4 + lookups * 8
         print(json.dumps({'case': f'gather_fwd {kind}', 'vocab': V, 'dim': D, 'rows': B, 'bag': bag,
                           'MB_per_launch': round(byts / 1e6, 1), 'us': round(ms * 1e3, 1),
-                          'GBps': round(byts / ms / 1e6, 1), 'frac_of_8TBps': round(byts / ms / 1e6 / PEAK, 3)}))
+                          'GBps': round(byts / ms / 1e6, 1), 'frac_of_8TBps': round(byts / ms / 1e6 / PEAK, 3),
+                          'frac_of_copy': round(byts / ms / 1e6 / copy_gbs, 3)}))
         # backward scatter into a table gradient with touch counts (lazy-Adam tables)
         grad = torch.zeros(V, D, device=dev)
         flag = torch.zeros(V, dtype=torch.int32, device=dev)
@@ -78,7 +80,8 @@ def main():
         byts = lookups * D * 4 + B * D * 4 + lookups * (8 + 4)
         print(json.dumps({'case': f'gather_bwd {kind} (touch counts)', 'MB_per_launch': round(byts / 1e6, 1),
                           'us': round(ms * 1e3, 1), 'GBps': round(byts / ms / 1e6, 1),
-                          'frac_of_8TBps': round(byts / ms / 1e6 / PEAK, 3)}))
+                          'frac_of_8TBps': round(byts / ms / 1e6 / PEAK, 3),
+                          'frac_of_copy': round(byts / ms / 1e6 / copy_gbs, 3)}))
         del grad, flag, lst
     assert err.item() == 0
 
