@@ -749,6 +749,270 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(
   }
 }
 
+// ------------------------------------------------------- bf16 MFMA, long histories (64 < L <= 256)
+// C5's encoder (L = 200): the per-wave kernels above hold every tile of one (b, h) in registers,
+// which stops at L = 64. Here one 4-wave workgroup owns one (b, h); K and V (forward) or Q, K, V
+// and dO (backward) sit once in LDS as fp32 [LP][kRowP] images and the waves split the tiles.
+//  forward: wave w takes query tiles w, w + 4, ...; per query tile the same S^T / softmax / P V
+//           sequence as attn_fwd_bf16_kernel (all NT key tiles in registers, 64 key-valid bits).
+//  backward, FlashAttention-2 split with no atomics: phase A (wave w: key tiles w, w + 4, ...)
+//           computes S = Q K^T and dP = dO V^T with the QUERY on the row, so the lane's P∘Z and
+//           dS tiles are directly the A operands of dV = (P∘Z)^T dO and dK = dS^T Q; phase B
+//           (wave w: query tiles w, w + 4, ...) recomputes S^T, dP^T with the KEY on the row, so
+//           dS^T is the A operand of dQ = dS K. D_i = dO_i . O_i comes from the forward output.
+// Dropout draws are the per-element keep_mult32 of index ((b H + h) L + i) L + j, as everywhere.
+template <int NT>
+__device__ __forceinline__ uint64_t key_bits_long(const uint8_t* __restrict__ key_pad, int b,
+                                                  int L, int lane, int q) {
+  uint64_t kb = 0;
+#pragma unroll
+  for (int g = 0; g < (NT + 3) / 4; ++g) {
+    const int j = 64 * g + lane;
+    const uint64_t vm = __ballot(j < L && key_pad[(int64_t)b * L + j] == 0);
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+      if (4 * g + tt < NT) kb |= ((vm >> (16 * tt + 4 * q)) & 0xFull) << (4 * (4 * g + tt));
+  }
+  return kb;
+}
+
+// rows [0, LP) of the head-h slice of matrix `which` (0 = Q, 1 = K, 2 = V) of qkv, zero past L,
+// into an fp32 [LP][kRowP] LDS image; 16-byte loads, 4 threads per 64-byte row slice
+template <int LP>
+__device__ __forceinline__ void load_head_image(const float* __restrict__ base, int ld, int L,
+                                                int off, float (*X)[kRowP]) {
+  for (int e = threadIdx.x; e < LP * 4; e += 256) {
+    const int row = e >> 2, c4 = (e & 3) * 4;
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < L) v = ld4(base + (int64_t)row * ld + off + c4);
+    *reinterpret_cast<f4*>(&X[row][c4]) = v;
+  }
+}
+
+template <int NT, bool DROP>
+__global__ __launch_bounds__(256) void attn_fwd_long_bf16_kernel(
+    const float* __restrict__ qkv, const uint8_t* __restrict__ key_pad, float* __restrict__ out,
+    float* __restrict__ lse, int B, int L, int d, int H, float scale, float pdrop,
+    const int64_t* __restrict__ key, int site) {
+  constexpr int LP = NT * 16;
+  __shared__ __attribute__((aligned(16))) float Ks[LP][kRowP];
+  __shared__ __attribute__((aligned(16))) float Vs[LP][kRowP];
+  __shared__ __attribute__((aligned(16))) float Tsm[4][16 * kRowP];
+  int b, h;
+  if (!map_bh(B, H, b, h)) return;  // uniform over the workgroup
+  const int bh = b * H + h;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int ld = 3 * d;
+  const float* base = qkv + (int64_t)b * L * ld + h * 16;
+  load_head_image<LP>(base, ld, L, d, Ks);
+  load_head_image<LP>(base, ld, L, 2 * d, Vs);
+  const uint64_t kbits = key_bits_long<NT>(key_pad, b, L, lane, q);
+  DropKey dk;
+  if (DROP) dk = make_key(key, site, pdrop);
+  const bool leven = (L & 1) == 0;
+  const float scale2 = scale * kLog2e;
+  __syncthreads();
+  s4v kb[NT], vb[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) kb[t] = bf4(ld4(&Ks[t * 16 + r][4 * q]));
+  col_frags<NT, kRowP>(&Vs[0][0], r, q, vb);
+  float* T = Tsm[wave];
+  for (int tq = wave; tq < NT; tq += 4) {
+    const int i = tq * 16 + r;
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    const s4v qb = bf4(i < L ? ld4(base + (int64_t)i * ld + 4 * q) : z);
+    f4 sv[NT];
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) sv[tk] = mfma16(kb[tk], qb, z);
+    float m = -INFINITY;
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if ((kbits >> (4 * tk + e)) & 1ull) m = fmaxf(m, sv[tk][e] * scale2);
+    m = xmax(m);
+    float l = 0.f;
+    const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) {
+      float mk[4] = {1.f, 1.f, 1.f, 1.f};
+      if (DROP) attn_keep4(dk, leven, rowbase + tk * 16 + 4 * q, mk);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = ((kbits >> (4 * tk + e)) & 1ull) ? __builtin_amdgcn_exp2f(sv[tk][e] * scale2 - m) : 0.f;
+        l += pv;
+        sv[tk][e] = DROP ? pv * mk[e] : pv;
+      }
+    }
+    l = xsum(l);
+    f4 o = z;
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) o = mfma16(bf4(sv[tk]), vb[tk], o);
+    if (q == 0 && i < L) lse[(int64_t)bh * L + i] = (m + __builtin_amdgcn_logf(l)) * kLn2;
+    f4 on;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) on[e] = o[e] * __builtin_amdgcn_rcpf(__shfl(l, 4 * q + e, 64));
+    const f4 v = tile_rows<kRowP>(T, on, r, q, lane);
+    const int row = tq * 16 + (lane >> 2);
+    if (row < L) st4q(out + ((int64_t)b * L + row) * d + h * 16 + 4 * (lane & 3), v);
+  }
+}
+
+template <int NT, bool DROP>
+__global__ __launch_bounds__(256) void attn_bwd_long_bf16_kernel(
+    const float* __restrict__ qkv, const uint8_t* __restrict__ key_pad,
+    const float* __restrict__ out, const float* __restrict__ dout, const float* __restrict__ lse,
+    float* __restrict__ dqkv, int B, int L, int d, int H, float scale, float pdrop,
+    const int64_t* __restrict__ key, int site) {
+  constexpr int LP = NT * 16;
+  constexpr int NW = (NT + 3) / 4;  // tiles per wave
+  constexpr int TP = 24;
+  __shared__ __attribute__((aligned(16))) float Qs[LP][kRowP];
+  __shared__ __attribute__((aligned(16))) float Ks[LP][kRowP];
+  __shared__ __attribute__((aligned(16))) float Vs[LP][kRowP];
+  __shared__ __attribute__((aligned(16))) float Gs[LP][kRowP];
+  __shared__ __attribute__((aligned(16))) float L2s[LP];  // lse * log2(e)
+  __shared__ __attribute__((aligned(16))) float Ds[LP];   // D_i = dO_i . O_i
+  __shared__ float Kv[LP];                                // 1: key j is valid
+  __shared__ __attribute__((aligned(16))) float Tsm[4][16 * TP];
+  int b, h;
+  if (!map_bh(B, H, b, h)) return;  // uniform over the workgroup
+  const int bh = b * H + h;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int ld = 3 * d;
+  const float* base = qkv + (int64_t)b * L * ld + h * 16;
+  load_head_image<LP>(base, ld, L, 0, Qs);
+  load_head_image<LP>(base, ld, L, d, Ks);
+  load_head_image<LP>(base, ld, L, 2 * d, Vs);
+  for (int e = threadIdx.x; e < LP * 4; e += 256) {
+    const int row = e >> 2, c4 = (e & 3) * 4;
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < L) v = ld4(dout + ((int64_t)b * L + row) * d + h * 16 + c4);
+    *reinterpret_cast<f4*>(&Gs[row][c4]) = v;
+  }
+  for (int i = threadIdx.x; i < LP; i += 256) {
+    float Di = 0.f, li = 0.f, kv = 0.f;
+    if (i < L) {
+      const float* o = out + ((int64_t)b * L + i) * d + h * 16;
+      const float* g = dout + ((int64_t)b * L + i) * d + h * 16;
+#pragma unroll
+      for (int c = 0; c < 16; c += 4) {
+        const f4 ov = ld4(o + c), gv = ld4(g + c);
+        Di += ov[0] * gv[0] + ov[1] * gv[1] + ov[2] * gv[2] + ov[3] * gv[3];
+      }
+      li = lse[(int64_t)bh * L + i] * kLog2e;
+      kv = key_pad[(int64_t)b * L + i] == 0 ? 1.f : 0.f;
+    }
+    Ds[i] = Di;
+    L2s[i] = li;
+    Kv[i] = kv;
+  }
+  const uint64_t kbits = key_bits_long<NT>(key_pad, b, L, lane, q);
+  DropKey dk;
+  if (DROP) dk = make_key(key, site, pdrop);
+  const bool leven = (L & 1) == 0;
+  const float scale2 = scale * kLog2e;
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  float* T = Tsm[wave];
+  float* dbase = dqkv + (int64_t)b * L * ld + h * 16;
+  __syncthreads();
+
+  // ---- phase A: dK, dV for key tiles wave, wave + 4, ... (query on the row)
+  {
+    s4v kr[NW], vr[NW];
+    float kval[NW];
+    f4 dk_acc[NW], dv_acc[NW];
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int tk = wave + 4 * u < NT ? wave + 4 * u : NT - 1;
+      kr[u] = bf4(ld4(&Ks[tk * 16 + r][4 * q]));
+      vr[u] = bf4(ld4(&Vs[tk * 16 + r][4 * q]));
+      kval[u] = Kv[tk * 16 + r];
+      dk_acc[u] = dv_acc[u] = z;
+    }
+    for (int tq = 0; tq < NT; ++tq) {
+      const s4v qr = bf4(ld4(&Qs[tq * 16 + r][4 * q]));
+      const s4v gr = bf4(ld4(&Gs[tq * 16 + r][4 * q]));
+      s4v qc[1], gc[1];
+      col_frags<1, kRowP>(&Qs[tq * 16][0], r, q, qc);
+      col_frags<1, kRowP>(&Gs[tq * 16][0], r, q, gc);
+      const f4 l2 = ld4(&L2s[tq * 16 + 4 * q]);
+      const f4 Dq = ld4(&Ds[tq * 16 + 4 * q]);
+#pragma unroll
+      for (int u = 0; u < NW; ++u) {
+        const int tk = wave + 4 * u;
+        if (tk >= NT) break;
+        const f4 sacc = mfma16(qr, kr[u], z);  // S[query 16 tq + 4q + e][key 16 tk + r]
+        const f4 pacc = mfma16(gr, vr[u], z);  // dP[query][key] = dO_i . V_j
+        const uint32_t j = (uint32_t)(tk * 16 + r);
+        f4 pz, ds;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = tq * 16 + 4 * q + e;
+          const float pv = (kval[u] != 0.f && i < L) ? __builtin_amdgcn_exp2f(sacc[e] * scale2 - l2[e]) : 0.f;
+          float mk = 1.f;
+          if (DROP) mk = keep_mult32(dk, ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L + j);
+          pz[e] = pv * mk;
+          ds[e] = pv * (mk * pacc[e] - Dq[e]);
+        }
+        dv_acc[u] = mfma16(bf4(pz), gc[0], dv_acc[u]);  // (P∘Z)^T dO
+        dk_acc[u] = mfma16(bf4(ds), qc[0], dk_acc[u]);  // dS^T Q
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int tk = wave + 4 * u;
+      if (tk >= NT) break;
+      const f4 vk = tile_rows<TP>(T, dk_acc[u] * scale, r, q, lane);
+      const f4 vv = tile_rows<TP>(T, dv_acc[u], r, q, lane);
+      const int row = tk * 16 + (lane >> 2);
+      if (row < L) {
+        st4q(dbase + (int64_t)row * ld + d + 4 * (lane & 3), vk);
+        st4q(dbase + (int64_t)row * ld + 2 * d + 4 * (lane & 3), vv);
+      }
+    }
+  }
+
+  // ---- phase B: dQ for query tiles wave, wave + 4, ... (key on the row)
+  {
+    s4v kb[NT], vb[NT], kc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      kb[t] = bf4(ld4(&Ks[t * 16 + r][4 * q]));
+      vb[t] = bf4(ld4(&Vs[t * 16 + r][4 * q]));
+    }
+    col_frags<NT, kRowP>(&Ks[0][0], r, q, kc);
+    for (int tq = wave; tq < NT; tq += 4) {
+      const int i = tq * 16 + r;
+      const s4v qr = bf4(ld4(&Qs[i][4 * q]));
+      const s4v gr = bf4(ld4(&Gs[i][4 * q]));
+      const float l2 = L2s[i], Di = Ds[i];
+      const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
+      f4 dq = z;
+#pragma unroll
+      for (int tk = 0; tk < NT; ++tk) {
+        const f4 sacc = mfma16(kb[tk], qr, z);  // S^T[key 16 tk + 4q + e][query i]
+        const f4 pacc = mfma16(vb[tk], gr, z);  // dP^T
+        float mk[4] = {1.f, 1.f, 1.f, 1.f};
+        if (DROP) attn_keep4(dk, leven, rowbase + tk * 16 + 4 * q, mk);
+        f4 ds;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float pv = (((kbits >> (4 * tk + e)) & 1ull) && i < L)
+                               ? __builtin_amdgcn_exp2f(sacc[e] * scale2 - l2) : 0.f;
+          ds[e] = pv * ((DROP ? mk[e] : 1.f) * pacc[e] - Di);
+        }
+        dq = mfma16(bf4(ds), kc[tk], dq);  // dS K
+      }
+      const f4 v = tile_rows<TP>(T, dq * scale, r, q, lane);
+      const int row = tq * 16 + (lane >> 2);
+      if (row < L) st4q(dbase + (int64_t)row * ld + 4 * (lane & 3), v);
+    }
+  }
+}
+
 int threads_for(int L) {
   int t = ((L + 63) / 64) * 64;
   return t > 256 ? 256 : t;
@@ -758,6 +1022,12 @@ int threads_for(int L) {
 }  // namespace rs
 
 using namespace rs;
+
+// bf16 compute mode, head_dim 16, 64 < L <= 256, fp32 qkv: the long-history MFMA kernels
+static bool long_bf16_ok(int hd, int L, int B, int H, int flags) {
+  return hd == 16 && L > 64 && L <= 256 && (flags & RS_GEMM_BF16) && !(flags & RS_ATTN_QKV_BF16) &&
+         (int64_t)B * H * L * L < ((int64_t)1 << 32) && !getenv_flag("RSYS_ATTN_VALU");
+}
 
 #define RS_ATTN_DISPATCH(HDV, DROPV, KERNEL, ...)                                         \
   switch (HDV * 2 + (DROPV ? 1 : 0)) {                                                    \
@@ -782,7 +1052,7 @@ extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out,
   RS_CHECK_ARG(hd == 8 || hd == 16 || hd == 32 || hd == 64, "rs_attn_fwd: head_dim %d unsupported", hd);
   if (B == 0) return 0;
   const size_t lds = (size_t)(2 * L * hd + L) * sizeof(float);
-  RS_CHECK_ARG(lds <= 64 * 1024, "rs_attn_fwd: L=%d hd=%d exceeds LDS", L, hd);
+  RS_CHECK_ARG(lds <= 64 * 1024 || long_bf16_ok(hd, L, B, H, flags), "rs_attn_fwd: L=%d hd=%d exceeds LDS", L, hd);
   RS_CHECK_ARG(d % 4 == 0 && aligned16(qkv) && aligned16(out), "rs_attn_fwd: needs 16-byte aligned rows");
   RS_CHECK_ARG(!(flags & RS_ATTN_QKV_BF16) || ((flags & RS_GEMM_BF16) && hd == 16 && L <= 64 &&
                                                  !getenv_flag("RSYS_ATTN_VALU")),
@@ -807,6 +1077,20 @@ extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out,
     RS_CHECK_LAUNCH("rs_attn_fwd mfma");
     return 0;
   }
+  if (long_bf16_ok(hd, L, B, H, flags)) {
+    const dim3 gl(bh_grid(B, H));
+#define RS_AFL(NTV)                                                                                 \
+  if (nt == NTV) {                                                                                  \
+    if (p > 0.f) attn_fwd_long_bf16_kernel<NTV, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    else attn_fwd_long_bf16_kernel<NTV, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+  }
+    const int nt = (L + 15) / 16;
+    RS_AFL(5) RS_AFL(6) RS_AFL(7) RS_AFL(8) RS_AFL(9) RS_AFL(10) RS_AFL(11) RS_AFL(12) RS_AFL(13)
+    RS_AFL(14) RS_AFL(15) RS_AFL(16)
+#undef RS_AFL
+    RS_CHECK_LAUNCH("rs_attn_fwd long bf16");
+    return 0;
+  }
   dim3 grid(bh_grid(B, H));
   int thr = threads_for(L);
   RS_ATTN_DISPATCH(hd, p > 0.f, attn_fwd_kernel, qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site);
@@ -825,7 +1109,7 @@ extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float
   RS_CHECK_ARG(hd == 8 || hd == 16 || hd == 32 || hd == 64, "rs_attn_bwd: head_dim %d unsupported", hd);
   if (B == 0) return 0;
   const size_t lds = (size_t)(4 * L * hd + 3 * L) * sizeof(float);
-  RS_CHECK_ARG(lds <= 64 * 1024, "rs_attn_bwd: L=%d hd=%d exceeds LDS", L, hd);
+  RS_CHECK_ARG(lds <= 64 * 1024 || long_bf16_ok(hd, L, B, H, flags), "rs_attn_bwd: L=%d hd=%d exceeds LDS", L, hd);
   RS_CHECK_ARG(d % 4 == 0 && aligned16(qkv) && aligned16(dout), "rs_attn_bwd: needs 16-byte aligned rows");
   RS_CHECK_ARG(!(flags & RS_ATTN_QKV_BF16) || ((flags & RS_GEMM_BF16) && hd == 16 && L <= 64 &&
                                                  !getenv_flag("RSYS_ATTN_VALU")),
@@ -849,6 +1133,21 @@ extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float
     RS_AB(1) RS_AB(2) RS_AB(3) RS_AB(4)
 #undef RS_AB
     RS_CHECK_LAUNCH("rs_attn_bwd mfma");
+    return 0;
+  }
+  if (long_bf16_ok(hd, L, B, H, flags)) {
+    RS_CHECK_ARG(aligned16(out), "rs_attn_bwd: needs 16-byte aligned rows");
+    const dim3 gl(bh_grid(B, H));
+#define RS_ABL(NTV)                                                                                 \
+  if (nt == NTV) {                                                                                  \
+    if (p > 0.f) attn_bwd_long_bf16_kernel<NTV, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    else attn_bwd_long_bf16_kernel<NTV, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+  }
+    const int nt = (L + 15) / 16;
+    RS_ABL(5) RS_ABL(6) RS_ABL(7) RS_ABL(8) RS_ABL(9) RS_ABL(10) RS_ABL(11) RS_ABL(12) RS_ABL(13)
+    RS_ABL(14) RS_ABL(15) RS_ABL(16)
+#undef RS_ABL
+    RS_CHECK_LAUNCH("rs_attn_bwd long bf16");
     return 0;
   }
   dim3 grid(bh_grid(B, H));

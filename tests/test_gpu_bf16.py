@@ -277,7 +277,9 @@ def _bf16_attention_ref(qkv, key_pad, dout, B, L, d, H):
     return o32, dqkv.float()
 
 
-@pytest.mark.parametrize('B,L', [(3, 50), (5, 16), (4, 33), (2, 64), (3, 1)])
+# L > 64: the long-history kernels (one workgroup per (b, h), FlashAttention-2 backward split)
+@pytest.mark.parametrize('B,L', [(3, 50), (5, 16), (4, 33), (2, 64), (3, 1), (3, 65), (2, 100), (2, 200),
+                                 (2, 256)])
 def test_bf16_attention(B, L, bf16_mode):
     d, H = 64, 4
     qkv = rnd(B * L, 3 * d, seed=11)
@@ -303,10 +305,11 @@ def test_bf16_attention(B, L, bf16_mode):
         assert not torch.equal(out, out32)
 
 
-def test_bf16_attention_dropout_matches_fp32_masks(bf16_mode):
-    """Same dropout masks as the fp32 MFMA kernel (the draw is per element): results agree to
+@pytest.mark.parametrize('L', [50, 120, 201])
+def test_bf16_attention_dropout_matches_fp32_masks(L, bf16_mode):
+    """Same dropout masks as the fp32 kernels (the draw is per element): results agree to
     bf16 precision, and differ clearly from the no-dropout output."""
-    B, L, d, H, p = 6, 50, 64, 4, 0.2
+    B, d, H, p = 6, 64, 4, 0.2
     qkv = rnd(B * L, 3 * d, seed=13)
     key_pad = torch.zeros(B, L, dtype=torch.uint8, device=DEV)
     key = torch.tensor([77, 3], dtype=torch.int64, device=DEV)
