@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, '_lib', 'librsys_hip.so')
+LIB_PATH = os.environ.get('RSYS_LIB_PATH') or os.path.join(_HERE, '_lib', 'librsys_hip.so')
 
 RS_EPI_BIAS, RS_EPI_RELU, RS_EPI_AUX_ADD, RS_EPI_AUX_MASK = 1, 2, 4, 8
 RS_GEMM_BF16 = 256

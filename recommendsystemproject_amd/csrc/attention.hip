@@ -754,7 +754,8 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(
 // which stops at L = 64. Here one 4-wave workgroup owns one (b, h); K and V (forward) or Q, K, V
 // and dO (backward) sit once in LDS as fp32 [LP][kRowP] images and the waves split the tiles.
 //  forward: wave w takes query tiles w, w + 4, ...; per query tile the same S^T / softmax / P V
-//           sequence as attn_fwd_bf16_kernel (all NT key tiles in registers, 64 key-valid bits).
+//           sequence as attn_fwd_bf16_kernel (all NT key tiles in registers, 64 key-valid bits);
+//           Q is staged in LDS with K and V, so the tile loop has no global-memory latency.
 //  backward, FlashAttention-2 split with no atomics: phase A (wave w: key tiles w, w + 4, ...)
 //           computes S = Q K^T and dP = dO V^T with the QUERY on the row, so the lane's P∘Z and
 //           dS tiles are directly the A operands of dV = (P∘Z)^T dO and dK = dS^T Q; phase B
@@ -778,23 +779,56 @@ __device__ __forceinline__ uint64_t key_bits_long(const uint8_t* __restrict__ ke
 
 // rows [0, LP) of the head-h slice of matrix `which` (0 = Q, 1 = K, 2 = V) of qkv, zero past L,
 // into an fp32 [LP][kRowP] LDS image; 16-byte loads, 4 threads per 64-byte row slice
-template <int LP>
-__device__ __forceinline__ void load_head_image(const float* __restrict__ base, int ld, int L,
+template <int LP, typename QT>
+__device__ __forceinline__ void load_head_image(const QT* __restrict__ base, int ld, int L,
                                                 int off, float (*X)[kRowP]) {
   for (int e = threadIdx.x; e < LP * 4; e += 256) {
     const int row = e >> 2, c4 = (e & 3) * 4;
     f4 v = {0.f, 0.f, 0.f, 0.f};
-    if (row < L) v = ld4(base + (int64_t)row * ld + off + c4);
+    if (row < L) v = ldq(base + (int64_t)row * ld + off + c4);
     *reinterpret_cast<f4*>(&X[row][c4]) = v;
   }
 }
 
-template <int NT, bool DROP>
-__global__ __launch_bounds__(256) void attn_fwd_long_bf16_kernel(
-    const float* __restrict__ qkv, const uint8_t* __restrict__ key_pad, float* __restrict__ out,
+// phase-A dropout multipliers of (query rb-row e, key j), e < 4, for the lane holding key j of 4
+// consecutive queries (row bases rb0 + e L): with L even, keys j and j ^ 1 of one query are one
+// hash pair, held by neighbour lanes r and r ^ 1; each lane hashes two of the four pairs and
+// passes the half it does not need across (one hash per two elements, as in the forward)
+__device__ __forceinline__ void keep_col4(const DropKey& dk, bool leven, uint32_t rb0, uint32_t L,
+                                          uint32_t j, int r, float (&mk)[4]) {
+  if (leven) {
+    const int p = r & 1;
+    float mine[2], recv[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t e = 2 * p + s;
+      const uint32_t h = pair_hash32(dk, (rb0 + e * L + (j & ~1u)) >> 1);
+      const float lo = (h & 0xffffu) >= dk.thresh ? dk.scale : 0.f;
+      const float hi = (h >> 16) >= dk.thresh ? dk.scale : 0.f;
+      mine[s] = p ? hi : lo;
+      recv[s] = __shfl_xor(p ? lo : hi, 1, 64);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) mk[e] = ((e >> 1) == p) ? mine[e & 1] : recv[e & 1];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) mk[e] = keep_mult32(dk, rb0 + e * L + j);
+  }
+}
+
+#ifndef RS_LONG_FWD_MINW
+#define RS_LONG_FWD_MINW 1
+#endif
+#ifndef RS_LONG_BWD_MINW
+#define RS_LONG_BWD_MINW 1
+#endif
+template <int NT, bool DROP, bool QB>
+__global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kernel(
+    const void* __restrict__ qkv_, const uint8_t* __restrict__ key_pad, float* __restrict__ out,
     float* __restrict__ lse, int B, int L, int d, int H, float scale, float pdrop,
     const int64_t* __restrict__ key, int site) {
   constexpr int LP = NT * 16;
+  __shared__ __attribute__((aligned(16))) float Qs[LP][kRowP];
   __shared__ __attribute__((aligned(16))) float Ks[LP][kRowP];
   __shared__ __attribute__((aligned(16))) float Vs[LP][kRowP];
   __shared__ __attribute__((aligned(16))) float Tsm[4][16 * kRowP];
@@ -804,7 +838,9 @@ __global__ __launch_bounds__(256) void attn_fwd_long_bf16_kernel(
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
   const int ld = 3 * d;
-  const float* base = qkv + (int64_t)b * L * ld + h * 16;
+  typedef typename std::conditional<QB, __bf16, float>::type QT;
+  const QT* base = reinterpret_cast<const QT*>(qkv_) + (int64_t)b * L * ld + h * 16;
+  load_head_image<LP>(base, ld, L, 0, Qs);  // Q too: no global load inside the tile loop
   load_head_image<LP>(base, ld, L, d, Ks);
   load_head_image<LP>(base, ld, L, 2 * d, Vs);
   const uint64_t kbits = key_bits_long<NT>(key_pad, b, L, lane, q);
@@ -821,7 +857,7 @@ __global__ __launch_bounds__(256) void attn_fwd_long_bf16_kernel(
   for (int tq = wave; tq < NT; tq += 4) {
     const int i = tq * 16 + r;
     const f4 z = {0.f, 0.f, 0.f, 0.f};
-    const s4v qb = bf4(i < L ? ld4(base + (int64_t)i * ld + 4 * q) : z);
+    const s4v qb = bf4(ld4(&Qs[i][4 * q]));
     f4 sv[NT];
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk) sv[tk] = mfma16(kb[tk], qb, z);
@@ -859,11 +895,11 @@ __global__ __launch_bounds__(256) void attn_fwd_long_bf16_kernel(
   }
 }
 
-template <int NT, bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_long_bf16_kernel(
-    const float* __restrict__ qkv, const uint8_t* __restrict__ key_pad,
+template <int NT, bool DROP, bool QB>
+__global__ __launch_bounds__(256, RS_LONG_BWD_MINW) void attn_bwd_long_bf16_kernel(
+    const void* __restrict__ qkv_, const uint8_t* __restrict__ key_pad,
     const float* __restrict__ out, const float* __restrict__ dout, const float* __restrict__ lse,
-    float* __restrict__ dqkv, int B, int L, int d, int H, float scale, float pdrop,
+    void* __restrict__ dqkv_, int B, int L, int d, int H, float scale, float pdrop,
     const int64_t* __restrict__ key, int site) {
   constexpr int LP = NT * 16;
   constexpr int NW = (NT + 3) / 4;  // tiles per wave
@@ -882,7 +918,8 @@ __global__ __launch_bounds__(256) void attn_bwd_long_bf16_kernel(
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
   const int ld = 3 * d;
-  const float* base = qkv + (int64_t)b * L * ld + h * 16;
+  typedef typename std::conditional<QB, __bf16, float>::type QT;
+  const QT* base = reinterpret_cast<const QT*>(qkv_) + (int64_t)b * L * ld + h * 16;
   load_head_image<LP>(base, ld, L, 0, Qs);
   load_head_image<LP>(base, ld, L, d, Ks);
   load_head_image<LP>(base, ld, L, 2 * d, Vs);
@@ -916,7 +953,7 @@ __global__ __launch_bounds__(256) void attn_bwd_long_bf16_kernel(
   const float scale2 = scale * kLog2e;
   const f4 z = {0.f, 0.f, 0.f, 0.f};
   float* T = Tsm[wave];
-  float* dbase = dqkv + (int64_t)b * L * ld + h * 16;
+  QT* dbase = reinterpret_cast<QT*>(dqkv_) + (int64_t)b * L * ld + h * 16;
   __syncthreads();
 
   // ---- phase A: dK, dV for key tiles wave, wave + 4, ... (query on the row)
@@ -947,15 +984,17 @@ __global__ __launch_bounds__(256) void attn_bwd_long_bf16_kernel(
         const f4 sacc = mfma16(qr, kr[u], z);  // S[query 16 tq + 4q + e][key 16 tk + r]
         const f4 pacc = mfma16(gr, vr[u], z);  // dP[query][key] = dO_i . V_j
         const uint32_t j = (uint32_t)(tk * 16 + r);
+        float mk[4] = {1.f, 1.f, 1.f, 1.f};
+        if (DROP)
+          keep_col4(dk, leven, ((uint32_t)bh * (uint32_t)L + (uint32_t)(tq * 16 + 4 * q)) * (uint32_t)L,
+                    (uint32_t)L, j, r, mk);
         f4 pz, ds;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = tq * 16 + 4 * q + e;
           const float pv = (kval[u] != 0.f && i < L) ? __builtin_amdgcn_exp2f(sacc[e] * scale2 - l2[e]) : 0.f;
-          float mk = 1.f;
-          if (DROP) mk = keep_mult32(dk, ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L + j);
-          pz[e] = pv * mk;
-          ds[e] = pv * (mk * pacc[e] - Dq[e]);
+          pz[e] = pv * mk[e];
+          ds[e] = pv * (mk[e] * pacc[e] - Dq[e]);
         }
         dv_acc[u] = mfma16(bf4(pz), gc[0], dv_acc[u]);  // (P∘Z)^T dO
         dk_acc[u] = mfma16(bf4(ds), qc[0], dk_acc[u]);  // dS^T Q
@@ -1013,6 +1052,157 @@ __global__ __launch_bounds__(256) void attn_bwd_long_bf16_kernel(
   }
 }
 
+// Single-pass backward (default): key-parallel as phase A above, plus dQ from the same tiles.
+// dQ = dS K contracts over keys, so the lane's dS tile (query on the row) is transposed through
+// the wave's LDS image into an A fragment; each wave keeps partial dQ tiles for every query tile
+// in registers and the four partials are summed in wave order at the end (deterministic). P and
+// dP are computed once per (query, key) pair instead of twice (one exp, half a hash per pair).
+template <int NT, bool DROP, bool QB>
+__global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
+    const void* __restrict__ qkv_, const uint8_t* __restrict__ key_pad,
+    const float* __restrict__ out, const float* __restrict__ dout, const float* __restrict__ lse,
+    void* __restrict__ dqkv_, int B, int L, int d, int H, float scale, float pdrop,
+    const int64_t* __restrict__ key, int site) {
+  constexpr int LP = NT * 16;
+  constexpr int NW = (NT + 3) / 4;  // key tiles per wave
+  constexpr int TP = 20;
+  __shared__ __attribute__((aligned(16))) float img[4][LP][kRowP];  // Q, K, V, dO; then dQ partials
+  __shared__ __attribute__((aligned(16))) float L2s[LP];  // lse * log2(e)
+  __shared__ __attribute__((aligned(16))) float Ds[LP];   // D_i = dO_i . O_i
+  __shared__ float Kv[LP];                                // 1: key j is valid
+  __shared__ __attribute__((aligned(16))) float Tsm[4][16 * TP];
+  float(*Qs)[kRowP] = img[0];
+  float(*Ks)[kRowP] = img[1];
+  float(*Vs)[kRowP] = img[2];
+  float(*Gs)[kRowP] = img[3];
+  int b, h;
+  if (!map_bh(B, H, b, h)) return;  // uniform over the workgroup
+  const int bh = b * H + h;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int ld = 3 * d;
+  typedef typename std::conditional<QB, __bf16, float>::type QT;
+  const QT* base = reinterpret_cast<const QT*>(qkv_) + (int64_t)b * L * ld + h * 16;
+  load_head_image<LP>(base, ld, L, 0, Qs);
+  load_head_image<LP>(base, ld, L, d, Ks);
+  load_head_image<LP>(base, ld, L, 2 * d, Vs);
+  for (int e = threadIdx.x; e < LP * 4; e += 256) {
+    const int row = e >> 2, c4 = (e & 3) * 4;
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < L) v = ld4(dout + ((int64_t)b * L + row) * d + h * 16 + c4);
+    *reinterpret_cast<f4*>(&Gs[row][c4]) = v;
+  }
+  for (int i = threadIdx.x; i < LP; i += 256) {
+    float Di = 0.f, li = 0.f, kv = 0.f;
+    if (i < L) {
+      const float* o = out + ((int64_t)b * L + i) * d + h * 16;
+      const float* g = dout + ((int64_t)b * L + i) * d + h * 16;
+#pragma unroll
+      for (int c = 0; c < 16; c += 4) {
+        const f4 ov = ld4(o + c), gv = ld4(g + c);
+        Di += ov[0] * gv[0] + ov[1] * gv[1] + ov[2] * gv[2] + ov[3] * gv[3];
+      }
+      li = lse[(int64_t)bh * L + i] * kLog2e;
+      kv = key_pad[(int64_t)b * L + i] == 0 ? 1.f : 0.f;
+    }
+    Ds[i] = Di;
+    L2s[i] = li;
+    Kv[i] = kv;
+  }
+  DropKey dk;
+  if (DROP) dk = make_key(key, site, pdrop);
+  const bool leven = (L & 1) == 0;
+  const float scale2 = scale * kLog2e;
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  float* T = Tsm[wave];
+  QT* dbase = reinterpret_cast<QT*>(dqkv_) + (int64_t)b * L * ld + h * 16;
+  __syncthreads();
+
+  s4v kr[NW], vr[NW], kc[NW];
+  float kval[NW];
+  f4 dk_acc[NW], dv_acc[NW], dq_acc[NT];
+#pragma unroll
+  for (int u = 0; u < NW; ++u) {
+    const int tk = wave + 4 * u < NT ? wave + 4 * u : NT - 1;
+    kr[u] = bf4(ld4(&Ks[tk * 16 + r][4 * q]));
+    vr[u] = bf4(ld4(&Vs[tk * 16 + r][4 * q]));
+    s4v c1[1];
+    col_frags<1, kRowP>(&Ks[tk * 16][0], r, q, c1);
+    kc[u] = c1[0];
+    kval[u] = Kv[tk * 16 + r];
+    dk_acc[u] = dv_acc[u] = z;
+  }
+#pragma unroll
+  for (int tq = 0; tq < NT; ++tq) {
+    const s4v qr = bf4(ld4(&Qs[tq * 16 + r][4 * q]));
+    const s4v gr = bf4(ld4(&Gs[tq * 16 + r][4 * q]));
+    s4v qc[1], gc[1];
+    col_frags<1, kRowP>(&Qs[tq * 16][0], r, q, qc);
+    col_frags<1, kRowP>(&Gs[tq * 16][0], r, q, gc);
+    const f4 l2 = ld4(&L2s[tq * 16 + 4 * q]);
+    const f4 Dq = ld4(&Ds[tq * 16 + 4 * q]);
+    dq_acc[tq] = z;
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int tk = wave + 4 * u;
+      if (tk >= NT) break;
+      const f4 sacc = mfma16(qr, kr[u], z);  // S[query 16 tq + 4q + e][key 16 tk + r]
+      const f4 pacc = mfma16(gr, vr[u], z);  // dP[query][key] = dO_i . V_j
+      float mk[4] = {1.f, 1.f, 1.f, 1.f};
+      if (DROP)
+        keep_col4(dk, leven, ((uint32_t)bh * (uint32_t)L + (uint32_t)(tq * 16 + 4 * q)) * (uint32_t)L,
+                  (uint32_t)L, (uint32_t)(tk * 16 + r), r, mk);
+      f4 pz, ds;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = tq * 16 + 4 * q + e;
+        const float pv = (kval[u] != 0.f && i < L) ? __builtin_amdgcn_exp2f(sacc[e] * scale2 - l2[e]) : 0.f;
+        pz[e] = pv * mk[e];
+        ds[e] = pv * (mk[e] * pacc[e] - Dq[e]);
+      }
+      dv_acc[u] = mfma16(bf4(pz), gc[0], dv_acc[u]);  // (P∘Z)^T dO
+      dk_acc[u] = mfma16(bf4(ds), qc[0], dk_acc[u]);  // dS^T Q
+      // dS with the key on the k side: T[query][key] -> lane (r, q) reads row r, keys 4q..4q+3
+#pragma unroll
+      for (int e = 0; e < 4; ++e) T[(4 * q + e) * TP + r] = ds[e];
+      __builtin_amdgcn_wave_barrier();
+      const f4 dst = ld4(&T[r * TP + 4 * q]);
+      __builtin_amdgcn_wave_barrier();
+      dq_acc[tq] = mfma16(bf4(dst), kc[u], dq_acc[tq]);  // dS K: [query 4q + e][c = r]
+    }
+  }
+  // dK / dV rows of this wave's key tiles
+#pragma unroll
+  for (int u = 0; u < NW; ++u) {
+    const int tk = wave + 4 * u;
+    if (tk >= NT) break;
+    const f4 vk = tile_rows<TP>(T, dk_acc[u] * scale, r, q, lane);
+    const f4 vv = tile_rows<TP>(T, dv_acc[u], r, q, lane);
+    const int row = tk * 16 + (lane >> 2);
+    if (row < L) {
+      st4q(dbase + (int64_t)row * ld + d + 4 * (lane & 3), vk);
+      st4q(dbase + (int64_t)row * ld + 2 * d + 4 * (lane & 3), vv);
+    }
+  }
+  // dQ: the four waves' partial tiles summed in wave order through the (now free) images
+  __syncthreads();
+  float* part = &img[0][0][0] + wave * LP * 16;
+#pragma unroll
+  for (int tq = 0; tq < NT; ++tq)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[(tq * 16 + 4 * q + e) * 16 + r] = dq_acc[tq][e];
+  __syncthreads();
+  const float* p0 = &img[0][0][0];
+  for (int e = threadIdx.x; e < LP * 4; e += 256) {
+    const int row = e >> 2, c4 = (e & 3) * 4;
+    if (row >= L) continue;
+    f4 v = ld4(p0 + row * 16 + c4);
+#pragma unroll
+    for (int w = 1; w < 4; ++w) v += ld4(p0 + w * LP * 16 + row * 16 + c4);
+    st4q(dbase + (int64_t)row * ld + c4, v * scale);
+  }
+}
+
 int threads_for(int L) {
   int t = ((L + 63) / 64) * 64;
   return t > 256 ? 256 : t;
@@ -1023,9 +1213,9 @@ int threads_for(int L) {
 
 using namespace rs;
 
-// bf16 compute mode, head_dim 16, 64 < L <= 256, fp32 qkv: the long-history MFMA kernels
+// bf16 compute mode, head_dim 16, 64 < L <= 256 (fp32 or bf16 qkv): the long-history MFMA kernels
 static bool long_bf16_ok(int hd, int L, int B, int H, int flags) {
-  return hd == 16 && L > 64 && L <= 256 && (flags & RS_GEMM_BF16) && !(flags & RS_ATTN_QKV_BF16) &&
+  return hd == 16 && L > 64 && L <= 256 && (flags & RS_GEMM_BF16) &&
          (int64_t)B * H * L * L < ((int64_t)1 << 32) && !getenv_flag("RSYS_ATTN_VALU");
 }
 
@@ -1054,9 +1244,9 @@ extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out,
   const size_t lds = (size_t)(2 * L * hd + L) * sizeof(float);
   RS_CHECK_ARG(lds <= 64 * 1024 || long_bf16_ok(hd, L, B, H, flags), "rs_attn_fwd: L=%d hd=%d exceeds LDS", L, hd);
   RS_CHECK_ARG(d % 4 == 0 && aligned16(qkv) && aligned16(out), "rs_attn_fwd: needs 16-byte aligned rows");
-  RS_CHECK_ARG(!(flags & RS_ATTN_QKV_BF16) || ((flags & RS_GEMM_BF16) && hd == 16 && L <= 64 &&
+  RS_CHECK_ARG(!(flags & RS_ATTN_QKV_BF16) || ((flags & RS_GEMM_BF16) && hd == 16 && L <= 256 &&
                                                  !getenv_flag("RSYS_ATTN_VALU")),
-               "rs_attn_fwd: bf16 qkv storage needs the bf16 MFMA path (head_dim 16, L <= 64)");
+               "rs_attn_fwd: bf16 qkv storage needs the bf16 MFMA path (head_dim 16, L <= 256)");
   hipStream_t st = as_stream(stream);
   if (hd == 16 && L <= 64 && (int64_t)B * H * L * L < ((int64_t)1 << 32) && !getenv_flag("RSYS_ATTN_VALU")) {
     const int nt = (L + 15) / 16;
@@ -1081,10 +1271,13 @@ extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out,
     const dim3 gl(bh_grid(B, H));
 #define RS_AFL(NTV)                                                                                 \
   if (nt == NTV) {                                                                                  \
-    if (p > 0.f) attn_fwd_long_bf16_kernel<NTV, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
-    else attn_fwd_long_bf16_kernel<NTV, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    if (qb && p > 0.f) attn_fwd_long_bf16_kernel<NTV, true, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    else if (qb) attn_fwd_long_bf16_kernel<NTV, false, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    else if (p > 0.f) attn_fwd_long_bf16_kernel<NTV, true, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    else attn_fwd_long_bf16_kernel<NTV, false, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
   }
     const int nt = (L + 15) / 16;
+    const bool qb = (flags & RS_ATTN_QKV_BF16) != 0;
     RS_AFL(5) RS_AFL(6) RS_AFL(7) RS_AFL(8) RS_AFL(9) RS_AFL(10) RS_AFL(11) RS_AFL(12) RS_AFL(13)
     RS_AFL(14) RS_AFL(15) RS_AFL(16)
 #undef RS_AFL
@@ -1111,9 +1304,9 @@ extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float
   const size_t lds = (size_t)(4 * L * hd + 3 * L) * sizeof(float);
   RS_CHECK_ARG(lds <= 64 * 1024 || long_bf16_ok(hd, L, B, H, flags), "rs_attn_bwd: L=%d hd=%d exceeds LDS", L, hd);
   RS_CHECK_ARG(d % 4 == 0 && aligned16(qkv) && aligned16(dout), "rs_attn_bwd: needs 16-byte aligned rows");
-  RS_CHECK_ARG(!(flags & RS_ATTN_QKV_BF16) || ((flags & RS_GEMM_BF16) && hd == 16 && L <= 64 &&
+  RS_CHECK_ARG(!(flags & RS_ATTN_QKV_BF16) || ((flags & RS_GEMM_BF16) && hd == 16 && L <= 256 &&
                                                  !getenv_flag("RSYS_ATTN_VALU")),
-               "rs_attn_bwd: bf16 qkv storage needs the bf16 MFMA path (head_dim 16, L <= 64)");
+               "rs_attn_bwd: bf16 qkv storage needs the bf16 MFMA path (head_dim 16, L <= 256)");
   hipStream_t st = as_stream(stream);
   if (hd == 16 && L <= 64 && (int64_t)B * H * L * L < ((int64_t)1 << 32) && !getenv_flag("RSYS_ATTN_VALU")) {
     RS_CHECK_ARG(aligned16(out), "rs_attn_bwd: needs 16-byte aligned rows");
@@ -1140,10 +1333,21 @@ extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float
     const dim3 gl(bh_grid(B, H));
 #define RS_ABL(NTV)                                                                                 \
   if (nt == NTV) {                                                                                  \
-    if (p > 0.f) attn_bwd_long_bf16_kernel<NTV, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
-    else attn_bwd_long_bf16_kernel<NTV, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    if (two_pass) {                                                                                 \
+      if (qb && p > 0.f) attn_bwd_long_bf16_kernel<NTV, true, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+      else if (qb) attn_bwd_long_bf16_kernel<NTV, false, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+      else if (p > 0.f) attn_bwd_long_bf16_kernel<NTV, true, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+      else attn_bwd_long_bf16_kernel<NTV, false, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    } else {                                                                                        \
+      if (qb && p > 0.f) attn_bwd_long1_bf16_kernel<NTV, true, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+      else if (qb) attn_bwd_long1_bf16_kernel<NTV, false, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+      else if (p > 0.f) attn_bwd_long1_bf16_kernel<NTV, true, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+      else attn_bwd_long1_bf16_kernel<NTV, false, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    }                                                                                               \
   }
     const int nt = (L + 15) / 16;
+    const bool qb = (flags & RS_ATTN_QKV_BF16) != 0;
+    const bool two_pass = getenv_flag("RSYS_ATTN_LONG_2PASS");  // the FA-2 split, for comparison
     RS_ABL(5) RS_ABL(6) RS_ABL(7) RS_ABL(8) RS_ABL(9) RS_ABL(10) RS_ABL(11) RS_ABL(12) RS_ABL(13)
     RS_ABL(14) RS_ABL(15) RS_ABL(16)
 #undef RS_ABL

@@ -171,8 +171,8 @@ def gather_bwd(segs, rows, dout):
 
 def qkv_bf16_ok(L, d, H):
     """Store the packed qkv (and dqkv) as bf16: bf16 compute mode on the bf16 MFMA attention
-    path (head_dim 16, L <= 64), where Q, K, V are only MFMA operands (RS_ATTN_QKV_BF16)."""
-    return (precision.compute_dtype() == 'bf16' and d // H == 16 and L <= 64 and
+    path (head_dim 16, L <= 256), where Q, K, V are only MFMA operands (RS_ATTN_QKV_BF16)."""
+    return (precision.compute_dtype() == 'bf16' and d // H == 16 and L <= 256 and
             not os.environ.get('RSYS_ATTN_VALU') and not os.environ.get('RSYS_QKV_FP32'))
 
 

@@ -250,7 +250,9 @@ def test_bf16_step_fused_ffn_vs_unfused(monkeypatch):
 def _bf16_attention_ref(qkv, key_pad, dout, B, L, d, H):
     """The bf16 MFMA attention's arithmetic in float64: Q, K, V, dO rounded to bf16; the
     unnormalised probabilities and dS rounded to bf16 where they enter a product; softmax,
-    dropout-free dS (D from P and dP) and the scale in full precision."""
+    dropout-free dS and the scale in full precision. D = sum_j P_ij dP_ij for L <= 64 (the
+    per-wave kernels form it from their register tiles); for L > 64 the key-parallel kernels take
+    D = dO_i . O_i from the fp32 dO and the forward output, which carries the bf16 rounding of P."""
     hd = d // H
     q, k, v = (r16(t).double() for t in qkv.view(B, L, 3, H, hd).permute(2, 0, 3, 1, 4))
     g = r16(dout).double().view(B, L, H, hd).transpose(1, 2)
@@ -268,6 +270,8 @@ def _bf16_attention_ref(qkv, key_pad, dout, B, L, d, H):
     # D_i = sum_j P_ij dP_ij (== dO_i . O_i in exact arithmetic): the kernel forms it from its
     # register tiles, with dP from the bf16-rounded dO and V
     D = (P * dp).sum(-1, keepdim=True)
+    if L > 64:
+        D = (dout.double().view(B, L, H, hd).transpose(1, 2) * out).sum(-1, keepdim=True)
     ds = P * (dp - D)
     dsb, Pb = r16(ds.float()).double(), r16(P.float()).double()
     dq = dsb @ k * sc
