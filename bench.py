@@ -58,7 +58,8 @@ def parse():
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--dtype', default='config', choices=['config', 'fp32', 'bf16'],
                     help='compute dtype of the GEMMs (bf16: bf16 MFMA, fp32 accumulate / master weights); '
-                         'config: bf16 for c2 (BASELINE configs[1] is quoted in bf16), fp32 otherwise')
+                         'config: bf16 for c2 (BASELINE configs[1] is quoted in bf16) and c5 (its L = 200 '
+                         'encoder runs on the bf16 MFMA attention), fp32 otherwise')
     ap.add_argument('--hard-negatives', type=int, default=0,
                     help='N sampled hard negatives per row, materialised from a device item catalog '
                          'each step (one grouped item-tower pass)')
@@ -151,7 +152,7 @@ def main():
     if args.zipf:
         cfg.setdefault('synthetic', {})['zipf'] = args.zipf
     if args.dtype == 'config':
-        args.dtype = 'bf16' if args.config == 'c2' else 'fp32'
+        args.dtype = 'bf16' if args.config in ('c2', 'c5') else 'fp32'
     precision.set_compute_dtype(args.dtype)
     B = args.batch or int(cfg['train']['batch_size'])
     T = float(cfg['train']['temperature'])
