@@ -73,7 +73,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* lo, const __bf16* hi) {
 // MODE 1: dU (own = U, str = I; lse of the owned user)
 // MODE 2: dI (own = I, str = U; lse of the streamed user)
 template <int D, int MODE>
-__global__ __launch_bounds__(64 * kWaves) void ce_tile_kernel(CeArgs a) {
+__device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split) {
   constexpr int KS = D / 16;          // 32x32x16 k-steps over the embedding
   constexpr int PT = D + 8;           // LDS pitch (bf16) of a streamed tile row
   constexpr int DB = D / 32;          // 32-wide blocks of the gradient
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(64 * kWaves) void ce_tile_kernel(CeArgs a) {
   const int B = a.B;
   const int o = blockIdx.x * (kOwnW * kWaves) + wave * kOwnW + c;  // this lane's owned row
   const bool o_ok = o < B;
-  const int t_begin = blockIdx.y * a.split_rows;
+  const int t_begin = split * a.split_rows;
   const int t_end = min(B, t_begin + a.split_rows);
 
   // owned fragments: B operand of the S tile, lane (c, h) holds own[o][16 s + 8 h .. +7]
@@ -276,7 +276,6 @@ __global__ __launch_bounds__(64 * kWaves) void ce_tile_kernel(CeArgs a) {
   if constexpr (MODE == 0) {
     if (has_dg && o_ok) a.diag[o] = dg;
   }
-  const int split = blockIdx.y;
   if constexpr (MODE == 0) {
     // merge the two lane halves (same owned row, different streamed rows)
     const float om = __shfl_xor(run_m, 32, 64), os = __shfl_xor(run_s, 32, 64);
@@ -301,6 +300,19 @@ __global__ __launch_bounds__(64 * kWaves) void ce_tile_kernel(CeArgs a) {
         }
     }
   }
+}
+
+template <int D, int MODE>
+__global__ __launch_bounds__(64 * kWaves) void ce_tile_kernel(CeArgs a) {
+  ce_tile_body<D, MODE>(a, blockIdx.y);
+}
+
+// dU and dI in one launch (blockIdx.z): the two halves are independent given lse, and 1,024
+// workgroups hide each other's tile latencies better than two back-to-back 512-workgroup grids
+template <int D>
+__global__ __launch_bounds__(64 * kWaves) void ce_bwd_pair_kernel(CeArgs aU, CeArgs aI) {
+  if (blockIdx.z == 0) ce_tile_body<D, 1>(aU, blockIdx.y);
+  else ce_tile_body<D, 2>(aI, blockIdx.y);
 }
 
 // per user row: merge the split statistics with the hard-negative logits -> lse, row loss
@@ -359,14 +371,29 @@ __global__ __launch_bounds__(256) void ce_hard_bwd_kernel(const float* __restric
   }
 }
 
-// out[r][d] = sum over splits (fixed order) of part[s][r][d]
+// out[r][d] = sum over splits (fixed order) of part[s][r][d]; two outputs in one launch
+// (out2 = the sums of part2, the block after part's NS slabs), 8 slab loads in flight
 __global__ void ce_reduce_kernel(const float* __restrict__ part, int NS, int64_t n,
-                                 float* __restrict__ out) {
-  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4;
-  if (i >= n) return;
+                                 float* __restrict__ out, float* __restrict__ out2) {
+  int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4;
+  if (i >= (out2 ? 2 * n : n)) return;
+  float* dst = out;
+  if (i >= n) {
+    i -= n;
+    part += (int64_t)NS * n;
+    dst = out2;
+  }
   floatx4 acc = *reinterpret_cast<const floatx4*>(part + i);
-  for (int s = 1; s < NS; ++s) acc += *reinterpret_cast<const floatx4*>(part + (int64_t)s * n + i);
-  *reinterpret_cast<floatx4*>(out + i) = acc;
+  int s = 1;
+  for (; s + 8 <= NS; s += 8) {
+    floatx4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const floatx4*>(part + (int64_t)(s + u) * n + i);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; s < NS; ++s) acc += *reinterpret_cast<const floatx4*>(part + (int64_t)s * n + i);
+  *reinterpret_cast<floatx4*>(dst + i) = acc;
 }
 
 int splits_for(int B) {
@@ -394,7 +421,7 @@ using namespace rs;
 extern "C" int64_t rs_inbatch_ce_fused_ws_bytes(int B, int D) {
   const int NS = splits_for(B);
   const int64_t fwd = (int64_t)NS * B * 2 + B;
-  const int64_t bwd = (int64_t)NS * B * D;
+  const int64_t bwd = (int64_t)2 * NS * B * D;  // dU and dI partials side by side
   return (fwd > bwd ? fwd : bwd) * (int64_t)sizeof(float);
 }
 
@@ -442,18 +469,17 @@ extern "C" int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const flo
   a.part_d = ws;
   const int NSr = cdiv(B, a.split_rows);
   const int64_t n = (int64_t)B * D;
-  // dU: users owned, items streamed
-  a.own = U; a.str = I;
-  launch_tiles<1>(a, D, NSr, st);
-  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd dU");
-  ce_reduce_kernel<<<(int)cdiv(n / 4, 256), 256, 0, st>>>(ws, NSr, n, dU);
-  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd dU reduce");
-  // dI: items owned, users streamed
-  a.own = I; a.str = U;
-  launch_tiles<2>(a, D, NSr, st);
-  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd dI");
-  ce_reduce_kernel<<<(int)cdiv(n / 4, 256), 256, 0, st>>>(ws, NSr, n, dI);
-  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd dI reduce");
+  // dU: users owned, items streamed; dI: items owned, users streamed -- one launch
+  CeArgs aU = a, aI = a;
+  aU.own = U; aU.str = I;
+  aI.own = I; aI.str = U;
+  aI.part_d = ws + (int64_t)NSr * n;
+  const dim3 grid(cdiv(B, kOwnW * kWaves), NSr, 2);
+  if (D == 128) ce_bwd_pair_kernel<128><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
+  else ce_bwd_pair_kernel<64><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
+  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd tiles");
+  ce_reduce_kernel<<<(int)cdiv(2 * n / 4, 256), 256, 0, st>>>(ws, NSr, n, dU, dI);
+  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd reduce");
   if (N) {
     const HStrideArgs hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
     ce_hard_bwd_kernel<<<cdiv(B, 4), 256, 0, st>>>(U, Hn, hs.row, hs.slot, B, N, D, a.invT, lse, grad_out, dhl);

@@ -237,15 +237,15 @@ __global__ void splitk_reduce_kernel(GemmArgs a) {
   if (a.epi & RS_EPI_DROP_B) kb = make_key(a.drop_key, a.site_b, a.drop_p);
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    float v[8];
+    float v[16];
     int z = 0;
     float acc = 0.f;
-    // fixed order, 8 independent loads in flight
-    for (; z + 8 <= a.split_k; z += 8) {
+    // fixed order, 16 independent loads in flight
+    for (; z + 16 <= a.split_k; z += 16) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = a.ws[(int64_t)(z + u) * total + idx];
+      for (int u = 0; u < 16; ++u) v[u] = a.ws[(int64_t)(z + u) * total + idx];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u];
+      for (int u = 0; u < 16; ++u) acc += v[u];
     }
     for (; z < a.split_k; ++z) acc += a.ws[(int64_t)z * total + idx];
     const int m = (int)(idx / a.N), n = (int)(idx % a.N);
@@ -281,9 +281,12 @@ extern "C" int rs_gemm_auto_split(int M, int N, int K) {
   // weight-gradient streaming kernel (gemm_stream.hip): needs a workspace only
   if (K >= 2048 && (int64_t)M * N <= 16384 && wgrad_instance(M, N)) return 2;
   int s = (int)((512 + tiles - 1) / tiles);
-  int maxs = K / (BK * 4);  // each split keeps >= 4 k-tiles
+  // each split keeps >= 256 rows of K: the fixed-order reduce then sums <= K/256 partials per
+  // output (a 64-way split of a K = 4096 weight gradient took 22 us to compute and 20 us to
+  // reduce; 16-way: one batch of loads in the reduce)
+  int maxs = K / 256;
   if (s > maxs) s = maxs;
-  if (s > 256) s = 256;
+  if (s > 64) s = 64;
   return s < 1 ? 1 : s;
 }
 
