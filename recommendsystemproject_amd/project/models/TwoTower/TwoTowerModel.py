@@ -27,12 +27,58 @@ class TwoTowerModel(nn.Module):
         self.user_feature_mapping = user_mapping
         self.item_feature_mapping = item_mapping
 
+    def _side_stream(self, dev):
+        """The item tower's stream: the two towers are independent until the loss, so the item
+        tower (all small, latency-bound kernels at B = 4096) runs beside the user tower's encoder.
+        RSYS_TOWER_STREAMS=0 keeps everything on the current stream."""
+        if os.environ.get('RSYS_TOWER_STREAMS', '1') == '0':
+            return None
+        s = getattr(self, '_rs_side_stream', None)
+        if s is None or s.device != dev:
+            s = torch.cuda.Stream(device=dev)
+            self._rs_side_stream = s
+        return s
+
     def forward(self, batch_data):
         """-> (user_emb [B,D], item_emb [B,D], hard_neg_emb [B,N,D] or None) (TwoTowerModel.py:35-62;
         T13: one item-tower pass per hard-negative slot, so BatchNorm statistics are per slot)."""
+        dev = self.user_tower.feature_bn.weight.device
         _hip.require_device(self.user_tower.feature_bn.weight)
         ensure_flat(self)
+        side = self._side_stream(dev)
+        if side is None:
+            user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
+            item_emb, hard_neg_emb = self._item_side(batch_data)
+            return user_emb, item_emb, hard_neg_emb
+        # fork: the item tower (and its hard-negative pass) on the side stream, the user tower on
+        # the current one; join before the loss. Autograd runs each tower's backward on the stream
+        # its forward used, so the backward overlaps the same way.
+        main = torch.cuda.current_stream(dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            item_emb, hard_neg_emb = self._item_side(batch_data)
         user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
+        main.wait_stream(side)
+        outs = [t for t in (item_emb, hard_neg_emb) if t is not None]
+        for t in outs:
+            t.record_stream(main)  # made on the side stream, read by the loss on the main one
+        if torch.is_grad_enabled() and item_emb.requires_grad:
+            joined = []
+
+            def _to_side(g):
+                # the loss's gradient (main stream) is read by the item tower's backward (side);
+                # once per backward, the main stream waits for the side stream's last kernels
+                g.record_stream(side)
+                if not joined:
+                    joined.append(True)
+                    torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_stream(side))
+                return g
+
+            for t in outs:
+                t.register_hook(_to_side)
+        return user_emb, item_emb, hard_neg_emb
+
+    def _item_side(self, batch_data):
         item_emb = self.item_tower(batch_data['item_tower'], self.item_feature_mapping)
         hard_neg_emb = None
         negs = batch_data.get('hard_negatives') if isinstance(batch_data, dict) else None
@@ -48,7 +94,7 @@ class TwoTowerModel(nn.Module):
             else:
                 hard_neg_emb = torch.stack([self.item_tower(neg, self.item_feature_mapping)
                                             for neg in negs], dim=1)
-        return user_emb, item_emb, hard_neg_emb
+        return item_emb, hard_neg_emb
 
     def predict(self, batch_data):
         user_emb, item_emb, _ = self.forward(batch_data)
