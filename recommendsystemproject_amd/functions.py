@@ -121,7 +121,8 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key):
     if p > 0:
         ops.dropout_bwd(dx, p, key, 0)
     lin = proc.feature_projection[0]
-    ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
+    # dx is final here (the dropout backward above ran in place before this point)
+    _wgrad_side(lambda: ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias)), dx, cat)
     dcat = ops.linear_bwd_input(dx, lin.weight)
     for s, t in zip(segs, tables):
         s.grad = grad_of(t).data_ptr()
@@ -185,6 +186,38 @@ def layer_fwd_last(lyr, x, key_pad, last, B, L, d, H, p, key, site):
     return x2, (x, qkv, att, lse, h1, x1, m1, r1) + ff
 
 
+_WGRAD_STREAMS = {}
+
+
+def _wgrad_side(fn, *reads):
+    """Run fn (weight-gradient GEMMs: they feed parameter gradients only) on a second stream,
+    beside the encoder backward's input-gradient chain (its critical path). The tensors fn reads
+    are recorded on that stream (their memory is not reused until it is done); the caller must not
+    modify them in place afterwards, and SeqEncoderFn.backward joins the stream at its end.
+    Off by default (RSYS_WGRAD_STREAM=1 enables it): measured at C2, the weight gradients compete
+    with the HBM-bound input-gradient kernels and the step got slower (1.877 -> 1.972 ms)."""
+    if os.environ.get('RSYS_WGRAD_STREAM', '0') != '1':
+        fn()
+        return
+    cur = torch.cuda.current_stream()
+    s = _WGRAD_STREAMS.get(cur.device)
+    if s is None:
+        s = _WGRAD_STREAMS[cur.device] = torch.cuda.Stream(device=cur.device)
+    s.wait_stream(cur)
+    with torch.cuda.stream(s):
+        fn()
+    for t in reads:
+        if t is not None:
+            t.record_stream(s)
+
+
+def _wgrad_join():
+    cur = torch.cuda.current_stream()
+    s = _WGRAD_STREAMS.get(cur.device)
+    if s is not None:
+        cur.wait_stream(s)
+
+
 def _post_attn_bwd(lyr, saved, dx2, p, key, site):
     """Backward of out-proj + LN1 + FFN + LN2 (any row count). Returns (dh1, datt): dh1 the
     gradient of the layer input through the residual, datt the gradient of the attention output."""
@@ -200,8 +233,12 @@ def _post_attn_bwd(lyr, saved, dx2, p, key, site):
         # dx1 = dh2 + dPre1 W1 (out of place: dff may be dh2 itself and is read again below)
         dh2, f1b, dpre = ops.ffn_bwd_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight,
                                           f1[1], dff, dh2, p)
-        ops.wgrad_bf16(dff, f1b, g(lyr.linear2.weight), db=g(lyr.linear2.bias))
-        ops.wgrad_bf16(dpre, x1, g(lyr.linear1.weight), db=g(lyr.linear1.bias))
+
+        def _ffn_wgrads(dff=dff, f1b=f1b, dpre=dpre):
+            ops.wgrad_bf16(dff, f1b, g(lyr.linear2.weight), db=g(lyr.linear2.bias))
+            ops.wgrad_bf16(dpre, x1, g(lyr.linear1.weight), db=g(lyr.linear1.bias))
+        # dff (possibly the old dh2) and x1 are not written again below: dh2 is a new tensor
+        _wgrad_side(_ffn_wgrads, dff, f1b, dpre, x1)
     else:
         ops.linear_bwd_weight(dff, f1, g(lyr.linear2.weight), db=g(lyr.linear2.bias))
         # f1 holds relu(.) after dropout: (f1 > 0) == kept & positive, kept scale 1/(1-p)
@@ -213,8 +250,13 @@ def _post_attn_bwd(lyr, saved, dx2, p, key, site):
     dsa = torch.empty_like(dh2) if p > 0 else None
     dh1 = ops.layernorm_bwd(h1, dh2, lyr.norm1.weight, m1, r1, g(lyr.norm1.weight), g(lyr.norm1.bias),
                             da=dsa, p=p, key=key, site=site + 1)
-    dsa = dh1 if dsa is None else dsa
-    ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
+    def _out_wgrad(dsa=dsa):
+        ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
+    if dsa is None:  # p == 0: dsa IS dh1, which the in-proj backward accumulates into: inline
+        dsa = dh1
+        _out_wgrad(dsa)
+    else:
+        _wgrad_side(_out_wgrad, dsa, att)
     datt = ops.linear_bwd_input(dsa, sa_mod.out_proj.weight)
     return dh1, datt
 
@@ -223,10 +265,12 @@ def _in_proj_bwd(lyr, x, dqkv, dx=None):
     """in_proj weight gradient and dx (+)= dqkv W_in."""
     g = grad_of
     sa_mod = lyr.self_attn
-    if dqkv.dtype == torch.bfloat16:  # bf16 dqkv (RS_ATTN_QKV_BF16): bf16-MFMA weight gradient
-        ops.wgrad_bf16(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
-    else:
-        ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
+    def _in_wgrad():
+        if dqkv.dtype == torch.bfloat16:  # bf16 dqkv (RS_ATTN_QKV_BF16): bf16-MFMA weight gradient
+            ops.wgrad_bf16(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
+        else:
+            ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
+    _wgrad_side(_in_wgrad, dqkv, x)  # neither is written again (dx is the layer-input gradient)
     if dx is None:
         return ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight)
     return ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight, out=dx, beta=1.0)  # dx = dh1 + dqkv Win
@@ -325,6 +369,7 @@ class SeqEncoderFn(torch.autograd.Function):
             dx = layer_bwd(ctx.layers[i], ctx.layer_saved[i], dx, ctx.key_pad, B, L, d, H, p, key,
                            _layer_site(i))
         seq_input_bwd(proc, ctx.in_saved, dx, B, L, p, key)
+        _wgrad_join()  # the weight gradients complete before anything after the encoder backward
         ctx.layer_saved = ctx.in_saved = None
         return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
