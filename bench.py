@@ -288,12 +288,25 @@ def main():
     el = float(el_t.item())
     final_loss = float(loss.item())
 
-    # roofline of the dominant kernel: HIP events on the launch stream, eager instrumented steps
+    # roofline of the dominant kernel: HIP events on the launch stream, eager instrumented steps.
+    # A spin kernel first gives the host a head start: the launches (Python + ctypes, slower than
+    # the small tower kernels themselves) then queue up behind it and the GPU runs them back to
+    # back, so an event pair times its kernel and not the host's launch latency.
+    # The towers run serially here (RSYS_TOWER_STREAMS=0): each event pair then times its kernel
+    # alone, not its kernel sharing the GPU with the other tower's.
+    torch.cuda.synchronize()
+    tower_streams = os.environ.get('RSYS_TOWER_STREAMS')
+    os.environ['RSYS_TOWER_STREAMS'] = '0'
+    torch.cuda._sleep(int(2.4e9 * 0.03))  # ~30 ms at the 2.4 GHz shader clock
     with KernelTimer() as kt:
         for _ in range(3):
             fwd_bwd()
             allreduce()
             opt_step()
+    if tower_streams is None:
+        del os.environ['RSYS_TOWER_STREAMS']
+    else:
+        os.environ['RSYS_TOWER_STREAMS'] = tower_streams
     summ = kt.summary()
     dom_name, dom = max(summ.items(), key=lambda kv: kv[1]['ms'])
     # the dominant entry point's MFMA peak: bf16 MFMA in the bf16 compute mode (its GEMMs), f32 else

@@ -128,6 +128,19 @@ WORK = {
 }
 
 
+TOKEN_ROWS = 32768  # rs_gemm_f32 calls streaming >= this many rows: the encoder's token GEMMs
+
+
+def entry_key(name, args):
+    """Timing / PMC key of one rs_* call. rs_gemm_f32 is split into its two regimes, which are
+    different kernels: the encoder's token-level streaming GEMMs (rows = B*L, HBM-bound) and the
+    batch-level tower / loss GEMMs (rows = B, latency-bound small grids)."""
+    if name == 'rs_gemm_f32':
+        rows = args[4] if args[0] else args[2]  # (transA, transB, M, N, K, ...): rows streamed
+        return 'rs_gemm_f32:tokens' if rows >= TOKEN_ROWS else 'rs_gemm_f32:batch'
+    return name
+
+
 class _CallPatch:
     """Swap `call` in _hip and in the modules that imported it by name."""
 
@@ -163,7 +176,7 @@ class PmcBracket(_CallPatch):
         orig = _hip.call
 
         def bracketed(name, *args):
-            if name != self.target:
+            if entry_key(name, args) != self.target:
                 return orig(name, *args)
             st = torch.cuda.current_stream().cuda_stream
             orig('rs_prof_marker', 1, st)
@@ -196,7 +209,7 @@ class KernelTimer(_CallPatch):
             e.record(torch.cuda.current_stream())
             fl, by = WORK[name](args) if name in WORK else (0.0, 0.0)
             shape = tuple(args[:5]) if name == 'rs_gemm_f32' else None
-            self.records.append((name, s, e, fl, by, shape))
+            self.records.append((entry_key(name, args), s, e, fl, by, shape))
             return rc
 
         self._install(timed)
