@@ -350,6 +350,18 @@ def main():
                               'bytes_per_launch': round(g['bytes'] / g['launches']),
                               'avg_launch_ms': round(g['ms'] / g['launches'], 4)}
 
+    # the batch similarity (U I^T inside the fused in-batch CE) against the bf16 MFMA peak
+    # (north_star: MFMA utilisation on the batch-dot)
+    batch_dot = {}
+    for k in ('rs_inbatch_ce_fused_fwd', 'rs_inbatch_ce_fused_bwd'):
+        if k in summ and summ[k]['ms'] > 0:
+            g = summ[k]
+            tf = g['flops'] / (g['ms'] * 1e-3) / 1e12
+            batch_dot[k] = {'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
+                            'frac': round(tf / PEAK_BF16_TFLOPS, 4),
+                            'flops_per_launch': round(g['flops'] / g['launches']),
+                            'avg_launch_ms': round(g['ms'] / g['launches'], 4)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, args.cpu_baseline_seconds)
@@ -374,6 +386,7 @@ def main():
                        'hard_negatives': args.hard_negatives},
             'roofline': roof,
             'gather_roofline': gather_roof,
+            'batch_dot_roofline': batch_dot or None,
             'step_roofline': step_roof,
             'cpu_baseline': cpu,
             'kernel_ms_per_step': {k: round(v['ms'] / 3, 4) for k, v in sorted(summ.items(), key=lambda kv: -kv[1]['ms'])},

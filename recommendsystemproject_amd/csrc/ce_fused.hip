@@ -34,6 +34,8 @@ constexpr int kOwnW = 32;    // owned rows per wave
 constexpr int kWaves = 4;    // owned rows per workgroup: 128
 constexpr int kTile = 32;    // streamed rows per tile
 constexpr float kMasked = -1e9f;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
 
 struct HStrideArgs {
   int64_t row, slot;  // hard-negative H element (i, n, c) at i*row + n*slot + c
@@ -72,14 +74,30 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* lo, const __bf16* hi) {
 // MODE 0: forward statistics (own = U, str = I)
 // MODE 1: dU (own = U, str = I; lse of the owned user)
 // MODE 2: dI (own = I, str = U; lse of the streamed user)
+// streamed tiles staged per batch of kBT: one batch's loads are in flight while the previous
+// batch is consumed from the other LDS half. With one tile per stage every tile exposed an L2/MALL
+// round trip (the loop ran at ~3,600 cycles per tile against ~600 of MFMA and exp work). The
+// backward stages kBT / 2 tiles per batch: its gradient accumulators leave no room for a 4-tile
+// register stage at two waves per SIMD.
+constexpr int kBT = 4;
+template <int MODE>
+constexpr int batch_tiles() { return MODE == 0 ? kBT : kBT / 2; }
+
+// v_exp_f32 directly: exp2f() adds a denormal-range fix-up (compare, select, ldexp) per call
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+template <int D>
+struct CeLds {
+  __bf16 Ts[2][kBT * kTile * (D + 8)];
+  int64_t sid[2][kBT * kTile];
+  float slse[2][kBT * kTile];
+};
+
 template <int D, int MODE>
-__device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split) {
+__device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, CeLds<D>& L) {
   constexpr int KS = D / 16;          // 32x32x16 k-steps over the embedding
   constexpr int PT = D + 8;           // LDS pitch (bf16) of a streamed tile row
   constexpr int DB = D / 32;          // 32-wide blocks of the gradient
-  __shared__ __attribute__((aligned(16))) __bf16 Ts[2][kTile * PT];
-  __shared__ __attribute__((aligned(16))) int64_t sid[2][kTile];
-  __shared__ __attribute__((aligned(16))) float slse[2][kTile];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int B = a.B;
@@ -101,62 +119,72 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split) {
     ob[s] = cvt8(x0, x1);
   }
   const int64_t id_o = (a.ids && o_ok) ? a.ids[(int64_t)o * a.id_stride] : 0;
-  float g = 0.f, lse_o = 0.f;
+  const int o_base = blockIdx.x * (kOwnW * kWaves) + __builtin_amdgcn_readfirstlane(wave) * kOwnW;
+  const bool wave_ok = o_base + kOwnW <= B;                           // every owned row valid
+  const float sc2 = a.invT * kLog2e;  // S -> log2-domain logits
+  float g = 0.f, lse2_o = 0.f;
   if constexpr (MODE != 0) {
     g = (a.grad_out ? *a.grad_out : 1.f) / (float)B * a.invT;  // d loss / d S = dlogits / T
-    if constexpr (MODE == 1) lse_o = o_ok ? a.lse[o] : 0.f;
+    if constexpr (MODE == 1) lse2_o = o_ok ? a.lse[o] * kLog2e : 0.f;
   }
-  float run_m = -INFINITY, run_s = 0.f;  // fwd: online statistics of this lane's values
+  float run_m = -INFINITY, run_s = 0.f;  // fwd: online statistics (log2 domain) of this lane's values
   floatx16 gacc[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i)
 #pragma unroll
     for (int e = 0; e < 16; ++e) gacc[i][e] = 0.f;
 
-  // streamed tile staging: 32 rows x D fp32 -> bf16 LDS, float4 per slot. Two register sets
-  // keep the loads of tiles i+1 and i+2 in flight while tile i is consumed (the kernel is short
-  // per tile; with one set every iteration waited for an L2 round trip).
+  // batch staging: kBT tiles of 32 rows x D fp32 -> bf16 LDS, float4 per slot
   constexpr int NTHR = 64 * kWaves;
-  constexpr int SL = kTile * D / 4 / NTHR;  // float4 slots per thread
+  constexpr int SL = kTile * D / 4 / NTHR;  // float4 slots per thread per tile
+  constexpr int BT = batch_tiles<MODE>();   // tiles per batch
+  constexpr int BR = BT * kTile;            // rows per batch
+  static_assert(BR <= NTHR, "one id / lse per thread and batch row");
   struct Stage {
-    floatx4 v[SL];
+    floatx4 v[BT][SL];
     int64_t id;
     float l;
   };
-  Stage RA, RB;
+  Stage R;
   // loads are unconditional (row index clamped to B - 1; rows >= B are masked when consumed):
   // a guarded load would sit in its own branch, and the waitcnt pass then drains vmcnt(0) at the
   // join -- waiting for the prefetch it was meant to overlap
-  auto load_tile = [&](int t0, Stage& R) {
+  auto load_batch = [&](int t0) {
 #pragma unroll
-    for (int i = 0; i < SL; ++i) {
-      const int slot = tid + NTHR * i;
-      const int row = slot / (D / 4), col = (slot % (D / 4)) * 4;
-      const int t = min(t0 + row, B - 1);
-      R.v[i] = *reinterpret_cast<const floatx4*>(a.str + (int64_t)t * D + col);
-    }
-    const int t = min(t0 + (tid & (kTile - 1)), B - 1);
+    for (int k = 0; k < BT; ++k)
+#pragma unroll
+      for (int i = 0; i < SL; ++i) {
+        const int slot = tid + NTHR * i;
+        const int row = slot / (D / 4), col = (slot % (D / 4)) * 4;
+        const int t = min(t0 + k * kTile + row, B - 1);
+        R.v[k][i] = *reinterpret_cast<const floatx4*>(a.str + (int64_t)t * D + col);
+      }
+    const int t = min(t0 + (tid & (BR - 1)), B - 1);
     R.id = a.ids ? a.ids[(int64_t)t * a.id_stride] : 0;
-    if constexpr (MODE == 2) R.l = a.lse[t];
+    if constexpr (MODE == 2) R.l = a.lse[t] * kLog2e;  // staged in the log2 domain
   };
-  auto store_tile = [&](int bf, const Stage& R) {
+  auto store_batch = [&](int hf) {
 #pragma unroll
-    for (int i = 0; i < SL; ++i) {
-      const int slot = tid + NTHR * i;
-      const int row = slot / (D / 4), col = (slot % (D / 4)) * 4;
-      bf16x4 v;
-      v[0] = (__bf16)R.v[i][0]; v[1] = (__bf16)R.v[i][1]; v[2] = (__bf16)R.v[i][2]; v[3] = (__bf16)R.v[i][3];
-      *reinterpret_cast<bf16x4*>(&Ts[bf][row * PT + col]) = v;
-    }
-    if (tid < kTile) {
-      sid[bf][tid] = R.id;
-      if constexpr (MODE == 2) slse[bf][tid] = R.l;
+    for (int k = 0; k < BT; ++k)
+#pragma unroll
+      for (int i = 0; i < SL; ++i) {
+        const int slot = tid + NTHR * i;
+        const int row = k * kTile + slot / (D / 4), col = (slot % (D / 4)) * 4;
+        bf16x4 v;
+        v[0] = (__bf16)R.v[k][i][0]; v[1] = (__bf16)R.v[k][i][1];
+        v[2] = (__bf16)R.v[k][i][2]; v[3] = (__bf16)R.v[k][i][3];
+        *reinterpret_cast<bf16x4*>(&L.Ts[hf][row * PT + col]) = v;
+      }
+    if (tid < BR) {
+      L.sid[hf][tid] = R.id;
+      if constexpr (MODE == 2) L.slse[hf][tid] = R.l;
     }
   };
   float dg = 0.f;  // fwd: S_oo / T, captured by the lane that meets the diagonal
   bool has_dg = false;
-  auto consume = [&](int buf, int t0) {
-    const __bf16* T = Ts[buf];
+  auto consume = [&](int hf, int k, int t0) {
+    const __bf16* T = &L.Ts[hf][k * kTile * PT];
+    const int64_t* sidk = &L.sid[hf][k * kTile];
     // S^T tile: C[t][o] = str[t] . own[o]; A = streamed rows (lane c: row t0 + c)
     // two accumulator chains (even / odd k-steps) halve the dependent-MFMA latency
     floatx16 acc, acc1;
@@ -171,47 +199,54 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split) {
     }
     acc += acc1;
     // element e of this lane: streamed row t = t0 + 8(e>>2) + 4h + (e&3), owned column o.
-    // The tile's ids (and lse) are read up front as vectors and the masks are selects: a
-    // per-element `if (ids && ...) sid[...]` became a divergent branch with its own LDS
-    // round trip, 16 serialised LDS latencies per tile.
+    // The tile's ids are read up front as vectors and the masks are selects: a per-element
+    // `if (ids && ...) sid[...]` became a divergent branch with its own LDS round trip.
+    // Exponentials run in the log2 domain (one v_exp_f32, the 1/T and log2(e) scales folded
+    // into one multiply). The diagonal (t == o: never masked, the label logit) and the rows past
+    // B sit in a few tiles only: tiles are aligned with the owned 32-row blocks, so the diagonal
+    // lies in the tile with t0 == o_base, and the rows past B in the last tile -- a wave-uniform
+    // test sends those tiles through the exact per-element path and all others skip it (the
+    // epilogue was ~12 VALU operations per element against 1/2 MFMA).
     bool coll[16];
     {
       const bool have_ids = a.ids != nullptr;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
-        const i64x2* sp = reinterpret_cast<const i64x2*>(&sid[buf][8 * g4 + 4 * h]);
+        const i64x2* sp = reinterpret_cast<const i64x2*>(&sidk[8 * g4 + 4 * h]);
         const i64x2 s01 = sp[0], s23 = sp[1];
         const int64_t sv[4] = {s01[0], s01[1], s23[0], s23[1]};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int t = t0 + 8 * g4 + 4 * h + j;
-          coll[4 * g4 + j] = have_ids & (t != o) & (sv[j] == id_o);
-        }
+        for (int j = 0; j < 4; ++j) coll[4 * g4 + j] = have_ids & (sv[j] == id_o);
       }
     }
+    const bool rare = (t0 == o_base) | (t0 + kTile > B) | !wave_ok;  // wave-uniform
     if constexpr (MODE == 0) {
       float v[16];
-      float tm = -INFINITY;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int tl = 8 * (e >> 2) + 4 * h + (e & 3);
-        const int t = t0 + tl;
-        float x = acc[e] * a.invT;
-        const bool diag = t == o;
-        dg = diag ? x : dg;
-        has_dg = has_dg | diag;
-        x = coll[e] ? kMasked : x;
-        x = t >= B ? -INFINITY : x;
-        v[e] = x;
-        tm = fmaxf(tm, x);
+      for (int e = 0; e < 16; ++e) v[e] = coll[e] ? kMasked : acc[e] * sc2;
+      if (rare) {
+        asm volatile("" ::: "memory");  // keep the branch: if-converted, every tile paid for it
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int t = t0 + 8 * (e >> 2) + 4 * h + (e & 3);
+          if (t == o) {
+            v[e] = acc[e] * sc2;
+            dg = acc[e] * a.invT;
+            has_dg = true;
+          }
+          if (t >= B) v[e] = -INFINITY;
+        }
       }
+      float tm = fmaxf(fmaxf(v[0], v[1]), v[2]);
+#pragma unroll
+      for (int e = 3; e < 16; e += 2) tm = fmaxf(fmaxf(tm, v[e]), e + 1 < 16 ? v[e + 1] : v[e]);
       const float nm = fmaxf(run_m, tm);
       if (nm != -INFINITY) {  // a lane may see only padding rows (t >= B) so far
         float ss = 0.f;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) ss += __expf(v[e] - nm);
-        run_s = (run_m == -INFINITY ? 0.f : run_s * __expf(run_m - nm)) + ss;
+        for (int e = 0; e < 16; ++e) ss += fast_exp2(v[e] - nm);
+        run_s = (run_m == -INFINITY ? 0.f : run_s * fast_exp2(run_m - nm)) + ss;
         run_m = nm;
       }
     } else {
@@ -221,21 +256,30 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split) {
       if constexpr (MODE == 2) {
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const floatx4 l4 = *reinterpret_cast<const floatx4*>(&slse[buf][8 * g4 + 4 * h]);
+          const floatx4 l4 = *reinterpret_cast<const floatx4*>(&L.slse[hf][k * kTile + 8 * g4 + 4 * h]);
 #pragma unroll
           for (int j = 0; j < 4; ++j) lt[4 * g4 + j] = l4[j];
         }
       }
+      float dv[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int tl = 8 * (e >> 2) + 4 * h + (e & 3);
-        const int t = t0 + tl;
-        const float x = acc[e] * a.invT;
-        const float l = MODE == 1 ? lse_o : lt[e];
-        const float p = coll[e] ? 0.f : __expf(x - l);  // collision: logit -1e9, P = 0
-        const float dv = (t >= B || !o_ok) ? 0.f : g * (p - (t == o ? 1.f : 0.f));
-        xf[e >> 3][e & 7] = (__bf16)dv;
+        const float l2 = MODE == 1 ? lse2_o : lt[e];  // log2-domain log-sum-exp
+        const float p = coll[e] ? 0.f : fast_exp2(acc[e] * sc2 - l2);  // collision: logit -1e9, P = 0
+        dv[e] = g * p;
       }
+      if (rare) {
+        asm volatile("" ::: "memory");  // keep the branch (see MODE 0)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int t = t0 + 8 * (e >> 2) + 4 * h + (e & 3);
+          const float l2 = MODE == 1 ? lse2_o : lt[e];
+          if (t == o) dv[e] = g * (fast_exp2(acc[e] * sc2 - l2) - 1.f);
+          if (t >= B || !o_ok) dv[e] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) xf[e >> 3][e & 7] = (__bf16)dv[e];
       // grad^T[d][o] += sum_t str^T[d][t] dS^T[t][o]: A = transposed streamed tile,
       // element j of lane half h <-> tile row 16 kstep + 8 (j>>2) + 4 h + (j&3)
       const int g16 = lane >> 4, lq = (lane & 15) >> 2, lp = lane & 3;
@@ -253,25 +297,25 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split) {
   };
 
   const int ntiles = t_begin < t_end ? (t_end - t_begin + kTile - 1) / kTile : 0;
+  const int nb = (ntiles + BT - 1) / BT;
   if (ntiles > 0) {
-    load_tile(t_begin, RA);
-    store_tile(0, RA);
-    load_tile(t_begin + kTile, RA);
-    load_tile(t_begin + 2 * kTile, RB);
+    load_batch(t_begin);
+    store_batch(0);
+    if (nb > 1) load_batch(t_begin + BR);
   }
   __syncthreads();
-  // two tiles per trip so the register sets are fixed: tile it+1 waits in RA, it+2 in RB
-  for (int it = 0; it < ntiles; it += 2) {
-    const int t0 = t_begin + it * kTile;
-    consume(0, t0);
-    store_tile(1, RA);
-    load_tile(t0 + 3 * kTile, RA);
-    __syncthreads();
-    if (it + 1 >= ntiles) break;
-    consume(1, t0 + kTile);
-    store_tile(0, RB);
-    load_tile(t0 + 4 * kTile, RB);
-    __syncthreads();
+  // batch b sits in half b & 1; batch b + 1's loads fly while it is consumed
+  for (int b = 0; b < nb; ++b) {
+    const int hf = b & 1;
+    const int t0 = t_begin + b * BR;
+    const int nt = min(BT, ntiles - b * BT);
+#pragma unroll 1
+    for (int k = 0; k < nt; ++k) consume(hf, k, t0 + k * kTile);
+    if (b + 1 < nb) {
+      store_batch(hf ^ 1);
+      if (b + 2 < nb) load_batch(t0 + 2 * BR);
+      __syncthreads();
+    }
   }
   if constexpr (MODE == 0) {
     if (has_dg && o_ok) a.diag[o] = dg;
@@ -281,10 +325,10 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split) {
     const float om = __shfl_xor(run_m, 32, 64), os = __shfl_xor(run_s, 32, 64);
     const float nm = fmaxf(run_m, om);
     const float ns = (nm == -INFINITY) ? 0.f
-                                       : (run_m == -INFINITY ? 0.f : run_s * __expf(run_m - nm)) +
-                                             (om == -INFINITY ? 0.f : os * __expf(om - nm));
+                                       : (run_m == -INFINITY ? 0.f : run_s * fast_exp2(run_m - nm)) +
+                                             (om == -INFINITY ? 0.f : os * fast_exp2(om - nm));
     if (h == 0 && o_ok) {
-      a.part_m[(int64_t)split * B + o] = nm;
+      a.part_m[(int64_t)split * B + o] = nm * kLn2;  // back to natural units for ce_finish
       a.part_s[(int64_t)split * B + o] = ns;
     }
   } else {
@@ -303,16 +347,18 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split) {
 }
 
 template <int D, int MODE>
-__global__ __launch_bounds__(64 * kWaves) void ce_tile_kernel(CeArgs a) {
-  ce_tile_body<D, MODE>(a, blockIdx.y);
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(2))) void ce_tile_kernel(CeArgs a) {
+  __shared__ __attribute__((aligned(16))) CeLds<D> lds;
+  ce_tile_body<D, MODE>(a, blockIdx.y, lds);
 }
 
 // dU and dI in one launch (blockIdx.z): the two halves are independent given lse, and 1,024
 // workgroups hide each other's tile latencies better than two back-to-back 512-workgroup grids
 template <int D>
-__global__ __launch_bounds__(64 * kWaves) void ce_bwd_pair_kernel(CeArgs aU, CeArgs aI) {
-  if (blockIdx.z == 0) ce_tile_body<D, 1>(aU, blockIdx.y);
-  else ce_tile_body<D, 2>(aI, blockIdx.y);
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(2))) void ce_bwd_pair_kernel(CeArgs aU, CeArgs aI) {
+  __shared__ __attribute__((aligned(16))) CeLds<D> lds;  // one image shared by both halves
+  if (blockIdx.z == 0) ce_tile_body<D, 1>(aU, blockIdx.y, lds);
+  else ce_tile_body<D, 2>(aI, blockIdx.y, lds);
 }
 
 // per user row: merge the split statistics with the hard-negative logits -> lse, row loss
@@ -396,9 +442,14 @@ __global__ void ce_reduce_kernel(const float* __restrict__ part, int NS, int64_t
   *reinterpret_cast<floatx4*>(dst + i) = acc;
 }
 
-int splits_for(int B) {
+// Column splits. Forward: ~2 workgroups per CU (512 at B = 4096), each wave latency-bound on its
+// tile epilogue, so more waves win. Backward: half as many (256 workgroups per direction): every
+// split writes a [B, D] fp32 partial that ce_reduce reads back, 8 MB per split at D = 128
+// (measured at B = 4096: 16 splits 57 us, 8 splits 46 us, 4 splits 53 us).
+int splits_for(int B, bool bwd) {
   const int blocks = cdiv(B, kOwnW * kWaves);
-  int ns = cdiv(512, blocks);  // two workgroups per CU: the waves hide each other's latency
+  int ns = cdiv(bwd ? 256 : 512, blocks);
+  if (const char* e = getenv("RSYS_CE_SPLITS")) ns = atoi(e) > 0 ? atoi(e) : ns;  // tuning only
   const int max_ns = cdiv(B, kTile);
   if (ns > max_ns) ns = max_ns;
   if (ns > 64) ns = 64;  // ce_finish reads the partials with one lane each
@@ -419,9 +470,8 @@ int launch_tiles(const CeArgs& a, int D, int NS, hipStream_t st) {
 using namespace rs;
 
 extern "C" int64_t rs_inbatch_ce_fused_ws_bytes(int B, int D) {
-  const int NS = splits_for(B);
-  const int64_t fwd = (int64_t)NS * B * 2 + B;
-  const int64_t bwd = (int64_t)2 * NS * B * D;  // dU and dI partials side by side
+  const int64_t fwd = (int64_t)splits_for(B, false) * B * 2 + B;
+  const int64_t bwd = (int64_t)2 * splits_for(B, true) * B * D;  // dU and dI partials side by side
   return (fwd > bwd ? fwd : bwd) * (int64_t)sizeof(float);
 }
 
@@ -436,7 +486,7 @@ extern "C" int rs_inbatch_ce_fused_fwd(const float* U, const float* I, const flo
   RS_CHECK_ARG(N == 0 || Hn, "rs_inbatch_ce_fused_fwd: hard negatives need H");
   RS_CHECK_ARG(aligned16(U) && aligned16(I), "rs_inbatch_ce_fused_fwd: U, I must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
-  const int NS = splits_for(B);
+  const int NS = splits_for(B, false);
   CeArgs a{};
   a.own = U; a.str = I; a.B = B; a.invT = 1.f / T; a.ids = item_ids; a.id_stride = id_stride;
   a.split_rows = cdiv(cdiv(B, NS), kTile) * kTile;
@@ -462,7 +512,7 @@ extern "C" int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const flo
   RS_CHECK_ARG(aligned16(U) && aligned16(I) && aligned16(dU) && aligned16(dI),
                "rs_inbatch_ce_fused_bwd: operands must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
-  const int NS = splits_for(B);
+  const int NS = splits_for(B, true);
   CeArgs a{};
   a.B = B; a.invT = 1.f / T; a.ids = item_ids; a.id_stride = id_stride; a.lse = lse; a.grad_out = grad_out;
   a.split_rows = cdiv(cdiv(B, NS), kTile) * kTile;

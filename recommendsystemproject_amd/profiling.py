@@ -105,7 +105,17 @@ def _ce_work(a, bwd=False):
     return 0.0, 4.0 * B * B * 2  # fwd: two passes over S; bwd: S read + dS written
 
 
+def _ce_fused_work(a, bwd=False):
+    B, D = a[7], a[9]
+    # forward: S = U I^T on the MFMA (one pass, never stored); backward: S recomputed in the dU
+    # and the dI halves, then dU = dS I and dI = dS^T U. Bytes: U, I read (+ partial gradients
+    # written and reduced in the backward: 2 directions x splits x B x D fp32, not counted).
+    return (8.0 if bwd else 2.0) * B * B * D, 4.0 * 2 * B * D * (2 if bwd else 1)
+
+
 WORK = {
+    'rs_inbatch_ce_fused_fwd': _ce_fused_work,
+    'rs_inbatch_ce_fused_bwd': lambda a: _ce_fused_work(a, True),
     'rs_gemm_add_layernorm': _gemm_ln_work,
     'rs_ffn_fwd_bf16': _ffn_fwd_work,
     'rs_ffn_bwd_bf16': _ffn_bwd_work,

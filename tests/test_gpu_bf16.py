@@ -369,6 +369,14 @@ def test_fused_inbatch_ce(B, D, N, coll, bf16_mode):
         assert (a - b_).abs().max().item() < 2e-2 * sc, ((a - b_).abs().max().item(), sc)
 
 
+@pytest.mark.parametrize('B,splits', [(4096, 3), (4096, 5), (2000, 2), (777, 1)])
+def test_fused_inbatch_ce_ragged_batches(B, splits, bf16_mode, monkeypatch):
+    """Column splits whose tile count is not a multiple of the staged batch (4 tiles forward, 2
+    backward), odd batch counts, and a last split shorter than the others."""
+    monkeypatch.setenv('RSYS_CE_SPLITS', str(splits))
+    test_fused_inbatch_ce(B, 128, 0, True, bf16_mode)
+
+
 def test_fused_ce_deterministic(bf16_mode):
     from recommendsystemproject_amd.functions import InBatchLossFn
     B, D = 4096, 128

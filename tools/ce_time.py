@@ -1,0 +1,74 @@
+"""Time the fused in-batch CE forward / backward entry points (bf16 compute mode) with HIP events
+on the launch stream, and report MFMA utilisation of the batch dot.
+
+    RSYS_CE_SPLITS=8 python tools/ce_time.py [B] [D] [iters]
+"""
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from recommendsystemproject_amd import _hip, ops  # noqa: E402
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    D = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+    n = int(sys.argv[3]) if len(sys.argv) > 3 else 50
+    dev = torch.device('cuda:0')
+    g = torch.Generator(device=dev).manual_seed(0)
+    U = F.normalize(torch.randn(B, D, device=dev, generator=g), dim=1)
+    I = F.normalize(torch.randn(B, D, device=dev, generator=g), dim=1)
+    ids = torch.randint(0, 3000, (B,), device=dev, generator=g)
+    lse = torch.empty(B, device=dev)
+    row_loss = torch.empty(B, device=dev)
+    loss = torch.empty((), device=dev)
+    dU, dI = torch.empty_like(U), torch.empty_like(I)
+    w = ops.ws(_hip.lib().rs_inbatch_ce_fused_ws_bytes(B, D), dev)
+    st = ops.stream()
+
+    def fwd():
+        _hip.call('rs_inbatch_ce_fused_fwd', U.data_ptr(), I.data_ptr(), None, 0, 0, ids.data_ptr(), 1,
+                  B, 0, D, 0.15, lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(), w.data_ptr(), st)
+
+    def bwd():
+        _hip.call('rs_inbatch_ce_fused_bwd', U.data_ptr(), I.data_ptr(), None, 0, 0, ids.data_ptr(), 1,
+                  B, 0, D, 0.15, lse.data_ptr(), None, dU.data_ptr(), dI.data_ptr(), None, w.data_ptr(), st)
+
+    fwd()
+    bwd()
+    torch.cuda.synchronize()
+    # reference on the same bf16-rounded operands
+    Ub, Ib = U.bfloat16().float(), I.bfloat16().float()
+    S = Ub @ Ib.T / 0.15
+    coll = (ids[:, None] == ids[None, :]) & ~torch.eye(B, dtype=torch.bool, device=dev)
+    S = S.masked_fill(coll, -1e9)
+    ref_loss = F.cross_entropy(S, torch.arange(B, device=dev))
+    P = torch.softmax(S, 1)
+    dS = (P - torch.eye(B, device=dev)) / B / 0.15
+    err_u = float((dS @ Ib - dU).abs().max() / (dS @ Ib).abs().max())
+    err_i = float((dS.T @ Ub - dI).abs().max() / (dS.T @ Ub).abs().max())
+    torch.cuda._sleep(int(2.4e9 * 0.01))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev[0].record()
+    for _ in range(n):
+        fwd()
+    ev[1].record()
+    for _ in range(n):
+        bwd()
+    ev[2].record()
+    torch.cuda.synchronize()
+    tf = ev[0].elapsed_time(ev[1]) / n * 1e3
+    tb = ev[1].elapsed_time(ev[2]) / n * 1e3
+    fl = 2.0 * B * B * D
+    print(json.dumps({'splits': os.environ.get('RSYS_CE_SPLITS', 'auto'), 'B': B, 'D': D,
+                      'fwd_us': round(tf, 1), 'bwd_us': round(tb, 1),
+                      'fwd_tflops': round(fl / tf / 1e6, 1), 'bwd_tflops': round(4 * fl / tb / 1e6, 1),
+                      'loss_err': abs(float(loss) - float(ref_loss)), 'dU_err': err_u, 'dI_err': err_i}))
+
+
+if __name__ == '__main__':
+    main()
