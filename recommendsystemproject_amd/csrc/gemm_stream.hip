@@ -1099,6 +1099,7 @@ bool wgrad_instance(int M, int N) {
   switch (mo_pad * 1000 + no_pad) {
     case 64064: case 64256: case 256064: case 192064: case 64192: case 128128: case 128064:
     case 64128: case 32064: case 64032: case 128256: case 256128: case 64096: case 96064:
+    case 256192:  // the user tower's first Linear (172 inputs): generic split-K GEMM + reduce was 32 us
       return true;
     default: return false;
   }
@@ -1136,7 +1137,7 @@ int wgrad_bf16_launch(const StreamArgs& s, bool y_bf16, bool x_bf16, hipStream_t
     RS_WB(192, 64, false, false) RS_WB(64, 192, false, false) RS_WB(128, 128, false, false)
     RS_WB(128, 64, false, false) RS_WB(64, 128, false, false) RS_WB(32, 64, false, false)
     RS_WB(64, 32, false, false) RS_WB(128, 256, false, false) RS_WB(256, 128, false, false)
-    RS_WB(64, 96, false, false) RS_WB(96, 64, false, false)
+    RS_WB(64, 96, false, false) RS_WB(96, 64, false, false) RS_WB(256, 192, false, false)
     RS_WB(64, 256, false, true) RS_WB(256, 64, true, false)  // the fused FFN's weight gradients
     RS_WB(192, 64, true, false)  // in_proj from the bf16 dqkv (RS_ATTN_QKV_BF16)
     default:
@@ -1166,7 +1167,7 @@ int wgrad_launch(const StreamArgs& s, hipStream_t st) {
   switch (mo_pad * 1000 + no_pad) {
     RS_WG(64, 64) RS_WG(64, 256) RS_WG(256, 64) RS_WG(192, 64) RS_WG(64, 192) RS_WG(128, 128)
     RS_WG(128, 64) RS_WG(64, 128) RS_WG(32, 64) RS_WG(64, 32) RS_WG(128, 256) RS_WG(256, 128)
-    RS_WG(64, 96) RS_WG(96, 64)
+    RS_WG(64, 96) RS_WG(96, 64) RS_WG(256, 192)
     default: set_error("wgrad: no instance for %dx%d", s.M, s.N); return -1;
   }
 #undef RS_WG

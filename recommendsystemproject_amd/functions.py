@@ -187,16 +187,21 @@ def layer_fwd_last(lyr, x, key_pad, last, B, L, d, H, p, key, site):
 
 
 _WGRAD_STREAMS = {}
+_JOIN_QUEUED = set()  # side streams whose end-of-backward join is queued
 
 
-def _wgrad_side(fn, *reads):
+def _wgrad_side(fn, *reads, env='RSYS_WGRAD_STREAM', default='0'):
     """Run fn (weight-gradient GEMMs: they feed parameter gradients only) on a second stream,
-    beside the encoder backward's input-gradient chain (its critical path). The tensors fn reads
-    are recorded on that stream (their memory is not reused until it is done); the caller must not
-    modify them in place afterwards, and SeqEncoderFn.backward joins the stream at its end.
-    Off by default (RSYS_WGRAD_STREAM=1 enables it): measured at C2, the weight gradients compete
-    with the HBM-bound input-gradient kernels and the step got slower (1.877 -> 1.972 ms)."""
-    if os.environ.get('RSYS_WGRAD_STREAM', '0') != '1':
+    beside the backward's input-gradient chain (its critical path). The tensors fn reads are
+    recorded on that stream (their memory is not reused until it is done); the caller must not
+    modify them in place afterwards. SeqEncoderFn.backward joins the stream at its end, and the
+    current stream joins it once more when the whole backward is done (autograd callback).
+    Encoder: off by default (RSYS_WGRAD_STREAM=1 enables it): measured at C2, the weight gradients
+    compete with the HBM-bound input-gradient kernels and the step got slower (1.877 -> 1.972 ms).
+    DSSM towers (RSYS_TOWER_WGRAD_STREAM=1): at B = 4096 every tower kernel is a small,
+    latency-bound grid, but a third stream in the graph made the C2 step slower too (1.82 -> 1.945
+    ms, A/B on one box): off by default."""
+    if os.environ.get(env, default) != '1':
         fn()
         return
     cur = torch.cuda.current_stream()
@@ -209,6 +214,17 @@ def _wgrad_side(fn, *reads):
     for t in reads:
         if t is not None:
             t.record_stream(s)
+    if s not in _JOIN_QUEUED:
+        _JOIN_QUEUED.add(s)
+
+        def _join_at_end():
+            _JOIN_QUEUED.discard(s)
+            _wgrad_join()
+
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(_join_at_end)
+        except RuntimeError:  # called outside an autograd backward: join right away
+            _join_at_end()
 
 
 def _wgrad_join():
@@ -528,6 +544,12 @@ class BatchNormFn(torch.autograd.Function):
 
 
 # ================================================================================ MLP tower
+def _tower_wgrad(dz, h, lin):
+    """dW += dz^T h, db += colsum(dz) of one tower Linear, beside the input-gradient chain."""
+    _wgrad_side(lambda: ops.linear_bwd_weight(dz, h, grad_of(lin.weight), db=grad_of(lin.bias)), dz, h,
+                env='RSYS_TOWER_WGRAD_STREAM', default='0')
+
+
 class MLPFn(torch.autograd.Function):
     """MLP_Tower.forward (Tower.py:16-41): [Linear -> BatchNorm1d -> ReLU -> Dropout] x n,
     Linear, F.normalize(p=2, dim=1)."""
@@ -566,7 +588,7 @@ class MLPFn(torch.autograd.Function):
         g = grad_of
         last = seq[len(seq) - 1]
         dz = ops.l2norm_bwd(ctx.out, ctx.norm, dout.contiguous())
-        ops.linear_bwd_weight(dz, ctx.h_last, g(last.weight), db=g(last.bias))
+        _tower_wgrad(dz, ctx.h_last, last)
         dh = ops.linear_bwd_input(dz, last.weight)
         for j in reversed(range(len(ctx.saved))):
             h, z, y, mean, rstd = ctx.saved[j]
@@ -575,7 +597,7 @@ class MLPFn(torch.autograd.Function):
             # backward is a scale on the same mask (fused into the BN backward)
             dz = ops.batchnorm_bwd(z, y, dh, bn.weight, mean, rstd, g(bn.weight), g(bn.bias), ctx.G,
                                    relu=True, drop_p=ctx.p)
-            ops.linear_bwd_weight(dz, h, g(lin.weight), db=g(lin.bias))
+            _tower_wgrad(dz, h, lin)
             dh = ops.linear_bwd_input(dz, lin.weight)
         ctx.saved = None
         return (None, None, dh, None) + (None,) * (len(ctx.needs_input_grad) - 4)

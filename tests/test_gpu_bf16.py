@@ -122,7 +122,7 @@ def test_bf16_training_step_close_to_fp32():
 
 @pytest.mark.parametrize('Mo,No', [(64, 64), (64, 256), (256, 64), (192, 64), (64, 192), (128, 128),
                                    (128, 64), (64, 128), (32, 64), (64, 32), (128, 256), (256, 128),
-                                   (64, 96), (96, 64), (60, 72)])
+                                   (64, 96), (96, 64), (60, 72), (256, 192), (256, 172)])
 def test_bf16_wgrad(Mo, No, bf16_mode):
     """dW = dY^T X on bf16 MFMA (operands rounded to bf16, fp32 accumulate); the fused bias
     gradient colsum(dY) stays fp32-exact; beta accumulate; ragged row tail; deterministic."""

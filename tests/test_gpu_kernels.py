@@ -64,7 +64,8 @@ def test_gemm_epilogues_and_split(M, N, K):
         assert torch.allclose(rs, dy.sum(0), atol=1e-3 * max(1, M / 1000), rtol=1e-5), split
 
 
-@pytest.mark.parametrize('Mo,No', [(64, 64), (64, 256), (256, 64), (192, 64), (64, 40), (128, 128), (64, 72), (80, 64), (64, 100)])
+@pytest.mark.parametrize('Mo,No', [(64, 64), (64, 256), (256, 64), (192, 64), (64, 40), (128, 128), (64, 72), (80, 64), (64, 100),
+                                   (256, 192), (256, 172)])
 def test_wgrad_streaming_kernel(Mo, No):
     """dW = dY^T X over a long M (wgrad path) incl. fused bias sums, beta accumulate, ragged tail."""
     M = 20000 + 37
