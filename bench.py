@@ -103,9 +103,37 @@ def load_traffic(args, B, entry):
     return out
 
 
+CPU_VOCAB_CAP = 10_000_000  # host-memory bound of the CPU baseline's tables (C5: 100M rows)
+
+
+def _cap_vocab(cfg, cap):
+    """cfg with every table capped at `cap` rows (ids are drawn within the vocab, so the sample
+    stays well-formed); returns (cfg, capped?)."""
+    import copy
+    cfg = copy.deepcopy(cfg)
+    capped = False
+
+    def walk(o):
+        nonlocal capped
+        if isinstance(o, dict):
+            if isinstance(o.get('vocab_size'), int) and o['vocab_size'] > cap:
+                o['vocab_size'] = cap
+                capped = True
+            for v in o.values():
+                walk(v)
+        elif isinstance(o, list):
+            for v in o:
+                walk(v)
+    walk(cfg)
+    return cfg, capped
+
+
 def cpu_baseline(cfg, seconds):
-    """The oracle (CPU restatement of the reference step, fp32) on a bounded sample."""
+    """The oracle (CPU restatement of the reference step, fp32) on a bounded sample. Tables above
+    CPU_VOCAB_CAP rows are capped (the oracle's dense Adam over a 100M x 64 table and its state
+    exceed the box's host-memory limit); the sample says so."""
     from oracle.twotower_oracle import OracleTrainer, model_state_shapes
+    cfg, capped = _cap_vocab(cfg, CPU_VOCAB_CAP)
     maps = {'user': synth.tower_layout(cfg['two_tower']['user_tower']),
             'item': synth.tower_layout(cfg['two_tower']['item_tower'])}
     shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
@@ -131,7 +159,8 @@ def cpu_baseline(cfg, seconds):
         pass
     return {'value': round(n * B / el, 1), 'unit': 'samples/s', 'cores': torch.get_num_threads(),
             'kind': 'port', 'sample': f'{n} steps x batch {B} of the same config (oracle, fp32, '
-                                      f'dropout as configured), {el:.1f} s',
+                                      f'dropout as configured), {el:.1f} s' +
+                                      (f'; tables capped at {CPU_VOCAB_CAP:,} rows (host memory)' if capped else ''),
             'nproc': os.cpu_count(), 'cpu_model': model}
 
 

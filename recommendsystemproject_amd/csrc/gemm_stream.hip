@@ -200,6 +200,37 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
   extern __shared__ __attribute__((aligned(16))) float Bs[];  // [NT*16][KP]
   const int tid = threadIdx.x;
   const int nb0 = blockIdx.y * NT * 16;  // this workgroup's column slice (small-M N split)
+  // the first row group's A loads are issued before the weight staging: the two global
+  // latencies overlap instead of adding up (small-M grids run one or two row groups per wave)
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int groups = (a.M + 16 * RG - 1) / (16 * RG);
+  DropKey ka{}, kb{};
+  if (a.epi & RS_EPI_DROP_A) ka = make_key(a.drop_key, a.site_a, a.drop_p);
+  if (a.epi & RS_EPI_DROP_B) kb = make_key(a.drop_key, a.site_b, a.drop_p);
+  const int stride = gridDim.x * 8;
+  int g = blockIdx.x * 8 + wave;
+  floatx4 areg[RG][KT];
+  // FULL (specialised instances): M % 16 == 0 and K == KT*16, so no row / k guards and no
+  // uniform branches in the loop body -- the waitcnt pass can then count the outstanding
+  // stores exactly instead of draining vmcnt(0) (which also waited for the prefetch)
+  constexpr bool FULL = EPI >= 0;
+  auto load_group = [&](int gg, floatx4 (*dst)[KT]) {
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) {
+      const int m = (gg * RG + rg) * 16 + r;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const int k = 16 * t + 4 * q;
+        floatx4 v = {0.f, 0.f, 0.f, 0.f};
+        // explicit global address space: a flat load would also count against lgkmcnt
+        if (FULL || (m < a.M && k < a.K))
+          v = *(const __attribute__((address_space(1))) floatx4*)(a.A + (int64_t)m * a.lda + k);
+        dst[rg][t] = v;
+      }
+    }
+  };
+  if (g < groups) load_group(g, areg);
   // stage op(B)[:, nb0 : nb0 + NT*16] as Bs[n][k], zero padded to NT*16 x KT*16
   // batched 16-byte loads (dispatch: K % 4 == 0; [K][N] weights also need N % 4 == 0)
   if (a.ldb % 4 == 0 && ((uintptr_t)a.B & 15) == 0 && (a.transB || a.N % 4 == 0)) {
@@ -252,35 +283,6 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
   }
   __syncthreads();
 
-  const int lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 15, q = lane >> 4;
-  const int groups = (a.M + 16 * RG - 1) / (16 * RG);
-  DropKey ka{}, kb{};
-  if (a.epi & RS_EPI_DROP_A) ka = make_key(a.drop_key, a.site_a, a.drop_p);
-  if (a.epi & RS_EPI_DROP_B) kb = make_key(a.drop_key, a.site_b, a.drop_p);
-  const int stride = gridDim.x * 8;
-  int g = blockIdx.x * 8 + wave;
-  floatx4 areg[RG][KT];
-  // FULL (specialised instances): M % 16 == 0 and K == KT*16, so no row / k guards and no
-  // uniform branches in the loop body -- the waitcnt pass can then count the outstanding
-  // stores exactly instead of draining vmcnt(0) (which also waited for the prefetch)
-  constexpr bool FULL = EPI >= 0;
-  auto load_group = [&](int gg, floatx4 (*dst)[KT]) {
-#pragma unroll
-    for (int rg = 0; rg < RG; ++rg) {
-      const int m = (gg * RG + rg) * 16 + r;
-#pragma unroll
-      for (int t = 0; t < KT; ++t) {
-        const int k = 16 * t + 4 * q;
-        floatx4 v = {0.f, 0.f, 0.f, 0.f};
-        // explicit global address space: a flat load would also count against lgkmcnt
-        if (FULL || (m < a.M && k < a.K))
-          v = *(const __attribute__((address_space(1))) floatx4*)(a.A + (int64_t)m * a.lda + k);
-        dst[rg][t] = v;
-      }
-    }
-  };
-  if (g < groups) load_group(g, areg);
   floatx4 lnacc[LN ? RG : 1][LN ? NT : 1];
   for (; g < groups; g += stride) {
     floatx4 lnres[LN ? RG : 1][LN ? NT : 1];

@@ -374,6 +374,15 @@ __global__ __launch_bounds__(256) void bn_fwd_norm_kernel(
   const int g = blockIdx.y, s = blockIdx.z;
   const double n = (double)Bg;
   double A, Bv;
+  // this block's first kBnU rows are loaded before the statistics are reduced from the partials:
+  // the two global latencies overlap (one row batch per thread at the usual 64-row chunks)
+  const int rpc = (Bg + S - 1) / S;
+  const int r1 = min(Bg, (s + 1) * rpc);
+  const int i_first = s * rpc + rl;
+  const int cc = min(c, C - 1);
+  float xv[kBnU];
+#pragma unroll
+  for (int u = 0; u < kBnU; ++u) xv[u] = x[((int64_t)g * Bg + min(i_first + 4 * u, r1 - 1)) * C + cc];
   if (g == 0 && s == 0 && running_mean) {
     if (blockIdx.x == 0 && threadIdx.x == 0 && num_batches) *num_batches += G;
     for (int gg = 0; gg < G; ++gg) {
@@ -401,15 +410,14 @@ __global__ __launch_bounds__(256) void bn_fwd_norm_kernel(
     rstd[g * C + c] = r;
   }
   const float wc = w[c], bc = b[c];
-  const int rpc = (Bg + S - 1) / S;
-  const int r1 = min(Bg, (s + 1) * rpc);
   DropKey dk{};
   const bool drop = drop_p > 0.f;
   if (drop) dk = make_key(key, site, drop_p);
-  for (int i0 = s * rpc + rl; i0 < r1; i0 += 4 * kBnU) {
-    float xv[kBnU];
+  for (int i0 = i_first; i0 < r1; i0 += 4 * kBnU) {
+    if (i0 != i_first) {
 #pragma unroll
-    for (int u = 0; u < kBnU; ++u) xv[u] = x[((int64_t)g * Bg + min(i0 + 4 * u, r1 - 1)) * C + c];
+      for (int u = 0; u < kBnU; ++u) xv[u] = x[((int64_t)g * Bg + min(i0 + 4 * u, r1 - 1)) * C + c];
+    }
 #pragma unroll
     for (int u = 0; u < kBnU; ++u) {
       if (i0 + 4 * u >= r1) break;
@@ -434,6 +442,19 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(
   const int c = blockIdx.x * 64 + cl;
   const int g = blockIdx.y, s = blockIdx.z;
   double A, Bv;
+  // first row batch loaded before the statistics (see bn_fwd_norm_kernel)
+  const int rpc = (Bg + S - 1) / S;
+  const int r1 = min(Bg, (s + 1) * rpc);
+  const int i_first = s * rpc + rl;
+  const int cc = min(c, C - 1);
+  float xv[kBnU], dv[kBnU], yv[kBnU];
+#pragma unroll
+  for (int u = 0; u < kBnU; ++u) {
+    const int64_t o = ((int64_t)g * Bg + min(i_first + 4 * u, r1 - 1)) * C + cc;
+    xv[u] = x[o];
+    dv[u] = dy[o];
+    yv[u] = relu ? y[o] : 1.f;
+  }
   if (g == 0 && s == 0) {
     double tw = 0.0, tb = 0.0;
     for (int gg = 0; gg < G; ++gg) {
@@ -450,16 +471,15 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(
   if (c >= C) return;
   const float mdy = (float)(A / Bg), mdyx = (float)(Bv / Bg);
   const float mu = mean[g * C + c], r = rstd[g * C + c], wr = w[c] * r;
-  const int rpc = (Bg + S - 1) / S;
-  const int r1 = min(Bg, (s + 1) * rpc);
-  for (int i0 = s * rpc + rl; i0 < r1; i0 += 4 * kBnU) {
-    float xv[kBnU], dv[kBnU], yv[kBnU];
+  for (int i0 = i_first; i0 < r1; i0 += 4 * kBnU) {
+    if (i0 != i_first) {
 #pragma unroll
-    for (int u = 0; u < kBnU; ++u) {
-      const int64_t o = ((int64_t)g * Bg + min(i0 + 4 * u, r1 - 1)) * C + c;
-      xv[u] = x[o];
-      dv[u] = dy[o];
-      yv[u] = relu ? y[o] : 1.f;
+      for (int u = 0; u < kBnU; ++u) {
+        const int64_t o = ((int64_t)g * Bg + min(i0 + 4 * u, r1 - 1)) * C + c;
+        xv[u] = x[o];
+        dv[u] = dy[o];
+        yv[u] = relu ? y[o] : 1.f;
+      }
     }
 #pragma unroll
     for (int u = 0; u < kBnU; ++u) {
