@@ -211,9 +211,12 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
   const int stride = gridDim.x * 8;
   int g = blockIdx.x * 8 + wave;
   floatx4 areg[RG][KT];
-  // FULL (specialised instances): M % 16 == 0 and K == KT*16, so no row / k guards and no
+  // FULL (specialised instances): M % 16 == 0 and K % 4 == 0, so no row / k guards and no
   // uniform branches in the loop body -- the waitcnt pass can then count the outstanding
-  // stores exactly instead of draining vmcnt(0) (which also waited for the prefetch)
+  // stores exactly instead of draining vmcnt(0) (which also waited for the prefetch). When K is
+  // not a multiple of 16 (the sequence projection, K = 40) the last k tile's out-of-range float4s
+  // re-read the row's last float4 (clamped address): the staged weight is zero for k >= K, so
+  // they contribute exact zeros.
   constexpr bool FULL = EPI >= 0;
   auto load_group = [&](int gg, floatx4 (*dst)[KT]) {
 #pragma unroll
@@ -222,10 +225,11 @@ __global__ __launch_bounds__(512) void rowgemm_kernel(StreamArgs a) {
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
         const int k = 16 * t + 4 * q;
+        const int kc = (FULL && t == KT - 1) ? min(k, a.K - 4) : k;
         floatx4 v = {0.f, 0.f, 0.f, 0.f};
         // explicit global address space: a flat load would also count against lgkmcnt
         if (FULL || (m < a.M && k < a.K))
-          v = *(const __attribute__((address_space(1))) floatx4*)(a.A + (int64_t)m * a.lda + k);
+          v = *(const __attribute__((address_space(1))) floatx4*)(a.A + (int64_t)m * a.lda + kc);
         dst[rg][t] = v;
       }
     }
@@ -1018,8 +1022,7 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   // specialised (compile-time epilogue) instances for the encoder's GEMMs
   const bool aux_small = !(s.epi & RS_EPI_AUX_ADD) || (int64_t)s.aux_mod * nt * 16 * 4 <= 48 * 1024;
   if (!small && rg == 1 && s.vec_epi && s.N % (nt * 16) == 0 && aux_small && s.M % 16 == 0 &&
-      s.K == kt * 16 &&
-      !getenv_flag("RSYS_ROWGEMM_GENERIC")) {
+      s.K % 4 == 0 && !getenv_flag("RSYS_ROWGEMM_GENERIC")) {
     const size_t lds2 = lds + (size_t)(nt * 16 + ((s.epi & RS_EPI_AUX_ADD) ? s.aux_mod * nt * 16 : 0)) * sizeof(float);
     const int per_cu2 = lds2 > 80 * 1024 ? 1 : (lds2 > 53 * 1024 ? 2 : (lds2 > 40 * 1024 ? 3 : 4));
     int bx2 = cdiv(groups, 16);

@@ -370,6 +370,26 @@ def test_l2norm():
     assert torch.allclose(dx, x.grad, atol=1e-4)
 
 
+@pytest.mark.parametrize('K', [40, 36, 64])
+@pytest.mark.parametrize('p', [0.0, 0.1])
+def test_projection_specialised_k_remainder(K, p, monkeypatch):
+    """The sequence projection (M >= 32768, N = 64, K = 40: bias + dropout + positional add +
+    dropout) on the compile-time-epilogue rowgemm, whose last k tile re-reads the row's last
+    float4 when K % 16 != 0: bit-equal to the generic kernel, and torch at p = 0."""
+    M, N, L = 50 * 700, 64, 50
+    x, W, b = rnd(M, K, seed=1), rnd(N, K, seed=2) * 0.2, rnd(N, seed=3)
+    pos = rnd(L, N, seed=4)
+    key = torch.tensor([23, 2], dtype=torch.int64, device=DEV)
+    outs = []
+    for generic in ('0', '1'):
+        monkeypatch.setenv('RSYS_ROWGEMM_GENERIC', generic)
+        outs.append(ops.linear_fwd(x, W, b, aux=pos, aux_mod=L, drop_p=p, drop_key=key, site_a=0, site_b=1))
+    assert torch.equal(outs[0], outs[1])
+    if p == 0.0:
+        ref = x @ W.t() + b + pos[torch.arange(M, device=DEV) % L]
+        assert torch.allclose(outs[0], ref, atol=1e-4, rtol=1e-5)
+
+
 @pytest.mark.parametrize('K', [64, 256, 40])
 @pytest.mark.parametrize('p', [0.0, 0.1])
 def test_linear_add_layernorm_fused(K, p, monkeypatch):
