@@ -170,6 +170,8 @@ def main():
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if os.environ.get('RSYS_DIST_BACKEND') == 'gloo':  # rehearsal: ranks share the box's GPUs
+        local %= max(torch.cuda.device_count(), 1)
     dev = torch.device(f'cuda:{local}')
     torch.cuda.set_device(dev)
 

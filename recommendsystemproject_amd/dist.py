@@ -32,7 +32,9 @@ def init_from_env(backend=None):
     if world <= 1 or (dist.is_available() and dist.is_initialized()):
         return
     if backend is None:
-        backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+        # RSYS_DIST_BACKEND=gloo: several ranks sharing one GPU (RCCL refuses two ranks on one
+        # device) -- rehearses the multi-rank path on a one-GPU box
+        backend = os.environ.get('RSYS_DIST_BACKEND') or ('nccl' if torch.cuda.is_available() else 'gloo')
     if backend == 'nccl':
         torch.cuda.set_device(int(os.environ.get('LOCAL_RANK', '0')))
     dist.init_process_group(backend=backend)
