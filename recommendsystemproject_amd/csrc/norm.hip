@@ -248,8 +248,13 @@ __global__ __launch_bounds__(256) void ln_bwd64_kernel(const float* __restrict__
 }
 
 int ln_blocks(int M) {
+  static const int cap = [] {  // RSYS_LN_BLOCKS: tuning only
+    const char* e = getenv("RSYS_LN_BLOCKS");
+    const int x = e ? atoi(e) : 0;
+    return x >= 64 ? x : 2048;
+  }();
   int nb = cdiv(M, 4 * 4 * 4);  // >= 4 row groups per wave
-  if (nb > 2048) nb = 2048;
+  if (nb > cap) nb = cap;
   if (nb < 1) nb = 1;
   return nb;
 }
