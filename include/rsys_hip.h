@@ -158,6 +158,18 @@ int rs_ffn_fwd_bf16(int M, int F, const float* x, const float* W1, const float* 
 int rs_ffn_bwd_bf16(int M, int F, const float* x, const float* W1, const float* b1, const float* W2,
                     const uint64_t* mask, const float* dff, const float* dres, float* dx, void* f1,
                     void* dpre, float p, void* stream);
+/* rs_ffn_bwd_bf16 with the backward of the LayerNorm that produced x (norm1 of the same
+ * TransformerEncoderLayer, x1 = LN1(h1)) fused into its epilogue: dx never reaches HBM; writes
+ * dh1 = LN1-backward(dx) (h1, gamma1, mean1, rstd1 of the forward), dsa = dropout-backward of
+ * dh1 at `site` (element m*64 + n; nullable when p == 0), and accumulates dgamma1 / dbeta1
+ * (fixed-order partials in ws: rs_ffn_bwd_ln_ws_bytes). Replaces the rs_ffn_bwd_bf16 +
+ * rs_layernorm_bwd pair of SequenceEncoder's layer backward. dh1 may alias dres (not dff). */
+int64_t rs_ffn_bwd_ln_ws_bytes(int M, int F);
+int rs_ffn_bwd_ln_bf16(int M, int F, const float* x, const float* W1, const float* b1,
+                       const float* W2, const uint64_t* mask, const float* dff, const float* dres,
+                       const float* h1, const float* gamma1, const float* mean1, const float* rstd1,
+                       float* dh1, float* dsa, float* dgamma1, float* dbeta1, void* f1, void* dpre,
+                       float p, const int64_t* key, int site, float* ws, void* stream);
 /* dW[Mo,No] = beta*dW + dY^T X over `rows` rows on bf16 MFMA (fp32 accumulate, fixed-order
  * reduction); db[Mo] += colsum(dY) (nullable). dY / X are fp32 or, with dy_bf16 / x_bf16, bf16
  * (the fused FFN's f1 / dPre1). Replaces the weight-gradient part of autograd's Linear backward

@@ -46,6 +46,9 @@ SIGNATURES = {
     'rs_ffn_fwd_bf16': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, f32, vp,
                               i32, i32, vp]),
     'rs_ffn_bwd_bf16': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, vp]),
+    'rs_ffn_bwd_ln_ws_bytes': (i64, [i32, i32]),
+    'rs_ffn_bwd_ln_bf16': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                 vp, vp, f32, vp, i32, vp, vp]),
     'rs_wgrad_ws_bytes': (i64, [i32, i32, i32]),
     'rs_wgrad_bf16': (i32, [i32, i32, i32, vp, i32, i32, vp, i32, i32, f32, vp, i32, vp, vp, vp]),
     'rs_colsum_ws_bytes': (i64, [i32, i32]),

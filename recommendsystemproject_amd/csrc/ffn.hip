@@ -62,6 +62,16 @@ struct FfnArgs {
   float p;
   const int64_t* key;
   int site1, site2;
+  // bwd with the next LayerNorm's backward fused (rs_ffn_bwd_ln_bf16): the block's x1 is
+  // LN1(h1); dx1 never reaches HBM, the kernel writes dh1 = LN1-backward(dx1) and
+  // dsa = dropout-backward(dh1) (site ln_site), and [grid][128] dgamma | dbeta partials
+  const float* ln_h;
+  const float* ln_gamma;
+  const float* ln_mean;
+  const float* ln_rstd;
+  float* ln_da;  // nullable (p == 0)
+  float* ln_ws;
+  int ln_site;
 };
 
 // k permutation of a 32-wide chunk: operand slot 8q + j (lane quad q, element j) holds column
@@ -244,7 +254,7 @@ __global__ __launch_bounds__(512) void ffn_fwd_bf16_kernel(FfnArgs a) {
   }
 }
 
-template <int F>
+template <int F, bool LN1 = false, bool LNDROP = false>
 __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
   constexpr int FP = F + 8;
   constexpr int NH = F / 16, NC = F / 32;
@@ -275,6 +285,18 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
     load_row64(a.x, (int64_t)g * 16 + r, q, xr);
     load_row64(a.dff, (int64_t)g * 16 + r, q, dr);
   }
+  // LN1: gamma at this lane's columns 16t + 4q + e, and its dgamma / dbeta partial sums
+  floatx4 lgm[LN1 ? 4 : 1], lpg[LN1 ? 4 : 1], lpb[LN1 ? 4 : 1];
+  DropKey ldk{};
+  if constexpr (LN1) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      lgm[t] = *(gptr4)(a.ln_gamma + 16 * t + 4 * q);
+      lpg[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+      lpb[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    if constexpr (LNDROP) ldk = make_key(a.key, a.ln_site, a.p);
+  }
   for (; g < groups; g += stride) {
     int zo = 0;
     asm volatile("" : "+s"(zo));
@@ -285,6 +307,14 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
     floatx4 res[4];  // dres[m][16t + 4q ..] (accumulated into)
 #pragma unroll
     for (int t = 0; t < 4; ++t) res[t] = *(gptr4)(a.dres + m * D + 16 * t + 4 * q);
+    floatx4 lh[LN1 ? 4 : 1];
+    float lmu = 0.f, lrs = 0.f;
+    if constexpr (LN1) {  // LN1 operands, issued with the residual rows
+#pragma unroll
+      for (int t = 0; t < 4; ++t) lh[t] = *(gptr4)(a.ln_h + m * D + 16 * t + 4 * q);
+      lmu = a.ln_mean[m];
+      lrs = a.ln_rstd[m];
+    }
     const uint64_t bits = a.mask[m * (F / 64) + q];
     bf16x8 ax[2] = {cvt8(xr[0], xr[1]), cvt8(xr[2], xr[3])};
     bf16x8 ad[2] = {cvt8(dr[0], dr[1]), cvt8(dr[2], dr[3])};
@@ -330,11 +360,74 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
       for (int t = 0; t < 4; ++t)
         acc3[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(W3i + (16 * t + r) * FP + 32 * c + 8 * q),
                                                            a3[c], acc3[t], 0, 0, 0);
+    if constexpr (!LN1) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      floatx4 v = acc3[t] * 1.0f;
-      v += 1.0f * res[t];
-      *reinterpret_cast<floatx4*>(a.dx + m * D + 16 * t + 4 * q) = v;
+      for (int t = 0; t < 4; ++t) {
+        floatx4 v = acc3[t] * 1.0f;
+        v += 1.0f * res[t];
+        *reinterpret_cast<floatx4*>(a.dx + m * D + 16 * t + 4 * q) = v;
+      }
+    } else {
+      // LayerNorm backward of the row (its 64 columns sit in the 4 lanes r, r+16, r+32, r+48):
+      // dh = rstd (g - mean(g) - xhat mean(g xhat)), g = dx1 * gamma
+      floatx4 v[4], xh[4], gg[4];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        v[t] = acc3[t] * 1.0f;
+        v[t] += 1.0f * res[t];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[t][e] = (lh[t][e] - lmu) * lrs;
+          gg[t][e] = v[t][e] * lgm[t][e];
+          s1 += gg[t][e];
+          s2 += gg[t][e] * xh[t][e];
+          lpg[t][e] += v[t][e] * xh[t][e];
+          lpb[t][e] += v[t][e];
+        }
+      }
+      s1 += __shfl_xor(s1, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      s1 /= 64.f;
+      s2 /= 64.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        floatx4 dh;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dh[e] = lrs * (gg[t][e] - s1 - xh[t][e] * s2);
+        *reinterpret_cast<floatx4*>(a.dx + m * D + 16 * t + 4 * q) = dh;
+        if constexpr (LNDROP) {
+          float mk[4];
+          keep4(ldk, (uint64_t)(m * D + 16 * t + 4 * q), mk);  // rs_dropout_fwd's draw
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dh[e] *= mk[e];
+          *reinterpret_cast<floatx4*>(a.ln_da + m * D + 16 * t + 4 * q) = dh;
+        }
+      }
+    }
+  }
+  if constexpr (LN1) {
+    // dgamma | dbeta partials of this workgroup: fixed-order sum over the 16 rows r of each
+    // lane quad and the 8 waves (the weight images are dead: the LDS is reused)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem_raw);  // [8 waves][64 lanes][32]
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        red[(wave * 64 + lane) * 32 + 4 * t + e] = lpg[t][e];
+        red[(wave * 64 + lane) * 32 + 16 + 4 * t + e] = lpb[t][e];
+      }
+    __syncthreads();
+    if (threadIdx.x < 128) {
+      const int st = threadIdx.x >> 6, c = threadIdx.x & 63;  // st 0: dgamma, 1: dbeta
+      const int t = c >> 4, qq = (c & 15) >> 2, e = c & 3;
+      float acc = 0.f;
+      for (int w = 0; w < 8; ++w)
+        for (int rr = 0; rr < 16; ++rr) acc += red[(w * 64 + rr + 16 * qq) * 32 + 16 * st + 4 * t + e];
+      a.ln_ws[(int64_t)blockIdx.x * 128 + threadIdx.x] = acc;
     }
   }
 }
@@ -382,6 +475,43 @@ extern "C" int rs_ffn_fwd_bf16(int M, int F, const float* x, const float* W1, co
   else ffn_fwd_bf16_kernel<256, false><<<bx, 512, lds, as_stream(stream)>>>(a);
   RS_CHECK_LAUNCH("rs_ffn_fwd_bf16");
   return 0;
+}
+
+extern "C" int64_t rs_ffn_bwd_ln_ws_bytes(int M, int F) {
+  return (int64_t)grid_for(M, bwd_lds(F)) * 128 * (int64_t)sizeof(float);
+}
+
+extern "C" int rs_ffn_bwd_ln_bf16(int M, int F, const float* x, const float* W1, const float* b1,
+                                  const float* W2, const uint64_t* mask, const float* dff,
+                                  const float* dres, const float* h1, const float* gamma1,
+                                  const float* mean1, const float* rstd1, float* dh1, float* dsa,
+                                  float* dgamma1, float* dbeta1, void* f1, void* dpre, float p,
+                                  const int64_t* key, int site, float* ws, void* stream) {
+  RS_CHECK_ARG(M >= 0 && M % 16 == 0 && F == 256, "rs_ffn_bwd_ln_bf16: need M %% 16 == 0 and F == 256 (M=%d F=%d)", M, F);
+  RS_CHECK_ARG(x && W1 && b1 && W2 && mask && dff && dres && h1 && gamma1 && mean1 && rstd1 && dh1 &&
+                   dgamma1 && dbeta1 && f1 && dpre && ws,
+               "rs_ffn_bwd_ln_bf16: null operand");
+  RS_CHECK_ARG(dh1 != dff && dh1 != h1 && (dh1 != dres || dff != dres),
+               "rs_ffn_bwd_ln_bf16: dh1 may alias dres only when dff is not dres");
+  RS_CHECK_ARG(aligned16(x) && aligned16(dff) && aligned16(dres) && aligned16(dh1) && aligned16(b1) &&
+                   aligned16(h1) && aligned16(gamma1) && (!dsa || aligned16(dsa)) &&
+                   ((uintptr_t)f1 & 7) == 0 && ((uintptr_t)dpre & 7) == 0,
+               "rs_ffn_bwd_ln_bf16: misaligned operand");
+  RS_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || (key && dsa)), "rs_ffn_bwd_ln_bf16: dropout needs a key and dsa, 0 <= p < 1");
+  if (M == 0) return 0;
+  FfnArgs a{};
+  a.M = M; a.x = x; a.W1 = W1; a.b1 = b1; a.W2 = W2; a.mask = const_cast<uint64_t*>(mask);
+  a.dff = dff; a.dres = dres; a.dx = dh1; a.f1 = reinterpret_cast<__bf16*>(f1);
+  a.dpre = reinterpret_cast<__bf16*>(dpre); a.p = p; a.key = key;
+  a.ln_h = h1; a.ln_gamma = gamma1; a.ln_mean = mean1; a.ln_rstd = rstd1; a.ln_da = dsa; a.ln_ws = ws;
+  a.ln_site = site;
+  const size_t lds = bwd_lds(F);
+  const int nb = grid_for(M, lds);
+  hipStream_t st = as_stream(stream);
+  if (p > 0.f) ffn_bwd_bf16_kernel<256, true, true><<<nb, 512, lds, st>>>(a);
+  else ffn_bwd_bf16_kernel<256, true, false><<<nb, 512, lds, st>>>(a);
+  RS_CHECK_LAUNCH("rs_ffn_bwd_ln_bf16");
+  return partials_reduce2(ws, nb, 128, 64, 1.f, 1.f, dgamma1, dbeta1, st);
 }
 
 extern "C" int rs_ffn_bwd_bf16(int M, int F, const float* x, const float* W1, const float* b1,

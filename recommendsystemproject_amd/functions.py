@@ -245,10 +245,18 @@ def _post_attn_bwd(lyr, saved, dx2, p, key, site):
     dh2 = ops.layernorm_bwd(h2, dx2, lyr.norm2.weight, m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias),
                             da=dff, p=p, key=key, site=site + 3)
     dff = dh2 if dff is None else dff
+    ln1_done = False
     if isinstance(f1, tuple):  # fused feed-forward block (bf16 mode)
-        # dx1 = dh2 + dPre1 W1 (out of place: dff may be dh2 itself and is read again below)
-        dh2, f1b, dpre = ops.ffn_bwd_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight,
-                                          f1[1], dff, dh2, p)
+        if not os.environ.get('RSYS_UNFUSED_FFN_LN'):
+            # dx1 = dh2 + dPre1 W1 and norm1's backward in one pass: dx1 stays on chip
+            dh1, dsa, f1b, dpre = ops.ffn_bwd_ln_bf16(
+                x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, f1[1], dff, dh2, h1,
+                lyr.norm1.weight, m1, r1, g(lyr.norm1.weight), g(lyr.norm1.bias), p, key, site + 1)
+            ln1_done = True
+        else:
+            # dx1 = dh2 + dPre1 W1 (out of place: dff may be dh2 itself and is read again below)
+            dh2, f1b, dpre = ops.ffn_bwd_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight,
+                                              f1[1], dff, dh2, p)
 
         def _ffn_wgrads(dff=dff, f1b=f1b, dpre=dpre):
             ops.wgrad_bf16(dff, f1b, g(lyr.linear2.weight), db=g(lyr.linear2.bias))
@@ -263,9 +271,10 @@ def _post_attn_bwd(lyr, saved, dx2, p, key, site):
         ops.linear_bwd_weight(df1, x1, g(lyr.linear1.weight), db=g(lyr.linear1.bias))
         ops.linear_bwd_input(df1, lyr.linear1.weight, out=dh2, beta=1.0)  # dx1 = dh2 + df1 W1
     # x1 = LN1(x + drop1(sa))
-    dsa = torch.empty_like(dh2) if p > 0 else None
-    dh1 = ops.layernorm_bwd(h1, dh2, lyr.norm1.weight, m1, r1, g(lyr.norm1.weight), g(lyr.norm1.bias),
-                            da=dsa, p=p, key=key, site=site + 1)
+    if not ln1_done:
+        dsa = torch.empty_like(dh2) if p > 0 else None
+        dh1 = ops.layernorm_bwd(h1, dh2, lyr.norm1.weight, m1, r1, g(lyr.norm1.weight), g(lyr.norm1.bias),
+                                da=dsa, p=p, key=key, site=site + 1)
     def _out_wgrad(dsa=dsa):
         ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
     if dsa is None:  # p == 0: dsa IS dh1, which the in-proj backward accumulates into: inline

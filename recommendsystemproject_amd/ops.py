@@ -124,6 +124,22 @@ def ffn_bwd_bf16(x, W1, b1, W2, mask, dff, dres, p, dx=None):
     return dx, f1, dpre
 
 
+def ffn_bwd_ln_bf16(x, W1, b1, W2, mask, dff, dres, h1, gamma1, mean1, rstd1, dgamma1, dbeta1, p,
+                    key, site):
+    """ffn_bwd_bf16 with norm1's backward fused: -> (dh1, dsa or None, f1 bf16, dPre1 bf16)."""
+    M, F = x.shape[0], W1.shape[0]
+    dev = x.device
+    dh1 = torch.empty_like(dres)
+    dsa = torch.empty_like(dres) if p > 0 else None
+    f1 = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    dpre = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    w = ws(_hip.lib().rs_ffn_bwd_ln_ws_bytes(M, F), dev)
+    call('rs_ffn_bwd_ln_bf16', M, F, P(x), P(W1), P(b1), P(W2), P(mask), P(dff), P(dres), P(h1), P(gamma1),
+         P(mean1), P(rstd1), P(dh1), P(dsa), P(dgamma1), P(dbeta1), P(f1), P(dpre), float(p), P(key), site,
+         P(w), stream())
+    return dh1, dsa, f1, dpre
+
+
 def wgrad_bf16(dy, x, dW, *, db=None, beta=1.0):
     """dW[Mo,No] = beta*dW + dy[rows,Mo]^T x[rows,No] on bf16 MFMA; db += colsum(dy). dy / x may be
     fp32 or bf16 tensors."""

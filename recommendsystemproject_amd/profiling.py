@@ -113,7 +113,15 @@ def _ce_fused_work(a, bwd=False):
     return (8.0 if bwd else 2.0) * B * B * D, 4.0 * 2 * B * D * (2 if bwd else 1)
 
 
+def _ffn_bwd_ln_work(a):
+    M, F = a[0], a[1]
+    # the FFN backward's operands plus norm1's: h1 read, dh1 (+ dsa) written instead of dx1
+    fl, by = _ffn_bwd_work(a)
+    return fl + 12.0 * M * 64, by + 4.0 * M * 64 * (2 if a[19] > 0 else 1)
+
+
 WORK = {
+    'rs_ffn_bwd_ln_bf16': _ffn_bwd_ln_work,
     'rs_inbatch_ce_fused_fwd': _ce_fused_work,
     'rs_inbatch_ce_fused_bwd': lambda a: _ce_fused_work(a, True),
     'rs_gemm_add_layernorm': _gemm_ln_work,

@@ -197,6 +197,43 @@ def test_fused_ffn_matches_unfused(p, bf16_mode):
     assert torch.allclose(db1, db1r, atol=1e-2 * db1r.abs().max().item())
 
 
+@pytest.mark.parametrize('p,M', [(0.0, 40960), (0.1, 40960), (0.1, 4112)])
+def test_fused_ffn_ln_backward(p, M, bf16_mode):
+    """rs_ffn_bwd_ln_bf16 (the FFN backward with norm1's backward in its epilogue) against the
+    rs_ffn_bwd_bf16 + rs_layernorm_bwd pair it replaces: f1 / dPre1 bit-exact, dh1 and dsa to
+    fp32 summation order (the row sums run over the columns in another order), the same dropout
+    masks (dsa zero exactly where the pair's is), dgamma / dbeta to fixed-order-sum tolerance."""
+    x = rnd(M, 64, seed=7)
+    W1, b1, W2, b2, g, be = _ffn_weights()
+    key = torch.tensor([4321, 6], dtype=torch.int64, device=DEV)
+    _, _, _, _, mask = ops.ffn_fwd_bf16(x, W1, b1, W2, b2, g, be, 1e-5, p, key, 18, 19)
+    dff, dres = rnd(M, 64, seed=8), rnd(M, 64, seed=9)
+    h1 = rnd(M, 64, seed=10) * 2 + 0.3
+    g1 = 1 + 0.1 * rnd(64, seed=11)
+    mu1 = h1.mean(1)
+    rs1 = 1.0 / torch.sqrt(h1.var(1, unbiased=False) + 1e-5)
+    dg0, db0 = rnd(64, seed=12), rnd(64, seed=13)
+    # reference pair
+    dx, f1r, dpr = ops.ffn_bwd_bf16(x, W1, b1, W2, mask, dff, dres, p)
+    dgr, dbr = dg0.clone(), db0.clone()
+    dar = torch.empty_like(dx) if p > 0 else None
+    dhr = ops.layernorm_bwd(h1, dx, g1, mu1, rs1, dgr, dbr, da=dar, p=p, key=key, site=21)
+    # fused
+    dgf, dbf = dg0.clone(), db0.clone()
+    dh1, dsa, f1b, dpre = ops.ffn_bwd_ln_bf16(x, W1, b1, W2, mask, dff, dres, h1, g1, mu1, rs1, dgf, dbf,
+                                              p, key, 21)
+    assert torch.equal(f1b, f1r) and torch.equal(dpre, dpr)
+    sc = dhr.abs().max().item()
+    assert (dh1 - dhr).abs().max().item() < 1e-5 * sc
+    if p > 0:
+        assert torch.equal(dsa == 0, dar == 0)
+        assert (dsa - dar).abs().max().item() < 2e-5 * sc
+    else:
+        assert dsa is None
+    for a, b_ in ((dgf, dgr), (dbf, dbr)):
+        assert (a - b_).abs().max().item() < 1e-5 * max(1.0, b_.abs().max().item())
+
+
 def test_fused_ffn_bad_args(bf16_mode):
     x = rnd(40, 64)  # M % 16 != 0
     W1, b1, W2, b2, g, be = _ffn_weights()
