@@ -776,8 +776,13 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(StreamArgs a, int rows_
 }
 
 int wgrad_blocks(int Kr) {
+  static const int cap = [] {  // RSYS_WGRAD_BLOCKS: tuning only
+    const char* e = getenv("RSYS_WGRAD_BLOCKS");
+    const int x = e ? atoi(e) : 0;
+    return x >= 16 ? x : 512;
+  }();
   int nb = Kr / 64;  // >= 64 rows per workgroup; short K (the MLP's B = 4096) still fills 64 CUs
-  if (nb > 512) nb = 512;
+  if (nb > cap) nb = cap;
   if (nb < 1) nb = 1;
   return nb;
 }
