@@ -204,6 +204,26 @@ def test_seq_mask_quirks():
     assert last.tolist() == [1, 0, 3, 0]  # T7: count-based, all-pad row -> 0
 
 
+@pytest.mark.parametrize('B,L', [(1000, 50), (37, 1), (300, 64), (300, 65), (257, 200), (64, 129)])
+def test_seq_mask_random(B, L):
+    """One wave per row (ballot count): bit-exact against the reference's mask / last-valid rules
+    (SequenceEncoder.py:32-74, T6/T7) on random padding patterns incl. all-padding rows, and on a
+    strided id matrix (a column slice of a wider [B, ld] tensor)."""
+    g = torch.Generator().manual_seed(B * 1000 + L)
+    wide = torch.randint(0, 4, (B, L + 3), generator=g)  # 0 = padding, ~25 %
+    wide[::7] = 0  # all-padding rows
+    seq = wide.to(DEV)[:, 2:2 + L]
+    key_pad, last = ops.seq_mask(seq, 0)
+    s = wide[:, 2:2 + L]
+    ref_pad = (s == 0)
+    allpad = ref_pad.all(1)
+    ref_pad[allpad, L - 1] = False
+    valid = (~(s == 0)).sum(1)
+    ref_last = torch.clamp(valid - 1, min=0)
+    assert torch.equal(key_pad.cpu().bool(), ref_pad)
+    assert torch.equal(last.cpu(), ref_last)
+
+
 def ref_attention(qkv, key_pad, B, L, d, H):
     hd = d // H
     q, k, v = qkv.view(B, L, 3, H, hd).permute(2, 0, 3, 1, 4)
