@@ -263,7 +263,12 @@ int ln_blocks(int M) {
 constexpr int kBnU = 16; // independent loads in flight per thread in the BatchNorm row loops
 
 int bn_chunks(int Bg) {
-  int s = cdiv(Bg, 64);  // 64-row chunks: 16 rows per thread in the partial kernel
+  static const int rows = [] {  // RSYS_BN_ROWS: tuning only
+    const char* e = getenv("RSYS_BN_ROWS");
+    const int x = e ? atoi(e) : 0;
+    return x >= 16 ? x : 64;
+  }();
+  int s = cdiv(Bg, rows);  // 64-row chunks: 16 rows per thread in the partial kernel
   if (s > 512) s = 512;
   if (s < 1) s = 1;
   return s;
