@@ -985,6 +985,7 @@ bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda)
   switch (nt * 100 + kt) {
     case 403: case 404: case 412: case 416: case 1204: case 1604: case 304: case 1216:
     case 204: case 804: case 408: case 808: case 1608:
+    case 405: case 504:  // C5's sequence projection (K = 72) and its input gradient (N = 72)
     case 203: case 208: case 211: case 212: case 216: return true;
     default: return false;
   }
@@ -1038,7 +1039,9 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
     return -1;
   }
   // specialised (compile-time epilogue) instances for the encoder's GEMMs
-  const bool aux_small = !(s.epi & RS_EPI_AUX_ADD) || (int64_t)s.aux_mod * nt * 16 * 4 <= 48 * 1024;
+  // the AUX_ADD table (positional rows) in LDS: up to 64 KB covers C5's L = 200 x 64 (51 KB; two
+  // workgroups per CU then)
+  const bool aux_small = !(s.epi & RS_EPI_AUX_ADD) || (int64_t)s.aux_mod * nt * 16 * 4 <= 64 * 1024;
   if (!small && rg == 1 && s.vec_epi && s.N % (nt * 16) == 0 && aux_small && s.M % 16 == 0 &&
       s.K % 4 == 0 && !getenv_flag("RSYS_ROWGEMM_GENERIC")) {
     const size_t lds2 = lds + (size_t)(nt * 16 + ((s.epi & RS_EPI_AUX_ADD) ? s.aux_mod * nt * 16 : 0)) * sizeof(float);
@@ -1054,7 +1057,7 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
     }
     RS_RGE(16, 4, 19) RS_RGE(16, 4, 3) RS_RGE(16, 4, 8) RS_RGE(16, 4, 0) RS_RGE(12, 4, 1)
     RS_RGE(4, 12, 64) RS_RGE(4, 16, 64) RS_RGE(4, 4, 0) RS_RGE(4, 4, 64) RS_RGE(4, 3, 53)
-    RS_RGE(4, 3, 5) RS_RGE(4, 16, 0) RS_RGE(4, 12, 0)
+    RS_RGE(4, 3, 5) RS_RGE(4, 16, 0) RS_RGE(4, 12, 0) RS_RGE(4, 5, 53) RS_RGE(4, 5, 5)
 #undef RS_RGE
   }
 #define RS_RG(NTV, KTV)                                                            \
@@ -1065,7 +1068,7 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   switch (nt * 100 + kt) {
     RS_RG(4, 3) RS_RG(4, 4) RS_RG(4, 12) RS_RG(4, 16) RS_RG(12, 4) RS_RG(16, 4) RS_RG(3, 4)
     RS_RG(12, 16) RS_RG(2, 4) RS_RG(8, 4) RS_RG(4, 8) RS_RG(8, 8) RS_RG(16, 8)
-    RS_RG(2, 3) RS_RG(2, 8) RS_RG(2, 11) RS_RG(2, 12) RS_RG(2, 16)
+    RS_RG(2, 3) RS_RG(2, 8) RS_RG(2, 11) RS_RG(2, 12) RS_RG(2, 16) RS_RG(4, 5) RS_RG(5, 4)
     default: set_error("rowgemm: no instance for N=%d K=%d", s.N, s.K); return -1;
   }
 #undef RS_RG

@@ -32,7 +32,8 @@ def test_gemm_transposes(M, N, K, ta, tb):
 
 
 @pytest.mark.parametrize('M,N,K', [(777, 96, 64), (5000, 256, 64), (5003, 64, 256), (4096, 192, 64),
-                                   (6000, 40, 64), (6000, 64, 40), (4100, 64, 192)])
+                                   (6000, 40, 64), (6000, 64, 40), (4100, 64, 192), (6000, 72, 64),
+                                   (6000, 64, 72), (40000, 72, 64), (40000, 64, 72)])
 def test_gemm_epilogues_and_split(M, N, K):
     x, W, b = rnd(M, K, seed=3), rnd(N, K, seed=4), rnd(N, seed=5)
     pos = rnd(13, N, seed=6)
@@ -390,7 +391,7 @@ def test_l2norm():
     assert torch.allclose(dx, x.grad, atol=1e-4)
 
 
-@pytest.mark.parametrize('K', [40, 36, 64])
+@pytest.mark.parametrize('K', [40, 36, 64, 72])
 @pytest.mark.parametrize('p', [0.0, 0.1])
 def test_projection_specialised_k_remainder(K, p, monkeypatch):
     """The sequence projection (M >= 32768, N = 64, K = 40: bias + dropout + positional add +
