@@ -413,6 +413,10 @@ int rs_dropout_bwd(float* dx, int64_t n, float p, const int64_t* key, int site, 
 /* ---------------------------------------------------------------- reductions */
 /* out = scale * sum(x[0..n)) (deterministic; mean loss) */
 int rs_sum(const float* x, int n, float scale, float* out, void* stream);
+/* *flag |= bit if x[0..n) holds a NaN (x 16-byte aligned). The loss inputs' NaN guard of
+ * TwoTowerModel.compute_loss (TwoTowerModel.py:88-91, 99-100): checked on the device every step,
+ * raised by the host at its log-point sync. */
+int rs_nan_check(const float* x, int64_t n, int* flag, int bit, void* stream);
 
 #ifdef __cplusplus
 }

@@ -91,6 +91,7 @@ SIGNATURES = {
     'rs_counter_add': (i32, [vp, i64, vp]),
     'rs_prof_marker': (i32, [i32, vp]),
     'rs_sum': (i32, [vp, i32, f32, vp, vp]),
+    'rs_nan_check': (i32, [vp, i64, vp, i32, vp]),
     'rs_rng_next': (i32, [vp, vp, vp]),
     'rs_adam_prepare': (i32, [vp, vp, i32, f32, f32, f32, vp]),
     'rs_sparse_touch': (i32, [vp, i32, i32, i64, i64, i64, vp, vp, vp, vp]),

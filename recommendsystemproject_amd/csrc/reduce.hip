@@ -140,3 +140,34 @@ extern "C" int rs_sum(const float* x, int n, float scale, float* out, void* stre
   RS_CHECK_LAUNCH("rs_sum");
   return 0;
 }
+
+// NaN guard of the loss inputs (TwoTowerModel.py:88-91 raises on NaN user/item/hard-negative
+// embeddings): flag |= bit when x[0..n) holds a NaN. No sync: the host reads the flag at its
+// existing log-point sync (training_utils.train_one_epoch) and raises there.
+namespace rs {
+namespace {
+__global__ __launch_bounds__(256) void nan_check_kernel(const float* __restrict__ x, int64_t n,
+                                                        int* __restrict__ flag, int bit) {
+  bool bad = false;
+  const int64_t n4 = n / 4;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = x4[i];
+    bad |= (v.x != v.x) | (v.y != v.y) | (v.z != v.z) | (v.w != v.w);
+  }
+  for (int64_t i = n4 * 4 + blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    bad |= x[i] != x[i];
+  if (__ballot(bad) != 0 && (threadIdx.x & 63) == 0) atomicOr(flag, bit);
+}
+}  // namespace
+}  // namespace rs
+
+extern "C" int rs_nan_check(const float* x, int64_t n, int* flag, int bit, void* stream) {
+  RS_CHECK_ARG(x && flag && n >= 0 && rs::aligned16(x), "rs_nan_check: bad args");
+  if (n == 0) return 0;
+  int blocks = rs::cdiv(n / 4 + 1, 256);
+  if (blocks > 1024) blocks = 1024;
+  rs::nan_check_kernel<<<blocks, 256, 0, rs::as_stream(stream)>>>(x, n, flag, bit);
+  RS_CHECK_LAUNCH("rs_nan_check");
+  return 0;
+}

@@ -48,6 +48,9 @@ __device__ __forceinline__ void replay(const Hyper& h, const float2* __restrict_
   }
 }
 
+// consts[0] (step 0 never runs) holds {cap as int bits, overflow flag as int bits}: every reader
+// clamps its step index to cap - 1, so a graph replayed past the capacity reads no memory past the
+// table (the constants it then uses are stale: Adam.check_errors raises on the overflow flag)
 __global__ void adam_prepare_kernel(int64_t* step, float2* consts, int cap, float lr, float b1,
                                     float b2) {
   const int64_t t = *step + 1;
@@ -55,7 +58,16 @@ __global__ void adam_prepare_kernel(int64_t* step, float2* consts, int cap, floa
   if (t < cap) {
     const double bc1 = 1.0 - pow((double)b1, (double)t), bc2 = 1.0 - pow((double)b2, (double)t);
     consts[t] = make_float2((float)((double)lr / bc1), (float)sqrt(bc2));
+    if (t == 1) consts[0] = make_float2(__int_as_float(cap), __int_as_float(0));
+  } else {
+    consts[0] = make_float2(__int_as_float(cap), __int_as_float(1));
   }
+}
+
+// the step index clamped into the constants table (see adam_prepare_kernel)
+__device__ __forceinline__ int clamp_step(const float2* consts, int64_t t) {
+  const int cap = __float_as_int(consts[0].x);
+  return t < cap ? (int)t : cap - 1;
 }
 
 __global__ void touch_kernel(const int64_t* __restrict__ ids, int rows, int bag, int64_t stride,
@@ -80,7 +92,7 @@ __global__ __launch_bounds__(256) void catchup_kernel(float* __restrict__ p, flo
                                                       const int64_t* __restrict__ step,
                                                       const float2* __restrict__ consts, Hyper h) {
   const int n = *count;
-  const int target = (int)*step;
+  const int target = clamp_step(consts, *step);
   const int lane = threadIdx.x & 63;
   for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4) {
     const int row = list[i];
@@ -102,7 +114,7 @@ __global__ __launch_bounds__(256) void sparse_adam_kernel(
     const int* __restrict__ count, int D, const int64_t* __restrict__ step,
     const float2* __restrict__ consts, Hyper h, float scale, const float* __restrict__ coef) {
   const int n = *count;
-  const int t = (int)*step;
+  const int t = clamp_step(consts, *step);
   const float s = scale * (coef ? *coef : 1.f);
   const float2 ct = consts[t];
   const int lane = threadIdx.x & 63;
@@ -149,7 +161,7 @@ __global__ void flush_kernel(float* __restrict__ p, float* __restrict__ m, float
                              int* __restrict__ last, int64_t V, int D,
                              const int64_t* __restrict__ step, const float2* __restrict__ consts,
                              Hyper h) {
-  const int target = (int)*step;
+  const int target = clamp_step(consts, *step);
   const int lane = threadIdx.x & 63;
   for (int64_t row = blockIdx.x * 4 + (threadIdx.x >> 6); row < V; row += (int64_t)gridDim.x * 4) {
     const int from = last[row] + 1;

@@ -70,8 +70,17 @@ def allreduce_gradients(model: torch.nn.Module, optimizer=None):
         exchange_lazy_grads(f)
     else:
         allreduce_flat_grad(f.grad)
-    if optimizer is not None:
-        optimizer.grad_scale = 1.0 / dist.get_world_size()
+    from .optim import Adam
+    world = dist.get_world_size()
+    if isinstance(optimizer, Adam):
+        # the flat gradient keeps the SUM; clip (clip_grad_norm_ or the fused clip) and the Adam
+        # kernel read it scaled by 1/world, so no extra pass over the gradient is needed
+        optimizer.grad_scale = 1.0 / world
+        f.grad_scale = 1.0 / world
+    else:
+        # another optimizer reads p.grad directly: turn the sum into the mean in place
+        _hip.call('rs_scale_inplace', f.grad.data_ptr(), f.numel, 1.0 / world, None, _stream())
+        f.grad_scale = 1.0
 
 
 def _stream():

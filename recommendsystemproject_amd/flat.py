@@ -113,6 +113,9 @@ class FlatParams:
         for t in self.lazy:
             t.param._rs_lazy = t
         self.lazy_opt = None  # set by optim.Adam: m, v, step_dev, consts, hyper
+        # the gradient holds grad_scale^-1 x the mean gradient (data parallel: the all-reduced sum,
+        # 1/world; dist.allreduce_gradients): clip_grad_norm_ measures the norm of the mean
+        self.grad_scale = 1.0
         self.attach_grads(zero=False)
 
     def grad_view(self, i):

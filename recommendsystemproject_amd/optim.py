@@ -57,16 +57,19 @@ def clip_grad_norm_(parameters, max_norm, norm_type=2.0, error_if_nonfinite=Fals
         raise NotImplementedError('only the 2-norm (the reference default) is implemented')
     if isinstance(parameters, torch.Tensor):
         parameters = [parameters]
+    parameters = list(parameters)  # a generator (model.parameters()) is read twice below
     params = [p for p in parameters if p.grad is not None]
     if not params:
         return torch.tensor(0.0)
     _hip.require_device(params[0])
-    f = _flat_cover(list(parameters))
+    f = _flat_cover(parameters)
     clip = _DeviceClip(params[0].device)
     if f is not None:
         # lazy tables: their unlisted gradient rows are zero, so scaling the whole region is
-        # correct (one sweep of the table gradient: the fused Adam clip avoids it)
-        clip.compute(f.grad, f.dense_numel, max_norm, lazy=f.lazy)
+        # correct (one sweep of the table gradient: the fused Adam clip avoids it). Under data
+        # parallelism the flat gradient holds the SUM over ranks: the norm is the mean's
+        # (f.grad_scale = 1/world), as torch DDP's averaged gradients give
+        clip.compute(f.grad, f.dense_numel, max_norm, scale=f.grad_scale, lazy=f.lazy)
         _hip.call('rs_scale_inplace', f.grad.data_ptr(), f.numel, 1.0, clip.coef.data_ptr(), ops.stream())
     else:
         # per-tensor partial sums into one workspace would need a multi-tensor kernel; gather
@@ -107,6 +110,9 @@ class Adam(torch.optim.Optimizer):
             if f.lazy:
                 # consts[s] = {lr/bc1(s), sqrt(bc2(s))} for every step s, replayed by catch-up
                 st['consts'] = torch.zeros(CONSTS_CAP, 2, dtype=torch.float32, device=f.data.device)
+                # row 0 (step 0 never runs): {capacity, overflow flag} as int bits; the kernels
+                # clamp their step index to it (csrc/sparse.hip adam_prepare_kernel)
+                st['consts'].view(torch.int32)[0, 0] = CONSTS_CAP
             self._flat_state[id(f)] = st
             for p, o in zip(f.params, f.offsets):
                 self.state[p] = {'step': torch.tensor(0.0),
@@ -195,6 +201,14 @@ class Adam(torch.optim.Optimizer):
                           float(b2), float(group['eps']), float(group['weight_decay']),
                           int(state['step'].item()), None, float(self.grad_scale), None, 0, ops.stream())
         return loss
+
+    def check_errors(self):
+        """Raise if a lazy table ran past its per-step constants (graph replays do not pass through
+        the host-side CONSTS_CAP check in step()). One host sync."""
+        for st in self._flat_state.values():
+            c = st.get('consts')
+            if c is not None and int(c.view(torch.int32)[0, 1].item()) != 0:
+                raise RuntimeError(f'lazy Adam: more than {CONSTS_CAP - 2} steps; raise optim.CONSTS_CAP')
 
     def state_dict(self):
         for st in self._flat_state.values():

@@ -19,9 +19,12 @@ class TwoTowerModel(nn.Module):
         self.item_tower = item_tower
         self.user_feature_mapping = user_feature_mapping
         self.item_feature_mapping = item_feature_mapping
-        # the reference raises on NaN embeddings with a host sync per step (TwoTowerModel.py:88-91);
-        # opt in with RSYS_CHECK_NAN=1 or model.check_nan = True
+        # the reference raises on NaN embeddings with a host sync per step (TwoTowerModel.py:88-91).
+        # Here every step ORs a device flag (rs_nan_check, no sync) and check_errors() raises the
+        # same RuntimeError at the caller's next sync (train_one_epoch's log points, validate);
+        # RSYS_CHECK_NAN=1 / model.check_nan = True restores the reference's per-step sync.
         self.check_nan = os.environ.get('RSYS_CHECK_NAN', '0') == '1'
+        self.register_buffer('nan_flag', torch.zeros(1, dtype=torch.int32), persistent=False)
 
     def set_feature_mappings(self, user_mapping, item_mapping):
         self.user_feature_mapping = user_mapping
@@ -103,8 +106,40 @@ class TwoTowerModel(nn.Module):
     def get_item_embeddings(self, item_inputs):
         return self.item_tower(item_inputs, self.item_feature_mapping)
 
+    _NAN_MSG = {1: 'Found NaN in User Embedding', 2: 'Found NaN in Item Embedding',
+                4: 'Found NaN in Hard Negative Embedding'}
+
+    def _flag_nan(self, t, bit):
+        if t.is_cuda and not t.is_contiguous() and t.dim() == 3 and t.transpose(0, 1).is_contiguous():
+            t = t.transpose(0, 1)  # the grouped hard-negative pass's [B, N, D] view of [N, B, D]
+        if not t.is_cuda or not t.is_contiguous() or t.data_ptr() % 16:
+            t = t.contiguous()
+        if self.nan_flag.device != t.device:
+            self.nan_flag = self.nan_flag.to(t.device)
+        _hip.call('rs_nan_check', t.data_ptr(), t.numel(), self.nan_flag.data_ptr(), bit,
+                  torch.cuda.current_stream(t.device).cuda_stream)
+
+    def check_errors(self):
+        """Raise what the reference would have raised since the last check: RuntimeError for NaN
+        loss inputs (TwoTowerModel.py:88-91, 99-100), IndexError for an embedding id outside its
+        table (GenericTower.py:184-196). One host sync; call it where the host syncs anyway."""
+        v = int(self.nan_flag.item())
+        if v:
+            self.nan_flag.zero_()
+            for bit in (1, 2, 4):
+                if v & bit:
+                    raise RuntimeError(self._NAN_MSG[bit])
+        for tower in (self.user_tower, self.item_tower):
+            if hasattr(tower, 'check_errors'):
+                tower.check_errors()
+
     def compute_loss(self, user_emb, item_emb, item_ids=None, hard_neg_emb=None, temperature=0.1):
         """In-batch softmax loss (TwoTowerModel.py:81-150)."""
+        if not self.check_nan and user_emb.is_cuda:
+            self._flag_nan(user_emb.detach(), 1)
+            self._flag_nan(item_emb.detach(), 2)
+            if hard_neg_emb is not None:
+                self._flag_nan(hard_neg_emb.detach(), 4)
         if self.check_nan:
             if torch.isnan(user_emb).any():
                 raise RuntimeError('Found NaN in User Embedding')

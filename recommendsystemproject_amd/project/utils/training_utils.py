@@ -74,6 +74,16 @@ def train_step(model, batch_data, optimizer, max_grad_norm=1.0, temperature=0.1,
     return loss.detach()
 
 
+def _check_errors(model, optimizer=None):
+    """Device error flags -> the reference's exceptions (one sync; see TwoTowerModel.check_errors)
+    and the lazy-Adam step-constant overflow (optim.Adam.check_errors)."""
+    m = getattr(model, 'module', model)
+    if hasattr(m, 'check_errors'):
+        m.check_errors()
+    if optimizer is not None and hasattr(optimizer, 'check_errors'):
+        optimizer.check_errors()
+
+
 def train_one_epoch(model, loader, optimizer, device, scheduler=None, log_every_n_batches=100,
                     epoch=None, max_grad_norm=1.0, temperature=0.1, item_id_feature='movie_id_enc',
                     item_id_type='sparse'):
@@ -90,7 +100,12 @@ def train_one_epoch(model, loader, optimizer, device, scheduler=None, log_every_
         losses.append(loss)
         if batch_idx % log_every_n_batches == 0:
             pbar.set_postfix({'loss': f'{loss.item():.4f}', 'lr': f"{optimizer.param_groups[0]['lr']:.6f}"})
+            # the reference raises at the failing op (IndexError at the lookup, GenericTower.py:
+            # 184-196; RuntimeError on NaN embeddings, TwoTowerModel.py:88-91); the device flags
+            # are read here, where loss.item() has already synchronised
+            _check_errors(model, optimizer)
     total = float(torch.stack(losses).sum().item()) if losses else 0.0
+    _check_errors(model, optimizer)
     avg_loss = total / max(len(loader), 1)
     print(f'Epoch {epoch} finished. Avg Loss: {avg_loss:.4f}')
     return avg_loss
@@ -230,6 +245,7 @@ def validate(model, loader, item_loader, device, epoch, k_list=[10, 20],
             num_samples += int(targets.shape[0])
             n_batches += 1
     avg_loss = total_loss.item() / max(len(loader), 1)
+    _check_errors(model)
     h = hits.cpu().tolist()
     acc_dict = {k: h[i] / max(num_samples, 1) for i, k in enumerate(k_list)}
     print(f"\nValidation Result - Loss: {avg_loss:.4f}")
