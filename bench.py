@@ -64,6 +64,11 @@ def parse():
                     help='N sampled hard negatives per row, materialised from a device item catalog '
                          'each step (one grouped item-tower pass)')
     ap.add_argument('--zipf', type=float, default=None, help='Zipf(alpha) ids instead of uniform (C3 variant)')
+    ap.add_argument('--batches', type=int, default=8,
+                    help='distinct resident batches cycled through by the timed steps')
+    ap.add_argument('--extra', default=None,
+                    help='comma-separated further workloads reported in the same JSON line under '
+                         '"extra" (default: c3 when --config is c2)')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--pmc-bracket', default=None, metavar='ENTRY|auto',
@@ -73,16 +78,20 @@ def parse():
     ap.add_argument('--traffic', default='auto',
                     help='PMC traffic summary (tools/pmc_traffic.py output) for roofline.traffic; '
                          'auto: profiles/traffic_<config>_<dtype>.json when it matches this run')
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.extra is None:
+        a.extra = 'c3' if a.config == 'c2' and a.batch is None and not a.zipf else ''
+    return a
 
 
-def run_key(args, B):
+def run_key(args, B, name=None, dtype=None, zipf=None, hard_negatives=None):
     """What a PMC traffic summary must match to be reported on this run's roofline."""
-    return {'config': args.config, 'dtype': args.dtype, 'batch': B, 'dropout': args.dropout,
-            'hard_negatives': args.hard_negatives, 'zipf': args.zipf}
+    return {'config': name or args.config, 'dtype': dtype or args.dtype, 'batch': B,
+            'dropout': args.dropout, 'hard_negatives': args.hard_negatives if hard_negatives is None else hard_negatives,
+            'zipf': zipf}
 
 
-def load_traffic(args, B, entry):
+def load_traffic(args, B, entry, name, dtype, zipf, hard_negatives):
     """roofline.traffic: HBM bytes per launch of `entry` from a committed rocprofv3 --pmc summary
     (FETCH_SIZE and WRITE_SIZE in separate passes, gfx950 read correction; tools/pmc_traffic.py),
     used only when it was collected on this same workload and entry point."""
@@ -90,11 +99,11 @@ def load_traffic(args, B, entry):
     if path == 'none':
         return None
     if path == 'auto':
-        path = os.path.join(ROOT, 'profiles', f'traffic_{args.config}_{args.dtype}.json')
+        path = os.path.join(ROOT, 'profiles', f'traffic_{name}_{dtype}.json')
     if not os.path.exists(path):
         return None
     tr = json.load(open(path))
-    if tr.get('entry') != entry or tr.get('run') != run_key(args, B):
+    if tr.get('entry') != entry or tr.get('run') != run_key(args, B, name, dtype, zipf, hard_negatives):
         return None
     out = {k: tr[k] for k in ('hbm_bytes_per_launch', 'hbm_read_bytes_per_launch',
                               'write_bytes_per_launch', 'alg_bytes_per_launch', 'launches') if k in tr}
@@ -128,18 +137,21 @@ def _cap_vocab(cfg, cap):
     return cfg, capped
 
 
-def cpu_baseline(cfg, seconds):
-    """The oracle (CPU restatement of the reference step, fp32) on a bounded sample. Tables above
-    CPU_VOCAB_CAP rows are capped (the oracle's dense Adam over a 100M x 64 table and its state
-    exceed the box's host-memory limit); the sample says so."""
+def _oracle_rate(cfg, seconds, B, dropout):
+    """Samples/s of the oracle's training step on the bench's own first batches (seed 1000 + i,
+    the GPU rank 0's), timed after one warm-up step, for about `seconds`."""
     from oracle.twotower_oracle import OracleTrainer, model_state_shapes
-    cfg, capped = _cap_vocab(cfg, CPU_VOCAB_CAP)
+    import copy
+    cfg = copy.deepcopy(cfg)
+    if dropout == '0':
+        for t in cfg['two_tower'].values():
+            t['dropout'] = 0.0
+            t.get('transformer_parameters', {})['dropout'] = 0.0
     maps = {'user': synth.tower_layout(cfg['two_tower']['user_tower']),
             'item': synth.tower_layout(cfg['two_tower']['item_tower'])}
     shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
     tr = OracleTrainer(cfg, synth.make_state(shapes, seed=1), lr=cfg['train']['learning_rate'], dropout=None)
-    B = 256
-    batches = [synth.batch_to_torch(synth.make_batch(cfg, B, seed=900 + i)) for i in range(2)]
+    batches = [synth.batch_to_torch(synth.make_batch(cfg, B, seed=1000 + i)) for i in range(2)]
     T = cfg['train']['temperature']
     tr.step(batches[0], maps, temperature=T)  # warm-up
     n, t0 = 0, time.perf_counter()
@@ -149,6 +161,18 @@ def cpu_baseline(cfg, seconds):
         el = time.perf_counter() - t0
         if el >= seconds or n >= 200:
             break
+    return n * B / el, n, el
+
+
+def cpu_baseline(cfg, seconds, B):
+    """The oracle (CPU restatement of the reference step, fp32) on a bounded sample of the same
+    workload: the configured batch B and the GPU's own batches, dropout as configured and p = 0
+    (half the time each), on the torch threads of the box's CPU share. Tables above CPU_VOCAB_CAP
+    rows are capped (the oracle's dense Adam over a 100M x 64 table and its state exceed the
+    box's host-memory limit); the sample says so."""
+    cfg, capped = _cap_vocab(cfg, CPU_VOCAB_CAP)
+    rate, n, el = _oracle_rate(cfg, seconds / 2, B, 'config')
+    rate0, n0, el0 = _oracle_rate(cfg, seconds / 2, B, '0')
     model = None
     try:
         for line in open('/proc/cpuinfo'):
@@ -157,34 +181,54 @@ def cpu_baseline(cfg, seconds):
                 break
     except OSError:
         pass
-    return {'value': round(n * B / el, 1), 'unit': 'samples/s', 'cores': torch.get_num_threads(),
-            'kind': 'port', 'sample': f'{n} steps x batch {B} of the same config (oracle, fp32, '
-                                      f'dropout as configured), {el:.1f} s' +
-                                      (f'; tables capped at {CPU_VOCAB_CAP:,} rows (host memory)' if capped else ''),
+    return {'value': round(rate, 1), 'unit': 'samples/s', 'cores': torch.get_num_threads(),
+            'kind': 'port', 'value_p0': round(rate0, 1),
+            'sample': f'{n} steps x batch {B} (the GPU run\'s first batches; oracle, fp32, dropout as '
+                      f'configured), {el:.1f} s; p = 0 leg: {n0} steps, {el0:.1f} s' +
+                      (f'; tables capped at {CPU_VOCAB_CAP:,} rows (host memory)' if capped else ''),
             'nproc': os.cpu_count(), 'cpu_model': model}
 
 
-def main():
-    args = parse()
-    rdist.init_from_env()
-    world = dist.get_world_size() if dist.is_initialized() else 1
-    rank = dist.get_rank() if dist.is_initialized() else 0
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if os.environ.get('RSYS_DIST_BACKEND') == 'gloo':  # rehearsal: ranks share the box's GPUs
-        local %= max(torch.cuda.device_count(), 1)
-    dev = torch.device(f'cuda:{local}')
-    torch.cuda.set_device(dev)
+def _copy_into(dst, src):
+    """Next resident batch -> the static input slot the captured graphs read (a device copy, as
+    a loader writing the next batch would)."""
+    if isinstance(src, torch.Tensor):
+        dst.copy_(src, non_blocking=True)
+    elif isinstance(src, dict):
+        for k, v in src.items():
+            _copy_into(dst[k], v)
+    elif isinstance(src, list):
+        for d, v in zip(dst, src):
+            _copy_into(d, v)
 
-    cfg = yaml.safe_load(open(os.path.join(ROOT, 'configs', f'{args.config}.yaml')))
+
+def _clone(b):
+    if isinstance(b, torch.Tensor):
+        return b.clone()
+    if isinstance(b, dict):
+        return {k: _clone(v) for k, v in b.items()}
+    if isinstance(b, list):
+        return [_clone(v) for v in b]
+    return b
+
+
+def load_cfg(name, args):
+    cfg = yaml.safe_load(open(os.path.join(ROOT, 'configs', f'{name}.yaml')))
     if args.dropout == '0':
         for t in cfg['two_tower'].values():
             t['dropout'] = 0.0
             t.get('transformer_parameters', {})['dropout'] = 0.0
-    if args.zipf:
-        cfg.setdefault('synthetic', {})['zipf'] = args.zipf
-    if args.dtype == 'config':
-        args.dtype = 'bf16' if args.config in ('c2', 'c5') else 'fp32'
-    precision.set_compute_dtype(args.dtype)
+    return cfg
+
+
+def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_seconds):
+    """Build the model of workload `name`, time args.steps steps (after args.warmup) cycling through
+    args.batches distinct resident batches, profile one instrumented pass. Returns the result dict
+    on rank 0 (None elsewhere); with args.pmc_bracket, prints the bracket line and returns None."""
+    cfg = load_cfg(name, args)
+    if zipf:
+        cfg.setdefault('synthetic', {})['zipf'] = zipf
+    precision.set_compute_dtype(dtype)
     B = args.batch or int(cfg['train']['batch_size'])
     T = float(cfg['train']['temperature'])
     maps = {'user': synth.tower_layout(cfg['two_tower']['user_tower']),
@@ -205,12 +249,19 @@ def main():
     rdist.broadcast_model(model)
     opt = Adam(model.parameters(), lr=float(cfg['train']['learning_rate']))
     opt.grad_scale = 1.0 / world
-    batch = synth.batch_to_torch(synth.make_batch(cfg, B, seed=1000 + rank), dev)  # resident in HBM
+    # K distinct batches resident in HBM (per rank), cycled through by every step: the lazy-Adam
+    # catch-up replays real skipped steps and the gathered rows are not one cache-resident set
+    K = max(1, args.batches)
+    batches = [synth.batch_to_torch(synth.make_batch(cfg, B, seed=1000 + 97 * rank + i), dev)
+               for i in range(K)]
+    batch = _clone(batches[0])  # the static slot the graphs read
     ids = extract_item_id(batch['item_tower'])
-    catalog = neg_ids = None
-    if args.hard_negatives:
+    catalog = None
+    neg_sets = neg_ids = None
+    if hard_negatives:
         # synthetic item catalog (id column = row, other features random) and uniformly sampled
-        # negative ids, resident; the N item-tower dicts are materialised inside every step
+        # negative ids (one set per resident batch); the N item-tower dicts are materialised
+        # inside every step
         from recommendsystemproject_amd.project.utils.hard_negatives import ItemCatalog
         item_cfg = cfg['two_tower']['item_tower']
         V = int(item_cfg['sparse_features'][0]['vocab_size'])
@@ -222,7 +273,8 @@ def main():
         seqc = {f['name']: torch.randint(0, int(f['vocab_size']), (V, 3), device=dev, generator=g, dtype=torch.int32)
                 for f in item_cfg['sparse_features'] if 'pooling' in f}
         catalog = ItemCatalog(sparse=sparse, sequence=seqc, device=dev)
-        neg_ids = torch.randint(1, V, (B, args.hard_negatives), device=dev, generator=g)
+        neg_sets = [torch.randint(1, V, (B, hard_negatives), device=dev, generator=g) for _ in range(K)]
+        neg_ids = neg_sets[0].clone()
 
     def fwd_bwd():
         opt.zero_grad()
@@ -240,8 +292,18 @@ def main():
         if world > 1:
             rdist.allreduce_gradients(model, opt)
 
+    counter = [0]
+
+    def next_batch():
+        i = counter[0] % K
+        counter[0] += 1
+        _copy_into(batch, batches[i])
+        if neg_sets is not None:
+            neg_ids.copy_(neg_sets[i], non_blocking=True)
+
     # eager warm-up (also allocates Adam state), then capture
     for _ in range(max(2, min(args.warmup, 3))):
+        next_batch()
         fwd_bwd()
         allreduce()
         opt_step()
@@ -250,11 +312,13 @@ def main():
         target = args.pmc_bracket
         if target == 'auto':
             with KernelTimer() as kt:
+                next_batch()
                 fwd_bwd()
                 allreduce()
                 opt_step()
             target = max(kt.summary().items(), key=lambda kv: kv[1]['ms'])[0]
         torch.cuda.synchronize()
+        next_batch()
         with PmcBracket(target) as pb:
             fwd_bwd()
             allreduce()
@@ -264,10 +328,8 @@ def main():
             print(json.dumps({'pmc_bracket': target, 'launches': pb.launches,
                               'alg_bytes_per_launch': pb.bytes / max(pb.launches, 1),
                               'alg_flops_per_launch': pb.flops / max(pb.launches, 1),
-                              'run': run_key(args, B)}))
-        if dist.is_initialized():
-            dist.destroy_process_group()
-        return
+                              'run': run_key(args, B, name, dtype, zipf, hard_negatives)}))
+        return None
     graphs = None
     if not args.no_graph:
         try:
@@ -291,6 +353,7 @@ def main():
             graphs = None
 
     def step():
+        next_batch()
         if graphs is not None:
             graphs[0].replay()
             allreduce()
@@ -318,6 +381,7 @@ def main():
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = float(el_t.item())
     final_loss = float(loss.item())
+    model.check_errors()  # device error flags (bad ids, NaN embeddings) of the timed steps
 
     # roofline of the dominant kernel: HIP events on the launch stream, eager instrumented steps.
     # A spin kernel first gives the host a head start: the launches (Python + ctypes, slower than
@@ -331,6 +395,7 @@ def main():
     torch.cuda._sleep(int(2.4e9 * 0.03))  # ~30 ms at the 2.4 GHz shader clock
     with KernelTimer() as kt:
         for _ in range(3):
+            next_batch()
             fwd_bwd()
             allreduce()
             opt_step()
@@ -341,7 +406,7 @@ def main():
     summ = kt.summary()
     dom_name, dom = max(summ.items(), key=lambda kv: kv[1]['ms'])
     # the dominant entry point's MFMA peak: bf16 MFMA in the bf16 compute mode (its GEMMs), f32 else
-    peak_mfma = PEAK_BF16_TFLOPS if args.dtype == 'bf16' and dom_name != 'rs_attn_fwd' and \
+    peak_mfma = PEAK_BF16_TFLOPS if dtype == 'bf16' and dom_name != 'rs_attn_fwd' and \
         dom_name != 'rs_attn_bwd' else PEAK_F32_TFLOPS
     flop_bound = dom['flops'] / max(dom['bytes'], 1.0) > peak_mfma * 1e12 / (PEAK_HBM_GBS * 1e9)
     avg_ms = dom['ms'] / dom['launches']
@@ -353,7 +418,7 @@ def main():
         roof = {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s'}
     roof['frac'] = round(roof['achieved'] / roof['peak'], 4)
     roof['traffic'] = None
-    tr = load_traffic(args, B, dom_name)
+    tr = load_traffic(args, B, dom_name, name, dtype, zipf, hard_negatives)
     if tr is not None:
         roof['traffic'] = tr['hbm_bytes_per_launch']
         roof['traffic_detail'] = tr
@@ -365,21 +430,25 @@ def main():
     step_flops = sum(v['flops'] for v in summ.values()) / 3
     step_bytes = sum(v['bytes'] for v in summ.values()) / 3
     bound_ms = max(step_bytes / (PEAK_HBM_GBS * 1e9),
-                   step_flops / ((PEAK_BF16_TFLOPS if args.dtype == 'bf16' else PEAK_F32_TFLOPS) * 1e12)) * 1e3
+                   step_flops / ((PEAK_BF16_TFLOPS if dtype == 'bf16' else PEAK_F32_TFLOPS) * 1e12)) * 1e3
     step_roof = {'flops_per_step': round(step_flops), 'bytes_per_step': round(step_bytes),
                  'bound_ms': round(bound_ms, 4), 'frac': round(bound_ms / (el / args.steps * 1e3), 4)}
     # the embedding gather against the HBM roofline (north_star: >= 70 % on the gather), against the
     # 8 TB/s spec and against the measured float4-copy bandwidth (report both)
     gather_roof = {}
-    for k in ('rs_gather_fwd', 'rs_gather_bwd'):
-        if k in summ and summ[k]['ms'] > 0:
-            g = summ[k]
+    # the table gradient = the scatter of ordinary tables (rs_gather_bwd) + the sorted segment
+    # sum of the large ones (rs_segsum); the sort itself runs in the forward (rs_lookup_sort)
+    groups = {'rs_gather_fwd': ('rs_gather_fwd',), 'table_grad': ('rs_gather_bwd', 'rs_segsum')}
+    for k, members in groups.items():
+        ms = [summ[m] for m in members if m in summ]
+        g = {'ms': sum(x['ms'] for x in ms), 'bytes': sum(x['bytes'] for x in ms)}
+        if g['ms'] > 0:
             gbs = g['bytes'] / (g['ms'] * 1e-3) / 1e9
             gather_roof[k] = {'achieved': round(gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                               'frac': round(gbs / PEAK_HBM_GBS, 4),
                               'frac_of_measured_copy': round(gbs / HBM_MEASURED_GBS, 4),
-                              'bytes_per_launch': round(g['bytes'] / g['launches']),
-                              'avg_launch_ms': round(g['ms'] / g['launches'], 4)}
+                              'bytes_per_step': round(g['bytes'] / 3),
+                              'ms_per_step': round(g['ms'] / 3, 4), 'entries': list(members)}
 
     # the batch similarity (U I^T inside the fused in-batch CE) against the bf16 MFMA peak
     # (north_star: MFMA utilisation on the batch-dot)
@@ -393,40 +462,82 @@ def main():
                             'flops_per_launch': round(g['flops'] / g['launches']),
                             'avg_launch_ms': round(g['ms'] / g['launches'], 4)}
 
+    used_graph = graphs is not None
+    del model, opt, batches, batch, graphs, catalog
+    torch.cuda.empty_cache()
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, args.cpu_baseline_seconds)
+    if rank == 0 and world == 1 and cpu_seconds > 0:
+        cpu = cpu_baseline(cfg, cpu_seconds, B)
 
+    if rank != 0:
+        return None
+    samples = world * B * args.steps
+    tp = cfg['two_tower']['user_tower'].get('transformer_parameters', {})
+    has_seq = bool(cfg['two_tower']['user_tower'].get('sequence_features'))
+    return {
+        'metric': 'training samples/sec (user-item pairs) at batch 4096; 1/2/4/8 MI355X',
+        'value': round(samples / el, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 3),
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': dtype,
+        'data': f'synthetic (MovieLens-1M-shaped ids, seeded numpy PCG64, {K} distinct batches '
+                f'resident in HBM, cycled)',
+        'config': {'workload': f'{name}: ' + WORKLOADS.get(name, 'MovieLens-1M DSSM') +
+                   (f' + Transformer seq encoder (seq_len {tp.get("max_seq_len")}, d={cfg["two_tower"]["user_tower"]["embedding_dim"]})' if has_seq else ''),
+                   'global_batch': world * B, 'per_gpu_batch': B,
+                   'seq_len': tp.get('max_seq_len') if has_seq else None,
+                   'dropout': args.dropout, 'parallelism': f'dp{world}',
+                   'hip_graph': used_graph, 'final_loss': round(final_loss, 5),
+                   'ids': f'zipf({zipf})' if zipf else 'uniform',
+                   'hard_negatives': hard_negatives, 'resident_batches': K},
+        'roofline': roof,
+        'gather_roofline': gather_roof,
+        'batch_dot_roofline': batch_dot or None,
+        'step_roofline': step_roof,
+        'cpu_baseline': cpu,
+        'kernel_ms_per_step': {k: round(v['ms'] / 3, 4) for k, v in sorted(summ.items(), key=lambda kv: -kv[1]['ms'])},
+        '_gemm_shapes': kt.gemm_shapes() if os.environ.get('RSYS_BENCH_DETAIL') else None,
+    }
+
+
+def main():
+    args = parse()
+    rdist.init_from_env()
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if os.environ.get('RSYS_DIST_BACKEND') == 'gloo':  # rehearsal: ranks share the box's GPUs
+        local %= max(torch.cuda.device_count(), 1)
+    dev = torch.device(f'cuda:{local}')
+    torch.cuda.set_device(dev)
+    if args.dtype == 'config':
+        args.dtype = 'bf16' if args.config in ('c2', 'c5') else 'fp32'
+    cpu_s = 0.0 if args.no_cpu_baseline else args.cpu_baseline_seconds
+    out = run_workload(args, args.config, args.dtype, args.zipf, args.hard_negatives, rank, world, dev,
+                       cpu_s)
+    if args.pmc_bracket:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return
+    extras = {}
+    for ex in [e for e in (args.extra or '').split(',') if e and e != args.config]:
+        # the other headline workloads in the same line (BASELINE configs[2] = C3; at N > 1 the
+        # same run is configs[3] = C4, C3 data-parallel)
+        ex_dtype = 'bf16' if ex in ('c2', 'c5') else 'fp32'
+        r = run_workload(args, ex, ex_dtype, None, 10 if ex == 'c5' else 0, rank, world, dev,
+                         cpu_s / 2)
+        if r is not None:
+            extras[ex] = {k: r[k] for k in ('value', 'unit', 'ms_per_step', 'dtype', 'config', 'roofline',
+                                            'gather_roofline', 'batch_dot_roofline', 'step_roofline',
+                                            'cpu_baseline', 'kernel_ms_per_step')}
     if rank == 0:
-        samples = world * B * args.steps
-        tp = cfg['two_tower']['user_tower'].get('transformer_parameters', {})
-        has_seq = bool(cfg['two_tower']['user_tower'].get('sequence_features'))
-        out = {
-            'metric': 'training samples/sec (user-item pairs) at batch 4096; 1/2/4/8 MI355X',
-            'value': round(samples / el, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 3),
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
-            'data': 'synthetic (MovieLens-1M-shaped ids, seeded numpy PCG64, resident in HBM)',
-            'config': {'workload': f'{args.config}: ' + WORKLOADS.get(args.config, 'MovieLens-1M DSSM') +
-                       (f' + Transformer seq encoder (seq_len {tp.get("max_seq_len")}, d={cfg["two_tower"]["user_tower"]["embedding_dim"]})' if has_seq else ''),
-                       'global_batch': world * B, 'per_gpu_batch': B,
-                       'seq_len': tp.get('max_seq_len') if has_seq else None,
-                       'dropout': args.dropout, 'parallelism': f'dp{world}',
-                       'hip_graph': graphs is not None, 'final_loss': round(final_loss, 5),
-                       'ids': f'zipf({args.zipf})' if args.zipf else 'uniform',
-                       'hard_negatives': args.hard_negatives},
-            'roofline': roof,
-            'gather_roofline': gather_roof,
-            'batch_dot_roofline': batch_dot or None,
-            'step_roofline': step_roof,
-            'cpu_baseline': cpu,
-            'kernel_ms_per_step': {k: round(v['ms'] / 3, 4) for k, v in sorted(summ.items(), key=lambda kv: -kv[1]['ms'])},
-        }
-        if os.environ.get('RSYS_BENCH_DETAIL'):
-            shp = sorted(kt.gemm_shapes().items(), key=lambda kv: -kv[1][0])
+        shapes = out.pop('_gemm_shapes', None)
+        if shapes:
+            shp = sorted(shapes.items(), key=lambda kv: -kv[1][0])
             print(json.dumps({'gemm_shapes_ms_per_step': [
                 [list(k), round(v[0] / 3, 4), round(v[2] / (v[0] * 1e-3) / 1e12, 2) if v[0] else 0]
                 for k, v in shp[:24]]}), file=sys.stderr)
+        if extras:
+            out['extra'] = extras
         print(json.dumps(out))
     if dist.is_initialized():
         dist.destroy_process_group()

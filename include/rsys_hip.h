@@ -361,42 +361,61 @@ int rs_counter_add(int64_t* counter, int64_t delta, void* stream);
  * Dense-gradient Adam semantics (every row moves every step, T16) without sweeping the table:
  * rows carry last[] = the optimizer step they were last brought to; consts[s] =
  * {lr/bc1(s), sqrt(bc2(s))} is written once per step by rs_adam_prepare (which also advances
- * the device step count). Per step: rs_sparse_touch (dedup the batch's ids into list/count via
- * flag) -> rs_sparse_catchup (replay skipped zero-gradient steps for listed rows, bitwise equal
- * to dense Adam, before the gather reads them) -> backward scatter-add -> rs_sparse_sqnorm
- * (clip norm partials, rs_sparse_sqnorm_parts of them) -> rs_sparse_adam (step t for listed rows,
- * zero their gradient, clear flags and count). rs_sparse_flush brings every row to the current
- * step (checkpoint / state_dict). rs_sparse_zero_grad zeroes the listed gradient rows.
+ * the device step count; consts[0] holds {capacity, overflow flag} as int bits and every reader
+ * clamps its step index to the capacity). rs_sparse_flush brings every row to the current step
+ * (checkpoint / state_dict). The per-step row work runs over sorted lookups (below).
  * Replaces torch.optim.Adam on sparse=False embeddings (GenericTower.py:45-49; train_twotower.py:111). */
 int rs_adam_prepare(int64_t* step, float* consts, int cap, float lr, float beta1, float beta2,
                     void* stream);
-int rs_sparse_touch(const int64_t* ids, int rows, int bag, int64_t row_stride, int64_t vocab,
-                    int64_t pad, int* flag, int* list, int* count, void* stream);
-int rs_sparse_catchup(float* p, float* m, float* v, int* last, const int* list, const int* count,
-                      int D, const int64_t* step, const float* consts, float beta1, float beta2,
-                      float eps, float weight_decay, void* stream);
-int rs_sparse_adam(float* p, float* g, float* m, float* v, int* last, int* flag, const int* list,
-                   int* count, int D, const int64_t* step, const float* consts, float beta1,
-                   float beta2, float eps, float weight_decay, float scale, const float* coef,
-                   void* stream);
-int rs_sparse_sqnorm_parts(void);
-int rs_sparse_sqnorm(const float* g, const int* list, const int* count, int D, float scale,
-                     double* ws, void* stream);
 int rs_sparse_flush(float* p, float* m, float* v, int* last, int64_t V, int D, const int64_t* step,
                     const float* consts, float beta1, float beta2, float eps, float weight_decay,
                     void* stream);
-int rs_sparse_zero_grad(float* g, const int* list, const int* count, int D, void* stream);
-/* Data-parallel row-sparse gradient exchange (replicated tables; replaces the dense
- * all-reduce of [V, D] embedding gradients the reference's DDP-style scaling would need).
- * rs_sparse_pack writes [cap int32 ids (-1 = unused)][cap x D rows] from the local list (flags
- * err_flag |= 2 on overflow); after an all-gather each rank rs_sparse_unpack_add's every rank's
- * buffer in rank order (ids unique within a buffer; sets flags) and rs_sparse_compact rebuilds
- * list/count in ascending row order, so every rank holds bitwise-identical gradients and lists. */
-int64_t rs_sparse_compact_ws_bytes(int64_t V);
-int rs_sparse_compact(const int* flag, int64_t V, int* list, int* count, int* ws, void* stream);
-int rs_sparse_pack(const float* g, const int* list, const int* count, int D, int cap, float* buf,
-                   int* err_flag, void* stream);
-int rs_sparse_unpack_add(float* g, int* flag, const float* buf, int D, int cap, void* stream);
+
+/* ---------------------------------------------------------------- sorted lookups (large tables)
+ * One forward lookup of a large table (a [rows, bag] id matrix, int64 or int32, row stride
+ * row_stride) is sorted by row id: keys[n] ascending (ids outside [0, vocab) last, as
+ * 0xFFFFFFFF), vals[n] = the lookup index r * bag + l, ascending within a row (stable LSD radix
+ * sort; n <= 4096 in one launch without workspace, else rs_lookup_sort_ws_bytes of workspace).
+ * Every per-row operation then walks the distinct rows (run heads) of keys:
+ *   rs_sorted_catchup  replay skipped zero-gradient Adam steps before the gather reads the rows
+ *                      (bitwise equal to dense Adam);
+ *   rs_segsum          the table gradient = embedding_dense_backward of the call
+ *                      (GenericTower.py:182; pooled mean/sum GenericTower.py:141-162): per row
+ *                      the contributions of its lookups in lookup order (mode 0: dout row r per
+ *                      lookup, 1: dout row / bag, 2: dout row), `pad` skipped; plain stores
+ *                      (accumulate = 1: added to the row), no atomics, bitwise reproducible;
+ *                      dout points at the feature's first column, row stride ldo floats;
+ *   rs_sorted_sqnorm   clip-norm partials (rs_sorted_sqnorm_parts doubles into ws);
+ *   rs_sorted_adam     step t on each row with its (scaled, clipped) gradient, gradient zeroed;
+ *   rs_sorted_owner    owner[row] = min(owner[row], call): with several calls in a step, sqnorm
+ *                      and Adam take a row only in the call equal to its owner (Adam resets it);
+ *   rs_sorted_zero_grad zero the rows' gradient.
+ * rs_pack_ids / rs_pack_rows: contiguous int32 ids and gradient rows of a call for the
+ * data-parallel all-gather (each rank then sorts and segment-sums the gathered
+ * calls, so all ranks hold bitwise-identical table gradients; replaces a dense all-reduce of
+ * [V, D] embedding gradients). */
+int64_t rs_lookup_sort_ws_bytes(int64_t n, int64_t vocab);
+int rs_lookup_sort(const void* ids, int id_bytes, int rows, int bag, int64_t row_stride,
+                   int64_t vocab, uint32_t* keys, uint32_t* vals, void* ws, void* stream);
+int rs_sorted_catchup(const uint32_t* keys, int64_t n, int D, float* p, float* m, float* v,
+                      int* last, const int64_t* step, const float* consts, float beta1, float beta2,
+                      float eps, float weight_decay, void* stream);
+int rs_sorted_adam(const uint32_t* keys, int64_t n, int D, float* p, float* g, float* m, float* v,
+                   int* last, int* owner, int call, const int64_t* step, const float* consts,
+                   float beta1, float beta2, float eps, float weight_decay, float scale,
+                   const float* coef, void* stream);
+int rs_sorted_sqnorm_parts(void);
+int rs_sorted_sqnorm(const uint32_t* keys, int64_t n, int D, const float* g, int* owner, int call,
+                     float scale, double* ws, void* stream);
+int rs_sorted_owner(const uint32_t* keys, int64_t n, int* owner, int call, void* stream);
+int rs_sorted_zero_grad(const uint32_t* keys, int64_t n, int D, float* g, void* stream);
+int64_t rs_segsum_ws_bytes(int64_t n, int D);
+int rs_segsum(const uint32_t* keys, const uint32_t* vals, int64_t n, int bag, int mode, int64_t pad,
+              const float* dout, int64_t ldo, int D, float* grad, int accumulate, void* ws,
+              void* stream);
+int rs_pack_ids(const void* ids, int id_bytes, int64_t rows, int bag, int64_t row_stride,
+                int32_t* out, void* stream);
+int rs_pack_rows(const float* src, int64_t ld, int64_t rows, int D, float* dst, void* stream);
 
 /* ---------------------------------------------------------------- dropout
  * Counter-based masks: element i of site `site` is kept iff hash(key[0], key[1], site, i) >= p,

@@ -94,17 +94,20 @@ SIGNATURES = {
     'rs_nan_check': (i32, [vp, i64, vp, i32, vp]),
     'rs_rng_next': (i32, [vp, vp, vp]),
     'rs_adam_prepare': (i32, [vp, vp, i32, f32, f32, f32, vp]),
-    'rs_sparse_touch': (i32, [vp, i32, i32, i64, i64, i64, vp, vp, vp, vp]),
-    'rs_sparse_catchup': (i32, [vp, vp, vp, vp, vp, vp, i32, vp, vp, f32, f32, f32, f32, vp]),
-    'rs_sparse_adam': (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, f32, f32, f32, f32, f32, vp, vp]),
-    'rs_sparse_sqnorm_parts': (i32, []),
-    'rs_sparse_sqnorm': (i32, [vp, vp, vp, i32, f32, vp, vp]),
     'rs_sparse_flush': (i32, [vp, vp, vp, vp, i64, i32, vp, vp, f32, f32, f32, f32, vp]),
-    'rs_sparse_zero_grad': (i32, [vp, vp, vp, i32, vp]),
-    'rs_sparse_compact_ws_bytes': (i64, [i64]),
-    'rs_sparse_compact': (i32, [vp, i64, vp, vp, vp, vp]),
-    'rs_sparse_pack': (i32, [vp, vp, vp, i32, i32, vp, vp, vp]),
-    'rs_sparse_unpack_add': (i32, [vp, vp, vp, i32, i32, vp]),
+    'rs_lookup_sort_ws_bytes': (i64, [i64, i64]),
+    'rs_lookup_sort': (i32, [vp, i32, i32, i32, i64, i64, vp, vp, vp, vp]),
+    'rs_sorted_catchup': (i32, [vp, i64, i32, vp, vp, vp, vp, vp, vp, f32, f32, f32, f32, vp]),
+    'rs_sorted_adam': (i32, [vp, i64, i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, f32, f32, f32, f32, f32,
+                             vp, vp]),
+    'rs_sorted_sqnorm_parts': (i32, []),
+    'rs_sorted_sqnorm': (i32, [vp, i64, i32, vp, vp, i32, f32, vp, vp]),
+    'rs_sorted_owner': (i32, [vp, i64, vp, i32, vp]),
+    'rs_sorted_zero_grad': (i32, [vp, i64, i32, vp, vp]),
+    'rs_segsum_ws_bytes': (i64, [i64, i32]),
+    'rs_segsum': (i32, [vp, vp, i64, i32, i32, i64, vp, i64, i32, vp, i32, vp, vp]),
+    'rs_pack_ids': (i32, [vp, i32, i64, i32, i64, vp, vp]),
+    'rs_pack_rows': (i32, [vp, i64, i64, i32, vp, vp]),
     'rs_dropout_fwd': (i32, [vp, i64, i32, vp, i32, i32, f32, vp, i32, vp]),
     'rs_dropout_bwd': (i32, [vp, i64, f32, vp, i32, vp]),
 }

@@ -1,0 +1,859 @@
+// Sorted lookups of the large embedding tables: a deterministic, atomic-free replacement of the
+// table-gradient scatter-add (GenericTower.py:182 nn.Embedding -> embedding_dense_backward) and
+// the row bookkeeping of lazy-exact Adam (sparse.hip).
+//
+// One "call" = one lookup of a table in the forward (a [rows, bag] id matrix read in place).
+//   rs_lookup_sort : stable LSD radix sort of the call's ids -> keys[n] (row ids ascending,
+//                    out-of-range ids last as 0xFFFFFFFF) and vals[n] (the lookup index
+//                    e = r * bag + l; ascending within a row because the sort is stable).
+//   rs_sorted_catchup / _adam / _sqnorm / _zero_grad / _owner : per distinct row (run head of
+//                    keys): lazy-Adam catch-up before the gather, the Adam step, the clip-norm
+//                    partials, gradient zeroing, and the lowest call index holding a row (a row
+//                    looked up by several calls in one step is stepped once).
+//   rs_segsum      : the table gradient. Fixed chunks of 64 sorted positions per wave; a run
+//                    (one row's lookups) that lies inside a chunk is summed in lookup order and
+//                    stored with a plain store; a run crossing chunk boundaries leaves per-chunk
+//                    partials that a fixup pass adds in chunk order. Work per wave is the same
+//                    whatever the id skew (a Zipf hot row with 10^4 lookups spreads over 10^2
+//                    chunks), there are no float atomics, and the result is bitwise
+//                    reproducible -- which is what lets every data-parallel rank rebuild the same
+//                    gradient from all-gathered bag gradients (dist.py).
+//
+// Radix sort (multi-tile): per pass, hist (per-tile digit counts) -> scan (one workgroup per
+// digit over the tiles) -> scatter (stable in-tile ranking by wave ballots, cross-wave prefix in
+// LDS). Digits of up to 9 bits; passes = ceil(bits(vocab) / 9): 3 for 1M-100M-row tables.
+// A call of at most 4096 lookups is sorted by one workgroup in one launch (keys in registers,
+// exchanged through LDS between passes).
+#include "common.h"
+#include "adam.h"
+
+#pragma clang fp contract(off)  // the Adam here must round exactly like adam_kernel / sparse.hip
+
+namespace rs {
+namespace {
+
+constexpr int kSortThreads = 1024;
+constexpr int kSortWaves = kSortThreads / 64;
+constexpr int kSortRounds = 4;
+constexpr int kSortTile = kSortThreads * kSortRounds;  // 4096 lookups per tile
+constexpr int kMaxDigitBits = 9;
+constexpr int kMaxRadix = 1 << kMaxDigitBits;
+constexpr uint32_t kSentinel = 0xFFFFFFFFu;
+
+struct SortPlan {
+  int bits;    // key bits (sentinel's low `bits` bits exceed every valid id)
+  int passes;
+  int dbits[4];
+  int shift[4];
+  int ntiles;
+};
+
+SortPlan make_plan(int64_t n, int64_t vocab) {
+  SortPlan p;
+  int bits = 1;
+  while (bits < 32 && ((int64_t)1 << bits) - 1 < vocab) ++bits;
+  p.bits = bits;
+  p.passes = (bits + kMaxDigitBits - 1) / kMaxDigitBits;
+  int sh = 0;
+  for (int i = 0; i < p.passes; ++i) {
+    const int left = bits - sh, passes_left = p.passes - i;
+    p.dbits[i] = (left + passes_left - 1) / passes_left;
+    p.shift[i] = sh;
+    sh += p.dbits[i];
+  }
+  p.ntiles = cdiv(n, kSortTile);
+  return p;
+}
+
+// pass-0 key of lookup e: the row id read in place from the [rows, bag] id matrix (row stride
+// `stride`, int64 or int32 ids); out-of-range ids sort last as the sentinel
+__device__ __forceinline__ uint32_t raw_key(const void* ids, int id_bytes, int bag, int64_t stride,
+                                            int64_t vocab, int64_t e) {
+  const int64_t r = e / bag, l = e - r * bag;
+  const int64_t id = id_bytes == 8 ? static_cast<const int64_t*>(ids)[r * stride + l]
+                                   : (int64_t) static_cast<const int32_t*>(ids)[r * stride + l];
+  return id >= 0 && id < vocab ? (uint32_t)id : kSentinel;
+}
+
+struct RankLds {
+  uint16_t wc[kSortWaves][kMaxRadix];   // per-wave digit counts of the current round (leaders)
+  uint16_t pre[kSortWaves][kMaxRadix];  // tile-local start of each wave's group of a digit
+  int run[kMaxRadix];                   // tile-local count of each digit before this round
+};
+
+// Stable rank of this lane's digit within the tile, for one round of kSortThreads keys (key
+// order = round, wave, lane). Returns the tile-local position among keys of the same digit
+// (counting earlier rounds through lds.run). Two barriers.
+__device__ __forceinline__ int rank_round(RankLds& lds, uint32_t d, bool valid, int dbits,
+                                          int radix) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t peers = __ballot(valid);
+  for (int b = 0; b < dbits; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const uint64_t bb = __ballot(bit);
+    peers &= bit ? bb : ~bb;
+  }
+  if (!valid) peers = 0;
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int lrank = __popcll(peers & lt);
+  if (valid && lrank == 0) lds.wc[w][d] = (uint16_t)__popcll(peers);
+  __syncthreads();
+  for (int t = threadIdx.x; t < radix; t += kSortThreads) {
+    int r = lds.run[t];
+#pragma unroll
+    for (int ww = 0; ww < kSortWaves; ++ww) {
+      const int c = lds.wc[ww][t];
+      lds.wc[ww][t] = 0;
+      lds.pre[ww][t] = (uint16_t)r;
+      r += c;
+    }
+    lds.run[t] = r;
+  }
+  __syncthreads();
+  return valid ? (int)lds.pre[w][d] + lrank : 0;
+}
+
+__device__ __forceinline__ void rank_reset(RankLds& lds, int radix) {
+  for (int t = threadIdx.x; t < radix; t += kSortThreads) lds.run[t] = 0;
+  for (int i = threadIdx.x; i < kSortWaves * kMaxRadix; i += kSortThreads)
+    (&lds.wc[0][0])[i] = 0;
+}
+
+// ---------------------------------------------------------------- multi-tile radix sort
+__global__ __launch_bounds__(kSortThreads) void sort_hist_kernel(
+    const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab,
+    const uint32_t* __restrict__ src, int64_t n, int shift, int dbits, int* __restrict__ hist) {
+  __shared__ int h[kMaxRadix];
+  const int radix = 1 << dbits;
+  for (int t = threadIdx.x; t < radix; t += kSortThreads) h[t] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int64_t e = base + r * kSortThreads + threadIdx.x;
+    if (e < n) {
+      const uint32_t k = src ? src[e] : raw_key(ids, id_bytes, bag, stride, vocab, e);
+      atomicAdd(&h[(k >> shift) & (radix - 1)], 1);
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < radix; t += kSortThreads) hist[(int64_t)t * gridDim.x + blockIdx.x] = h[t];
+}
+
+// one workgroup per digit: exclusive scan of hist[d][0 .. ntiles) in place, total -> tot[d]
+__global__ __launch_bounds__(256) void sort_scan_kernel(int* __restrict__ hist, int ntiles,
+                                                        int* __restrict__ tot) {
+  __shared__ int wsum[4];
+  __shared__ int carry;
+  int* row = hist + (int64_t)blockIdx.x * ntiles;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int b0 = 0; b0 < ntiles; b0 += 256) {
+    const int i = b0 + threadIdx.x;
+    const int x = i < ntiles ? row[i] : 0;
+    int y = x;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(y, o, 64);
+      if (lane >= o) y += t;
+    }
+    if (lane == 63) wsum[w] = y;
+    __syncthreads();
+    int pre = carry;
+    for (int k = 0; k < w; ++k) pre += wsum[k];
+    if (i < ntiles) row[i] = pre + y - x;
+    __syncthreads();
+    if (threadIdx.x == 255) carry = pre + y;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tot[blockIdx.x] = carry;
+}
+
+__global__ __launch_bounds__(kSortThreads) void sort_scatter_kernel(
+    const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab,
+    const uint32_t* __restrict__ ksrc, const uint32_t* __restrict__ vsrc, int64_t n, int shift,
+    int dbits, const int* __restrict__ hist, const int* __restrict__ tot,
+    uint32_t* __restrict__ kdst, uint32_t* __restrict__ vdst) {
+  __shared__ RankLds lds;
+  __shared__ int gbase[kMaxRadix];
+  const int radix = 1 << dbits;
+  rank_reset(lds, radix);
+  // global base of digit d for this tile: (keys of smaller digits) + (digit d in earlier tiles)
+  if (threadIdx.x < 64) {
+    int carry = 0;
+    const int lane = threadIdx.x;
+    for (int d0 = 0; d0 < radix; d0 += 64) {
+      const int x = d0 + lane < radix ? tot[d0 + lane] : 0;
+      int y = x;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(y, o, 64);
+        if (lane >= o) y += t;
+      }
+      if (d0 + lane < radix)
+        gbase[d0 + lane] = carry + y - x + hist[(int64_t)(d0 + lane) * gridDim.x + blockIdx.x];
+      carry += __shfl(y, 63, 64);
+    }
+  }
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  uint32_t key[kSortRounds], val[kSortRounds];
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int64_t e = base + r * kSortThreads + threadIdx.x;
+    key[r] = kSentinel;
+    val[r] = 0;
+    if (e < n) {
+      key[r] = ksrc ? ksrc[e] : raw_key(ids, id_bytes, bag, stride, vocab, e);
+      val[r] = vsrc ? vsrc[e] : (uint32_t)e;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int64_t e = base + r * kSortThreads + threadIdx.x;
+    const bool valid = e < n;
+    const uint32_t d = (key[r] >> shift) & (radix - 1);
+    const int lp = rank_round(lds, d, valid, dbits, radix);
+    if (valid) {
+      const int64_t pos = (int64_t)gbase[d] + lp;
+      kdst[pos] = key[r];
+      vdst[pos] = val[r];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- one-tile sort (n <= 4096)
+__global__ __launch_bounds__(kSortThreads) void sort_tile_kernel(
+    const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab, int n,
+    SortPlan plan, uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+  __shared__ RankLds lds;
+  __shared__ int tbase[kMaxRadix];
+  __shared__ uint32_t xchg[kSortTile];
+  uint32_t key[kSortRounds], val[kSortRounds];
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int e = r * kSortThreads + threadIdx.x;
+    key[r] = e < n ? raw_key(ids, id_bytes, bag, stride, vocab, e) : kSentinel;
+    val[r] = (uint32_t)e;
+  }
+  for (int p = 0; p < plan.passes; ++p) {
+    const int radix = 1 << plan.dbits[p], shift = plan.shift[p];
+    rank_reset(lds, radix);
+    for (int t = threadIdx.x; t < radix; t += kSortThreads) tbase[t] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortRounds; ++r)
+      if (r * kSortThreads + (int)threadIdx.x < n) atomicAdd(&tbase[(key[r] >> shift) & (radix - 1)], 1);
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the digit counts
+      int carry = 0;
+      const int lane = threadIdx.x;
+      for (int d0 = 0; d0 < radix; d0 += 64) {
+        const int x = d0 + lane < radix ? tbase[d0 + lane] : 0;
+        int y = x;
+        for (int o = 1; o < 64; o <<= 1) {
+          const int t = __shfl_up(y, o, 64);
+          if (lane >= o) y += t;
+        }
+        if (d0 + lane < radix) tbase[d0 + lane] = carry + y - x;
+        carry += __shfl(y, 63, 64);
+      }
+    }
+    __syncthreads();
+    int pos[kSortRounds];
+#pragma unroll
+    for (int r = 0; r < kSortRounds; ++r) {
+      const bool valid = r * kSortThreads + (int)threadIdx.x < n;
+      const uint32_t d = (key[r] >> shift) & (radix - 1);
+      const int lp = rank_round(lds, d, valid, plan.dbits[p], radix);
+      pos[r] = valid ? tbase[d] + lp : -1;
+    }
+    // exchange keys, then values, through LDS into the new order
+#pragma unroll
+    for (int r = 0; r < kSortRounds; ++r) if (pos[r] >= 0) xchg[pos[r]] = key[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortRounds; ++r) {
+      const int e = r * kSortThreads + threadIdx.x;
+      if (e < n) key[r] = xchg[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortRounds; ++r) if (pos[r] >= 0) xchg[pos[r]] = val[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortRounds; ++r) {
+      const int e = r * kSortThreads + threadIdx.x;
+      if (e < n) val[r] = xchg[e];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int e = r * kSortThreads + threadIdx.x;
+    if (e < n) {
+      kout[e] = key[r];
+      vout[e] = val[r];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- per distinct row
+__device__ __forceinline__ void replay(const AdamConst& h, const float2* __restrict__ consts, int from,
+                                       int to, float& p, float& m, float& v) {
+  if (h.wd == 0.f && m == 0.f && v == 0.f) return;  // exact: such an element does not move
+  for (int s = from; s <= to; ++s) {
+    const float2 c = consts[s];
+    adam_update(h, c.x, c.y, 0.f, p, m, v);
+  }
+}
+
+__device__ __forceinline__ int clamp_step(const float2* consts, int64_t t) {
+  const int cap = __float_as_int(consts[0].x);
+  return t < cap ? (int)t : cap - 1;
+}
+
+enum RowOp { kCatchup = 0, kAdam = 1, kSqnorm = 2, kOwner = 3, kZero = 4 };
+
+struct RowArgs {
+  const uint32_t* keys;
+  int64_t n;
+  int D;
+  float* p;
+  float* g;
+  float* m;
+  float* v;
+  int* last;
+  int* owner;   // null: the call is the only one of its step
+  int call;
+  const int64_t* step;
+  const float2* consts;
+  AdamConst h;
+  float scale;
+  const float* coef;
+  double* ws;   // kSqnorm: one partial per workgroup
+};
+
+// One group of G lanes per sorted position (G = the lanes that cover a row 4 columns each:
+// D = 128 -> 32 lanes, two rows per wave; D <= 4 G); a group whose position is a run head (a
+// distinct row) processes that row with float4 loads (a whole wave walking its 64 positions' heads
+// one at a time was a chain of dependent row round trips: 3-4x slower). U > 1 takes U positions
+// per group iteration with their loads issued together; measured slower at U = 4 (168 VGPRs, fewer
+// resident waves: tools/lazy_bench.py), so U = 1 (RSYS_ROW_UNROLL4 = 1 for the A/B).
+constexpr int kRowUnroll = 1;
+
+template <int OP, int G, int U>
+__global__ __launch_bounds__(256) void sorted_rows_kernel(RowArgs a) {
+  __shared__ double red[4];
+  const int gl = threadIdx.x & (G - 1);
+  double acc = 0.0;
+  int t = 0;
+  float2 ct = make_float2(0.f, 0.f);
+  float s = 1.f;
+  if (OP == kCatchup || OP == kAdam) t = clamp_step(a.consts, *a.step);
+  if (OP == kAdam) {
+    ct = a.consts[t];
+    s = a.scale * (a.coef ? *a.coef : 1.f);
+  }
+  const int64_t ngroups = (int64_t)gridDim.x * (256 / G);
+  const int c0 = gl * 4;
+  const int w = c0 < a.D ? (a.D - c0 < 4 ? a.D - c0 : 4) : 0;  // columns of this lane
+  const bool vec = (a.D & 3) == 0;
+  for (int64_t i0 = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G; i0 < a.n; i0 += ngroups * U) {
+    int64_t row[U];
+    bool act[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * ngroups;
+      const uint32_t k = i < a.n ? a.keys[i] : kSentinel;
+      const uint32_t kp = i > 0 && i < a.n ? a.keys[i - 1] : kSentinel;
+      act[u] = k != kSentinel && (i == 0 || kp != k);
+      row[u] = k;
+    }
+    if (OP == kOwner) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (act[u] && gl == 0) atomicMin(&a.owner[row[u]], a.call);
+      continue;
+    }
+    int from[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      from[u] = 1;
+      if (act[u] && OP != kCatchup && a.owner && a.owner[row[u]] != a.call) act[u] = false;
+      if (act[u] && (OP == kCatchup || OP == kAdam)) from[u] = a.last[row[u]] + 1;
+      // catch-up: nothing to replay, or a row never stepped (its m = v = 0 from the start: with
+      // weight_decay == 0 the replay is the identity, exactly)
+      if (OP == kCatchup && act[u] && (from[u] > t || (from[u] == 1 && a.h.wd == 0.f))) act[u] = false;
+    }
+    float pp[U][4], mm[U][4], vv[U][4], gg[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!act[u] || w == 0) continue;
+      const int64_t o = row[u] * a.D + c0;
+      if (OP == kCatchup || OP == kAdam) {
+        if (vec) {
+          const float4 p4 = *reinterpret_cast<const float4*>(a.p + o);
+          pp[u][0] = p4.x; pp[u][1] = p4.y; pp[u][2] = p4.z; pp[u][3] = p4.w;
+          if (from[u] == 1 && a.h.wd == 0.f && OP == kAdam) {  // never stepped: m = v = 0
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { mm[u][j] = 0.f; vv[u][j] = 0.f; }
+          } else {
+            const float4 m4 = *reinterpret_cast<const float4*>(a.m + o);
+            const float4 v4 = *reinterpret_cast<const float4*>(a.v + o);
+            mm[u][0] = m4.x; mm[u][1] = m4.y; mm[u][2] = m4.z; mm[u][3] = m4.w;
+            vv[u][0] = v4.x; vv[u][1] = v4.y; vv[u][2] = v4.z; vv[u][3] = v4.w;
+          }
+        } else {
+          for (int j = 0; j < w; ++j) { pp[u][j] = a.p[o + j]; mm[u][j] = a.m[o + j]; vv[u][j] = a.v[o + j]; }
+        }
+      }
+      if (OP == kAdam || OP == kSqnorm) {
+        if (vec) {
+          const float4 g4 = *reinterpret_cast<const float4*>(a.g + o);
+          gg[u][0] = g4.x; gg[u][1] = g4.y; gg[u][2] = g4.z; gg[u][3] = g4.w;
+        } else {
+          for (int j = 0; j < w; ++j) gg[u][j] = a.g[o + j];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!act[u]) continue;
+      if (w > 0) {
+        const int64_t o = row[u] * a.D + c0;
+        if (OP == kCatchup) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < w) replay(a.h, a.consts, from[u], t, pp[u][j], mm[u][j], vv[u][j]);
+        } else if (OP == kAdam) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (j >= w) continue;
+            if (from[u] <= t - 1) replay(a.h, a.consts, from[u], t - 1, pp[u][j], mm[u][j], vv[u][j]);
+            adam_update(a.h, ct.x, ct.y, gg[u][j] * s, pp[u][j], mm[u][j], vv[u][j]);
+          }
+        } else if (OP == kSqnorm) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < w) {
+              const float x = gg[u][j] * a.scale;
+              acc += (double)(x * x);
+            }
+        }
+        if (OP == kCatchup || OP == kAdam) {
+          if (vec) {
+            *reinterpret_cast<float4*>(a.p + o) = make_float4(pp[u][0], pp[u][1], pp[u][2], pp[u][3]);
+            *reinterpret_cast<float4*>(a.m + o) = make_float4(mm[u][0], mm[u][1], mm[u][2], mm[u][3]);
+            *reinterpret_cast<float4*>(a.v + o) = make_float4(vv[u][0], vv[u][1], vv[u][2], vv[u][3]);
+          } else {
+            for (int j = 0; j < w; ++j) { a.p[o + j] = pp[u][j]; a.m[o + j] = mm[u][j]; a.v[o + j] = vv[u][j]; }
+          }
+        }
+        if (OP == kAdam || OP == kZero) {
+          if (vec) *reinterpret_cast<float4*>(a.g + o) = make_float4(0.f, 0.f, 0.f, 0.f);
+          else for (int j = 0; j < w; ++j) a.g[o + j] = 0.f;
+        }
+      }
+      if ((OP == kCatchup || OP == kAdam) && gl == 0) {
+        a.last[row[u]] = t;
+        if (OP == kAdam && a.owner) a.owner[row[u]] = 0x7fffffff;
+      }
+    }
+  }
+  if (OP == kSqnorm) {
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) a.ws[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  }
+}
+
+constexpr int kRowGrid = 2048;
+
+// ---------------------------------------------------------------- segment sum (table gradient)
+constexpr int kChunk = 64;
+constexpr int kSegBatch = 16;  // positions whose contributions are loaded together
+
+struct SegArgs {
+  const uint32_t* keys;
+  const uint32_t* vals;
+  int64_t n;
+  int bag;
+  int mode;       // 0 one id per dout row, 1 mean bag, 2 sum bag
+  int64_t pad;    // skipped row (no gradient), -1 none
+  const float* dout;
+  int64_t ldo;
+  int D;
+  float* grad;
+  int accumulate;
+  float* part;    // [nchunks][2][D]: head / tail partial of runs crossing chunk borders
+  int* flags;     // [nchunks]: 1 = a run starts in this chunk and continues past it
+  int nchunks;
+};
+
+template <int NV>  // columns per lane (D <= 64 * NV)
+__device__ __forceinline__ void load_contrib(const SegArgs& a, uint32_t e, float inv, float* x) {
+  const int64_t b = a.mode == 0 ? (int64_t)e : (int64_t)(e / (uint32_t)a.bag);
+  const float* src = a.dout + b * a.ldo;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = lane + 64 * j;
+    x[j] = c < a.D ? src[c] : 0.f;
+  }
+  if (a.mode == 1) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) x[j] = x[j] / inv;  // mean backward: grad / bag, per lookup
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void put_row(const SegArgs& a, int64_t row, const float* acc) {
+  const int lane = threadIdx.x & 63;
+  float* dst = a.grad + row * a.D;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = lane + 64 * j;
+    if (c < a.D) dst[c] = a.accumulate ? dst[c] + acc[j] : acc[j];
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void put_part(const SegArgs& a, int chunk, int which, const float* acc) {
+  const int lane = threadIdx.x & 63;
+  float* dst = a.part + ((int64_t)chunk * 2 + which) * a.D;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = lane + 64 * j;
+    if (c < a.D) dst[c] = acc[j];
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void segsum_kernel(SegArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (chunk >= a.nchunks) return;
+  const int64_t c0 = (int64_t)chunk * kChunk;
+  const int cn = (int)(a.n - c0 < kChunk ? a.n - c0 : kChunk);
+  const uint32_t k = lane < cn ? a.keys[c0 + lane] : kSentinel;
+  const uint32_t e = lane < cn ? a.vals[c0 + lane] : 0u;
+  const uint32_t kprev = c0 > 0 ? a.keys[c0 - 1] : kSentinel;
+  const uint32_t knext = c0 + kChunk < a.n ? a.keys[c0 + kChunk] : kSentinel;
+  const float inv = (float)a.bag;
+  float acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) acc[j] = 0.f;
+  int flag = 0;
+  int s = 0;  // start of the current run within the chunk
+  for (int i0 = 0; i0 < cn; i0 += kSegBatch) {
+    // the contributions of kSegBatch positions are loaded before any is added (that many rows
+    // in flight per wave)
+    float x[kSegBatch][NV];
+    uint32_t kk[kSegBatch];
+#pragma unroll
+    for (int u = 0; u < kSegBatch; ++u) {
+      const int i = i0 + u;
+      kk[u] = (uint32_t)__builtin_amdgcn_readlane((int)k, i < 64 ? i : 63);
+      const uint32_t ee = (uint32_t)__builtin_amdgcn_readlane((int)e, i < 64 ? i : 63);
+      const bool use = i < cn && kk[u] != kSentinel && (int64_t)kk[u] != a.pad;
+      if (use) load_contrib<NV>(a, ee, inv, x[u]);
+      else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) x[u][j] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kSegBatch; ++u) {
+      const int i = i0 + u;
+      if (i >= cn) break;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) acc[j] += x[u][j];
+      // end of run at position i: the next key differs (inside the chunk) or the chunk ends
+      const uint32_t kn = i + 1 < cn ? (uint32_t)__builtin_amdgcn_readlane((int)k, i + 1 < 64 ? i + 1 : 63)
+                                     : (c0 + cn < a.n ? knext : kSentinel);
+      if (kn == kk[u] && i + 1 < cn) continue;
+      const uint32_t key = kk[u];
+      if (key != kSentinel && (int64_t)key != a.pad) {
+        const bool head = s == 0 && kprev == key;         // began in an earlier chunk
+        const bool tail = i + 1 == cn && kn == key;       // continues into the next chunk
+        if (!head && !tail) put_row<NV>(a, key, acc);
+        else if (head) put_part<NV>(a, chunk, 0, acc);    // (also when it continues: "through")
+        else {
+          put_part<NV>(a, chunk, 1, acc);
+          flag = 1;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NV; ++j) acc[j] = 0.f;
+      s = i + 1;
+    }
+  }
+  if (lane == 0) a.flags[chunk] = flag;
+}
+
+// runs crossing chunk borders: the chunk where the run starts adds its tail partial and the head
+// partials of the following chunks, in chunk order
+template <int NV>
+__global__ __launch_bounds__(256) void segsum_fixup_kernel(SegArgs a) {
+  const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (chunk >= a.nchunks || !a.flags[chunk]) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t last = (int64_t)chunk * kChunk + kChunk - 1;
+  const uint32_t key = a.keys[last];
+  float acc[NV];
+  const float* t = a.part + ((int64_t)chunk * 2 + 1) * a.D;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) acc[j] = lane + 64 * j < a.D ? t[lane + 64 * j] : 0.f;
+  // the following chunks' head partials, kFixBatch at a time with their loads in flight together
+  // (a hot row's run spans hundreds of chunks; one dependent round trip per chunk made this
+  // pass the longest of the backward under Zipf ids); added in chunk order
+  constexpr int kFixBatch = 16;
+  bool done = false;
+  for (int c = chunk + 1; c < a.nchunks && !done; c += kFixBatch) {
+    float h[kFixBatch][NV];
+    uint32_t kend[kFixBatch];
+#pragma unroll
+    for (int u = 0; u < kFixBatch; ++u) {
+      const int cc = c + u < a.nchunks ? c + u : a.nchunks - 1;
+      const float* hp = a.part + ((int64_t)cc * 2) * a.D;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) h[u][j] = lane + 64 * j < a.D ? hp[lane + 64 * j] : 0.f;
+      const int64_t end = (int64_t)cc * kChunk + kChunk;  // first position after chunk cc
+      kend[u] = end < a.n ? a.keys[end] : kSentinel;
+    }
+#pragma unroll
+    for (int u = 0; u < kFixBatch; ++u) {
+      if (done || c + u >= a.nchunks) { done = true; continue; }
+#pragma unroll
+      for (int j = 0; j < NV; ++j) acc[j] += h[u][j];
+      if (kend[u] != key) done = true;  // the run ends in chunk c + u
+    }
+  }
+  put_row<NV>(a, key, acc);
+}
+
+AdamConst make_hyper(float b1, float b2, float eps, float wd) {
+  AdamConst h;
+  h.one_m_b1 = 1.f - b1; h.b2 = b2; h.one_m_b2 = 1.f - b2; h.eps = eps; h.wd = wd;
+  return h;
+}
+
+int64_t sort_ws_bytes(int64_t n, int64_t vocab) {
+  if (n <= kSortTile) return 0;
+  const SortPlan p = make_plan(n, vocab);
+  return 2 * n * 4 + ((int64_t)kMaxRadix * p.ntiles + kMaxRadix) * 4 + 256;
+}
+
+}  // namespace
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int64_t rs_lookup_sort_ws_bytes(int64_t n, int64_t vocab) { return sort_ws_bytes(n, vocab); }
+
+extern "C" int rs_lookup_sort(const void* ids, int id_bytes, int rows, int bag, int64_t row_stride,
+                              int64_t vocab, uint32_t* keys, uint32_t* vals, void* ws, void* stream) {
+  RS_CHECK_ARG(ids && keys && vals && rows >= 0 && bag >= 1 && row_stride >= bag &&
+                   (id_bytes == 4 || id_bytes == 8) && vocab >= 1 && vocab < ((int64_t)1 << 31),
+               "rs_lookup_sort: bad args");
+  const int64_t n = (int64_t)rows * bag;
+  RS_CHECK_ARG(n < ((int64_t)1 << 31), "rs_lookup_sort: %lld lookups exceed 2^31", (long long)n);
+  if (n == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  const SortPlan p = make_plan(n, vocab);
+  if (n <= kSortTile) {
+    sort_tile_kernel<<<1, kSortThreads, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, (int)n, p,
+                                                keys, vals);
+    RS_CHECK_LAUNCH("rs_lookup_sort tile");
+    return 0;
+  }
+  RS_CHECK_ARG(ws, "rs_lookup_sort: workspace needed for %lld lookups", (long long)n);
+  uint32_t* tk = static_cast<uint32_t*>(ws);
+  uint32_t* tv = tk + n;
+  int* hist = reinterpret_cast<int*>(tv + n);
+  int* tot = hist + (int64_t)kMaxRadix * p.ntiles;
+  // ping-pong so that the last pass lands in (keys, vals)
+  for (int q = 0; q < p.passes; ++q) {
+    const bool to_out = ((p.passes - 1 - q) & 1) == 0;
+    uint32_t* kd = to_out ? keys : tk;
+    uint32_t* vd = to_out ? vals : tv;
+    const uint32_t* ks = q == 0 ? nullptr : (to_out ? tk : keys);
+    const uint32_t* vs = q == 0 ? nullptr : (to_out ? tv : vals);
+    sort_hist_kernel<<<p.ntiles, kSortThreads, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, ks, n,
+                                                        p.shift[q], p.dbits[q], hist);
+    RS_CHECK_LAUNCH("rs_lookup_sort hist");
+    sort_scan_kernel<<<1 << p.dbits[q], 256, 0, st>>>(hist, p.ntiles, tot);
+    RS_CHECK_LAUNCH("rs_lookup_sort scan");
+    sort_scatter_kernel<<<p.ntiles, kSortThreads, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, ks,
+                                                           vs, n, p.shift[q], p.dbits[q], hist, tot,
+                                                           kd, vd);
+    RS_CHECK_LAUNCH("rs_lookup_sort scatter");
+  }
+  return 0;
+}
+
+static int sorted_rows(int op, const uint32_t* keys, int64_t n, int D, float* p, float* g, float* m,
+                       float* v, int* last, int* owner, int call, const int64_t* step,
+                       const float* consts, float b1, float b2, float eps, float wd, float scale,
+                       const float* coef, double* ws, hipStream_t st) {
+  if (n == 0 && op != kSqnorm) return 0;
+  RowArgs a;
+  a.keys = keys; a.n = n; a.D = D; a.p = p; a.g = g; a.m = m; a.v = v; a.last = last;
+  a.owner = owner; a.call = call; a.step = step;
+  a.consts = reinterpret_cast<const float2*>(consts); a.h = make_hyper(b1, b2, eps, wd);
+  a.scale = scale; a.coef = coef; a.ws = ws;
+  // lanes per row: 4 columns each, a power of two in [4, 64]
+  const int G = D <= 16 ? 4 : D <= 32 ? 8 : D <= 64 ? 16 : D <= 128 ? 32 : 64;
+  int grid = op == kSqnorm ? kRowGrid
+                           : std::max<int64_t>(1, std::min<int64_t>(kRowGrid * 4, cdiv(n, 256 / G * kRowUnroll)));
+  const bool u1 = !getenv_flag("RSYS_ROW_UNROLL4");  // A/B switch: 4 rows per group iteration (slower: occupancy)
+  if (u1 && op != kSqnorm) grid = std::max<int64_t>(1, std::min<int64_t>(kRowGrid * 4, cdiv(n, 256 / G)));
+#define RS_ROWS_U(OPV, UV)                                                        \
+  switch (G) {                                                                    \
+    case 4: sorted_rows_kernel<OPV, 4, UV><<<grid, 256, 0, st>>>(a); break;        \
+    case 8: sorted_rows_kernel<OPV, 8, UV><<<grid, 256, 0, st>>>(a); break;        \
+    case 16: sorted_rows_kernel<OPV, 16, UV><<<grid, 256, 0, st>>>(a); break;      \
+    case 32: sorted_rows_kernel<OPV, 32, UV><<<grid, 256, 0, st>>>(a); break;      \
+    default: sorted_rows_kernel<OPV, 64, UV><<<grid, 256, 0, st>>>(a); break;      \
+  }
+#define RS_ROWS(OPV) if (u1) { RS_ROWS_U(OPV, 1) } else { RS_ROWS_U(OPV, 4) }
+  switch (op) {
+    case kCatchup: RS_ROWS(kCatchup) break;
+    case kAdam: RS_ROWS(kAdam) break;
+    case kSqnorm: RS_ROWS(kSqnorm) break;
+    case kOwner: RS_ROWS(kOwner) break;
+    default: RS_ROWS(kZero) break;
+  }
+#undef RS_ROWS_U
+#undef RS_ROWS
+  RS_CHECK_LAUNCH("rs_sorted_rows");
+  return 0;
+}
+
+extern "C" int rs_sorted_catchup(const uint32_t* keys, int64_t n, int D, float* p, float* m, float* v,
+                                 int* last, const int64_t* step, const float* consts, float beta1,
+                                 float beta2, float eps, float weight_decay, void* stream) {
+  RS_CHECK_ARG(keys && p && m && v && last && step && consts && D >= 1 && n >= 0,
+               "rs_sorted_catchup: bad args");
+  return sorted_rows(kCatchup, keys, n, D, p, nullptr, m, v, last, nullptr, 0, step, consts, beta1,
+                     beta2, eps, weight_decay, 1.f, nullptr, nullptr, as_stream(stream));
+}
+
+extern "C" int rs_sorted_adam(const uint32_t* keys, int64_t n, int D, float* p, float* g, float* m,
+                              float* v, int* last, int* owner, int call, const int64_t* step,
+                              const float* consts, float beta1, float beta2, float eps,
+                              float weight_decay, float scale, const float* coef, void* stream) {
+  RS_CHECK_ARG(keys && p && g && m && v && last && step && consts && D >= 1 && n >= 0,
+               "rs_sorted_adam: bad args");
+  return sorted_rows(kAdam, keys, n, D, p, g, m, v, last, owner, call, step, consts, beta1, beta2,
+                     eps, weight_decay, scale, coef, nullptr, as_stream(stream));
+}
+
+extern "C" int rs_sorted_sqnorm_parts(void) { return kRowGrid; }
+
+extern "C" int rs_sorted_sqnorm(const uint32_t* keys, int64_t n, int D, const float* g, int* owner,
+                                int call, float scale, double* ws, void* stream) {
+  RS_CHECK_ARG(keys && g && ws && D >= 1 && n >= 0, "rs_sorted_sqnorm: bad args");
+  return sorted_rows(kSqnorm, keys, n, D, nullptr, const_cast<float*>(g), nullptr, nullptr, nullptr,
+                     owner, call, nullptr, nullptr, 0.f, 0.f, 0.f, 0.f, scale, nullptr, ws,
+                     as_stream(stream));
+}
+
+extern "C" int rs_sorted_owner(const uint32_t* keys, int64_t n, int* owner, int call, void* stream) {
+  RS_CHECK_ARG(keys && owner && n >= 0, "rs_sorted_owner: bad args");
+  return sorted_rows(kOwner, keys, n, 1, nullptr, nullptr, nullptr, nullptr, nullptr, owner, call,
+                     nullptr, nullptr, 0.f, 0.f, 0.f, 0.f, 1.f, nullptr, nullptr, as_stream(stream));
+}
+
+extern "C" int rs_sorted_zero_grad(const uint32_t* keys, int64_t n, int D, float* g, void* stream) {
+  RS_CHECK_ARG(keys && g && D >= 1 && n >= 0, "rs_sorted_zero_grad: bad args");
+  return sorted_rows(kZero, keys, n, D, nullptr, g, nullptr, nullptr, nullptr, nullptr, 0, nullptr,
+                     nullptr, 0.f, 0.f, 0.f, 0.f, 1.f, nullptr, nullptr, as_stream(stream));
+}
+
+extern "C" int64_t rs_segsum_ws_bytes(int64_t n, int D) {
+  const int64_t nc = (n + kChunk - 1) / kChunk;
+  return nc * 2 * D * 4 + nc * 4 + 256;
+}
+
+extern "C" int rs_segsum(const uint32_t* keys, const uint32_t* vals, int64_t n, int bag, int mode,
+                         int64_t pad, const float* dout, int64_t ldo, int D, float* grad,
+                         int accumulate, void* ws, void* stream) {
+  RS_CHECK_ARG(keys && vals && dout && grad && ws && n >= 0 && bag >= 1 && mode >= 0 && mode <= 2 &&
+                   D >= 1 && D <= 256 && ldo >= D,
+               "rs_segsum: bad args");
+  if (n == 0) return 0;
+  RS_CHECK_ARG(n < ((int64_t)1 << 31), "rs_segsum: n too large");
+  SegArgs a;
+  a.keys = keys; a.vals = vals; a.n = n; a.bag = bag; a.mode = mode; a.pad = pad; a.dout = dout;
+  a.ldo = ldo; a.D = D; a.grad = grad; a.accumulate = accumulate;
+  a.nchunks = cdiv(n, kChunk);
+  a.part = static_cast<float*>(ws);
+  a.flags = reinterpret_cast<int*>(a.part + (int64_t)a.nchunks * 2 * D);
+  hipStream_t st = as_stream(stream);
+  const int grid = cdiv(a.nchunks, 4);
+#define RS_SEGSUM(NV)                                                  \
+  segsum_kernel<NV><<<grid, 256, 0, st>>>(a);                          \
+  RS_CHECK_LAUNCH("rs_segsum");                                        \
+  segsum_fixup_kernel<NV><<<grid, 256, 0, st>>>(a);                    \
+  RS_CHECK_LAUNCH("rs_segsum fixup");
+  if (D <= 64) { RS_SEGSUM(1) }
+  else if (D <= 128) { RS_SEGSUM(2) }
+  else { RS_SEGSUM(4) }
+#undef RS_SEGSUM
+  return 0;
+}
+
+// ---------------------------------------------------------------- data-parallel exchange packing
+// The data-parallel exchange of a large table (dist.py) all-gathers, per lookup call, the ids as
+// int32 [rows, bag] and the call's output gradient [rows, D]; every rank then sorts the gathered
+// ids and runs rs_segsum over them (identical inputs -> bitwise identical gradients on every rank).
+namespace rs {
+namespace {
+__global__ void pack_ids_kernel(const void* __restrict__ ids, int id_bytes, int64_t rows, int bag,
+                                int64_t stride, int32_t* __restrict__ out) {
+  const int64_t n = rows * bag;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / bag, l = e - r * bag;
+    out[e] = id_bytes == 8 ? (int32_t) static_cast<const int64_t*>(ids)[r * stride + l]
+                           : static_cast<const int32_t*>(ids)[r * stride + l];
+  }
+}
+
+__global__ void pack_rows_kernel(const float* __restrict__ src, int64_t ld, int64_t rows, int D,
+                                 float* __restrict__ dst) {
+  const int64_t n = rows * D;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / D;
+    dst[e] = src[r * ld + (e - r * D)];
+  }
+}
+}  // namespace
+}  // namespace rs
+
+extern "C" int rs_pack_ids(const void* ids, int id_bytes, int64_t rows, int bag, int64_t row_stride,
+                           int32_t* out, void* stream) {
+  RS_CHECK_ARG(ids && out && rows >= 0 && bag >= 1 && row_stride >= bag &&
+                   (id_bytes == 4 || id_bytes == 8),
+               "rs_pack_ids: bad args");
+  const int64_t n = rows * bag;
+  if (n == 0) return 0;
+  pack_ids_kernel<<<std::min<int64_t>(cdiv(n, 256), 8192), 256, 0, as_stream(stream)>>>(
+      ids, id_bytes, rows, bag, row_stride, out);
+  RS_CHECK_LAUNCH("rs_pack_ids");
+  return 0;
+}
+
+extern "C" int rs_pack_rows(const float* src, int64_t ld, int64_t rows, int D, float* dst,
+                            void* stream) {
+  RS_CHECK_ARG(src && dst && rows >= 0 && D >= 1 && ld >= D, "rs_pack_rows: bad args");
+  const int64_t n = rows * D;
+  if (n == 0) return 0;
+  pack_rows_kernel<<<std::min<int64_t>(cdiv(n, 256), 8192), 256, 0, as_stream(stream)>>>(
+      src, ld, rows, D, dst);
+  RS_CHECK_LAUNCH("rs_pack_rows");
+  return 0;
+}

@@ -4,6 +4,7 @@
 // step is one streaming kernel (28 B/param: read p, g, m, v; write p, m, v) regardless of how
 // many tensors the model has. The clip coefficient stays on the device: no host sync.
 #include "common.h"
+#include "adam.h"
 
 // no fma contraction: the dense and the lazy (sparse.hip) Adam must round identically
 #pragma clang fp contract(off)
@@ -78,7 +79,8 @@ __global__ void scale_kernel(float* __restrict__ g, int64_t n, float scale,
 struct AdamArgs {
   float* p; float* g; float* m; float* v;
   int64_t n;
-  float lr, step_size, b1, b2, one_m_b1, one_m_b2, eps, wd, bc2_sqrt, scale;
+  float lr, step_size, b1, b2, eps, wd, inv_bc2_sqrt, scale;
+  AdamConst h;
   const float* coef;
   const int64_t* step_dev;  // when set, bias corrections come from *step_dev (graph replay)
   int write_grad;
@@ -86,23 +88,16 @@ struct AdamArgs {
 
 __device__ __forceinline__ void adam_elem(const AdamArgs& a, float s, float& p, float& g, float& m,
                                           float& v) {
-  float gs = g * s;
+  const float gs = g * s;
   if (a.write_grad) g = gs;
-  if (a.wd != 0.f) gs = gs + a.wd * p;
-  m = m + a.one_m_b1 * (gs - m);                // exp_avg.lerp_(grad, 1 - beta1)
-  v = v * a.b2 + a.one_m_b2 * gs * gs;          // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
-  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
-  p = p - a.step_size * (m / denom);            // param.addcdiv_(exp_avg, denom, -step_size)
+  adam_update(a.h, a.step_size, a.inv_bc2_sqrt, gs, p, m, v);
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const float s = a.scale * (a.coef ? *a.coef : 1.f);
-  if (a.step_dev) {
-    const double t = (double)*a.step_dev;
-    const double bc1 = 1.0 - pow((double)a.b1, t), bc2 = 1.0 - pow((double)a.b2, t);
-    a.step_size = (float)((double)a.lr / bc1);
-    a.bc2_sqrt = (float)sqrt(bc2);
-  }
+  if (a.step_dev)
+    adam_step_consts((double)a.lr, (double)a.b1, (double)a.b2, (double)*a.step_dev, &a.step_size,
+                     &a.inv_bc2_sqrt);
   const int64_t stride = (int64_t)gridDim.x * 256;
   const bool vec = ((reinterpret_cast<uintptr_t>(a.p) | reinterpret_cast<uintptr_t>(a.g) |
                      reinterpret_cast<uintptr_t>(a.m) | reinterpret_cast<uintptr_t>(a.v)) & 15) == 0;
@@ -140,20 +135,6 @@ __global__ void counter_add_kernel(int64_t* c, int64_t delta) { *c += delta; }
 using namespace rs;
 
 extern "C" int64_t rs_sqnorm_ws_bytes(int64_t n) { return (int64_t)sq_blocks(n) * sizeof(double); }
-
-__global__ void zero_rows_kernel(float* __restrict__ g, const int* __restrict__ list,
-                                 const int* __restrict__ count, int D) {
-  const int n = *count;
-  for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4)
-    for (int c = threadIdx.x & 63; c < D; c += 64) g[(int64_t)list[i] * D + c] = 0.f;
-}
-
-extern "C" int rs_sparse_zero_grad(float* g, const int* list, const int* count, int D, void* stream) {
-  RS_CHECK_ARG(g && list && count && D >= 1, "rs_sparse_zero_grad: bad args");
-  zero_rows_kernel<<<1024, 256, 0, as_stream(stream)>>>(g, list, count, D);
-  RS_CHECK_LAUNCH("rs_sparse_zero_grad");
-  return 0;
-}
 
 extern "C" int rs_grad_sqnorm(const float* g, int64_t n, float scale, double* ws, void* stream) {
   RS_CHECK_ARG(g && ws && n >= 0, "rs_grad_sqnorm: bad args");
@@ -209,14 +190,12 @@ extern "C" int rs_adam_step(float* p, float* g, float* m, float* v, int64_t n, f
   AdamArgs a;
   a.p = p; a.g = g; a.m = m; a.v = v; a.n = n;
   const double t = step >= 1 ? (double)step : 1.0;
-  const double bc1 = 1.0 - pow((double)beta1, t);
-  const double bc2 = 1.0 - pow((double)beta2, t);
   a.lr = lr;
   a.step_dev = step_dev;
-  a.step_size = (float)((double)lr / bc1);
-  a.bc2_sqrt = (float)sqrt(bc2);
+  adam_step_consts((double)lr, (double)beta1, (double)beta2, t, &a.step_size, &a.inv_bc2_sqrt);
   a.b1 = beta1; a.b2 = beta2;
-  a.one_m_b1 = 1.f - beta1; a.one_m_b2 = 1.f - beta2;
+  a.h.one_m_b1 = 1.f - beta1; a.h.b2 = beta2; a.h.one_m_b2 = 1.f - beta2; a.h.eps = eps;
+  a.h.wd = weight_decay;
   a.eps = eps; a.wd = weight_decay; a.scale = scale; a.coef = coef; a.write_grad = write_grad;
   int64_t blocks = (n / 4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;

@@ -6,10 +6,14 @@ and an identical clip + Adam on every rank. Parameters are broadcast from rank 0
 
 Large tables trained by lazy-exact Adam (flat.py) stay replicated (a 10M x 128 table with its
 Adam state is ~20 GB: it fits 288 GB of HBM many times over) but their gradient is NOT
-all-reduced densely (5 GB per table per step): each rank packs only the rows its batch touched,
-one all-gather moves [ids | rows] of every rank, and every rank adds the W buffers in rank order
-and rebuilds the touched-row list in ascending order, so all ranks hold bitwise-identical
-gradients and lists (csrc/sparse.hip rs_sparse_pack / rs_sparse_unpack_add / rs_sparse_compact).
+all-reduced densely (5 GB per table per step). SURVEY §8e's bag-gradient exchange instead: for
+every lookup call of such a table the backward keeps the call's OUTPUT gradient ([rows, D]: the
+pooled bag gradient, the single-id feature gradient, or the per-token gradient); one all-gather
+moves every rank's [rows, bag] int32 ids and [rows, D] gradient (C3 pooled history: 0.8 + 2 MB
+per rank), and every rank sorts the gathered ids and runs the deterministic segment sum over
+them (csrc/lookup.hip). All ranks therefore hold bitwise-identical gradient rows and step the
+same rows in the same order: the clip norm and Adam agree bitwise, with no host sync and no
+count exchange.
 """
 from __future__ import annotations
 
@@ -87,35 +91,57 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+class _ExchangeBuffers:
+    """Per (table, call) all-gather buffers, reused while the call shapes stay the same."""
+
+    def __init__(self):
+        self.bufs = {}
+
+    def get(self, key, shape, dtype, dev):
+        b = self.bufs.get(key)
+        if b is None or b.shape != shape or b.dtype != dtype or b.device != dev:
+            b = torch.empty(shape, dtype=dtype, device=dev)
+            self.bufs[key] = b
+        return b
+
+
+def _all_gather(out, inp):
+    if dist.get_backend() == 'nccl':
+        dist.all_gather_into_tensor(out, inp)
+    else:
+        dist.all_gather(list(out.chunk(dist.get_world_size())), inp)
+
+
 def exchange_lazy_grads(f):
-    """Row-sparse gradient exchange of every lazy table of flat buffer f (see module doc)."""
+    """Bag-gradient exchange of every lazy table of flat buffer f (see module doc)."""
     world = dist.get_world_size()
     dev = f.data.device
-    # ids looked up since the last exchange (host count; a replayed hipGraph does not re-run the
-    # host side, so the last non-zero count stands in for the replayed forward)
     for t in f.lazy:
-        if t.cap > 0:
-            t.cap_used, t.cap = t.cap, 0
-    caps = torch.tensor([max(1, min(t.cap_used, t.V)) for t in f.lazy], dtype=torch.int64, device=dev)
-    dist.all_reduce(caps, op=dist.ReduceOp.MAX)
-    caps = caps.tolist()
-    nccl = dist.get_backend() == 'nccl'
-    for t, cap in zip(f.lazy, caps):
-        n = cap * (t.D + 1)
-        buf = torch.empty(n, dtype=torch.float32, device=dev)
-        _hip.call('rs_sparse_pack', t.ptr(f.grad), t.list.data_ptr(), t.count.data_ptr(), t.D, cap,
-                  buf.data_ptr(), None, _stream())
-        allbuf = torch.empty(world * n, dtype=torch.float32, device=dev)
-        if nccl:
-            dist.all_gather_into_tensor(allbuf, buf)
-        else:
-            dist.all_gather(list(allbuf.split(n)), buf)
-        _hip.call('rs_sparse_zero_grad', t.ptr(f.grad), t.list.data_ptr(), t.count.data_ptr(), t.D,
-                  _stream())
-        for r in range(world):  # fixed summation order: identical rows on every rank
-            _hip.call('rs_sparse_unpack_add', t.ptr(f.grad), t.flag.data_ptr(),
-                      allbuf.data_ptr() + 4 * r * n, t.D, cap, _stream())
-        ws = torch.empty(int(_hip.lib().rs_sparse_compact_ws_bytes(t.V)) // 4 + 1, dtype=torch.int32,
-                         device=dev)
-        _hip.call('rs_sparse_compact', t.flag.data_ptr(), t.V, t.list.data_ptr(), t.count.data_ptr(),
-                  ws.data_ptr(), _stream())
+        if not t.calls:
+            continue
+        bufs = getattr(t, '_dp_bufs', None)
+        if bufs is None:
+            bufs = t._dp_bufs = _ExchangeBuffers()
+        union = []
+        for i, c in enumerate(t.calls):
+            if c.mode < 0:
+                raise NotImplementedError('data-parallel max-pooled large tables (arg-max scatter) '
+                                          'are not supported')
+            if c.dseg is None:  # looked up without a backward (e.g. under no_grad)
+                continue
+            ids = bufs.get(('ids', i), (c.n,), torch.int32, dev)
+            _hip.call('rs_pack_ids', c.ids_ptr, c.id_bytes, c.rows, c.bag, c.row_stride, ids.data_ptr(),
+                      _stream())
+            all_ids = bufs.get(('all_ids', i), (world * c.n,), torch.int32, dev)
+            all_g = bufs.get(('all_g', i), (world * c.rows, t.D), torch.float32, dev)
+            _all_gather(all_ids, ids)
+            _all_gather(all_g, c.dseg)
+            union.append((all_ids, all_g, c))
+        calls = []
+        for all_ids, all_g, c in union:
+            u = t.sort_call(all_ids.data_ptr(), world * c.rows, c.bag, c.bag, c.pad, c.mode, id_bytes=4,
+                            keep=(all_ids, all_g))
+            calls.append((u, all_g))
+        t.exchanged = [u for u, _ in calls]
+        for u, all_g in calls:
+            t.segsum(u, all_g.data_ptr(), t.D, accumulate=len(calls) > 1)

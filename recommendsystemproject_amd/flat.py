@@ -10,8 +10,8 @@ slots, reference parameters() order) and every .grad into a second one. Conseque
 
 Large embedding tables (>= RSYS_LAZY_ROWS rows, default 65536) are placed after every other
 parameter and trained by lazy-exact Adam (csrc/sparse.hip, trap T16): each one gets a LazyTable
-(per-row `last` step, touched-row flag/list/count). The dense kernels then only sweep
-[0, dense_numel); the tables are touched row-by-row. State (weights, exp_avg, exp_avg_sq) stays
+(per-row `last` step, this step's sorted lookups: csrc/lookup.hip). The dense kernels then only
+sweep [0, dense_numel); the tables are touched row-by-row. State (weights, exp_avg, exp_avg_sq) stays
 bitwise what dense Adam would produce; rows are brought current before every read (forward
 gather, state_dict, load_state_dict).
 """
@@ -30,35 +30,125 @@ def lazy_rows_threshold() -> int:
     return int(os.environ.get('RSYS_LAZY_ROWS', 1 << 16))
 
 
+class LookupCall:
+    """One forward lookup of a large table: the call's ids sorted by row (rs_lookup_sort).
+    keys[n] = row ids ascending (out-of-range ids last as 0xFFFFFFFF), vals[n] = lookup index
+    r * bag + l, ascending within a row. Kept until the optimizer step (catch-up, gradient
+    segment sums, clip norm and Adam all walk the distinct rows of `keys`). Under data
+    parallelism the backward keeps the call's output gradient rows (dseg) for the exchange."""
+
+    __slots__ = ('keys', 'vals', 'n', 'rows', 'bag', 'pad', 'mode', 'ids_ptr', 'id_bytes',
+                 'row_stride', 'keep', 'dseg')
+
+    def __init__(self, keys, vals, n, rows, bag, pad, mode, ids_ptr, id_bytes, row_stride, keep):
+        self.keys, self.vals, self.n, self.rows, self.bag = keys, vals, n, rows, bag
+        self.pad, self.mode = pad, mode
+        self.ids_ptr, self.id_bytes, self.row_stride, self.keep = ids_ptr, id_bytes, row_stride, keep
+        self.dseg = None
+
+
+# rs_segsum modes: one id per gradient row, mean bag, sum bag (max pooling: atomic scatter)
+SEG_ONE, SEG_MEAN, SEG_SUM = 0, 1, 2
+
+
 class LazyTable:
-    """Row bookkeeping of one large [V, D] table trained by lazy-exact Adam."""
+    """Row bookkeeping of one large [V, D] table trained by lazy-exact Adam.
+
+    Every lookup of the table in a step is a LookupCall (sorted ids). Per step:
+      forward  : rs_lookup_sort, then rs_sorted_catchup brings the call's rows to the current
+                 optimizer step before the gather reads them;
+      backward : rs_segsum writes each distinct row's gradient (plain stores; added to the row
+                 when the table has several calls this step), deterministic;
+      optimizer: rs_sorted_sqnorm (clip-norm partials) and rs_sorted_adam over each call's
+                 distinct rows; a row looked up by several calls is stepped once, by the first
+                 (rs_sorted_owner). The calls are then dropped.
+    The gradient rows of a large table are zero except the rows of this step's calls."""
 
     def __init__(self, flat, index, param, offset):
         self.flat, self.index, self.param, self.offset = flat, index, param, offset
         self.V, self.D = int(param.shape[0]), int(param.shape[1])
         dev = param.device
-        self.flag = torch.zeros(self.V, dtype=torch.int32, device=dev)
-        self.list = torch.zeros(self.V, dtype=torch.int32, device=dev)
-        self.count = torch.zeros(1, dtype=torch.int32, device=dev)
         self.last = torch.zeros(self.V, dtype=torch.int32, device=dev)
-        self.cap = 0       # ids looked up since the last DP exchange (upper bound of count)
-        self.cap_used = 0  # the count the last exchange used
+        self.owner = None   # [V] lowest call index per row; allocated for multi-call steps
+        self.calls = []     # this step's LookupCalls, in forward order
+        self.exchanged = None  # data parallel: the union calls that replaced the local ones
 
     def ptr(self, t):
         return t.data_ptr() + 4 * self.offset
 
-    def touch(self, ids, rows, bag, row_stride, pad):
-        """Forward hook: list this step's rows and bring them to the current optimizer step
-        before they are gathered."""
-        _hip.call('rs_sparse_touch', ids, rows, bag, row_stride, self.V, pad, self.flag.data_ptr(),
-                  self.list.data_ptr(), self.count.data_ptr(), _stream())
-        self.cap += rows * bag
+    def sort_call(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None):
+        """Sort a [rows, bag] id matrix by row (rs_lookup_sort) into a LookupCall."""
+        dev = self.param.device
+        n = rows * bag
+        keys = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        vals = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        wsb = int(_hip.lib().rs_lookup_sort_ws_bytes(n, self.V))
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.int32, device=dev) if wsb else None
+        _hip.call('rs_lookup_sort', ids_ptr, id_bytes, rows, bag, row_stride, self.V, keys.data_ptr(),
+                  vals.data_ptr(), None if ws is None else ws.data_ptr(), _stream())
+        return LookupCall(keys, vals, n, rows, bag, -1 if pad is None else int(pad), mode, ids_ptr,
+                          id_bytes, row_stride, keep)
+
+    def lookup(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None):
+        """Forward hook: sort the call's ids, list it for the step, and bring its rows to the
+        current optimizer step before they are gathered."""
+        c = self.sort_call(ids_ptr, rows, bag, row_stride, pad, mode, id_bytes, keep)
+        self.calls.append(c)
+        self.catchup(c)
+        return c
+
+    def catchup(self, c):
         opt = self.flat.lazy_opt
-        if opt is not None:
-            _hip.call('rs_sparse_catchup', self.ptr(self.flat.data), self.ptr(opt['m']),
-                      self.ptr(opt['v']), self.last.data_ptr(), self.list.data_ptr(),
-                      self.count.data_ptr(), self.D, opt['step_dev'].data_ptr(),
-                      opt['consts'].data_ptr(), *opt['hyper'], _stream())
+        if opt is not None and c.n > 0:
+            _hip.call('rs_sorted_catchup', c.keys.data_ptr(), c.n, self.D, self.ptr(self.flat.data),
+                      self.ptr(opt['m']), self.ptr(opt['v']), self.last.data_ptr(),
+                      opt['step_dev'].data_ptr(), opt['consts'].data_ptr(), *opt['hyper'], _stream())
+
+    def segsum(self, c, dout_ptr, ldo, accumulate=None):
+        """Backward: the table gradient of call c from its output gradient (dout_ptr = the
+        feature's first column, row stride ldo floats). Under data parallelism a local call only
+        keeps its output gradient rows; dist.exchange_lazy_grads sums every rank's."""
+        if c.n == 0:
+            return
+        dev = self.param.device
+        if accumulate is None:
+            if _dp_active():
+                c.dseg = torch.empty(c.rows, self.D, dtype=torch.float32, device=dev)
+                _hip.call('rs_pack_rows', dout_ptr, ldo, c.rows, self.D, c.dseg.data_ptr(), _stream())
+                return
+            accumulate = len(self.calls) > 1
+        ws = torch.empty(int(_hip.lib().rs_segsum_ws_bytes(c.n, self.D)) // 4 + 1, dtype=torch.int32,
+                         device=dev)
+        _hip.call('rs_segsum', c.keys.data_ptr(), c.vals.data_ptr(), c.n, c.bag, c.mode, c.pad,
+                  dout_ptr, ldo, self.D, self.ptr(self.flat.grad), int(accumulate), ws.data_ptr(),
+                  _stream())
+
+    def step_calls(self):
+        """The calls whose rows the optimizer steps (the data-parallel union calls once the
+        gradients were exchanged). Output gradients kept for an exchange that did not happen
+        (a model stepped without dist.allreduce_gradients inside a distributed job) are
+        segment-summed locally here, so the gradient is never lost."""
+        if self.exchanged is not None:
+            return self.exchanged
+        for c in self.calls:
+            if c.dseg is not None:
+                g, c.dseg = c.dseg, None
+                self.segsum(c, g.data_ptr(), self.D, accumulate=len(self.calls) > 1)
+        return self.calls
+
+    def mark_owners(self):
+        calls = self.step_calls()
+        if len(calls) <= 1:
+            return None
+        if self.owner is None:
+            self.owner = torch.full((self.V,), 0x7fffffff, dtype=torch.int32, device=self.param.device)
+        for i, c in enumerate(calls):
+            _hip.call('rs_sorted_owner', c.keys.data_ptr(), c.n, self.owner.data_ptr(), i, _stream())
+        return self.owner
+
+    def end_step(self):
+        self.calls = []
+        self.exchanged = None
 
     def flush(self):
         opt = self.flat.lazy_opt
@@ -69,12 +159,23 @@ class LazyTable:
                   opt['consts'].data_ptr(), *opt['hyper'], _stream())
 
     def zero_grad(self):
-        _hip.call('rs_sparse_zero_grad', self.ptr(self.flat.grad), self.list.data_ptr(),
-                  self.count.data_ptr(), self.D, _stream())
+        """Zero the gradient rows of pending calls (a backward not followed by an optimizer
+        step) and drop them: their rows are current, and a row with a zero gradient needs no
+        explicit Adam step (the next catch-up replays it)."""
+        for c in self.calls + (self.exchanged or []):
+            if c.n > 0:
+                _hip.call('rs_sorted_zero_grad', c.keys.data_ptr(), c.n, self.D, self.ptr(self.flat.grad),
+                          _stream())
+        self.end_step()
 
 
 def _stream():
     return torch.cuda.current_stream().cuda_stream
+
+
+def _dp_active():
+    d = torch.distributed
+    return d.is_available() and d.is_initialized() and d.get_world_size() > 1
 
 
 def _is_lazy(p, lazy_ids):
@@ -220,11 +321,13 @@ def _flush_load_hook(module, state_dict, prefix, *args):
     _flush_table(module)  # rows become current, so the loaded weights start from `last` = step
 
 
-def touch_table(weight, ids_ptr, rows, bag, row_stride, pad):
-    """Forward-side hook of the custom ops for a table lookup (no-op for small tables)."""
+def lookup_table(weight, ids_ptr, rows, bag, row_stride, pad, mode, keep=None):
+    """Forward-side hook of the custom ops for a table lookup: a LookupCall for large
+    (lazy-Adam) tables, None for ordinary ones."""
     t = getattr(weight, '_rs_lazy', None)
-    if t is not None and rows > 0:
-        t.touch(ids_ptr, rows, bag, row_stride, -1 if pad is None else pad)
+    if t is None or flat_of(weight) is not t.flat:
+        return None
+    return t.lookup(ids_ptr, rows, bag, row_stride, pad, mode, keep=keep)
 
 
 def grad_of(p):

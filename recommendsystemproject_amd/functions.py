@@ -24,7 +24,7 @@ import torch
 from torch.autograd.function import once_differentiable
 
 from . import _hip, ops, precision
-from .flat import grad_of, touch_table
+from .flat import SEG_MEAN, SEG_ONE, SEG_SUM, grad_of, lookup_table
 
 
 def _seg(**kw):
@@ -39,14 +39,41 @@ def _pad(v):
     return -1 if v is None else int(v)
 
 
-def _touch_lazy(segs, tables, rows):
-    """Lazy-exact Adam tables (flat.py): list the rows this lookup reads and bring them to the
-    current optimizer step before the gather (no-op for ordinary tables)."""
-    for s, t in zip(segs, tables):
+def _lookup_lazy(segs, tables, rows, keep=None):
+    """Large (lazy-Adam) tables, flat.py: sort this call's ids by row (csrc/lookup.hip) and bring
+    those rows to the current optimizer step before the gather reads them. Returns
+    {segment index: LookupCall}; ordinary tables are not listed. `keep` (the id tensors the
+    segments point into) stays referenced by the calls until the optimizer step (the
+    data-parallel exchange re-reads the ids after the backward)."""
+    calls = {}
+    for i, (s, t) in enumerate(zip(segs, tables)):
         if s.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL) and hasattr(t, '_rs_lazy'):
-            bag = s.bag if s.kind == _hip.RS_SEG_POOL else 1
-            touch_table(t, s.idx, rows, bag, s.idx_stride, s.pad_idx)
-            s.touch_count = t._rs_lazy.flag.data_ptr()
+            pool = s.kind == _hip.RS_SEG_POOL
+            bag = s.bag if pool else 1
+            mode = SEG_ONE
+            if pool:
+                mode = {_hip.RS_POOL['mean']: SEG_MEAN, _hip.RS_POOL['sum']: SEG_SUM}.get(s.pool_mode)
+            if mode is not None and s.dim > 256:
+                mode = None
+            c = lookup_table(t, s.idx, rows, bag, s.idx_stride, None if s.pad_idx < 0 else s.pad_idx,
+                             -1 if mode is None else mode, keep=keep)
+            if c is not None:
+                calls[i] = c
+    return calls
+
+
+def _grad_lazy(segs, calls, dout, tables):
+    """Backward of the large-table segments: rs_segsum per call (deterministic, no atomics).
+    Returns the segments left for rs_gather_bwd (ordinary tables, dense, copies, and max-pooled
+    large tables, whose arg-max gradient keeps the atomic scatter)."""
+    rest = []
+    for i, s in enumerate(segs):
+        c = calls.get(i) if calls else None
+        if c is not None and c.mode >= 0:
+            tables[i]._rs_lazy.segsum(c, dout.data_ptr() + 4 * s.out_col, dout.stride(0))
+        else:
+            rest.append(s)
+    return rest
 
 
 # ================================================================================ sequence input
@@ -100,19 +127,19 @@ def seq_input_fwd(proc, seqd, B, L, p, key, err):
     M = B * L
     dev = proc.pos_emb.weight.device
     cat = torch.empty(M, dcat, device=dev, dtype=torch.float32)
-    _touch_lazy(segs, tables, M)
+    calls = _lookup_lazy(segs, tables, M, keep)
     ops.gather_fwd(segs, M, cat, err)
     lin = proc.feature_projection[0]
     pos = proc.pos_emb.weight
     # drop_b(drop_a(cat W^T + b) + pos[l]) in the GEMM epilogue (sites 0, 1 = rs_dropout masks)
     x = ops.linear_fwd(cat, lin.weight, lin.bias, aux=pos, aux_mod=L, drop_p=p, drop_key=key,
                        site_a=0, site_b=1)
-    return x, (segs, tables, cat, keep)
+    return x, (segs, tables, cat, keep, calls)
 
 
 def seq_input_bwd(proc, saved, dx, B, L, p, key):
     """Backward of seq_input_fwd; dx [B*L, d] is consumed (modified in place)."""
-    segs, tables, cat, _ = saved
+    segs, tables, cat, _, calls = saved
     d = proc.target_dim
     if p > 0:
         ops.dropout_bwd(dx, p, key, 1)
@@ -126,7 +153,9 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key):
     dcat = ops.linear_bwd_input(dx, lin.weight)
     for s, t in zip(segs, tables):
         s.grad = grad_of(t).data_ptr()
-    ops.gather_bwd(segs, B * L, dcat)
+    rest = _grad_lazy(segs, calls, dcat, tables)
+    if rest:
+        ops.gather_bwd(rest, B * L, dcat)
 
 
 # ================================================================================ encoder layer
@@ -500,10 +529,10 @@ class TowerFeatureFn(torch.autograd.Function):
             raise RuntimeError(f'too many features in one tower ({len(segs)} > {_hip.MAX_SEGMENTS})')
         dev = tower.feature_bn.weight.device
         out = torch.empty(B, col, device=dev, dtype=torch.float32)
-        _touch_lazy(segs, [w for w, _ in pp], B)
+        calls = _lookup_lazy(segs, [w for w, _ in pp], B, keep)
         ops.gather_fwd(segs, B, out, tower.err_flag)
         if need:
-            ctx.segs, ctx.pp, ctx.keep, ctx.B = segs, pp, keep, B
+            ctx.segs, ctx.pp, ctx.keep, ctx.B, ctx.calls = segs, pp, keep, B, calls
             ctx.has_seq = seq_vec is not None
             ctx.seq_shape = tuple(seq_vec.shape) if seq_vec is not None else None
         return out
@@ -522,8 +551,11 @@ class TowerFeatureFn(torch.autograd.Function):
         if ctx.has_seq:
             dseq = torch.empty(ctx.seq_shape, device=dout.device, dtype=torch.float32)
             segs[-1].grad = dseq.data_ptr()
-        ops.gather_bwd(segs, ctx.B, dout)
-        ctx.segs = ctx.keep = None
+        tables = [w for w, _ in ctx.pp] + [None] * (len(segs) - n_feat)
+        rest = _grad_lazy(segs, ctx.calls, dout, tables)
+        if rest:
+            ops.gather_bwd(rest, ctx.B, dout)
+        ctx.segs = ctx.keep = ctx.calls = None
         return (None, None, None, None, dseq) + (None,) * (len(ctx.needs_input_grad) - 5)
 
 

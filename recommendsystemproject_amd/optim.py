@@ -36,17 +36,23 @@ class _DeviceClip:
         self.coef = torch.ones((), device=device, dtype=torch.float32)
 
     def compute(self, g, n, max_norm, scale=1.0, lazy=()):
-        """2-norm of g[:n] plus the listed rows of every lazy table (their other rows hold no
-        gradient), one double partial per block, summed in one fixed order."""
+        """2-norm of g[:n] plus the distinct rows of every lazy table's step calls (their other
+        rows hold no gradient), one double partial per block, summed in one fixed order."""
         L = _hip.lib()
         nd = int(L.rs_sqnorm_parts(n))
-        ns = int(L.rs_sparse_sqnorm_parts())
-        ws = torch.empty(nd + ns * len(lazy) + 2, dtype=torch.float64, device=g.device)
+        ns = int(L.rs_sorted_sqnorm_parts())
+        work = []
+        for t in lazy:
+            owner = t.mark_owners()
+            for i, c in enumerate(t.step_calls()):
+                work.append((t, c, owner, i))
+        ws = torch.empty(nd + ns * len(work) + 2, dtype=torch.float64, device=g.device)
         _hip.call('rs_grad_sqnorm', g.data_ptr(), n, float(scale), ws.data_ptr(), ops.stream())
-        for k, t in enumerate(lazy):
-            _hip.call('rs_sparse_sqnorm', t.ptr(g), t.list.data_ptr(), t.count.data_ptr(), t.D,
-                      float(scale), ws.data_ptr() + 8 * (nd + k * ns), ops.stream())
-        _hip.call('rs_clip_coef', ws.data_ptr(), nd + ns * len(lazy), float(max_norm),
+        for k, (t, c, owner, i) in enumerate(work):
+            _hip.call('rs_sorted_sqnorm', c.keys.data_ptr(), c.n, t.D, t.ptr(g),
+                      None if owner is None else owner.data_ptr(), i, float(scale),
+                      ws.data_ptr() + 8 * (nd + k * ns), ops.stream())
+        _hip.call('rs_clip_coef', ws.data_ptr(), nd + ns * len(work), float(max_norm),
                   self.norm.data_ptr(), self.coef.data_ptr(), ops.stream())
 
 
@@ -177,11 +183,17 @@ class Adam(torch.optim.Optimizer):
                     f.lazy_opt = dict(m=st['m'], v=st['v'], step_dev=st['step_dev'],
                                       consts=st['consts'], hyper=hyper)
                     for t in f.lazy:
-                        _hip.call('rs_sparse_adam', t.ptr(f.data), t.ptr(f.grad), t.ptr(st['m']),
-                                  t.ptr(st['v']), t.last.data_ptr(), t.flag.data_ptr(),
-                                  t.list.data_ptr(), t.count.data_ptr(), t.D,
-                                  st['step_dev'].data_ptr(), st['consts'].data_ptr(), *hyper,
-                                  float(self.grad_scale), coef, ops.stream())
+                        owner = t.mark_owners() if coef is None else t.owner
+                        calls = t.step_calls()
+                        for i, c in enumerate(calls):
+                            if c.n == 0:
+                                continue
+                            _hip.call('rs_sorted_adam', c.keys.data_ptr(), c.n, t.D, t.ptr(f.data),
+                                      t.ptr(f.grad), t.ptr(st['m']), t.ptr(st['v']), t.last.data_ptr(),
+                                      None if owner is None or len(calls) <= 1 else owner.data_ptr(), i,
+                                      st['step_dev'].data_ptr(), st['consts'].data_ptr(), *hyper,
+                                      float(self.grad_scale), coef, ops.stream())
+                        t.end_step()
                 continue
             if clip_max_norm is not None and clip_max_norm > 0:
                 clip_grad_norm_(group['params'], clip_max_norm)

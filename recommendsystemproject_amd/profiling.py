@@ -46,8 +46,8 @@ def _gather_work(a, bwd=False):
         s = segs[i]
         if s.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL):
             bag = s.bag if s.kind == _hip.RS_SEG_POOL else 1
-            # table rows read (fwd) / atomically read-modify-written (bwd scatter-add) + int64 ids
-            byts += rows * bag * (s.dim * (8 if bwd else 4) + 8)
+            # table rows read (fwd) / scattered (bwd) + int64 ids
+            byts += rows * bag * (s.dim * 4 + 8)
         elif s.kind == _hip.RS_SEG_DENSE:
             byts += rows * 4
         else:
@@ -140,9 +140,12 @@ WORK = {
     'rs_batchnorm_fwd': _bn_work,
     'rs_batchnorm_bwd': lambda a: _bn_work(a, True),
     'rs_adam_step': _adam_work,
-    # lazy tables: ids read + flag read-modify-write; the row work of catch-up / sparse Adam
-    # depends on the device-side touched count and is timed only
-    'rs_sparse_touch': lambda a: (0.0, a[1] * a[2] * 12.0),
+    # large tables (csrc/lookup.hip): the sort reads the ids and writes keys + vals; the table
+    # gradient is priced by SURVEY §8d's gather formula (lookups x D x 4 + dout rows x D x 4 +
+    # ids) like the scatter it replaces; the per-row catch-up / Adam / sqnorm work depends on the
+    # device-side distinct-row count and is timed only
+    'rs_lookup_sort': lambda a: (0.0, a[2] * a[3] * (a[1] + 8.0)),
+    'rs_segsum': lambda a: (0.0, a[2] * a[8] * 4.0 + a[2] / a[3] * a[8] * 4.0 + a[2] * 4.0),
 }
 
 

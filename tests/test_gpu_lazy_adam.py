@@ -1,10 +1,19 @@
-"""Lazy-exact Adam for large tables (csrc/sparse.hip, flat.py; SURVEY.md §7.2 / trap T16).
+"""Sorted lookups and lazy-exact Adam for large tables (csrc/lookup.hip, csrc/sparse.hip, flat.py;
+SURVEY.md §7.2 / trap T16).
 
-The reference trains its embeddings with dense gradients and torch.optim.Adam, so every row
-moves every step once its exp_avg is non-zero. The lazy path touches only looked-up rows and
-replays the skipped zero-gradient steps when a row is next read; these tests require it to be
-BITWISE equal to the dense kernel on the same gradients, at every read and after a flush.
+The reference trains its embeddings with dense gradients (nn.Embedding -> embedding_dense_backward)
+and torch.optim.Adam, so every row moves every step once its exp_avg is non-zero. Here a large
+table's lookups are radix-sorted by row; the gradient is a deterministic segment sum over the
+sorted lookups, and only looked-up rows are stepped (skipped zero-gradient steps are replayed when
+a row is next read). These tests hold:
+  * the sort bit-exact against numpy's stable argsort (int64 / int32 ids, pad, out-of-range ids,
+    one-tile and multi-tile sizes, 300 .. 100M-row vocabularies);
+  * the segment sum against a float64 restatement of embedding_dense_backward (single ids, mean
+    and sum bags, Zipf-skewed ids whose hot rows span hundreds of chunks), bitwise reproducible;
+  * lazy Adam BITWISE equal to the dense kernel on the same gradients, at every read and after a
+    flush, with one and with several lookup calls per step.
 """
+import numpy as np
 import pytest
 import torch
 
@@ -13,61 +22,208 @@ from recommendsystemproject_amd import _hip, ops
 pytestmark = pytest.mark.gpu
 DEV = torch.device('cuda:0')
 LR, B1, B2, EPS = 1e-2, 0.9, 0.999, 1e-8
+SENT = 0xFFFFFFFF
 
 
-def _i32(n):
-    return torch.zeros(n, dtype=torch.int32, device=DEV)
+def _sort(ids, vocab, bag=None, stride=None):
+    """rs_lookup_sort of a [rows, bag] id tensor on the device -> (keys, vals) as numpy uint32."""
+    rows = ids.shape[0]
+    bag = bag or (ids.shape[1] if ids.dim() == 2 else 1)
+    stride = stride or (ids.stride(0) if ids.dim() == 2 else 1)
+    n = rows * bag
+    keys = torch.empty(max(n, 1), dtype=torch.int32, device=DEV)
+    vals = torch.empty(max(n, 1), dtype=torch.int32, device=DEV)
+    wsb = int(_hip.lib().rs_lookup_sort_ws_bytes(n, vocab))
+    ws = torch.empty(wsb // 4 + 1, dtype=torch.int32, device=DEV) if wsb else None
+    _hip.call('rs_lookup_sort', ids.data_ptr(), ids.element_size(), rows, bag, stride, vocab,
+              keys.data_ptr(), vals.data_ptr(), None if ws is None else ws.data_ptr(), ops.stream())
+    return keys, vals
 
 
-@pytest.mark.parametrize('D,wd,clip', [(40, 0.0, False), (128, 0.0, True), (16, 0.0, False)])
-def test_lazy_adam_bitwise_equals_dense(D, wd, clip):
+def _expect(ids_np, vocab):
+    flat = ids_np.reshape(-1).astype(np.int64)
+    key = np.where((flat >= 0) & (flat < vocab), flat, SENT).astype(np.uint64)
+    order = np.argsort(key, kind='stable')
+    return key[order].astype(np.uint32), order.astype(np.uint32)
+
+
+@pytest.mark.parametrize('n,bag,vocab,dtype', [
+    (1, 1, 300, torch.int64), (4096, 1, 1_000_000, torch.int64), (3000, 3, 19, torch.int64),
+    (4097, 1, 10_000_000, torch.int64), (204_800, 50, 10_000_000, torch.int64),
+    (100_000, 1, 100_000_000, torch.int32), (65_536, 4, 65_536, torch.int64),
+    (819_200, 1, 100_000_000, torch.int64)])
+def test_lookup_sort_bit_exact(n, bag, vocab, dtype):
+    g = np.random.default_rng(n + bag)
+    rows = max(n // bag, 1)
+    ids = g.integers(0, vocab, size=(rows, bag))
+    ids[g.random((rows, bag)) < 0.1] = 0                    # padding-like repeats
+    ids[g.random((rows, bag)) < 0.05] = g.integers(0, 50, size=1)  # a hot row
+    if ids.size > 10:
+        ids.reshape(-1)[3] = vocab + 5                       # out of range
+        ids.reshape(-1)[7] = -2
+    t = torch.from_numpy(ids).to(dtype).to(DEV)
+    keys, vals = _sort(t, vocab)
+    ek, ev = _expect(ids, vocab)
+    assert np.array_equal(keys.cpu().numpy().view(np.uint32)[:ids.size], ek)
+    assert np.array_equal(vals.cpu().numpy().view(np.uint32)[:ids.size], ev)
+
+
+def test_lookup_sort_strided_column():
+    """A single-id feature is a column of the [B, S] sparse matrix, read in place (stride S)."""
+    g = np.random.default_rng(5)
+    m = g.integers(0, 5_000_000, size=(6000, 5))
+    t = torch.from_numpy(m).to(DEV)
+    col = 3
+    keys = torch.empty(6000, dtype=torch.int32, device=DEV)
+    vals = torch.empty(6000, dtype=torch.int32, device=DEV)
+    wsb = int(_hip.lib().rs_lookup_sort_ws_bytes(6000, 5_000_000))
+    ws = torch.empty(wsb // 4 + 1, dtype=torch.int32, device=DEV)
+    _hip.call('rs_lookup_sort', t.data_ptr() + 8 * col, 8, 6000, 1, 5, 5_000_000, keys.data_ptr(),
+              vals.data_ptr(), ws.data_ptr(), ops.stream())
+    ek, ev = _expect(m[:, col], 5_000_000)
+    assert np.array_equal(keys.cpu().numpy().view(np.uint32), ek)
+    assert np.array_equal(vals.cpu().numpy().view(np.uint32), ev)
+
+
+def _segsum(keys, vals, n, bag, mode, pad, dout, V, D, acc=0, grad=None):
+    grad = torch.zeros(V, D, device=DEV) if grad is None else grad
+    ws = torch.empty(int(_hip.lib().rs_segsum_ws_bytes(n, D)) // 4 + 1, dtype=torch.int32, device=DEV)
+    _hip.call('rs_segsum', keys.data_ptr(), vals.data_ptr(), n, bag, mode, pad, dout.data_ptr(),
+              dout.stride(0), D, grad.data_ptr(), acc, ws.data_ptr(), ops.stream())
+    return grad
+
+
+def _ref_grad(ids, dout, V, mode, pad):
+    """float64 embedding_dense_backward of the lookup (mean: grad / bag per lookup)."""
+    ids = ids.reshape(ids.shape[0], -1)
+    bag = ids.shape[1]
+    g = np.zeros((V, dout.shape[1]))
+    d = dout.astype(np.float64) / (bag if mode == 1 else 1)
+    for l in range(bag):
+        col = ids[:, l]
+        ok = (col >= 0) & (col < V) & (col != pad)
+        np.add.at(g, col[ok], d[ok])
+    return g
+
+
+@pytest.mark.parametrize('mode,bag,D,zipf', [(0, 1, 128, False), (1, 50, 128, False), (2, 3, 40, False),
+                                             (1, 50, 128, True), (0, 1, 64, True), (1, 20, 200, True),
+                                             (0, 1, 16, False)])
+def test_segsum_matches_dense_backward(mode, bag, D, zipf):
+    g = np.random.default_rng(D + bag)
+    V, B, pad = 300_000, 4096, 0
+    if zipf:
+        ids = np.minimum(g.zipf(1.05, size=(B, bag)) - 1, V - 1)
+    else:
+        ids = g.integers(0, V, size=(B, bag))
+    ids[g.random((B, bag)) < 0.3] = pad
+    ids[0, 0] = V + 1  # out of range: no gradient
+    t = torch.from_numpy(ids).to(DEV)
+    dout = torch.randn(B, D + 8, device=DEV)[:, 4:4 + D]  # a column slice of a wider gradient
+    keys, vals = _sort(t, V)
+    got = _segsum(keys, vals, B * bag, bag, mode, pad, dout, V, D)
+    want = _ref_grad(ids, dout.cpu().numpy(), V, mode, pad)
+    err = np.abs(got.cpu().numpy() - want).max()
+    assert err <= 1e-5 * max(1.0, np.abs(want).max()), err
+    again = _segsum(keys, vals, B * bag, bag, mode, pad, dout, V, D)
+    assert torch.equal(got, again)  # deterministic
+    assert not got[pad].any()
+    # accumulate = 1 adds to what is there
+    base = torch.randn(V, D, device=DEV)
+    acc = _segsum(keys, vals, B * bag, bag, mode, pad, dout, V, D, acc=1, grad=base.clone())
+    assert torch.allclose(acc, base + got, atol=1e-5)
+
+
+def test_segsum_equals_atomic_scatter():
+    """rs_segsum == the atomic scatter of rs_gather_bwd (ordinary tables) up to summation order."""
+    from recommendsystemproject_amd.functions import _seg
+    V, D, B, bag, pad = 200_000, 128, 512, 7, 3
+    gen = torch.Generator().manual_seed(11)
+    ids = torch.randint(0, V, (B, bag), generator=gen)
+    ids[:40] = torch.randint(0, 50, (40, bag), generator=gen)
+    ids[0, :3] = pad
+    ids = ids.to(DEV)
+    table = torch.randn(V, D, device=DEV)
+    dout = torch.randn(B, D, device=DEV)
+    g1 = torch.zeros(V, D, device=DEV)
+    s = _seg(kind=_hip.RS_SEG_POOL, dim=D, out_col=0, vocab=V, idx_stride=bag, bag=bag,
+             pool_mode=_hip.RS_POOL['mean'], idx=ids.data_ptr(), table=table.data_ptr(), pad_idx=pad)
+    s.grad = g1.data_ptr()
+    ops.gather_bwd([s], B, dout)
+    keys, vals = _sort(ids, V)
+    g2 = _segsum(keys, vals, B * bag, bag, 1, pad, dout, V, D)
+    assert torch.allclose(g1, g2, atol=1e-6, rtol=1e-5)
+
+
+def _sorted_rows(keys):
+    k = keys.cpu().numpy().view(np.uint32)
+    return sorted(set(int(x) for x in k if x != SENT))
+
+
+@pytest.mark.parametrize('D,wd,clip,calls', [(40, 0.0, False, 1), (128, 0.0, True, 1), (16, 0.0, False, 1),
+                                             (64, 0.01, True, 1), (32, 0.0, True, 2)])
+def test_lazy_adam_bitwise_equals_dense(D, wd, clip, calls):
     V, pad, steps, cap = 3000, 7, 9, 64
-    gen = torch.Generator().manual_seed(D)
+    gen = torch.Generator().manual_seed(D + calls)
     p0 = torch.randn(V, D, generator=gen).to(DEV)
     pd, md, vd = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
     pl, ml, vl = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
     gl = torch.zeros_like(p0)
-    flag, lst, cnt, last = _i32(V), _i32(V), _i32(1), _i32(V)
+    last = torch.zeros(V, dtype=torch.int32, device=DEV)
+    owner = torch.full((V,), 0x7fffffff, dtype=torch.int32, device=DEV)
     step_d = torch.zeros((), dtype=torch.int64, device=DEV)
     step_l = torch.zeros((), dtype=torch.int64, device=DEV)
     consts = torch.zeros(cap, 2, device=DEV)
+    consts.view(torch.int32)[0, 0] = cap
     coef = torch.tensor(0.37, device=DEV) if clip else None
     cptr = coef.data_ptr() if clip else None
     S = ops.stream()
     hyper = (B1, B2, EPS, wd)
     for t in range(1, steps + 1):
-        # this step's lookups: [rows, bag] ids with repeats, the padding id and out-of-range ids;
-        # step 4 touches nothing at all (rows must still replay step 4 later)
-        n_ids = 0 if t == 4 else 300
-        ids = torch.randint(0, V // (1 if t % 2 else 6), (300,), generator=gen)
-        ids[:5] = pad
-        ids[5] = V + 3
-        ids = ids[:n_ids].view(-1, 3)
-        idsd = ids.to(DEV)
-        _hip.call('rs_sparse_touch', idsd.data_ptr(), ids.shape[0], 3, 3, V, pad, flag.data_ptr(),
-                  lst.data_ptr(), cnt.data_ptr(), S) if n_ids else None
-        _hip.call('rs_sparse_catchup', pl.data_ptr(), ml.data_ptr(), vl.data_ptr(), last.data_ptr(),
-                  lst.data_ptr(), cnt.data_ptr(), D, step_l.data_ptr(), consts.data_ptr(), *hyper, S)
-        # what the forward reads: touched rows equal the dense weights exactly
-        rows = sorted({int(i) for i in ids.reshape(-1).tolist() if 0 <= i < V and i != pad})
+        # this step's lookups (calls x [rows, 3] ids with repeats, the padding id and
+        # out-of-range ids); step 4 touches nothing at all (rows must still replay step 4 later)
+        sorted_calls, rows = [], set()
+        for c in range(calls):
+            n_ids = 0 if t == 4 else 300
+            ids = torch.randint(0, V // (1 if t % 2 else 6), (300,), generator=gen)
+            ids[:5] = pad
+            ids[5] = V + 3
+            ids = ids[:n_ids].view(-1, 3)
+            if n_ids == 0:
+                continue
+            keys, _ = _sort(ids.to(DEV), V)
+            sorted_calls.append(keys)
+            _hip.call('rs_sorted_catchup', keys.data_ptr(), ids.numel(), D, pl.data_ptr(), ml.data_ptr(),
+                      vl.data_ptr(), last.data_ptr(), step_l.data_ptr(), consts.data_ptr(), *hyper, S)
+            rows |= set(_sorted_rows(keys))
+        rows = sorted(rows)
+        # what the forward reads: touched rows (pad included) equal the dense weights exactly
         if rows:
             r = torch.tensor(rows, device=DEV)
             assert torch.equal(pl[r], pd[r]), t
-        # gradient of the touched rows (what the scatter-add would leave)
+        # gradient of the touched rows except the pad row (what the segment sum leaves)
         g = torch.zeros(V, D)
-        if rows:
-            g[rows] = torch.randn(len(rows), D, generator=gen)
+        grows = [x for x in rows if x != pad]
+        if grows:
+            g[grows] = torch.randn(len(grows), D, generator=gen)
         g = g.to(DEV)
         gl.copy_(g)
         _hip.call('rs_counter_add', step_d.data_ptr(), 1, S)
         _hip.call('rs_adam_step', pd.data_ptr(), g.data_ptr(), md.data_ptr(), vd.data_ptr(), V * D, LR,
                   B1, B2, EPS, wd, 0, step_d.data_ptr(), 0.5, cptr, 0, S)
         _hip.call('rs_adam_prepare', step_l.data_ptr(), consts.data_ptr(), cap, LR, B1, B2, S)
-        _hip.call('rs_sparse_adam', pl.data_ptr(), gl.data_ptr(), ml.data_ptr(), vl.data_ptr(),
-                  last.data_ptr(), flag.data_ptr(), lst.data_ptr(), cnt.data_ptr(), D,
-                  step_l.data_ptr(), consts.data_ptr(), *hyper, 0.5, cptr, S)
-        assert cnt.item() == 0 and int(flag.sum().item()) == 0
-        assert not gl.any().item()  # listed gradient rows re-zeroed
+        multi = len(sorted_calls) > 1
+        if multi:
+            for i, keys in enumerate(sorted_calls):
+                _hip.call('rs_sorted_owner', keys.data_ptr(), keys.numel(), owner.data_ptr(), i, S)
+        for i, keys in enumerate(sorted_calls):
+            _hip.call('rs_sorted_adam', keys.data_ptr(), keys.numel(), D, pl.data_ptr(), gl.data_ptr(),
+                      ml.data_ptr(), vl.data_ptr(), last.data_ptr(), owner.data_ptr() if multi else None,
+                      i, step_l.data_ptr(), consts.data_ptr(), *hyper, 0.5, cptr, S)
+        assert not gl.any().item()  # stepped gradient rows re-zeroed
+        assert int(owner.min().item()) == 0x7fffffff  # owners reset by the step
+        if rows:  # every touched row stepped exactly once
+            assert torch.equal(pl[r], pd[r]), t
     assert step_l.item() == steps
     _hip.call('rs_sparse_flush', pl.data_ptr(), ml.data_ptr(), vl.data_ptr(), last.data_ptr(), V, D,
               step_l.data_ptr(), consts.data_ptr(), *hyper, S)
@@ -77,117 +233,49 @@ def test_lazy_adam_bitwise_equals_dense(D, wd, clip):
     assert int(last.min().item()) == steps
 
 
-def test_sparse_sqnorm_matches_dense():
+def test_consts_overflow_clamped():
+    """Past the constants capacity (graph replays skip the host check) the step index is clamped
+    on the device and the overflow flag set."""
+    cap = 4
+    consts = torch.zeros(cap, 2, device=DEV)
+    consts.view(torch.int32)[0, 0] = cap
+    step = torch.zeros((), dtype=torch.int64, device=DEV)
+    for _ in range(cap + 2):
+        _hip.call('rs_adam_prepare', step.data_ptr(), consts.data_ptr(), cap, LR, B1, B2, ops.stream())
+    assert int(consts.view(torch.int32)[0, 1].item()) == 1
+    V, D = 10, 8
+    p = torch.randn(V, D, device=DEV)
+    m, v = torch.ones_like(p), torch.ones_like(p)
+    last = torch.zeros(V, dtype=torch.int32, device=DEV)
+    _hip.call('rs_sparse_flush', p.data_ptr(), m.data_ptr(), v.data_ptr(), last.data_ptr(), V, D,
+              step.data_ptr(), consts.data_ptr(), B1, B2, EPS, 0.0, ops.stream())
+    assert int(last.max().item()) == cap - 1
+
+
+def test_sorted_sqnorm_matches_dense():
     V, D = 5000, 64
     g = torch.zeros(V, D, device=DEV)
-    rows = torch.randperm(V)[:700].to(DEV)
-    g[rows] = torch.randn(700, D, device=DEV)
-    flag, lst, cnt = _i32(V), _i32(V), _i32(1)
-    ids = rows.long()
-    _hip.call('rs_sparse_touch', ids.data_ptr(), 700, 1, 1, V, -1, flag.data_ptr(), lst.data_ptr(),
-              cnt.data_ptr(), ops.stream())
-    ns = int(_hip.lib().rs_sparse_sqnorm_parts())
+    rows = torch.randperm(V)[:700]
+    g[rows.to(DEV)] = torch.randn(700, D, device=DEV)
+    ids = torch.cat([rows, rows[:100]]).to(DEV)  # repeats: each row counted once
+    keys, _ = _sort(ids.view(-1, 1), V)
+    ns = int(_hip.lib().rs_sorted_sqnorm_parts())
     ws = torch.zeros(ns, dtype=torch.float64, device=DEV)
-    _hip.call('rs_sparse_sqnorm', g.data_ptr(), lst.data_ptr(), cnt.data_ptr(), D, 2.0, ws.data_ptr(),
-              ops.stream())
+    _hip.call('rs_sorted_sqnorm', keys.data_ptr(), ids.numel(), D, g.data_ptr(), None, 0, 2.0,
+              ws.data_ptr(), ops.stream())
     norm, coef = torch.zeros((), device=DEV), torch.zeros((), device=DEV)
     _hip.call('rs_clip_coef', ws.data_ptr(), ns, 1.0, norm.data_ptr(), coef.data_ptr(), ops.stream())
     want = (2.0 * g.double()).norm().item()
     assert abs(norm.item() - want) < 1e-6 * want
 
 
-def test_compact_pack_unpack_roundtrip():
-    """Row-sparse DP exchange kernels: ordered compaction, pack, rank-ordered unpack-add."""
-    V, D, cap = 20000, 24, 512
-    gen = torch.Generator().manual_seed(3)
-    S = ops.stream()
-    gsum = torch.zeros(V, D, device=DEV)
-    bufs, union = [], set()
-    for r in range(3):  # three "ranks"
-        rows = torch.randperm(V, generator=gen)[:300 + 50 * r]
-        union |= set(rows.tolist())
-        g = torch.zeros(V, D)
-        g[rows] = torch.randn(len(rows), D, generator=gen)
-        g = g.to(DEV)
-        gsum += g
-        flag, lst, cnt = _i32(V), _i32(V), _i32(1)
-        ids = rows.to(DEV)
-        _hip.call('rs_sparse_touch', ids.data_ptr(), len(rows), 1, 1, V, -1, flag.data_ptr(),
-                  lst.data_ptr(), cnt.data_ptr(), S)
-        buf = torch.empty(cap * (D + 1), device=DEV)
-        err = _i32(1)
-        _hip.call('rs_sparse_pack', g.data_ptr(), lst.data_ptr(), cnt.data_ptr(), D, cap, buf.data_ptr(),
-                  err.data_ptr(), S)
-        assert err.item() == 0
-        ids_back = buf[:cap].view(torch.int32)
-        assert sorted(x for x in ids_back.tolist() if x >= 0) == sorted(rows.tolist())
-        bufs.append(buf)
-    out = torch.zeros(V, D, device=DEV)
-    flag = _i32(V)
-    for buf in bufs:
-        _hip.call('rs_sparse_unpack_add', out.data_ptr(), flag.data_ptr(), buf.data_ptr(), D, cap, S)
-    assert torch.allclose(out, gsum, atol=1e-6)
-    lst, cnt = _i32(V), _i32(1)
-    ws = torch.empty(int(_hip.lib().rs_sparse_compact_ws_bytes(V)) // 4 + 1, dtype=torch.int32, device=DEV)
-    _hip.call('rs_sparse_compact', flag.data_ptr(), V, lst.data_ptr(), cnt.data_ptr(), ws.data_ptr(), S)
-    n = cnt.item()
-    assert n == len(union)
-    assert lst[:n].tolist() == sorted(union)
-    # overflow is flagged
-    err = _i32(1)
-    cnt.fill_(cap + 1)
-    _hip.call('rs_sparse_pack', out.data_ptr(), lst.data_ptr(), cnt.data_ptr(), D, cap,
-              torch.empty(cap * (D + 1), device=DEV).data_ptr(), err.data_ptr(), S)
-    assert err.item() == 2
-
-
-def test_compact_large_vocab():
-    V = 10_000_019
-    flag = torch.zeros(V, dtype=torch.int32, device=DEV)
-    idx = torch.unique(torch.randint(0, V, (200000,), device=DEV))
-    flag[idx] = 1
-    lst, cnt = _i32(V), _i32(1)
-    ws = torch.empty(int(_hip.lib().rs_sparse_compact_ws_bytes(V)) // 4 + 1, dtype=torch.int32, device=DEV)
-    _hip.call('rs_sparse_compact', flag.data_ptr(), V, lst.data_ptr(), cnt.data_ptr(), ws.data_ptr(),
-              ops.stream())
-    n = cnt.item()
-    assert n == idx.numel()
-    assert torch.equal(lst[:n].long(), idx)
-
-
-@pytest.mark.parametrize('kind', ['sparse', 'pool_mean', 'pool_sum'])
-def test_scatter_store_for_single_lookup_rows(kind):
-    """rs_gather_bwd with touch counts: rows looked up once this step are stored, the others
-    atomically added; the table gradient must equal the all-atomic scatter."""
-    from recommendsystemproject_amd.functions import _seg
-    V, D, B, bag, pad = 200_000, 128, 512, 7, 3
-    gen = torch.Generator().manual_seed(11)
-    ids = torch.randint(0, V, (B, bag), generator=gen)
-    ids[:40] = torch.randint(0, 50, (40, bag), generator=gen)  # heavy repeats
-    ids[0, :3] = pad
-    ids = ids.to(DEV)
-    if kind == 'sparse':
-        ids = ids[:, :1].contiguous()
-    nb = ids.shape[1]
-    table = torch.randn(V, D, device=DEV)
-    dout = torch.randn(B, D, device=DEV)
-    grads = []
-    for use_count in (False, True):
-        g = torch.zeros(V, D, device=DEV)
-        flag, lst, cnt = _i32(V), _i32(V), _i32(1)
-        if kind == 'sparse':
-            s = _seg(kind=_hip.RS_SEG_SPARSE, dim=D, out_col=0, vocab=V, idx_stride=1, idx=ids.data_ptr(),
-                     table=table.data_ptr(), pad_idx=pad)
-        else:
-            s = _seg(kind=_hip.RS_SEG_POOL, dim=D, out_col=0, vocab=V, idx_stride=nb, bag=nb,
-                     pool_mode=_hip.RS_POOL[kind[5:]], idx=ids.data_ptr(), table=table.data_ptr(), pad_idx=pad)
-        s.grad = g.data_ptr()
-        if use_count:
-            _hip.call('rs_sparse_touch', ids.data_ptr(), B, nb, nb, V, pad, flag.data_ptr(), lst.data_ptr(),
-                      cnt.data_ptr(), ops.stream())
-            s.touch_count = flag.data_ptr()
-            assert int(flag.max().item()) > 1
-        ops.gather_bwd([s], B, dout)
-        grads.append(g)
-    assert torch.allclose(grads[0], grads[1], atol=1e-5, rtol=1e-6)
-    assert not grads[1][pad].any()
+def test_pack_ids_and_rows():
+    g = np.random.default_rng(2)
+    m = torch.from_numpy(g.integers(0, 1 << 30, size=(300, 9))).to(DEV)
+    out = torch.empty(300 * 4, dtype=torch.int32, device=DEV)
+    _hip.call('rs_pack_ids', m.data_ptr() + 8 * 2, 8, 300, 4, 9, out.data_ptr(), ops.stream())
+    assert torch.equal(out.view(300, 4).long(), m[:, 2:6])
+    x = torch.randn(300, 50, device=DEV)
+    y = torch.empty(300, 16, device=DEV)
+    _hip.call('rs_pack_rows', x.data_ptr() + 4 * 7, 50, 300, 16, y.data_ptr(), ops.stream())
+    assert torch.equal(y, x[:, 7:23])
