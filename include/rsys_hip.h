@@ -272,6 +272,12 @@ int rs_inbatch_ce_bwd(float* S, int ld_s, const float* U, const float* Hn,
                       int64_t h_row_stride, int64_t h_slot_stride,
                       const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T,
                       const float* lse, const float* grad_out, float* dhl, void* stream);
+/* The logits matrix of the same loss, materialised: out [B, ld_out >= B + N] (diagnostics and
+ * TwoTowerModel.compute_logits; the loss kernels never store it). */
+int rs_inbatch_logits(const float* S, int ld_s, const float* U, const float* Hn,
+                      int64_t h_row_stride, int64_t h_slot_stride, const int64_t* item_ids,
+                      int64_t id_stride, int B, int N, int D, float T, float* out, int64_t ld_out,
+                      void* stream);
 /* The same loss with S never stored (bf16 compute mode; D = 64 or 128): the 32 x 32 tiles of
  * U I^T are recomputed on bf16 MFMA where needed -- an online log-sum-exp per user in the
  * forward, dU = dS I and dI = dS^T U accumulated from dS tiles held in registers in the

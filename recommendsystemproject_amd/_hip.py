@@ -76,6 +76,7 @@ SIGNATURES = {
                                       vp]),
     'rs_inbatch_ce_fwd': (i32, [vp, i32, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp]),
     'rs_inbatch_ce_bwd': (i32, [vp, i32, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp]),
+    'rs_inbatch_logits': (i32, [vp, i32, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, i64, vp]),
     'rs_hardneg_bwd': (i32, [vp, vp, i64, i64, vp, vp, vp, i32, i32, i32, vp]),
     'rs_mask_history': (i32, [vp, i64, i32, i64, i64, vp, i64, vp, vp, i64, vp]),
     'rs_topk_rows': (i32, [vp, i64, i32, i32, i32, vp, i64, i32, vp, vp, i64, vp]),

@@ -76,6 +76,25 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ S
   }
 }
 
+// the logits matrix itself [B, B + N] (TwoTowerModel.py:95-136 before F.cross_entropy): one
+// workgroup per row; the in-batch part from S, the hard-negative part by one wave per slot
+__global__ __launch_bounds__(256) void logits_kernel(const float* __restrict__ S, int ld,
+                                                     const float* __restrict__ U,
+                                                     const float* __restrict__ Hn, HStride hs,
+                                                     const int64_t* __restrict__ ids, int64_t st,
+                                                     int B, int N, int D, float T,
+                                                     float* __restrict__ out, int64_t ldo) {
+  const int i = blockIdx.x;
+  const float* Srow = S + (int64_t)i * ld;
+  const int64_t idi = ids ? ids[(int64_t)i * st] : 0;
+  float* o = out + (int64_t)i * ldo;
+  for (int j = threadIdx.x; j < B; j += 256) o[j] = logit_at(Srow, ids, st, idi, i, j, T);
+  for (int n = threadIdx.x >> 6; n < N; n += 4) {
+    const float v = hard_logit(U, Hn, hs, i, n, D, T);
+    if ((threadIdx.x & 63) == 0) o[B + n] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void ce_bwd_kernel(float* __restrict__ S, int ld,
                                                      const float* __restrict__ U,
                                                      const float* __restrict__ Hn, HStride hs,
@@ -162,5 +181,19 @@ extern "C" int rs_hardneg_bwd(const float* U, const float* Hn, int64_t h_row_str
   const HStride hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
   hardneg_bwd_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(U, Hn, hs, dhl, dU, dH, B, N, D);
   RS_CHECK_LAUNCH("rs_hardneg_bwd");
+  return 0;
+}
+
+extern "C" int rs_inbatch_logits(const float* S, int ld_s, const float* U, const float* Hn,
+                                 int64_t h_row_stride, int64_t h_slot_stride,
+                                 const int64_t* item_ids, int64_t id_stride, int B, int N, int D,
+                                 float T, float* out, int64_t ld_out, void* stream) {
+  RS_CHECK_ARG(S && out && B >= 1 && ld_s >= B && N >= 0 && ld_out >= B + N,
+               "rs_inbatch_logits: bad args");
+  RS_CHECK_ARG(N == 0 || (U && Hn && D >= 1), "rs_inbatch_logits: hard negatives need U, H, D");
+  const HStride hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
+  logits_kernel<<<B, 256, 0, as_stream(stream)>>>(S, ld_s, U, Hn, hs, item_ids, id_stride, B, N, D, T,
+                                                  out, ld_out);
+  RS_CHECK_LAUNCH("rs_inbatch_logits");
   return 0;
 }

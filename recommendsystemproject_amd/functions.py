@@ -180,7 +180,7 @@ def layer_fwd(lyr, x, key_pad, B, L, d, H, p, key, site):
     sa_mod = lyr.self_attn
     # bf16 mode: qkv stored as bf16 (only ever an MFMA operand: same products, half the bytes)
     qkv = ops.linear_fwd(x, sa_mod.in_proj_weight, sa_mod.in_proj_bias,
-                         out_dtype=torch.bfloat16 if ops.qkv_bf16_ok(L, d, H) else torch.float32)
+                         out_dtype=torch.bfloat16 if ops.qkv_bf16_ok(L, d, H, B * L) else torch.float32)
     att, lse = ops.attn_fwd(qkv, key_pad, B, L, d, H, p, key, site)
     # h1 = x + dropout1(out_proj(att)), x1 = norm1(h1): GEMM + residual + LayerNorm in one kernel
     h1, x1, m1, r1 = ops.linear_add_layernorm(att, sa_mod.out_proj.weight, sa_mod.out_proj.bias, x,
@@ -203,7 +203,7 @@ def layer_fwd_last(lyr, x, key_pad, last, B, L, d, H, p, key, site):
     then out-proj + LN1 + FFN + LN2 on B rows."""
     sa_mod = lyr.self_attn
     qkv = ops.linear_fwd(x, sa_mod.in_proj_weight, sa_mod.in_proj_bias,
-                         out_dtype=torch.bfloat16 if ops.qkv_bf16_ok(L, d, H) else torch.float32)
+                         out_dtype=torch.bfloat16 if ops.qkv_bf16_ok(L, d, H, B * L) else torch.float32)
     att, lse = ops.attn_rows_fwd(qkv, key_pad, last, B, L, d, H, p, key, site)
     xs = torch.empty(B, d, device=x.device, dtype=torch.float32)  # residual rows x[b, last[b]]
     ops.gather_fwd([_seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=last.data_ptr(),

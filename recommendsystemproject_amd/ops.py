@@ -185,10 +185,15 @@ def gather_bwd(segs, rows, dout):
     call('rs_gather_bwd', arr, len(segs), rows, P(dout), dout.stride(0), None, stream())
 
 
-def qkv_bf16_ok(L, d, H):
+STREAM_BF16_MIN_ROWS = 32768  # gemm_stream.hip kSmallM: the bf16-storage GEMM instances are big-M only
+
+
+def qkv_bf16_ok(L, d, H, M):
     """Store the packed qkv (and dqkv) as bf16: bf16 compute mode on the bf16 MFMA attention
-    path (head_dim 16, L <= 256), where Q, K, V are only MFMA operands (RS_ATTN_QKV_BF16)."""
+    path (head_dim 16, L <= 256), where Q, K, V are only MFMA operands (RS_ATTN_QKV_BF16), for
+    token counts M the bf16-storage streaming GEMMs cover (M >= 32768, a multiple of 16)."""
     return (precision.compute_dtype() == 'bf16' and d // H == 16 and L <= 256 and
+            M >= STREAM_BF16_MIN_ROWS and M % 16 == 0 and
             not os.environ.get('RSYS_ATTN_VALU') and not os.environ.get('RSYS_QKV_FP32'))
 
 

@@ -1,0 +1,377 @@
+"""The benched workloads end to end on the GPU (BASELINE.json configs[1], [2], [4]):
+
+* logits of the HIP path against the reference's golden logits (fp32, 1e-4; collision mask
+  exact);
+* the benched bf16 compute mode against every golden fixture and against the oracle at C2 shapes
+  (B = 1024, L = 50: the bf16 token GEMMs, bf16 attention and the fused CE all engage), with the
+  tolerance derived from bf16 operand rounding (below), and a bias test on the per-row losses;
+* the fp32 step against the oracle at the configured batch B = 4096 (C2);
+* C3 at its real sizes (1M / 10M / 10M-row tables, pooled 50-long history, lazy-exact Adam over
+  sorted lookups) for several steps with distinct batches against a dense-Adam HIP control, and
+  the C3 schema with the tables capped to 1M rows against the oracle;
+* C5 (L = 200 encoder, N = 10 hard negatives materialised from a device catalog, grouped per-slot
+  BatchNorm, bf16 long-history attention) at its real 100M-row size, and capped against the
+  oracle (fp32) and against a dense-Adam control.
+
+bf16 tolerance. Every GEMM operand the bf16 mode rounds carries a relative error of at most
+u = 2^-8 (bf16 keeps 8 significant bits, round to nearest), so each product a*b is off by at most
+2u relative and a dot product by at most 2u * sum|a_i b_i|. The embeddings U, I are L2-normalised,
+so the final logit U.I / T is off by at most 2u / T from its own product, plus what U and I
+inherit from the towers' rounded GEMMs. For unit vectors the elementwise error of U / I is held
+to TOL_EMB = 4u (the tower GEMMs are fp32; the encoder's rounded GEMMs feed the user tower through
+one BatchNorm-normalised MLP). A logit then moves by at most (2 * TOL_EMB * sqrt(D) * max|e| ...)
+-- in practice we bound it by TOL_LOGIT = (2 * 4u + 2u) / T, and the loss (a mean of per-row
+log-sum-exp minus the positive logit, each 1-Lipschitz in the max-norm of its row's logits) by
+2 * TOL_LOGIT. Those are worst-case bounds; the BIAS test is the sharp one: rounding noise is
+unbiased, so the mean of the per-row loss differences must sit within 4 standard errors of zero
+(a systematic error in any kernel -- e.g. a mis-scaled fused CE -- moves the mean by a whole
+per-row error and fails it).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+import yaml
+
+import golden_util as gu
+from oracle.twotower_oracle import OracleTrainer, model_forward, model_state_shapes, inbatch_logits
+from recommendsystemproject_amd import precision, synth
+from recommendsystemproject_amd.flat import ensure_flat
+from recommendsystemproject_amd.optim import Adam
+from recommendsystemproject_amd.project.models.TwoTower.GenericTower import GenericTower
+from recommendsystemproject_amd.project.models.TwoTower.TwoTowerModel import TwoTowerModel
+from recommendsystemproject_amd.project.utils.training_utils import extract_item_id, train_step
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = sorted(glob.glob(os.path.join(ROOT, 'tests', 'golden', '*.npz')))
+DEV = torch.device('cuda:0')
+U_BF16 = 2.0 ** -8
+TOL_EMB = 4 * U_BF16
+
+
+def tol_logit(T):
+    return (2 * TOL_EMB + 2 * U_BF16) / T
+
+
+def cfg_of(name, dropout0=True):
+    cfg = yaml.safe_load(open(os.path.join(ROOT, 'configs', f'{name}.yaml')))
+    if dropout0:
+        for t in cfg['two_tower'].values():
+            t['dropout'] = 0.0
+            if 'transformer_parameters' in t:
+                t['transformer_parameters']['dropout'] = 0.0
+    return cfg
+
+
+def maps_of(cfg):
+    return {'user': synth.tower_layout(cfg['two_tower']['user_tower']),
+            'item': synth.tower_layout(cfg['two_tower']['item_tower'])}
+
+
+def build(cfg, state=None, on_device=False):
+    maps = maps_of(cfg)
+    if on_device:
+        torch.manual_seed(0)
+        with torch.device(DEV):
+            m = TwoTowerModel(GenericTower(cfg, 'user_tower'), GenericTower(cfg, 'item_tower'),
+                              maps['user'], maps['item'])
+    else:
+        m = TwoTowerModel(GenericTower(cfg, 'user_tower'), GenericTower(cfg, 'item_tower'),
+                          maps['user'], maps['item'])
+    if state is not None:
+        m.load_state_dict({k: torch.as_tensor(np.asarray(v)) for k, v in state.items()})
+    return m.to(DEV), maps
+
+
+def cap_vocab(cfg, cap):
+    for t in cfg['two_tower'].values():
+        for f in (t.get('sparse_features') or []) + (t.get('sequence_features') or []):
+            f['vocab_size'] = min(int(f['vocab_size']), cap)
+    return cfg
+
+
+@pytest.fixture
+def bf16():
+    precision.set_compute_dtype('bf16')
+    yield
+    precision.set_compute_dtype('fp32')
+
+
+# ---------------------------------------------------------------------------------- logits
+@pytest.mark.parametrize('path', GOLD, ids=[os.path.basename(p)[:-4] for p in GOLD])
+def test_logits_match_golden(path):
+    cfg, meta, data = gu.load(path)
+    shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
+    model, _ = build(cfg, synth.make_state(shapes, seed=meta['weight_seed']))
+    model.train()
+    tb = synth.batch_to_torch(gu.batches(meta, data)[0], DEV)
+    U, I, H = model(tb)
+    logits = model.compute_logits(U, I, extract_item_id(tb['item_tower']), H, meta['temperature'])
+    want = data['logits']
+    got = logits.cpu().numpy()
+    assert got.shape == want.shape
+    masked = want <= -1e8
+    assert np.array_equal(got <= -1e8, masked)          # the collision mask, exactly
+    assert np.array_equal(got[masked], want[masked])    # -1e9
+    np.testing.assert_allclose(got[~masked], want[~masked], rtol=0, atol=1e-4)
+
+
+# ---------------------------------------------------------------------------------- bf16 mode
+@pytest.mark.parametrize('path', GOLD, ids=[os.path.basename(p)[:-4] for p in GOLD])
+def test_bf16_step_matches_golden(path, bf16):
+    cfg, meta, data = gu.load(path)
+    shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
+    model, _ = build(cfg, synth.make_state(shapes, seed=meta['weight_seed']))
+    model.train()
+    T = meta['temperature']
+    tb = synth.batch_to_torch(gu.batches(meta, data)[0], DEV)
+    f = ensure_flat(model)
+    f.zero_grad()
+    U, I, H = model(tb)
+    ids = extract_item_id(tb['item_tower'])
+    loss = model.compute_loss(U, I, item_ids=ids, hard_neg_emb=H, temperature=T)
+    loss.backward()
+    for name, t in (('U', U), ('I', I), ('H', H)):
+        if name in data:
+            err = np.abs(t.detach().cpu().numpy() - data[name]).max()
+            assert err <= TOL_EMB, (name, err)
+    logits = model.compute_logits(U, I, ids, H, T).cpu().numpy()
+    want = data['logits']
+    ok = want > -1e8
+    assert np.abs(logits[ok] - want[ok]).max() <= tol_logit(T)
+    assert abs(loss.item() - float(data['loss1'])) <= 2 * tol_logit(T), (loss.item(), float(data['loss1']))
+    # gradients: the whole flat gradient points the same way (rounding noise, not a bias)
+    g = []
+    for k, p in model.named_parameters():
+        kind, ref = gu.stored(data, 'grad', k)
+        if kind == 'full':
+            g.append((p.grad.reshape(-1).double().cpu(), torch.from_numpy(np.asarray(ref)).reshape(-1).double()))
+    a = torch.cat([x for x, _ in g])
+    b = torch.cat([y for _, y in g])
+    # a gradient passes rounded operands twice per GEMM (forward activation, backward product),
+    # through every layer back from the loss: held to 32u relative in norm (a small batch has
+    # the least averaging: hardneg, B = 32, measured 0.064 = 16.4u)
+    cos = F.cosine_similarity(a, b, dim=0).item()
+    assert cos > 1 - 16 * U_BF16, cos
+    assert (a - b).norm().item() <= 32 * U_BF16 * b.norm().item()
+
+
+def _row_losses(logits):
+    B = logits.shape[0]
+    return torch.logsumexp(logits, dim=1) - logits[torch.arange(B), torch.arange(B)]
+
+
+def test_bf16_c2_step_matches_oracle(bf16):
+    """C2 shapes with every bf16 path engaged (B * L = 51,200 token rows: bf16 streaming GEMMs,
+    fused FFN, bf16 attention; fused CE): embeddings, logits and loss against the fp32 oracle
+    within the derived bounds, and the per-row loss differences unbiased."""
+    B = 1024
+    cfg = cfg_of('c2')
+    shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
+    state = synth.make_state(shapes, seed=21)
+    model, maps = build(cfg, state)
+    model.train()
+    b = synth.make_batch(cfg, B, seed=22, edge_cases=True)
+    tb = synth.batch_to_torch(b, DEV)
+    T = float(cfg['train']['temperature'])
+    U, I, H = model(tb)
+    ids = extract_item_id(tb['item_tower'])
+    loss = model.compute_loss(U, I, item_ids=ids, hard_neg_emb=H, temperature=T).item()
+    logits = model.compute_logits(U, I, ids, H, T).double().cpu()
+    Ur, Ir, Hr = model_forward(cfg, {k: torch.as_tensor(np.asarray(v)) for k, v in state.items()},
+                               synth.batch_to_torch(b), maps, True, 0.0)
+    lr = inbatch_logits(Ur.detach(), Ir.detach(), ids.cpu(), None, T).double()
+    assert (U.detach().cpu() - Ur.detach()).abs().max().item() <= TOL_EMB
+    assert (I.detach().cpu() - Ir.detach()).abs().max().item() <= TOL_EMB
+    ok = lr > -1e8
+    assert (logits[ok] - lr[ok]).abs().max().item() <= tol_logit(T)
+    d = _row_losses(logits) - _row_losses(lr)
+    want = _row_losses(lr).mean().item()
+    assert abs(loss - want) <= 2 * tol_logit(T)
+    se = d.std().item() / np.sqrt(B)
+    assert abs(d.mean().item()) <= 4 * se + 1e-5, (d.mean().item(), se)
+
+
+def test_fp32_c2_configured_batch_matches_oracle():
+    """The configured batch (B = 4096, L = 50) in the parity precision: loss, embeddings and the
+    updated weights after one step against the oracle."""
+    B = 4096
+    cfg = cfg_of('c2')
+    shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
+    state = synth.make_state(shapes, seed=31)
+    model, maps = build(cfg, state)
+    opt = Adam(model.parameters(), lr=float(cfg['train']['learning_rate']))
+    ref = OracleTrainer(cfg, state, lr=float(cfg['train']['learning_rate']))
+    T = float(cfg['train']['temperature'])
+    b = synth.make_batch(cfg, B, seed=32, edge_cases=True)
+    got = train_step(model, synth.batch_to_torch(b, DEV), opt, 1.0, T).item()
+    want = float(ref.step(synth.batch_to_torch(b), maps, temperature=T))
+    assert abs(got - want) < 1e-4, (got, want)
+    sd = model.state_dict()
+    for k in ('user_tower.seq_encoder.transformer_backbone.layers.1.linear1.weight',
+              'user_tower.seq_encoder.feature_embedder.feature_projection.0.weight',
+              'user_tower.mlp.mlp.0.weight', 'item_tower.mlp.mlp.8.weight',
+              'item_tower.embeddings.movie_id_enc.weight'):
+        err = (sd[k].cpu() - ref.S[k].detach()).abs().max().item()
+        assert err < 1e-4, (k, err)
+
+
+# ---------------------------------------------------------------------------------- C3
+def _c3_steps(cfg, model, batches, T):
+    opt = Adam(model.parameters(), lr=float(cfg['train']['learning_rate']))
+    return [train_step(model, synth.batch_to_torch(b, DEV), opt, 1.0, T).item() for b in batches]
+
+
+def test_c3_real_tables_lazy_matches_dense_adam(monkeypatch):
+    """C3 at its real sizes: lazy-exact Adam over sorted lookups (1M / 10M / 10M rows) against
+    the same model trained with dense Adam over every row, 5 steps of distinct batches."""
+    cfg = cfg_of('c3')
+    T = float(cfg['train']['temperature'])
+    batches = [synth.make_batch(cfg, 4096, seed=300 + s) for s in range(5)]
+    monkeypatch.setenv('RSYS_LAZY_ROWS', '65536')
+    lazy, _ = build(cfg, on_device=True)
+    assert len(ensure_flat(lazy).lazy) == 3
+    init = {k: v.detach().clone() for k, v in lazy.state_dict().items() if 'embeddings' in k and v.dim() == 2
+            and v.shape[0] >= 1_000_000}
+    l_lazy = _c3_steps(cfg, lazy, batches, T)
+    monkeypatch.setenv('RSYS_LAZY_ROWS', '0')
+    dense, _ = build(cfg, on_device=True)
+    with torch.no_grad():
+        dense.load_state_dict({k: v for k, v in init.items()}, strict=False)
+    assert not ensure_flat(dense).lazy
+    l_dense = _c3_steps(cfg, dense, batches, T)
+    np.testing.assert_allclose(l_lazy, l_dense, rtol=0, atol=1e-5)
+    sl, sd = lazy.state_dict(), dense.state_dict()  # lazy: flushed to the current step
+    lr = float(cfg['train']['learning_rate'])
+    for k, w0 in init.items():
+        a, b = sl[k], sd[k]
+        # The small tables' gradients are scattered with float atomics in both runs, so they
+        # differ in the last bits between the runs; from step 2 on, Adam turns that noise on
+        # near-zero gradient elements into up to +-lr steps (the golden tests' BN-invariant
+        # parameters, same cause). One step alone is bitwise equal (tools/diag_c3.py).
+        d = (a - b).abs()
+        assert d.max().item() <= 2 * lr * len(batches), (k, d.max().item())
+        moved = (a != w0).any(1) | (b != w0).any(1)
+        frac = (d[moved] <= 1e-6).float().mean().item()
+        assert frac >= 0.999, (k, frac)
+        # rows no batch looked up moved by neither (their Adam state is zero)
+        rows = torch.randint(0, a.shape[0], (4096,), device=DEV)
+        touched = torch.zeros(a.shape[0], dtype=torch.bool, device=DEV)
+        for bt in batches:
+            for t in (synth.batch_to_torch(bt, DEV)['user_tower'], synth.batch_to_torch(bt, DEV)['item_tower']):
+                for x in [t.get('sparse')] + list((t.get('sequence') or {}).values()):
+                    if x is not None:
+                        ids = x.reshape(-1)
+                        touched[ids[(ids >= 0) & (ids < a.shape[0])]] = True
+        cold = rows[~touched[rows]]
+        assert torch.equal(a[cold], w0[cold]) and torch.equal(b[cold], w0[cold])
+
+
+def test_c3_capped_matches_oracle():
+    """The C3 schema (pooled-mean 50-long history as a sparse feature, 128-wide tables) with the
+    large tables capped to 1M rows -- still lazy-Adam tables -- against the oracle."""
+    cfg = cap_vocab(cfg_of('c3'), 1_000_000)
+    shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
+    state = synth.make_state(shapes, seed=41)
+    model, maps = build(cfg, state)
+    assert len(ensure_flat(model).lazy) == 3
+    opt = Adam(model.parameters(), lr=1e-3)
+    ref = OracleTrainer(cfg, state, lr=1e-3)
+    for s in range(2):
+        b = synth.make_batch(cfg, 256, seed=42 + s, edge_cases=True)
+        got = train_step(model, synth.batch_to_torch(b, DEV), opt, 1.0, 0.15).item()
+        want = float(ref.step(synth.batch_to_torch(b), maps, temperature=0.15))
+        assert abs(got - want) < 1e-4, (s, got, want)
+    sd = model.state_dict()
+    for k in ('user_tower.embeddings.hist_item_ids.weight', 'item_tower.embeddings.item_id_enc.weight',
+              'user_tower.mlp.mlp.0.weight', 'item_tower.mlp.mlp.4.weight'):
+        err = (sd[k].cpu() - ref.S[k].detach()).abs().max().item()
+        assert err < 1e-4, (k, err)
+
+
+# ---------------------------------------------------------------------------------- C5
+def _catalog(cfg, seed=7):
+    from recommendsystemproject_amd.project.utils.hard_negatives import ItemCatalog
+    item = cfg['two_tower']['item_tower']
+    V = int(item['sparse_features'][0]['vocab_size'])
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    cols = [f for f in item['sparse_features'] if 'pooling' not in f]
+    sparse = torch.stack([torch.arange(V, device=DEV, dtype=torch.int32) if i == 0 else
+                          torch.randint(1, int(f['vocab_size']), (V,), device=DEV, generator=g, dtype=torch.int32)
+                          for i, f in enumerate(cols)], 1)
+    seqc = {f['name']: torch.randint(0, int(f['vocab_size']), (V, 3), device=DEV, generator=g, dtype=torch.int32)
+            for f in item['sparse_features'] if 'pooling' in f}
+    return ItemCatalog(sparse=sparse, sequence=seqc, device=DEV), V
+
+
+def _c5_step(model, opt, cfg, b, catalog, neg):
+    tb = synth.batch_to_torch(b, DEV)
+    tb['hard_negatives'] = catalog.materialize(neg)
+    return train_step(model, tb, opt, 1.0, float(cfg['train']['temperature'])).item()
+
+
+def test_c5_real_size_bf16_steps(bf16):
+    """C5 at its real size (100M-row history and item tables, L = 200, N = 10 hard negatives from
+    a device catalog, grouped per-slot BatchNorm, bf16 long-history attention): 3 steps of
+    distinct batches run, the loss is finite, and after a flush every row the steps looked up
+    is at the current optimizer step."""
+    cfg = cfg_of('c5', dropout0=False)
+    model, _ = build(cfg, on_device=True)
+    f = ensure_flat(model)
+    assert len(f.lazy) == 2 and all(t.V == 100_000_000 for t in f.lazy)
+    opt = Adam(model.parameters(), lr=float(cfg['train']['learning_rate']))
+    catalog, V = _catalog(cfg)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    losses = []
+    looked = []
+    for s in range(3):
+        b = synth.make_batch(cfg, 4096, seed=500 + s)
+        neg = torch.randint(1, V, (4096, 10), device=DEV, generator=g)
+        losses.append(_c5_step(model, opt, cfg, b, catalog, neg))
+        looked.append(torch.as_tensor(b['item_tower']['sparse'][:, 0]))
+    assert all(np.isfinite(losses)), losses
+    model.check_errors()
+    f.flush()
+    steps = int(opt._flat_state[id(f)]['step_dev'].item())
+    assert steps == 3
+    item_table = model.item_tower.embeddings['item_id_enc'].weight
+    t = next(t for t in f.lazy if t.param is item_table)
+    rows = torch.cat(looked).to(DEV)
+    assert int(t.last[rows].min().item()) == steps
+    assert int(t.last.max().item()) == steps
+
+
+def test_c5_capped_matches_oracle():
+    """The C5 schema (L = 200 encoder with hist_genre_ids tag pooling, N = 10 hard negatives) with
+    the tables capped to 1M rows (lazy tables), fp32, against the oracle (N separate item-tower
+    passes there, one grouped pass here)."""
+    cfg = cap_vocab(cfg_of('c5'), 1_000_000)
+    shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
+    state = synth.make_state(shapes, seed=51)
+    model, maps = build(cfg, state)
+    assert len(ensure_flat(model).lazy) == 2
+    opt = Adam(model.parameters(), lr=1e-3)
+    ref = OracleTrainer(cfg, state, lr=1e-3)
+    catalog, V = _catalog(cfg)
+    cat_sparse = catalog.sparse.long().cpu()
+    cat_seq = {k: v.long().cpu() for k, v in catalog.sequence.items()}
+    g = torch.Generator().manual_seed(4)
+    for s in range(2):
+        b = synth.make_batch(cfg, 64, seed=52 + s, edge_cases=True)
+        neg = torch.randint(1, V, (64, 10), generator=g)
+        got = _c5_step(model, opt, cfg, b, catalog, neg.to(DEV))
+        rb = synth.batch_to_torch(b)
+        rb['hard_negatives'] = [{'sparse': cat_sparse[neg[:, n]],
+                                 'sequence': {k: v[neg[:, n]] for k, v in cat_seq.items()}}
+                                for n in range(10)]
+        want = float(ref.step(rb, maps, temperature=float(cfg['train']['temperature'])))
+        assert abs(got - want) < 1e-4, (s, got, want)
+    sd = model.state_dict()
+    for k in ('user_tower.seq_encoder.feature_embedder.embeddings.hist_item_ids.weight',
+              'item_tower.embeddings.item_id_enc.weight', 'item_tower.mlp.mlp.0.weight'):
+        err = (sd[k].cpu() - ref.S[k].detach()).abs().max().item()
+        assert err < 1e-4, (k, err)
