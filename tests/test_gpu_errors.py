@@ -1,0 +1,111 @@
+"""The reference's failure behaviour, and the RCCL branches of the data-parallel exchange.
+
+* An embedding id outside its table raises IndexError (the reference raises at the offending
+  nn.Embedding call, GenericTower.py:184-196); here the gather flags it on the device and
+  train_one_epoch raises at its log-point sync, validate at its end.
+* NaN embeddings raise RuntimeError('Found NaN in ... Embedding') (TwoTowerModel.py:88-91),
+  flagged on the device every step, raised at the same syncs.
+* The 'nccl' (RCCL) branches of dist.allreduce_gradients / exchange_lazy_grads run on one GPU
+  with world_size = 1 and the exchange forced on: the step must equal the local step.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import yaml
+
+from oracle.twotower_oracle import model_state_shapes
+from recommendsystemproject_amd import dist as rdist
+from recommendsystemproject_amd import synth
+from recommendsystemproject_amd.flat import ensure_flat
+from recommendsystemproject_amd.optim import Adam
+from recommendsystemproject_amd.project.models.TwoTower.GenericTower import GenericTower
+from recommendsystemproject_amd.project.models.TwoTower.TwoTowerModel import TwoTowerModel
+from recommendsystemproject_amd.project.utils.training_utils import train_one_epoch, train_step
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEV = torch.device('cuda:0')
+
+
+def _model(seed=1):
+    cfg = yaml.safe_load(open(os.path.join(ROOT, 'configs', 'demo.yaml')))
+    for t in cfg['two_tower'].values():
+        t['dropout'] = 0.0
+        t.get('transformer_parameters', {})['dropout'] = 0.0
+    maps = {'user': synth.tower_layout(cfg['two_tower']['user_tower']),
+            'item': synth.tower_layout(cfg['two_tower']['item_tower'])}
+    shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
+    state = synth.make_state(shapes, seed=seed)
+    m = TwoTowerModel(GenericTower(cfg, 'user_tower'), GenericTower(cfg, 'item_tower'), maps['user'], maps['item'])
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()})
+    return m.to(DEV), cfg
+
+
+def _batches(cfg, n, B=32):
+    return [synth.batch_to_torch(synth.make_batch(cfg, B, seed=70 + i), DEV) for i in range(n)]
+
+
+def test_bad_id_raises_index_error_at_log_point():
+    model, cfg = _model()
+    opt = Adam(model.parameters(), lr=1e-3)
+    batches = _batches(cfg, 3)
+    batches[1]['item_tower']['sparse'][5, 0] = 10 ** 9  # outside the item table
+    with pytest.raises(IndexError):
+        train_one_epoch(model, batches, opt, DEV, log_every_n_batches=1, epoch=0, temperature=0.15)
+    model.check_errors()  # the flag was consumed by the raise
+
+
+def test_nan_embedding_raises_runtime_error():
+    model, cfg = _model()
+    opt = Adam(model.parameters(), lr=1e-3)
+    with torch.no_grad():
+        model.item_tower.mlp.mlp[8].weight[0, 0] = float('nan')
+    with pytest.raises(RuntimeError, match='Found NaN in Item Embedding'):
+        train_one_epoch(model, _batches(cfg, 2), opt, DEV, log_every_n_batches=100, epoch=0, temperature=0.15)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_rccl_exchange_world_size_one(monkeypatch):
+    """dist.is_active() is False at world_size 1, so the exchange is forced (is_active patched):
+    the RCCL all_reduce of the dense gradient and the all_gather_into_tensor of every lazy table's
+    ids and output gradients run, and the resulting step equals the plain local step."""
+    monkeypatch.setenv('RSYS_LAZY_ROWS', '1')
+    monkeypatch.setenv('MASTER_ADDR', '127.0.0.1')
+    monkeypatch.setenv('MASTER_PORT', str(_free_port()))
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=DEV)
+    try:
+        assert dist.get_backend() == 'nccl'
+        ref, cfg = _model()
+        opt_r = Adam(ref.parameters(), lr=1e-3)
+        b = _batches(cfg, 2)
+        for x in b:
+            train_step(ref, x, opt_r, 1.0, 0.15)
+        ensure_flat(ref).flush()
+
+        monkeypatch.setattr(rdist, 'is_active', lambda: True)
+        import recommendsystemproject_amd.flat as flat
+        monkeypatch.setattr(flat, '_dp_active', lambda: True)
+        model, _ = _model()
+        opt = Adam(model.parameters(), lr=1e-3)
+        f = ensure_flat(model)
+        assert len(f.lazy) >= 3
+        for x in b:
+            train_step(model, x, opt, 1.0, 0.15)
+            assert all(t.calls == [] and t.exchanged is None for t in f.lazy)
+        f.flush()
+        torch.cuda.synchronize()
+        assert torch.equal(f.data, ensure_flat(ref).data) or \
+            (f.data - ensure_flat(ref).data).abs().max().item() < 1e-6
+    finally:
+        dist.destroy_process_group()
