@@ -53,8 +53,8 @@ def _lookup_lazy(segs, tables, rows, keep=None):
             mode = SEG_ONE
             if pool:
                 mode = {_hip.RS_POOL['mean']: SEG_MEAN, _hip.RS_POOL['sum']: SEG_SUM}.get(s.pool_mode)
-            if mode is not None and s.dim > 256:
-                mode = None
+            if mode is not None and (s.dim > 256 or s.dim % 4):
+                mode = None  # rs_segsum: D <= 256, a multiple of 4 (float4 rows)
             c = lookup_table(t, s.idx, rows, bag, s.idx_stride, None if s.pad_idx < 0 else s.pad_idx,
                              -1 if mode is None else mode, keep=keep)
             if c is not None:
@@ -69,8 +69,9 @@ def _grad_lazy(segs, calls, dout, tables):
     rest = []
     for i, s in enumerate(segs):
         c = calls.get(i) if calls else None
-        if c is not None and c.mode >= 0:
-            tables[i]._rs_lazy.segsum(c, dout.data_ptr() + 4 * s.out_col, dout.stride(0))
+        ptr = dout.data_ptr() + 4 * s.out_col
+        if c is not None and c.mode >= 0 and ptr % 16 == 0 and dout.stride(0) % 4 == 0:
+            tables[i]._rs_lazy.segsum(c, ptr, dout.stride(0))
         else:
             rest.append(s)
     return rest
