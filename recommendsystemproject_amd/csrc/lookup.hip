@@ -473,6 +473,10 @@ constexpr int kRowGrid = 2048;
 // ---------------------------------------------------------------- segment sum (table gradient)
 constexpr int kChunk = 64;
 constexpr int kSegBatch = 16;  // positions whose contributions are loaded together
+// partial flags (per chunk, then per block of 64 chunks): a run comes in over the left border
+// (head partial), goes on over the right border too (through), or starts here and goes on
+// (tail partial)
+constexpr int kTail = 1, kHead = 2, kThrough = 4;
 
 struct SegArgs {
   const uint32_t* keys;
@@ -558,13 +562,14 @@ __global__ __launch_bounds__(256) void segsum_kernel(SegArgs a) {
   const uint32_t kn = lane < cn && pi + 1 < a.n ? a.keys[pi + 1] : kSentinel;
   const bool valid = k != kSentinel && (int64_t)k != a.pad;
   const bool single = valid && kp != k && kn != k;
+  const int brow = lane < cn ? (int)contrib_row(a, e) : 0;  // dout row of this lane's position
   const uint64_t smask = __ballot(single);
   const uint64_t mmask = __ballot(valid && !single);
   const float nbag = (float)a.bag;
   // ---- singletons
   if (smask) {
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    if (single) slot[wv][__popcll(smask & lt)] = make_int2((int)contrib_row(a, e), (int)k);
+    if (single) slot[wv][__popcll(smask & lt)] = make_int2(brow, (int)k);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const int ns = __popcll(smask);
@@ -614,16 +619,14 @@ __global__ __launch_bounds__(256) void segsum_kernel(SegArgs a) {
       for (int u = 0; u < kSegBatch; ++u) {
         pos[u] = m ? __ffsll((long long)m) - 1 : -1;
         if (m) m &= m - 1;
-        x[u][0] = 0.f;
-        if (pos[u] >= 0) {
-          const uint32_t ee = (uint32_t)__builtin_amdgcn_readlane((int)e, pos[u]);
-          const float* src = a.dout + contrib_row(a, ee) * a.ldo;
+        // loaded unconditionally (position 0's row stands in past the end of the mask): a load
+        // under a branch is waited for at the join
+        const int64_t row = (int64_t)__builtin_amdgcn_readlane((int)brow, pos[u] >= 0 ? pos[u] : 0);
+        const float* src = a.dout + row * a.ldo;
 #pragma unroll
-          for (int j = 0; j < NV; ++j) {
-            const int cc = lane + 64 * j;
-            x[u][j] = cc < a.D ? src[cc] : 0.f;
-            if (a.mode == 1) x[u][j] = x[u][j] / nbag;
-          }
+        for (int j = 0; j < NV; ++j) {
+          const int cc = lane + 64 * j;
+          x[u][j] = cc < a.D ? src[cc] : 0.f;
         }
       }
 #pragma unroll
@@ -632,17 +635,19 @@ __global__ __launch_bounds__(256) void segsum_kernel(SegArgs a) {
         if (i < 0) break;
         if (first < 0) first = i;
 #pragma unroll
-        for (int j = 0; j < NV; ++j) acc[j] += x[u][j];
+        for (int j = 0; j < NV; ++j) acc[j] += a.mode == 1 ? x[u][j] / nbag : x[u][j];
         const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)k, i);
         const uint32_t nk = (uint32_t)__builtin_amdgcn_readlane((int)kn, i);  // key after position i
         if (nk == key && i + 1 < cn) continue;  // the run goes on inside this chunk
         const bool head = first == 0 && kprev == key;   // began in an earlier chunk
         const bool tail = i + 1 == cn && knext == key;  // continues into the next chunk
         if (!head && !tail) put_row<NV>(a, key, acc);
-        else if (head) put_part<NV>(a, chunk, 0, acc);  // (also when it continues: "through")
-        else {
+        else if (head) {
+          put_part<NV>(a, chunk, 0, acc);  // (also when it continues: "through")
+          flag |= tail ? (kHead | kThrough) : kHead;
+        } else {
           put_part<NV>(a, chunk, 1, acc);
-          flag = 1;
+          flag |= kTail;
         }
 #pragma unroll
         for (int j = 0; j < NV; ++j) acc[j] = 0.f;
@@ -653,42 +658,128 @@ __global__ __launch_bounds__(256) void segsum_kernel(SegArgs a) {
   if (lane == 0) a.flags[chunk] = flag;
 }
 
-// runs crossing chunk borders: the chunk where the run starts adds its tail partial and the head
-// partials of the following chunks, in chunk order
+// Runs crossing chunk borders, in two levels of fixed-order partial sums (a Zipf hot row spans
+// hundreds to thousands of chunks; one wave walking them all was the longest step of the
+// backward). Level 1: one wave per block of kFixBlock chunks walks their partials in order,
+// stores the runs that start and end inside the block, and leaves a head / tail partial for the
+// runs crossing the block's borders. Level 2: the block where such a run starts adds its tail
+// partial and the following blocks' head partials. Both levels load their partials 16 at a time.
+constexpr int kFixBatch = 16;
+constexpr int kFixBlock = 16;  // chunks per level-1 block: one batch of loads per block wave
+
 template <int NV>
-__global__ __launch_bounds__(256) void segsum_fixup_kernel(SegArgs a) {
-  const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (chunk >= a.nchunks || !a.flags[chunk]) return;
+__device__ __forceinline__ void load_vec(const float* src, int D, float* v) {
   const int lane = threadIdx.x & 63;
-  const int64_t last = (int64_t)chunk * kChunk + kChunk - 1;
-  const uint32_t key = a.keys[last];
-  float acc[NV];
-  const float* t = a.part + ((int64_t)chunk * 2 + 1) * a.D;
 #pragma unroll
-  for (int j = 0; j < NV; ++j) acc[j] = lane + 64 * j < a.D ? t[lane + 64 * j] : 0.f;
-  // the following chunks' head partials, kFixBatch at a time with their loads in flight together
-  // (a hot row's run spans hundreds of chunks; one dependent round trip per chunk made this
-  // pass the longest of the backward under Zipf ids); added in chunk order
-  constexpr int kFixBatch = 16;
+  for (int j = 0; j < NV; ++j) v[j] = lane + 64 * j < D ? src[lane + 64 * j] : 0.f;
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void segsum_fix_blocks_kernel(SegArgs a) {
+  const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nblk = (a.nchunks + kFixBlock - 1) / kFixBlock;
+  if (blk >= nblk) return;
+  const int lane = threadIdx.x & 63;
+  const int j0 = blk * kFixBlock;
+  const int nc = a.nchunks - j0 < kFixBlock ? a.nchunks - j0 : kFixBlock;
+  const int fl = lane < nc ? a.flags[j0 + lane] : 0;
+  // first / last key of every chunk of the block, loaded up front (not inside the ordered walk)
+  const int64_t p0 = (int64_t)(j0 + lane) * kChunk;
+  const uint32_t kfirst = fl ? a.keys[p0] : kSentinel;
+  const uint32_t klast = fl ? a.keys[p0 + kChunk - 1 < a.n ? p0 + kChunk - 1 : a.n - 1] : kSentinel;
+  const uint64_t any = __ballot(fl != 0);
+  int bflag = 0;
+  if (any) {
+    float acc[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) acc[j] = 0.f;
+    bool open = false, from_left = false;
+    uint32_t key = kSentinel;
+    uint64_t m = any;
+    while (m) {
+      int cj[kFixBatch];
+      float hv[kFixBatch][NV], tv[kFixBatch][NV];
+#pragma unroll
+      for (int u = 0; u < kFixBatch; ++u) {
+        cj[u] = m ? __ffsll((long long)m) - 1 : -1;
+        if (m) m &= m - 1;
+        // both partials of every chunk of the batch, unconditionally (a load under a branch
+        // made the compiler wait for it at the join: one round trip per chunk)
+        const int64_t c = j0 + (cj[u] >= 0 ? cj[u] : 0);
+        load_vec<NV>(a.part + (c * 2) * a.D, a.D, hv[u]);
+        load_vec<NV>(a.part + (c * 2 + 1) * a.D, a.D, tv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kFixBatch; ++u) {
+        if (cj[u] < 0) break;
+        const int f = __builtin_amdgcn_readlane(fl, cj[u]);
+        if (f & kHead) {
+          if (!open) {  // the run came in over the block's left border
+            open = true;
+            from_left = true;
+            key = (uint32_t)__builtin_amdgcn_readlane((int)kfirst, cj[u]);
+#pragma unroll
+            for (int j = 0; j < NV; ++j) acc[j] = 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < NV; ++j) acc[j] += hv[u][j];
+          if (!(f & kThrough)) {  // ends in chunk c
+            if (from_left) {
+              put_part<NV>(a, a.nchunks + blk, 0, acc);
+              bflag |= kHead;
+            } else {
+              put_row<NV>(a, key, acc);
+            }
+            open = false;
+          }
+        }
+        if (f & kTail) {
+          open = true;
+          from_left = false;
+          key = (uint32_t)__builtin_amdgcn_readlane((int)klast, cj[u]);
+#pragma unroll
+          for (int j = 0; j < NV; ++j) acc[j] = tv[u][j];
+        }
+      }
+    }
+    if (open) {  // continues over the block's right border
+      if (from_left) {
+        put_part<NV>(a, a.nchunks + blk, 0, acc);
+        bflag |= kHead | kThrough;
+      } else {
+        put_part<NV>(a, a.nchunks + blk, 1, acc);
+        bflag |= kTail;
+      }
+    }
+  }
+  if (lane == 0) a.flags[a.nchunks + blk] = bflag;
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void segsum_fix_runs_kernel(SegArgs a) {
+  const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nblk = (a.nchunks + kFixBlock - 1) / kFixBlock;
+  if (blk >= nblk || !(a.flags[a.nchunks + blk] & kTail)) return;
+  const int64_t lastpos = (int64_t)(blk * kFixBlock + kFixBlock - 1) * kChunk + kChunk - 1;
+  const uint32_t key = a.keys[lastpos < a.n ? lastpos : a.n - 1];
+  float acc[NV];
+  load_vec<NV>(a.part + ((int64_t)(a.nchunks + blk) * 2 + 1) * a.D, a.D, acc);
   bool done = false;
-  for (int c = chunk + 1; c < a.nchunks && !done; c += kFixBatch) {
+  for (int b = blk + 1; b < nblk && !done; b += kFixBatch) {
     float h[kFixBatch][NV];
-    uint32_t kend[kFixBatch];
+    int f[kFixBatch];
 #pragma unroll
     for (int u = 0; u < kFixBatch; ++u) {
-      const int cc = c + u < a.nchunks ? c + u : a.nchunks - 1;
-      const float* hp = a.part + ((int64_t)cc * 2) * a.D;
-#pragma unroll
-      for (int j = 0; j < NV; ++j) h[u][j] = lane + 64 * j < a.D ? hp[lane + 64 * j] : 0.f;
-      const int64_t end = (int64_t)cc * kChunk + kChunk;  // first position after chunk cc
-      kend[u] = end < a.n ? a.keys[end] : kSentinel;
+      const int bb = b + u < nblk ? b + u : nblk - 1;
+      f[u] = a.flags[a.nchunks + bb];
+      load_vec<NV>(a.part + ((int64_t)(a.nchunks + bb) * 2) * a.D, a.D, h[u]);
     }
 #pragma unroll
     for (int u = 0; u < kFixBatch; ++u) {
-      if (done || c + u >= a.nchunks) { done = true; continue; }
+      if (done || b + u >= nblk) { done = true; continue; }
 #pragma unroll
       for (int j = 0; j < NV; ++j) acc[j] += h[u][j];
-      if (kend[u] != key) done = true;  // the run ends in chunk c + u
+      if (!(f[u] & kThrough)) done = true;  // the run ends in block b + u
     }
   }
   put_row<NV>(a, key, acc);
@@ -835,7 +926,8 @@ extern "C" int rs_sorted_zero_grad(const uint32_t* keys, int64_t n, int D, float
 
 extern "C" int64_t rs_segsum_ws_bytes(int64_t n, int D) {
   const int64_t nc = (n + kChunk - 1) / kChunk;
-  return nc * 2 * D * 4 + nc * 4 + 256;
+  const int64_t np = nc + (nc + kFixBlock - 1) / kFixBlock;  // chunk partials, then block partials
+  return np * 2 * D * 4 + np * 4 + 256;
 }
 
 extern "C" int rs_segsum(const uint32_t* keys, const uint32_t* vals, int64_t n, int bag, int mode,
@@ -851,16 +943,20 @@ extern "C" int rs_segsum(const uint32_t* keys, const uint32_t* vals, int64_t n, 
   a.ldo = ldo; a.D = D; a.grad = grad; a.accumulate = accumulate;
   a.nchunks = cdiv(n, kChunk);
   a.part = static_cast<float*>(ws);
-  a.flags = reinterpret_cast<int*>(a.part + (int64_t)a.nchunks * 2 * D);
+  const int64_t np = a.nchunks + (a.nchunks + kFixBlock - 1) / kFixBlock;
+  a.flags = reinterpret_cast<int*>(a.part + np * 2 * D);
   hipStream_t st = as_stream(stream);
   const int grid = cdiv(a.nchunks, 4);
   RS_CHECK_ARG(D % 4 == 0 && ldo % 4 == 0 && aligned16(dout) && aligned16(grad),
                "rs_segsum: D, ldo multiples of 4 and 16-byte aligned dout / grad required");
+  const int bgrid = cdiv(cdiv(a.nchunks, kFixBlock), 4);
 #define RS_SEGSUM(NV, G)                                               \
   segsum_kernel<NV, G><<<grid, 256, 0, st>>>(a);                       \
   RS_CHECK_LAUNCH("rs_segsum");                                        \
-  segsum_fixup_kernel<NV><<<grid, 256, 0, st>>>(a);                    \
-  RS_CHECK_LAUNCH("rs_segsum fixup");
+  segsum_fix_blocks_kernel<NV><<<bgrid, 256, 0, st>>>(a);              \
+  RS_CHECK_LAUNCH("rs_segsum blocks");                                 \
+  segsum_fix_runs_kernel<NV><<<bgrid, 256, 0, st>>>(a);                \
+  RS_CHECK_LAUNCH("rs_segsum runs");
   if (D <= 16) { RS_SEGSUM(1, 4) }
   else if (D <= 32) { RS_SEGSUM(1, 8) }
   else if (D <= 64) { RS_SEGSUM(1, 16) }
