@@ -58,8 +58,9 @@ def parse():
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--dtype', default='config', choices=['config', 'fp32', 'bf16'],
                     help='compute dtype of the GEMMs (bf16: bf16 MFMA, fp32 accumulate / master weights); '
-                         'config: bf16 for c2 (BASELINE configs[1] is quoted in bf16) and c5 (its L = 200 '
-                         'encoder runs on the bf16 MFMA attention), fp32 otherwise')
+                         'config: bf16 for c2 (BASELINE configs[1] is quoted in bf16), c3 (the fused bf16 '
+                         'in-batch CE) and c5 (its L = 200 encoder runs on the bf16 MFMA attention), fp32 '
+                         'otherwise; --dtype fp32 is the parity precision')
     ap.add_argument('--hard-negatives', type=int, default=0,
                     help='N sampled hard negatives per row, materialised from a device item catalog '
                          'each step (one grouped item-tower pass)')
@@ -510,7 +511,7 @@ def main():
     dev = torch.device(f'cuda:{local}')
     torch.cuda.set_device(dev)
     if args.dtype == 'config':
-        args.dtype = 'bf16' if args.config in ('c2', 'c5') else 'fp32'
+        args.dtype = 'bf16' if args.config in ('c2', 'c3', 'c5') else 'fp32'
     cpu_s = 0.0 if args.no_cpu_baseline else args.cpu_baseline_seconds
     out = run_workload(args, args.config, args.dtype, args.zipf, args.hard_negatives, rank, world, dev,
                        cpu_s)
@@ -522,7 +523,7 @@ def main():
     for ex in [e for e in (args.extra or '').split(',') if e and e != args.config]:
         # the other headline workloads in the same line (BASELINE configs[2] = C3; at N > 1 the
         # same run is configs[3] = C4, C3 data-parallel)
-        ex_dtype = 'bf16' if ex in ('c2', 'c5') else 'fp32'
+        ex_dtype = 'bf16' if ex in ('c2', 'c3', 'c5') else 'fp32'
         r = run_workload(args, ex, ex_dtype, None, 10 if ex == 'c5' else 0, rank, world, dev,
                          cpu_s / 2)
         if r is not None:
