@@ -121,7 +121,12 @@ def _history_csr(user_history, all_item_ids_cpu, device):
     max_id = int(ids.max())
     id_to_index = np.full(max_id + 1, -1, dtype=np.int64)
     id_to_index[ids] = np.arange(len(ids))
-    users = [int(u) for u in user_history.keys() if int(u) >= 0]
+    def _uid(u):  # the reference's build_user_history can key by column NAME (list columns)
+        try:
+            return int(u)
+        except (TypeError, ValueError):
+            return -1
+    users = [_uid(u) for u in user_history.keys() if _uid(u) >= 0]
     U = (max(users) + 1) if users else 0
     counts = np.zeros(U + 1, dtype=np.int64)
     cols = []
