@@ -230,3 +230,36 @@ class Adam(torch.optim.Optimizer):
                 if p in self.state:
                     self.state[p]['step'] = torch.tensor(step)
         return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        """torch.optim.Adam.load_state_dict, then the loaded exp_avg / exp_avg_sq / step copied
+        into the flat buffers the kernels read (the per-parameter state stays views of them).
+        Every row of a lazy table is marked current at the loaded step (a checkpoint is written
+        flushed), so no earlier step is ever replayed."""
+        flats = [self._group_flat(g) for g in self.param_groups]
+        for f in flats:  # the flat buffers exist before the loaded per-parameter state lands
+            if f is not None:
+                self._state_for_flat(f)
+        super().load_state_dict(state_dict)
+        for f in flats:
+            if f is None:
+                continue
+            st = self._flat_state[id(f)]
+            step = 0
+            with torch.no_grad():
+                for p, o in zip(f.params, f.offsets):
+                    s = self.state.get(p)
+                    if not s or 'exp_avg' not in s:
+                        continue
+                    n = p.numel()
+                    st['m'][o:o + n].copy_(s['exp_avg'].reshape(-1))
+                    st['v'][o:o + n].copy_(s['exp_avg_sq'].reshape(-1))
+                    step = max(step, int(float(s['step'])))
+                    self.state[p] = {'step': torch.tensor(float(step)),
+                                     'exp_avg': st['m'][o:o + n].view(p.shape),
+                                     'exp_avg_sq': st['v'][o:o + n].view(p.shape)}
+            st['step'] = step
+            st['step_dev'].fill_(step)
+            for t in f.lazy:
+                t.last.fill_(step)
+                t.end_step()
