@@ -3,10 +3,11 @@ target is reported on a launch of >= 100 MB).
 
     python tools/gather_bench.py [--vocab 10000000] [--dim 128] [--rows 65536] [--bag 50]
 
-Pooled-mean bags (the C3 history feature) and single-id lookups, forward gather and backward
-scatter (touch counts on, as for a lazy-Adam table). Algorithmic bytes per launch:
+Pooled-mean bags (the C3 history feature) and single-id lookups, forward gather and the
+backward table gradient of a large table (rs_lookup_sort + rs_segsum). Algorithmic bytes per
+launch:
   fwd: lookups * D * 4 (rows read) + rows * D * 4 (written) + lookups * 8 (int64 ids)
-  bwd: the same rows written (first lookup: plain store) + dout read + ids
+  bwd: lookups * D * 4 (rows scattered) + rows * D * 4 (dout read) + lookups * 4
 Prints one JSON line per case.
 """
 import argparse
@@ -43,6 +44,7 @@ def main():
     ap.add_argument('--rows', type=int, default=65536)
     ap.add_argument('--bag', type=int, default=50)
     ap.add_argument('--iters', type=int, default=20)
+    ap.add_argument('--zipf', type=float, default=None)
     args = ap.parse_args()
     dev = torch.device('cuda:0')
     V, D, B, L = args.vocab, args.dim, args.rows, args.bag
@@ -52,6 +54,11 @@ def main():
     copy_gbs = 6290.0  # MI355X_MICROARCH.md: measured float4 copy bandwidth
     for kind, bag in (('pooled_mean', L), ('single_id', 1)):
         ids = torch.randint(1, V, (B, bag), device=dev, generator=g)
+        if args.zipf:
+            import numpy as np
+            z = np.random.default_rng(0).zipf(args.zipf, size=(B, bag)).astype(np.uint64) - np.uint64(1)
+            z = ((z * np.uint64(2654435761)) % np.uint64(V - 1)).astype(np.int64) + 1
+            ids = torch.from_numpy(z).to(dev)
         out = torch.empty(B, D, device=dev)
         if bag > 1:
             seg = _seg(kind=_hip.RS_SEG_POOL, dim=D, out_col=0, pool_mode=_hip.RS_POOL['mean'], bag=bag,
@@ -66,23 +73,30 @@ def main():
                           'MB_per_launch': round(byts / 1e6, 1), 'us': round(ms * 1e3, 1),
                           'GBps': round(byts / ms / 1e6, 1), 'frac_of_8TBps': round(byts / ms / 1e6 / PEAK, 3),
                           'frac_of_copy': round(byts / ms / 1e6 / copy_gbs, 3)}))
-        # backward scatter into a table gradient with touch counts (lazy-Adam tables)
+        # backward: the table gradient of a large (lazy-Adam) table -- the lookups sorted by row
+        # (rs_lookup_sort, forward side) and segment-summed (rs_segsum), csrc/lookup.hip
         grad = torch.zeros(V, D, device=dev)
-        flag = torch.zeros(V, dtype=torch.int32, device=dev)
-        lst = torch.zeros(V, dtype=torch.int32, device=dev)
-        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-        _hip.call('rs_sparse_touch', ids.data_ptr(), B, bag, bag, V, 0, flag.data_ptr(), lst.data_ptr(),
-                  cnt.data_ptr(), ops.stream())
-        seg.grad = grad.data_ptr()
-        seg.touch_count = flag.data_ptr()
+        n = B * bag
+        keys = torch.empty(n, dtype=torch.int32, device=dev)
+        vals = torch.empty(n, dtype=torch.int32, device=dev)
+        wsb = int(_hip.lib().rs_lookup_sort_ws_bytes(n, V))
+        wso = torch.empty(wsb // 4 + 1, dtype=torch.int32, device=dev)
+        sort = lambda: _hip.call('rs_lookup_sort', ids.data_ptr(), 8, B, bag, bag, V, keys.data_ptr(),  # noqa: E731
+                                 vals.data_ptr(), wso.data_ptr(), ops.stream())
+        ms_sort = timed(sort, args.iters)
         dout = torch.randn(B, D, device=dev)
-        ms = timed(lambda: ops.gather_bwd([seg], B, dout), args.iters)
-        byts = lookups * D * 4 + B * D * 4 + lookups * (8 + 4)
-        print(json.dumps({'case': f'gather_bwd {kind} (touch counts)', 'MB_per_launch': round(byts / 1e6, 1),
+        wss = torch.empty(int(_hip.lib().rs_segsum_ws_bytes(n, D)) // 4 + 1, dtype=torch.int32, device=dev)
+        seg_fn = lambda: _hip.call('rs_segsum', keys.data_ptr(), vals.data_ptr(), n, bag,  # noqa: E731
+                                   1 if bag > 1 else 0, 0, dout.data_ptr(), D, D, grad.data_ptr(), 0,
+                                   wss.data_ptr(), ops.stream())
+        ms = timed(seg_fn, args.iters)
+        byts = lookups * D * 4 + B * D * 4 + lookups * 4
+        print(json.dumps({'case': f'table_grad {kind} (rs_segsum)', 'MB_per_launch': round(byts / 1e6, 1),
                           'us': round(ms * 1e3, 1), 'GBps': round(byts / ms / 1e6, 1),
                           'frac_of_8TBps': round(byts / ms / 1e6 / PEAK, 3),
-                          'frac_of_copy': round(byts / ms / 1e6 / copy_gbs, 3)}))
-        del grad, flag, lst
+                          'frac_of_copy': round(byts / ms / 1e6 / copy_gbs, 3),
+                          'sort_us': round(ms_sort * 1e3, 1)}))
+        del grad
     assert err.item() == 0
 
 
