@@ -548,11 +548,8 @@ __device__ __forceinline__ int64_t contrib_row(const SegArgs& a, uint32_t e) {
 //    contributions loaded kSegBatch at a time; a run crossing the chunk border leaves a head or
 //    tail partial for the fixup pass.
 template <int NV, int G>
-__global__ __launch_bounds__(256) void segsum_kernel(SegArgs a) {
-  __shared__ int2 slot[4][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int chunk = blockIdx.x * 4 + wv;
-  if (chunk >= a.nchunks) return;
+__device__ __forceinline__ void segsum_chunk(const SegArgs& a, int chunk, int2* slot) {
+  const int lane = threadIdx.x & 63;
   const int64_t c0 = (int64_t)chunk * kChunk;
   const int cn = (int)(a.n - c0 < kChunk ? a.n - c0 : kChunk);
   const int64_t pi = c0 + lane;
@@ -569,7 +566,7 @@ __global__ __launch_bounds__(256) void segsum_kernel(SegArgs a) {
   // ---- singletons
   if (smask) {
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    if (single) slot[wv][__popcll(smask & lt)] = make_int2(brow, (int)k);
+    if (single) slot[__popcll(smask & lt)] = make_int2(brow, (int)k);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const int ns = __popcll(smask);
@@ -583,7 +580,7 @@ __global__ __launch_bounds__(256) void segsum_kernel(SegArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int j = r0 + u * R + g;
-        sl[u] = j < ns ? slot[wv][j] : make_int2(-1, 0);
+        sl[u] = j < ns ? slot[j] : make_int2(-1, 0);
         x[u] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (sl[u].x >= 0 && c < a.D)
           x[u] = *reinterpret_cast<const float4*>(a.dout + (int64_t)sl[u].x * a.ldo + c);
@@ -675,8 +672,7 @@ __device__ __forceinline__ void load_vec(const float* src, int D, float* v) {
 }
 
 template <int NV>
-__global__ __launch_bounds__(256) void segsum_fix_blocks_kernel(SegArgs a) {
-  const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+__device__ __forceinline__ void fix_block(const SegArgs& a, int blk) {
   const int nblk = (a.nchunks + kFixBlock - 1) / kFixBlock;
   if (blk >= nblk) return;
   const int lane = threadIdx.x & 63;
@@ -756,8 +752,7 @@ __global__ __launch_bounds__(256) void segsum_fix_blocks_kernel(SegArgs a) {
 }
 
 template <int NV>
-__global__ __launch_bounds__(256) void segsum_fix_runs_kernel(SegArgs a) {
-  const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+__device__ __forceinline__ void fix_run(const SegArgs& a, int blk) {
   const int nblk = (a.nchunks + kFixBlock - 1) / kFixBlock;
   if (blk >= nblk || !(a.flags[a.nchunks + blk] & kTail)) return;
   const int64_t lastpos = (int64_t)(blk * kFixBlock + kFixBlock - 1) * kChunk + kChunk - 1;
@@ -783,6 +778,23 @@ __global__ __launch_bounds__(256) void segsum_fix_runs_kernel(SegArgs a) {
     }
   }
   put_row<NV>(a, key, acc);
+}
+
+template <int NV, int G>
+__global__ __launch_bounds__(256) void segsum_kernel(SegArgs a) {
+  __shared__ int2 slot[4][64];
+  const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (chunk < a.nchunks) segsum_chunk<NV, G>(a, chunk, slot[threadIdx.x >> 6]);
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void segsum_fix_blocks_kernel(SegArgs a) {
+  fix_block<NV>(a, blockIdx.x * 4 + (threadIdx.x >> 6));
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void segsum_fix_runs_kernel(SegArgs a) {
+  fix_run<NV>(a, blockIdx.x * 4 + (threadIdx.x >> 6));
 }
 
 AdamConst make_hyper(float b1, float b2, float eps, float wd) {
