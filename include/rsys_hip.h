@@ -249,6 +249,55 @@ int rs_batchnorm_bwd(const float* x, const float* y, const float* dy, const floa
                      const float* mean, const float* rstd, float* dx, float* dw, float* db,
                      int G, int Bg, int C, int relu, float drop_scale, float* ws, void* stream);
 
+/* ---------------------------------------------------------------- fused DSSM tower chain
+ * GenericTower.feature_bn + MLP_Tower in training mode (GenericTower.py:229-236, Tower.py:16-41;
+ * K12-K14): one kernel per Linear. A BatchNorm's batch statistics are produced by the kernel
+ * that writes its input: per-row-tile column values go to `part` (rs_tower_part_floats(G, Bg, N,
+ * kind) floats; kind 0 = rs_tower_stats, 1 = the GEMM kernels) and the last workgroup of each
+ * (group, 64-column block) merges them in a fixed order and publishes the results; `sync` is
+ * rs_tower_sync_ints(G, N) ints that must be ZERO on entry (they are zero again on exit:
+ * allocate once, reuse), `scratch` is G * 2 * N doubles. bf16 != 0: GEMM operands rounded to
+ * bf16 (bf16 compute mode), fp32 otherwise; accumulation and every stored tensor fp32.
+ *
+ * rs_tower_stats: feature_bn's batch statistics of x [G*Bg, C] (GenericTower.py:234): mean /
+ *   rstd [G*C] published, running statistics updated group by group (momentum, unbiased
+ *   variance), num_batches_tracked += G.
+ * rs_tower_fwd: A [G*Bg, K] -> BN with the published in_mean / in_rstd and bn_w / bn_b (+ ReLU
+ *   + dropout (key, site) when relu: the rs_dropout_fwd draw of element row*K + k, Tower.py:17-19)
+ *   -> h (written to h_out when non-NULL: the weight-gradient operand) -> h W^T + bias (W [N][K],
+ *   nn.Linear, Tower.py:16). Hidden layer: z [G*Bg, N] with the statistics of ITS BatchNorm
+ *   published as for rs_tower_stats (mean / rstd, running statistics); final layer (z == NULL):
+ *   out = F.normalize(.) (Tower.py:41) and norm [G*Bg] (N <= 128).
+ * rs_tower_bwd: the input gradient through one Linear. Prologue, y != NULL: dz = F.normalize
+ *   backward of gin (y = out, norm); else dz = BatchNorm backward of gin (the masked gradient at
+ *   that BN's output) from z, its mean / rstd / bn_w and the published means mg, mgx of g and
+ *   g*xhat. dz is written (the weight-gradient operand). N > 0: g = mask(dz W) (W [K][N]), mask =
+ *   the ReLU + dropout of the BatchNorm below (e_relu, e_drop_p, e_key, e_site; recomputed from
+ *   its pre-BN ez and e_mean / e_rstd / e_w / e_b), written, and that BatchNorm's means of g and
+ *   g*xhat published to out_mg / out_mgx with e_dgamma += sum g*xhat, e_dbeta += sum g.
+ *   N == 0: dz is feature_bn's dx (no GEMM). */
+int64_t rs_tower_part_floats(int G, int Bg, int N, int kind);
+/* profiling only: per-workgroup phase timestamps of the tower GEMM kernels into buf (NULL: off) */
+int rs_tower_debug_buffer(unsigned long long* buf);
+int rs_tower_sync_ints(int G, int N);
+int rs_tower_stats(const float* x, int G, int Bg, int C, float* part, int* sync, double* scratch,
+                   float* mean, float* rstd, float* running_mean, float* running_var,
+                   int64_t* num_batches, float momentum, float eps, void* stream);
+int rs_tower_fwd(const float* A, int G, int Bg, int K, const float* in_mean, const float* in_rstd,
+                 const float* bn_w, const float* bn_b, int relu, float drop_p, const int64_t* key,
+                 int site, float* h_out, const float* W, const float* bias, int N, float* z,
+                 float* part, int* sync, double* scratch, float* mean, float* rstd,
+                 float* running_mean, float* running_var, int64_t* num_batches, float momentum,
+                 float eps, float* out, float* norm, float l2_eps, int bf16, void* stream);
+int rs_tower_bwd(const float* gin, int G, int Bg, int K, const float* y, const float* norm,
+                 float l2_eps, const float* z, const float* mean, const float* rstd,
+                 const float* bn_w, const float* mg, const float* mgx, float* dz, const float* W,
+                 int N, const float* ez, const float* e_mean, const float* e_rstd,
+                 const float* e_w, const float* e_b, int e_relu, float e_drop_p,
+                 const int64_t* e_key, int e_site, float* g, float* part, int* sync,
+                 double* scratch, float* out_mg, float* out_mgx, float* e_dgamma, float* e_dbeta,
+                 int bf16, void* stream);
+
 /* ---------------------------------------------------------------- misc elementwise */
 /* y = x / max(||x||_2, eps) per row (F.normalize, Tower.py:41; K14); norm [M] saved */
 int rs_l2norm_fwd(const float* x, float* y, float* norm, int M, int N, float eps, void* stream);

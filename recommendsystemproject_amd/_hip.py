@@ -67,6 +67,14 @@ SIGNATURES = {
     'rs_batchnorm_ws_bytes': (i64, [i32, i32, i32]),
     'rs_batchnorm_fwd': (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, i32, i32,
                                f32, vp, i32, vp, vp]),
+    'rs_tower_part_floats': (i64, [i32, i32, i32, i32]),
+    'rs_tower_debug_buffer': (i32, [vp]),
+    'rs_tower_sync_ints': (i32, [i32, i32]),
+    'rs_tower_stats': (i32, [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, f32, vp]),
+    'rs_tower_fwd': (i32, [vp, i32, i32, i32, vp, vp, vp, vp, i32, f32, vp, i32, vp, vp, vp, i32, vp, vp,
+                           vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, vp, f32, i32, vp]),
+    'rs_tower_bwd': (i32, [vp, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp,
+                           vp, vp, vp, i32, f32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp]),
     'rs_batchnorm_bwd': (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp, vp]),
     'rs_l2norm_fwd': (i32, [vp, vp, vp, i32, i32, f32, vp]),
     'rs_l2norm_bwd': (i32, [vp, vp, vp, vp, i32, i32, f32, vp]),

@@ -645,6 +645,164 @@ class MLPFn(torch.autograd.Function):
         return (None, None, dh, None) + (None,) * (len(ctx.needs_input_grad) - 4)
 
 
+# ================================================================================ fused tower chain
+def tower_chain_supported(feature_bn, mlp, x, G) -> bool:
+    """The fused chain (csrc/tower.hip) covers training mode with batch statistics: feature_bn and
+    every hidden BatchNorm with a momentum, inputs of width <= 512, hidden widths <= 256, an output
+    of width <= 128, all multiples of 4. Eval mode (running statistics) and other shapes take the
+    per-op path (BatchNormFn + MLPFn). RSYS_TOWER_CHAIN=0 forces the per-op path (A/B)."""
+    if os.environ.get('RSYS_TOWER_CHAIN', '1') == '0':
+        return False
+    if not (feature_bn.training and mlp.training) or x.dim() != 2:
+        return False
+    seq = mlp.mlp
+    n_hidden = (len(seq) - 1) // 4
+    bns = [feature_bn] + [seq[4 * j + 1] for j in range(n_hidden)]
+    if any(b.momentum is None for b in bns):
+        return False
+    C0 = int(x.shape[1])
+    widths = [int(seq[4 * j].out_features) for j in range(n_hidden)]
+    out = int(seq[len(seq) - 1].out_features)
+    M = int(x.shape[0])
+    if C0 % 4 or C0 > 512 or any(w % 4 or w > 256 for w in widths) or out % 4 or out > 128:
+        return False
+    return M % G == 0 and M * max([C0, out] + widths) < 2 ** 32
+
+
+def _tower_sync(mlp, dev, n):
+    """Zeroed int32 tickets for the chain's statistics hand-offs (csrc/tower.hip): every kernel
+    leaves them zero again, so one buffer per tower module serves every call (and graph replay)."""
+    t = getattr(mlp, '_rs_tower_sync', None)
+    if t is None or t.device != dev or t.numel() < n:
+        t = torch.zeros(max(n, 64), dtype=torch.int32, device=dev)
+        mlp._rs_tower_sync = t
+    return t
+
+
+class TowerChainFn(torch.autograd.Function):
+    """GenericTower.feature_bn + MLP_Tower in training mode (GenericTower.py:229-236; Tower.py:16-41)
+    as one kernel per Linear (csrc/tower.hip): a BatchNorm's statistics are merged by the last
+    workgroup of the kernel that produces its input and applied in the next GEMM's operand
+    staging; F.normalize is the last GEMM's epilogue. Same dropout draws as MLPFn (key from the
+    MLP's rng state, site 256 + j), same running-statistic updates. Parameter gradients are
+    accumulated into the flat buffers."""
+
+    @staticmethod
+    def forward(ctx, need, feature_bn, mlp, x, G, *params):
+        L = _hip.lib()
+        seq = mlp.mlp
+        n_hidden = (len(seq) - 1) // 4
+        p = mlp.dropout_p
+        key = ops.rng_next(mlp.rng_state) if p > 0 else None
+        bf = int(precision.compute_dtype() == 'bf16')
+        x = x.contiguous()
+        dev = x.device
+        M = int(x.shape[0])
+        Bg = M // G
+        f32 = torch.float32
+        widths = [int(x.shape[1])] + [int(seq[4 * j].out_features) for j in range(n_hidden)]
+        nsync = [L.rs_tower_sync_ints(G, w) for w in widths]
+        sync = _tower_sync(mlp, dev, 2 * sum(nsync) + 2 * L.rs_tower_sync_ints(G, int(seq[-1].in_features)))
+        ctx_sync_off = sum(nsync)
+
+        def handoff(w, kind, bn, j):
+            """part, sync slice, scratch, mean, rstd and running stats of one BatchNorm."""
+            part = torch.empty(L.rs_tower_part_floats(G, Bg, w, kind), device=dev, dtype=f32)
+            off = sum(nsync[:j])
+            scr = torch.empty(G * 2 * w, device=dev, dtype=torch.float64)
+            mean = torch.empty(G * w, device=dev, dtype=f32)
+            rstd = torch.empty(G * w, device=dev, dtype=f32)
+            track = bn.track_running_stats and bn.running_mean is not None
+            return (part.data_ptr(), sync[off:].data_ptr(), scr.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                    ops.P(bn.running_mean) if track else None, ops.P(bn.running_var) if track else None,
+                    ops.P(bn.num_batches_tracked) if track else None, float(bn.momentum), float(bn.eps)), \
+                (part, scr, mean, rstd)
+
+        hf, keep = handoff(widths[0], 0, feature_bn, 0)
+        ops.call('rs_tower_stats', x.data_ptr(), G, Bg, widths[0], *hf, ops.stream())
+        A, bn, relu, dp, site = x, feature_bn, 0, 0.0, 0
+        mean, rstd = keep[2], keep[3]
+        layers = []
+        out = norm = None
+        for j in range(n_hidden + 1):
+            lin = seq[4 * j]
+            K, N = int(A.shape[1]), int(lin.out_features)
+            final = j == n_hidden
+            h = torch.empty(M, K, device=dev, dtype=f32) if need else None
+            if final:
+                z = None
+                out = torch.empty(M, N, device=dev, dtype=f32)
+                norm = torch.empty(M, device=dev, dtype=f32)
+                hf_out, keep_out = (None,) * 8 + (0.0, 0.0), None
+            else:
+                z = torch.empty(M, N, device=dev, dtype=f32)
+                hf_out, keep_out = handoff(N, 1, seq[4 * j + 1], j + 1)
+            ops.call('rs_tower_fwd', A.data_ptr(), G, Bg, K, mean.data_ptr(), rstd.data_ptr(),
+                     ops.P(bn.weight), ops.P(bn.bias), relu, dp, ops.P(key) if dp > 0 else None, site,
+                     ops.P(h), lin.weight.data_ptr(), lin.bias.data_ptr(), N, ops.P(z), *hf_out,
+                     ops.P(out), ops.P(norm), 1e-12, bf, ops.stream())
+            layers.append((A, h, mean, rstd, bn, relu, dp, site))
+            if not final:
+                A, mean, rstd = z, keep_out[2], keep_out[3]
+                bn, relu, dp, site = seq[4 * j + 1], 1, p, 256 + j
+        if need:
+            ctx.mlp, ctx.feature_bn, ctx.G, ctx.key, ctx.bf = mlp, feature_bn, G, key, bf
+            ctx.layers, ctx.out, ctx.norm = layers, out, norm
+            ctx.sync, ctx.sync_off = sync, ctx_sync_off
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dout):
+        L = _hip.lib()
+        seq = ctx.mlp.mlp
+        layers = ctx.layers
+        n_hidden = len(layers) - 1
+        G, bf, key = ctx.G, ctx.bf, ctx.key
+        dout = dout.contiguous()
+        M = int(dout.shape[0])
+        Bg = M // G
+        dev = dout.device
+        f32 = torch.float32
+        off = ctx.sync_off
+        gin, mg, mgx = dout, None, None
+        for j in range(n_hidden, -1, -1):
+            lin = seq[4 * j]
+            A, h, mean, rstd, bn_in, relu, dp, site = layers[j]
+            Kj, N = int(lin.out_features), int(lin.in_features)
+            dz = torch.empty(M, Kj, device=dev, dtype=f32)
+            g = torch.empty(M, N, device=dev, dtype=f32)
+            part = torch.empty(L.rs_tower_part_floats(G, Bg, N, 1), device=dev, dtype=f32)
+            scr = torch.empty(G * 2 * N, device=dev, dtype=torch.float64)
+            omg = torch.empty(G * N, device=dev, dtype=f32)
+            omgx = torch.empty(G * N, device=dev, dtype=f32)
+            if j == n_hidden:  # F.normalize backward in the prologue
+                pro = (ctx.out.data_ptr(), ctx.norm.data_ptr(), 1e-12, None, None, None, None, None, None)
+            else:  # BN_j backward in the prologue: its z / statistics are layer j+1's input
+                zj, _, mj, rj, bnj = layers[j + 1][:5]
+                pro = (None, None, 0.0, zj.data_ptr(), mj.data_ptr(), rj.data_ptr(), bnj.weight.data_ptr(),
+                       mg.data_ptr(), mgx.data_ptr())
+            ops.call('rs_tower_bwd', gin.data_ptr(), G, Bg, Kj, *pro, dz.data_ptr(), lin.weight.data_ptr(), N,
+                     A.data_ptr(), mean.data_ptr(), rstd.data_ptr(), ops.P(bn_in.weight) if relu else None,
+                     ops.P(bn_in.bias) if relu else None, relu, dp, ops.P(key) if dp > 0 else None, site,
+                     g.data_ptr(), part.data_ptr(), ctx.sync[off:].data_ptr(), scr.data_ptr(), omg.data_ptr(),
+                     omgx.data_ptr(), grad_of(bn_in.weight).data_ptr(), grad_of(bn_in.bias).data_ptr(), bf,
+                     ops.stream())
+            off += L.rs_tower_sync_ints(G, N)
+            _tower_wgrad(dz, h, lin)
+            gin, mg, mgx = g, omg, omgx
+        # feature_bn's dx: the BatchNorm backward prologue with no GEMM
+        x, _, m0, r0, fbn = layers[0][:5]
+        C0 = int(x.shape[1])
+        dx = torch.empty(M, C0, device=dev, dtype=f32)
+        ops.call('rs_tower_bwd', gin.data_ptr(), G, Bg, C0, None, None, 0.0, x.data_ptr(), m0.data_ptr(),
+                 r0.data_ptr(), fbn.weight.data_ptr(), mg.data_ptr(), mgx.data_ptr(), dx.data_ptr(), None, 0,
+                 None, None, None, None, None, 0, 0.0, None, 0, None, None, None, None, None, None, None, None,
+                 bf, ops.stream())
+        ctx.layers = None
+        return (None, None, None, dx, None) + (None,) * (len(ctx.needs_input_grad) - 5)
+
+
 # ================================================================================ loss
 class InBatchLossFn(torch.autograd.Function):
     """TwoTowerModel.compute_loss (TwoTowerModel.py:81-140, T12): logits = U I^T / T with

@@ -9,7 +9,8 @@ import torch.nn as nn
 
 from recommendsystemproject_amd import _hip
 from recommendsystemproject_amd.flat import ensure_flat
-from recommendsystemproject_amd.functions import BatchNormFn, TowerFeatureFn
+from recommendsystemproject_amd.functions import (BatchNormFn, TowerChainFn, TowerFeatureFn,
+                                                   tower_chain_supported)
 from recommendsystemproject_amd.project.models.TwoTower.SequenceEncoder import SequenceEncoder
 from recommendsystemproject_amd.project.models.TwoTower.Tower import MLP_Tower
 
@@ -93,6 +94,11 @@ class GenericTower(nn.Module):
                 seq_vec = self.seq_encoder(seqd)
         x = TowerFeatureFn.apply(need, self, input_dict, feature_column_mapping, seq_vec,
                                  *self.embeddings.parameters())
+        if tower_chain_supported(self.feature_bn, self.mlp, x, int(groups)):
+            # feature_bn + MLP_Tower as one fused kernel chain (training mode)
+            ensure_flat(self.mlp)
+            return TowerChainFn.apply(need, self.feature_bn, self.mlp, x, int(groups),
+                                      *self.feature_bn.parameters(), *self.mlp.parameters())
         x = BatchNormFn.apply(need, self.feature_bn, x, int(groups), self.feature_bn.weight,
                               self.feature_bn.bias)
         return self.mlp(x, groups=int(groups))
