@@ -289,6 +289,18 @@ int rs_tower_fwd(const float* A, int G, int Bg, int K, const float* in_mean, con
                  float* part, int* sync, double* scratch, float* mean, float* rstd,
                  float* running_mean, float* running_var, int64_t* num_batches, float momentum,
                  float eps, float* out, float* norm, float l2_eps, int bf16, void* stream);
+/* Weight gradients of up to 4 tower Linears in one launch (bf16 compute mode; Tower.py:16 nn.Linear
+ * backward): per layer i, dW_i [N_i][K_i] += dz_i^T h_i over M rows, db_i [N_i] += colsum(dz_i)
+ * (db_i may be NULL). ws_i: rs_tower_wgrad_ws_floats(M, N_i, K_i) floats of scratch; sync_i:
+ * rs_tower_wgrad_sync_ints(N_i, K_i) ints, zero on entry and again on exit. The row splits of a
+ * tile are summed in a fixed order (deterministic). Host arrays (Ns, Ks, pointer arrays) are read
+ * during the call only. */
+int rs_tower_wgrad_split(int M, int N, int K);
+int64_t rs_tower_wgrad_ws_floats(int M, int N, int K);
+int rs_tower_wgrad_sync_ints(int N, int K);
+int rs_tower_wgrad(int nlayers, int M, const int* Ns, const int* Ks, const float* const* dz,
+                   const float* const* h, float* const* dW, float* const* db, float* const* ws,
+                   int* const* sync, void* stream);
 int rs_tower_bwd(const float* gin, int G, int Bg, int K, const float* y, const float* norm,
                  float l2_eps, const float* z, const float* mean, const float* rstd,
                  const float* bn_w, const float* mg, const float* mgx, float* dz, const float* W,

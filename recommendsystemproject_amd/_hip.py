@@ -69,6 +69,10 @@ SIGNATURES = {
                                f32, vp, i32, vp, vp]),
     'rs_tower_part_floats': (i64, [i32, i32, i32, i32]),
     'rs_tower_debug_buffer': (i32, [vp]),
+    'rs_tower_wgrad_split': (i32, [i32, i32, i32]),
+    'rs_tower_wgrad_ws_floats': (i64, [i32, i32, i32]),
+    'rs_tower_wgrad_sync_ints': (i32, [i32, i32]),
+    'rs_tower_wgrad': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     'rs_tower_sync_ints': (i32, [i32, i32]),
     'rs_tower_stats': (i32, [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, f32, vp]),
     'rs_tower_fwd': (i32, [vp, i32, i32, i32, vp, vp, vp, vp, i32, f32, vp, i32, vp, vp, vp, i32, vp, vp,

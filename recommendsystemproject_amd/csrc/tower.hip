@@ -611,11 +611,13 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
 
     TW_MARK(1);
     // D chunks in flight per thread: a chunk's loads are issued D iterations before it is staged
-    for (int kc0 = 0; kc0 < nk; kc0 += D) {
+    // the chunk count is padded to a multiple of D (padding chunks stage zeros): no exit inside
+    // the unrolled body, so the waitcnt pass sees straight-line code with D chunks in flight
+    const int nkp = (nk + D - 1) / D * D;
+    for (int kc0 = 0; kc0 < nkp; kc0 += D) {
 #pragma unroll
       for (int st = 0; st < D; ++st) {
         const int kc = kc0 + st;
-        if (kc >= nk) break;
         const int buf = kc & 1;
         store(kc, buf, ra[st], ra2[st], rw[st]);
         lds_barrier();
@@ -871,6 +873,167 @@ int bwd_dispatch(const TwArgs& a, hipStream_t st) {
   return launch<T, 64, PRO, EPI_BWD>(a, cdiv(a.N, 64), st, "rs_tower_bwd");
 }
 
+
+// ------------------------------------------------------------------------ weight gradients
+// dW[N][K] += dz^T h and db[N] += colsum(dz) of every Linear of a tower in ONE launch (a grouped
+// GEMM over the layers' tiles), bf16 mode: 64 x 64 dW tiles, the M rows split S ways per tile;
+// each workgroup streams 32-row chunks of dz and h (fp32, rounded to bf16 while staged
+// row-major in LDS) and reads the MFMA operands with ds_read_b64_tr_b16 (8 consecutive rows of a
+// column per lane) into v_mfma_f32_32x32x16_bf16. The S partial tiles meet in a fixed order: the
+// workgroup arriving last for a tile (write-through partials, one ticket per workgroup) sums them
+// s = 0..S-1 and adds the sum into dW (and db: fp32 column sums of the unrounded dz).
+typedef short wshortx4 __attribute__((ext_vector_type(4)));
+typedef short wshortx8 __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+constexpr int WG_MAXJ = 4;
+constexpr int WCH = 32;         // rows per chunk
+constexpr int WPITCH = 96;      // bf16 LDS pitch of a 64-wide image (4 rows of a transposed read in distinct 64-B windows)
+
+struct WgJob {
+  const float* dz;  // [M][N]
+  const float* h;   // [M][K]
+  float* dW;        // [N][K] (+=)
+  float* db;        // [N] (+=)
+  float* part;      // [tiles][S][16][256] dW partials, then [tiles_n][S][64] db partials
+  int* cnt;         // [tiles] tickets (zero on entry and exit)
+  int N, K, tn, tk, S, R, wg0;
+};
+struct WgArgs {
+  WgJob j[WG_MAXJ];
+  int nj, M;
+};
+
+__device__ __forceinline__ bf16x8t wtr_frag(const __bf16* lo, const __bf16* hi) {
+  typedef __attribute__((address_space(3))) wshortx4* lptr;
+  const wshortx4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lptr)(lo));
+  const wshortx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lptr)(hi));
+  const wshortx8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8t, v);
+}
+
+__global__ __launch_bounds__(256) void tower_wgrad_kernel(WgArgs a) {
+  constexpr int D = 3;  // chunks of loads in flight per thread
+  __shared__ __attribute__((aligned(16))) __bf16 Ys[2][WCH][WPITCH];
+  __shared__ __attribute__((aligned(16))) __bf16 Xs[2][WCH][WPITCH];
+  __shared__ float csum[16][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int ji = 0;
+  for (int q = 1; q < a.nj; ++q)
+    if ((int)blockIdx.x >= a.j[q].wg0) ji = q;
+  const WgJob& J = a.j[ji];
+  const int local = blockIdx.x - J.wg0;
+  const int tile = local / J.S, s = local % J.S;
+  const int tn = tile / J.tk, tk = tile % J.tk;
+  const int n0 = tn * 64, k0 = tk * 64;
+  const int r0 = s * J.R, r1 = min(a.M, r0 + J.R);
+  const int N = J.N, K = J.K;
+  const bool do_db = tk == 0 && J.db;
+  // loads: dz rows [32][64] and h rows [32][64], 2 float4 each per thread
+  const int lr = tid >> 4, lc = (tid & 15) * 4;  // rows lr, lr + 16; columns lc..lc+3
+  f4 ry[D][2], rx[D][2];
+  const int nch = (r1 - r0 + WCH - 1) / WCH;
+  auto load = [&](int ch, f4 (&ry)[2], f4 (&rx)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int m = min(r0 + ch * WCH + lr + 16 * u, r1 - 1);
+      ry[u] = *reinterpret_cast<const f4*>(J.dz + (size_t)m * N + min(n0 + lc, N - 4));
+      rx[u] = *reinterpret_cast<const f4*>(J.h + (size_t)m * K + min(k0 + lc, K - 4));
+    }
+  };
+  float ysum[4] = {0.f, 0.f, 0.f, 0.f};
+  auto stage = [&](int ch, int buf, f4 (&ry)[2], f4 (&rx)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = lr + 16 * u;
+      const bool rok = r0 + ch * WCH + row < r1;
+      const f4 y = rok && n0 + lc < N ? ry[u] : f4{0.f, 0.f, 0.f, 0.f};
+      const f4 x = rok && k0 + lc < K ? rx[u] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ysum[e] += y[e];
+      lds_put4<__bf16>(&Ys[buf][row][lc], y);
+      lds_put4<__bf16>(&Xs[buf][row][lc], x);
+    }
+  };
+  f16v acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  const int wm = wave >> 1, wn = wave & 1;  // 32 x 32 sub-tile of the wave: n rows wm, k cols wn
+  const int gq = lane >> 4, lq = (lane & 15) >> 2, lp = lane & 3;
+  const int trow = 8 * (gq >> 1) + lq, tcol = 16 * (gq & 1) + 4 * lp;
+#pragma unroll
+  for (int st = 0; st < D; ++st) load(min(st, nch - 1), ry[st], rx[st]);
+  const int nchp = (nch + D - 1) / D * D;  // padded: padding chunks stage zeros
+  for (int c0 = 0; c0 < nchp; c0 += D) {
+#pragma unroll
+    for (int st = 0; st < D; ++st) {
+      const int ch = c0 + st;
+      const int buf = ch & 1;
+      stage(ch, buf, ry[st], rx[st]);
+      lds_barrier();
+      load(min(ch + D, nch - 1), ry[st], rx[st]);
+#pragma unroll
+      for (int ks = 0; ks < WCH / 16; ++ks) {
+        const __bf16* py = &Ys[buf][16 * ks + trow][32 * wm + tcol];
+        const __bf16* px = &Xs[buf][16 * ks + trow][32 * wn + tcol];
+        const bf16x8t af = wtr_frag(py, py + 4 * WPITCH);
+        const bf16x8t bf = wtr_frag(px, px + 4 * WPITCH);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
+      }
+    }
+  }
+  // column sums of dz (db), per thread over its rows, then the 16 row lanes in order
+  float dbv = 0.f;
+  if (do_db) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) csum[lr][lc + e] = ysum[e];
+    lds_barrier();
+    if (tid < 64)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dbv += csum[r][tid];
+  }
+  // partial -> write-through, ticket; the last arriver of the tile sums the S partials in order
+  float* pt = J.part + ((size_t)tile * J.S) * 4096;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) st_sc1(pt + (size_t)s * 4096 + e * 256 + tid, acc[e]);
+  float* pdb = J.part + (size_t)J.tn * J.tk * J.S * 4096 + ((size_t)tn * J.S) * 64;
+  if (do_db && tid < 64) st_sc1(pdb + s * 64 + tid, dbv);
+  if (!ticket(J.cnt + tile, J.S - 1)) return;
+  f16v sum;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) sum[e] = 0.f;
+  for (int q = 0; q < J.S; ++q) {
+    f16v v;
+    if (q == s) {
+      v = acc;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = ld_sc1(pt + (size_t)q * 4096 + e * 256 + tid);
+    }
+    sum += v;
+  }
+  // dW += sum: every old value loaded before any is stored (a load after a store to the same
+  // array would wait for the store: 16 serial round trips)
+  const int kk = k0 + 32 * wn + (lane & 31);
+  float* __restrict__ dWp = J.dW;
+  float old[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int nn = min(n0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5), N - 1);
+    old[e] = dWp[(size_t)nn * K + min(kk, K - 1)];
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int nn = n0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+    if (nn < N && kk < K) dWp[(size_t)nn * K + kk] = old[e] + sum[e];
+  }
+  if (do_db && tid < 64 && n0 + tid < N) {
+    float t = 0.f;
+    for (int q = 0; q < J.S; ++q) t += q == s ? dbv : ld_sc1(pdb + q * 64 + tid);
+    J.db[n0 + tid] += t;
+  }
+  if (tid == 0) __hip_atomic_store(J.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 bool al16(const void* p) { return !p || aligned16(p); }
 
 }  // namespace
@@ -986,4 +1149,49 @@ extern "C" int rs_tower_bwd(const float* gin, int G, int Bg, int K, const float*
   }
   if (l2) return bf16 ? bwd_dispatch<__bf16, PRO_L2B>(a, st) : bwd_dispatch<float, PRO_L2B>(a, st);
   return bf16 ? bwd_dispatch<__bf16, PRO_BNB>(a, st) : bwd_dispatch<float, PRO_BNB>(a, st);
+}
+
+// Weight gradients of up to 4 Linears in one launch (tower_wgrad_kernel). Per layer i: dz_i
+// [M][N_i], h_i [M][K_i], dW_i [N_i][K_i] += dz^T h, db_i [N_i] += colsum(dz) (may be NULL);
+// ws_i: rs_tower_wgrad_ws_floats(M, N_i, K_i) floats; sync_i: rs_tower_wgrad_sync_ints(N_i, K_i)
+// ints, zero on entry (zero again on exit). bf16 MFMA (bf16 compute mode only).
+extern "C" int rs_tower_wgrad_split(int M, int N, int K) {
+  const int tiles = cdiv(N, 64) * cdiv(K, 64);
+  int S = (256 + tiles - 1) / tiles;
+  const int smax = cdiv(M, 256);  // >= 256 rows per split
+  if (S > smax) S = smax;
+  if (S < 1) S = 1;
+  return S;
+}
+extern "C" int64_t rs_tower_wgrad_ws_floats(int M, int N, int K) {
+  const int S = rs_tower_wgrad_split(M, N, K);
+  return (int64_t)cdiv(N, 64) * cdiv(K, 64) * S * 4096 + (int64_t)cdiv(N, 64) * S * 64;
+}
+extern "C" int rs_tower_wgrad_sync_ints(int N, int K) { return cdiv(N, 64) * cdiv(K, 64); }
+
+extern "C" int rs_tower_wgrad(int nlayers, int M, const int* Ns, const int* Ks,
+                              const float* const* dz, const float* const* h, float* const* dW,
+                              float* const* db, float* const* ws, int* const* sync, void* stream) {
+  RS_CHECK_ARG(nlayers >= 1 && nlayers <= WG_MAXJ && M >= 1, "rs_tower_wgrad: bad nlayers %d / M %d", nlayers, M);
+  WgArgs a{};
+  a.nj = nlayers;
+  a.M = M;
+  int wg = 0;
+  for (int i = 0; i < nlayers; ++i) {
+    const int N = Ns[i], K = Ks[i];
+    RS_CHECK_ARG(N >= 4 && K >= 4 && N % 4 == 0 && K % 4 == 0, "rs_tower_wgrad: bad shape N=%d K=%d", N, K);
+    RS_CHECK_ARG(dz[i] && h[i] && dW[i] && ws[i] && sync[i], "rs_tower_wgrad: null pointer (layer %d)", i);
+    RS_CHECK_ARG(al16(dz[i]) && al16(h[i]), "rs_tower_wgrad: operands must be 16-byte aligned");
+    WgJob& j = a.j[i];
+    j.dz = dz[i]; j.h = h[i]; j.dW = dW[i]; j.db = db[i]; j.part = ws[i]; j.cnt = sync[i];
+    j.N = N; j.K = K; j.tn = cdiv(N, 64); j.tk = cdiv(K, 64);
+    j.S = rs_tower_wgrad_split(M, N, K);
+    j.R = cdiv(cdiv(M, j.S), WCH) * WCH;
+    j.S = cdiv(M, j.R);  // splits that hold rows
+    j.wg0 = wg;
+    wg += j.tn * j.tk * j.S;
+  }
+  tower_wgrad_kernel<<<wg, 256, 0, as_stream(stream)>>>(a);
+  RS_CHECK_LAUNCH("rs_tower_wgrad");
+  return 0;
 }

@@ -679,6 +679,32 @@ def _tower_sync(mlp, dev, n):
     return t
 
 
+def _tower_wgrad_grouped(mlp, jobs, M):
+    """dW += dz^T h, db += colsum(dz) of every Linear of the tower in one launch (rs_tower_wgrad,
+    bf16 compute mode): 64 x 64 dW tiles x row splits, fixed-order reduction of the splits."""
+    import ctypes as C
+    L = _hip.lib()
+    dev = jobs[0][0].device
+    n = len(jobs)
+    Ns = [int(lin.out_features) for _, _, lin in jobs]
+    Ks = [int(lin.in_features) for _, _, lin in jobs]
+    wsz = [int(L.rs_tower_wgrad_ws_floats(M, a, b)) for a, b in zip(Ns, Ks)]
+    ssz = [int(L.rs_tower_wgrad_sync_ints(a, b)) for a, b in zip(Ns, Ks)]
+    ws = torch.empty(sum(wsz), device=dev, dtype=torch.float32)
+    t = getattr(mlp, '_rs_tower_wsync', None)
+    if t is None or t.device != dev or t.numel() < sum(ssz):
+        t = mlp._rs_tower_wsync = torch.zeros(max(sum(ssz), 64), dtype=torch.int32, device=dev)
+    woff = [sum(wsz[:i]) for i in range(n)]
+    soff = [sum(ssz[:i]) for i in range(n)]
+    P = C.c_void_p * n
+    arrs = [(C.c_int * n)(*Ns), (C.c_int * n)(*Ks),
+            P(*[d.data_ptr() for d, _, _ in jobs]), P(*[h.data_ptr() for _, h, _ in jobs]),
+            P(*[grad_of(lin.weight).data_ptr() for _, _, lin in jobs]),
+            P(*[grad_of(lin.bias).data_ptr() if lin.bias is not None else None for _, _, lin in jobs]),
+            P(*[ws[o:].data_ptr() for o in woff]), P(*[t[o:].data_ptr() for o in soff])]
+    ops.call('rs_tower_wgrad', n, M, *[C.addressof(a) for a in arrs], ops.stream())
+
+
 class TowerChainFn(torch.autograd.Function):
     """GenericTower.feature_bn + MLP_Tower in training mode (GenericTower.py:229-236; Tower.py:16-41)
     as one kernel per Linear (csrc/tower.hip): a BatchNorm's statistics are merged by the last
@@ -766,6 +792,7 @@ class TowerChainFn(torch.autograd.Function):
         f32 = torch.float32
         off = ctx.sync_off
         gin, mg, mgx = dout, None, None
+        wjobs = []  # bf16 mode: every layer's weight gradient in one grouped launch at the end
         for j in range(n_hidden, -1, -1):
             lin = seq[4 * j]
             A, h, mean, rstd, bn_in, relu, dp, site = layers[j]
@@ -789,7 +816,10 @@ class TowerChainFn(torch.autograd.Function):
                      omgx.data_ptr(), grad_of(bn_in.weight).data_ptr(), grad_of(bn_in.bias).data_ptr(), bf,
                      ops.stream())
             off += L.rs_tower_sync_ints(G, N)
-            _tower_wgrad(dz, h, lin)
+            if bf:
+                wjobs.append((dz, h, lin))
+            else:
+                _tower_wgrad(dz, h, lin)
             gin, mg, mgx = g, omg, omgx
         # feature_bn's dx: the BatchNorm backward prologue with no GEMM
         x, _, m0, r0, fbn = layers[0][:5]
@@ -799,6 +829,8 @@ class TowerChainFn(torch.autograd.Function):
                  r0.data_ptr(), fbn.weight.data_ptr(), mg.data_ptr(), mgx.data_ptr(), dx.data_ptr(), None, 0,
                  None, None, None, None, None, 0, 0.0, None, 0, None, None, None, None, None, None, None, None,
                  bf, ops.stream())
+        if wjobs:
+            _tower_wgrad_grouped(ctx.mlp, wjobs, M)
         ctx.layers = None
         return (None, None, None, dx, None) + (None,) * (len(ctx.needs_input_grad) - 5)
 
