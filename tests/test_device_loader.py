@@ -160,3 +160,79 @@ def test_device_loader_empty_lists_and_save_load(tmp_path):
     L = max(len(v) for v in df['hist_movie_ids'][:50])
     assert first['user_tower']['sequence']['hist_genre_ids'].shape == (50, L, 3)
     a.check_errors()
+
+
+# ------------------------------------------------------------------ pinned by the reference itself
+# tests/golden/loader_demo.npz: one epoch of the reference's CombinedTwoTowerDataLoader
+# (CombineTwoTower.py:13-105, shuffle under torch.manual_seed(7)), made by make_loader_golden.py
+def _golden():
+    import json
+    d = np.load(os.path.join(ROOT, 'tests', 'golden', 'loader_demo.npz'))
+    meta = json.loads(bytes(d['meta']).decode())
+    cols = {}
+    for c in meta['columns']:
+        if f'df/{c}' in d:
+            cols[c] = d[f'df/{c}']
+        else:
+            vals, offs = d[f'df/{c}/vals'], d[f'df/{c}/offs']
+            cols[c] = [vals[offs[i]:offs[i + 1]].tolist() for i in range(len(offs) - 1)]
+    return pd.DataFrame(cols), d, meta
+
+
+def _golden_batch(d, k):
+    out = {}
+    for tower in ('user_tower', 'item_tower'):
+        b = {}
+        for key in ('sparse', 'dense'):
+            if f'b{k}/{tower}/{key}' in d:
+                b[key] = torch.from_numpy(d[f'b{k}/{tower}/{key}'])
+        pre = f'b{k}/{tower}/seq:'
+        b['sequence'] = {name[len(pre):]: torch.from_numpy(d[name]) for name in d.files if name.startswith(pre)}
+        out[tower] = b
+    return out
+
+
+def _assert_batch_equal(o, r):
+    for tower in r:
+        for key in ('sparse', 'dense'):
+            if key in r[tower]:
+                assert o[tower][key].dtype == r[tower][key].dtype
+                assert torch.equal(o[tower][key].cpu(), r[tower][key]), (tower, key)
+        assert set(o[tower]['sequence']) == set(r[tower]['sequence'])
+        for f in r[tower]['sequence']:
+            assert o[tower]['sequence'][f].shape == r[tower]['sequence'][f].shape, f
+            assert torch.equal(o[tower]['sequence'][f].cpu(), r[tower]['sequence'][f]), f
+
+
+def test_restated_collate_matches_reference_fixture():
+    """The host restatement used by the GPU tests (ref_tower_samples + ref_collate in
+    reference_shuffle_order) reproduces the reference loader's own epoch bit for bit."""
+    df, d, meta = _golden()
+    B, n = meta['B'], meta['N']
+    ug = ref_tower_samples(df, CFG['two_tower']['user_tower'])
+    ig = ref_tower_samples(df, CFG['two_tower']['item_tower'])
+    torch.manual_seed(meta['seed'])
+    order = reference_shuffle_order(n)
+    for k in range(meta['batches']):
+        idx = order[k * B:(k + 1) * B]
+        got = {'user_tower': ref_collate([ug(i) for i in idx]), 'item_tower': ref_collate([ig(i) for i in idx])}
+        _assert_batch_equal(got, _golden_batch(d, k))
+
+
+@pytest.mark.gpu
+def test_device_loader_matches_reference_fixture():
+    """DeviceCombinedLoader (device collate) against the reference loader's epoch: same shuffle
+    order under the same seed, every tensor bit-exact, same feature column mappings."""
+    df, d, meta = _golden()
+    torch.manual_seed(meta['seed'])
+    loader = DeviceCombinedLoader(CFG, df, batch_size=meta['B'], shuffle=True, device=torch.device('cuda:0'))
+    assert len(loader) == meta['batches']
+    mapping = loader.get_feature_mappings() if hasattr(loader, 'get_feature_mappings') else None
+    if mapping is not None:
+        assert mapping == meta['mapping']
+    nb = 0
+    for k, batch in enumerate(loader):
+        _assert_batch_equal(batch, _golden_batch(d, k))
+        nb += 1
+    assert nb == meta['batches']
+    loader.check_errors()
