@@ -1,0 +1,73 @@
+"""Host-code AddressSanitizer harness (run by test_cpu_host.py in a subprocess with the ASan
+runtime preloaded and RSYS_LIB_PATH = librsys_hip_asan.so, the --offload-host-only ASan build of
+the same sources). It drives the host side of the entry points -- argument validation, launch
+planning over host segment tables, workspace sizing, the grouped weight-gradient job tables --
+with valid and invalid arguments. No GPU: a launch that the planning reaches fails cleanly (no
+device code, no device), which is part of what is exercised. Any heap / stack / global overflow
+or use-after-free in that host code aborts the process with an ASan report."""
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from recommendsystemproject_amd import _hip  # noqa: E402
+from recommendsystemproject_amd.functions import _seg  # noqa: E402
+
+
+def expect_fail(name, *args):
+    rc = getattr(L, name)(*args)
+    assert rc != 0, name
+    assert L.rs_last_error(), name
+
+
+L = _hip.lib()
+assert 'asan' in _hip.LIB_PATH, _hip.LIB_PATH
+assert L.rs_version() >= 1
+# size queries over a range of shapes
+for n in (0, 1, 4095, 4096, 204800, 10 ** 7):
+    assert L.rs_lookup_sort_ws_bytes(n, 10 ** 7) >= 0
+    assert L.rs_segsum_ws_bytes(n, 128) >= 0
+for B in (1, 64, 4096):
+    assert L.rs_inbatch_ce_fused_ws_bytes(B, 128) > 0
+    assert L.rs_batchnorm_ws_bytes(3, B, 256) > 0
+    assert L.rs_layernorm_ws_bytes(B * 50, 64) > 0
+    for kind in (0, 1):
+        assert L.rs_tower_part_floats(11, B, 300, kind) > 0
+    assert L.rs_tower_wgrad_ws_floats(B, 256, 300) > 0
+    assert 1 <= L.rs_tower_wgrad_split(B, 128, 128) <= max(1, (B + 255) // 256)
+assert L.rs_tower_sync_ints(11, 300) == 12 * 5
+# gather planning over a multi-segment host table (the C2 user tower's kinds), then a launch
+# that cannot happen on this host
+fake = 1 << 20  # never dereferenced on the host
+segs = [_seg(kind=_hip.RS_SEG_SPARSE, dim=64, out_col=0, vocab=6060, idx_stride=5, idx=fake, table=fake, pad_idx=-1),
+        _seg(kind=_hip.RS_SEG_POOL, dim=128, out_col=64, pool_mode=_hip.RS_POOL['mean'], bag=50, vocab=10 ** 7,
+             idx_stride=50, idx=fake, table=fake, pad_idx=0),
+        _seg(kind=_hip.RS_SEG_DENSE, dim=8, out_col=192, vocab=1, idx_stride=1, idx=fake, table=fake,
+             x=fake, bias=fake),
+        _seg(kind=_hip.RS_SEG_POOL, dim=8, out_col=200, pool_mode=_hip.RS_POOL['sum'], bag=3, vocab=30,
+             idx_stride=3, idx=fake, table=fake, pad_idx=0)]
+arr = (_hip.FeatureSeg * len(segs))(*segs)
+assert L.rs_gather_ws_bytes(arr, len(segs), 4096) >= 0
+for rows in (1, 4096):
+    rc = L.rs_gather_fwd(arr, len(segs), rows, fake, 208, None, None)
+    assert rc != 0  # no device: the launch fails after planning
+expect_fail('rs_gather_fwd', arr, 0, 16, fake, 208, None, None)     # nseg out of range
+expect_fail('rs_gather_fwd', arr, 64, 16, fake, 208, None, None)    # nseg past kMaxSeg
+# tower chain and grouped weight gradients: argument checks and job tables
+expect_fail('rs_tower_fwd', None, 1, 64, 300, None, None, None, None, 0, 0.0, None, 0, None, None, None, 256, None,
+            None, None, None, None, None, None, None, None, 0.0, 0.0, None, None, 0.0, 0, None)
+n = 3
+Ns, Ks = (C.c_int * n)(256, 128, 128), (C.c_int * n)(300, 256, 128)
+P = C.c_void_p * n
+ptrs = P(fake, fake, fake)
+rc = L.rs_tower_wgrad(n, 4096, C.addressof(Ns), C.addressof(Ks), C.addressof(ptrs), C.addressof(ptrs),
+                      C.addressof(ptrs), C.addressof(ptrs), C.addressof(ptrs), C.addressof(ptrs), None)
+assert rc != 0
+expect_fail('rs_tower_wgrad', 9, 4096, C.addressof(Ns), C.addressof(Ks), C.addressof(ptrs), C.addressof(ptrs),
+            C.addressof(ptrs), C.addressof(ptrs), C.addressof(ptrs), C.addressof(ptrs), None)
+# assorted entry points with bad shapes
+expect_fail('rs_gemm_f32', 0, 0, -1, 4, 4, 1.0, None, 4, None, 4, 0.0, None, 4, 0, None, None,
+            0, 0, 0.0, None, 0, 0, None, 1, None, None)
+expect_fail('rs_attn_fwd', 1, 1, 1, 1, 2, 5, 60, 4, 1.0, 0.0, None, 0, 0, None)
+expect_fail('rs_tower_stats', None, 1, 1, 1, None, None, None, None, None, None, None, None, 0.1, 1e-5, None)
+print('asan harness ok')

@@ -122,3 +122,25 @@ def test_history_csr_filters_like_reference():
     off, idx = off.numpy(), idx.numpy()
     rows = [sorted(idx[off[u]:off[u + 1]].tolist()) for u in range(U)]
     assert rows == [[0, 2], [], [1, 3], []]
+
+
+def test_host_code_under_asan():
+    """The host side of the C-ABI (argument checks, launch planning, workspace sizing, job tables)
+    under AddressSanitizer: tests/asan_harness.py in a subprocess against librsys_hip_asan.so
+    (csrc/Makefile target `asan`, host-only ASan build), with the clang ASan runtime preloaded."""
+    import glob
+    import subprocess
+    import sys
+    lib = os.path.join(ROOT, 'recommendsystemproject_amd', '_lib', 'librsys_hip_asan.so')
+    if not os.path.exists(lib):
+        subprocess.run(['make', '-C', os.path.join(ROOT, 'recommendsystemproject_amd', 'csrc'), 'asan', '-j8'],
+                       check=True, capture_output=True)
+    rt = sorted(glob.glob('/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so'))
+    if not rt:
+        pytest.skip('clang ASan runtime not found')
+    env = dict(os.environ, RSYS_LIB_PATH=lib, LD_PRELOAD=rt[-1], HIP_VISIBLE_DEVICES='',
+               ASAN_OPTIONS='detect_leaks=0:abort_on_error=1:verify_asan_link_order=0')
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'tests', 'asan_harness.py')], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and 'asan harness ok' in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    assert 'ERROR: AddressSanitizer' not in r.stderr
