@@ -45,6 +45,10 @@ def main():
     ap.add_argument('--bag', type=int, default=50)
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--zipf', type=float, default=None)
+    ap.add_argument('--batches', type=int, default=1,
+                    help='distinct id sets rotated through the timed loop (8: working set > the 256 MB '
+                         'Infinity Cache, as in the training step)')
+    ap.add_argument('--fwd-only', action='store_true')
     args = ap.parse_args()
     dev = torch.device('cuda:0')
     V, D, B, L = args.vocab, args.dim, args.rows, args.bag
@@ -53,26 +57,38 @@ def main():
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     copy_gbs = 6290.0  # MI355X_MICROARCH.md: measured float4 copy bandwidth
     for kind, bag in (('pooled_mean', L), ('single_id', 1)):
-        ids = torch.randint(1, V, (B, bag), device=dev, generator=g)
+        ids_all = [torch.randint(1, V, (B, bag), device=dev, generator=g) for _ in range(args.batches)]
+        ids = ids_all[0]
         if args.zipf:
             import numpy as np
             z = np.random.default_rng(0).zipf(args.zipf, size=(B, bag)).astype(np.uint64) - np.uint64(1)
             z = ((z * np.uint64(2654435761)) % np.uint64(V - 1)).astype(np.int64) + 1
             ids = torch.from_numpy(z).to(dev)
+            ids_all = [ids]
         out = torch.empty(B, D, device=dev)
-        if bag > 1:
-            seg = _seg(kind=_hip.RS_SEG_POOL, dim=D, out_col=0, pool_mode=_hip.RS_POOL['mean'], bag=bag,
-                       vocab=V, idx_stride=bag, idx=ids.data_ptr(), table=table.data_ptr(), pad_idx=0)
-        else:
-            seg = _seg(kind=_hip.RS_SEG_SPARSE, dim=D, out_col=0, vocab=V, idx_stride=1, idx=ids.data_ptr(),
-                       table=table.data_ptr(), pad_idx=0)
-        ms = timed(lambda: ops.gather_fwd([seg], B, out, err), args.iters)
+        segs = []
+        for idt in ids_all:
+            if bag > 1:
+                segs.append(_seg(kind=_hip.RS_SEG_POOL, dim=D, out_col=0, pool_mode=_hip.RS_POOL['mean'], bag=bag,
+                                 vocab=V, idx_stride=bag, idx=idt.data_ptr(), table=table.data_ptr(), pad_idx=0))
+            else:
+                segs.append(_seg(kind=_hip.RS_SEG_SPARSE, dim=D, out_col=0, vocab=V, idx_stride=1,
+                                 idx=idt.data_ptr(), table=table.data_ptr(), pad_idx=0))
+        it = [0]
+
+        def fwd():
+            ops.gather_fwd([segs[it[0] % len(segs)]], B, out, err)
+            it[0] += 1
+        ms = timed(fwd, args.iters)
         lookups = B * bag
         byts = lookups * D * 4 + B * D * 4 + lookups * 8
         print(json.dumps({'case': f'gather_fwd {kind}', 'vocab': V, 'dim': D, 'rows': B, 'bag': bag,
+                          'batches': len(segs),
                           'MB_per_launch': round(byts / 1e6, 1), 'us': round(ms * 1e3, 1),
                           'GBps': round(byts / ms / 1e6, 1), 'frac_of_8TBps': round(byts / ms / 1e6 / PEAK, 3),
                           'frac_of_copy': round(byts / ms / 1e6 / copy_gbs, 3)}))
+        if args.fwd_only:
+            continue
         # backward: the table gradient of a large (lazy-Adam) table -- the lookups sorted by row
         # (rs_lookup_sort, forward side) and segment-summed (rs_segsum), csrc/lookup.hip
         grad = torch.zeros(V, D, device=dev)
