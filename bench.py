@@ -92,7 +92,7 @@ def run_key(args, B, name=None, dtype=None, zipf=None, hard_negatives=None):
             'zipf': zipf}
 
 
-def load_traffic(args, B, entry, name, dtype, zipf, hard_negatives):
+def load_traffic(args, B, entry, name, dtype, zipf, hard_negatives, suffix=''):
     """roofline.traffic: HBM bytes per launch of `entry` from a committed rocprofv3 --pmc summary
     (FETCH_SIZE and WRITE_SIZE in separate passes, gfx950 read correction; tools/pmc_traffic.py),
     used only when it was collected on this same workload and entry point."""
@@ -100,7 +100,7 @@ def load_traffic(args, B, entry, name, dtype, zipf, hard_negatives):
     if path == 'none':
         return None
     if path == 'auto':
-        path = os.path.join(ROOT, 'profiles', f'traffic_{name}_{dtype}.json')
+        path = os.path.join(ROOT, 'profiles', f'traffic_{name}_{dtype}{suffix}.json')
     if not os.path.exists(path):
         return None
     tr = json.load(open(path))
@@ -450,6 +450,11 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
                               'frac_of_measured_copy': round(gbs / HBM_MEASURED_GBS, 4),
                               'bytes_per_step': round(g['bytes'] / 3),
                               'ms_per_step': round(g['ms'] / 3, 4), 'entries': list(members)}
+            if k == 'rs_gather_fwd':  # PMC traffic of the gather (profiles/traffic_<cfg>_<dt>_gather.json)
+                tr = load_traffic(args, B, 'rs_gather_fwd', name, dtype, zipf, hard_negatives, suffix='_gather')
+                gather_roof[k]['traffic'] = tr['hbm_bytes_per_launch'] if tr else None
+                if tr:
+                    gather_roof[k]['traffic_detail'] = tr
 
     # the batch similarity (U I^T inside the fused in-batch CE) against the bf16 MFMA peak
     # (north_star: MFMA utilisation on the batch-dot)

@@ -72,6 +72,34 @@ def _bn_work(a, bwd=False):
     return 6.0 * n, 4.0 * n * (4 if bwd else 3)
 
 
+def _tower_fwd_work(a):
+    """rs_tower_fwd: A read (BN applied on the fly), W read, z / out written, h written when asked."""
+    M, K, N = a[1] * a[2], a[3], a[15]
+    byts = 4.0 * (M * K + N * K + M * N) + (4.0 * M * K if a[12] else 0.0) + (4.0 * M if a[28] else 0.0)
+    return 2.0 * M * N * K, byts
+
+
+def _tower_bwd_work(a):
+    """rs_tower_bwd: the incoming gradient and the prologue's second operand (z or y) read, dz
+    written; N > 0: W read, the lower BatchNorm's z read and g written."""
+    M, K, N = a[1] * a[2], a[3], a[15]
+    byts = 4.0 * M * K * 3 + (4.0 * (K * N + 2 * M * N) if N else 0.0)
+    return 2.0 * M * N * K, byts
+
+
+def _tower_wgrad_work(a):
+    import ctypes as C
+    n, M = a[0], a[1]
+    Ns = C.cast(a[2], C.POINTER(C.c_int))
+    Ks = C.cast(a[3], C.POINTER(C.c_int))
+    fl = by = 0.0
+    for i in range(n):
+        N, K = Ns[i], Ks[i]
+        fl += 2.0 * M * N * K
+        by += 4.0 * M * (N + K) + 8.0 * N * K
+    return fl, by
+
+
 def _adam_work(a):
     n = a[4]
     return 12.0 * n, 28.0 * n
@@ -140,6 +168,10 @@ WORK = {
     'rs_batchnorm_fwd': _bn_work,
     'rs_batchnorm_bwd': lambda a: _bn_work(a, True),
     'rs_adam_step': _adam_work,
+    'rs_tower_stats': lambda a: (3.0 * a[1] * a[2] * a[3], 4.0 * a[1] * a[2] * a[3]),
+    'rs_tower_fwd': _tower_fwd_work,
+    'rs_tower_bwd': _tower_bwd_work,
+    'rs_tower_wgrad': _tower_wgrad_work,
     # large tables (csrc/lookup.hip): the sort reads the ids and writes keys + vals; the table
     # gradient is priced by SURVEY §8d's gather formula (lookups x D x 4 + dout rows x D x 4 +
     # ids) like the scatter it replaces; the per-row catch-up / Adam / sqnorm work depends on the

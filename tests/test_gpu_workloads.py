@@ -18,8 +18,8 @@ u = 2^-8 (bf16 keeps 8 significant bits, round to nearest), so each product a*b 
 2u relative and a dot product by at most 2u * sum|a_i b_i|. The embeddings U, I are L2-normalised,
 so the final logit U.I / T is off by at most 2u / T from its own product, plus what U and I
 inherit from the towers' rounded GEMMs. For unit vectors the elementwise error of U / I is held
-to TOL_EMB = 4u (the tower GEMMs are fp32; the encoder's rounded GEMMs feed the user tower through
-one BatchNorm-normalised MLP). A logit then moves by at most (2 * TOL_EMB * sqrt(D) * max|e| ...)
+to TOL_EMB = 4u (the encoder's and the towers' rounded GEMMs -- the fused tower chain rounds its
+operands too -- reach U and I through BatchNorm-normalised MLPs). A logit then moves by at most (2 * TOL_EMB * sqrt(D) * max|e| ...)
 -- in practice we bound it by TOL_LOGIT = (2 * 4u + 2u) / T, and the loss (a mean of per-row
 log-sum-exp minus the positive logit, each 1-Lipschitz in the max-norm of its row's logits) by
 2 * TOL_LOGIT. Those are worst-case bounds; the BIAS test is the sharp one: rounding noise is

@@ -13,7 +13,7 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   ( cd /tmp && timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d $ROOT/gpurun_out/prof/pmc_$ctr -o run --output-format csv -- python3 $ROOT/bench.py --warmup 2 --pmc-bracket ${BRACKET:-auto} ${BENCH_ARGS} ) > gpurun_out/prof/pmc_$ctr.log 2>&1
   rc=$?; echo "pmc $ctr rc=$rc"; tail -2 gpurun_out/prof/pmc_$ctr.log; [ $rc -eq 0 ] || exit $rc
 done
-python3 tools/pmc_traffic.py gpurun_out/prof gpurun_out/prof/pmc_FETCH_SIZE.log > gpurun_out/prof/traffic.json
+python3 tools/pmc_traffic.py gpurun_out/prof gpurun_out/prof/pmc_FETCH_SIZE.log > gpurun_out/prof/traffic.json 2> gpurun_out/prof/traffic.err
 echo "traffic rc=$?"; cat gpurun_out/prof/traffic.json | head -12
 fi
 python3 tools/prof_summary.py gpurun_out/prof > gpurun_out/prof/summary.txt; echo "summary rc=$?"
