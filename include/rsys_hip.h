@@ -445,7 +445,9 @@ int rs_sparse_flush(float* p, float* m, float* v, int* last, int64_t V, int D, c
  * sort; n <= 4096 in one launch without workspace, else rs_lookup_sort_ws_bytes of workspace).
  * Every per-row operation then walks the distinct rows (run heads) of keys:
  *   rs_sorted_catchup  replay skipped zero-gradient Adam steps before the gather reads the rows
- *                      (bitwise equal to dense Adam);
+ *                      (bitwise equal to dense Adam); rs_lookup_catchup does the same straight
+ *                      from the unsorted id matrix (one compare-and-swap on last[row] picks the
+ *                      lookup that replays the row), so the sort can leave the forward path;
  *   rs_segsum          the table gradient = embedding_dense_backward of the call
  *                      (GenericTower.py:182; pooled mean/sum GenericTower.py:141-162): per row
  *                      the contributions of its lookups in lookup order (mode 0: dout row r per
@@ -467,6 +469,10 @@ int rs_lookup_sort(const void* ids, int id_bytes, int rows, int bag, int64_t row
 int rs_sorted_catchup(const uint32_t* keys, int64_t n, int D, float* p, float* m, float* v,
                       int* last, const int64_t* step, const float* consts, float beta1, float beta2,
                       float eps, float weight_decay, void* stream);
+int rs_lookup_catchup(const void* ids, int id_bytes, int rows, int bag, int64_t row_stride,
+                      int64_t vocab, int D, float* p, float* m, float* v, int* last,
+                      const int64_t* step, const float* consts, float beta1, float beta2, float eps,
+                      float weight_decay, void* stream);
 int rs_sorted_adam(const uint32_t* keys, int64_t n, int D, float* p, float* g, float* m, float* v,
                    int* last, int* owner, int call, const int64_t* step, const float* consts,
                    float beta1, float beta2, float eps, float weight_decay, float scale,

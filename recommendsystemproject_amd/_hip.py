@@ -110,6 +110,8 @@ SIGNATURES = {
     'rs_sparse_flush': (i32, [vp, vp, vp, vp, i64, i32, vp, vp, f32, f32, f32, f32, vp]),
     'rs_lookup_sort_ws_bytes': (i64, [i64, i64]),
     'rs_lookup_sort': (i32, [vp, i32, i32, i32, i64, i64, vp, vp, vp, vp]),
+    'rs_lookup_catchup': (i32, [vp, i32, i32, i32, i64, i64, i32, vp, vp, vp, vp, vp, vp, f32, f32, f32, f32,
+                                vp]),
     'rs_sorted_catchup': (i32, [vp, i64, i32, vp, vp, vp, vp, vp, vp, f32, f32, f32, f32, vp]),
     'rs_sorted_adam': (i32, [vp, i64, i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, f32, f32, f32, f32, f32,
                              vp, vp]),

@@ -470,6 +470,75 @@ __global__ __launch_bounds__(256) void sorted_rows_kernel(RowArgs a) {
 
 constexpr int kRowGrid = 2048;
 
+// ---------------------------------------------------------------- catch-up in lookup order
+// The forward catch-up without the sort: one group of G lanes per lookup e of the [rows, bag] id
+// matrix. The group whose compare-and-swap moves last[row] from its stale value to t is the one
+// that replays the row (any one of the row's lookups: the replay only depends on the row's
+// state, so the result is the same bits as the sorted catch-up's); every other lookup of the row
+// sees last == t, or loses the swap, and does nothing. The gather is the next kernel, so every
+// row it reads is current. This takes the sort off the forward path: it only feeds the backward
+// (segment sums) and the optimizer, and runs on a side stream (flat.py).
+struct IdCatchArgs {
+  const void* ids;
+  int id_bytes;
+  int bag;
+  int64_t stride;
+  int64_t vocab;
+  int64_t n;
+  int D;
+  float* p;
+  float* m;
+  float* v;
+  int* last;
+  const int64_t* step;
+  const float2* consts;
+  AdamConst h;
+};
+
+template <int G>
+__global__ __launch_bounds__(256) void lookup_catchup_kernel(IdCatchArgs a) {
+  const int gl = threadIdx.x & (G - 1);
+  const int t = clamp_step(a.consts, *a.step);
+  const int64_t ngroups = (int64_t)gridDim.x * (256 / G);
+  const int c0 = gl * 4;
+  const int w = c0 < a.D ? (a.D - c0 < 4 ? a.D - c0 : 4) : 0;
+  const bool vec = (a.D & 3) == 0;
+  for (int64_t e = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G; e < a.n; e += ngroups) {
+    const uint32_t k = raw_key(a.ids, a.id_bytes, a.bag, a.stride, a.vocab, e);
+    if (k == kSentinel) continue;  // the gather flags it
+    const int l = a.last[k];
+    // nothing to replay, or a row never stepped (m = v = 0: with weight_decay == 0 the replay is
+    // the identity, exactly)
+    if (l + 1 > t || (l == 0 && a.h.wd == 0.f)) continue;
+    int won = 0;
+    if (gl == 0) won = atomicCAS(&a.last[k], l, t) == l;
+    won = __shfl(won, 0, G);
+    if (!won || w == 0) continue;
+    const int64_t o = (int64_t)k * a.D + c0;
+    float pp[4], mm[4], vv[4];
+    if (vec) {
+      const float4 p4 = *reinterpret_cast<const float4*>(a.p + o);
+      const float4 m4 = *reinterpret_cast<const float4*>(a.m + o);
+      const float4 v4 = *reinterpret_cast<const float4*>(a.v + o);
+      pp[0] = p4.x; pp[1] = p4.y; pp[2] = p4.z; pp[3] = p4.w;
+      mm[0] = m4.x; mm[1] = m4.y; mm[2] = m4.z; mm[3] = m4.w;
+      vv[0] = v4.x; vv[1] = v4.y; vv[2] = v4.z; vv[3] = v4.w;
+    } else {
+      for (int j = 0; j < w; ++j) { pp[j] = a.p[o + j]; mm[j] = a.m[o + j]; vv[j] = a.v[o + j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < w) replay(a.h, a.consts, l + 1, t, pp[j], mm[j], vv[j]);
+    if (vec) {
+      *reinterpret_cast<float4*>(a.p + o) = make_float4(pp[0], pp[1], pp[2], pp[3]);
+      *reinterpret_cast<float4*>(a.m + o) = make_float4(mm[0], mm[1], mm[2], mm[3]);
+      *reinterpret_cast<float4*>(a.v + o) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    } else {
+      for (int j = 0; j < w; ++j) { a.p[o + j] = pp[j]; a.m[o + j] = mm[j]; a.v[o + j] = vv[j]; }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- segment sum (table gradient)
 constexpr int kChunk = 64;
 constexpr int kSegBatch = 16;  // positions whose contributions are loaded together
@@ -902,6 +971,36 @@ extern "C" int rs_sorted_catchup(const uint32_t* keys, int64_t n, int D, float* 
                "rs_sorted_catchup: bad args");
   return sorted_rows(kCatchup, keys, n, D, p, nullptr, m, v, last, nullptr, 0, step, consts, beta1,
                      beta2, eps, weight_decay, 1.f, nullptr, nullptr, as_stream(stream));
+}
+
+extern "C" int rs_lookup_catchup(const void* ids, int id_bytes, int rows, int bag, int64_t row_stride,
+                                 int64_t vocab, int D, float* p, float* m, float* v, int* last,
+                                 const int64_t* step, const float* consts, float beta1, float beta2,
+                                 float eps, float weight_decay, void* stream) {
+  RS_CHECK_ARG(ids && p && m && v && last && step && consts && D >= 1 && rows >= 0 && bag >= 1 &&
+                   row_stride >= bag && (id_bytes == 4 || id_bytes == 8) && vocab >= 1 &&
+                   vocab < ((int64_t)1 << 31),
+               "rs_lookup_catchup: bad args");
+  const int64_t n = (int64_t)rows * bag;
+  if (n == 0) return 0;
+  IdCatchArgs a;
+  a.ids = ids; a.id_bytes = id_bytes; a.bag = bag; a.stride = row_stride; a.vocab = vocab; a.n = n;
+  a.D = D; a.p = p; a.m = m; a.v = v; a.last = last; a.step = step;
+  a.consts = reinterpret_cast<const float2*>(consts);
+  a.h = make_hyper(beta1, beta2, eps, weight_decay);
+  const int G = D <= 16 ? 4 : D <= 32 ? 8 : D <= 64 ? 16 : D <= 128 ? 32 : 64;
+  RS_CHECK_ARG(D <= 4 * G, "rs_lookup_catchup: D %d > 256", D);
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(kRowGrid * 4, cdiv(n, 256 / G)));
+  hipStream_t st = as_stream(stream);
+  switch (G) {
+    case 4: lookup_catchup_kernel<4><<<grid, 256, 0, st>>>(a); break;
+    case 8: lookup_catchup_kernel<8><<<grid, 256, 0, st>>>(a); break;
+    case 16: lookup_catchup_kernel<16><<<grid, 256, 0, st>>>(a); break;
+    case 32: lookup_catchup_kernel<32><<<grid, 256, 0, st>>>(a); break;
+    default: lookup_catchup_kernel<64><<<grid, 256, 0, st>>>(a); break;
+  }
+  RS_CHECK_LAUNCH("rs_lookup_catchup");
+  return 0;
 }
 
 extern "C" int rs_sorted_adam(const uint32_t* keys, int64_t n, int D, float* p, float* g, float* m,

@@ -33,18 +33,66 @@ def lazy_rows_threshold() -> int:
 class LookupCall:
     """One forward lookup of a large table: the call's ids sorted by row (rs_lookup_sort).
     keys[n] = row ids ascending (out-of-range ids last as 0xFFFFFFFF), vals[n] = lookup index
-    r * bag + l, ascending within a row. Kept until the optimizer step (catch-up, gradient
-    segment sums, clip norm and Adam all walk the distinct rows of `keys`). Under data
-    parallelism the backward keeps the call's output gradient rows (dseg) for the exchange."""
+    r * bag + l, ascending within a row. Kept until the optimizer step (gradient segment sums,
+    clip norm and Adam all walk the distinct rows of `keys`). Under data parallelism the backward
+    keeps the call's output gradient rows (dseg) for the exchange.
 
-    __slots__ = ('keys', 'vals', 'n', 'rows', 'bag', 'pad', 'mode', 'ids_ptr', 'id_bytes',
-                 'row_stride', 'keep', 'dseg')
+    The sort may run on a side stream (LazyTable.lookup): `ready` is then that stream, and
+    reading `keys` / `vals` first makes the current stream wait for everything queued on it
+    (torch's wait_stream). Every backward joins its calls (functions._grad_lazy) even when it
+    does not read their keys: a graph capture must not end with the side stream unjoined. keys, vals
+    and the sort workspace are allocated on the forward's stream and held here, so their memory
+    is not reused before that join."""
 
-    def __init__(self, keys, vals, n, rows, bag, pad, mode, ids_ptr, id_bytes, row_stride, keep):
-        self.keys, self.vals, self.n, self.rows, self.bag = keys, vals, n, rows, bag
+    __slots__ = ('_keys', '_vals', 'ws', 'ready', 'n', 'rows', 'bag', 'pad', 'mode', 'ids_ptr',
+                 'id_bytes', 'row_stride', 'keep', 'dseg')
+
+    def __init__(self, keys, vals, n, rows, bag, pad, mode, ids_ptr, id_bytes, row_stride, keep,
+                 ws=None, ready=None):
+        self._keys, self._vals, self.n, self.rows, self.bag = keys, vals, n, rows, bag
         self.pad, self.mode = pad, mode
         self.ids_ptr, self.id_bytes, self.row_stride, self.keep = ids_ptr, id_bytes, row_stride, keep
+        self.ws, self.ready = ws, ready
         self.dseg = None
+
+    def sync(self):
+        if self.ready is not None:
+            torch.cuda.current_stream(self._keys.device).wait_stream(self.ready)
+            self.ready = None
+
+    @property
+    def keys(self):
+        self.sync()
+        return self._keys
+
+    @property
+    def vals(self):
+        self.sync()
+        return self._vals
+
+
+_SORT_STREAMS = {}
+_BRANCH_STREAMS = set()  # stream handles already forked from the main one (the item tower's)
+
+
+def mark_branch_stream(stream):
+    """Register a stream the model forks from its main one (TwoTowerModel's item tower). Lookups
+    issued on it sort in line: a second-level fork (that stream joining the sort stream, then
+    the main stream joining both) makes hipStreamEndCapture crash on this ROCm
+    (tools/capture_fork_repro.py nested), and the branch already runs beside the main stream."""
+    _BRANCH_STREAMS.add(stream.cuda_stream)
+
+
+def _sort_stream(dev):
+    """The side stream the forward's lookup sorts run on (RSYS_SORT_STREAM=1; default in line)."""
+    if os.environ.get('RSYS_SORT_STREAM', '0') != '1':
+        return None
+    if torch.cuda.current_stream(dev).cuda_stream in _BRANCH_STREAMS:
+        return None
+    s = _SORT_STREAMS.get(dev)
+    if s is None:
+        s = _SORT_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 # rs_segsum modes: one id per gradient row, mean bag, sum bag (max pooling: atomic scatter)
@@ -56,7 +104,8 @@ class LazyTable:
 
     Every lookup of the table in a step is a LookupCall (sorted ids). Per step:
       forward  : rs_lookup_sort, then rs_sorted_catchup brings the call's rows to the current
-                 optimizer step before the gather reads them;
+                 optimizer step before the gather reads them (a lookup without a backward:
+                 rs_lookup_catchup in id order, no sort);
       backward : rs_segsum writes each distinct row's gradient (plain stores; added to the row
                  when the table has several calls this step), deterministic;
       optimizer: rs_sorted_sqnorm (clip-norm partials) and rs_sorted_adam over each call's
@@ -76,33 +125,49 @@ class LazyTable:
     def ptr(self, t):
         return t.data_ptr() + 4 * self.offset
 
-    def sort_call(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None):
-        """Sort a [rows, bag] id matrix by row (rs_lookup_sort) into a LookupCall."""
+    def sort_call(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None, side=None):
+        """Sort a [rows, bag] id matrix by row (rs_lookup_sort) into a LookupCall; on stream
+        `side` (forked from the current one, joined when the call's keys are first read) if
+        given."""
         dev = self.param.device
         n = rows * bag
         keys = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         vals = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         wsb = int(_hip.lib().rs_lookup_sort_ws_bytes(n, self.V))
         ws = torch.empty(wsb // 4 + 1, dtype=torch.int32, device=dev) if wsb else None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(dev))
+        st = _stream() if side is None else side.cuda_stream
         _hip.call('rs_lookup_sort', ids_ptr, id_bytes, rows, bag, row_stride, self.V, keys.data_ptr(),
-                  vals.data_ptr(), None if ws is None else ws.data_ptr(), _stream())
+                  vals.data_ptr(), None if ws is None else ws.data_ptr(), st)
         return LookupCall(keys, vals, n, rows, bag, -1 if pad is None else int(pad), mode, ids_ptr,
-                          id_bytes, row_stride, keep)
+                          id_bytes, row_stride, keep, ws, side)
 
-    def lookup(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None):
-        """Forward hook: sort the call's ids, list it for the step, and bring its rows to the
-        current optimizer step before they are gathered."""
-        c = self.sort_call(ids_ptr, rows, bag, row_stride, pad, mode, id_bytes, keep)
-        self.calls.append(c)
-        self.catchup(c)
-        return c
-
-    def catchup(self, c):
+    def lookup(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None, record=True):
+        """Forward hook: bring the call's rows to the current optimizer step before they are
+        gathered and, when the step will train on this lookup (`record`), list it for the step
+        with its ids sorted by row. Default: sort, then rs_sorted_catchup over the distinct rows.
+        A lookup no backward follows (evaluation) is not sorted at all: rs_lookup_catchup works
+        in id order. RSYS_SORT_STREAM=1 moves the sort of recorded lookups to a side stream
+        (their catch-up then in id order too); measured at C3 it only trades the sort for a
+        slower catch-up (0.833 vs 0.839 ms/step), so it is off by default."""
+        c = None
+        side = _sort_stream(self.param.device) if record else None
+        if record:
+            c = self.sort_call(ids_ptr, rows, bag, row_stride, pad, mode, id_bytes, keep, side=side)
+            self.calls.append(c)
         opt = self.flat.lazy_opt
-        if opt is not None and c.n > 0:
+        if opt is None or rows * bag == 0:
+            return c
+        hyper = (opt['step_dev'].data_ptr(), opt['consts'].data_ptr(), *opt['hyper'], _stream())
+        if c is not None and side is None:
             _hip.call('rs_sorted_catchup', c.keys.data_ptr(), c.n, self.D, self.ptr(self.flat.data),
-                      self.ptr(opt['m']), self.ptr(opt['v']), self.last.data_ptr(),
-                      opt['step_dev'].data_ptr(), opt['consts'].data_ptr(), *opt['hyper'], _stream())
+                      self.ptr(opt['m']), self.ptr(opt['v']), self.last.data_ptr(), *hyper)
+        else:
+            _hip.call('rs_lookup_catchup', ids_ptr, id_bytes, rows, bag, row_stride, self.V, self.D,
+                      self.ptr(self.flat.data), self.ptr(opt['m']), self.ptr(opt['v']), self.last.data_ptr(),
+                      *hyper)
+        return c
 
     def segsum(self, c, dout_ptr, ldo, accumulate=None):
         """Backward: the table gradient of call c from its output gradient (dout_ptr = the
@@ -147,6 +212,8 @@ class LazyTable:
         return self.owner
 
     def end_step(self):
+        for c in self.calls + (self.exchanged or []):
+            c.sync()  # the memory of a call's sort is released on the forward's stream
         self.calls = []
         self.exchanged = None
 
@@ -298,7 +365,9 @@ def lazy_tables(module: torch.nn.Module):
     tables = [m for owner in module.modules() if isinstance(getattr(owner, 'embeddings', None), torch.nn.ModuleDict)
               for m in owner.embeddings.values()]
     for m in tables:
-        if isinstance(m, torch.nn.Embedding) and m.num_embeddings >= thr and thr > 0:
+        # the per-row kernels cover a row with at most 64 lanes x 4 columns (csrc/lookup.hip)
+        if isinstance(m, torch.nn.Embedding) and m.num_embeddings >= thr and thr > 0 and \
+                m.embedding_dim <= 256:
             out.append(m.weight)
             if not getattr(m, '_rs_lazy_hooks', False):
                 m.register_state_dict_pre_hook(_flush_hook)
@@ -321,13 +390,14 @@ def _flush_load_hook(module, state_dict, prefix, *args):
     _flush_table(module)  # rows become current, so the loaded weights start from `last` = step
 
 
-def lookup_table(weight, ids_ptr, rows, bag, row_stride, pad, mode, keep=None):
+def lookup_table(weight, ids_ptr, rows, bag, row_stride, pad, mode, keep=None, record=True):
     """Forward-side hook of the custom ops for a table lookup: a LookupCall for large
-    (lazy-Adam) tables, None for ordinary ones."""
+    (lazy-Adam) tables (None for ordinary ones, and for a lookup no backward follows: `record`
+    False, the rows are only brought current)."""
     t = getattr(weight, '_rs_lazy', None)
     if t is None or flat_of(weight) is not t.flat:
         return None
-    return t.lookup(ids_ptr, rows, bag, row_stride, pad, mode, keep=keep)
+    return t.lookup(ids_ptr, rows, bag, row_stride, pad, mode, keep=keep, record=record)
 
 
 def grad_of(p):

@@ -39,12 +39,12 @@ def _pad(v):
     return -1 if v is None else int(v)
 
 
-def _lookup_lazy(segs, tables, rows, keep=None):
-    """Large (lazy-Adam) tables, flat.py: sort this call's ids by row (csrc/lookup.hip) and bring
-    those rows to the current optimizer step before the gather reads them. Returns
-    {segment index: LookupCall}; ordinary tables are not listed. `keep` (the id tensors the
-    segments point into) stays referenced by the calls until the optimizer step (the
-    data-parallel exchange re-reads the ids after the backward)."""
+def _lookup_lazy(segs, tables, rows, keep=None, record=True):
+    """Large (lazy-Adam) tables, flat.py: bring this call's rows to the current optimizer step
+    before the gather reads them and (`record`: a backward follows) sort its ids by row
+    (csrc/lookup.hip). Returns {segment index: LookupCall}; ordinary tables are not listed.
+    `keep` (the id tensors the segments point into) stays referenced by the calls until the
+    optimizer step (the data-parallel exchange re-reads the ids after the backward)."""
     calls = {}
     for i, (s, t) in enumerate(zip(segs, tables)):
         if s.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL) and hasattr(t, '_rs_lazy'):
@@ -56,7 +56,7 @@ def _lookup_lazy(segs, tables, rows, keep=None):
             if mode is not None and (s.dim > 256 or s.dim % 4):
                 mode = None  # rs_segsum: D <= 256, a multiple of 4 (float4 rows)
             c = lookup_table(t, s.idx, rows, bag, s.idx_stride, None if s.pad_idx < 0 else s.pad_idx,
-                             -1 if mode is None else mode, keep=keep)
+                             -1 if mode is None else mode, keep=keep, record=record)
             if c is not None:
                 calls[i] = c
     return calls
@@ -74,6 +74,10 @@ def _grad_lazy(segs, calls, dout, tables):
             tables[i]._rs_lazy.segsum(c, ptr, dout.stride(0))
         else:
             rest.append(s)
+    for c in (calls or {}).values():
+        # join the side-stream sorts this backward did not read (atomic-scatter segments, the
+        # data-parallel path): a hipGraph capture must not end with a forked stream unjoined
+        c.sync()
     return rest
 
 
@@ -119,7 +123,7 @@ def seq_feature_segments(proc, seqd, B, L):
     return segs, tables, col, keep
 
 
-def seq_input_fwd(proc, seqd, B, L, p, key, err):
+def seq_input_fwd(proc, seqd, B, L, p, key, err, need=True):
     """gather -> Linear(sum dims -> d) -> Dropout -> + pos_emb -> F.dropout (T5). Returns x [B*L, d]."""
     segs, tables, dcat, keep = seq_feature_segments(proc, seqd, B, L)
     if dcat != proc.feature_projection[0].in_features:
@@ -128,7 +132,7 @@ def seq_input_fwd(proc, seqd, B, L, p, key, err):
     M = B * L
     dev = proc.pos_emb.weight.device
     cat = torch.empty(M, dcat, device=dev, dtype=torch.float32)
-    calls = _lookup_lazy(segs, tables, M, keep)
+    calls = _lookup_lazy(segs, tables, M, keep, record=need)
     ops.gather_fwd(segs, M, cat, err)
     lin = proc.feature_projection[0]
     pos = proc.pos_emb.weight
@@ -377,7 +381,7 @@ class SeqEncoderFn(torch.autograd.Function):
         p = enc.dropout_p if enc.training else 0.0
         key = ops.rng_next(enc.rng_state) if p > 0 else None
         err = enc.err_flag
-        x, in_saved = seq_input_fwd(proc, seqd, B, L, p, key, err)
+        x, in_saved = seq_input_fwd(proc, seqd, B, L, p, key, err, need)
         layers = list(enc.transformer_backbone.layers)
         if enc.transformer_backbone.norm is not None:
             raise NotImplementedError('TransformerEncoder(norm=...) is not used by the reference')
@@ -530,7 +534,7 @@ class TowerFeatureFn(torch.autograd.Function):
             raise RuntimeError(f'too many features in one tower ({len(segs)} > {_hip.MAX_SEGMENTS})')
         dev = tower.feature_bn.weight.device
         out = torch.empty(B, col, device=dev, dtype=torch.float32)
-        calls = _lookup_lazy(segs, [w for w, _ in pp], B, keep)
+        calls = _lookup_lazy(segs, [w for w, _ in pp], B, keep, record=need)
         ops.gather_fwd(segs, B, out, tower.err_flag)
         if need:
             ctx.segs, ctx.pp, ctx.keep, ctx.B, ctx.calls = segs, pp, keep, B, calls

@@ -6,11 +6,20 @@ seeded from the key name, so any element error e shows up at ~|e| in the project
 """
 from __future__ import annotations
 
+import glob
 import io
+import os
 import zlib
 
 import numpy as np
 import yaml
+
+def training_fixtures(golden_dir: str):
+    """The training-step fixtures of make_golden.py (per-step 'losses'); the loader and
+    validate() fixtures beside them have their own tests."""
+    return [p for p in sorted(glob.glob(os.path.join(golden_dir, '*.npz')))
+            if 'losses' in np.load(p, allow_pickle=False).files]
+
 
 FULL_LIMIT = 4096  # tensors with at most this many elements are stored whole in summary mode
 

@@ -160,9 +160,12 @@ def _sorted_rows(keys):
     return sorted(set(int(x) for x in k if x != SENT))
 
 
+@pytest.mark.parametrize('catch', ['sorted', 'ids'])
 @pytest.mark.parametrize('D,wd,clip,calls', [(40, 0.0, False, 1), (128, 0.0, True, 1), (16, 0.0, False, 1),
-                                             (64, 0.01, True, 1), (32, 0.0, True, 2)])
-def test_lazy_adam_bitwise_equals_dense(D, wd, clip, calls):
+                                             (64, 0.01, True, 1), (32, 0.0, True, 2), (6, 0.01, False, 2)])
+def test_lazy_adam_bitwise_equals_dense(D, wd, clip, calls, catch):
+    """Forward catch-up either over the sorted keys (rs_sorted_catchup) or straight from the id
+    matrix (rs_lookup_catchup: one compare-and-swap per row picks the replaying lookup)."""
     V, pad, steps, cap = 3000, 7, 9, 64
     gen = torch.Generator().manual_seed(D + calls)
     p0 = torch.randn(V, D, generator=gen).to(DEV)
@@ -191,10 +194,16 @@ def test_lazy_adam_bitwise_equals_dense(D, wd, clip, calls):
             ids = ids[:n_ids].view(-1, 3)
             if n_ids == 0:
                 continue
-            keys, _ = _sort(ids.to(DEV), V)
+            ids_d = ids.to(DEV)
+            keys, _ = _sort(ids_d, V)
             sorted_calls.append(keys)
-            _hip.call('rs_sorted_catchup', keys.data_ptr(), ids.numel(), D, pl.data_ptr(), ml.data_ptr(),
-                      vl.data_ptr(), last.data_ptr(), step_l.data_ptr(), consts.data_ptr(), *hyper, S)
+            if catch == 'sorted':
+                _hip.call('rs_sorted_catchup', keys.data_ptr(), ids.numel(), D, pl.data_ptr(), ml.data_ptr(),
+                          vl.data_ptr(), last.data_ptr(), step_l.data_ptr(), consts.data_ptr(), *hyper, S)
+            else:
+                _hip.call('rs_lookup_catchup', ids_d.data_ptr(), 8, ids.shape[0], 3, 3, V, D, pl.data_ptr(),
+                          ml.data_ptr(), vl.data_ptr(), last.data_ptr(), step_l.data_ptr(), consts.data_ptr(),
+                          *hyper, S)
             rows |= set(_sorted_rows(keys))
         rows = sorted(rows)
         # what the forward reads: touched rows (pad included) equal the dense weights exactly

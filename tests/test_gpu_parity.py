@@ -20,7 +20,7 @@ from recommendsystemproject_amd.project.utils.training_utils import extract_item
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-GOLD = sorted(glob.glob(os.path.join(ROOT, 'tests', 'golden', '*.npz')))
+GOLD = gu.training_fixtures(os.path.join(ROOT, 'tests', 'golden'))
 DEV = torch.device('cuda:0')
 
 

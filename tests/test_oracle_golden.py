@@ -11,7 +11,7 @@ import golden_util as gu
 from oracle.twotower_oracle import OracleTrainer, model_state_shapes
 from recommendsystemproject_amd import synth
 
-GOLD = sorted(glob.glob(os.path.join(os.path.dirname(__file__), 'golden', '*.npz')))
+GOLD = gu.training_fixtures(os.path.join(os.path.dirname(__file__), 'golden'))
 
 
 def _tb(b):
