@@ -175,6 +175,16 @@ int rs_ffn_bwd_ln_bf16(int M, int F, const float* x, const float* W1, const floa
  * (the fused FFN's f1 / dPre1). Replaces the weight-gradient part of autograd's Linear backward
  * (Tower.py:16-25, TransformerEncoderLayer). ws: rs_wgrad_ws_bytes. */
 int64_t rs_wgrad_ws_bytes(int Mo, int No, int rows);
+/* The FFN block's weight gradients without its [M, F] activations in HBM (bf16 mode):
+ * dW1 += dPre1^T x, db1 += colsum(dPre1), dW2 += dff^T f1, db2 += colsum(dff), with f1 and
+ * dPre1 recomputed from x, dff and the forward's mask exactly as rs_ffn_bwd_bf16 forms them
+ * (which then runs with f1 = dpre = NULL). Replaces the two rs_wgrad_bf16 calls of
+ * linear2.weight / linear1.weight (.grad accumulation of nn.TransformerEncoderLayer's
+ * feed-forward, SequenceEncoder.py:17-29). ws: rs_ffn_wgrad_ws_bytes; deterministic. */
+int64_t rs_ffn_wgrad_ws_bytes(int M, int F);
+int rs_ffn_wgrad_bf16(int M, int F, const float* x, const float* W1, const float* b1, const float* W2,
+                      const uint64_t* mask, const float* dff, float p, float* dW1, float* db1,
+                      float* dW2, float* db2, float* ws, void* stream);
 int rs_wgrad_bf16(int rows, int Mo, int No, const void* dy, int ldy, int dy_bf16, const void* x,
                   int ldx, int x_bf16, float beta, float* dW, int ldw, float* db, float* ws,
                   void* stream);

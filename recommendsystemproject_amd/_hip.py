@@ -50,6 +50,8 @@ SIGNATURES = {
     'rs_ffn_bwd_ln_bf16': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                  vp, vp, f32, vp, i32, vp, vp]),
     'rs_wgrad_ws_bytes': (i64, [i32, i32, i32]),
+    'rs_ffn_wgrad_ws_bytes': (i64, [i32, i32]),
+    'rs_ffn_wgrad_bf16': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp]),
     'rs_wgrad_bf16': (i32, [i32, i32, i32, vp, i32, i32, vp, i32, i32, f32, vp, i32, vp, vp, vp]),
     'rs_colsum_ws_bytes': (i64, [i32, i32]),
     'rs_colsum': (i32, [vp, i32, i32, i32, f32, f32, vp, vp, vp]),

@@ -254,17 +254,19 @@ __global__ __launch_bounds__(512) void ffn_fwd_bf16_kernel(FfnArgs a) {
   }
 }
 
-template <int F, bool LN1 = false, bool LNDROP = false>
+// ACTS: also write f1 and dPre1 (bf16) for rs_wgrad_bf16; without them (the weight gradients
+// by rs_ffn_wgrad_bf16) linear1 is not recomputed and its W1 image is not staged.
+template <int F, bool LN1 = false, bool LNDROP = false, bool ACTS = true>
 __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
   constexpr int FP = F + 8;
   constexpr int NH = F / 16, NC = F / 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  __bf16* W1s = reinterpret_cast<__bf16*>(smem_raw);  // [F][DP]  (x1 W1^T)
-  __bf16* W2t = W1s + F * DP;                           // [F][DP]  W2^T (dff W2)
+  __bf16* W1s = reinterpret_cast<__bf16*>(smem_raw);  // [F][DP]  (x1 W1^T; ACTS only)
+  __bf16* W2t = W1s + (ACTS ? F * DP : 0);              // [F][DP]  W2^T (dff W2)
   __bf16* W1t = W2t + F * DP;                           // [D][FP]  W1^T, k-permuted (dPre1 W1)
   float* sb1 = reinterpret_cast<float*>(W1t + D * FP);  // [F]
   stage_batched<F, D, 512>(a.W1, D, [&](int n1, int k, const floatx4& v) {
-    put4(W1s + n1 * DP + k, v);
+    if constexpr (ACTS) put4(W1s + n1 * DP + k, v);
 #pragma unroll
     for (int e = 0; e < 4; ++e) W1t[(k + e) * FP + kslot(n1)] = (__bf16)v[e];  // W1^T, k-permuted
   });
@@ -282,8 +284,12 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
   int g = blockIdx.x * 8 + wave;
   floatx4 xr[4], dr[4];
   if (g < groups) {
-    load_row64(a.x, (int64_t)g * 16 + r, q, xr);
+    if constexpr (ACTS) load_row64(a.x, (int64_t)g * 16 + r, q, xr);
     load_row64(a.dff, (int64_t)g * 16 + r, q, dr);
+  }
+  if constexpr (!ACTS) {  // x1 only feeds linear1's recompute
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xr[u] = floatx4{0.f, 0.f, 0.f, 0.f};
   }
   // LN1: gamma at this lane's columns 16t + 4q + e, and its dgamma / dbeta partial sums
   floatx4 lgm[LN1 ? 4 : 1], lpg[LN1 ? 4 : 1], lpb[LN1 ? 4 : 1];
@@ -319,7 +325,7 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
     bf16x8 ax[2] = {cvt8(xr[0], xr[1]), cvt8(xr[2], xr[3])};
     bf16x8 ad[2] = {cvt8(dr[0], dr[1]), cvt8(dr[2], dr[3])};
     const int gn = g + stride < groups ? g + stride : g;
-    load_row64(a.x, (int64_t)gn * 16 + r, q, xr);
+    if constexpr (ACTS) load_row64(a.x, (int64_t)gn * 16 + r, q, xr);
     load_row64(a.dff, (int64_t)gn * 16 + r, q, dr);
     bf16x8 a3[NC];
 #pragma unroll
@@ -329,7 +335,7 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
       for (int hh = 0; hh < 4; ++hh) {
         acc[hh] = floatx4{0.f, 0.f, 0.f, 0.f};
         accd[hh] = floatx4{0.f, 0.f, 0.f, 0.f};
-        RS_MFMA2(acc[hh], W1i, DP, (h0 + hh) * 16 + r, ax);
+        if constexpr (ACTS) RS_MFMA2(acc[hh], W1i, DP, (h0 + hh) * 16 + r, ax);
         RS_MFMA2(accd[hh], W2i, DP, (h0 + hh) * 16 + r, ad);
       }
 #pragma unroll
@@ -347,8 +353,10 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
           d4[i] = (__bf16)d;
           a3[h >> 1][4 * (h & 1) + i] = d4[i];
         }
-        *reinterpret_cast<bf16x4*>(a.f1 + m * F + n0) = f4;
-        *reinterpret_cast<bf16x4*>(a.dpre + m * F + n0) = d4;
+        if constexpr (ACTS) {
+          *reinterpret_cast<bf16x4*>(a.f1 + m * F + n0) = f4;
+          *reinterpret_cast<bf16x4*>(a.dpre + m * F + n0) = d4;
+        }
       }
     }
     floatx4 acc3[4];
@@ -432,10 +440,247 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ fused weight gradients
+// rs_ffn_wgrad_bf16: dW1 += dPre1^T x1, db1 += colsum(dPre1), dW2 += dff^T f1, db2 += colsum(dff)
+// with f1 = drop(relu(x1 W1^T + b1)) and dPre1 = (dff W2) * mask / (1 - p) recomputed on the
+// MFMA from x1, dff and the forward's bit mask -- the [M, F] activations never reach HBM (the
+// unfused pair wrote them as bf16 in the backward and read them back in two rs_wgrad_bf16
+// passes: 3 KB per token against 544 B here).
+//
+// A workgroup streams a contiguous row range in chunks of 64 rows (x1, dff rounded to bf16 into
+// row-major LDS images, the mask words beside them; registers double-buffer the next chunk).
+// Wave w owns the F columns n1 in [32w, 32w + 32): its W1 / W2^T fragments live in registers, it
+// recomputes linear1 and dff W2 for its columns with x1 / dff as the A operand (the same k split
+// as the forward and rs_ffn_bwd_bf16, so f1 and dPre1 are the same bits), which leaves the
+// 16 x 16 results in exactly the operand layout of a 16x16x16 MFMA that contracts over the rows:
+//   dW2[n2][n1] += dff^T (ds_read_b64_tr_b16 from the dff image) x f1 (registers),
+//   dW1[n1][k]  += dPre1 (registers) x x1 (transposed read from the x1 image).
+// Per workgroup partials [dW1 | dW2 | db1 | db2] go to ws in fixed order; ffn_wgrad_reduce adds
+// them into the gradients (deterministic).
+constexpr int WG_ROWS = 64;
+constexpr int WXP = 96;  // LDS pitch (bf16) of the [64][64] images: the 4 rows of a transposed
+                         // read fall in distinct 64-byte windows (wb_pitch rule)
+constexpr int WG_F = 256;
+constexpr int WG_OUT = 2 * WG_F * D + WG_F + D;  // dW1 [F][D], dW2 [D][F], db1 [F], db2 [D]
+
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ shortx4 tr4(const __bf16* p) {
+  typedef __attribute__((address_space(3))) shortx4* lptr;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lptr)(p));
+}
+
+__device__ __forceinline__ short bf16_bits(float v) { return __builtin_bit_cast(short, (__bf16)v); }
+
+__global__ __launch_bounds__(512) void ffn_wgrad_bf16_kernel(FfnArgs a, float* ws, int rows_per_block) {
+  constexpr int F = WG_F;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  __bf16* Xs = reinterpret_cast<__bf16*>(smem_raw);                      // [2][64][WXP]
+  __bf16* Ds = Xs + 2 * WG_ROWS * WXP;                                    // [2][64][WXP]
+  uint64_t* Ms = reinterpret_cast<uint64_t*>(Ds + 2 * WG_ROWS * WXP);      // [2][64][4]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(a.M, r0 + rows_per_block);
+  const float scale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+  // this wave's W fragments: column n1 = 32 wave + 16 j + r of W1 (k = 16q + 8h ..) and of W2^T
+  bf16x8 w1f[2][2], w2f[2][2];
+  float b1v[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n1 = 32 * wave + 16 * j + r;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float* w1 = a.W1 + n1 * D + 16 * q + 8 * h;
+      const floatx4 lo = *(gptr4)(w1), hi = *(gptr4)(w1 + 4);
+      w1f[j][h] = cvt8(lo, hi);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w2f[j][h][e] = (__bf16)a.W2[(16 * q + 8 * h + e) * F + n1];
+    }
+    b1v[j] = a.b1[n1];
+  }
+  // staging: thread slots tid, tid + 512 of x1 and of dff (64 rows x 16 float4 each), and for
+  // tid < 128 two mask words (64 rows x 4 words)
+  floatx4 st[4];
+  u32x4 mst = {0u, 0u, 0u, 0u};
+  float ysum[4] = {0.f, 0.f, 0.f, 0.f};  // colsum(dff) partials of this thread's 4 columns
+  auto load_chunk = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s2 = tid + 512 * (i & 1), row = c0 + s2 / 16, col = (s2 % 16) * 4;
+      const float* src = i < 2 ? a.x : a.dff;
+      st[i] = row < r1 ? *(gptr4)(src + (int64_t)row * D + col) : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (tid < 128) {
+      const int row = c0 + tid / 2;
+      mst = row < r1 ? *reinterpret_cast<const u32x4*>(a.mask + (int64_t)row * 4 + 2 * (tid & 1))
+                     : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s2 = tid + 512 * (i & 1), row = s2 / 16, col = (s2 % 16) * 4;
+      if (i >= 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ysum[e] += st[i][e];
+      }
+      put4((i < 2 ? Xs : Ds) + (buf * WG_ROWS + row) * WXP + col, st[i]);
+    }
+    if (tid < 128) *reinterpret_cast<u32x4*>(Ms + (buf * WG_ROWS + tid / 2) * 4 + 2 * (tid & 1)) = mst;
+  };
+  floatx4 acc1[2][4], acc2[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      acc1[j][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+      acc2[j][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  // db1 = colsum(dPre1) as one more 16x16x16 product with a ones operand (every column of the
+  // result holds the partial column sums)
+  floatx4 accb[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+  const short one = bf16_bits(1.f);
+  const shortx4 ones = {one, one, one, one};
+  const int lq = (lane & 15) >> 2, lp = lane & 3;  // transposed-read row / column group
+  int buf = 0;
+  if (r0 < r1) {
+    load_chunk(r0);
+    store_chunk(0);
+  }
+  __syncthreads();
+  for (int c0 = r0; c0 < r1; c0 += WG_ROWS) {
+    const bool more = c0 + WG_ROWS < r1;
+    if (more) load_chunk(c0 + WG_ROWS);
+    const __bf16* X = Xs + buf * WG_ROWS * WXP;
+    const __bf16* DF = Ds + buf * WG_ROWS * WXP;
+    const uint64_t* MK = Ms + buf * WG_ROWS * 4;
+#pragma unroll
+    for (int mt = 0; mt < WG_ROWS / 16; ++mt) {
+      // recompute operands: row mt*16 + r, k = 16q .. 16q + 15
+      const __bf16* xrow = X + (mt * 16 + r) * WXP + 16 * q;
+      const __bf16* drow = DF + (mt * 16 + r) * WXP + 16 * q;
+      const bf16x8 xa0 = lds8(xrow), xa1 = lds8(xrow + 8), da0 = lds8(drow), da1 = lds8(drow + 8);
+      // contraction operands over the rows: lane -> column 16t + r, rows mt*16 + 4q .. + 3
+      shortx4 xt[4], dt[4];
+      const int trow = mt * 16 + 4 * q + lq;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        xt[t] = tr4(X + trow * WXP + 16 * t + 4 * lp);
+        dt[t] = tr4(DF + trow * WXP + 16 * t + 4 * lp);
+      }
+      // mask words of this lane's rows 4q + e: column n1 = 16 T + r sits in word r >> 2, bit
+      // 4 T + (r & 3) (the forward's layout)
+      uint64_t mw[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mw[e] = MK[(mt * 16 + 4 * q + e) * 4 + (r >> 2)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        floatx4 pre = {0.f, 0.f, 0.f, 0.f}, dpr = {0.f, 0.f, 0.f, 0.f};
+        pre = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa0, w1f[j][0], pre, 0, 0, 0);
+        pre = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa1, w1f[j][1], pre, 0, 0, 0);
+        dpr = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da0, w2f[j][0], dpr, 0, 0, 0);
+        dpr = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da1, w2f[j][1], dpr, 0, 0, 0);
+        const int bit = 4 * (2 * wave + j) + (r & 3);
+        shortx4 f4, d4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool keep = (mw[e] >> bit) & 1ull;
+          const float pv = pre[e] * 1.0f + b1v[j];
+          const float f = keep ? pv * scale : 0.f;  // == rs_ffn_bwd_bf16's f1
+          const float d = keep ? scale * dpr[e] : 0.f;
+          f4[e] = bf16_bits(f);
+          d4[e] = bf16_bits(d);
+        }
+        accb[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(d4, ones, accb[j], 0, 0, 0);  // db1 (bf16 dPre1)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          acc2[j][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(dt[t], f4, acc2[j][t], 0, 0, 0);
+          acc1[j][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(d4, xt[t], acc1[j][t], 0, 0, 0);
+        }
+      }
+    }
+    if (more) store_chunk(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // partials of this workgroup -> ws[block]: dW1 [n1][k], dW2 [n2][n1], db1, db2
+  float* out = ws + (int64_t)blockIdx.x * WG_OUT;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int T = 2 * wave + j;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        out[(16 * T + 4 * q + e) * D + 16 * t + r] = acc1[j][t][e];
+        out[F * D + (16 * t + 4 * q + e) * F + 16 * T + r] = acc2[j][t][e];
+      }
+  }
+  if (r == 0) {  // accb rows n1 = 16 T + 4 q + e (every column alike)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[2 * F * D + 16 * (2 * wave + j) + 4 * q + e] = accb[j][e];
+  }
+  float* red = reinterpret_cast<float*>(smem_raw);  // the images are dead
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[1024 + tid * 4 + e] = ysum[e];
+  __syncthreads();
+  if (tid >= F && tid < F + D) {  // column c of dff: the threads 16 row + c / 4 (32 rows of slots)
+    const int c = tid - F;
+    float v = 0.f;
+    for (int rw = 0; rw < 32; ++rw) v += red[1024 + (16 * rw + c / 4) * 4 + (c & 3)];
+    out[2 * F * D + F + c] = v;
+  }
+}
+
+// grad[i] += sum over the P workgroup partials of entry i, in partial order
+__global__ __launch_bounds__(1024) void ffn_wgrad_reduce_kernel(const float* __restrict__ ws, int P, float* dW1,
+                                                                float* dW2, float* db1, float* db2) {
+  __shared__ float red[16][64];
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int l = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (e < WG_OUT) {
+    int p = l;
+    for (; p + 16 * 7 < P; p += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ws[(int64_t)(p + 16 * u) * WG_OUT + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; p < P; p += 16) acc += ws[(int64_t)p * WG_OUT + e];
+  }
+  red[l][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (l != 0 || e >= WG_OUT) return;
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
+  constexpr int FD = WG_F * D;
+  if (e < FD) dW1[e] += t;
+  else if (e < 2 * FD) dW2[e - FD] += t;
+  else if (e < 2 * FD + WG_F) db1[e - 2 * FD] += t;
+  else db2[e - 2 * FD - WG_F] += t;
+}
+
+int wgrad_fused_grid(int M) {
+  const int chunks = cdiv(M, WG_ROWS);
+  int g = cdiv(chunks, 4);  // >= 4 chunks per workgroup: the partials stay well below the reads
+  return g < 1 ? 1 : (g > 256 ? 256 : g);
+}
+
+size_t wgrad_fused_lds() { return (size_t)2 * 2 * WG_ROWS * WXP * 2 + (size_t)2 * WG_ROWS * 4 * 8; }
+
 #undef RS_MFMA2
 
 size_t fwd_lds(int F) { return (size_t)F * DP * 2 + (size_t)D * (F + 8) * 2 + (size_t)(F + 3 * D) * 4; }
-size_t bwd_lds(int F) { return (size_t)2 * F * DP * 2 + (size_t)D * (F + 8) * 2 + (size_t)F * 4; }
+size_t bwd_lds(int F, bool acts = true) {
+  return (size_t)(acts ? 2 : 1) * F * DP * 2 + (size_t)D * (F + 8) * 2 + (size_t)F * 4;
+}
 
 int grid_for(int M, size_t lds) {
   const int per_cu = lds > 80 * 1024 ? 1 : 2;
@@ -489,7 +734,7 @@ extern "C" int rs_ffn_bwd_ln_bf16(int M, int F, const float* x, const float* W1,
                                   const int64_t* key, int site, float* ws, void* stream) {
   RS_CHECK_ARG(M >= 0 && M % 16 == 0 && F == 256, "rs_ffn_bwd_ln_bf16: need M %% 16 == 0 and F == 256 (M=%d F=%d)", M, F);
   RS_CHECK_ARG(x && W1 && b1 && W2 && mask && dff && dres && h1 && gamma1 && mean1 && rstd1 && dh1 &&
-                   dgamma1 && dbeta1 && f1 && dpre && ws,
+                   dgamma1 && dbeta1 && ws && (!f1) == (!dpre),
                "rs_ffn_bwd_ln_bf16: null operand");
   RS_CHECK_ARG(dh1 != dff && dh1 != h1 && (dh1 != dres || dff != dres),
                "rs_ffn_bwd_ln_bf16: dh1 may alias dres only when dff is not dres");
@@ -505,11 +750,17 @@ extern "C" int rs_ffn_bwd_ln_bf16(int M, int F, const float* x, const float* W1,
   a.dpre = reinterpret_cast<__bf16*>(dpre); a.p = p; a.key = key;
   a.ln_h = h1; a.ln_gamma = gamma1; a.ln_mean = mean1; a.ln_rstd = rstd1; a.ln_da = dsa; a.ln_ws = ws;
   a.ln_site = site;
-  const size_t lds = bwd_lds(F);
-  const int nb = grid_for(M, lds);
+  const bool acts = f1 != nullptr;
+  const size_t lds = bwd_lds(F, acts);
+  const int nb = grid_for(M, bwd_lds(F));  // the partials' count (rs_ffn_bwd_ln_ws_bytes)
   hipStream_t st = as_stream(stream);
-  if (p > 0.f) ffn_bwd_bf16_kernel<256, true, true><<<nb, 512, lds, st>>>(a);
-  else ffn_bwd_bf16_kernel<256, true, false><<<nb, 512, lds, st>>>(a);
+  if (acts) {
+    if (p > 0.f) ffn_bwd_bf16_kernel<256, true, true><<<nb, 512, lds, st>>>(a);
+    else ffn_bwd_bf16_kernel<256, true, false><<<nb, 512, lds, st>>>(a);
+  } else {
+    if (p > 0.f) ffn_bwd_bf16_kernel<256, true, true, false><<<nb, 512, lds, st>>>(a);
+    else ffn_bwd_bf16_kernel<256, true, false, false><<<nb, 512, lds, st>>>(a);
+  }
   RS_CHECK_LAUNCH("rs_ffn_bwd_ln_bf16");
   return partials_reduce2(ws, nb, 128, 64, 1.f, 1.f, dgamma1, dbeta1, st);
 }
@@ -519,7 +770,7 @@ extern "C" int rs_ffn_bwd_bf16(int M, int F, const float* x, const float* W1, co
                                const float* dres, float* dx, void* f1, void* dpre, float p,
                                void* stream) {
   RS_CHECK_ARG(M >= 0 && M % 16 == 0 && F == 256, "rs_ffn_bwd_bf16: need M %% 16 == 0 and F == 256 (M=%d F=%d)", M, F);
-  RS_CHECK_ARG(x && W1 && b1 && W2 && mask && dff && dres && dx && f1 && dpre,
+  RS_CHECK_ARG(x && W1 && b1 && W2 && mask && dff && dres && dx && (!f1) == (!dpre),
                "rs_ffn_bwd_bf16: null operand");
   RS_CHECK_ARG(dx != dff || dx == dres, "rs_ffn_bwd_bf16: dx may alias dres only");
   RS_CHECK_ARG(aligned16(x) && aligned16(dff) && aligned16(dres) && aligned16(dx) && aligned16(b1) &&
@@ -531,9 +782,38 @@ extern "C" int rs_ffn_bwd_bf16(int M, int F, const float* x, const float* W1, co
   a.M = M; a.x = x; a.W1 = W1; a.b1 = b1; a.W2 = W2; a.mask = const_cast<uint64_t*>(mask);
   a.dff = dff; a.dres = dres; a.dx = dx; a.f1 = reinterpret_cast<__bf16*>(f1); a.dpre = reinterpret_cast<__bf16*>(dpre);
   a.p = p;
-  const size_t lds = bwd_lds(F);
-  ffn_bwd_bf16_kernel<256><<<grid_for(M, lds), 512, lds, as_stream(stream)>>>(a);
+  const bool acts = f1 != nullptr;
+  const size_t lds = bwd_lds(F, acts);
+  if (acts) ffn_bwd_bf16_kernel<256><<<grid_for(M, lds), 512, lds, as_stream(stream)>>>(a);
+  else ffn_bwd_bf16_kernel<256, false, false, false><<<grid_for(M, lds), 512, lds, as_stream(stream)>>>(a);
   RS_CHECK_LAUNCH("rs_ffn_bwd_bf16");
+  return 0;
+}
+
+extern "C" int64_t rs_ffn_wgrad_ws_bytes(int M, int F) {
+  return F == 256 && M > 0 ? (int64_t)wgrad_fused_grid(M) * WG_OUT * (int64_t)sizeof(float) : 0;
+}
+
+extern "C" int rs_ffn_wgrad_bf16(int M, int F, const float* x, const float* W1, const float* b1,
+                                 const float* W2, const uint64_t* mask, const float* dff, float p,
+                                 float* dW1, float* db1, float* dW2, float* db2, float* ws, void* stream) {
+  RS_CHECK_ARG(M >= 0 && M % 16 == 0 && F == 256, "rs_ffn_wgrad_bf16: need M %% 16 == 0 and F == 256 (M=%d F=%d)", M, F);
+  RS_CHECK_ARG(x && W1 && b1 && W2 && mask && dff && dW1 && db1 && dW2 && db2 && (ws || M == 0),
+               "rs_ffn_wgrad_bf16: null operand");
+  RS_CHECK_ARG(aligned16(x) && aligned16(dff) && aligned16(W1) && aligned16(mask),
+               "rs_ffn_wgrad_bf16: misaligned operand");
+  RS_CHECK_ARG(p >= 0.f && p < 1.f, "rs_ffn_wgrad_bf16: 0 <= p < 1");
+  if (M == 0) return 0;
+  FfnArgs a{};
+  a.M = M; a.x = x; a.W1 = W1; a.b1 = b1; a.W2 = W2; a.mask = const_cast<uint64_t*>(mask); a.dff = dff;
+  a.p = p;
+  const int G = wgrad_fused_grid(M);
+  const int rpb = cdiv(cdiv(M, WG_ROWS), G) * WG_ROWS;
+  hipStream_t st = as_stream(stream);
+  ffn_wgrad_bf16_kernel<<<cdiv(M, rpb), 512, wgrad_fused_lds(), st>>>(a, ws, rpb);
+  RS_CHECK_LAUNCH("rs_ffn_wgrad_bf16");
+  ffn_wgrad_reduce_kernel<<<cdiv(WG_OUT, 64), 1024, 0, st>>>(ws, cdiv(M, rpb), dW1, dW2, db1, db2);
+  RS_CHECK_LAUNCH("rs_ffn_wgrad_bf16 reduce");
   return 0;
 }
 

@@ -281,22 +281,30 @@ def _post_attn_bwd(lyr, saved, dx2, p, key, site):
     dff = dh2 if dff is None else dff
     ln1_done = False
     if isinstance(f1, tuple):  # fused feed-forward block (bf16 mode)
+        # fused weight gradients: f1 / dPre1 recomputed on chip, never written (csrc/ffn.hip)
+        acts = not ops.ffn_wgrad_fused()
         if not os.environ.get('RSYS_UNFUSED_FFN_LN'):
             # dx1 = dh2 + dPre1 W1 and norm1's backward in one pass: dx1 stays on chip
             dh1, dsa, f1b, dpre = ops.ffn_bwd_ln_bf16(
                 x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, f1[1], dff, dh2, h1,
-                lyr.norm1.weight, m1, r1, g(lyr.norm1.weight), g(lyr.norm1.bias), p, key, site + 1)
+                lyr.norm1.weight, m1, r1, g(lyr.norm1.weight), g(lyr.norm1.bias), p, key, site + 1,
+                acts=acts)
             ln1_done = True
         else:
             # dx1 = dh2 + dPre1 W1 (out of place: dff may be dh2 itself and is read again below)
             dh2, f1b, dpre = ops.ffn_bwd_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight,
-                                              f1[1], dff, dh2, p)
+                                              f1[1], dff, dh2, p, acts=acts)
 
-        def _ffn_wgrads(dff=dff, f1b=f1b, dpre=dpre):
+        def _ffn_wgrads(dff=dff, f1b=f1b, dpre=dpre, mask=f1[1]):
+            if not acts:
+                ops.ffn_wgrad_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, mask, dff, p,
+                                   g(lyr.linear1.weight), g(lyr.linear1.bias), g(lyr.linear2.weight),
+                                   g(lyr.linear2.bias))
+                return
             ops.wgrad_bf16(dff, f1b, g(lyr.linear2.weight), db=g(lyr.linear2.bias))
             ops.wgrad_bf16(dpre, x1, g(lyr.linear1.weight), db=g(lyr.linear1.bias))
         # dff (possibly the old dh2) and x1 are not written again below: dh2 is a new tensor
-        _wgrad_side(_ffn_wgrads, dff, f1b, dpre, x1)
+        _wgrad_side(_ffn_wgrads, *[t for t in (dff, f1b, dpre, x1, f1[1]) if t is not None])
     else:
         ops.linear_bwd_weight(dff, f1, g(lyr.linear2.weight), db=g(lyr.linear2.bias))
         # f1 holds relu(.) after dropout: (f1 > 0) == kept & positive, kept scale 1/(1-p)

@@ -111,33 +111,50 @@ def ffn_fwd_bf16(x, W1, b1, W2, b2, gamma, beta, eps, p, key, site1, site2):
     return h, y, mean, rstd, mask
 
 
-def ffn_bwd_bf16(x, W1, b1, W2, mask, dff, dres, p, dx=None):
-    """-> (dx = dres + dPre1 W1, f1 bf16 [M,F], dPre1 bf16 [M,F])."""
+def ffn_bwd_bf16(x, W1, b1, W2, mask, dff, dres, p, dx=None, acts=True):
+    """-> (dx = dres + dPre1 W1, f1 bf16 [M,F], dPre1 bf16 [M,F]); acts=False: f1 / dPre1 are
+    not written (None; the weight gradients by ffn_wgrad_bf16)."""
     M, F = x.shape[0], W1.shape[0]
     dev = x.device
     if dx is None:
         dx = torch.empty_like(dres)
-    f1 = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
-    dpre = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    f1 = torch.empty(M, F, device=dev, dtype=torch.bfloat16) if acts else None
+    dpre = torch.empty(M, F, device=dev, dtype=torch.bfloat16) if acts else None
     call('rs_ffn_bwd_bf16', M, F, P(x), P(W1), P(b1), P(W2), P(mask), P(dff), P(dres), P(dx), P(f1), P(dpre),
          float(p), stream())
     return dx, f1, dpre
 
 
 def ffn_bwd_ln_bf16(x, W1, b1, W2, mask, dff, dres, h1, gamma1, mean1, rstd1, dgamma1, dbeta1, p,
-                    key, site):
-    """ffn_bwd_bf16 with norm1's backward fused: -> (dh1, dsa or None, f1 bf16, dPre1 bf16)."""
+                    key, site, acts=True):
+    """ffn_bwd_bf16 with norm1's backward fused: -> (dh1, dsa or None, f1 bf16, dPre1 bf16)
+    (acts=False: f1 / dPre1 None, as in ffn_bwd_bf16)."""
     M, F = x.shape[0], W1.shape[0]
     dev = x.device
     dh1 = torch.empty_like(dres)
     dsa = torch.empty_like(dres) if p > 0 else None
-    f1 = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
-    dpre = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    f1 = torch.empty(M, F, device=dev, dtype=torch.bfloat16) if acts else None
+    dpre = torch.empty(M, F, device=dev, dtype=torch.bfloat16) if acts else None
     w = ws(_hip.lib().rs_ffn_bwd_ln_ws_bytes(M, F), dev)
     call('rs_ffn_bwd_ln_bf16', M, F, P(x), P(W1), P(b1), P(W2), P(mask), P(dff), P(dres), P(h1), P(gamma1),
          P(mean1), P(rstd1), P(dh1), P(dsa), P(dgamma1), P(dbeta1), P(f1), P(dpre), float(p), P(key), site,
          P(w), stream())
     return dh1, dsa, f1, dpre
+
+
+def ffn_wgrad_bf16(x, W1, b1, W2, mask, dff, p, dW1, db1, dW2, db2):
+    """dW1 += dPre1^T x, db1 += colsum(dPre1), dW2 += dff^T f1, db2 += colsum(dff), f1 / dPre1
+    recomputed on chip (csrc/ffn.hip rs_ffn_wgrad_bf16)."""
+    M, F = x.shape[0], W1.shape[0]
+    w = ws(_hip.lib().rs_ffn_wgrad_ws_bytes(M, F), x.device)
+    call('rs_ffn_wgrad_bf16', M, F, P(x), P(W1), P(b1), P(W2), P(mask), P(dff), float(p), P(dW1), P(db1),
+         P(dW2), P(db2), P(w), stream())
+
+
+def ffn_wgrad_fused() -> bool:
+    """RSYS_FFN_WGRAD=split keeps the activation round trip (rs_ffn_bwd_bf16 writes f1 / dPre1,
+    two rs_wgrad_bf16 passes read them) for A/B measurements."""
+    return os.environ.get('RSYS_FFN_WGRAD', 'fused') != 'split'
 
 
 def wgrad_bf16(dy, x, dW, *, db=None, beta=1.0):

@@ -197,6 +197,37 @@ def test_fused_ffn_matches_unfused(p, bf16_mode):
     assert torch.allclose(db1, db1r, atol=1e-2 * db1r.abs().max().item())
 
 
+@pytest.mark.parametrize('p,M', [(0.0, 40960), (0.15, 40960), (0.15, 4112), (0.0, 16), (0.1, 204800)])
+def test_fused_ffn_wgrad(p, M, bf16_mode):
+    """rs_ffn_wgrad_bf16 (f1 / dPre1 recomputed on chip) against the split pair it replaces:
+    rs_ffn_bwd_bf16 writing f1 / dPre1, then two rs_wgrad_bf16 passes over them. Same bf16
+    operands, so the weight gradients agree to fp32 summation order; db2 is the fp32 colsum of
+    dff, db1 the colsum of the bf16 dPre1 in both. The backward without the activations gives
+    the same dx bits. Deterministic; accumulates into the gradients."""
+    x = rnd(M, 64, seed=7)
+    W1, b1, W2, b2, g, be = _ffn_weights()
+    key = torch.tensor([99, 3], dtype=torch.int64, device=DEV)
+    _, _, _, _, mask = ops.ffn_fwd_bf16(x, W1, b1, W2, b2, g, be, 1e-5, p, key, 18, 19)
+    dff, dres = rnd(M, 64, seed=8), rnd(M, 64, seed=9)
+    dx, f1b, dpre = ops.ffn_bwd_bf16(x, W1, b1, W2, mask, dff, dres, p)
+    dx2, f1n, dpn = ops.ffn_bwd_bf16(x, W1, b1, W2, mask, dff, dres, p, acts=False)
+    assert f1n is None and dpn is None and torch.equal(dx, dx2)
+    init = [rnd(*t.shape, seed=30 + i) for i, t in enumerate((W1, b1, W2, b2))]
+    ref = [t.clone() for t in init]
+    ops.wgrad_bf16(dff, f1b, ref[2], db=ref[3])
+    ops.wgrad_bf16(dpre, x, ref[0], db=ref[1])
+    outs = []
+    for _ in range(2):
+        got = [t.clone() for t in init]
+        ops.ffn_wgrad_bf16(x, W1, b1, W2, mask, dff, p, *got)
+        outs.append(got)
+    for a, b_ in zip(outs[0], outs[1]):
+        assert torch.equal(a, b_)
+    for name, a, r, i in zip(('dW1', 'db1', 'dW2', 'db2'), outs[0], ref, init):
+        sc = (r - i).abs().max().item()
+        assert (a - r).abs().max().item() <= 1e-5 * sc + 1e-6, (name, (a - r).abs().max().item(), sc)
+
+
 @pytest.mark.parametrize('p,M', [(0.0, 40960), (0.1, 40960), (0.1, 4112)])
 def test_fused_ffn_ln_backward(p, M, bf16_mode):
     """rs_ffn_bwd_ln_bf16 (the FFN backward with norm1's backward in its epilogue) against the

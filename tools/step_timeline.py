@@ -1,7 +1,9 @@
 """One training step's kernel timeline from a rocprofv3 --kernel-trace run: the kernels between
 the last two launches of a marker kernel (default: the loss tile kernel), with start offset,
 duration, gap to the previous kernel's end, stream and grid. Usage:
-python tools/step_timeline.py gpurun_out/<dir>/trace [marker]"""
+python tools/step_timeline.py gpurun_out/<dir>/trace [marker] [must_contain]
+(must_contain: pick the last step that launches a kernel with this substring, e.g. attn for the
+C2 steps of a bench run that also runs C3)"""
 import csv
 import os
 import sys
@@ -12,11 +14,17 @@ def short(n):
     return n.split('(')[0][:60]
 
 
-def main(path, marker='ce_tile_kernel'):
+def main(path, marker='ce_tile_kernel', must=None):
     rows = list(csv.DictReader(open(os.path.join(path, 'run_kernel_trace.csv'))))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
     idx = [i for i, r in enumerate(rows) if marker in r['Kernel_Name']]
-    a, b = idx[-2], idx[-1]
+    pairs = list(zip(idx[:-1], idx[1:]))
+    if must:
+        pairs = [(x, y) for x, y in pairs if any(must in r['Kernel_Name'] for r in rows[x:y])]
+        # the shortest such span: the last one may run into the next workload's setup
+        pairs.sort(key=lambda p: int(rows[p[1]]['Start_Timestamp']) - int(rows[p[0]]['Start_Timestamp']))
+        pairs = pairs[:1]
+    a, b = pairs[-1]
     t0 = int(rows[a]['Start_Timestamp'])
     end = t0
     busy = {}
