@@ -23,6 +23,10 @@ constexpr int kMaxSeg = 24;  // segments travel by value in the kernel arguments
 constexpr int64_t kSmallTableBytes = 48 * 1024;
 
 constexpr int kBagBatch = 16;              // bag ids (and rows) loaded per batch
+// forward: a table of at most this size whose workgroup reads at least as many row bytes as the
+// table holds is staged whole into LDS first (every row of such a table is hot: the genre / age /
+// occupation tables are read thousands of times per step), and its lookups are served from LDS
+constexpr int kStageBytes = 16 * 1024;
 
 struct SegLaunch {
   rs_feature_seg_t segs[kMaxSeg];
@@ -41,6 +45,8 @@ struct SegLaunch {
   int sblocks[kMaxSeg];
   int small_lds;        // bytes of dynamic LDS for the small-table kernel
   int split[kMaxSeg];   // pooled bags: row groups sharing one bag (positions split S ways)
+  int stage[kMaxSeg];   // fwd: bytes of the table staged into LDS (0: read from HBM / L2)
+  int stage_lds;        // fwd: dynamic LDS bytes (the largest staged table)
 };
 static_assert(sizeof(SegLaunch) <= 4096, "SegLaunch must fit the kernel-argument segment");
 
@@ -183,9 +189,16 @@ __device__ void gather_pool_split(const SegLaunch& a, const rs_feature_seg_t& sg
 }
 
 __global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
+  extern __shared__ float4 stage_lds[];
   const int s = find_seg(a, blockIdx.x);
-  const rs_feature_seg_t& sg = a.segs[s];
+  rs_feature_seg_t sg = a.segs[s];
   const int lb = blockIdx.x - a.block_start[s];
+  if (a.stage[s]) {  // uniform per workgroup: the whole table into LDS, then read it from there
+    const float4* src = reinterpret_cast<const float4*>(sg.table);
+    for (int i = threadIdx.x; i < a.stage[s] / 16; i += 256) stage_lds[i] = src[i];
+    __syncthreads();
+    sg.table = reinterpret_cast<const float*>(stage_lds);
+  }
   if (a.split[s] > 1) {  // uniform per workgroup: the barrier inside is reached by every thread
     if (a.vec[s]) gather_pool_split<true>(a, sg, s, lb);
     else gather_pool_split<false>(a, sg, s, lb);
@@ -392,6 +405,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
          const float* out_ptr_for_align, bool bwd = false) {
   RS_CHECK_ARG(nseg >= 1 && nseg <= kMaxSeg, "gather: nseg %d out of [1,%d]", nseg, kMaxSeg);
   int blocks = 0;
+  a.stage_lds = 0;
   for (int s = 0; s < nseg; ++s) {
     const rs_feature_seg_t& g = segs_host[s];
     RS_CHECK_ARG(g.dim >= 1 && g.dim <= 1024, "gather: seg %d dim %d", s, g.dim);
@@ -418,6 +432,15 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     }
     a.split[s] = S;
     a.rpb[s] = 256 / (C * S);
+    a.stage[s] = 0;
+    if (!bwd && table_kind && vec) {
+      const int64_t tbytes = g.vocab * g.dim * 4;
+      const int64_t read = (int64_t)a.rpb[s] * (g.kind == RS_SEG_POOL ? g.bag : 1) * g.dim * 4;
+      if (tbytes <= kStageBytes && tbytes <= read && !getenv_flag("RSYS_NO_LDS_STAGE")) {
+        a.stage[s] = (int)tbytes;
+        if (a.stage[s] > a.stage_lds) a.stage_lds = a.stage[s];
+      }
+    }
     a.block_start[s] = blocks;
     if (!a.small[s]) blocks += cdiv(rows, a.rpb[s]);
   }
@@ -482,7 +505,7 @@ extern "C" int rs_gather_fwd(const rs_feature_seg_t* segs, int nseg, int rows, f
   RS_RET_IF(plan(a, segs_host, nseg, rows, ldo, out));
   for (int i = 0; i < nseg; ++i) a.segs[i] = segs[i];
   a.out = out; a.dout = nullptr; a.err = err_flag;
-  gather_fwd_kernel<<<a.block_start[nseg], 256, 0, as_stream(stream)>>>(a);
+  gather_fwd_kernel<<<a.block_start[nseg], 256, a.stage_lds, as_stream(stream)>>>(a);
   RS_CHECK_LAUNCH("rs_gather_fwd");
   return 0;
 }

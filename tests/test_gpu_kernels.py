@@ -95,6 +95,44 @@ def test_colsum_deterministic():
     assert torch.equal(o1, o2)
 
 
+def test_gather_small_tables_staged_in_lds(monkeypatch):
+    """Tables of at most 16 KB are staged whole into LDS by the forward gather (gather.hip
+    kStageBytes); the result is the same bits as reading them from HBM (RSYS_NO_LDS_STAGE=1),
+    for sparse, pooled mean / sum / max and split bags; out-of-range ids still raise the flag."""
+    B = 4096
+    cases = [(30, 8, 6, 'mean'), (25, 8, 1, None), (3, 4, 1, None), (152, 8, 1, None), (30, 8, 6, 'max'),
+             (500, 8, 40, 'sum'), (1000, 4, 12, 'mean')]
+    for V, D, Lb, mode in cases:
+        t = rnd(V, D, seed=V + D)
+        ids = torch.randint(0, V, (B, Lb), device=DEV)
+        ids[::7, 0] = 0
+        kind = _hip.RS_SEG_SPARSE if mode is None else _hip.RS_SEG_POOL
+        seg = dict(kind=kind, dim=D, out_col=4, vocab=V, idx_stride=Lb, idx=ids.data_ptr(), table=t.data_ptr())
+        if mode is not None:
+            seg.update(pool_mode=_hip.RS_POOL[mode], bag=Lb)
+        outs = []
+        for off in ('', '1'):
+            monkeypatch.setenv('RSYS_NO_LDS_STAGE', off)
+            out = torch.zeros(B, D + 8, device=DEV)
+            err = torch.zeros(1, dtype=torch.int32, device=DEV)
+            ops.gather_fwd([_seg(**seg)], B, out, err)
+            assert err.item() == 0
+            outs.append(out)
+        assert torch.equal(outs[0], outs[1]), (V, D, Lb, mode)
+        ref = t[ids]
+        ref = ref[:, 0] if mode is None else {'mean': ref.mean(1), 'sum': ref.sum(1), 'max': ref.max(1)[0]}[mode]
+        assert torch.allclose(outs[0][:, 4:4 + D], ref, atol=1e-5), (V, D, Lb, mode)
+    monkeypatch.setenv('RSYS_NO_LDS_STAGE', '')
+    bad = torch.randint(0, 30, (B, 6), device=DEV)
+    bad[5, 2] = 31
+    out = torch.empty(B, 8, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    tb = rnd(30, 8)
+    ops.gather_fwd([_seg(kind=_hip.RS_SEG_POOL, dim=8, out_col=0, pool_mode=0, bag=6, vocab=30, idx_stride=6,
+                         idx=bad.data_ptr(), table=tb.data_ptr())], B, out, err)
+    assert err.item() == 1
+
+
 def test_gather_bit_exact_all_kinds():
     B = 257
     V1, D1 = 1000, 64
