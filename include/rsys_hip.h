@@ -510,6 +510,13 @@ int rs_pack_rows(const float* src, int64_t ld, int64_t rows, int D, float* dst, 
 int rs_rng_next(int64_t* state, int64_t* key, void* stream);
 int rs_dropout_fwd(float* x, int64_t n, int N, const float* aux, int ld_aux, int aux_mod, float p,
                    const int64_t* key, int site, void* stream);
+/* Backward of SequenceFeatureProcessor's drop_b(drop_a(.) + pos[l]) (SequenceFeatureProcessor.py:
+ * 77-83) in one pass over dx [rows, N = L*d]: dx <- dx * mask_b * mask_a, pos_grad[n] += sum over
+ * rows of dx * mask_b (deterministic). Replaces rs_dropout_bwd + rs_colsum + rs_dropout_bwd.
+ * ws: rs_seq_input_dropout_bwd_ws_bytes. */
+int64_t rs_seq_input_dropout_bwd_ws_bytes(int rows, int N);
+int rs_seq_input_dropout_bwd(float* dx, int rows, int N, float p, const int64_t* key, int site_a,
+                             int site_b, float* pos_grad, float* ws, void* stream);
 int rs_dropout_bwd(float* dx, int64_t n, float p, const int64_t* key, int site, void* stream);
 
 /* ---------------------------------------------------------------- reductions */

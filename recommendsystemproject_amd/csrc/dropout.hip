@@ -38,6 +38,60 @@ __global__ void dropout_bwd_kernel(float* __restrict__ dx, int64_t n, float p,
     dx[i] *= keep_mult(k, (uint64_t)i);
 }
 
+// Backward of the sequence input's two dropouts around the positional-embedding add
+// (SequenceFeatureProcessor.py:77-83: x = drop_b(drop_a(cat W^T + b) + pos[l])) in one pass over
+// dx [rows, N] (N = L * d): v = dx * mask_b, pos_grad[n] += sum over rows of v (fixed-order
+// per-workgroup partials), dx = v * mask_a. The three-pass form (rs_dropout_bwd, rs_colsum,
+// rs_dropout_bwd) read and wrote dx twice more. Element i = row * N + n draws exactly as
+// rs_dropout_* (keep4: two pair hashes per 4 elements).
+constexpr int kSeqDropCols = 4;  // float4 groups per thread and row (N <= 4 * 4 * 256)
+
+__global__ __launch_bounds__(256) void seq_input_dropout_bwd_kernel(float* __restrict__ dx, int rows, int N,
+                                                                    int rows_per_block, float p,
+                                                                    const int64_t* __restrict__ key,
+                                                                    int site_a, int site_b,
+                                                                    float* __restrict__ ws) {
+  const DropKey ka = make_key(key, site_a, p), kb = make_key(key, site_b, p);
+  const int G4 = N / 4;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  float4 acc[kSeqDropCols];
+#pragma unroll
+  for (int u = 0; u < kSeqDropCols; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int row = r0; row < r1; ++row) {
+    float4 v[kSeqDropCols];
+#pragma unroll
+    for (int u = 0; u < kSeqDropCols; ++u) {  // loads first, then the hashes
+      const int g = threadIdx.x + 256 * u;
+      if (g < G4) v[u] = *reinterpret_cast<const float4*>(dx + (int64_t)row * N + 4 * g);
+    }
+#pragma unroll
+    for (int u = 0; u < kSeqDropCols; ++u) {
+      const int g = threadIdx.x + 256 * u;
+      if (g >= G4) continue;
+      const uint64_t i0 = (uint64_t)row * N + 4 * g;
+      float mb[4], ma[4];
+      keep4(kb, i0, mb);
+      keep4(ka, i0, ma);
+      float4 t = v[u];
+      t.x *= mb[0]; t.y *= mb[1]; t.z *= mb[2]; t.w *= mb[3];
+      acc[u].x += t.x; acc[u].y += t.y; acc[u].z += t.z; acc[u].w += t.w;
+      t.x *= ma[0]; t.y *= ma[1]; t.z *= ma[2]; t.w *= ma[3];
+      *reinterpret_cast<float4*>(dx + (int64_t)row * N + 4 * g) = t;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kSeqDropCols; ++u) {
+    const int g = threadIdx.x + 256 * u;
+    if (g < G4) *reinterpret_cast<float4*>(ws + (int64_t)blockIdx.x * N + 4 * g) = acc[u];
+  }
+}
+
+int seq_drop_blocks(int rows) {
+  int b = cdiv(rows, 8);  // >= 8 rows per workgroup
+  return b > 512 ? 512 : (b < 1 ? 1 : b);
+}
+
 int grid_for(int64_t n) {
   int64_t b = (n + 255) / 256;
   if (b > 8192) b = 8192;
@@ -65,6 +119,24 @@ extern "C" int rs_dropout_fwd(float* x, int64_t n, int N, const float* aux, int 
                                                                   aux_mod, p, key, site);
   RS_CHECK_LAUNCH("rs_dropout_fwd");
   return 0;
+}
+
+extern "C" int64_t rs_seq_input_dropout_bwd_ws_bytes(int rows, int N) {
+  return (int64_t)seq_drop_blocks(rows) * N * (int64_t)sizeof(float);
+}
+
+extern "C" int rs_seq_input_dropout_bwd(float* dx, int rows, int N, float p, const int64_t* key, int site_a,
+                                        int site_b, float* pos_grad, float* ws, void* stream) {
+  RS_CHECK_ARG(dx && key && pos_grad && ws && rows >= 0 && N > 0 && N % 4 == 0 &&
+                   N <= 4 * kSeqDropCols * 256 && p >= 0.f && p < 1.f && aligned16(dx),
+               "rs_seq_input_dropout_bwd: bad args (N=%d)", N);
+  if (rows == 0) return 0;
+  const int nb = seq_drop_blocks(rows);
+  const int rpb = cdiv(rows, nb);
+  hipStream_t st = as_stream(stream);
+  seq_input_dropout_bwd_kernel<<<cdiv(rows, rpb), 256, 0, st>>>(dx, rows, N, rpb, p, key, site_a, site_b, ws);
+  RS_CHECK_LAUNCH("rs_seq_input_dropout_bwd");
+  return partials_reduce(ws, cdiv(rows, rpb), N, 1.f, 1.f, pos_grad, st);
 }
 
 extern "C" int rs_dropout_bwd(float* dx, int64_t n, float p, const int64_t* key, int site,

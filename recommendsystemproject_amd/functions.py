@@ -146,12 +146,16 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key):
     """Backward of seq_input_fwd; dx [B*L, d] is consumed (modified in place)."""
     segs, tables, cat, _, calls = saved
     d = proc.target_dim
-    if p > 0:
-        ops.dropout_bwd(dx, p, key, 1)
     pos_g = grad_of(proc.pos_emb.weight)
-    ops.colsum(dx, pos_g, M=B, N=L * d, ldx=L * d)  # d pos_emb[l] = sum_b dx[b, l]
-    if p > 0:
-        ops.dropout_bwd(dx, p, key, 0)
+    if p > 0 and (L * d) % 4 == 0 and L * d <= 4096:
+        # drop_b backward, d pos_emb[l] = sum_b dx[b, l], drop_a backward: one pass
+        ops.seq_input_dropout_bwd(dx, pos_g, B, L * d, p, key, 0, 1)
+    else:
+        if p > 0:
+            ops.dropout_bwd(dx, p, key, 1)
+        ops.colsum(dx, pos_g, M=B, N=L * d, ldx=L * d)  # d pos_emb[l] = sum_b dx[b, l]
+        if p > 0:
+            ops.dropout_bwd(dx, p, key, 0)
     lin = proc.feature_projection[0]
     # dx is final here (the dropout backward above ran in place before this point)
     _wgrad_side(lambda: ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias)), dx, cat)

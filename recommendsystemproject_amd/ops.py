@@ -306,6 +306,14 @@ def dropout_fwd(x, p, key, site, aux=None, aux_mod=0):
     return x
 
 
+def seq_input_dropout_bwd(dx, pos_grad, rows, N, p, key, site_a, site_b):
+    """dx [rows, N] <- dx * mask_b * mask_a; pos_grad[:N] += colsum(dx * mask_b) (one pass)."""
+    w = ws(_hip.lib().rs_seq_input_dropout_bwd_ws_bytes(rows, N), dx.device)
+    call('rs_seq_input_dropout_bwd', P(dx), rows, N, float(p), P(key), site_a, site_b, P(pos_grad), P(w),
+         stream())
+    return dx
+
+
 def dropout_bwd(dx, p, key, site):
     call('rs_dropout_bwd', P(dx), dx.numel(), float(p), P(key), site, stream())
     return dx

@@ -534,3 +534,25 @@ def test_clip_coefficient():
     tn = (0.5 * g).norm().item()
     assert abs(norm.item() - tn) < 1e-5 * tn
     assert abs(coef.item() - min(1.0, 1.0 / (tn + 1e-6))) < 1e-6
+
+
+@pytest.mark.parametrize('B,L,d,p', [(4096, 50, 64, 0.15), (37, 7, 64, 0.3), (300, 20, 16, 0.5)])
+def test_seq_input_dropout_bwd_fused(B, L, d, p):
+    """rs_seq_input_dropout_bwd (one pass: drop_b backward, positional-embedding colsum, drop_a
+    backward) against rs_dropout_bwd + rs_colsum + rs_dropout_bwd: dx bit-exact (same draws,
+    same products), the colsum to fp32 summation order; accumulates into pos_grad."""
+    key = torch.tensor([77, 12], dtype=torch.int64, device=DEV)
+    dx = rnd(B * L, d, seed=3)
+    pos0 = rnd(L + 5, d, seed=4)
+    ref, pr = dx.clone(), pos0.clone()
+    ops.dropout_bwd(ref, p, key, 1)
+    ops.colsum(ref, pr, M=B, N=L * d, ldx=L * d)
+    ops.dropout_bwd(ref, p, key, 0)
+    got, pg = dx.clone(), pos0.clone()
+    ops.seq_input_dropout_bwd(got, pg, B, L * d, p, key, 0, 1)
+    assert torch.equal(got, ref)
+    assert torch.equal(pg[L:], pos0[L:])
+    assert torch.allclose(pg, pr, atol=1e-4 * max(1.0, B / 1000), rtol=1e-5)
+    g2, p2 = dx.clone(), pos0.clone()
+    ops.seq_input_dropout_bwd(g2, p2, B, L * d, p, key, 0, 1)
+    assert torch.equal(p2, pg)
