@@ -92,12 +92,14 @@ def test_tower_chain_fp32_matches_per_op(G, Bg, C0, hidden, out, p):
     # Backward: the ReLU/dropout mask is recomputed from each path's own fp32 z, and a decision at
     # |BN output| ~ 1e-7 can differ between the two summation orders (~1 of 1.5M elements at
     # B = 4096): each such flip moves one entry of the masked gradient by O(|dh|), ~1e-4 of the
-    # gradient norm downstream. Index or statistics errors show up at O(1).
-    assert _rel(dxa, dxb) < 1e-3
+    # gradient norm downstream. Index or statistics errors show up at O(1). The flip count depends
+    # on the dropout masks, whose key differs with the number of models built before in the same
+    # process (rng.py): 1.5e-3 was seen inside the full suite, so the bound is 5e-3.
+    assert _rel(dxa, dxb) < 5e-3
     for n in gb:
         if n in _bn_invariant(a):
             continue  # exact gradient 0 (shifts removed by the BatchNorm after them): fp32 noise
-        assert _rel(ga[n], gb[n]) < 1e-3, n
+        assert _rel(ga[n], gb[n]) < 5e-3, n
     for n in bb:
         if bb[n].dtype.is_floating_point:
             assert _rel(ba[n], bb[n]) < 1e-6, n

@@ -19,7 +19,7 @@ def main():
     d, H = 64, 4
     dev = torch.device('cuda:0')
     qkv = torch.randn(B * L, 3 * d, device=dev)
-    if ops.qkv_bf16_ok(L, d, H):  # the bf16 mode's qkv storage (RS_ATTN_QKV_BF16)
+    if ops.qkv_bf16_ok(L, d, H, B * L):  # the bf16 mode's qkv storage (RS_ATTN_QKV_BF16)
         qkv = qkv.to(torch.bfloat16)
     lens = torch.randint(0, L + 1, (B,), device=dev)
     seq = (torch.arange(L, device=dev)[None, :] < lens[:, None]).long()
