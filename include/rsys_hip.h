@@ -496,6 +496,11 @@ int64_t rs_segsum_ws_bytes(int64_t n, int D);
 int rs_segsum(const uint32_t* keys, const uint32_t* vals, int64_t n, int bag, int mode, int64_t pad,
               const float* dout, int64_t ldo, int D, float* grad, int accumulate, void* ws,
               void* stream);
+/* Row-sharded large tables under data parallelism (dist.py): rank r of W owns rows id % W == r
+ * at local row id / W. Maps all-gathered int32 ids to int64 local rows (-1: owned elsewhere);
+ * out-of-range ids set *err_flag (nullable) as rs_gather_fwd does (GenericTower.py:184-196). */
+int rs_shard_map_ids(const int32_t* ids, int64_t n, int64_t vocab, int world, int rank, int64_t* local,
+                     int* err_flag, void* stream);
 int rs_pack_ids(const void* ids, int id_bytes, int64_t rows, int bag, int64_t row_stride,
                 int32_t* out, void* stream);
 int rs_pack_rows(const float* src, int64_t ld, int64_t rows, int D, float* dst, void* stream);

@@ -1106,6 +1106,33 @@ __global__ void pack_rows_kernel(const float* __restrict__ src, int64_t ld, int6
 }  // namespace
 }  // namespace rs
 
+// Row-sharded tables (flat.py / dist.py): rank `rank` of `world` owns the rows id % world ==
+// rank, stored at local row id / world. Maps the all-gathered int32 ids of a lookup call to local
+// rows (int64, -1 where another rank owns the row: the gather reads it as 0 and the sort puts it
+// last); out-of-range ids raise the error flag as the gather would.
+__global__ void shard_map_kernel(const int32_t* __restrict__ ids, int64_t n, int64_t V, int world, int rank,
+                                 int64_t* __restrict__ local, int* err) {
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t id = ids[i];
+    const bool ok = id >= 0 && id < V;
+    bad |= !ok;
+    local[i] = ok && id % world == rank ? id / world : -1;
+  }
+  if (bad && err) atomicOr(err, 1);
+}
+
+extern "C" int rs_shard_map_ids(const int32_t* ids, int64_t n, int64_t vocab, int world, int rank,
+                                int64_t* local, int* err_flag, void* stream) {
+  RS_CHECK_ARG(ids && local && n >= 0 && vocab >= 1 && world >= 1 && rank >= 0 && rank < world,
+               "rs_shard_map_ids: bad args");
+  if (n == 0) return 0;
+  shard_map_kernel<<<std::min<int64_t>(cdiv(n, 256), 8192), 256, 0, as_stream(stream)>>>(ids, n, vocab, world,
+                                                                                            rank, local, err_flag);
+  RS_CHECK_LAUNCH("rs_shard_map_ids");
+  return 0;
+}
+
 extern "C" int rs_pack_ids(const void* ids, int id_bytes, int64_t rows, int bag, int64_t row_stride,
                            int32_t* out, void* stream) {
   RS_CHECK_ARG(ids && out && rows >= 0 && bag >= 1 && row_stride >= bag &&

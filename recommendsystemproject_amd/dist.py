@@ -14,6 +14,12 @@ per rank), and every rank sorts the gathered ids and runs the deterministic segm
 them (csrc/lookup.hip). All ranks therefore hold bitwise-identical gradient rows and step the
 same rows in the same order: the clip norm and Adam agree bitwise, with no host sync and no
 count exchange.
+
+Row-sharded tables (RSYS_SHARD_ROWS, flat.py): rank r holds only the rows id % W == r. Their
+forward all-gathers the call's ids and reduce-scatters per-rank partial bags
+(LazyTable.shard_lookup); here the kept output gradient rows are all-gathered and every rank
+segment-sums the contributions to the rows it owns (the call's keys are already the union's,
+mapped to local rows). No table bytes ever cross the link, only ids and [rows, D] bag rows.
 """
 from __future__ import annotations
 
@@ -49,7 +55,8 @@ def broadcast_model(model: torch.nn.Module, src: int = 0):
     if not is_active():
         return
     f = ensure_flat(model)
-    dist.broadcast(f.data, src)
+    # the row-sharded tables (the end of the buffer) differ by rank by construction
+    dist.broadcast(f.data[:f.replicated_numel], src)
     for b in model.buffers():
         if b.dtype in (torch.float32, torch.int64) and b.numel() > 0:
             dist.broadcast(b, src)
@@ -112,6 +119,35 @@ def _all_gather(out, inp):
         dist.all_gather(list(out.chunk(dist.get_world_size())), inp)
 
 
+all_gather_into = _all_gather
+
+
+def reduce_scatter_sum(out, inp):
+    """out = sum over ranks of inp's block `rank` (inp: world blocks of out's size). RCCL's
+    reduce-scatter; other backends (gloo sharing one GPU in tests): an all-reduce of inp and the
+    block."""
+    if dist.get_backend() == 'nccl':
+        dist.reduce_scatter_tensor(out, inp)
+        return
+    dist.all_reduce(inp)
+    r = dist.get_rank()
+    n = out.numel()
+    out.view(-1).copy_(inp.view(-1)[r * n:(r + 1) * n])
+
+
+def _exchange_sharded(t, bufs, world, dev):
+    """Row-sharded table: all-gather each call's output gradient rows; the call's sorted keys
+    are the union's local rows, so the segment sum lands on the rows this rank owns."""
+    calls = [c for c in t.calls if c.dseg is not None]
+    for i, c in enumerate(calls):
+        all_g = bufs.get(('shard_g', i), (world * c.local_rows, t.D), torch.float32, dev)
+        _all_gather(all_g, c.dseg)
+        c.dseg = None
+        c.keep = (c.keep, all_g)
+        t.segsum(c, all_g.data_ptr(), t.D, accumulate=len(calls) > 1)
+    t.exchanged = calls
+
+
 def exchange_lazy_grads(f):
     """Bag-gradient exchange of every lazy table of flat buffer f (see module doc)."""
     world = dist.get_world_size()
@@ -122,6 +158,9 @@ def exchange_lazy_grads(f):
         bufs = getattr(t, '_dp_bufs', None)
         if bufs is None:
             bufs = t._dp_bufs = _ExchangeBuffers()
+        if t.shard is not None:
+            _exchange_sharded(t, bufs, world, dev)
+            continue
         union = []
         for i, c in enumerate(t.calls):
             if c.mode < 0:

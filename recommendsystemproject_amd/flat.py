@@ -14,6 +14,16 @@ parameter and trained by lazy-exact Adam (csrc/sparse.hip, trap T16): each one g
 sweep [0, dense_numel); the tables are touched row-by-row. State (weights, exp_avg, exp_avg_sq) stays
 bitwise what dense Adam would produce; rows are brought current before every read (forward
 gather, state_dict, load_state_dict).
+
+Row sharding (data parallel only): with RSYS_SHARD_ROWS=N > 0 and a process group
+of W > 1 ranks, a large table of at least N rows is split by rows, rank r owning rows
+id % W == r at local row id / W (its weight, exp_avg and exp_avg_sq: 1/W of the memory each;
+placed last in the flat buffer, never broadcast or all-reduced). A lookup all-gathers the call's
+ids, each rank catches up and sums the rows it owns into per-requester partial bags, and a
+reduce-scatter hands every rank the pooled rows of its own batch (LazyTable.shard_lookup). The
+backward keeps the call's output gradient; dist.exchange_lazy_grads all-gathers it and every
+rank segment-sums the contributions to the rows it owns. state_dict() assembles the full table
+(a collective: every rank calls it); load_state_dict takes the owned rows of a full table.
 """
 from __future__ import annotations
 
@@ -45,7 +55,7 @@ class LookupCall:
     is not reused before that join."""
 
     __slots__ = ('_keys', '_vals', 'ws', 'ready', 'n', 'rows', 'bag', 'pad', 'mode', 'ids_ptr',
-                 'id_bytes', 'row_stride', 'keep', 'dseg')
+                 'id_bytes', 'row_stride', 'keep', 'dseg', 'local_rows')
 
     def __init__(self, keys, vals, n, rows, bag, pad, mode, ids_ptr, id_bytes, row_stride, keep,
                  ws=None, ready=None):
@@ -54,6 +64,7 @@ class LookupCall:
         self.ids_ptr, self.id_bytes, self.row_stride, self.keep = ids_ptr, id_bytes, row_stride, keep
         self.ws, self.ready = ws, ready
         self.dseg = None
+        self.local_rows = rows  # row-sharded call: the calling rank's rows (rows = world x local)
 
     def sync(self):
         if self.ready is not None:
@@ -113,9 +124,11 @@ class LazyTable:
                  (rs_sorted_owner). The calls are then dropped.
     The gradient rows of a large table are zero except the rows of this step's calls."""
 
-    def __init__(self, flat, index, param, offset):
+    def __init__(self, flat, index, param, offset, shard=None, vocab=None):
         self.flat, self.index, self.param, self.offset = flat, index, param, offset
-        self.V, self.D = int(param.shape[0]), int(param.shape[1])
+        self.V, self.D = int(param.shape[0]), int(param.shape[1])  # local rows when sharded
+        self.shard = shard  # (world, rank) of a row-sharded table, else None
+        self.V_full = int(vocab) if vocab is not None else self.V
         dev = param.device
         self.last = torch.zeros(self.V, dtype=torch.int32, device=dev)
         self.owner = None   # [V] lowest call index per row; allocated for multi-call steps
@@ -169,6 +182,57 @@ class LazyTable:
                       *hyper)
         return c
 
+    def shard_lookup(self, seg, rows, record=True, err_ptr=None):
+        """Forward of a lookup of a row-sharded table (module doc): -> (LookupCall or None, the
+        call's pooled rows [rows, D] for this rank). seg: the rs_feature_seg_t of the lookup
+        (sparse, or pooled mean / sum)."""
+        from . import ops
+        from .dist import all_gather_into, reduce_scatter_sum
+        W, r = self.shard
+        dev = self.param.device
+        pooled = seg.kind == _hip.RS_SEG_POOL
+        bag = seg.bag if pooled else 1
+        if pooled and seg.pool_mode not in (_hip.RS_POOL['mean'], _hip.RS_POOL['sum']):
+            raise NotImplementedError('row-sharded tables: max pooling is not supported')
+        mode = SEG_ONE if not pooled else (SEG_MEAN if seg.pool_mode == _hip.RS_POOL['mean'] else SEG_SUM)
+        n = rows * bag
+        ids32 = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        if n:
+            _hip.call('rs_pack_ids', seg.idx, 8, rows, bag, seg.idx_stride, ids32.data_ptr(), _stream())
+        all32 = torch.empty(W * ids32.numel(), dtype=torch.int32, device=dev)
+        all_gather_into(all32, ids32)
+        if n == 0:
+            return None, torch.zeros(rows, self.D, device=dev)
+        all32 = all32.view(W, -1)[:, :n].contiguous()
+        local = torch.empty(W * n, dtype=torch.int64, device=dev)
+        _hip.call('rs_shard_map_ids', all32.data_ptr(), W * n, self.V_full, W, r, local.data_ptr(), err_ptr,
+                  _stream())
+        opt = self.flat.lazy_opt
+        if opt is not None:
+            _hip.call('rs_lookup_catchup', local.data_ptr(), 8, W * rows, bag, bag, self.V, self.D,
+                      self.ptr(self.flat.data), self.ptr(opt['m']), self.ptr(opt['v']), self.last.data_ptr(),
+                      opt['step_dev'].data_ptr(), opt['consts'].data_ptr(), *opt['hyper'], _stream())
+        # per requesting rank and row: the sum of the owned rows of its bag (others read as 0)
+        part = torch.empty(W * rows, self.D, device=dev)
+        ps = _hip.FeatureSeg()
+        ps.kind, ps.dim, ps.out_col, ps.pool_mode, ps.bag, ps.pad_idx = (_hip.RS_SEG_POOL, self.D, 0,
+                                                                         _hip.RS_POOL['sum'], bag, -1)
+        ps.vocab, ps.idx_stride, ps.idx, ps.table = self.V, bag, local.data_ptr(), self.ptr(self.flat.data)
+        ops.gather_fwd([ps], W * rows, part, None)
+        out = torch.empty(rows, self.D, device=dev)
+        reduce_scatter_sum(out, part)
+        if mode == SEG_MEAN:
+            _hip.call('rs_scale_inplace', out.data_ptr(), out.numel(), 1.0 / bag, None, _stream())
+        c = None
+        if record:
+            pad = seg.pad_idx
+            pad_local = pad // W if pad >= 0 and pad % W == r else -1
+            c = self.sort_call(local.data_ptr(), W * rows, bag, bag, pad_local if pad_local >= 0 else None,
+                               mode, id_bytes=8, keep=(local, all32))
+            c.local_rows = rows
+            self.calls.append(c)
+        return c, out
+
     def segsum(self, c, dout_ptr, ldo, accumulate=None):
         """Backward: the table gradient of call c from its output gradient (dout_ptr = the
         feature's first column, row stride ldo floats). Under data parallelism a local call only
@@ -178,8 +242,9 @@ class LazyTable:
         dev = self.param.device
         if accumulate is None:
             if _dp_active():
-                c.dseg = torch.empty(c.rows, self.D, dtype=torch.float32, device=dev)
-                _hip.call('rs_pack_rows', dout_ptr, ldo, c.rows, self.D, c.dseg.data_ptr(), _stream())
+                # this rank's output gradient rows (a row-sharded call spans world x local_rows)
+                c.dseg = torch.empty(c.local_rows, self.D, dtype=torch.float32, device=dev)
+                _hip.call('rs_pack_rows', dout_ptr, ldo, c.local_rows, self.D, c.dseg.data_ptr(), _stream())
                 return
             accumulate = len(self.calls) > 1
         ws = torch.empty(int(_hip.lib().rs_segsum_ws_bytes(c.n, self.D)) // 4 + 1, dtype=torch.int32,
@@ -249,35 +314,81 @@ def _is_lazy(p, lazy_ids):
     return id(p) in lazy_ids
 
 
+def shard_threshold() -> int:
+    """RSYS_SHARD_ROWS: tables with at least this many rows are row-sharded under data
+    parallelism (0, the default: every large table stays replicated)."""
+    return int(os.environ.get('RSYS_SHARD_ROWS', '0'))
+
+
+def shard_spec(param):
+    """(world, rank) if this lazy table is row-sharded, else None."""
+    thr = shard_threshold()
+    if thr <= 0 or not _dp_active() or int(param.shape[0]) < thr:
+        return None
+    d = torch.distributed
+    return d.get_world_size(), d.get_rank()
+
+
+def shard_rows(V: int, world: int, rank: int) -> int:
+    """Rows of a V-row table owned by `rank` (ids rank, rank + world, ...)."""
+    return (V - rank + world - 1) // world if rank < V else 0
+
+
+def unshard(parts, V: int):
+    """Full [V, D] table from every rank's [shard_rows(V, W, r), D] shard (rank order)."""
+    W = len(parts)
+    full = parts[0].new_empty(V, parts[0].shape[1])
+    for r, p in enumerate(parts):
+        full[r::W] = p[:shard_rows(V, W, r)]
+    return full
+
+
 class FlatParams:
     def __init__(self, params, device, lazy=()):
         """params: in module.parameters() order; lazy: the subset (large [V, D] embedding
         weights) trained by lazy-exact Adam, laid out after all other parameters."""
         self.params = list(params)
         lazy_ids = {id(p) for p in lazy}
+        # row-sharded lazy tables (module doc): their local shard only, laid out last
+        shards = {id(p): shard_spec(p) for p in self.params if _is_lazy(p, lazy_ids)}
+        shapes = []
+        for p in self.params:
+            sp = shards.get(id(p))
+            shapes.append(p.shape if sp is None else torch.Size((shard_rows(p.shape[0], *sp), p.shape[1])))
         self.offsets = [0] * len(self.params)
         off = 0
-        for second in (False, True):
+        for group in (0, 1, 2):  # dense, replicated lazy, row-sharded lazy
             for i, p in enumerate(self.params):
-                if _is_lazy(p, lazy_ids) == second:
+                g = 0 if not _is_lazy(p, lazy_ids) else (2 if shards[id(p)] is not None else 1)
+                if g == group:
                     self.offsets[i] = off
-                    off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
-            if not second:
+                    off += (shapes[i].numel() + ALIGN - 1) // ALIGN * ALIGN
+            if group == 0:
                 self.dense_numel = off
+            elif group == 1:
+                self.replicated_numel = off  # broadcast / all-reduce never touch the shards
         self.numel = off
         self.data = torch.zeros(off, dtype=torch.float32, device=device)
         self.grad = torch.zeros(off, dtype=torch.float32, device=device)
         with torch.no_grad():
-            for p, o in zip(self.params, self.offsets):
+            for p, o, shp in zip(self.params, self.offsets, shapes):
                 if p.dtype != torch.float32:
                     raise TypeError(f'only fp32 parameters are supported, got {p.dtype}')
-                self.data[o:o + p.numel()].copy_(p.detach().reshape(-1))
-        for p, o in zip(self.params, self.offsets):
-            p.data = self.data[o:o + p.numel()].view(p.shape)
+                sp = shards.get(id(p))
+                if sp is None:
+                    self.data[o:o + p.numel()].copy_(p.detach().reshape(-1))
+                else:  # rank 0's initial table, then this rank's rows
+                    full = p.detach().to(device).contiguous()
+                    torch.distributed.broadcast(full, 0)
+                    self.data[o:o + shp.numel()].copy_(full[sp[1]::sp[0]].reshape(-1))
+        vocab = {}
+        for p, o, shp in zip(self.params, self.offsets, shapes):
+            vocab[id(p)] = int(p.shape[0]) if len(p.shape) else 0
+            p.data = self.data[o:o + shp.numel()].view(shp)
             p._rs_flat = self
             p._rs_offset = o
-        self.lazy = [LazyTable(self, i, p, o) for i, (p, o) in enumerate(zip(self.params, self.offsets))
-                     if _is_lazy(p, lazy_ids)]
+        self.lazy = [LazyTable(self, i, p, o, shard=shards[id(p)], vocab=vocab[id(p)])
+                     for i, (p, o) in enumerate(zip(self.params, self.offsets)) if _is_lazy(p, lazy_ids)]
         for t in self.lazy:
             t.param._rs_lazy = t
         self.lazy_opt = None  # set by optim.Adam: m, v, step_dev, consts, hyper
@@ -371,6 +482,7 @@ def lazy_tables(module: torch.nn.Module):
             out.append(m.weight)
             if not getattr(m, '_rs_lazy_hooks', False):
                 m.register_state_dict_pre_hook(_flush_hook)
+                m._register_state_dict_hook(_shard_state_hook)
                 m._register_load_state_dict_pre_hook(_flush_load_hook, with_module=True)
                 m._rs_lazy_hooks = True
     return out
@@ -388,6 +500,28 @@ def _flush_hook(module, prefix, keep_vars):
 
 def _flush_load_hook(module, state_dict, prefix, *args):
     _flush_table(module)  # rows become current, so the loaded weights start from `last` = step
+    t = getattr(module.weight, '_rs_lazy', None)
+    k = prefix + 'weight'
+    if t is not None and t.shard is not None and k in state_dict and \
+            state_dict[k].shape[0] == t.V_full and t.V_full != t.V:
+        W, r = t.shard
+        state_dict[k] = state_dict[k][r::W]  # a full table: this rank's rows
+
+
+def _shard_state_hook(module, state_dict, prefix, local_metadata):
+    """state_dict() of a row-sharded table: the full [V, D] table, gathered from every rank (a
+    collective), so checkpoints keep the reference's shapes."""
+    t = getattr(module.weight, '_rs_lazy', None)
+    k = prefix + 'weight'
+    if t is None or t.shard is None or k not in state_dict:
+        return
+    W, r = t.shard
+    n = -(-t.V_full // W)
+    local = torch.zeros(n, t.D, device=t.param.device)
+    local[:t.V] = t.param.detach()
+    parts = [torch.empty_like(local) for _ in range(W)]
+    torch.distributed.all_gather(parts, local)
+    state_dict[k] = unshard(parts, t.V_full)
 
 
 def lookup_table(weight, ids_ptr, rows, bag, row_stride, pad, mode, keep=None, record=True):

@@ -24,7 +24,7 @@ import torch
 from torch.autograd.function import once_differentiable
 
 from . import _hip, ops, precision
-from .flat import SEG_MEAN, SEG_ONE, SEG_SUM, grad_of, lookup_table
+from .flat import SEG_MEAN, SEG_ONE, SEG_SUM, flat_of, grad_of, lookup_table
 
 
 def _seg(**kw):
@@ -39,15 +39,25 @@ def _pad(v):
     return -1 if v is None else int(v)
 
 
-def _lookup_lazy(segs, tables, rows, keep=None, record=True):
+def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
     """Large (lazy-Adam) tables, flat.py: bring this call's rows to the current optimizer step
     before the gather reads them and (`record`: a backward follows) sort its ids by row
     (csrc/lookup.hip). Returns {segment index: LookupCall}; ordinary tables are not listed.
     `keep` (the id tensors the segments point into) stays referenced by the calls until the
-    optimizer step (the data-parallel exchange re-reads the ids after the backward)."""
+    optimizer step (the data-parallel exchange re-reads the ids after the backward).
+    A row-sharded table (flat.py module doc) is looked up here: its segment becomes a copy of
+    the pooled rows the reduce-scatter returned (kept alive through `keep`)."""
     calls = {}
     for i, (s, t) in enumerate(zip(segs, tables)):
         if s.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL) and hasattr(t, '_rs_lazy'):
+            lt = t._rs_lazy
+            if getattr(lt, 'shard', None) is not None and flat_of(t) is lt.flat:
+                c, res = lt.shard_lookup(s, rows, record, None if err is None else err.data_ptr())
+                keep.append(res)
+                segs[i] = _seg(kind=_hip.RS_SEG_COPY, dim=s.dim, out_col=s.out_col, table=res.data_ptr())
+                if c is not None:
+                    calls[i] = c
+                continue
             pool = s.kind == _hip.RS_SEG_POOL
             bag = s.bag if pool else 1
             mode = SEG_ONE
@@ -70,7 +80,9 @@ def _grad_lazy(segs, calls, dout, tables):
     for i, s in enumerate(segs):
         c = calls.get(i) if calls else None
         ptr = dout.data_ptr() + 4 * s.out_col
-        if c is not None and c.mode >= 0 and ptr % 16 == 0 and dout.stride(0) % 4 == 0:
+        sharded = c is not None and getattr(tables[i]._rs_lazy, 'shard', None) is not None
+        if sharded or (c is not None and c.mode >= 0 and ptr % 16 == 0 and dout.stride(0) % 4 == 0):
+            # (a row-sharded call only keeps its output gradient rows here: rs_pack_rows)
             tables[i]._rs_lazy.segsum(c, ptr, dout.stride(0))
         else:
             rest.append(s)
@@ -132,7 +144,7 @@ def seq_input_fwd(proc, seqd, B, L, p, key, err, need=True):
     M = B * L
     dev = proc.pos_emb.weight.device
     cat = torch.empty(M, dcat, device=dev, dtype=torch.float32)
-    calls = _lookup_lazy(segs, tables, M, keep, record=need)
+    calls = _lookup_lazy(segs, tables, M, keep, record=need, err=err)
     ops.gather_fwd(segs, M, cat, err)
     lin = proc.feature_projection[0]
     pos = proc.pos_emb.weight
@@ -546,7 +558,7 @@ class TowerFeatureFn(torch.autograd.Function):
             raise RuntimeError(f'too many features in one tower ({len(segs)} > {_hip.MAX_SEGMENTS})')
         dev = tower.feature_bn.weight.device
         out = torch.empty(B, col, device=dev, dtype=torch.float32)
-        calls = _lookup_lazy(segs, [w for w, _ in pp], B, keep, record=need)
+        calls = _lookup_lazy(segs, [w for w, _ in pp], B, keep, record=need, err=tower.err_flag)
         ops.gather_fwd(segs, B, out, tower.err_flag)
         if need:
             ctx.segs, ctx.pp, ctx.keep, ctx.B, ctx.calls = segs, pp, keep, B, calls

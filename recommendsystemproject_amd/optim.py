@@ -42,7 +42,9 @@ class _DeviceClip:
         nd = int(L.rs_sqnorm_parts(n))
         ns = int(L.rs_sorted_sqnorm_parts())
         work = []
-        for t in lazy:
+        # row-sharded tables last: their partials are per-rank shards of the norm, summed over
+        # the ranks before the coefficient (every rank then holds the same total)
+        for t in sorted(lazy, key=lambda t: getattr(t, 'shard', None) is not None):
             owner = t.mark_owners()
             for i, c in enumerate(t.step_calls()):
                 work.append((t, c, owner, i))
@@ -52,6 +54,9 @@ class _DeviceClip:
             _hip.call('rs_sorted_sqnorm', c.keys.data_ptr(), c.n, t.D, t.ptr(g),
                       None if owner is None else owner.data_ptr(), i, float(scale),
                       ws.data_ptr() + 8 * (nd + k * ns), ops.stream())
+        first = next((k for k, w in enumerate(work) if getattr(w[0], 'shard', None) is not None), None)
+        if first is not None:
+            torch.distributed.all_reduce(ws[nd + first * ns:nd + len(work) * ns])
         _hip.call('rs_clip_coef', ws.data_ptr(), nd + ns * len(work), float(max_norm),
                   self.norm.data_ptr(), self.coef.data_ptr(), ops.stream())
 
