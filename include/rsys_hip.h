@@ -170,6 +170,21 @@ int rs_ffn_bwd_ln_bf16(int M, int F, const float* x, const float* W1, const floa
                        const float* h1, const float* gamma1, const float* mean1, const float* rstd1,
                        float* dh1, float* dsa, float* dgamma1, float* dbeta1, void* f1, void* dpre,
                        float p, const int64_t* key, int site, float* ws, void* stream);
+/* rs_ffn_bwd_ln_bf16 with norm2's backward as its prologue (bf16 mode, F = 256, M % 16 == 0):
+ * x2 = LN2(x1 + drop2(ffn(x1))) with x1 = LN1(h1). Reads dy2 = dL/dx2 and h2 (+ norm2's
+ * mean2 / rstd2 / gamma2) instead of dff / dres; writes dff = drop2(dh2) [M, 64] (the operand of
+ * rs_ffn_wgrad_bf16), dh1, dsa (p > 0) and accumulates dgamma1/dbeta1, dgamma2/dbeta2
+ * (fixed-order partials in ws: rs_ffn_bwd_ln2_ws_bytes). Replaces rs_layernorm_bwd (norm2) +
+ * rs_ffn_bwd_ln_bf16 of TransformerEncoderLayer's backward (SequenceEncoder.py:17-29; post-LN,
+ * norm_first=False). Only dh1 may alias dy2. */
+int64_t rs_ffn_bwd_ln2_ws_bytes(int M, int F);
+int rs_ffn_bwd_ln2_bf16(int M, int F, const float* x, const float* W1, const float* b1,
+                        const float* W2, const uint64_t* mask, const float* dy2, const float* h2,
+                        const float* gamma2, const float* mean2, const float* rstd2, float* dff,
+                        float* dgamma2, float* dbeta2, const float* h1, const float* gamma1,
+                        const float* mean1, const float* rstd1, float* dh1, float* dsa,
+                        float* dgamma1, float* dbeta1, float p, const int64_t* key, int site1,
+                        int site2, float* ws, void* stream);
 /* dW[Mo,No] = beta*dW + dY^T X over `rows` rows on bf16 MFMA (fp32 accumulate, fixed-order
  * reduction); db[Mo] += colsum(dY) (nullable). dY / X are fp32 or, with dy_bf16 / x_bf16, bf16
  * (the fused FFN's f1 / dPre1). Replaces the weight-gradient part of autograd's Linear backward

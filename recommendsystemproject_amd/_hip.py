@@ -49,6 +49,9 @@ SIGNATURES = {
     'rs_ffn_bwd_ln_ws_bytes': (i64, [i32, i32]),
     'rs_ffn_bwd_ln_bf16': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                  vp, vp, f32, vp, i32, vp, vp]),
+    'rs_ffn_bwd_ln2_ws_bytes': (i64, [i32, i32]),
+    'rs_ffn_bwd_ln2_bf16': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                  vp, vp, vp, vp, vp, vp, f32, vp, i32, i32, vp, vp]),
     'rs_wgrad_ws_bytes': (i64, [i32, i32, i32]),
     'rs_ffn_wgrad_ws_bytes': (i64, [i32, i32]),
     'rs_ffn_wgrad_bf16': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp]),

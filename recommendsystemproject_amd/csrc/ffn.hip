@@ -72,6 +72,17 @@ struct FfnArgs {
   float* ln_da;  // nullable (p == 0)
   float* ln_ws;
   int ln_site;
+  // bwd with norm2's backward fused as the prologue too (rs_ffn_bwd_ln2_bf16): the kernel reads
+  // the gradient of the layer output dy2 and norm2's input h2 instead of dff / dres, and writes
+  // dff = dropout2-backward(dh2) for the weight gradients; [grid][128] dgamma2 | dbeta2 partials
+  const float* ln2_h;
+  const float* ln2_dy;
+  const float* ln2_gamma;
+  const float* ln2_mean;
+  const float* ln2_rstd;
+  float* ln2_ws;
+  float* dff_out;
+  int ln2_site;
 };
 
 // k permutation of a 32-wide chunk: operand slot 8q + j (lane quad q, element j) holds column
@@ -256,8 +267,13 @@ __global__ __launch_bounds__(512) void ffn_fwd_bf16_kernel(FfnArgs a) {
 
 // ACTS: also write f1 and dPre1 (bf16) for rs_wgrad_bf16; without them (the weight gradients
 // by rs_ffn_wgrad_bf16) linear1 is not recomputed and its W1 image is not staged.
-template <int F, bool LN1 = false, bool LNDROP = false, bool ACTS = true>
+// LN2 (with LN1, !ACTS): norm2's backward is the prologue. Lane (r, q) holds row r's columns
+// 16t + 4q + e (the layout of the residual add after the last product), so dh2 IS the residual
+// gradient; dff = drop2(dh2) is stored (fp32, for rs_ffn_wgrad_bf16) and goes through a per-wave
+// LDS tile as bf16 to reach the 16q .. 16q+15 layout of the dff W2 product's operand.
+template <int F, bool LN1 = false, bool LNDROP = false, bool ACTS = true, bool LN2 = false>
 __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
+  static_assert(!LN2 || (LN1 && !ACTS), "LN2 prologue needs the LN1 epilogue and no activations");
   constexpr int FP = F + 8;
   constexpr int NH = F / 16, NC = F / 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -265,6 +281,10 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
   __bf16* W2t = W1s + (ACTS ? F * DP : 0);              // [F][DP]  W2^T (dff W2)
   __bf16* W1t = W2t + F * DP;                           // [D][FP]  W1^T, k-permuted (dPre1 W1)
   float* sb1 = reinterpret_cast<float*>(W1t + D * FP);  // [F]
+  float* sg2 = sb1 + F;                                 // [D] gamma2 (LN2)
+  __bf16* dsc = reinterpret_cast<__bf16*>(sg2 + D);     // [8 waves][16][DP] dff tiles (LN2)
+  if constexpr (LN2)
+    for (int i = threadIdx.x; i < D; i += blockDim.x) sg2[i] = a.ln2_gamma[i];
   stage_batched<F, D, 512>(a.W1, D, [&](int n1, int k, const floatx4& v) {
     if constexpr (ACTS) put4(W1s + n1 * DP + k, v);
 #pragma unroll
@@ -283,9 +303,32 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
   const int stride = gridDim.x * 8;
   int g = blockIdx.x * 8 + wave;
   floatx4 xr[4], dr[4];
+  // LN2: the next group's dy2 / h2 rows (t layout) and statistics, loaded one group ahead
+  floatx4 pdy[LN2 ? 4 : 1], ph2[LN2 ? 4 : 1], lpg2[LN2 ? 4 : 1], lpb2[LN2 ? 4 : 1];
+  float pmu2 = 0.f, prs2 = 0.f;
+  DropKey ldk2{};
   if (g < groups) {
     if constexpr (ACTS) load_row64(a.x, (int64_t)g * 16 + r, q, xr);
-    load_row64(a.dff, (int64_t)g * 16 + r, q, dr);
+    if constexpr (LN2) {
+      const int64_t m0 = (int64_t)g * 16 + r;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        pdy[t] = *(gptr4)(a.ln2_dy + m0 * D + 16 * t + 4 * q);
+        ph2[t] = *(gptr4)(a.ln2_h + m0 * D + 16 * t + 4 * q);
+      }
+      pmu2 = a.ln2_mean[m0];
+      prs2 = a.ln2_rstd[m0];
+    } else {
+      load_row64(a.dff, (int64_t)g * 16 + r, q, dr);
+    }
+  }
+  if constexpr (LN2) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      lpg2[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+      lpb2[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    if constexpr (LNDROP) ldk2 = make_key(a.key, a.ln2_site, a.p);
   }
   if constexpr (!ACTS) {  // x1 only feeds linear1's recompute
 #pragma unroll
@@ -311,8 +354,10 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
     const __bf16* W3i = W1t + zo;
     const int64_t m = (int64_t)g * 16 + r;
     floatx4 res[4];  // dres[m][16t + 4q ..] (accumulated into)
+    if constexpr (!LN2) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) res[t] = *(gptr4)(a.dres + m * D + 16 * t + 4 * q);
+      for (int t = 0; t < 4; ++t) res[t] = *(gptr4)(a.dres + m * D + 16 * t + 4 * q);
+    }
     floatx4 lh[LN1 ? 4 : 1];
     float lmu = 0.f, lrs = 0.f;
     if constexpr (LN1) {  // LN1 operands, issued with the residual rows
@@ -323,10 +368,72 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
     }
     const uint64_t bits = a.mask[m * (F / 64) + q];
     bf16x8 ax[2] = {cvt8(xr[0], xr[1]), cvt8(xr[2], xr[3])};
-    bf16x8 ad[2] = {cvt8(dr[0], dr[1]), cvt8(dr[2], dr[3])};
+    bf16x8 ad[2];
     const int gn = g + stride < groups ? g + stride : g;
     if constexpr (ACTS) load_row64(a.x, (int64_t)gn * 16 + r, q, xr);
-    load_row64(a.dff, (int64_t)gn * 16 + r, q, dr);
+    if constexpr (LN2) {
+      // norm2 backward of row m (its 64 columns in the 4 lanes r, r+16, r+32, r+48), as
+      // ln_bwd64_kernel: dh2 = rstd (g - mean(g) - xhat mean(g xhat)), g = dy2 * gamma2
+      floatx4 xh[4], gg[4];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const floatx4 gm = *reinterpret_cast<const floatx4*>(sg2 + 16 * t + 4 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[t][e] = (ph2[t][e] - pmu2) * prs2;
+          lpg2[t][e] += pdy[t][e] * xh[t][e];
+          lpb2[t][e] += pdy[t][e];
+          gg[t][e] = pdy[t][e] * gm[e];
+          s1 += gg[t][e];
+          s2 += gg[t][e] * xh[t][e];
+        }
+      }
+      s1 += __shfl_xor(s1, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      s1 /= 64.f;
+      s2 /= 64.f;
+      const float rs2 = prs2;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) res[t][e] = rs2 * (gg[t][e] - s1 - xh[t][e] * s2);
+      // the current dy2 / h2 are dead: the next group's go in flight behind this one's products
+      const int64_t mn = (int64_t)gn * 16 + r;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        pdy[t] = *(gptr4)(a.ln2_dy + mn * D + 16 * t + 4 * q);
+        ph2[t] = *(gptr4)(a.ln2_h + mn * D + 16 * t + 4 * q);
+      }
+      pmu2 = a.ln2_mean[mn];
+      prs2 = a.ln2_rstd[mn];
+      // dff = drop2(dh2): stored for the weight gradients, and as bf16 through this wave's LDS
+      // tile into the operand layout (lane quad q: columns 16q .. 16q+15 of row r)
+      __bf16* tile = dsc + (wave * 16 + r) * DP;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        floatx4 f = res[t];
+        if constexpr (LNDROP) {
+          float mk[4];
+          keep4(ldk2, (uint64_t)(m * D + 16 * t + 4 * q), mk);  // ln_bwd64_kernel's draw
+#pragma unroll
+          for (int e = 0; e < 4; ++e) f[e] *= mk[e];
+        }
+        *reinterpret_cast<floatx4*>(a.dff_out + m * D + 16 * t + 4 * q) = f;
+        put4(tile + 16 * t + 4 * q, f);
+      }
+      // one wave writes and reads its own tile: LDS executes a wave's operations in order
+      asm volatile("" ::: "memory");
+      ad[0] = lds8(tile + 16 * q);
+      ad[1] = lds8(tile + 16 * q + 8);
+      asm volatile("" ::: "memory");
+    } else {
+      ad[0] = cvt8(dr[0], dr[1]);
+      ad[1] = cvt8(dr[2], dr[3]);
+      load_row64(a.dff, (int64_t)gn * 16 + r, q, dr);
+    }
     bf16x8 a3[NC];
 #pragma unroll
     for (int h0 = 0; h0 < NH; h0 += 4) {
@@ -436,6 +543,25 @@ __global__ __launch_bounds__(512) void ffn_bwd_bf16_kernel(FfnArgs a) {
       for (int w = 0; w < 8; ++w)
         for (int rr = 0; rr < 16; ++rr) acc += red[(w * 64 + rr + 16 * qq) * 32 + 16 * st + 4 * t + e];
       a.ln_ws[(int64_t)blockIdx.x * 128 + threadIdx.x] = acc;
+    }
+    if constexpr (LN2) {  // the same for norm2's dgamma2 | dbeta2 (columns in the same t layout)
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          red[(wave * 64 + lane) * 32 + 4 * t + e] = lpg2[t][e];
+          red[(wave * 64 + lane) * 32 + 16 + 4 * t + e] = lpb2[t][e];
+        }
+      __syncthreads();
+      if (threadIdx.x < 128) {
+        const int st = threadIdx.x >> 6, c = threadIdx.x & 63;
+        const int t = c >> 4, qq = (c & 15) >> 2, e = c & 3;
+        float acc = 0.f;
+        for (int w = 0; w < 8; ++w)
+          for (int rr = 0; rr < 16; ++rr) acc += red[(w * 64 + rr + 16 * qq) * 32 + 16 * st + 4 * t + e];
+        a.ln2_ws[(int64_t)blockIdx.x * 128 + threadIdx.x] = acc;
+      }
     }
   }
 }
@@ -681,6 +807,8 @@ size_t fwd_lds(int F) { return (size_t)F * DP * 2 + (size_t)D * (F + 8) * 2 + (s
 size_t bwd_lds(int F, bool acts = true) {
   return (size_t)(acts ? 2 : 1) * F * DP * 2 + (size_t)D * (F + 8) * 2 + (size_t)F * 4;
 }
+// + gamma2 and the 8 waves' [16][DP] bf16 dff tiles
+size_t bwd_ln2_lds(int F) { return bwd_lds(F, false) + (size_t)D * 4 + (size_t)8 * 16 * DP * 2; }
 
 int grid_for(int M, size_t lds) {
   const int per_cu = lds > 80 * 1024 ? 1 : 2;
@@ -763,6 +891,48 @@ extern "C" int rs_ffn_bwd_ln_bf16(int M, int F, const float* x, const float* W1,
   }
   RS_CHECK_LAUNCH("rs_ffn_bwd_ln_bf16");
   return partials_reduce2(ws, nb, 128, 64, 1.f, 1.f, dgamma1, dbeta1, st);
+}
+
+extern "C" int64_t rs_ffn_bwd_ln2_ws_bytes(int M, int F) { return 2 * rs_ffn_bwd_ln_ws_bytes(M, F); }
+
+extern "C" int rs_ffn_bwd_ln2_bf16(int M, int F, const float* x, const float* W1, const float* b1,
+                                   const float* W2, const uint64_t* mask, const float* dy2,
+                                   const float* h2, const float* gamma2, const float* mean2,
+                                   const float* rstd2, float* dff, float* dgamma2, float* dbeta2,
+                                   const float* h1, const float* gamma1, const float* mean1,
+                                   const float* rstd1, float* dh1, float* dsa, float* dgamma1,
+                                   float* dbeta1, float p, const int64_t* key, int site1, int site2,
+                                   float* ws, void* stream) {
+  RS_CHECK_ARG(M >= 0 && M % 16 == 0 && F == 256, "rs_ffn_bwd_ln2_bf16: need M %% 16 == 0 and F == 256 (M=%d F=%d)", M, F);
+  RS_CHECK_ARG(x && W1 && b1 && W2 && mask && dy2 && h2 && gamma2 && mean2 && rstd2 && dff && dgamma2 &&
+                   dbeta2 && h1 && gamma1 && mean1 && rstd1 && dh1 && dgamma1 && dbeta1 && ws,
+               "rs_ffn_bwd_ln2_bf16: null operand");
+  // each 16-row group is read and written by one wave: only dh1 may alias dy2
+  RS_CHECK_ARG(dff != dy2 && dff != h2 && dff != h1 && dff != dh1 && dff != dsa && dh1 != h2 && dh1 != h1 &&
+                   (!dsa || (dsa != dy2 && dsa != h2 && dsa != h1 && dsa != dh1)),
+               "rs_ffn_bwd_ln2_bf16: overlapping outputs");
+  RS_CHECK_ARG(aligned16(x) && aligned16(dy2) && aligned16(h2) && aligned16(dff) && aligned16(dh1) &&
+                   aligned16(b1) && aligned16(h1) && aligned16(gamma1) && aligned16(gamma2) &&
+                   (!dsa || aligned16(dsa)),
+               "rs_ffn_bwd_ln2_bf16: misaligned operand");
+  RS_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || (key && dsa)), "rs_ffn_bwd_ln2_bf16: dropout needs a key and dsa, 0 <= p < 1");
+  if (M == 0) return 0;
+  FfnArgs a{};
+  a.M = M; a.x = x; a.W1 = W1; a.b1 = b1; a.W2 = W2; a.mask = const_cast<uint64_t*>(mask);
+  a.dx = dh1; a.p = p; a.key = key;
+  a.ln_h = h1; a.ln_gamma = gamma1; a.ln_mean = mean1; a.ln_rstd = rstd1; a.ln_da = dsa; a.ln_site = site1;
+  a.ln2_h = h2; a.ln2_dy = dy2; a.ln2_gamma = gamma2; a.ln2_mean = mean2; a.ln2_rstd = rstd2;
+  a.dff_out = dff; a.ln2_site = site2;
+  const int nb = grid_for(M, bwd_lds(F));  // the partials' count (rs_ffn_bwd_ln2_ws_bytes)
+  a.ln_ws = ws;
+  a.ln2_ws = ws + (int64_t)nb * 128;
+  const size_t lds = bwd_ln2_lds(F);
+  hipStream_t st = as_stream(stream);
+  if (p > 0.f) ffn_bwd_bf16_kernel<256, true, true, false, true><<<nb, 512, lds, st>>>(a);
+  else ffn_bwd_bf16_kernel<256, true, false, false, true><<<nb, 512, lds, st>>>(a);
+  RS_CHECK_LAUNCH("rs_ffn_bwd_ln2_bf16");
+  RS_RET_IF(partials_reduce2(ws, nb, 128, 64, 1.f, 1.f, dgamma1, dbeta1, st));
+  return partials_reduce2(a.ln2_ws, nb, 128, 64, 1.f, 1.f, dgamma2, dbeta2, st);
 }
 
 extern "C" int rs_ffn_bwd_bf16(int M, int F, const float* x, const float* W1, const float* b1,

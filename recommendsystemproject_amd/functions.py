@@ -291,14 +291,32 @@ def _post_attn_bwd(lyr, saved, dx2, p, key, site):
     g = grad_of
     sa_mod = lyr.self_attn
     # x2 = LN2(x1 + drop2(ff))
-    dff = torch.empty_like(dx2) if p > 0 else None
-    dh2 = ops.layernorm_bwd(h2, dx2, lyr.norm2.weight, m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias),
-                            da=dff, p=p, key=key, site=site + 3)
-    dff = dh2 if dff is None else dff
     ln1_done = False
-    if isinstance(f1, tuple):  # fused feed-forward block (bf16 mode)
+    fused_ffn = isinstance(f1, tuple)
+    acts = fused_ffn and not ops.ffn_wgrad_fused()
+    if fused_ffn and not acts and not os.environ.get('RSYS_UNFUSED_FFN_LN') \
+            and not os.environ.get('RSYS_UNFUSED_FFN_LN2'):
+        # norm2 backward + FFN backward + norm1 backward in one pass (csrc/ffn.hip): dh2 and
+        # dx1 stay on chip; dff = drop2(dh2) is written for the fused weight gradients
+        dh1, dsa, dff = ops.ffn_bwd_ln2_bf16(
+            x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, f1[1], dx2, h2, lyr.norm2.weight,
+            m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias), h1, lyr.norm1.weight, m1, r1,
+            g(lyr.norm1.weight), g(lyr.norm1.bias), p, key, site + 1, site + 3)
+        ln1_done = True
+        def _ffn_wgrads2(dff=dff, mask=f1[1]):
+            ops.ffn_wgrad_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, mask, dff, p,
+                               g(lyr.linear1.weight), g(lyr.linear1.bias), g(lyr.linear2.weight),
+                               g(lyr.linear2.bias))
+        _wgrad_side(_ffn_wgrads2, dff, x1, f1[1])
+    else:
+        dff = torch.empty_like(dx2) if p > 0 else None
+        dh2 = ops.layernorm_bwd(h2, dx2, lyr.norm2.weight, m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias),
+                                da=dff, p=p, key=key, site=site + 3)
+        dff = dh2 if dff is None else dff
+    if ln1_done:
+        pass
+    elif fused_ffn:  # fused feed-forward block (bf16 mode)
         # fused weight gradients: f1 / dPre1 recomputed on chip, never written (csrc/ffn.hip)
-        acts = not ops.ffn_wgrad_fused()
         if not os.environ.get('RSYS_UNFUSED_FFN_LN'):
             # dx1 = dh2 + dPre1 W1 and norm1's backward in one pass: dx1 stays on chip
             dh1, dsa, f1b, dpre = ops.ffn_bwd_ln_bf16(

@@ -142,6 +142,21 @@ def ffn_bwd_ln_bf16(x, W1, b1, W2, mask, dff, dres, h1, gamma1, mean1, rstd1, dg
     return dh1, dsa, f1, dpre
 
 
+def ffn_bwd_ln2_bf16(x, W1, b1, W2, mask, dy2, h2, gamma2, mean2, rstd2, dgamma2, dbeta2, h1, gamma1,
+                     mean1, rstd1, dgamma1, dbeta1, p, key, site1, site2):
+    """norm2's backward + the FFN backward + norm1's backward in one pass (weight gradients by
+    ffn_wgrad_bf16 from the returned dff): -> (dh1, dsa or None, dff = drop2(dh2))."""
+    M, F = x.shape[0], W1.shape[0]
+    dff = torch.empty_like(dy2)
+    dh1 = torch.empty_like(dy2)
+    dsa = torch.empty_like(dy2) if p > 0 else None
+    w = ws(_hip.lib().rs_ffn_bwd_ln2_ws_bytes(M, F), x.device)
+    call('rs_ffn_bwd_ln2_bf16', M, F, P(x), P(W1), P(b1), P(W2), P(mask), P(dy2), P(h2), P(gamma2), P(mean2),
+         P(rstd2), P(dff), P(dgamma2), P(dbeta2), P(h1), P(gamma1), P(mean1), P(rstd1), P(dh1), P(dsa),
+         P(dgamma1), P(dbeta1), float(p), P(key), site1, site2, P(w), stream())
+    return dh1, dsa, dff
+
+
 def ffn_wgrad_bf16(x, W1, b1, W2, mask, dff, p, dW1, db1, dW2, db2):
     """dW1 += dPre1^T x, db1 += colsum(dPre1), dW2 += dff^T f1, db2 += colsum(dff), f1 / dPre1
     recomputed on chip (csrc/ffn.hip rs_ffn_wgrad_bf16)."""

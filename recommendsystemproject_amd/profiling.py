@@ -117,10 +117,15 @@ def _ffn_fwd_work(a):
     return 4.0 * M * F * 64, 4.0 * (3 * M * 64 + 2 * M) + M * F / 8.0
 
 
-def _ffn_bwd_work(a):
+def _ffn_bwd_work(a, acts=None):
     M, F = a[0], a[1]
-    # x, dff, dres read, dx written (fp32); f1, dPre1 written (bf16); mask bits read
-    return 6.0 * M * F * 64, 4.0 * 4 * M * 64 + 2.0 * 2 * M * F + M * F / 8.0
+    if acts is None:
+        acts = a[10] is not None
+    # dff, dres read, dx written (fp32); mask bits read; with the activations (acts): x read,
+    # linear1 recomputed, f1 and dPre1 written (bf16)
+    if acts:
+        return 6.0 * M * F * 64, 4.0 * 4 * M * 64 + 2.0 * 2 * M * F + M * F / 8.0
+    return 4.0 * M * F * 64, 4.0 * 3 * M * 64 + M * F / 8.0
 
 
 def _wgrad_work(a):
@@ -144,12 +149,20 @@ def _ce_fused_work(a, bwd=False):
 def _ffn_bwd_ln_work(a):
     M, F = a[0], a[1]
     # the FFN backward's operands plus norm1's: h1 read, dh1 (+ dsa) written instead of dx1
-    fl, by = _ffn_bwd_work(a)
-    return fl + 12.0 * M * 64, by + 4.0 * M * 64 * (2 if a[19] > 0 else 1)
+    fl, by = _ffn_bwd_work(a, acts=a[17] is not None)
+    return fl + 12.0 * M * 64, by + 4.0 * M * 64 * (2 if a[19] > 0 else 1) + 8.0 * M
+
+
+def _ffn_bwd_ln2_work(a):
+    M, F = a[0], a[1]
+    # dy2, h2, h1 read, dff, dh1 (+ dsa) written (fp32); mask bits; both rows' mean / rstd
+    return (4.0 * M * F * 64 + 24.0 * M * 64,
+            4.0 * M * 64 * (5 + (1 if a[23] > 0 else 0)) + 16.0 * M + M * F / 8.0)
 
 
 WORK = {
     'rs_ffn_bwd_ln_bf16': _ffn_bwd_ln_work,
+    'rs_ffn_bwd_ln2_bf16': _ffn_bwd_ln2_work,
     'rs_inbatch_ce_fused_fwd': _ce_fused_work,
     'rs_inbatch_ce_fused_bwd': lambda a: _ce_fused_work(a, True),
     'rs_gemm_add_layernorm': _gemm_ln_work,

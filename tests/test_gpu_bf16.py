@@ -265,6 +265,56 @@ def test_fused_ffn_ln_backward(p, M, bf16_mode):
         assert (a - b_).abs().max().item() < 1e-5 * max(1.0, b_.abs().max().item())
 
 
+@pytest.mark.parametrize('p,M', [(0.0, 40960), (0.1, 40960), (0.1, 4112), (0.15, 16)])
+def test_fused_ffn_ln2_backward(p, M, bf16_mode):
+    """rs_ffn_bwd_ln2_bf16 (norm2's backward as the prologue of rs_ffn_bwd_ln_bf16) against the
+    rs_layernorm_bwd (norm2, with dropout2's backward) + rs_ffn_bwd_ln_bf16 pair it replaces.
+    The row sums of norm2's backward run over the columns in another order, so dff, dh1, dsa and
+    the four LayerNorm parameter gradients agree to fp32 summation order; dropout masks are the
+    same draws (zeros in the same places); the bf16 operand of dff W2 may round differently where
+    dff sits on a bf16 rounding boundary, hence the relative bound on dh1."""
+    x = rnd(M, 64, seed=7)
+    W1, b1, W2, b2, g, be = _ffn_weights()
+    key = torch.tensor([4321, 6], dtype=torch.int64, device=DEV)
+    h2, _, mu2, rs2, mask = ops.ffn_fwd_bf16(x, W1, b1, W2, b2, g, be, 1e-5, p, key, 18, 19)
+    g2 = 1 + 0.1 * rnd(64, seed=14)
+    dy2 = rnd(M, 64, seed=8)
+    h1 = rnd(M, 64, seed=10) * 2 + 0.3
+    g1 = 1 + 0.1 * rnd(64, seed=11)
+    mu1 = h1.mean(1)
+    rs1 = 1.0 / torch.sqrt(h1.var(1, unbiased=False) + 1e-5)
+    init = [rnd(64, seed=20 + i) for i in range(4)]  # dgamma2, dbeta2, dgamma1, dbeta1
+    # reference pair
+    r = [t.clone() for t in init]
+    dffr = torch.empty_like(dy2) if p > 0 else None
+    dh2r = ops.layernorm_bwd(h2, dy2.clone(), g2, mu2, rs2, r[0], r[1], da=dffr, p=p, key=key, site=19)
+    dffr = dh2r if dffr is None else dffr
+    dh1r, dsar, _, _ = ops.ffn_bwd_ln_bf16(x, W1, b1, W2, mask, dffr, dh2r, h1, g1, mu1, rs1, r[2], r[3],
+                                           p, key, 17, acts=False)
+    # fused
+    outs = []
+    for _ in range(2):
+        f = [t.clone() for t in init]
+        dh1, dsa, dff = ops.ffn_bwd_ln2_bf16(x, W1, b1, W2, mask, dy2, h2, g2, mu2, rs2, f[0], f[1], h1, g1,
+                                             mu1, rs1, f[2], f[3], p, key, 17, 19)
+        outs.append((dh1, dsa, dff, f))
+    (dh1, dsa, dff, f), second = outs[0], outs[1]
+    assert torch.equal(dh1, second[0]) and torch.equal(dff, second[2])  # deterministic
+    assert all(torch.equal(a, b_) for a, b_ in zip(f, second[3]))
+    assert torch.equal(dff == 0, dffr == 0)
+    assert (dff - dffr).abs().max().item() < 1e-5 * dffr.abs().max().item()
+    sc = dh1r.abs().max().item()
+    assert (dh1 - dh1r).abs().max().item() < 2e-3 * sc
+    assert (dh1 - dh1r).abs().mean().item() < 1e-5 * sc
+    if p > 0:
+        assert torch.equal(dsa == 0, dsar == 0)
+        assert (dsa - dsar).abs().max().item() < 3e-3 * sc
+    else:
+        assert dsa is None
+    for a, b_ in zip(f, r):
+        assert (a - b_).abs().max().item() < 2e-3 * max(1.0, b_.abs().max().item())
+
+
 def test_fused_ffn_bad_args(bf16_mode):
     x = rnd(40, 64)  # M % 16 != 0
     W1, b1, W2, b2, g, be = _ffn_weights()
