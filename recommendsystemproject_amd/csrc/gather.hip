@@ -37,16 +37,31 @@ struct SegLaunch {
   int ldo;
   int* err;
   int block_start[kMaxSeg + 1];
-  int rpb[kMaxSeg];   // rows per block
-  int chunks[kMaxSeg];  // lanes per row
-  int vec[kMaxSeg];
-  int small[kMaxSeg];   // bwd: table gradient accumulated in LDS (kernel gather_bwd_small)
+  int16_t rpb[kMaxSeg];   // rows per block
+  int16_t chunks[kMaxSeg];  // lanes per row
+  uint8_t vec[kMaxSeg];
+  uint8_t small[kMaxSeg];   // bwd: table gradient accumulated in LDS (kernel gather_bwd_small)
   int sblock_start[kMaxSeg + 1];
   int sblocks[kMaxSeg];
   int small_lds;        // bytes of dynamic LDS for the small-table kernel
-  int split[kMaxSeg];   // pooled bags: row groups sharing one bag (positions split S ways)
+  int16_t split[kMaxSeg];   // pooled bags: row groups sharing one bag (positions split S ways)
   int stage[kMaxSeg];   // fwd: bytes of the table staged into LDS (0: read from HBM / L2)
   int stage_lds;        // fwd: dynamic LDS bytes (the largest staged table)
+  // bwd, hot mid-size tables (gather_bwd_range_kernel): rows per range, ranges, lookup chunks,
+  // first block, offset (floats) of the segment's [chunks][vocab][dim] partials in ws
+  int rrows[kMaxSeg];
+  int16_t rranges[kMaxSeg];
+  int16_t rchunks[kMaxSeg];
+  int rblock_start[kMaxSeg + 1];
+  uint8_t onehot[kMaxSeg];   // bwd: tiny table by the one-hot MFMA kernel
+  int16_t oblocks[kMaxSeg];
+  int oblock_start[kMaxSeg + 1];
+  // bwd partials (small and ranged tables): [pchunks][vocab][dim] floats at ws + pws_off
+  int16_t pchunks[kMaxSeg];
+  int64_t pws_off[kMaxSeg];
+  int64_t ws_floats;
+  int range_lds;
+  float* ws;
 };
 static_assert(sizeof(SegLaunch) <= 4096, "SegLaunch must fit the kernel-argument segment");
 
@@ -351,9 +366,263 @@ __global__ __launch_bounds__(256) void gather_bwd_small_kernel(SegLaunch a) {
     }
   }
   __syncthreads();
+  // one global atomic per touched element
   for (int e = threadIdx.x; e < n; e += 256) {
     const float v = lds[e];
     if (v != 0.f) atomicAdd(sg.grad + e, v);
+  }
+}
+
+// Tiny tables (V <= 32 rows, D <= 32: C2's genre / age / occupation / gender tables) by one f32
+// MFMA per two lookup rows: dT[V, D] = Cnt^T dout, where Cnt[row][v] = number of the row's bag
+// ids equal to v (padding skipped; times 1/bag for a mean bag). v_mfma_f32_32x32x2_f32: lane l
+// supplies A[v = l % 32][k = l / 32] = Cnt[row_k][v] and B[k][c = l % 32] = dout[row_k][c]; the
+// products are exact (small integer counts) and accumulate in fp32. Each wave owns rows w, w + W,
+// ...; the 4 waves' tiles are summed in wave order through LDS, the workgroup's tile goes to
+// ws[block] and reduce_partials_kernel adds the blocks in order: bitwise reproducible, unlike the
+// small-table kernel's atomics. Opt-in (RSYS_ONEHOT_GRAD=1): at C2's 30 x 8 genre table (614,400
+// bag ids) it measured 45 + 8 us against the small-table kernel's 33 us (latency-bound: ~100 rows
+// per wave in steps of 32, each step one round trip for the ids and the dout column).
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+constexpr int kOneHotRows = 32;  // lookup rows per wave step (16 MFMAs, loads issued together)
+
+__global__ __launch_bounds__(256) void gather_bwd_onehot_kernel(SegLaunch a) {
+  __shared__ float red[4][32 * 32];
+  int s = 0;
+  while (s + 1 < a.nseg && (int)blockIdx.x >= a.oblock_start[s + 1]) ++s;
+  const rs_feature_seg_t& sg = a.segs[s];
+  const int lb = blockIdx.x - a.oblock_start[s];
+  const int nblk = a.oblocks[s];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int mv = lane & 31, k = lane >> 5;  // A: table row v = mv, lookup row k; B: column mv
+  const int bag = sg.kind == RS_SEG_POOL ? sg.bag : 1;
+  const float sc = sg.kind == RS_SEG_POOL && sg.pool_mode == RS_POOL_MEAN ? 1.f / (float)bag : 1.f;
+  const int64_t pad = sg.pad_idx;
+  floatx16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  const int64_t nw = (int64_t)nblk * 4;
+  for (int64_t r0 = ((int64_t)lb * 4 + w) * kOneHotRows; r0 < a.rows; r0 += nw * kOneHotRows) {
+    float av[kOneHotRows / 2], bv[kOneHotRows / 2];
+#pragma unroll
+    for (int u = 0; u < kOneHotRows / 2; ++u) {
+      const int64_t row = r0 + 2 * u + k;
+      const bool ok = row < a.rows;
+      const int64_t* ids = sg.idx + (ok ? row : 0) * sg.idx_stride;
+      int cnt = 0;
+      for (int l = 0; l < bag; ++l) {
+        const int64_t id = ids[l];
+        cnt += (ok && id == mv && id != pad) ? 1 : 0;
+      }
+      av[u] = (float)cnt * sc;
+      bv[u] = ok && mv < sg.dim ? a.dout[(ok ? row : 0) * a.ldo + sg.out_col + mv] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kOneHotRows / 2; ++u)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+  }
+  // C[v][c]: lane l, element e -> v = (e & 3) + 8 (e >> 2) + 4 (l >> 5), c = l & 31
+#pragma unroll
+  for (int e = 0; e < 16; ++e) red[w][((e & 3) + 8 * (e >> 2) + 4 * k) * 32 + mv] = acc[e];
+  __syncthreads();
+  const int n = (int)(sg.vocab * sg.dim);
+  float* dst = a.ws + a.pws_off[s] + (int64_t)lb * n;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const int v = i / sg.dim, c = i - v * sg.dim;
+    dst[i] = ((red[0][v * 32 + c] + red[1][v * 32 + c]) + red[2][v * 32 + c]) + red[3][v * 32 + c];
+  }
+}
+
+// LDS-image table gradient of hot mid-size tables: no atomics, deterministic. C2's 3,500 x 32
+// hist_movie_ids table gets 204,800 token lookups per step (~58 per row); the atomic scatter
+// serialises on the hot rows' L2 lines (90 us per step). A workgroup owns one RANGE of table rows
+// (rrows[s] rows = 64 KB of LDS) x one CHUNK of the lookups:
+//  1. the chunk's ids are staged into LDS 8,192 at a time as int16 local rows (-1 outside the
+//     range or padding);
+//  2. wave w owns the rows with local row % 16 == w: it scans the staged ids (8 per lane per LDS
+//     read) in a fixed order and queues its hits (ballot + mbcnt);
+//  3. D/4 lanes per queued lookup read its dout row (float4 slices, 4 steps of G = 64 / (D/4)
+//     lookups in flight) and add it into the image by plain LDS read-modify-write: a row belongs
+//     to one wave, and lookups of the same row inside one step are applied one group at a time in
+//     queue order, so every row is summed in the same order every time;
+//  4. the image is written whole to ws[chunk] and reduce_partials_kernel adds the chunks in order.
+// Every dout row is read once and the gradient is bitwise reproducible. LDS float atomics were
+// measured first (the same plan with ds_add_f32): ~0.5 lane-adds per clock per CU whatever the bank
+// pattern, 61 us at C2's shape. Block order is XCD-aware: the ranges of one chunk (which read the
+// same ids) share an XCD.
+constexpr int kRangeBytes = 64 * 1024;
+constexpr int kRangeThreads = 1024;
+constexpr int kRangeWaves = kRangeThreads / 64;
+constexpr int kRangeIds = 8192;    // ids staged per pass (LDS, int16 local rows)
+constexpr int kRangeQueue = 1024;  // per-wave queue entries
+
+__device__ __forceinline__ int64_t lookup_id(const rs_feature_seg_t& sg, int64_t e) {
+  if (sg.kind == RS_SEG_POOL) {
+    const int64_t r = e / sg.bag;
+    return sg.idx[r * sg.idx_stride + (e - r * sg.bag)];
+  }
+  return sg.idx[e * sg.idx_stride];
+}
+
+__device__ __forceinline__ void range_rmw(float* lds, int loc, int D, int c4, float4 v, float scale) {
+  float4* d = reinterpret_cast<float4*>(lds + loc * D + c4);
+  float4 x = *d;
+  x.x += v.x * scale; x.y += v.y * scale; x.z += v.z * scale; x.w += v.w * scale;
+  *d = x;
+}
+
+__global__ __launch_bounds__(kRangeThreads) void gather_bwd_range_kernel(SegLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // the range image [R][D]
+  __shared__ __attribute__((aligned(16))) short sid[kRangeIds];
+  __shared__ int queue[kRangeWaves][kRangeQueue];
+  int s = 0;
+  while (s + 1 < a.nseg && (int)blockIdx.x >= a.rblock_start[s + 1]) ++s;
+  const rs_feature_seg_t& sg = a.segs[s];
+  const int lb = blockIdx.x - a.rblock_start[s];
+  const int nr = a.rranges[s], nch = a.rchunks[s];
+  // lb -> (range, chunk): xcd = lb % 8 is the chunk's residue, so the ranges of a chunk share it
+  const int xcd = lb & 7, slot = lb >> 3;
+  const int range = slot % nr, chunk = (slot / nr) * 8 + xcd;
+  const int R = a.rrows[s], D = sg.dim;
+  const int64_t v0 = (int64_t)range * R;
+  const int nrow = (int)(sg.vocab - v0 < R ? sg.vocab - v0 : R);
+  const int nel = nrow * D;  // a multiple of 4
+  for (int i = threadIdx.x * 4; i < nel; i += 4 * kRangeThreads)
+    *reinterpret_cast<float4*>(lds + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int64_t n = (int64_t)a.rows * (sg.kind == RS_SEG_POOL ? sg.bag : 1);
+  const int64_t per = (n + nch - 1) / nch;
+  const int64_t e0 = (int64_t)chunk * per, e1 = e0 + per < n ? e0 + per : n;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int C = D / 4, G = 64 / C;  // lanes per lookup (a float4 of columns each), lookups per step
+  const int g = lane / C, c4 = (lane % C) * 4;
+  const float scale = sg.kind == RS_SEG_POOL && sg.pool_mode == RS_POOL_MEAN ? 1.f / (float)sg.bag : 1.f;
+  const int bag = sg.kind == RS_SEG_POOL ? sg.bag : 1;
+  const int64_t pad = sg.pad_idx;
+  int* q = queue[w];
+  for (int64_t p0 = e0; p0 < e1; p0 += kRangeIds) {
+    const int np = (int)(e1 - p0 < kRangeIds ? e1 - p0 : kRangeIds);
+    __syncthreads();  // the image is zeroed / the previous pass's scans are done with sid
+#pragma unroll
+    for (int u = 0; u < kRangeIds / kRangeThreads; ++u) {
+      const int i = u * kRangeThreads + threadIdx.x;
+      const int64_t id = i < np ? lookup_id(sg, p0 + i) : -1;
+      const int64_t loc = id - v0;
+      sid[i] = (short)((i < np && loc >= 0 && loc < nrow && id != pad) ? (int)loc : -1);
+    }
+    __syncthreads();
+    int nq = 0;
+    // 8 staged ids per lane per LDS read (ids b + 8 lane + u): the queue order is fixed, so each
+    // row's lookups are always summed in the same order
+    for (int b = 0; b < np; b += 512) {
+      const int4 raw = *reinterpret_cast<const int4*>(&sid[b + 8 * lane]);  // sid is -1 past np
+      const int packed[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int loc = (int)(short)(packed[u >> 1] >> (16 * (u & 1)));
+        const bool hit = loc >= 0 && (loc & (kRangeWaves - 1)) == w;
+        const uint64_t m = __ballot(hit);
+        const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        if (hit) q[nq + pos] = ((b + 8 * lane + u) << 14) | loc;  // i < 8192, loc < 16384
+        nq += __popcll(m);
+      }
+      if (nq <= kRangeQueue - 512 && b + 512 < np) continue;  // wave-uniform
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      for (int j = 0; j < nq; j += 4 * G) {
+        float4 v[4];
+        int lk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int qi = j + k * G + g;
+          const bool ok = qi < nq;
+          const int ent = q[ok ? qi : 0];
+          lk[k] = ok ? (ent & 0x3fff) : -1;
+          const int64_t row = (p0 + (ent >> 14)) / bag;
+          v[k] = *reinterpret_cast<const float4*>(a.dout + (ok ? row : 0) * a.ldo + sg.out_col + c4);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          // another group earlier in this step on the same row: apply the step group by group
+          bool dup = false;
+          for (int gg = 0; gg < G; ++gg) {
+            const int o = __shfl(lk[k], gg * C);
+            dup |= gg < g && o == lk[k] && o >= 0;
+          }
+          if (__ballot(dup) == 0) {
+            if (lk[k] >= 0) range_rmw(lds, lk[k], D, c4, v[k], scale);
+          } else {
+            for (int gg = 0; gg < G; ++gg) {
+              if (g == gg && lk[k] >= 0) range_rmw(lds, lk[k], D, c4, v[k], scale);
+              __builtin_amdgcn_wave_barrier();
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      nq = 0;
+    }
+  }
+  __syncthreads();
+  float* dst = a.ws + a.pws_off[s] + (int64_t)chunk * sg.vocab * D + v0 * D;
+  for (int i = threadIdx.x * 4; i < nel; i += 4 * kRangeThreads)
+    *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(lds + i);
+}
+
+// grad[e] += sum of the partials ws[k][e] over k (small and ranged tables), in a fixed order:
+// a 1024-thread workgroup takes 64 float4 elements of every partial segment; wave w sums the
+// partials k = w, w + 16, ... in k order, the 16 wave sums are added in wave order through LDS.
+constexpr int kReduceWaves = 16;
+__global__ __launch_bounds__(kReduceWaves * 64) void reduce_partials_kernel(SegLaunch a) {
+  __shared__ float4 red[kReduceWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int s = 0; s < a.nseg; ++s) {
+    const int nch = a.pchunks[s];
+    if (!nch) continue;
+    const rs_feature_seg_t& sg = a.segs[s];
+    const int64_t n = sg.vocab * sg.dim;
+    const int64_t n4 = n / 4;
+    const float* src = a.ws + a.pws_off[s];
+    const bool v4 = (n & 3) == 0;
+    const int64_t nel = v4 ? n4 : n;  // float4 elements (scalar when vocab * dim % 4 != 0)
+    for (int64_t base = (int64_t)blockIdx.x * 64; base < nel; base += (int64_t)gridDim.x * 64) {
+      const int64_t i = base + lane;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < nel) {
+        for (int k0 = w; k0 < nch; k0 += 8 * kReduceWaves) {
+          float4 t[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int k = k0 + u * kReduceWaves;
+            if (k >= nch) { t[u] = make_float4(0.f, 0.f, 0.f, 0.f); continue; }
+            if (v4) t[u] = reinterpret_cast<const float4*>(src + (int64_t)k * n)[i];
+            else t[u] = make_float4(src[(int64_t)k * n + i], 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            acc.x += t[u].x; acc.y += t[u].y; acc.z += t[u].z; acc.w += t[u].w;
+          }
+        }
+      }
+      red[w][lane] = acc;
+      __syncthreads();
+      if (w == 0 && i < nel) {
+        float4 r = red[0][lane];
+        for (int q = 1; q < kReduceWaves; ++q) {
+          const float4 t = red[q][lane];
+          r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
+        }
+        if (v4) {
+          float4* g = reinterpret_cast<float4*>(sg.grad) + i;
+          float4 o = *g;
+          o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+          *g = o;
+        } else {
+          sg.grad[i] += r.x;
+        }
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -401,6 +670,37 @@ __global__ __launch_bounds__(1024) void dense_bwd_kernel(SegLaunch a) {
   }
 }
 
+// Ranged table-gradient plan of one segment (0 ranges: the atomic scatter). Sparse ids and sum /
+// mean bags of a table of 48 KB - 4 MB (smaller ones: the small-table kernel) hit >= 8 times per
+// row on average, D in {16, 32, 64, 128, 256} (D/4 lanes per lookup divide a wave into <= 16
+// groups); ranges of 64 KB; chunks of >= 2 x vocab lookups (the [vocab, dim] partial of a chunk
+// costs no more than its dout rows), a multiple of 8 (XCD mapping), at most 1024 / ranges.
+struct RangePlan { int rows, ranges, chunks; };
+
+RangePlan range_plan(const rs_feature_seg_t& g, int rows, bool vec) {
+  RangePlan r{0, 0, 0};
+  const bool table_kind = g.kind == RS_SEG_SPARSE || (g.kind == RS_SEG_POOL && g.pool_mode != RS_POOL_MAX);
+  const bool dim_ok = g.dim >= 16 && g.dim <= 256 && 256 % g.dim == 0;
+  const int64_t tbytes = g.vocab * g.dim * 4;
+  const int64_t n = (int64_t)rows * (g.kind == RS_SEG_POOL ? g.bag : 1);
+  if (!table_kind || !vec || !dim_ok || tbytes <= kSmallTableBytes || tbytes > (4 << 20) ||
+      n < 8 * g.vocab || getenv_flag("RSYS_NO_RANGE_GRAD"))
+    return r;
+  int R = kRangeBytes / (g.dim * 4);
+  const int nr = (int)((g.vocab + R - 1) / R);
+  R = (int)((g.vocab + nr - 1) / nr);  // balanced ranges
+  int nch = (int)(n / (2 * g.vocab)) / 8 * 8;
+  const int one_pass = (cdiv(n, kRangeIds) + 7) / 8 * 8;  // every chunk staged in one pass
+  if (nch < one_pass) nch = one_pass;
+  const int cap = (1024 / nr) / 8 * 8;
+  if (nch > cap) nch = cap;
+  if (nch < 8) nch = 8;
+  r.rows = R;
+  r.ranges = nr;
+  r.chunks = nch;
+  return r;
+}
+
 int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, int ldo,
          const float* out_ptr_for_align, bool bwd = false) {
   RS_CHECK_ARG(nseg >= 1 && nseg <= kMaxSeg, "gather: nseg %d out of [1,%d]", nseg, kMaxSeg);
@@ -421,7 +721,9 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.vec[s] = vec;
     a.chunks[s] = C;
     const bool table_kind = g.kind == RS_SEG_SPARSE || g.kind == RS_SEG_POOL;
-    a.small[s] = bwd && table_kind && g.vocab * g.dim * 4 <= kSmallTableBytes;
+    a.onehot[s] = bwd && table_kind && !(g.kind == RS_SEG_POOL && g.pool_mode == RS_POOL_MAX) &&
+                  g.vocab <= 32 && g.dim <= 32 && getenv_flag("RSYS_ONEHOT_GRAD");
+    a.small[s] = bwd && table_kind && g.vocab * g.dim * 4 <= kSmallTableBytes && !a.onehot[s];
     // Split long sum/mean bags over S row groups while the launch is short of ~8 waves per SIMD
     // and every group keeps >= 8 positions (C3: B = 4096, L = 50, D = 128 -> S = 4).
     int S = 1;
@@ -441,10 +743,43 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
         if (a.stage[s] > a.stage_lds) a.stage_lds = a.stage[s];
       }
     }
+    a.rranges[s] = 0;
+    a.rchunks[s] = 0;
+    a.rrows[s] = 0;
+    if (bwd && !a.small[s]) {
+      const RangePlan rp = range_plan(g, rows, vec);
+      a.rrows[s] = rp.rows;
+      a.rranges[s] = rp.ranges;
+      a.rchunks[s] = rp.chunks;
+    }
     a.block_start[s] = blocks;
-    if (!a.small[s]) blocks += cdiv(rows, a.rpb[s]);
+    if (!a.small[s] && !a.rranges[s] && !a.onehot[s]) blocks += cdiv(rows, a.rpb[s]);
   }
   a.block_start[nseg] = blocks;
+  int rb = 0;
+  a.range_lds = 0;
+  for (int s = 0; s < nseg; ++s) {
+    a.rblock_start[s] = rb;
+    if (a.rranges[s]) {
+      rb += a.rranges[s] * a.rchunks[s];
+      const int bytes = a.rrows[s] * segs_host[s].dim * 4;
+      if (bytes > a.range_lds) a.range_lds = bytes;
+    }
+  }
+  a.rblock_start[nseg] = rb;
+  int ob = 0;
+  for (int s = 0; s < nseg; ++s) {
+    a.oblock_start[s] = ob;
+    a.oblocks[s] = 0;
+    if (a.onehot[s]) {  // >= 32 lookup rows per wave, at most 512 workgroups
+      int nb = cdiv(rows, 128);
+      a.oblocks[s] = (int16_t)(nb > 512 ? 512 : nb);
+      ob += a.oblocks[s];
+    }
+  }
+  a.oblock_start[nseg] = ob;
+  a.ws = nullptr;
+
   int sb = 0;
   a.small_lds = 0;
   for (int s = 0; s < nseg; ++s) {
@@ -464,6 +799,14 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     }
   }
   a.sblock_start[nseg] = sb;
+  int64_t off = 0;
+  for (int s = 0; s < nseg; ++s) {
+    a.pchunks[s] = a.rranges[s] ? a.rchunks[s] : (a.onehot[s] ? a.oblocks[s] : 0);
+    a.pws_off[s] = off;
+    off += (int64_t)a.pchunks[s] * segs_host[s].vocab * segs_host[s].dim;
+    off = (off + 3) / 4 * 4;  // float4-aligned partials
+  }
+  a.ws_floats = off;
   a.nseg = nseg;
   a.rows = rows;
   a.ldo = ldo;
@@ -510,14 +853,21 @@ extern "C" int rs_gather_fwd(const rs_feature_seg_t* segs, int nseg, int rows, f
   return 0;
 }
 
+// rs_gather_bwd's workspace: the small and ranged tables' partials. Planned with float4-aligned
+// dout rows (the condition under which a segment is ranged at all): an upper bound.
 extern "C" int64_t rs_gather_ws_bytes(const rs_feature_seg_t* segs_host, int nseg, int rows) {
-  (void)segs_host; (void)nseg; (void)rows;
-  return 0;
+  if (!segs_host || nseg < 1 || nseg > kMaxSeg || rows <= 0) return 0;
+  int ldo = 4;
+  for (int s = 0; s < nseg; ++s) ldo = std::max(ldo, segs_host[s].out_col + segs_host[s].dim);
+  ldo = (ldo + 3) / 4 * 4;
+  SegLaunch a;
+  alignas(16) static const float dummy[4] = {0.f, 0.f, 0.f, 0.f};
+  if (plan(a, segs_host, nseg, rows, ldo, dummy, true) != 0) return 0;
+  return a.ws_floats * 4;
 }
 
 extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, const float* dout,
                              int ldo, float* ws, void* stream) {
-  (void)ws;
   RS_CHECK_ARG(segs && dout, "rs_gather_bwd: null pointer");
   const rs_feature_seg_t* segs_host = segs;
   if (rows == 0) return 0;
@@ -530,6 +880,9 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
   }
   for (int i = 0; i < nseg; ++i) a.segs[i] = segs[i];
   a.out = nullptr; a.dout = dout; a.err = nullptr;
+  a.ws = ws;
+  RS_CHECK_ARG(ws || a.ws_floats == 0,
+               "rs_gather_bwd: small / ranged table gradients need ws (rs_gather_ws_bytes)");
   hipStream_t st = as_stream(stream);
   if (a.block_start[nseg] > 0) {
     gather_bwd_kernel<<<a.block_start[nseg], 256, 0, st>>>(a);
@@ -538,6 +891,21 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
   if (a.sblock_start[nseg] > 0) {
     gather_bwd_small_kernel<<<a.sblock_start[nseg], 256, a.small_lds, st>>>(a);
     RS_CHECK_LAUNCH("rs_gather_bwd small");
+  }
+  if (a.rblock_start[nseg] > 0) {
+    gather_bwd_range_kernel<<<a.rblock_start[nseg], kRangeThreads, a.range_lds, st>>>(a);
+    RS_CHECK_LAUNCH("rs_gather_bwd range");
+  }
+  if (a.oblock_start[nseg] > 0) {
+    gather_bwd_onehot_kernel<<<a.oblock_start[nseg], 256, 0, st>>>(a);
+    RS_CHECK_LAUNCH("rs_gather_bwd onehot");
+  }
+  if (a.ws_floats > 0) {
+    int64_t nel = 0;
+    for (int s = 0; s < nseg; ++s)
+      if (a.pchunks[s]) nel = std::max<int64_t>(nel, segs_host[s].vocab * segs_host[s].dim / 4 + 1);
+    reduce_partials_kernel<<<(int)std::min<int64_t>(cdiv(nel, 64), 1024), kReduceWaves * 64, 0, st>>>(a);
+    RS_CHECK_LAUNCH("rs_gather_bwd partials");
   }
   bool any_dense = false;
   for (int s = 0; s < nseg; ++s) any_dense |= segs_host[s].kind == RS_SEG_DENSE;

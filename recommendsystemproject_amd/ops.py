@@ -214,7 +214,9 @@ def gather_fwd(segs, rows, out, err_flag=None):
 
 def gather_bwd(segs, rows, dout):
     arr = segments_array(segs)
-    call('rs_gather_bwd', arr, len(segs), rows, P(dout), dout.stride(0), None, stream())
+    # hot mid-size tables (C2's 3,500-row history table) reduce per-chunk partials from ws
+    w = ws(_hip.lib().rs_gather_ws_bytes(arr, len(segs), rows), dout.device)
+    call('rs_gather_bwd', arr, len(segs), rows, P(dout), dout.stride(0), P(w), stream())
 
 
 STREAM_BF16_MIN_ROWS = 32768  # gemm_stream.hip kSmallM: the bf16-storage GEMM instances are big-M only

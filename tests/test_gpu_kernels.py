@@ -200,6 +200,65 @@ def test_gather_backward_matches_embedding_backward(V):
     assert (g[0] == 0).all()
 
 
+@pytest.mark.parametrize('V,D,rows,Lb,mode', [(3500, 32, 204800, 1, None), (5001, 64, 50000, 1, None),
+                                               (3000, 16, 20000, 20, 'mean'), (2000, 8, 9000, 7, 'sum'),
+                                               (70000, 4, 600000, 1, None), (30, 8, 204800, 3, 'mean'),
+                                               (25, 8, 4096, 1, None), (700, 16, 4096, 1, None),
+                                               (3, 4, 5000, 1, None), (40, 64, 3000, 5, 'sum')])
+def test_gather_backward_ranged_hot_tables(monkeypatch, V, D, rows, Lb, mode):
+    """Hot mid-size tables (48 KB - 4 MB, >= 8 lookups per row, D in 16..256: C2's 3,500 x 32
+    history table at 204,800 token lookups) take the ranged LDS path (gather.hip
+    gather_bwd_range_kernel: row-owner waves, chunk partials reduced in order; bitwise
+    reproducible); tables of <= 32 rows x <= 32 columns the one-hot MFMA kernel (bitwise
+    reproducible); the other cases check the small-table kernel and the atomic scatter: against the embedding backward and the atomic scatter
+    (RSYS_NO_RANGE_GRAD=1), padding row skipped, out-of-range ids ignored, grad accumulated (+=)."""
+    t = rnd(V, D, seed=31).requires_grad_(True)
+    shape = (rows,) if mode is None else (rows, Lb)
+    ids = torch.randint(0, V, shape, device=DEV)
+    ids.view(-1)[::97] = 0  # padding row
+    ids.view(-1)[:64] = min(17, V - 1)  # one hot row many times in one wave
+    kind = _hip.RS_SEG_SPARSE if mode is None else _hip.RS_SEG_POOL
+    ldo = D + 8
+    dout = rnd(rows, ldo, seed=32)
+    emb = F.embedding(ids, t, padding_idx=0)
+    ref = emb if mode is None else (emb.mean(1) if mode == 'mean' else emb.sum(1))
+    ref.backward(dout[:, 4:4 + D])
+    seg = dict(kind=kind, dim=D, out_col=4, vocab=V, idx_stride=1 if mode is None else Lb, idx=ids.data_ptr(),
+               table=t.data_ptr(), pad_idx=0)
+    if mode is not None:
+        seg.update(pool_mode=_hip.RS_POOL[mode], bag=Lb)
+    arr = ops.segments_array([_seg(**seg)])
+    n = rows * Lb
+    ranged = 48 * 1024 < V * D * 4 <= 4 << 20 and D >= 16 and n >= 8 * V
+    onehot = V <= 32 and D <= 32  # tiny tables: the one-hot MFMA kernel (RSYS_ONEHOT_GRAD=1)
+    assert (_hip.lib().rs_gather_ws_bytes(arr, 1, rows) > 0) == ranged  # partials in ws
+    grads = []
+    # the planned path twice, the one-hot kernel twice, the atomic / small-table scatter
+    for off, oh in (('', ''), ('', ''), ('', '1'), ('', '1'), ('1', '')):
+        monkeypatch.setenv('RSYS_NO_RANGE_GRAD', off)
+        monkeypatch.setenv('RSYS_ONEHOT_GRAD', oh)
+        g = torch.full((V, D), 0.25, device=DEV)
+        ops.gather_bwd([_seg(**seg, grad=g.data_ptr())], rows, dout)
+        grads.append(g)
+    monkeypatch.setenv('RSYS_NO_RANGE_GRAD', '')
+    monkeypatch.setenv('RSYS_ONEHOT_GRAD', '')
+    scale = max(1.0, t.grad.abs().max().item())
+    for gr in grads:
+        assert (gr - 0.25 - t.grad).abs().max().item() <= 2e-5 * scale
+        assert (gr[0] == 0.25).all()
+    if ranged:  # ranged and one-hot gradients are bitwise reproducible
+        assert torch.equal(grads[0], grads[1])
+    if onehot:
+        assert torch.equal(grads[2], grads[3])
+    # out-of-range / negative ids contribute nothing and do not fault
+    bad = ids.clone()
+    bad.view(-1)[5] = V + 100
+    bad.view(-1)[6] = -3
+    g = torch.zeros(V, D, device=DEV)
+    ops.gather_bwd([_seg(**dict(seg, idx=bad.data_ptr()), grad=g.data_ptr())], rows, dout)
+    assert torch.isfinite(g).all()
+
+
 @pytest.mark.parametrize('B,D,Lb,mode', [(300, 128, 50, 'mean'), (300, 128, 50, 'sum'), (257, 64, 17, 'mean'),
                                           (4096, 128, 50, 'mean'), (5, 128, 33, 'mean')])
 def test_pooled_split_bags(B, D, Lb, mode):
