@@ -53,9 +53,9 @@ struct SegLaunch {
   int16_t rranges[kMaxSeg];
   int16_t rchunks[kMaxSeg];
   int rblock_start[kMaxSeg + 1];
-  uint8_t onehot[kMaxSeg];   // bwd: tiny table by the one-hot MFMA kernel
-  int16_t oblocks[kMaxSeg];
-  int oblock_start[kMaxSeg + 1];
+  uint8_t tiny[kMaxSeg];   // bwd: tiny table by the register-accumulator kernel
+  int16_t tblocks[kMaxSeg];
+  int tblock_start[kMaxSeg + 1];
   // bwd partials (small and ranged tables): [pchunks][vocab][dim] floats at ws + pws_off
   int16_t pchunks[kMaxSeg];
   int64_t pws_off[kMaxSeg];
@@ -373,63 +373,70 @@ __global__ __launch_bounds__(256) void gather_bwd_small_kernel(SegLaunch a) {
   }
 }
 
-// Tiny tables (V <= 32 rows, D <= 32: C2's genre / age / occupation / gender tables) by one f32
-// MFMA per two lookup rows: dT[V, D] = Cnt^T dout, where Cnt[row][v] = number of the row's bag
-// ids equal to v (padding skipped; times 1/bag for a mean bag). v_mfma_f32_32x32x2_f32: lane l
-// supplies A[v = l % 32][k = l / 32] = Cnt[row_k][v] and B[k][c = l % 32] = dout[row_k][c]; the
-// products are exact (small integer counts) and accumulate in fp32. Each wave owns rows w, w + W,
-// ...; the 4 waves' tiles are summed in wave order through LDS, the workgroup's tile goes to
-// ws[block] and reduce_partials_kernel adds the blocks in order: bitwise reproducible, unlike the
-// small-table kernel's atomics. Opt-in (RSYS_ONEHOT_GRAD=1): at C2's 30 x 8 genre table (614,400
-// bag ids) it measured 45 + 8 us against the small-table kernel's 33 us (latency-bound: ~100 rows
-// per wave in steps of 32, each step one round trip for the ids and the dout column).
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-constexpr int kOneHotRows = 32;  // lookup rows per wave step (16 MFMAs, loads issued together)
+// Tiny tables (<= 32 rows, D | 64, bags of <= 4 ids: C2's genre / age / occupation / gender
+// tables): per-lane register accumulators instead of LDS float atomics (which run at ~0.5
+// lane-adds per clock per CU: C2's 30 x 8 genre table, 614,400 bag ids per step, took 33 us in
+// the small-table kernel). Lane (stream, c) owns column c of a stream of lookup rows and keeps
+// acc[v] for every table row v: each bag id adds its row's dout column to acc[id] by 32
+// compare-selects (VALU is idle here; 147 M selects at C2 are ~1 us of the chip). Rows are taken
+// 8 at a time with their ids and dout columns loaded together. The streams of a workgroup are
+// summed in stream order through LDS, the workgroup's [V, D] tile goes to ws[block], and
+// reduce_partials_kernel adds the blocks in order: bitwise reproducible, unlike the small-table
+// kernel's atomics. Opt-in (RSYS_TINY_GRAD=1): at C2's genre table it measured 46 + 8 us against
+// the small-table kernel's 33 us (a one-hot f32-MFMA variant, Cnt^T dout on 32x32x2 tiles, 45 us:
+// both latency-bound at ~100 lookup rows per wave).
+constexpr int kTinyRows = 32;
+constexpr int kTinyBag = 4;
+constexpr int kTinyUnroll = 8;
 
-__global__ __launch_bounds__(256) void gather_bwd_onehot_kernel(SegLaunch a) {
-  __shared__ float red[4][32 * 32];
+__global__ __launch_bounds__(256) void gather_bwd_tiny_kernel(SegLaunch a) {
+  __shared__ float red[256][kTinyRows + 1];
   int s = 0;
-  while (s + 1 < a.nseg && (int)blockIdx.x >= a.oblock_start[s + 1]) ++s;
+  while (s + 1 < a.nseg && (int)blockIdx.x >= a.tblock_start[s + 1]) ++s;
   const rs_feature_seg_t& sg = a.segs[s];
-  const int lb = blockIdx.x - a.oblock_start[s];
-  const int nblk = a.oblocks[s];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int mv = lane & 31, k = lane >> 5;  // A: table row v = mv, lookup row k; B: column mv
+  const int lb = blockIdx.x - a.tblock_start[s];
+  const int nblk = a.tblocks[s];
+  const int D = sg.dim;
+  const int c = threadIdx.x % D, str = threadIdx.x / D, nstr = 256 / D;
   const int bag = sg.kind == RS_SEG_POOL ? sg.bag : 1;
   const float sc = sg.kind == RS_SEG_POOL && sg.pool_mode == RS_POOL_MEAN ? 1.f / (float)bag : 1.f;
   const int64_t pad = sg.pad_idx;
-  floatx16 acc;
+  const int64_t step = (int64_t)nblk * nstr;
+  float acc[kTinyRows];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-  const int64_t nw = (int64_t)nblk * 4;
-  for (int64_t r0 = ((int64_t)lb * 4 + w) * kOneHotRows; r0 < a.rows; r0 += nw * kOneHotRows) {
-    float av[kOneHotRows / 2], bv[kOneHotRows / 2];
+  for (int v = 0; v < kTinyRows; ++v) acc[v] = 0.f;
+  for (int64_t r0 = (int64_t)lb * nstr + str; r0 < a.rows; r0 += step * kTinyUnroll) {
+    float gv[kTinyUnroll];
+    int id[kTinyUnroll][kTinyBag];
 #pragma unroll
-    for (int u = 0; u < kOneHotRows / 2; ++u) {
-      const int64_t row = r0 + 2 * u + k;
+    for (int u = 0; u < kTinyUnroll; ++u) {
+      const int64_t row = r0 + u * step;
       const bool ok = row < a.rows;
-      const int64_t* ids = sg.idx + (ok ? row : 0) * sg.idx_stride;
-      int cnt = 0;
-      for (int l = 0; l < bag; ++l) {
-        const int64_t id = ids[l];
-        cnt += (ok && id == mv && id != pad) ? 1 : 0;
+      const int64_t rr = ok ? row : 0;
+      gv[u] = ok ? a.dout[rr * a.ldo + sg.out_col + c] * sc : 0.f;
+#pragma unroll
+      for (int l = 0; l < kTinyBag; ++l) {
+        const int64_t x = ok && l < bag ? sg.idx[rr * sg.idx_stride + l] : -1;
+        id[u][l] = (x == pad || x < 0 || x >= kTinyRows) ? -1 : (int)x;
       }
-      av[u] = (float)cnt * sc;
-      bv[u] = ok && mv < sg.dim ? a.dout[(ok ? row : 0) * a.ldo + sg.out_col + mv] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < kOneHotRows / 2; ++u)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
-  }
-  // C[v][c]: lane l, element e -> v = (e & 3) + 8 (e >> 2) + 4 (l >> 5), c = l & 31
+    for (int u = 0; u < kTinyUnroll; ++u)
 #pragma unroll
-  for (int e = 0; e < 16; ++e) red[w][((e & 3) + 8 * (e >> 2) + 4 * k) * 32 + mv] = acc[e];
+      for (int l = 0; l < kTinyBag; ++l)
+#pragma unroll
+        for (int v = 0; v < kTinyRows; ++v) acc[v] += id[u][l] == v ? gv[u] : 0.f;
+  }
+#pragma unroll
+  for (int v = 0; v < kTinyRows; ++v) red[threadIdx.x][v] = acc[v];
   __syncthreads();
-  const int n = (int)(sg.vocab * sg.dim);
+  const int n = (int)(sg.vocab * D);
   float* dst = a.ws + a.pws_off[s] + (int64_t)lb * n;
   for (int i = threadIdx.x; i < n; i += 256) {
-    const int v = i / sg.dim, c = i - v * sg.dim;
-    dst[i] = ((red[0][v * 32 + c] + red[1][v * 32 + c]) + red[2][v * 32 + c]) + red[3][v * 32 + c];
+    const int v = i / D, cc = i - v * D;
+    float t = 0.f;
+    for (int k = 0; k < nstr; ++k) t += red[k * D + cc][v];
+    dst[i] = t;
   }
 }
 
@@ -721,9 +728,10 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.vec[s] = vec;
     a.chunks[s] = C;
     const bool table_kind = g.kind == RS_SEG_SPARSE || g.kind == RS_SEG_POOL;
-    a.onehot[s] = bwd && table_kind && !(g.kind == RS_SEG_POOL && g.pool_mode == RS_POOL_MAX) &&
-                  g.vocab <= 32 && g.dim <= 32 && getenv_flag("RSYS_ONEHOT_GRAD");
-    a.small[s] = bwd && table_kind && g.vocab * g.dim * 4 <= kSmallTableBytes && !a.onehot[s];
+    a.tiny[s] = bwd && table_kind && !(g.kind == RS_SEG_POOL && g.pool_mode == RS_POOL_MAX) &&
+               g.vocab <= kTinyRows && g.dim <= 64 && 64 % g.dim == 0 &&
+               (g.kind == RS_SEG_SPARSE || g.bag <= kTinyBag) && getenv_flag("RSYS_TINY_GRAD");
+    a.small[s] = bwd && table_kind && g.vocab * g.dim * 4 <= kSmallTableBytes && !a.tiny[s];
     // Split long sum/mean bags over S row groups while the launch is short of ~8 waves per SIMD
     // and every group keeps >= 8 positions (C3: B = 4096, L = 50, D = 128 -> S = 4).
     int S = 1;
@@ -753,7 +761,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
       a.rchunks[s] = rp.chunks;
     }
     a.block_start[s] = blocks;
-    if (!a.small[s] && !a.rranges[s] && !a.onehot[s]) blocks += cdiv(rows, a.rpb[s]);
+    if (!a.small[s] && !a.rranges[s] && !a.tiny[s]) blocks += cdiv(rows, a.rpb[s]);
   }
   a.block_start[nseg] = blocks;
   int rb = 0;
@@ -769,15 +777,15 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
   a.rblock_start[nseg] = rb;
   int ob = 0;
   for (int s = 0; s < nseg; ++s) {
-    a.oblock_start[s] = ob;
-    a.oblocks[s] = 0;
-    if (a.onehot[s]) {  // >= 32 lookup rows per wave, at most 512 workgroups
-      int nb = cdiv(rows, 128);
-      a.oblocks[s] = (int16_t)(nb > 512 ? 512 : nb);
-      ob += a.oblocks[s];
+    a.tblock_start[s] = ob;
+    a.tblocks[s] = 0;
+    if (a.tiny[s]) {  // >= 16 lookup rows per stream, at most 256 workgroups
+      int nb = cdiv(rows, 16 * (256 / segs_host[s].dim));
+      a.tblocks[s] = (int16_t)(nb > 256 ? 256 : nb);
+      ob += a.tblocks[s];
     }
   }
-  a.oblock_start[nseg] = ob;
+  a.tblock_start[nseg] = ob;
   a.ws = nullptr;
 
   int sb = 0;
@@ -801,7 +809,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
   a.sblock_start[nseg] = sb;
   int64_t off = 0;
   for (int s = 0; s < nseg; ++s) {
-    a.pchunks[s] = a.rranges[s] ? a.rchunks[s] : (a.onehot[s] ? a.oblocks[s] : 0);
+    a.pchunks[s] = a.rranges[s] ? a.rchunks[s] : (a.tiny[s] ? a.tblocks[s] : 0);
     a.pws_off[s] = off;
     off += (int64_t)a.pchunks[s] * segs_host[s].vocab * segs_host[s].dim;
     off = (off + 3) / 4 * 4;  // float4-aligned partials
@@ -896,9 +904,9 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
     gather_bwd_range_kernel<<<a.rblock_start[nseg], kRangeThreads, a.range_lds, st>>>(a);
     RS_CHECK_LAUNCH("rs_gather_bwd range");
   }
-  if (a.oblock_start[nseg] > 0) {
-    gather_bwd_onehot_kernel<<<a.oblock_start[nseg], 256, 0, st>>>(a);
-    RS_CHECK_LAUNCH("rs_gather_bwd onehot");
+  if (a.tblock_start[nseg] > 0) {
+    gather_bwd_tiny_kernel<<<a.tblock_start[nseg], 256, 0, st>>>(a);
+    RS_CHECK_LAUNCH("rs_gather_bwd tiny");
   }
   if (a.ws_floats > 0) {
     int64_t nel = 0;

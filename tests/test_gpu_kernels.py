@@ -209,7 +209,7 @@ def test_gather_backward_ranged_hot_tables(monkeypatch, V, D, rows, Lb, mode):
     """Hot mid-size tables (48 KB - 4 MB, >= 8 lookups per row, D in 16..256: C2's 3,500 x 32
     history table at 204,800 token lookups) take the ranged LDS path (gather.hip
     gather_bwd_range_kernel: row-owner waves, chunk partials reduced in order; bitwise
-    reproducible); tables of <= 32 rows x <= 32 columns the one-hot MFMA kernel (bitwise
+    reproducible); tables of <= 32 rows (bags <= 4) the register-accumulator kernel (bitwise
     reproducible); the other cases check the small-table kernel and the atomic scatter: against the embedding backward and the atomic scatter
     (RSYS_NO_RANGE_GRAD=1), padding row skipped, out-of-range ids ignored, grad accumulated (+=)."""
     t = rnd(V, D, seed=31).requires_grad_(True)
@@ -230,25 +230,25 @@ def test_gather_backward_ranged_hot_tables(monkeypatch, V, D, rows, Lb, mode):
     arr = ops.segments_array([_seg(**seg)])
     n = rows * Lb
     ranged = 48 * 1024 < V * D * 4 <= 4 << 20 and D >= 16 and n >= 8 * V
-    onehot = V <= 32 and D <= 32  # tiny tables: the one-hot MFMA kernel (RSYS_ONEHOT_GRAD=1)
+    tiny = V <= 32 and 64 % D == 0 and Lb <= 4  # the register-accumulator kernel (RSYS_TINY_GRAD=1)
     assert (_hip.lib().rs_gather_ws_bytes(arr, 1, rows) > 0) == ranged  # partials in ws
     grads = []
-    # the planned path twice, the one-hot kernel twice, the atomic / small-table scatter
-    for off, oh in (('', ''), ('', ''), ('', '1'), ('', '1'), ('1', '')):
+    # the planned path twice, the tiny-table kernel twice, the atomic / small-table scatter
+    for off, ty in (('', ''), ('', ''), ('', '1'), ('', '1'), ('1', '')):
         monkeypatch.setenv('RSYS_NO_RANGE_GRAD', off)
-        monkeypatch.setenv('RSYS_ONEHOT_GRAD', oh)
+        monkeypatch.setenv('RSYS_TINY_GRAD', ty)
         g = torch.full((V, D), 0.25, device=DEV)
         ops.gather_bwd([_seg(**seg, grad=g.data_ptr())], rows, dout)
         grads.append(g)
     monkeypatch.setenv('RSYS_NO_RANGE_GRAD', '')
-    monkeypatch.setenv('RSYS_ONEHOT_GRAD', '')
+    monkeypatch.setenv('RSYS_TINY_GRAD', '')
     scale = max(1.0, t.grad.abs().max().item())
     for gr in grads:
         assert (gr - 0.25 - t.grad).abs().max().item() <= 2e-5 * scale
         assert (gr[0] == 0.25).all()
-    if ranged:  # ranged and one-hot gradients are bitwise reproducible
+    if ranged:  # ranged and tiny-table gradients are bitwise reproducible
         assert torch.equal(grads[0], grads[1])
-    if onehot:
+    if tiny:
         assert torch.equal(grads[2], grads[3])
     # out-of-range / negative ids contribute nothing and do not fault
     bad = ids.clone()
