@@ -622,6 +622,11 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(
   // one 6 KB image per wave: Q, K and dO pass through it once (column fragments), then it is the
   // transpose buffer of P∘Z, dS and the output tiles
   __shared__ __attribute__((aligned(16))) float Xsm[4][LP * TP];
+  // the Q and dO column fragments (each used once per query tile) wait in LDS, one 8-byte slot
+  // per lane (conflict-free b64 accesses): held in registers they pushed the kernel past its
+  // 168-VGPR budget (3 waves per SIMD) and the spill stores were ~56 MB of scratch writes per
+  // launch at C2 (PMC WRITE_SIZE 135 MB against 79 MB of dqkv)
+  __shared__ __attribute__((aligned(16))) s4v Fsm[4][2][NT][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
   const int bh = blockIdx.x * 4 + wave;
@@ -635,7 +640,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(
   s4v qb[NT], kb[NT], vb[NT], gb[NT];
   float lsei[NT];
   // column fragments (B operands of dQ = dS K, dK = dS^T Q, dV = PZ^T dO) via the LDS image
-  s4v qc[NT], kc[NT], gc[NT];
+  s4v kc[NT];
   {
     f4 qf[NT], kf[NT], gf[NT];
 #pragma unroll
@@ -655,9 +660,14 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(
       for (int t = 0; t < NT; ++t)
         *reinterpret_cast<f4*>(&T[(t * 16 + r) * TP + 4 * q]) = pass == 0 ? qf[t] : (pass == 1 ? kf[t] : gf[t]);
       __builtin_amdgcn_wave_barrier();
-      if (pass == 0) col_frags<NT, TP>(T, r, q, qc);
-      else if (pass == 1) col_frags<NT, TP>(T, r, q, kc);
-      else col_frags<NT, TP>(T, r, q, gc);
+      if (pass == 1) {
+        col_frags<NT, TP>(T, r, q, kc);
+      } else {
+        s4v cf[NT];
+        col_frags<NT, TP>(T, r, q, cf);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) Fsm[wave][pass >> 1][t][lane] = cf[t];
+      }
       __builtin_amdgcn_wave_barrier();
     }
 #pragma unroll
@@ -724,7 +734,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk)
-      dv_acc[tk] = mfma16(bf4(ld4(&T[(tk * 16 + r) * TP + 4 * q])), gc[tq], dv_acc[tk]);
+      dv_acc[tk] = mfma16(bf4(ld4(&T[(tk * 16 + r) * TP + 4 * q])), Fsm[wave][1][tq][lane], dv_acc[tk]);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk)
@@ -733,7 +743,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk)
-      dk_acc[tk] = mfma16(bf4(ld4(&T[(tk * 16 + r) * TP + 4 * q])), qc[tq], dk_acc[tk]);
+      dk_acc[tk] = mfma16(bf4(ld4(&T[(tk * 16 + r) * TP + 4 * q])), Fsm[wave][0][tq][lane], dk_acc[tk]);
     __builtin_amdgcn_wave_barrier();
   }
   // dK / dV rows: acc[e] = X[key 16 tk + 4 q + e][c = r]

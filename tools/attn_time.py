@@ -20,7 +20,7 @@ def main():
     d, H = 64, 4
     dev = torch.device('cuda:0')
     qkv = torch.randn(B * L, 3 * d, device=dev)
-    if ops.qkv_bf16_ok(L, d, H):
+    if ops.qkv_bf16_ok(L, d, H, B * L):
         qkv = qkv.to(torch.bfloat16)
     lens = torch.randint(0, L + 1, (B,), device=dev)
     seq = (torch.arange(L, device=dev)[None, :] < lens[:, None]).long()
