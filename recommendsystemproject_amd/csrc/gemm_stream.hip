@@ -821,20 +821,26 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
   float* sbias = reinterpret_cast<float*>(smem_raw + (size_t)NTN * KPH * 2);
   float* saux = sbias + NTN;  // AUX_ADD table, or LN gamma / beta
   const int tid = threadIdx.x;
+  // K tail (K < KK, K % 4 == 0, fp32 A only): op(B) columns k >= K are staged as zeros and the A
+  // float4s at k >= K are not loaded (zeros), so the padded k slots add exact zeros
+  const int K = a.K;
+  // N tail (N < NTN, N % 4 == 0, no LN): op(B) rows n >= N are zeros and columns n >= N are
+  // neither loaded (epilogue operands) nor stored
+  const int N = a.N;
   if (a.transB) {  // B = W[N][K]: rows n (dispatch: ldb % 4 == 0, 16-byte aligned)
     stage_batched<NTN, KK, 512>(a.B, a.ldb, [&](int n, int k, const floatx4& v) {
       bf16x4w h;
       h[0] = (__bf16)v[0]; h[1] = (__bf16)v[1]; h[2] = (__bf16)v[2]; h[3] = (__bf16)v[3];
       *reinterpret_cast<bf16x4w*>(Bs + n * KPH + k) = h;
-    });
+    }, [&](int n, int k) { return k < K && n < N; });
   } else {  // B = W[K][N]: rows k
     stage_batched<KK, NTN, 512>(a.B, a.ldb, [&](int k, int n, const floatx4& v) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) Bs[(n + e) * KPH + k] = (__bf16)v[e];
-    });
+    }, [&](int k, int n) { return k < K && n < N; });
   }
   if constexpr ((EPI & RS_EPI_BIAS) != 0)
-    for (int n = tid; n < NTN; n += 512) sbias[n] = a.bias[n];
+    for (int n = tid; n < NTN; n += 512) sbias[n] = n < N ? a.bias[n] : 0.f;
   if constexpr (LN) {
     for (int n = tid; n < NTN; n += 512) {
       saux[n] = a.ln_gamma[n];
@@ -843,7 +849,7 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
   } else if constexpr ((EPI & RS_EPI_AUX_ADD) != 0) {
     for (int idx = tid; idx < a.aux_mod * NTN; idx += 512) {
       const int rr = idx / NTN, n = idx % NTN;
-      saux[idx] = a.aux[(int64_t)rr * a.ld_aux + n];
+      saux[idx] = n < N ? a.aux[(int64_t)rr * a.ld_aux + n] : 0.f;
     }
   }
   __syncthreads();
@@ -873,7 +879,9 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
 #pragma unroll
       for (int c = 0; c < KC; ++c)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) dst[c][u] = *(gptr4)(row + 64 * c + 4 * u);
+        for (int u = 0; u < 4; ++u)
+          dst[c][u] = (c + 1) * 64 <= K || 64 * c + 16 * q + 4 * u < K ? *(gptr4)(row + 64 * c + 4 * u)
+                                                                      : floatx4{0.f, 0.f, 0.f, 0.f};
     }
   };
   if (g < groups) load_raw(g, araw);
@@ -890,7 +898,8 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int n0 = t * 16 + 4 * q;
-        if constexpr ((EPI & RS_EPI_AUX_MASK) != 0) epre[t] = *(gptr4)(a.aux + (int64_t)m * a.ld_aux + n0);
+        if (n0 >= N) epre[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+        else if constexpr ((EPI & RS_EPI_AUX_MASK) != 0) epre[t] = *(gptr4)(a.aux + (int64_t)m * a.ld_aux + n0);
         else epre[t] = *(gptr4)(a.C + (int64_t)m * a.ldc + n0);
       }
     }
@@ -942,6 +951,7 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
             auxv = *reinterpret_cast<const floatx4*>(saux + (m % a.aux_mod) * NTN + nl);
           if constexpr ((EPI & RS_EPI_AUX_MASK) != 0) auxv = epre[j0 + h];
           if constexpr ((EPI & kEpiBeta) != 0) cv = epre[j0 + h];
+          if (nl >= N) continue;  // N tail
           const floatx4 v = epi4_ct<EPI>(a, m, nl, acc[h] * a.alpha, ka, kb, biasv, auxv, cv);
           if constexpr (CBF) {
             bf16x4w o;
@@ -1012,12 +1022,14 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   // bf16 compute mode: the bf16-MFMA instances (fp32 kernels below for anything else)
   const int io = ((s.epi & RS_GEMM_A_BF16) ? 1 : 0) | ((s.epi & RS_GEMM_C_BF16) ? 2 : 0);
   const int ekey = (s.epi & ~(RS_GEMM_BF16 | RS_GEMM_A_BF16 | RS_GEMM_C_BF16)) | (s.beta != 0.f ? kEpiBeta : 0);
-  if ((s.epi & RS_GEMM_BF16) && !small && s.vec_epi && s.M % 16 == 0 && s.K % 64 == 0 &&
+  // K: a multiple of 64, or (fp32 A) of 4 with the tail zero-padded in the kernel
+  if ((s.epi & RS_GEMM_BF16) && !small && s.vec_epi && s.M % 16 == 0 &&
+      (s.K % 64 == 0 || (s.K % 4 == 0 && !(io & 1))) &&
       s.ldb % 4 == 0 && aligned16(s.B) &&
-      s.N == nt * 16 && s.lda % ((io & 1) ? 8 : 4) == 0 && (!(io & 1) || aligned16(s.A)) &&
+      (s.N == nt * 16 || (s.N % 4 == 0 && io == 0)) && s.lda % ((io & 1) ? 8 : 4) == 0 && (!(io & 1) || aligned16(s.A)) &&
       (!(s.epi & RS_EPI_AUX_ADD) || (int64_t)s.aux_mod * nt * 16 * 4 <= 48 * 1024)) {
-    const int kc = s.K / 64;
-    const size_t ldsb = (size_t)nt * 16 * (s.K + 8) * 2 + (size_t)(nt * 16 + ((s.epi & RS_EPI_AUX_ADD) ? s.aux_mod * nt * 16 : 0)) * 4;
+    const int kc = (s.K + 63) / 64;
+    const size_t ldsb = (size_t)nt * 16 * (kc * 64 + 8) * 2 + (size_t)(nt * 16 + ((s.epi & RS_EPI_AUX_ADD) ? s.aux_mod * nt * 16 : 0)) * 4;
     const int per_cub = ldsb > 80 * 1024 ? 1 : (ldsb > 53 * 1024 ? 2 : (ldsb > 40 * 1024 ? 3 : 4));
     int bxb = cdiv(s.M / 16, stream_groups_per_wg());
     if (bxb > 256 * per_cub) bxb = 256 * per_cub;
@@ -1029,7 +1041,9 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
     }
     RS_RGB(16, 1, 19, 0) RS_RGB(16, 1, 3, 0) RS_RGB(16, 1, 8, 0) RS_RGB(16, 1, 0, 0) RS_RGB(12, 1, 1, 0)
     RS_RGB(4, 3, 64, 0) RS_RGB(4, 4, 64, 0) RS_RGB(4, 1, 0, 0) RS_RGB(4, 1, 64, 0) RS_RGB(4, 4, 0, 0)
-    RS_RGB(4, 3, 0, 0)
+    RS_RGB(4, 3, 0, 0) RS_RGB(3, 1, 0, 0) RS_RGB(3, 1, 64, 0)
+    // the sequence projection (K = 48 at C2, 72 at C5: zero-padded k tail) and its input gradient
+    RS_RGB(4, 1, 53, 0) RS_RGB(4, 1, 5, 0) RS_RGB(4, 2, 53, 0) RS_RGB(4, 2, 5, 0)
     // bf16 storage: the qkv projection's output (C) and its input gradient's dqkv operand (A)
     RS_RGB(12, 1, 1, 2) RS_RGB(12, 1, 0, 2) RS_RGB(4, 3, 64, 1) RS_RGB(4, 3, 0, 1)
 #undef RS_RGB
