@@ -974,17 +974,32 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
 constexpr int kSmallM = 32768;
 constexpr int kSmallNT = 2;  // small M (the MLP at B = 4096): 32 columns per workgroup
 
-// 16-row groups per workgroup of the big-M streaming GEMMs (8 waves: 4 groups per wave); each
-// workgroup stages the whole weight once, so fewer, longer-lived workgroups re-read less of it.
-// Measured at C2 (token GEMMs per step): 16 groups 0.303 ms, 32 0.288 ms, 48 0.347 ms.
-// RSYS_STREAM_GROUPS overrides (tuning only).
-int stream_groups_per_wg() {
-  static int v = [] {
+// Grid of the big-M streaming GEMMs (persistent workgroups of 8 waves; each stages the whole
+// weight once, so fewer, longer-lived workgroups re-read less of it). The grid is a whole number
+// of workgroups per CU: the row groups are dealt round-robin, so every workgroup gets the same
+// share and the kernel's time is that of the busiest CU. A fixed 32 groups per workgroup gave 400
+// workgroups at C2 (12,800 groups): 144 CUs ran two, 112 one. Measured at C2 (token GEMMs per
+// step): 32 per workgroup 0.280 ms, 25 (512 workgroups) 0.270, 50 (256) 0.264.
+// RSYS_STREAM_GROUPS = g (>= 8) restores a fixed g groups per workgroup (tuning only).
+int stream_grid(int groups, int per_cu, int min_per_wg = 40) {
+  static const int fixed = [] {
     const char* e = getenv("RSYS_STREAM_GROUPS");
     const int x = e ? atoi(e) : 0;
-    return x >= 8 ? x : 32;
+    return x >= 8 ? x : 0;
   }();
-  return v;
+  int bx;
+  if (fixed) {
+    bx = cdiv(groups, fixed);
+    if (bx > 256 * per_cu) bx = 256 * per_cu;
+  } else if (groups <= 256 * 8) {
+    bx = cdiv(groups, 8);  // one row group per wave
+  } else {
+    int k = groups / (256 * min_per_wg);  // >= min_per_wg groups per workgroup
+    if (k < 1) k = 1;
+    if (k > per_cu) k = per_cu;
+    bx = 256 * k;
+  }
+  return bx < 1 ? 1 : bx;
 }
 
 bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda) {
@@ -1031,8 +1046,7 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
     const int kc = (s.K + 63) / 64;
     const size_t ldsb = (size_t)nt * 16 * (kc * 64 + 8) * 2 + (size_t)(nt * 16 + ((s.epi & RS_EPI_AUX_ADD) ? s.aux_mod * nt * 16 : 0)) * 4;
     const int per_cub = ldsb > 80 * 1024 ? 1 : (ldsb > 53 * 1024 ? 2 : (ldsb > 40 * 1024 ? 3 : 4));
-    int bxb = cdiv(s.M / 16, stream_groups_per_wg());
-    if (bxb > 256 * per_cub) bxb = 256 * per_cub;
+    const int bxb = stream_grid(s.M / 16, per_cub);
 #define RS_RGB(NTV, KCV, EV, IOV)                                                                 \
     if (nt == NTV && kc == KCV && ekey == EV && io == IOV) {                                      \
       rowgemm_bf16_kernel<NTV, KCV, false, EV, IOV><<<bxb, 512, ldsb, st>>>(s);                   \
@@ -1060,9 +1074,7 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
       s.K % 4 == 0 && !getenv_flag("RSYS_ROWGEMM_GENERIC")) {
     const size_t lds2 = lds + (size_t)(nt * 16 + ((s.epi & RS_EPI_AUX_ADD) ? s.aux_mod * nt * 16 : 0)) * sizeof(float);
     const int per_cu2 = lds2 > 80 * 1024 ? 1 : (lds2 > 53 * 1024 ? 2 : (lds2 > 40 * 1024 ? 3 : 4));
-    int bx2 = cdiv(groups, stream_groups_per_wg());
-    if (bx2 > 256 * per_cu2) bx2 = 256 * per_cu2;
-    if (bx2 < 1) bx2 = 1;
+    const int bx2 = stream_grid(groups, per_cu2);
 #define RS_RGE(NTV, KTV, EV)                                                                     \
     if (nt == NTV && kt == KTV && ekey == EV) {                                                  \
       rowgemm_kernel<NTV, KTV, false, 1, EV><<<dim3(bx2, 1), 512, lds2, st>>>(s);               \
@@ -1113,8 +1125,9 @@ int rowgemm_ln_launch(const StreamArgs& s, hipStream_t st) {
     const int kc = s.K / 64;
     const size_t ldsb = (size_t)64 * (s.K + 8) * 2 + (size_t)3 * 64 * 4;
     const int per_cub = ldsb > 80 * 1024 ? 1 : (ldsb > 53 * 1024 ? 2 : (ldsb > 40 * 1024 ? 3 : 4));
-    int bxb = cdiv(s.M / 16, stream_groups_per_wg());
-    if (bxb > 256 * per_cub) bxb = 256 * per_cub;
+    // the LayerNorm-epilogue instances measured best at 2 workgroups per CU (25 groups each at
+    // C2: 0.060 ms per step against 0.062 at one and 0.065 at the old 400 workgroups)
+    const int bxb = stream_grid(s.M / 16, per_cub, 20);
 #define RS_LNB(KCV, EV) \
   if (kc == KCV && ekey == EV) { rowgemm_bf16_kernel<4, KCV, true, EV><<<bxb, 512, ldsb, st>>>(s); RS_CHECK_LAUNCH("rowgemm_ln bf16"); return 0; }
     RS_LNB(1, 0) RS_LNB(1, 1) RS_LNB(1, 16) RS_LNB(1, 17) RS_LNB(4, 0) RS_LNB(4, 1) RS_LNB(4, 16) RS_LNB(4, 17)
