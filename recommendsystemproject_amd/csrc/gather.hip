@@ -22,6 +22,7 @@ constexpr int kMaxSeg = 24;  // segments travel by value in the kernel arguments
 // would otherwise serialise on a few hundred addresses
 constexpr int64_t kSmallTableBytes = 48 * 1024;
 
+constexpr int kRowsPerLane = 4;            // forward sparse rows per lane on token-sized launches
 constexpr int kBagBatch = 16;              // bag ids (and rows) loaded per batch
 // forward: a table of at most this size whose workgroup reads at least as many row bytes as the
 // table holds is staged whole into LDS first (every row of such a table is hot: the genre / age /
@@ -54,6 +55,7 @@ struct SegLaunch {
   int16_t rchunks[kMaxSeg];
   int rblock_start[kMaxSeg + 1];
   uint8_t tiny[kMaxSeg];   // bwd: tiny table by the register-accumulator kernel
+  uint8_t rpt[kMaxSeg];    // fwd sparse segments: rows per lane (kRowsPerLane on token-sized launches)
   int16_t tblocks[kMaxSeg];
   int tblock_start[kMaxSeg + 1];
   // bwd partials (small and ranged tables): [pchunks][vocab][dim] floats at ws + pws_off
@@ -170,6 +172,39 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
   }
 }
 
+// Sparse lookups, R rows per lane (token-sized launches: C2's 204,800-row sequence gather was 6,400
+// workgroups of one float4 per lane, each a serial id -> row -> store chain). The workgroup owns
+// rows [lb R rpb, (lb + 1) R rpb); all R ids are loaded, then all R rows, then the R stores, so a
+// lane has R independent chains in flight. Same values as gather_seg (bad ids: zeros + err flag).
+template <int R>
+__device__ void gather_sparse_rows(const SegLaunch& a, const rs_feature_seg_t& sg, int rpb, int lb,
+                                   int r, int chunk) {
+  const int c = chunk * 4;
+  int64_t id[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int row = (lb * R + k) * rpb + r;
+    id[k] = row < a.rows ? sg.idx[(int64_t)row * sg.idx_stride] : 0;
+  }
+  float v[R][4];
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int row = (lb * R + k) * rpb + r;
+    const bool ok = id[k] >= 0 && id[k] < sg.vocab;
+    bad |= row < a.rows && !ok;
+    load_row<true>(sg.table + (ok ? id[k] : 0) * sg.dim + c, v[k]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[k][j] = ok ? v[k][j] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int row = (lb * R + k) * rpb + r;
+    if (row < a.rows) store_row<true>(a.out + (int64_t)row * a.ldo + sg.out_col + c, v[k]);
+  }
+  if (bad && a.err) atomicOr(a.err, 1);
+}
+
 // Pooled bag split over S row groups (small batches: more loads in flight per bag). Row group
 // g = r * S + p sums positions [p * per, (p + 1) * per) of bag r; the S partial sums are added
 // in p order through LDS by group p = 0.
@@ -222,6 +257,10 @@ __global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
   const int C = a.chunks[s];
   const int r = threadIdx.x / C, chunk = threadIdx.x % C;
   if (r >= a.rpb[s]) return;
+  if (a.rpt[s] == kRowsPerLane) {  // plan: sparse, vec only
+    gather_sparse_rows<kRowsPerLane>(a, sg, a.rpb[s], lb, r, chunk);
+    return;
+  }
   const int row = lb * a.rpb[s] + r;
   if (row >= a.rows) return;
   if (a.vec[s]) gather_seg<true>(a, sg, row, chunk);
@@ -741,6 +780,9 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
         S *= 2;
     }
     a.split[s] = S;
+    // token-sized sparse forward launches: kRowsPerLane rows per lane (>= 2048 workgroups otherwise)
+    a.rpt[s] = (!bwd && vec && g.kind == RS_SEG_SPARSE && (int64_t)rows * C >= (int64_t)2048 * 256 &&
+                !getenv_flag("RSYS_GATHER_RPT1")) ? kRowsPerLane : 1;
     a.rpb[s] = 256 / (C * S);
     a.stage[s] = 0;
     if (!bwd && table_kind && vec) {
@@ -761,7 +803,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
       a.rchunks[s] = rp.chunks;
     }
     a.block_start[s] = blocks;
-    if (!a.small[s] && !a.rranges[s] && !a.tiny[s]) blocks += cdiv(rows, a.rpb[s]);
+    if (!a.small[s] && !a.rranges[s] && !a.tiny[s]) blocks += cdiv(rows, a.rpb[s] * a.rpt[s]);
   }
   a.block_start[nseg] = blocks;
   int rb = 0;
