@@ -274,7 +274,10 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
         for (int e = 0; e < 16; ++e) {
           const int t = t0 + 8 * (e >> 2) + 4 * h + (e & 3);
           const float l2 = MODE == 1 ? lse2_o : lt[e];
-          if (t == o) dv[e] = g * (fast_exp2(acc[e] * sc2 - l2) - 1.f);
+          // the label's -1 is NOT part of the bf16 operand: g (p_oo - 1) sits just below -g,
+          // where every row rounds the same way (a systematic -0.06 % on dU / dI at B = 1024);
+          // ce_reduce adds -g * (the other operand's row o) in fp32 instead
+          if (t == o) dv[e] = g * fast_exp2(acc[e] * sc2 - l2);
           if (t >= B || !o_ok) dv[e] = 0.f;
         }
       }
@@ -417,10 +420,13 @@ __global__ __launch_bounds__(256) void ce_hard_bwd_kernel(const float* __restric
   }
 }
 
-// out[r][d] = sum over splits (fixed order) of part[s][r][d]; two outputs in one launch
-// (out2 = the sums of part2, the block after part's NS slabs), 8 slab loads in flight
+// out[r][d] = sum over splits (fixed order) of part[s][r][d] - g * lab[r][d]; two outputs in one
+// launch (out2 = the sums of part2, the block after part's NS slabs, minus g * lab2), 8 slab loads
+// in flight. lab / lab2 (the label term's operand: I for dU, U for dI) may be null (no label term).
 __global__ void ce_reduce_kernel(const float* __restrict__ part, int NS, int64_t n,
-                                 float* __restrict__ out, float* __restrict__ out2) {
+                                 float* __restrict__ out, float* __restrict__ out2,
+                                 const float* __restrict__ lab, const float* __restrict__ lab2,
+                                 const float* __restrict__ grad_out, int B, float invT) {
   int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4;
   if (i >= (out2 ? 2 * n : n)) return;
   float* dst = out;
@@ -428,7 +434,11 @@ __global__ void ce_reduce_kernel(const float* __restrict__ part, int NS, int64_t
     i -= n;
     part += (int64_t)NS * n;
     dst = out2;
+    lab = lab2;
   }
+  floatx4 lv = {0.f, 0.f, 0.f, 0.f};
+  if (lab) lv = *reinterpret_cast<const floatx4*>(lab + i);
+  const float g = (grad_out ? *grad_out : 1.f) / (float)B * invT;  // as ce_tile_body's g
   floatx4 acc = *reinterpret_cast<const floatx4*>(part + i);
   int s = 1;
   for (; s + 8 <= NS; s += 8) {
@@ -439,7 +449,7 @@ __global__ void ce_reduce_kernel(const float* __restrict__ part, int NS, int64_t
     for (int u = 0; u < 8; ++u) acc += v[u];
   }
   for (; s < NS; ++s) acc += *reinterpret_cast<const floatx4*>(part + (int64_t)s * n + i);
-  *reinterpret_cast<floatx4*>(dst + i) = acc;
+  *reinterpret_cast<floatx4*>(dst + i) = acc - g * lv;
 }
 
 // Column splits. Forward: ~2 workgroups per CU (512 at B = 4096), each wave latency-bound on its
@@ -528,7 +538,7 @@ extern "C" int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const flo
   if (D == 128) ce_bwd_pair_kernel<128><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
   else ce_bwd_pair_kernel<64><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
   RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd tiles");
-  ce_reduce_kernel<<<(int)cdiv(2 * n / 4, 256), 256, 0, st>>>(ws, NSr, n, dU, dI);
+  ce_reduce_kernel<<<(int)cdiv(2 * n / 4, 256), 256, 0, st>>>(ws, NSr, n, dU, dI, I, U, grad_out, B, a.invT);
   RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd reduce");
   if (N) {
     const HStrideArgs hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};

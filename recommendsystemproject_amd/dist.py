@@ -62,6 +62,36 @@ def broadcast_model(model: torch.nn.Module, src: int = 0):
             dist.broadcast(b, src)
 
 
+def broadcast_buffers(model: torch.nn.Module, src: int = 0):
+    """Rank-0 buffers (BatchNorm running statistics, num_batches_tracked) to every rank, as DDP's
+    broadcast_buffers=True does before each forward: each rank's training batches move its own
+    running statistics, so without this an eval-mode pass (validate) differs by rank."""
+    if not is_active():
+        return
+    for b in model.buffers():
+        if b.dtype in (torch.float32, torch.int64) and b.numel() > 0:
+            dist.broadcast(b, src)
+
+
+def broadcast_scalar(x: float, src: int = 0) -> float:
+    """Rank src's value of a host scalar on every rank (one decision for all ranks)."""
+    if not is_active():
+        return x
+    dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend() == 'nccl' else torch.device('cpu')
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    dist.broadcast(t, src)
+    return float(t.item())
+
+
+def sync_seed(src: int = 0) -> int:
+    """Seed torch's default generator with rank src's initial seed on every rank, so that every
+    rank draws the same epoch order (the shards of one permutation)."""
+    seed = int(torch.initial_seed()) % (1 << 52)
+    seed = int(broadcast_scalar(float(seed), src))
+    torch.manual_seed(seed)
+    return seed
+
+
 def allreduce_flat_grad(flat_grad: torch.Tensor):
     """Sum the flat gradient over ranks (the mean is folded into the optimizer's grad_scale)."""
     dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM)

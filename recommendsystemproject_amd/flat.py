@@ -476,9 +476,10 @@ def lazy_tables(module: torch.nn.Module):
     tables = [m for owner in module.modules() if isinstance(getattr(owner, 'embeddings', None), torch.nn.ModuleDict)
               for m in owner.embeddings.values()]
     for m in tables:
-        # the per-row kernels cover a row with at most 64 lanes x 4 columns (csrc/lookup.hip)
+        # the per-row kernels cover a row with at most 64 lanes x 4 columns (csrc/lookup.hip) and
+        # the segment sum works on float4 rows: other widths stay ordinary (dense-Adam) tables
         if isinstance(m, torch.nn.Embedding) and m.num_embeddings >= thr and thr > 0 and \
-                m.embedding_dim <= 256:
+                m.embedding_dim <= 256 and m.embedding_dim % 4 == 0:
             out.append(m.weight)
             if not getattr(m, '_rs_lazy_hooks', False):
                 m.register_state_dict_pre_hook(_flush_hook)
@@ -515,13 +516,19 @@ def _shard_state_hook(module, state_dict, prefix, local_metadata):
     k = prefix + 'weight'
     if t is None or t.shard is None or k not in state_dict:
         return
+    state_dict[k] = gather_shards(t.param.detach(), t)
+
+
+def gather_shards(local, t):
+    """The full [V, D] tensor of row-sharded table t from every rank's [shard rows, D] slice
+    `local` (its weights or an Adam moment): one all-gather, a collective every rank calls."""
     W, r = t.shard
     n = -(-t.V_full // W)
-    local = torch.zeros(n, t.D, device=t.param.device)
-    local[:t.V] = t.param.detach()
-    parts = [torch.empty_like(local) for _ in range(W)]
-    torch.distributed.all_gather(parts, local)
-    state_dict[k] = unshard(parts, t.V_full)
+    pad = torch.zeros(n, t.D, device=t.param.device, dtype=local.dtype)
+    pad[:t.V] = local.to(t.param.device)
+    parts = [torch.empty_like(pad) for _ in range(W)]
+    torch.distributed.all_gather(parts, pad)
+    return unshard(parts, t.V_full)
 
 
 def lookup_table(weight, ids_ptr, rows, bag, row_stride, pad, mode, keep=None, record=True):

@@ -63,8 +63,6 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
             mode = SEG_ONE
             if pool:
                 mode = {_hip.RS_POOL['mean']: SEG_MEAN, _hip.RS_POOL['sum']: SEG_SUM}.get(s.pool_mode)
-            if mode is not None and (s.dim > 256 or s.dim % 4):
-                mode = None  # rs_segsum: D <= 256, a multiple of 4 (float4 rows)
             c = lookup_table(t, s.idx, rows, bag, s.idx_stride, None if s.pad_idx < 0 else s.pad_idx,
                              -1 if mode is None else mode, keep=keep, record=record)
             if c is not None:
@@ -76,13 +74,21 @@ def _grad_lazy(segs, calls, dout, tables):
     """Backward of the large-table segments: rs_segsum per call (deterministic, no atomics).
     Returns the segments left for rs_gather_bwd (ordinary tables, dense, copies, and max-pooled
     large tables, whose arg-max gradient keeps the atomic scatter)."""
+    from .flat import _dp_active
     rest = []
+    dp = _dp_active()
     for i, s in enumerate(segs):
         c = calls.get(i) if calls else None
         ptr = dout.data_ptr() + 4 * s.out_col
         sharded = c is not None and getattr(tables[i]._rs_lazy, 'shard', None) is not None
-        if sharded or (c is not None and c.mode >= 0 and ptr % 16 == 0 and dout.stride(0) % 4 == 0):
-            # (a row-sharded call only keeps its output gradient rows here: rs_pack_rows)
+        if c is not None and dp and c.mode < 0:
+            # the arg-max scatter below would write this rank's gradient into the local rows only:
+            # the data-parallel exchange has no max-pooled form
+            raise NotImplementedError('data-parallel max-pooled large tables (arg-max scatter) are not '
+                                      'supported')
+        # under data parallelism a call only keeps its output gradient rows here (rs_pack_rows,
+        # any alignment / row stride); the exchange segment-sums every rank's
+        if sharded or (c is not None and c.mode >= 0 and (dp or (ptr % 16 == 0 and dout.stride(0) % 4 == 0))):
             tables[i]._rs_lazy.segsum(c, ptr, dout.stride(0))
         else:
             rest.append(s)

@@ -227,14 +227,49 @@ class Adam(torch.optim.Optimizer):
             if c is not None and int(c.view(torch.int32)[0, 1].item()) != 0:
                 raise RuntimeError(f'lazy Adam: more than {CONSTS_CAP - 2} steps; raise optim.CONSTS_CAP')
 
+    def _param_index(self):
+        """torch.optim's state_dict numbering: parameters in param-group order."""
+        idx, i = {}, 0
+        for g in self.param_groups:
+            for p in g['params']:
+                if id(p) not in idx:
+                    idx[id(p)] = i
+                    i += 1
+        return idx
+
+    def _sharded(self):
+        """(param, LazyTable) of every row-sharded lazy table this optimizer steps."""
+        out = []
+        for st in self._flat_state.values():
+            for t in st['f'].lazy:
+                if getattr(t, 'shard', None) is not None:
+                    out.append((t.param, t))
+        return out
+
     def state_dict(self):
+        """torch.optim.Adam's state_dict. Row-sharded tables (flat.py): every rank calls it (a
+        collective, as model.state_dict()); exp_avg / exp_avg_sq are the FULL [V, D] moments,
+        gathered from the ranks' shards, so the checkpoint has the reference's shapes."""
         for st in self._flat_state.values():
             st['f'].flush()  # lazy tables: exp_avg / exp_avg_sq rows current
             step = float(st['step_dev'].item())  # authoritative (graph replays advance it)
             for p in st['f'].params:
                 if p in self.state:
                     self.state[p]['step'] = torch.tensor(step)
-        return super().state_dict()
+        sd = super().state_dict()
+        sharded = self._sharded()
+        if sharded:
+            from .flat import gather_shards
+            idx = self._param_index()
+            for p, t in sharded:
+                s = sd['state'].get(idx[id(p)])
+                if s is None:
+                    continue
+                s = dict(s)
+                for k in ('exp_avg', 'exp_avg_sq'):
+                    s[k] = gather_shards(s[k], t)
+                sd['state'][idx[id(p)]] = s
+        return sd
 
     def load_state_dict(self, state_dict):
         """torch.optim.Adam.load_state_dict, then the loaded exp_avg / exp_avg_sq / step copied
@@ -245,6 +280,21 @@ class Adam(torch.optim.Optimizer):
         for f in flats:  # the flat buffers exist before the loaded per-parameter state lands
             if f is not None:
                 self._state_for_flat(f)
+        sharded = self._sharded()
+        if sharded:  # full [V, D] moments of a row-sharded table: this rank's rows
+            idx = self._param_index()
+            state_dict = dict(state_dict)
+            state_dict['state'] = dict(state_dict['state'])
+            for p, t in sharded:
+                s = state_dict['state'].get(idx[id(p)])
+                if s is None:
+                    continue
+                s = dict(s)
+                W, r = t.shard
+                for k in ('exp_avg', 'exp_avg_sq'):
+                    if k in s and s[k].shape[0] == t.V_full and t.V_full != t.V:
+                        s[k] = s[k][r::W]
+                state_dict['state'][idx[id(p)]] = s
         super().load_state_dict(state_dict)
         for f in flats:
             if f is None:

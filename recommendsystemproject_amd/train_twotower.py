@@ -49,13 +49,16 @@ def _read_table(path):
 
 
 class _ShardedLoader:
-    """Rank r of W takes every W-th batch of the epoch (the global batch is W x batch_size)."""
+    """Rank r of W takes every W-th batch of the epoch (the global batch is W x batch_size). The
+    wrapped loader must draw the same order on every rank (dist.sync_seed) and drop its short last
+    batch (drop_last): every rank's batch then has the same size, as the all-gathers of the
+    lazy-table exchange require."""
 
     def __init__(self, loader, rank, world):
         self.loader, self.rank, self.world = loader, rank, world
 
     def __len__(self):
-        return max(len(self.loader) // self.world, 1)
+        return len(self.loader) // self.world  # equal on every rank (0 if fewer batches than ranks)
 
     def __iter__(self):
         n = len(self)
@@ -84,9 +87,12 @@ def main(config_path='config.yaml', train_data_path='./data/cleaned/train_set.pk
     print(f'Using device: {device}')
     bs = config['train']['batch_size']
 
+    if world > 1:
+        rdist.sync_seed()  # one epoch order (and one model init) for every rank
     print('Setting up training dataloader...')
     train_df = _read_table(train_data_path)
-    train_loader = DeviceCombinedLoader(config, train_df, batch_size=bs, shuffle=True, device=device)
+    train_loader = DeviceCombinedLoader(config, train_df, batch_size=bs, shuffle=True, device=device,
+                                        drop_last=world > 1)
     if world > 1:
         train_loader = _ShardedLoader(train_loader, rank, world)
     print('Setting up validation dataloader...')
@@ -126,17 +132,21 @@ def main(config_path='config.yaml', train_data_path='./data/cleaned/train_set.pk
         print(f"\n{'=' * 70}\nEpoch {epoch}/{num_epochs}\n{'=' * 70}")
         avg_train_loss = train_one_epoch(model=model, loader=train_loader, optimizer=optimizer, device=device,
                                          log_every_n_batches=100, epoch=epoch, temperature=temperature)
+        # data parallel: rank 0's BatchNorm running statistics everywhere (DDP's broadcast_buffers),
+        # so every rank validates the same model; the decisions below are rank 0's
+        rdist.broadcast_buffers(model)
         movie_id_col_idx = item_mapping['sparse'].get('movie_id_enc', 0)
         avg_val_loss, metrics = validate(model=model, loader=val_loader, item_loader=item_loader,
                                          meta_data_loader=val_metadata_loader, device=device, epoch=epoch,
                                          k_list=[10, 20, 50], item_id_feature='movie_id_enc',
                                          item_id_type='sparse', item_id_col_idx=movie_id_col_idx,
                                          log_embeddings=True, user_history=user_history)
-        current_recall = metrics[10]
+        current_recall = rdist.broadcast_scalar(metrics[10])
         if current_recall > best_recall:
             best_recall = current_recall
             patience_counter = 0
             save_path = Path(checkpoint_dir) / f'best_model_epoch_{epoch}.pt'
+            # every rank: state_dict() gathers row-sharded tables (a collective)
             ckpt = {'epoch': epoch, 'model_state_dict': model.state_dict(),
                     'optimizer_state_dict': optimizer.state_dict(), 'train_loss': avg_train_loss,
                     'val_loss': avg_val_loss, 'metrics': metrics, 'user_mapping': user_mapping,

@@ -248,6 +248,204 @@ def test_row_sharded_table_state_gloo_cpu():
     assert all(r[0] == 'ok' for r in res), res
 
 
+def _shard_adam_cpu_worker(rank, world, port, q):
+    """Adam.state_dict of a row-sharded table gathers the FULL exp_avg / exp_avg_sq (a collective,
+    reference shapes); load_state_dict of a full checkpoint keeps this rank's rows. Plus the
+    rank-agreement helpers of the training entry (sync_seed, broadcast_scalar, broadcast_buffers)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    try:
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), RSYS_LAZY_ROWS='100', RSYS_SHARD_ROWS='100')
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        from recommendsystemproject_amd import dist as rdist
+        from recommendsystemproject_amd.flat import ensure_flat
+        from recommendsystemproject_amd.optim import Adam
+        V, D = 1003, 8
+        m = torch.nn.Module()
+        m.embeddings = torch.nn.ModuleDict({'big': torch.nn.Embedding(V, D), 'small': torch.nn.Embedding(50, D)})
+        m.bn = torch.nn.BatchNorm1d(4)
+        f = ensure_flat(m)
+        big = m.embeddings['big'].weight
+        t = big._rs_lazy
+        opt = Adam(m.parameters(), lr=1e-3)
+        st = opt._state_for_flat(f)
+        g = torch.Generator().manual_seed(3)
+        M, Vv = torch.randn(V, D, generator=g), torch.rand(V, D, generator=g)
+        o = big._rs_offset
+        st['m'][o:o + t.V * D] = M[rank::world].reshape(-1)
+        st['v'][o:o + t.V * D] = Vv[rank::world].reshape(-1)
+        sd = opt.state_dict()  # collective
+        i = [id(p) for p in m.parameters()].index(id(big))
+        ok = torch.equal(sd['state'][i]['exp_avg'], M) and torch.equal(sd['state'][i]['exp_avg_sq'], Vv)
+        ok &= tuple(sd['state'][i]['exp_avg'].shape) == (V, D)
+        # a full checkpoint into a fresh optimizer: this rank's rows land in its flat moments
+        sd['state'][i]['exp_avg'] = M * 2
+        opt2 = Adam(m.parameters(), lr=1e-3)
+        opt2.load_state_dict(sd)
+        st2 = opt2._flat_state[id(f)]
+        ok &= torch.equal(st2['m'][o:o + t.V * D].view(t.V, D), (M * 2)[rank::world])
+        ok &= torch.equal(st2['v'][o:o + t.V * D].view(t.V, D), Vv[rank::world])
+        # the entry's agreement helpers
+        torch.manual_seed(11 + rank)
+        seed = rdist.sync_seed()
+        seeds = [None] * world
+        dist.all_gather_object(seeds, (seed, torch.randint(0, 1 << 30, (4,)).tolist()))
+        ok &= all(s == seeds[0] for s in seeds)
+        ok &= rdist.broadcast_scalar(0.25 + rank) == 0.25
+        m.bn.running_mean.fill_(float(rank))
+        rdist.broadcast_buffers(m)
+        ok &= float(m.bn.running_mean.abs().max()) == 0.0
+        q.put(('ok' if ok else 'mismatch', rank))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put(('err', repr(e), traceback.format_exc()[-1500:]))
+
+
+def test_row_sharded_adam_state_and_rank_agreement_gloo_cpu():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_adam_cpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+    assert all(r[0] == 'ok' for r in res), res
+
+
+def test_sharded_loader_equal_batches():
+    """Data parallel entry: with drop_last every rank's batches have the same size, also when the
+    loader's length is a multiple of the world size (rank W-1 got the short batch)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from recommendsystemproject_amd.train_twotower import _ShardedLoader
+
+    class Fake:
+        def __init__(self, n, B, drop_last):
+            self.n, self.B, self.drop_last = n, B, drop_last
+
+        def __len__(self):
+            return self.n // self.B if self.drop_last else -(-self.n // self.B)
+
+        def __iter__(self):
+            for k in range(len(self)):
+                yield min(self.B, self.n - k * self.B)
+
+    for n in (750, 768, 700, 64, 100):
+        for W in (2, 4):
+            sizes = [list(_ShardedLoader(Fake(n, 64, True), r, W)) for r in range(W)]
+            assert all(len(s) == len(sizes[0]) for s in sizes)
+            assert all(b == 64 for s in sizes for b in s), (n, W, sizes)
+            assert sum(map(len, sizes)) == (n // 64) // W * W
+
+
+def _bits_checksum(t):
+    """A bitwise-sensitive checksum of a float tensor: per 1M-element chunk, the int64 sums of its
+    int32 bit patterns and of the patterns weighted by position (any flipped bit changes it)."""
+    x = t.detach().reshape(-1).view(torch.int32).to(torch.int64)
+    n = x.numel() // (1 << 20) * (1 << 20)
+    a = x[:n].view(-1, 1 << 20)
+    w = torch.arange(1, (1 << 20) + 1, device=x.device, dtype=torch.int64)
+    return torch.cat([a.sum(1), (a * w).sum(1), x[n:].sum().view(1)])
+
+
+def _c3_gpu_worker(rank, world, port, q):
+    """C4's workload on the HIP path: the C3 model at its real table sizes (1M / 10M / 10M rows
+    x 128, lazy-exact Adam) data-parallel over 2 ranks sharing cuda:0 (gloo), per-rank batch 4096.
+    One DP step against rank 0's single-process emulation (both shards' gradients summed, mean,
+    clip + Adam), then two more steps after which the ranks' weights must be bitwise identical."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from recommendsystemproject_amd import dist as rdist
+    from recommendsystemproject_amd import synth
+    from recommendsystemproject_amd.flat import ensure_flat
+    from recommendsystemproject_amd.optim import Adam
+    from recommendsystemproject_amd.project.models.TwoTower.GenericTower import GenericTower
+    from recommendsystemproject_amd.project.models.TwoTower.TwoTowerModel import TwoTowerModel
+    from recommendsystemproject_amd.project.utils.training_utils import extract_item_id, train_step
+    try:
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world))
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        dev = torch.device('cuda:0')
+        cfg = yaml.safe_load(open(os.path.join(ROOT, 'configs', 'c3.yaml')))
+        for t in cfg['two_tower'].values():
+            t['dropout'] = 0.0
+        maps = {'user': synth.tower_layout(cfg['two_tower']['user_tower']),
+                'item': synth.tower_layout(cfg['two_tower']['item_tower'])}
+        T, lr = float(cfg['train']['temperature']), float(cfg['train']['learning_rate'])
+
+        def build():
+            torch.manual_seed(0)
+            with torch.device(dev):
+                return TwoTowerModel(GenericTower(cfg, 'user_tower'), GenericTower(cfg, 'item_tower'),
+                                     maps['user'], maps['item'])
+
+        batches = [synth.batch_to_torch(synth.make_batch(cfg, 4096, seed=900 + r), dev) for r in range(world)]
+        model = build()
+        f = ensure_flat(model)
+        assert len(f.lazy) == 3 and max(t.V for t in f.lazy) == 10_000_000
+        rdist.broadcast_model(model)
+        opt = Adam(model.parameters(), lr=lr)
+        train_step(model, batches[rank], opt, 1.0, T)  # exchange inside (dist is active)
+        f.flush()
+        res = None
+        if rank == 0:
+            dp_w = f.data.detach().clone()
+            ref = build()
+            rf = ensure_flat(ref)
+            ropt = Adam(ref.parameters(), lr=lr)
+            ropt.zero_grad()
+            for b in batches:
+                U, I, H = ref(b)
+                ref.compute_loss(U, I, item_ids=extract_item_id(b['item_tower']), temperature=T).backward()
+            ropt.grad_scale = 1.0 / world
+            ropt.step(clip_max_norm=1.0)
+            rf.flush()
+            d = (rf.data - dp_w).abs()
+            # summation order of a row's contributions differs (union segment sum vs two calls):
+            # fp32 rounding, which Adam's normalised step turns into up to +-lr on elements whose
+            # gradient is ~0 -- a handful of the ~54M touched elements
+            res = (float(d.max()), int((d > 1e-5).sum()), int((rf.data != dp_w).sum()))
+            del ref, rf, ropt, dp_w, d
+            torch.cuda.empty_cache()
+        for s in range(2):
+            train_step(model, batches[(rank + s + 1) % world], opt, 1.0, T)
+        f.flush()
+        cs = _bits_checksum(f.data)
+        cs_all = [torch.empty_like(cs) for _ in range(world)]
+        dist.all_gather(cs_all, cs)
+        same = all(torch.equal(c, cs_all[0]) for c in cs_all)
+        if rank == 0:
+            q.put(('ok', same) + res)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put(('err', repr(e), traceback.format_exc()[-1500:]))
+
+
+@pytest.mark.gpu
+def test_c4_workload_two_ranks_real_tables_one_gpu():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c3_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=280)
+    for p in procs:
+        p.join(timeout=120)
+    assert res[0] == 'ok', res
+    _, same, dmax, off, nonequal = res
+    assert same, 'ranks diverged'
+    assert off <= 64 and dmax <= 2 * 5e-4 * 1.01, res
+
+
 def _bn_invariant_bias(k, sd):
     """A Linear bias followed by a training-mode BatchNorm1d (its exact gradient is 0)."""
     head, _, leaf = k.rpartition('.')
