@@ -38,7 +38,12 @@ from recommendsystemproject_amd.project.utils.training_utils import extract_item
 PEAK_F32_TFLOPS = 157.3   # MI355X f32 (vector = f32-input MFMA) peak, MI355X_MICROARCH.md
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0     # HBM3E spec
-HBM_MEASURED_GBS = 6290.0  # MI355X_MICROARCH.md: measured float4 copy (79 % of spec)
+HBM_MEASURED_GBS = 6290.0  # MI355X_MICROARCH.md: measured float4 copy (79 % of spec); replaced by
+                           # this run's own copy measurement (measure_peaks)
+# v_exp_f32 issues in 8 cycles per wave on one SIMD (MI355X_MICROARCH.md cycle constants):
+# 64 lanes / 8 cycles x 4 SIMDs x 256 CUs x 2.4 GHz
+PEAK_EXP_PER_S = 64 / 8 * 4 * 256 * 2.4e9
+SOFTMAX_ENTRIES = ('rs_attn_fwd', 'rs_attn_bwd', 'rs_inbatch_ce_fused_fwd', 'rs_inbatch_ce_fused_bwd')
 
 
 WORKLOADS = {
@@ -69,7 +74,12 @@ def parse():
                     help='distinct resident batches cycled through by the timed steps')
     ap.add_argument('--extra', default=None,
                     help='comma-separated further workloads reported in the same JSON line under '
-                         '"extra" (default: c3 when --config is c2)')
+                         '"extra", each NAME or NAME:DTYPE (default when --config is c2: c3 at fp32, the '
+                         "reference's precision and the credited C3 number, and c3:bf16 beside it)")
+    ap.add_argument('--prof-markers', action='store_true',
+                    help='profiling runs: an rs_prof_marker dispatch right before and after every timed '
+                         'loop, so tools/prof_summary.py can bracket a rocprofv3 kernel trace to the '
+                         'timed steps')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--pmc-bracket', default=None, metavar='ENTRY|auto',
@@ -81,7 +91,7 @@ def parse():
                          'auto: profiles/traffic_<config>_<dtype>.json when it matches this run')
     a = ap.parse_args()
     if a.extra is None:
-        a.extra = 'c3' if a.config == 'c2' and a.batch is None and not a.zipf else ''
+        a.extra = 'c3:fp32,c3:bf16' if a.config == 'c2' and a.batch is None and not a.zipf else ''
     return a
 
 
@@ -190,6 +200,41 @@ def cpu_baseline(cfg, seconds, B):
             'nproc': os.cpu_count(), 'cpu_model': model}
 
 
+def measure_peaks(dev, copy_bytes=1 << 31, reps=5):
+    """This box's own peaks, measured in the same run (report against the datasheet
+    AND the measured figures): a float4 streaming copy of 2 GiB (HBM read + write bytes over the
+    event time, best of `reps`) and back-to-back v_mfma_f32_32x32x16_bf16 on every SIMD
+    (csrc/peaks.hip)."""
+    from recommendsystemproject_amd import _hip
+    st = torch.cuda.current_stream()
+    src = torch.empty(copy_bytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
+    dst = torch.empty_like(src)
+    best_copy = 0.0
+    for _ in range(reps + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        _hip.call('rs_peak_copy', src.data_ptr(), dst.data_ptr(), copy_bytes, st.cuda_stream)
+        e1.record(st)
+        e1.synchronize()
+        best_copy = max(best_copy, 2.0 * copy_bytes / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    del src, dst
+    blocks, iters = 2048, 2048  # 8 waves per SIMD on 256 CUs
+    out = torch.empty(blocks * 4, dtype=torch.float32, device=dev)
+    flops = int(_hip.lib().rs_peak_mfma_flops(blocks, iters))
+    best_mfma = 0.0
+    for _ in range(reps + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        _hip.call('rs_peak_mfma', out.data_ptr(), blocks, iters, st.cuda_stream)
+        e1.record(st)
+        e1.synchronize()
+        best_mfma = max(best_mfma, flops / (e0.elapsed_time(e1) * 1e-3) / 1e12)
+    torch.cuda.empty_cache()
+    return {'hbm_copy_GBs': round(best_copy, 1), 'bf16_mfma_TFLOPs': round(best_mfma, 1),
+            'how': 'float4 copy of 2 GiB (read + write bytes), best of 5; back-to-back '
+                   'v_mfma_f32_32x32x16_bf16, 2048 x 256-thread workgroups, best of 5 (csrc/peaks.hip)'}
+
+
 def _copy_into(dst, src):
     """Next resident batch -> the static input slot the captured graphs read (a device copy, as
     a loader writing the next batch would)."""
@@ -222,7 +267,7 @@ def load_cfg(name, args):
     return cfg
 
 
-def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_seconds):
+def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_seconds, peaks=None):
     """Build the model of workload `name`, time args.steps steps (after args.warmup) cycling through
     args.batches distinct resident batches, profile one instrumented pass. Returns the result dict
     on rank 0 (None elsewhere); with args.pmc_bracket, prints the bracket line and returns None."""
@@ -370,6 +415,9 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if args.prof_markers:
+        from recommendsystemproject_amd import _hip as _h
+        _h.call('rs_prof_marker', 7, torch.cuda.current_stream().cuda_stream)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -377,6 +425,9 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if args.prof_markers:
+        _h.call('rs_prof_marker', 8, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
     el_t = torch.tensor([el], device=dev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
@@ -406,9 +457,9 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
         os.environ['RSYS_TOWER_STREAMS'] = tower_streams
     summ = kt.summary()
     dom_name, dom = max(summ.items(), key=lambda kv: kv[1]['ms'])
-    # the dominant entry point's MFMA peak: bf16 MFMA in the bf16 compute mode (its GEMMs), f32 else
-    peak_mfma = PEAK_BF16_TFLOPS if dtype == 'bf16' and dom_name != 'rs_attn_fwd' and \
-        dom_name != 'rs_attn_bwd' else PEAK_F32_TFLOPS
+    # the dominant entry point's MFMA peak: bf16 MFMA in the bf16 compute mode (its products,
+    # attention's included: they run on v_mfma_*_bf16), f32 else
+    peak_mfma = PEAK_BF16_TFLOPS if dtype == 'bf16' else PEAK_F32_TFLOPS
     flop_bound = dom['flops'] / max(dom['bytes'], 1.0) > peak_mfma * 1e12 / (PEAK_HBM_GBS * 1e9)
     avg_ms = dom['ms'] / dom['launches']
     if flop_bound:
@@ -418,6 +469,17 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
         achieved = dom['bytes'] / dom['launches'] / (avg_ms * 1e-3) / 1e9
         roof = {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s'}
     roof['frac'] = round(roof['achieved'] / roof['peak'], 4)
+    if peaks:  # against this box's own measured peak too
+        pm = peaks['hbm_copy_GBs'] if roof['unit'] == 'GB/s' else \
+            (peaks['bf16_mfma_TFLOPs'] if peak_mfma == PEAK_BF16_TFLOPS else None)
+        if pm:
+            roof['peak_measured'] = pm
+            roof['frac_of_measured'] = round(roof['achieved'] / pm, 4)
+    if dom.get('exps'):  # softmax kernels: their exponentials against the v_exp issue rate
+        roof['valu_exp'] = {'exps_per_launch': dom['exps'] / dom['launches'],
+                            'achieved_per_s': dom['exps'] / (dom['ms'] * 1e-3),
+                            'peak_per_s': PEAK_EXP_PER_S,
+                            'frac': round(dom['exps'] / (dom['ms'] * 1e-3) / PEAK_EXP_PER_S, 4)}
     roof['traffic'] = None
     tr = load_traffic(args, B, dom_name, name, dtype, zipf, hard_negatives)
     if tr is not None:
@@ -447,7 +509,7 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
             gbs = g['bytes'] / (g['ms'] * 1e-3) / 1e9
             gather_roof[k] = {'achieved': round(gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                               'frac': round(gbs / PEAK_HBM_GBS, 4),
-                              'frac_of_measured_copy': round(gbs / HBM_MEASURED_GBS, 4),
+                              'frac_of_measured_copy': round(gbs / (peaks or {}).get('hbm_copy_GBs', HBM_MEASURED_GBS), 4),
                               'bytes_per_step': round(g['bytes'] / 3),
                               'ms_per_step': round(g['ms'] / 3, 4), 'entries': list(members)}
             if k == 'rs_gather_fwd':  # PMC traffic of the gather (profiles/traffic_<cfg>_<dt>_gather.json)
@@ -465,8 +527,20 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
             tf = g['flops'] / (g['ms'] * 1e-3) / 1e12
             batch_dot[k] = {'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
                             'frac': round(tf / PEAK_BF16_TFLOPS, 4),
+                            'exp_frac': round(g['exps'] / (g['ms'] * 1e-3) / PEAK_EXP_PER_S, 4),
                             'flops_per_launch': round(g['flops'] / g['launches']),
                             'avg_launch_ms': round(g['ms'] / g['launches'], 4)}
+
+    # the softmax kernels against both their bounds: the bf16 MFMA (their products) and the
+    # v_exp issue rate (one exponential per (query, key) / logit per direction)
+    softmax = {}
+    for k in SOFTMAX_ENTRIES:
+        if k in summ and summ[k]['ms'] > 0 and summ[k]['exps'] > 0:
+            g = summ[k]
+            sec = g['ms'] * 1e-3
+            softmax[k] = {'ms_per_step': round(g['ms'] / 3, 4),
+                          'mfma_frac': round(g['flops'] / sec / 1e12 / (PEAK_BF16_TFLOPS if dtype == 'bf16' else PEAK_F32_TFLOPS), 4),
+                          'exp_frac': round(g['exps'] / sec / PEAK_EXP_PER_S, 4)}
 
     used_graph = graphs is not None
     del model, opt, batches, batch, graphs, catalog
@@ -498,6 +572,7 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
         'roofline': roof,
         'gather_roofline': gather_roof,
         'batch_dot_roofline': batch_dot or None,
+        'softmax_roofline': softmax or None,
         'step_roofline': step_roof,
         'cpu_baseline': cpu,
         'kernel_ms_per_step': {k: round(v['ms'] / 3, 4) for k, v in sorted(summ.items(), key=lambda kv: -kv[1]['ms'])},
@@ -518,24 +593,45 @@ def main():
     if args.dtype == 'config':
         args.dtype = 'bf16' if args.config in ('c2', 'c3', 'c5') else 'fp32'
     cpu_s = 0.0 if args.no_cpu_baseline else args.cpu_baseline_seconds
+    peaks = None if args.pmc_bracket else measure_peaks(dev)
     out = run_workload(args, args.config, args.dtype, args.zipf, args.hard_negatives, rank, world, dev,
-                       cpu_s)
+                       cpu_s, peaks)
     if args.pmc_bracket:
         if dist.is_initialized():
             dist.destroy_process_group()
         return
     extras = {}
-    for ex in [e for e in (args.extra or '').split(',') if e and e != args.config]:
+    order = [args.config]
+    cpu_done = set()
+    for ex in [e for e in (args.extra or '').split(',') if e]:
         # the other headline workloads in the same line (BASELINE configs[2] = C3; at N > 1 the
-        # same run is configs[3] = C4, C3 data-parallel)
-        ex_dtype = 'bf16' if ex in ('c2', 'c3', 'c5') else 'fp32'
-        r = run_workload(args, ex, ex_dtype, None, 10 if ex == 'c5' else 0, rank, world, dev,
-                         cpu_s / 2)
+        # same run is configs[3] = C4, C3 data-parallel). NAME:DTYPE; the reference computes in
+        # fp32, so an fp32 entry is reported under NAME and another precision under NAME_DTYPE
+        name, _, ex_dtype = ex.partition(':')
+        ex_dtype = ex_dtype or ('bf16' if name in ('c2', 'c3', 'c5') else 'fp32')
+        key = name if ex_dtype == 'fp32' else f'{name}_{ex_dtype}'
+        if (name, ex_dtype) == (args.config, args.dtype):
+            continue
+        r = run_workload(args, name, ex_dtype, None, 10 if name == 'c5' else 0, rank, world, dev,
+                         0.0 if name in cpu_done else cpu_s / 2, peaks)
+        cpu_done.add(name)
+        order.append(key)
         if r is not None:
-            extras[ex] = {k: r[k] for k in ('value', 'unit', 'ms_per_step', 'dtype', 'config', 'roofline',
-                                            'gather_roofline', 'batch_dot_roofline', 'step_roofline',
-                                            'cpu_baseline', 'kernel_ms_per_step')}
+            extras[key] = {k: r[k] for k in ('value', 'unit', 'ms_per_step', 'dtype', 'config', 'roofline',
+                                             'gather_roofline', 'batch_dot_roofline', 'softmax_roofline',
+                                             'step_roofline', 'cpu_baseline', 'kernel_ms_per_step')}
+            if ex_dtype != 'fp32':
+                extras[key]['note'] = (f'{ex_dtype} compute mode, beside the fp32 entry "{name}" (the '
+                                       "reference's precision)")
+    if rank == 0 and world == 1 and cpu_s > 0:
+        # BASELINE configs[0] (C1): the reference's CPU-runnable case -- demo schema without the
+        # sequence encoder, batch 256 -- on the CPU restatement, beside the GPU numbers
+        c1 = load_cfg('c1', args)
+        out['c1_cpu_baseline'] = cpu_baseline(c1, min(cpu_s, 10.0), int(c1['train']['batch_size']))
     if rank == 0:
+        out['peaks_measured'] = peaks
+        if args.prof_markers:
+            out['prof_marker_order'] = order
         shapes = out.pop('_gemm_shapes', None)
         if shapes:
             shp = sorted(shapes.items(), key=lambda kv: -kv[1][0])

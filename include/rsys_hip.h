@@ -29,6 +29,13 @@ int rs_device_check(void);            /* 0 if a gfx950 device is current, else h
  * a rocprofv3 --pmc pass can attribute the dispatches between two markers to one entry point
  * (bench.py --pmc-bracket, tools/pmc_traffic.py). Not on the training path. */
 int rs_prof_marker(int tag, void* stream);
+/* Measurement only (bench.py, not on the training path): the on-box peaks the rooflines are
+ * reported against beside the datasheet's. rs_peak_copy: a float4 streaming copy
+ * of `bytes` (16-byte aligned buffers); rs_peak_mfma: `blocks` 256-thread workgroups each wave
+ * issuing iters x 4 back-to-back v_mfma_f32_32x32x16_bf16; rs_peak_mfma_flops: its flop count. */
+int rs_peak_copy(const void* src, void* dst, int64_t bytes, void* stream);
+int rs_peak_mfma(float* out, int blocks, int iters, void* stream);
+int64_t rs_peak_mfma_flops(int blocks, int iters);
 
 /* ---------------------------------------------------------------- GEMM (fp32 MFMA)
  * C = epi(alpha * op(A) @ op(B))  with op(A)[m,k] = transA ? A[k*lda+m] : A[m*lda+k],

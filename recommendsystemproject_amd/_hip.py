@@ -108,6 +108,9 @@ SIGNATURES = {
     'rs_adam_step': (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, vp, f32, vp, i32, vp]),
     'rs_counter_add': (i32, [vp, i64, vp]),
     'rs_prof_marker': (i32, [i32, vp]),
+    'rs_peak_copy': (i32, [vp, vp, i64, vp]),
+    'rs_peak_mfma': (i32, [vp, i32, i32, vp]),
+    'rs_peak_mfma_flops': (i64, [i32, i32]),
     'rs_sum': (i32, [vp, i32, f32, vp, vp]),
     'rs_nan_check': (i32, [vp, i64, vp, i32, vp]),
     'rs_rng_next': (i32, [vp, vp, vp]),

@@ -194,6 +194,17 @@ WORK = {
 }
 
 
+# Exponentials per call (the VALU-bound part of the softmax kernels): attention one v_exp per
+# (query, key) pair in each direction (csrc/attention.hip: the backward recomputes P), the fused
+# in-batch CE one per logit in the forward and one per logit in each backward half.
+EXPS = {
+    'rs_attn_fwd': lambda a: float(a[4] * a[7] * a[5] * a[5]),
+    'rs_attn_bwd': lambda a: float(a[6] * a[9] * a[7] * a[7]),
+    'rs_inbatch_ce_fused_fwd': lambda a: float(a[7]) * (a[7] + a[8]),
+    'rs_inbatch_ce_fused_bwd': lambda a: 2.0 * a[7] * (a[7] + a[8]),
+}
+
+
 TOKEN_ROWS = 32768  # rs_gemm_f32 calls streaming >= this many rows: the encoder's token GEMMs
 
 
@@ -274,8 +285,9 @@ class KernelTimer(_CallPatch):
             rc = orig(name, *args)
             e.record(torch.cuda.current_stream())
             fl, by = WORK[name](args) if name in WORK else (0.0, 0.0)
+            ex = EXPS[name](args) if name in EXPS else 0.0
             shape = tuple(args[:5]) if name == 'rs_gemm_f32' else None
-            self.records.append((entry_key(name, args), s, e, fl, by, shape))
+            self.records.append((entry_key(name, args), s, e, fl, by, shape, ex))
             return rc
 
         self._install(timed)
@@ -285,7 +297,7 @@ class KernelTimer(_CallPatch):
         """{(transA, transB, M, N, K): [ms, launches, flops]} for rs_gemm_f32."""
         torch.cuda.synchronize()
         out = {}
-        for name, s, e, fl, by, shape in self.records:
+        for name, s, e, fl, by, shape, _ in self.records:
             if shape is None:
                 continue
             d = out.setdefault(shape, [0.0, 0, 0.0])
@@ -297,10 +309,11 @@ class KernelTimer(_CallPatch):
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for name, s, e, fl, by, _ in self.records:
-            d = out.setdefault(name, {'ms': 0.0, 'launches': 0, 'flops': 0.0, 'bytes': 0.0})
+        for name, s, e, fl, by, _, ex in self.records:
+            d = out.setdefault(name, {'ms': 0.0, 'launches': 0, 'flops': 0.0, 'bytes': 0.0, 'exps': 0.0})
             d['ms'] += s.elapsed_time(e)
             d['launches'] += 1
             d['flops'] += fl
             d['bytes'] += by
+            d['exps'] += ex
         return out

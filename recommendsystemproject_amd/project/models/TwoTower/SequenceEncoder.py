@@ -2,14 +2,14 @@
 
 Same constructor and state_dict keys (feature_embedder.*, transformer_backbone.layers.{i}.*);
 the torch nn.TransformerEncoder is kept as the parameter container, the forward/backward run
-as one fused HIP op sequence (functions.SeqEncoderFn).
+as one fused HIP op sequence: the custom op rsys::seq_encoder (library.py, kernels in
+functions.SeqEncoderFn).
 """
 import torch
 import torch.nn as nn
 
-from recommendsystemproject_amd import _hip, ops
+from recommendsystemproject_amd import _hip, library, ops
 from recommendsystemproject_amd.flat import ensure_flat
-from recommendsystemproject_amd.functions import SeqEncoderFn
 from recommendsystemproject_amd.project.utils.SequenceFeatureProcessor import SequenceFeatureProcessor as pr
 from recommendsystemproject_amd.rng import new_rng_state
 
@@ -40,7 +40,7 @@ class SequenceEncoder(nn.Module):
         for lyr in self.transformer_backbone.layers:
             if getattr(lyr, 'norm_first', False) or getattr(lyr.activation, '__name__', 'relu') != 'relu':
                 raise NotImplementedError('only the reference layer (post-LN, ReLU) is supported')
-        return SeqEncoderFn.apply(torch.is_grad_enabled(), self, input_dict, *self.parameters())
+        return library.seq_encoder(self, input_dict)
 
     def _gather_last_valid(self, seq_output, padding_mask):
         """seq_output [B, L, D], padding_mask [B, L] bool -> [B, D] (SequenceEncoder.py:58-74)."""

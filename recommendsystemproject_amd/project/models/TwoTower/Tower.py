@@ -1,11 +1,11 @@
 """MLP_Tower — drop-in for project/models/TwoTower/Tower.py (same Sequential layout
-mlp.{0,1,4,5,8}, same init); forward/backward run as one HIP op sequence (functions.MLPFn)."""
+mlp.{0,1,4,5,8}, same init); forward/backward run as one HIP op sequence: the custom op
+rsys::mlp_tower (library.py, kernels in functions.MLPFn)."""
 import torch
 import torch.nn as nn
 
-from recommendsystemproject_amd import _hip
+from recommendsystemproject_amd import _hip, library
 from recommendsystemproject_amd.flat import ensure_flat
-from recommendsystemproject_amd.functions import MLPFn
 from recommendsystemproject_amd.rng import new_rng_state
 
 
@@ -45,4 +45,4 @@ class MLP_Tower(nn.Module):
         BatchNorm statistics per block of B rows (one hard-negative slot per block, T13)."""
         _hip.require_device(x)
         ensure_flat(self)
-        return MLPFn.apply(torch.is_grad_enabled(), self, x, int(groups), *self.parameters())
+        return library.mlp_tower(self, x, int(groups))

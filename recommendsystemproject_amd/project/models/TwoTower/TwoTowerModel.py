@@ -1,15 +1,14 @@
 """TwoTowerModel — drop-in for project/models/TwoTower/TwoTowerModel.py (same API:
 forward / predict / get_item_embeddings / compute_loss / set_feature_mappings). compute_loss is
-one fused HIP op (functions.InBatchLossFn): U I^T on the MFMA GEMM, collision mask, hard
-negatives and the softmax cross-entropy in one row kernel."""
+one custom op, rsys::inbatch_softmax_loss (library.py; kernels in functions.InBatchLossFn): U I^T
+on the MFMA, collision mask, hard negatives and the softmax cross-entropy fused."""
 import os
 
 import torch
 import torch.nn as nn
 
-from recommendsystemproject_amd import _hip
+from recommendsystemproject_amd import _hip, library
 from recommendsystemproject_amd.flat import ensure_flat, mark_branch_stream
-from recommendsystemproject_amd.functions import InBatchLossFn
 
 
 class TwoTowerModel(nn.Module):
@@ -50,7 +49,7 @@ class TwoTowerModel(nn.Module):
         _hip.require_device(self.user_tower.feature_bn.weight)
         ensure_flat(self)
         side = self._side_stream(dev)
-        if side is None:
+        if side is None or library.is_fake(self.user_tower.feature_bn.weight) or library.fake_mode_active():
             user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
             item_emb, hard_neg_emb = self._item_side(batch_data)
             return user_emb, item_emb, hard_neg_emb
@@ -161,7 +160,7 @@ class TwoTowerModel(nn.Module):
 
     def compute_loss(self, user_emb, item_emb, item_ids=None, hard_neg_emb=None, temperature=0.1):
         """In-batch softmax loss (TwoTowerModel.py:81-150)."""
-        if not self.check_nan and user_emb.is_cuda:
+        if not self.check_nan and user_emb.is_cuda and not library.is_fake(user_emb):
             self._flag_nan(user_emb.detach(), 1)
             self._flag_nan(item_emb.detach(), 2)
             if hard_neg_emb is not None:
@@ -177,4 +176,4 @@ class TwoTowerModel(nn.Module):
                 raise RuntimeError('Found NaN in Hard Negative Embedding')
             assert hard_neg_emb.dim() == 3, f'Expected shape [B, N, D], got {hard_neg_emb.shape}'
             assert hard_neg_emb.size(0) == batch_size, 'Batch size mismatch'
-        return InBatchLossFn.apply(user_emb, item_emb, item_ids, hard_neg_emb, float(temperature))
+        return library.inbatch_softmax_loss(user_emb, item_emb, item_ids, hard_neg_emb, float(temperature))
