@@ -523,6 +523,22 @@ int rs_segsum(const uint32_t* keys, const uint32_t* vals, int64_t n, int bag, in
  * out-of-range ids set *err_flag (nullable) as rs_gather_fwd does (GenericTower.py:184-196). */
 int rs_shard_map_ids(const int32_t* ids, int64_t n, int64_t vocab, int world, int rank, int64_t* local,
                      int* err_flag, void* stream);
+/* All-to-all row exchange of a one-id-per-row lookup of a row-sharded table (csrc/shard.hip;
+ * replaces the reference's nn.Embedding lookup, GenericTower.py:182 / SequenceFeatureProcessor.py:60,
+ * when the table is split across ranks). rs_shard_bucket, from a call's sorted keys / vals
+ * (rs_lookup_sort over global ids): its distinct ids packed per owner into send_ids [world][cap]
+ * (the owner's local row id / world), counts[o] (capped; *flag |= 2 past cap), idx [n] (lookup
+ * order: the slot o * cap + s holding the lookup's row once the rows come back) and ckey [n]
+ * (sorted order: the slot, or 0xFFFFFFFF for the padding id / out-of-range ids, the keys of the
+ * backward's segment sum into the [world * cap, D] slot gradient; *flag |= 1 on an out-of-range
+ * id). rs_shard_recv, owner side: received slots as gather ids (ids64, invalid slots -> 0) and
+ * sort ids (ids32, invalid -> vocab: sorted last and skipped). */
+int64_t rs_shard_bucket_ws_bytes(int64_t n, int world);
+int rs_shard_bucket(const uint32_t* keys, const uint32_t* vals, int64_t n, int world, int cap, int64_t pad,
+                    int32_t* send_ids, int* counts, uint32_t* ckey, int64_t* idx, int* flag, void* ws,
+                    void* stream);
+int rs_shard_recv(const int32_t* recv_ids, const int* recv_counts, int world, int cap, int64_t vocab,
+                  int64_t* ids64, int32_t* ids32, int* flag, void* stream);
 int rs_pack_ids(const void* ids, int id_bytes, int64_t rows, int bag, int64_t row_stride,
                 int32_t* out, void* stream);
 int rs_pack_rows(const float* src, int64_t ld, int64_t rows, int D, float* dst, void* stream);

@@ -130,6 +130,9 @@ SIGNATURES = {
     'rs_segsum_ws_bytes': (i64, [i64, i32]),
     'rs_segsum': (i32, [vp, vp, i64, i32, i32, i64, vp, i64, i32, vp, i32, vp, vp]),
     'rs_shard_map_ids': (i32, [vp, i64, i64, i32, i32, vp, vp, vp]),
+    'rs_shard_bucket_ws_bytes': (i64, [i64, i32]),
+    'rs_shard_bucket': (i32, [vp, vp, i64, i32, i32, i64, vp, vp, vp, vp, vp, vp, vp]),
+    'rs_shard_recv': (i32, [vp, vp, i32, i32, i64, vp, vp, vp, vp]),
     'rs_pack_ids': (i32, [vp, i32, i64, i32, i64, vp, vp]),
     'rs_pack_rows': (i32, [vp, i64, i64, i32, vp, vp]),
     'rs_dropout_fwd': (i32, [vp, i64, i32, vp, i32, i32, f32, vp, i32, vp]),

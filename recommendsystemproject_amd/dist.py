@@ -4,8 +4,8 @@ B samples (own in-batch negatives, own BatchNorm statistics, as DDP applied to t
 then ONE all-reduce of the flat gradient buffer (all parameters, ~3.5 MB for the demo schema)
 and an identical clip + Adam on every rank. Parameters are broadcast from rank 0 at start.
 
-Large tables trained by lazy-exact Adam (flat.py) stay replicated (a 10M x 128 table with its
-Adam state is ~20 GB: it fits 288 GB of HBM many times over) but their gradient is NOT
+Below W = 4, large tables trained by lazy-exact Adam (flat.py) stay replicated (a 10M x 128 table
+with its Adam state is ~20 GB: it fits 288 GB of HBM many times over) but their gradient is NOT
 all-reduced densely (5 GB per table per step). SURVEY §8e's bag-gradient exchange instead: for
 every lookup call of such a table the backward keeps the call's OUTPUT gradient ([rows, D]: the
 pooled bag gradient, the single-id feature gradient, or the per-token gradient); one all-gather
@@ -15,11 +15,11 @@ them (csrc/lookup.hip). All ranks therefore hold bitwise-identical gradient rows
 same rows in the same order: the clip norm and Adam agree bitwise, with no host sync and no
 count exchange.
 
-Row-sharded tables (RSYS_SHARD_ROWS, flat.py): rank r holds only the rows id % W == r. Their
-forward all-gathers the call's ids and reduce-scatters per-rank partial bags
-(LazyTable.shard_lookup); here the kept output gradient rows are all-gathered and every rank
-segment-sums the contributions to the rows it owns (the call's keys are already the union's,
-mapped to local rows). No table bytes ever cross the link, only ids and [rows, D] bag rows.
+Row-sharded tables (flat.py; default for every large table at W >= 4): rank r holds only the
+rows id % W == r. One-id-per-row lookups exchange the rows of their distinct ids all-to-all (the
+backward returns per-id gradient rows to the owners); pooled bags all-gather ids and
+reduce-scatter per-rank partial bags, their backward all-gathers the bag gradients
+(LazyTable.shard_lookup, exchange below). Per-rank row work stays constant in W.
 """
 from __future__ import annotations
 
@@ -152,6 +152,17 @@ def _all_gather(out, inp):
 all_gather_into = _all_gather
 
 
+def all_to_all(out, inp):
+    """out block s = rank s's inp block `rank` (equal splits along dim 0): RCCL's all-to-all; on
+    other backends (gloo: ranks sharing one GPU in tests) through host copies."""
+    if dist.get_backend() == 'nccl':
+        dist.all_to_all_single(out, inp)
+        return
+    o = torch.empty(out.shape, dtype=out.dtype)
+    dist.all_to_all_single(o, inp.cpu())
+    out.copy_(o)
+
+
 def reduce_scatter_sum(out, inp):
     """out = sum over ranks of inp's block `rank` (inp: world blocks of out's size). RCCL's
     reduce-scatter; other backends (gloo sharing one GPU in tests): an all-reduce of inp and the
@@ -166,51 +177,65 @@ def reduce_scatter_sum(out, inp):
 
 
 def _exchange_sharded(t, bufs, world, dev):
-    """Row-sharded table: all-gather each call's output gradient rows; the call's sorted keys
-    are the union's local rows, so the segment sum lands on the rows this rank owns."""
+    """Row-sharded table. All-to-all calls: each rank's per-slot gradient buckets go to the
+    owners (all_to_all_single), which segment-sum them onto their rows. Pooled-bag calls:
+    all-gather each call's output gradient rows; the call's sorted keys are the union's local
+    rows, so the segment sum lands on the rows this rank owns."""
     calls = [c for c in t.calls if c.dseg is not None]
     for i, c in enumerate(calls):
+        acc = len(calls) > 1
+        if c.a2a is not None:
+            recv = bufs.get(('shard_a2a', i), tuple(c.dseg.shape), torch.float32, dev)
+            all_to_all(recv, c.dseg)
+            c.dseg = None
+            t.a2a_owner_segsum(c, recv, acc)
+            continue
         all_g = bufs.get(('shard_g', i), (world * c.local_rows, t.D), torch.float32, dev)
         _all_gather(all_g, c.dseg)
         c.dseg = None
         c.keep = (c.keep, all_g)
-        t.segsum(c, all_g.data_ptr(), t.D, accumulate=len(calls) > 1)
+        t.segsum(c, all_g.data_ptr(), t.D, accumulate=acc)
     t.exchanged = calls
 
 
 def exchange_lazy_grads(f):
     """Bag-gradient exchange of every lazy table of flat buffer f (see module doc)."""
-    world = dist.get_world_size()
-    dev = f.data.device
     for t in f.lazy:
-        if not t.calls:
+        if t.calls:
+            exchange_table(t)
+
+
+def exchange_table(t):
+    """The gradient exchange of one lazy table's calls this step (module doc): every rank calls
+    it for the same tables in the same order."""
+    world = dist.get_world_size()
+    dev = t.flat.data.device
+    bufs = getattr(t, '_dp_bufs', None)
+    if bufs is None:
+        bufs = t._dp_bufs = _ExchangeBuffers()
+    if t.shard is not None:
+        _exchange_sharded(t, bufs, world, dev)
+        return
+    union = []
+    for i, c in enumerate(t.calls):
+        if c.mode < 0:
+            raise NotImplementedError('data-parallel max-pooled large tables (arg-max scatter) '
+                                      'are not supported')
+        if c.dseg is None:  # looked up without a backward (e.g. under no_grad)
             continue
-        bufs = getattr(t, '_dp_bufs', None)
-        if bufs is None:
-            bufs = t._dp_bufs = _ExchangeBuffers()
-        if t.shard is not None:
-            _exchange_sharded(t, bufs, world, dev)
-            continue
-        union = []
-        for i, c in enumerate(t.calls):
-            if c.mode < 0:
-                raise NotImplementedError('data-parallel max-pooled large tables (arg-max scatter) '
-                                          'are not supported')
-            if c.dseg is None:  # looked up without a backward (e.g. under no_grad)
-                continue
-            ids = bufs.get(('ids', i), (c.n,), torch.int32, dev)
-            _hip.call('rs_pack_ids', c.ids_ptr, c.id_bytes, c.rows, c.bag, c.row_stride, ids.data_ptr(),
-                      _stream())
-            all_ids = bufs.get(('all_ids', i), (world * c.n,), torch.int32, dev)
-            all_g = bufs.get(('all_g', i), (world * c.rows, t.D), torch.float32, dev)
-            _all_gather(all_ids, ids)
-            _all_gather(all_g, c.dseg)
-            union.append((all_ids, all_g, c))
-        calls = []
-        for all_ids, all_g, c in union:
-            u = t.sort_call(all_ids.data_ptr(), world * c.rows, c.bag, c.bag, c.pad, c.mode, id_bytes=4,
-                            keep=(all_ids, all_g))
-            calls.append((u, all_g))
-        t.exchanged = [u for u, _ in calls]
-        for u, all_g in calls:
-            t.segsum(u, all_g.data_ptr(), t.D, accumulate=len(calls) > 1)
+        ids = bufs.get(('ids', i), (c.n,), torch.int32, dev)
+        _hip.call('rs_pack_ids', c.ids_ptr, c.id_bytes, c.rows, c.bag, c.row_stride, ids.data_ptr(),
+                  _stream())
+        all_ids = bufs.get(('all_ids', i), (world * c.n,), torch.int32, dev)
+        all_g = bufs.get(('all_g', i), (world * c.rows, t.D), torch.float32, dev)
+        _all_gather(all_ids, ids)
+        _all_gather(all_g, c.dseg)
+        union.append((all_ids, all_g, c))
+    calls = []
+    for all_ids, all_g, c in union:
+        u = t.sort_call(all_ids.data_ptr(), world * c.rows, c.bag, c.bag, c.pad, c.mode, id_bytes=4,
+                        keep=(all_ids, all_g))
+        calls.append((u, all_g))
+    t.exchanged = [u for u, _ in calls]
+    for u, all_g in calls:
+        t.segsum(u, all_g.data_ptr(), t.D, accumulate=len(calls) > 1)

@@ -15,15 +15,23 @@ sweep [0, dense_numel); the tables are touched row-by-row. State (weights, exp_a
 bitwise what dense Adam would produce; rows are brought current before every read (forward
 gather, state_dict, load_state_dict).
 
-Row sharding (data parallel only): with RSYS_SHARD_ROWS=N > 0 and a process group
-of W > 1 ranks, a large table of at least N rows is split by rows, rank r owning rows
-id % W == r at local row id / W (its weight, exp_avg and exp_avg_sq: 1/W of the memory each;
-placed last in the flat buffer, never broadcast or all-reduced). A lookup all-gathers the call's
-ids, each rank catches up and sums the rows it owns into per-requester partial bags, and a
-reduce-scatter hands every rank the pooled rows of its own batch (LazyTable.shard_lookup). The
-backward keeps the call's output gradient; dist.exchange_lazy_grads all-gathers it and every
-rank segment-sums the contributions to the rows it owns. state_dict() assembles the full table
-(a collective: every rank calls it); load_state_dict takes the owned rows of a full table.
+Row sharding (data parallel only): a large table is split by rows across the W
+ranks, rank r owning rows id % W == r at local row id / W (its weight, exp_avg and exp_avg_sq:
+1/W of the memory each; placed last in the flat buffer, never broadcast or all-reduced). By
+default every large table is sharded once W >= 4 (then the replicated form's per-rank row work,
+which grows with W, would dominate); RSYS_SHARD_ROWS=N shards tables of at least N rows at any
+W > 1 (0: never). Two exchange forms (LazyTable.shard_lookup):
+  * one id per output row (single-id features, the encoder's per-token history): all-to-all of
+    ROWS (csrc/shard.hip). Each rank buckets its distinct ids by owner, the owners gather (after
+    the catch-up) and return exactly those rows; the backward segment-sums the call's gradient
+    per distinct id and returns it to the owners, which segment-sum what they receive onto their
+    rows. Per-rank work and traffic: the call's distinct ids, independent of W;
+  * pooled bags (mean / sum): all-gather of the ids, each rank sums the rows it owns into
+    per-requester partial bags, a reduce-scatter hands every rank the pooled rows of its own
+    batch ([W x rows, D]: one row per bag, not per lookup); the backward all-gathers the bag
+    gradients and each rank segment-sums the contributions to its own rows.
+state_dict() assembles the full table (a collective: every rank calls it); load_state_dict takes
+the owned rows of a full table.
 """
 from __future__ import annotations
 
@@ -55,7 +63,7 @@ class LookupCall:
     is not reused before that join."""
 
     __slots__ = ('_keys', '_vals', 'ws', 'ready', 'n', 'rows', 'bag', 'pad', 'mode', 'ids_ptr',
-                 'id_bytes', 'row_stride', 'keep', 'dseg', 'local_rows')
+                 'id_bytes', 'row_stride', 'keep', 'dseg', 'local_rows', 'a2a')
 
     def __init__(self, keys, vals, n, rows, bag, pad, mode, ids_ptr, id_bytes, row_stride, keep,
                  ws=None, ready=None):
@@ -65,6 +73,7 @@ class LookupCall:
         self.ws, self.ready = ws, ready
         self.dseg = None
         self.local_rows = rows  # row-sharded call: the calling rank's rows (rows = world x local)
+        self.a2a = None  # all-to-all row-sharded call: the requester side (A2ARequest)
 
     def sync(self):
         if self.ready is not None:
@@ -108,6 +117,27 @@ def _sort_stream(dev):
 
 # rs_segsum modes: one id per gradient row, mean bag, sum bag (max pooling: atomic scatter)
 SEG_ONE, SEG_MEAN, SEG_SUM = 0, 1, 2
+
+
+class A2ARequest:
+    """The requester side of an all-to-all row-sharded lookup (LazyTable.shard_lookup): its
+    sorted ids (keys, vals), the segment-sum keys of the slots (ckey), the bucket capacity and the
+    buffers the backward reuses."""
+
+    __slots__ = ('keys', 'vals', 'ckey', 'idx', 'n', 'cap', 'recv_rows', 'send_grad', 'keep')
+
+    def __init__(self, **kw):
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+
+def shard_capacity(n: int, world: int) -> int:
+    """Bucket capacity per (rank, owner) pair of an all-to-all lookup of n ids: the expected n / W
+    distinct ids with a margin (RSYS_SHARD_CAPACITY, default 1.5x) plus 64. Ids are deduplicated
+    before bucketing, so hot (Zipf) ids do not skew the buckets; ids are spread over owners by
+    id % W. An overflow raises at the next check_errors() (the flag's bit 2)."""
+    f = float(os.environ.get('RSYS_SHARD_CAPACITY', '1.5'))
+    return int(-(-n * f // world)) + 64
 
 
 class LazyTable:
@@ -183,18 +213,86 @@ class LazyTable:
         return c
 
     def shard_lookup(self, seg, rows, record=True, err_ptr=None):
-        """Forward of a lookup of a row-sharded table (module doc): -> (LookupCall or None, the
-        call's pooled rows [rows, D] for this rank). seg: the rs_feature_seg_t of the lookup
-        (sparse, or pooled mean / sum)."""
+        """Forward of a lookup of a row-sharded table (module doc) -> (LookupCall or None, the
+        segment that now reads this rank's rows, tensors to keep alive until the step ends). seg:
+        the rs_feature_seg_t of the lookup (sparse: all-to-all; pooled mean / sum: partial bags)."""
+        if seg.kind == _hip.RS_SEG_SPARSE:
+            return self._shard_lookup_a2a(seg, rows, record, err_ptr)
+        return self._shard_lookup_bags(seg, rows, record, err_ptr)
+
+    def _shard_lookup_a2a(self, seg, rows, record, err_ptr):
+        """One id per output row: all-to-all of the distinct ids' rows (csrc/shard.hip)."""
+        from .dist import all_to_all
+        W, r = self.shard
+        dev = self.param.device
+        L = _hip.lib()
+        n = rows
+        keys = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        vals = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        wsb = int(L.rs_lookup_sort_ws_bytes(n, self.V_full))
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.int32, device=dev) if wsb else None
+        if n:
+            _hip.call('rs_lookup_sort', seg.idx, 8, rows, 1, seg.idx_stride, self.V_full, keys.data_ptr(),
+                      vals.data_ptr(), None if ws is None else ws.data_ptr(), _stream())
+        cap = shard_capacity(n, W)
+        send_ids = torch.empty(W * cap, dtype=torch.int32, device=dev)
+        counts = torch.empty(W, dtype=torch.int32, device=dev)
+        ckey = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        idx = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        bws = torch.empty(int(L.rs_shard_bucket_ws_bytes(n, W)) // 4 + 1, dtype=torch.int32, device=dev)
+        _hip.call('rs_shard_bucket', keys.data_ptr(), vals.data_ptr(), n, W, cap, int(seg.pad_idx),
+                  send_ids.data_ptr(), counts.data_ptr(), ckey.data_ptr(), idx.data_ptr(), err_ptr, bws.data_ptr(),
+                  _stream())
+        recv_counts = torch.empty_like(counts)
+        all_to_all(recv_counts, counts)
+        recv_ids = torch.empty_like(send_ids)
+        all_to_all(recv_ids, send_ids)
+        # owner: the requested local rows, brought current, gathered into the return buckets
+        ids64 = torch.empty(W * cap, dtype=torch.int64, device=dev)
+        ids32 = torch.empty(W * cap, dtype=torch.int32, device=dev)
+        _hip.call('rs_shard_recv', recv_ids.data_ptr(), recv_counts.data_ptr(), W, cap, self.V, ids64.data_ptr(),
+                  ids32.data_ptr(), err_ptr, _stream())
+        pad = seg.pad_idx
+        pad_local = pad // W if pad >= 0 and pad % W == r else None
+        c = self.sort_call(ids32.data_ptr(), W * cap, 1, 1, pad_local, SEG_ONE, id_bytes=4, keep=(ids32,))
+        opt = self.flat.lazy_opt
+        if opt is not None:
+            _hip.call('rs_sorted_catchup', c.keys.data_ptr(), c.n, self.D, self.ptr(self.flat.data),
+                      self.ptr(opt['m']), self.ptr(opt['v']), self.last.data_ptr(), opt['step_dev'].data_ptr(),
+                      opt['consts'].data_ptr(), *opt['hyper'], _stream())
+        from . import ops
+        send_rows = torch.empty(W * cap, self.D, device=dev)
+        gs = _hip.FeatureSeg()
+        gs.kind, gs.dim, gs.out_col, gs.pool_mode, gs.bag, gs.pad_idx = _hip.RS_SEG_SPARSE, self.D, 0, 0, 1, -1
+        gs.vocab, gs.idx_stride, gs.idx, gs.table = self.V, 1, ids64.data_ptr(), self.ptr(self.flat.data)
+        ops.gather_fwd([gs], W * cap, send_rows, None)
+        recv_rows = torch.empty_like(send_rows)
+        all_to_all(recv_rows, send_rows)
+        # this rank's lookups read their rows out of the returned buckets
+        out = _hip.FeatureSeg()
+        out.kind, out.dim, out.out_col, out.pool_mode, out.bag, out.pad_idx = (_hip.RS_SEG_SPARSE, self.D,
+                                                                                 seg.out_col, 0, 1, -1)
+        out.vocab, out.idx_stride, out.idx, out.table = W * cap, 1, idx.data_ptr(), recv_rows.data_ptr()
+        keep = (idx, recv_rows)
+        if not record:
+            return None, out, keep
+        c.local_rows = rows
+        c.a2a = A2ARequest(keys=keys, vals=vals, ckey=ckey, idx=idx, n=n, cap=cap, recv_rows=recv_rows,
+                           send_grad=None, keep=(ws, bws, recv_counts, recv_ids, ids64, send_ids, counts))
+        self.calls.append(c)
+        return c, out, keep
+
+    def _shard_lookup_bags(self, seg, rows, record, err_ptr):
+        """Pooled bags: all-gather of the ids, per-requester partial bags of the owned rows, a
+        reduce-scatter of the [W x rows, D] partial bags (module doc)."""
         from . import ops
         from .dist import all_gather_into, reduce_scatter_sum
         W, r = self.shard
         dev = self.param.device
-        pooled = seg.kind == _hip.RS_SEG_POOL
-        bag = seg.bag if pooled else 1
-        if pooled and seg.pool_mode not in (_hip.RS_POOL['mean'], _hip.RS_POOL['sum']):
+        bag = seg.bag
+        if seg.pool_mode not in (_hip.RS_POOL['mean'], _hip.RS_POOL['sum']):
             raise NotImplementedError('row-sharded tables: max pooling is not supported')
-        mode = SEG_ONE if not pooled else (SEG_MEAN if seg.pool_mode == _hip.RS_POOL['mean'] else SEG_SUM)
+        mode = SEG_MEAN if seg.pool_mode == _hip.RS_POOL['mean'] else SEG_SUM
         n = rows * bag
         ids32 = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         if n:
@@ -202,7 +300,8 @@ class LazyTable:
         all32 = torch.empty(W * ids32.numel(), dtype=torch.int32, device=dev)
         all_gather_into(all32, ids32)
         if n == 0:
-            return None, torch.zeros(rows, self.D, device=dev)
+            res = torch.zeros(rows, self.D, device=dev)
+            return None, _copy_seg(seg, res), (res,)
         all32 = all32.view(W, -1)[:, :n].contiguous()
         local = torch.empty(W * n, dtype=torch.int64, device=dev)
         _hip.call('rs_shard_map_ids', all32.data_ptr(), W * n, self.V_full, W, r, local.data_ptr(), err_ptr,
@@ -231,7 +330,7 @@ class LazyTable:
                                mode, id_bytes=8, keep=(local, all32))
             c.local_rows = rows
             self.calls.append(c)
-        return c, out
+        return c, _copy_seg(seg, out), (out,)
 
     def segsum(self, c, dout_ptr, ldo, accumulate=None):
         """Backward: the table gradient of call c from its output gradient (dout_ptr = the
@@ -240,6 +339,9 @@ class LazyTable:
         if c.n == 0:
             return
         dev = self.param.device
+        if c.a2a is not None:  # all-to-all sharded call: the gradient of each distinct id, per slot
+            self._a2a_local_segsum(c, dout_ptr, ldo)
+            return
         if accumulate is None:
             if _dp_active():
                 # this rank's output gradient rows (a row-sharded call spans world x local_rows)
@@ -253,12 +355,45 @@ class LazyTable:
                   dout_ptr, ldo, self.D, self.ptr(self.flat.grad), int(accumulate), ws.data_ptr(),
                   _stream())
 
+    def _a2a_local_segsum(self, c, dout_ptr, ldo):
+        """Backward, requester side of an all-to-all call: the call's output gradient summed per
+        distinct id into its bucket slot (send_grad [W x cap, D]); dist.exchange_lazy_grads sends
+        the buckets to the owners."""
+        q = c.a2a
+        dev = self.param.device
+        W = self.shard[0]
+        if dout_ptr % 16 or ldo % 4:  # rs_segsum reads float4 rows
+            packed = torch.empty(q.n, self.D, device=dev)
+            _hip.call('rs_pack_rows', dout_ptr, ldo, q.n, self.D, packed.data_ptr(), _stream())
+            dout_ptr, ldo = packed.data_ptr(), self.D
+            q.keep = q.keep + (packed,)
+        q.send_grad = torch.empty(W * q.cap, self.D, device=dev)
+        ws = torch.empty(int(_hip.lib().rs_segsum_ws_bytes(q.n, self.D)) // 4 + 1, dtype=torch.int32, device=dev)
+        if q.n:
+            _hip.call('rs_segsum', q.ckey.data_ptr(), q.vals.data_ptr(), q.n, 1, SEG_ONE, -1, dout_ptr, ldo,
+                      self.D, q.send_grad.data_ptr(), 0, ws.data_ptr(), _stream())
+        q.keep = q.keep + (ws,)
+        c.dseg = q.send_grad  # pending: the exchange sends it to the owners
+
+    def a2a_owner_segsum(self, c, recv_grad, accumulate):
+        """Owner side: the received per-slot gradients segment-summed onto the owned rows (the
+        owner call's keys are the received slots sorted by local row)."""
+        ws = torch.empty(int(_hip.lib().rs_segsum_ws_bytes(c.n, self.D)) // 4 + 1, dtype=torch.int32,
+                         device=self.param.device)
+        _hip.call('rs_segsum', c.keys.data_ptr(), c.vals.data_ptr(), c.n, 1, SEG_ONE, c.pad, recv_grad.data_ptr(),
+                  self.D, self.D, self.ptr(self.flat.grad), int(accumulate), ws.data_ptr(), _stream())
+        c.keep = (c.keep, recv_grad, ws)
+
     def step_calls(self):
         """The calls whose rows the optimizer steps (the data-parallel union calls once the
         gradients were exchanged). Output gradients kept for an exchange that did not happen
         (a model stepped without dist.allreduce_gradients inside a distributed job) are
         segment-summed locally here, so the gradient is never lost."""
         if self.exchanged is not None:
+            return self.exchanged
+        if self.shard is not None and any(c.dseg is not None for c in self.calls):
+            from .dist import exchange_table  # row-sharded: only the owners can sum (a collective)
+            exchange_table(self)
             return self.exchanged
         for c in self.calls:
             if c.dseg is not None:
@@ -314,18 +449,27 @@ def _is_lazy(p, lazy_ids):
     return id(p) in lazy_ids
 
 
-def shard_threshold() -> int:
-    """RSYS_SHARD_ROWS: tables with at least this many rows are row-sharded under data
-    parallelism (0, the default: every large table stays replicated)."""
-    return int(os.environ.get('RSYS_SHARD_ROWS', '0'))
+SHARD_AUTO_WORLD = 4  # default: every large (lazy) table row-sharded from this world size on
+
+
+def shard_threshold(world: int) -> int:
+    """Tables with at least this many rows are row-sharded under data parallelism (0: none).
+    RSYS_SHARD_ROWS=N sets it; by default every large table is sharded once world >= 4, where
+    the replicated form's union row work (world x the rows) would dominate the step."""
+    env = os.environ.get('RSYS_SHARD_ROWS')
+    if env is not None and env != '':
+        return int(env)
+    return lazy_rows_threshold() if world >= SHARD_AUTO_WORLD else 0
 
 
 def shard_spec(param):
     """(world, rank) if this lazy table is row-sharded, else None."""
-    thr = shard_threshold()
-    if thr <= 0 or not _dp_active() or int(param.shape[0]) < thr:
+    if not _dp_active():
         return None
     d = torch.distributed
+    thr = shard_threshold(d.get_world_size())
+    if thr <= 0 or int(param.shape[0]) < thr:
+        return None
     return d.get_world_size(), d.get_rank()
 
 
@@ -435,6 +579,14 @@ class FlatParams:
     def covers(self, params) -> bool:
         ps = list(params)
         return len(ps) == len(self.params) and all(a is b for a, b in zip(ps, self.params))
+
+
+def _copy_seg(seg, rows_t):
+    """A segment copying precomputed rows [rows, D] into seg's columns."""
+    s = _hip.FeatureSeg()
+    s.kind, s.dim, s.out_col, s.pad_idx = _hip.RS_SEG_COPY, seg.dim, seg.out_col, -1
+    s.table = rows_t.data_ptr()
+    return s
 
 
 def flat_of(p):

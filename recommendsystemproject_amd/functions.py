@@ -45,16 +45,17 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
     (csrc/lookup.hip). Returns {segment index: LookupCall}; ordinary tables are not listed.
     `keep` (the id tensors the segments point into) stays referenced by the calls until the
     optimizer step (the data-parallel exchange re-reads the ids after the backward).
-    A row-sharded table (flat.py module doc) is looked up here: its segment becomes a copy of
-    the pooled rows the reduce-scatter returned (kept alive through `keep`)."""
+    A row-sharded table (flat.py module doc) is looked up here: its segment is replaced by one
+    reading this rank's rows as the exchange returned them (the all-to-all's row buckets, or
+    the reduce-scatter's pooled bags), kept alive through `keep`."""
     calls = {}
     for i, (s, t) in enumerate(zip(segs, tables)):
         if s.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL) and hasattr(t, '_rs_lazy'):
             lt = t._rs_lazy
             if getattr(lt, 'shard', None) is not None and flat_of(t) is lt.flat:
-                c, res = lt.shard_lookup(s, rows, record, None if err is None else err.data_ptr())
-                keep.append(res)
-                segs[i] = _seg(kind=_hip.RS_SEG_COPY, dim=s.dim, out_col=s.out_col, table=res.data_ptr())
+                c, newseg, held = lt.shard_lookup(s, rows, record, None if err is None else err.data_ptr())
+                keep.extend(held)
+                segs[i] = newseg
                 if c is not None:
                     calls[i] = c
                 continue

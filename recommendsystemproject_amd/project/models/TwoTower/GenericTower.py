@@ -107,6 +107,10 @@ class GenericTower(nn.Module):
         if self.seq_encoder is not None:
             flags.append(self.seq_encoder.err_flag)
         for f in flags:
-            if int(f.item()) != 0:
+            v = int(f.item())
+            if v != 0:
                 f.zero_()
-                raise IndexError('index out of range in self (embedding id outside [0, vocab_size))')
+                if v & 1:
+                    raise IndexError('index out of range in self (embedding id outside [0, vocab_size))')
+                raise RuntimeError('row-sharded table: a rank requested more distinct ids from one owner than '
+                                   'the all-to-all bucket holds; raise RSYS_SHARD_CAPACITY (flat.shard_capacity)')

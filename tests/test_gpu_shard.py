@@ -1,0 +1,117 @@
+"""The all-to-all row-sharding kernels (csrc/shard.hip) against a numpy restatement: bucketing
+of a call's distinct ids by owner (id % W), the per-lookup slot index, the segment-sum keys (padding
+and out-of-range ids excluded) and the owner-side masking of the received buckets; bit-exact.
+(The end-to-end sharded training step runs in tests/test_dist.py.)"""
+import numpy as np
+import pytest
+import torch
+
+from recommendsystemproject_amd import _hip
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+SENT = 0xFFFFFFFF
+
+
+def _sort(ids, vocab):
+    """rs_lookup_sort of a [n, 1] int64 id column -> (keys, vals) as uint32 numpy."""
+    n = ids.numel()
+    keys = torch.empty(max(n, 1), dtype=torch.int32, device=DEV)
+    vals = torch.empty(max(n, 1), dtype=torch.int32, device=DEV)
+    wsb = int(_hip.lib().rs_lookup_sort_ws_bytes(n, vocab))
+    ws = torch.empty(wsb // 4 + 1, dtype=torch.int32, device=DEV)
+    _hip.call('rs_lookup_sort', ids.data_ptr(), 8, n, 1, 1, vocab, keys.data_ptr(), vals.data_ptr(), ws.data_ptr(),
+              torch.cuda.current_stream().cuda_stream)
+    return keys, vals
+
+
+def _bucket_ref(ids, W, cap, pad, vocab):
+    """numpy restatement: distinct valid ids ascending; bucket o holds those with id % W == o in
+    ascending order (local row id // W); a lookup's slot is its id's position."""
+    valid = (ids >= 0) & (ids < vocab)
+    uniq = np.unique(ids[valid])
+    send = {}
+    slot_of = {}
+    counts = np.zeros(W, np.int64)
+    over = False
+    for u in uniq:
+        o = int(u % W)
+        s = counts[o]
+        counts[o] += 1
+        if s < cap:
+            send[o * cap + s] = u // W
+            slot_of[int(u)] = o * cap + s
+        else:
+            over = True
+    idx = np.array([slot_of.get(int(i), 0) if v else 0 for i, v in zip(ids, valid)], np.int64)
+    return send, np.minimum(counts, cap), idx, slot_of, over
+
+
+@pytest.mark.parametrize('n,W,vocab,zipf,pad', [(1, 2, 10, False, 0), (1000, 2, 50, False, 0),
+                                                (5000, 8, 1_000_000, False, 0), (70000, 4, 300_000, True, 0),
+                                                (3000, 3, 100, False, -1), (4096, 64, 10_000_000, False, 0)])
+def test_shard_bucket_matches_numpy(n, W, vocab, zipf, pad):
+    rng = np.random.default_rng(n + W)
+    if zipf:
+        ids = (rng.zipf(1.1, n) - 1) % vocab
+    else:
+        ids = rng.integers(0, vocab, n)
+    ids[::97] = vocab + 5  # out of range: flagged, no gradient
+    ids[1::53] = 0         # the padding id (when pad = 0): fetched, no gradient
+    cap = int(-(-n * 1.5 // W)) + 64
+    t_ids = torch.as_tensor(ids, dtype=torch.int64, device=DEV)
+    keys, vals = _sort(t_ids, vocab)
+    send = torch.full((W * cap,), -7, dtype=torch.int32, device=DEV)
+    counts = torch.empty(W, dtype=torch.int32, device=DEV)
+    ckey = torch.empty(max(n, 1), dtype=torch.int32, device=DEV)
+    idx = torch.empty(max(n, 1), dtype=torch.int64, device=DEV)
+    flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ws = torch.empty(int(_hip.lib().rs_shard_bucket_ws_bytes(n, W)) // 4 + 1, dtype=torch.int32, device=DEV)
+    _hip.call('rs_shard_bucket', keys.data_ptr(), vals.data_ptr(), n, W, cap, pad, send.data_ptr(), counts.data_ptr(),
+              ckey.data_ptr(), idx.data_ptr(), flag.data_ptr(), ws.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    r_send, r_counts, r_idx, slot_of, over = _bucket_ref(ids, W, cap, pad, vocab)
+    assert not over
+    assert np.array_equal(counts.cpu().numpy(), r_counts)
+    got = send.cpu().numpy()
+    for o in range(W):
+        for s in range(int(r_counts[o])):
+            assert got[o * cap + s] == r_send[o * cap + s], (o, s)
+    assert np.array_equal(idx.cpu().numpy()[:n], r_idx)
+    # segment-sum keys, in sorted order: the lookup's slot, the sentinel for padding / out of range
+    k = keys.cpu().numpy().astype(np.uint32)[:n]
+    want = np.array([SENT if kk == SENT or int(kk) == pad else slot_of[int(kk)] for kk in k], np.uint64)
+    assert np.array_equal(ckey.cpu().numpy().astype(np.uint32)[:n].astype(np.uint64), want)
+    assert int(flag.item()) == 1  # the out-of-range ids
+
+
+def test_shard_bucket_overflow_flag():
+    W, n = 2, 4000
+    ids = torch.arange(0, 2 * n, 2, dtype=torch.int64, device=DEV)  # every id owned by rank 0
+    keys, vals = _sort(ids, 2 * n)
+    cap = 100
+    send = torch.empty(W * cap, dtype=torch.int32, device=DEV)
+    counts = torch.empty(W, dtype=torch.int32, device=DEV)
+    ckey = torch.empty(n, dtype=torch.int32, device=DEV)
+    idx = torch.empty(n, dtype=torch.int64, device=DEV)
+    flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ws = torch.empty(int(_hip.lib().rs_shard_bucket_ws_bytes(n, W)) // 4 + 1, dtype=torch.int32, device=DEV)
+    _hip.call('rs_shard_bucket', keys.data_ptr(), vals.data_ptr(), n, W, cap, -1, send.data_ptr(), counts.data_ptr(),
+              ckey.data_ptr(), idx.data_ptr(), flag.data_ptr(), ws.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert int(flag.item()) == 2
+    assert counts.tolist() == [cap, 0]
+    c = ckey.cpu().numpy().astype(np.uint32)
+    assert (c[cap:] == SENT).all() and (c[:cap] != SENT).all()  # past the capacity: no gradient
+
+
+def test_shard_recv_masks_invalid_slots():
+    W, cap, vocab = 3, 5, 40
+    recv = torch.tensor([1, 2, 3, 99, 99, 4, 5, 6, 7, 8, 39, 40, 0, 0, 0], dtype=torch.int32, device=DEV)
+    counts = torch.tensor([3, 5, 2], dtype=torch.int32, device=DEV)
+    ids64 = torch.empty(W * cap, dtype=torch.int64, device=DEV)
+    ids32 = torch.empty(W * cap, dtype=torch.int32, device=DEV)
+    flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+    _hip.call('rs_shard_recv', recv.data_ptr(), counts.data_ptr(), W, cap, vocab, ids64.data_ptr(), ids32.data_ptr(),
+              flag.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert ids64.tolist() == [1, 2, 3, 0, 0, 4, 5, 6, 7, 8, 39, 0, 0, 0, 0]
+    assert ids32.tolist() == [1, 2, 3, 40, 40, 4, 5, 6, 7, 8, 39, 40, 40, 40, 40]
+    assert int(flag.item()) == 1  # 40 is out of range in a valid slot
