@@ -766,11 +766,12 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(
 //  forward: wave w takes query tiles w, w + 4, ...; per query tile the same S^T / softmax / P V
 //           sequence as attn_fwd_bf16_kernel (all NT key tiles in registers, 64 key-valid bits);
 //           Q is staged in LDS with K and V, so the tile loop has no global-memory latency.
-//  backward, FlashAttention-2 split with no atomics: phase A (wave w: key tiles w, w + 4, ...)
-//           computes S = Q K^T and dP = dO V^T with the QUERY on the row, so the lane's P∘Z and
-//           dS tiles are directly the A operands of dV = (P∘Z)^T dO and dK = dS^T Q; phase B
-//           (wave w: query tiles w, w + 4, ...) recomputes S^T, dP^T with the KEY on the row, so
-//           dS^T is the A operand of dQ = dS K. D_i = dO_i . O_i comes from the forward output.
+//  backward, single pass with no atomics (attn_bwd_long1_bf16_kernel): wave w takes key tiles
+//           w, w + 4, ... and computes S = Q K^T and dP = dO V^T with the QUERY on the row, so the
+//           lane's P∘Z and dS tiles are directly the A operands of dV = (P∘Z)^T dO and
+//           dK = dS^T Q; dQ = dS K from the same tiles (below). D_i = dO_i . O_i comes from the
+//           forward output. (Measured and removed: the FlashAttention-2 split that recomputed S^T
+//           and dP^T in a second, query-parallel phase for dQ -- twice the exp / hash work.)
 // Dropout draws are the per-element keep_mult32 of index ((b H + h) L + i) L + j, as everywhere.
 template <int NT>
 __device__ __forceinline__ uint64_t key_bits_long(const uint8_t* __restrict__ key_pad, int b,
@@ -828,9 +829,6 @@ __device__ __forceinline__ void keep_col4(const DropKey& dk, bool leven, uint32_
 
 #ifndef RS_LONG_FWD_MINW
 #define RS_LONG_FWD_MINW 1
-#endif
-#ifndef RS_LONG_BWD_MINW
-#define RS_LONG_BWD_MINW 1
 #endif
 template <int NT, bool DROP, bool QB>
 __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kernel(
@@ -905,164 +903,7 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
   }
 }
 
-template <int NT, bool DROP, bool QB>
-__global__ __launch_bounds__(256, RS_LONG_BWD_MINW) void attn_bwd_long_bf16_kernel(
-    const void* __restrict__ qkv_, const uint8_t* __restrict__ key_pad,
-    const float* __restrict__ out, const float* __restrict__ dout, const float* __restrict__ lse,
-    void* __restrict__ dqkv_, int B, int L, int d, int H, float scale, float pdrop,
-    const int64_t* __restrict__ key, int site) {
-  constexpr int LP = NT * 16;
-  constexpr int NW = (NT + 3) / 4;  // tiles per wave
-  constexpr int TP = 24;
-  __shared__ __attribute__((aligned(16))) float Qs[LP][kRowP];
-  __shared__ __attribute__((aligned(16))) float Ks[LP][kRowP];
-  __shared__ __attribute__((aligned(16))) float Vs[LP][kRowP];
-  __shared__ __attribute__((aligned(16))) float Gs[LP][kRowP];
-  __shared__ __attribute__((aligned(16))) float L2s[LP];  // lse * log2(e)
-  __shared__ __attribute__((aligned(16))) float Ds[LP];   // D_i = dO_i . O_i
-  __shared__ float Kv[LP];                                // 1: key j is valid
-  __shared__ __attribute__((aligned(16))) float Tsm[4][16 * TP];
-  int b, h;
-  if (!map_bh(B, H, b, h)) return;  // uniform over the workgroup
-  const int bh = b * H + h;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 15, q = lane >> 4;
-  const int ld = 3 * d;
-  typedef typename std::conditional<QB, __bf16, float>::type QT;
-  const QT* base = reinterpret_cast<const QT*>(qkv_) + (int64_t)b * L * ld + h * 16;
-  load_head_image<LP>(base, ld, L, 0, Qs);
-  load_head_image<LP>(base, ld, L, d, Ks);
-  load_head_image<LP>(base, ld, L, 2 * d, Vs);
-  for (int e = threadIdx.x; e < LP * 4; e += 256) {
-    const int row = e >> 2, c4 = (e & 3) * 4;
-    f4 v = {0.f, 0.f, 0.f, 0.f};
-    if (row < L) v = ld4(dout + ((int64_t)b * L + row) * d + h * 16 + c4);
-    *reinterpret_cast<f4*>(&Gs[row][c4]) = v;
-  }
-  for (int i = threadIdx.x; i < LP; i += 256) {
-    float Di = 0.f, li = 0.f, kv = 0.f;
-    if (i < L) {
-      const float* o = out + ((int64_t)b * L + i) * d + h * 16;
-      const float* g = dout + ((int64_t)b * L + i) * d + h * 16;
-#pragma unroll
-      for (int c = 0; c < 16; c += 4) {
-        const f4 ov = ld4(o + c), gv = ld4(g + c);
-        Di += ov[0] * gv[0] + ov[1] * gv[1] + ov[2] * gv[2] + ov[3] * gv[3];
-      }
-      li = lse[(int64_t)bh * L + i] * kLog2e;
-      kv = key_pad[(int64_t)b * L + i] == 0 ? 1.f : 0.f;
-    }
-    Ds[i] = Di;
-    L2s[i] = li;
-    Kv[i] = kv;
-  }
-  const uint64_t kbits = key_bits_long<NT>(key_pad, b, L, lane, q);
-  DropKey dk;
-  if (DROP) dk = make_key(key, site, pdrop);
-  const bool leven = (L & 1) == 0;
-  const float scale2 = scale * kLog2e;
-  const f4 z = {0.f, 0.f, 0.f, 0.f};
-  float* T = Tsm[wave];
-  QT* dbase = reinterpret_cast<QT*>(dqkv_) + (int64_t)b * L * ld + h * 16;
-  __syncthreads();
-
-  // ---- phase A: dK, dV for key tiles wave, wave + 4, ... (query on the row)
-  {
-    s4v kr[NW], vr[NW];
-    float kval[NW];
-    f4 dk_acc[NW], dv_acc[NW];
-#pragma unroll
-    for (int u = 0; u < NW; ++u) {
-      const int tk = wave + 4 * u < NT ? wave + 4 * u : NT - 1;
-      kr[u] = bf4(ld4(&Ks[tk * 16 + r][4 * q]));
-      vr[u] = bf4(ld4(&Vs[tk * 16 + r][4 * q]));
-      kval[u] = Kv[tk * 16 + r];
-      dk_acc[u] = dv_acc[u] = z;
-    }
-    for (int tq = 0; tq < NT; ++tq) {
-      const s4v qr = bf4(ld4(&Qs[tq * 16 + r][4 * q]));
-      const s4v gr = bf4(ld4(&Gs[tq * 16 + r][4 * q]));
-      s4v qc[1], gc[1];
-      col_frags<1, kRowP>(&Qs[tq * 16][0], r, q, qc);
-      col_frags<1, kRowP>(&Gs[tq * 16][0], r, q, gc);
-      const f4 l2 = ld4(&L2s[tq * 16 + 4 * q]);
-      const f4 Dq = ld4(&Ds[tq * 16 + 4 * q]);
-#pragma unroll
-      for (int u = 0; u < NW; ++u) {
-        const int tk = wave + 4 * u;
-        if (tk >= NT) break;
-        const f4 sacc = mfma16(qr, kr[u], z);  // S[query 16 tq + 4q + e][key 16 tk + r]
-        const f4 pacc = mfma16(gr, vr[u], z);  // dP[query][key] = dO_i . V_j
-        const uint32_t j = (uint32_t)(tk * 16 + r);
-        float mk[4] = {1.f, 1.f, 1.f, 1.f};
-        if (DROP)
-          keep_col4(dk, leven, ((uint32_t)bh * (uint32_t)L + (uint32_t)(tq * 16 + 4 * q)) * (uint32_t)L,
-                    (uint32_t)L, j, r, mk);
-        f4 pz, ds;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = tq * 16 + 4 * q + e;
-          const float pv = (kval[u] != 0.f && i < L) ? __builtin_amdgcn_exp2f(sacc[e] * scale2 - l2[e]) : 0.f;
-          pz[e] = pv * mk[e];
-          ds[e] = pv * (mk[e] * pacc[e] - Dq[e]);
-        }
-        dv_acc[u] = mfma16(bf4(pz), gc[0], dv_acc[u]);  // (P∘Z)^T dO
-        dk_acc[u] = mfma16(bf4(ds), qc[0], dk_acc[u]);  // dS^T Q
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < NW; ++u) {
-      const int tk = wave + 4 * u;
-      if (tk >= NT) break;
-      const f4 vk = tile_rows<TP>(T, dk_acc[u] * scale, r, q, lane);
-      const f4 vv = tile_rows<TP>(T, dv_acc[u], r, q, lane);
-      const int row = tk * 16 + (lane >> 2);
-      if (row < L) {
-        st4q(dbase + (int64_t)row * ld + d + 4 * (lane & 3), vk);
-        st4q(dbase + (int64_t)row * ld + 2 * d + 4 * (lane & 3), vv);
-      }
-    }
-  }
-
-  // ---- phase B: dQ for query tiles wave, wave + 4, ... (key on the row)
-  {
-    s4v kb[NT], vb[NT], kc[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      kb[t] = bf4(ld4(&Ks[t * 16 + r][4 * q]));
-      vb[t] = bf4(ld4(&Vs[t * 16 + r][4 * q]));
-    }
-    col_frags<NT, kRowP>(&Ks[0][0], r, q, kc);
-    for (int tq = wave; tq < NT; tq += 4) {
-      const int i = tq * 16 + r;
-      const s4v qr = bf4(ld4(&Qs[i][4 * q]));
-      const s4v gr = bf4(ld4(&Gs[i][4 * q]));
-      const float l2 = L2s[i], Di = Ds[i];
-      const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
-      f4 dq = z;
-#pragma unroll
-      for (int tk = 0; tk < NT; ++tk) {
-        const f4 sacc = mfma16(kb[tk], qr, z);  // S^T[key 16 tk + 4q + e][query i]
-        const f4 pacc = mfma16(vb[tk], gr, z);  // dP^T
-        float mk[4] = {1.f, 1.f, 1.f, 1.f};
-        if (DROP) attn_keep4(dk, leven, rowbase + tk * 16 + 4 * q, mk);
-        f4 ds;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float pv = (((kbits >> (4 * tk + e)) & 1ull) && i < L)
-                               ? __builtin_amdgcn_exp2f(sacc[e] * scale2 - l2) : 0.f;
-          ds[e] = pv * ((DROP ? mk[e] : 1.f) * pacc[e] - Di);
-        }
-        dq = mfma16(bf4(ds), kc[tk], dq);  // dS K
-      }
-      const f4 v = tile_rows<TP>(T, dq * scale, r, q, lane);
-      const int row = tq * 16 + (lane >> 2);
-      if (row < L) st4q(dbase + (int64_t)row * ld + 4 * (lane & 3), v);
-    }
-  }
-}
-
-// Single-pass backward (default): key-parallel as phase A above, plus dQ from the same tiles.
+// Single-pass backward: key-parallel (the lane's query-on-row tiles feed dV and dK), plus dQ.
 // dQ = dS K contracts over keys, so the lane's dS tile (query on the row) is transposed through
 // the wave's LDS image into an A fragment; each wave keeps partial dQ tiles for every query tile
 // in registers and the four partials are summed in wave order at the end (deterministic). P and
@@ -1343,21 +1184,13 @@ extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float
     const dim3 gl(bh_grid(B, H));
 #define RS_ABL(NTV)                                                                                 \
   if (nt == NTV) {                                                                                  \
-    if (two_pass) {                                                                                 \
-      if (qb && p > 0.f) attn_bwd_long_bf16_kernel<NTV, true, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
-      else if (qb) attn_bwd_long_bf16_kernel<NTV, false, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
-      else if (p > 0.f) attn_bwd_long_bf16_kernel<NTV, true, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
-      else attn_bwd_long_bf16_kernel<NTV, false, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
-    } else {                                                                                        \
-      if (qb && p > 0.f) attn_bwd_long1_bf16_kernel<NTV, true, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
-      else if (qb) attn_bwd_long1_bf16_kernel<NTV, false, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
-      else if (p > 0.f) attn_bwd_long1_bf16_kernel<NTV, true, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
-      else attn_bwd_long1_bf16_kernel<NTV, false, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
-    }                                                                                               \
+    if (qb && p > 0.f) attn_bwd_long1_bf16_kernel<NTV, true, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    else if (qb) attn_bwd_long1_bf16_kernel<NTV, false, true><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    else if (p > 0.f) attn_bwd_long1_bf16_kernel<NTV, true, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    else attn_bwd_long1_bf16_kernel<NTV, false, false><<<gl, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
   }
     const int nt = (L + 15) / 16;
     const bool qb = (flags & RS_ATTN_QKV_BF16) != 0;
-    const bool two_pass = getenv_flag("RSYS_ATTN_LONG_2PASS");  // the FA-2 split, for comparison
     RS_ABL(5) RS_ABL(6) RS_ABL(7) RS_ABL(8) RS_ABL(9) RS_ABL(10) RS_ABL(11) RS_ABL(12) RS_ABL(13)
     RS_ABL(14) RS_ABL(15) RS_ABL(16)
 #undef RS_ABL

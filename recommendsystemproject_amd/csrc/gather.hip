@@ -781,8 +781,8 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     }
     a.split[s] = S;
     // token-sized sparse forward launches: kRowsPerLane rows per lane (>= 2048 workgroups otherwise)
-    a.rpt[s] = (!bwd && vec && g.kind == RS_SEG_SPARSE && (int64_t)rows * C >= (int64_t)2048 * 256 &&
-                !getenv_flag("RSYS_GATHER_RPT1")) ? kRowsPerLane : 1;
+    a.rpt[s] = (!bwd && vec && g.kind == RS_SEG_SPARSE && (int64_t)rows * C >= (int64_t)2048 * 256)
+                   ? kRowsPerLane : 1;
     a.rpb[s] = 256 / (C * S);
     a.stage[s] = 0;
     if (!bwd && table_kind && vec) {

@@ -776,11 +776,9 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(StreamArgs a, int rows_
 }
 
 int wgrad_blocks(int Kr) {
-  static const int cap = [] {  // RSYS_WGRAD_BLOCKS: tuning only
-    const char* e = getenv("RSYS_WGRAD_BLOCKS");
-    const int x = e ? atoi(e) : 0;
-    return x >= 16 ? x : 512;
-  }();
+  // row splits: 512 measured best at C2 (256 -> 0.101, 384 -> 0.091, 512 -> 0.083, 768 -> 0.082,
+  // 1024 -> 0.099 ms per step of rs_wgrad_bf16)
+  constexpr int cap = 512;
   int nb = Kr / 64;  // >= 64 rows per workgroup; short K (the MLP's B = 4096) still fills 64 CUs
   if (nb > cap) nb = cap;
   if (nb < 1) nb = 1;
@@ -980,18 +978,9 @@ constexpr int kSmallNT = 2;  // small M (the MLP at B = 4096): 32 columns per wo
 // share and the kernel's time is that of the busiest CU. A fixed 32 groups per workgroup gave 400
 // workgroups at C2 (12,800 groups): 144 CUs ran two, 112 one. Measured at C2 (token GEMMs per
 // step): 32 per workgroup 0.280 ms, 25 (512 workgroups) 0.270, 50 (256) 0.264.
-// RSYS_STREAM_GROUPS = g (>= 8) restores a fixed g groups per workgroup (tuning only).
 int stream_grid(int groups, int per_cu, int min_per_wg = 40) {
-  static const int fixed = [] {
-    const char* e = getenv("RSYS_STREAM_GROUPS");
-    const int x = e ? atoi(e) : 0;
-    return x >= 8 ? x : 0;
-  }();
   int bx;
-  if (fixed) {
-    bx = cdiv(groups, fixed);
-    if (bx > 256 * per_cu) bx = 256 * per_cu;
-  } else if (groups <= 256 * 8) {
+  if (groups <= 256 * 8) {
     bx = cdiv(groups, 8);  // one row group per wave
   } else {
     int k = groups / (256 * min_per_wg);  // >= min_per_wg groups per workgroup
@@ -1025,10 +1014,9 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   const int nt = small ? kSmallNT : (s.N + 15) / 16, kt = (s.K + 15) / 16;
   const int nsplit = small ? cdiv(s.N, kSmallNT * 16) : 1;
   const size_t lds = (size_t)nt * 16 * (kt * 16 + 4) * sizeof(float);
-  // RG = 2: two 16-row groups per wave step (B fragments reused across both)
-  // measured slower than one group per step on every K = 64 shape (kept for experiments)
-  const int rg = (!small && kt <= 4 && getenv_flag("RSYS_ROWGEMM_RG2")) ? 2 : 1;
-  const int groups = (s.M + 16 * rg - 1) / (16 * rg);
+  // one 16-row group per wave step (measured and removed: two groups per step sharing the B
+  // fragments, 10-25 % slower on every K = 64 shape: more VGPRs, fewer resident waves)
+  const int groups = (s.M + 15) / 16;
   int bx = cdiv(groups, small ? 8 : 8 * 2);  // small M: one row group per wave
   const int per_cu = lds > 80 * 1024 ? 1 : (lds > 53 * 1024 ? 2 : (lds > 40 * 1024 ? 3 : 4));
   if (bx > 256 * per_cu) bx = 256 * per_cu;
@@ -1070,7 +1058,7 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   // the AUX_ADD table (positional rows) in LDS: up to 64 KB covers C5's L = 200 x 64 (51 KB; two
   // workgroups per CU then)
   const bool aux_small = !(s.epi & RS_EPI_AUX_ADD) || (int64_t)s.aux_mod * nt * 16 * 4 <= 64 * 1024;
-  if (!small && rg == 1 && s.vec_epi && s.N % (nt * 16) == 0 && aux_small && s.M % 16 == 0 &&
+  if (!small && s.vec_epi && s.N % (nt * 16) == 0 && aux_small && s.M % 16 == 0 &&
       s.K % 4 == 0 && !getenv_flag("RSYS_ROWGEMM_GENERIC")) {
     const size_t lds2 = lds + (size_t)(nt * 16 + ((s.epi & RS_EPI_AUX_ADD) ? s.aux_mod * nt * 16 : 0)) * sizeof(float);
     const int per_cu2 = lds2 > 80 * 1024 ? 1 : (lds2 > 53 * 1024 ? 2 : (lds2 > 40 * 1024 ? 3 : 4));
@@ -1088,8 +1076,7 @@ int rowgemm_launch(const StreamArgs& s_in, hipStream_t st) {
   }
 #define RS_RG(NTV, KTV)                                                            \
   case NTV * 100 + KTV:                                                            \
-    if (rg == 2 && KTV <= 4) rowgemm_kernel<NTV, KTV, false, (KTV <= 4 ? 2 : 1)><<<blocks, 512, lds, st>>>(s); \
-    else rowgemm_kernel<NTV, KTV><<<blocks, 512, lds, st>>>(s);                     \
+    rowgemm_kernel<NTV, KTV><<<blocks, 512, lds, st>>>(s);                          \
     break;
   switch (nt * 100 + kt) {
     RS_RG(4, 3) RS_RG(4, 4) RS_RG(4, 12) RS_RG(4, 16) RS_RG(12, 4) RS_RG(16, 4) RS_RG(3, 4)

@@ -338,7 +338,7 @@ struct RowArgs {
 // distinct row) processes that row with float4 loads (a whole wave walking its 64 positions' heads
 // one at a time was a chain of dependent row round trips: 3-4x slower). U > 1 takes U positions
 // per group iteration with their loads issued together; measured slower at U = 4 (168 VGPRs, fewer
-// resident waves: tools/lazy_bench.py), so U = 1 (RSYS_ROW_UNROLL4 = 1 for the A/B).
+// resident waves: tools/lazy_bench.py), so U = 1.
 constexpr int kRowUnroll = 1;
 
 template <int OP, int G, int U>
@@ -938,10 +938,8 @@ static int sorted_rows(int op, const uint32_t* keys, int64_t n, int D, float* p,
   a.scale = scale; a.coef = coef; a.ws = ws;
   // lanes per row: 4 columns each, a power of two in [4, 64]
   const int G = D <= 16 ? 4 : D <= 32 ? 8 : D <= 64 ? 16 : D <= 128 ? 32 : 64;
-  int grid = op == kSqnorm ? kRowGrid
-                           : std::max<int64_t>(1, std::min<int64_t>(kRowGrid * 4, cdiv(n, 256 / G * kRowUnroll)));
-  const bool u1 = !getenv_flag("RSYS_ROW_UNROLL4");  // A/B switch: 4 rows per group iteration (slower: occupancy)
-  if (u1 && op != kSqnorm) grid = std::max<int64_t>(1, std::min<int64_t>(kRowGrid * 4, cdiv(n, 256 / G)));
+  const int grid = op == kSqnorm ? kRowGrid
+                                 : std::max<int64_t>(1, std::min<int64_t>(kRowGrid * 4, cdiv(n, 256 / G * kRowUnroll)));
 #define RS_ROWS_U(OPV, UV)                                                        \
   switch (G) {                                                                    \
     case 4: sorted_rows_kernel<OPV, 4, UV><<<grid, 256, 0, st>>>(a); break;        \
@@ -950,7 +948,7 @@ static int sorted_rows(int op, const uint32_t* keys, int64_t n, int D, float* p,
     case 32: sorted_rows_kernel<OPV, 32, UV><<<grid, 256, 0, st>>>(a); break;      \
     default: sorted_rows_kernel<OPV, 64, UV><<<grid, 256, 0, st>>>(a); break;      \
   }
-#define RS_ROWS(OPV) if (u1) { RS_ROWS_U(OPV, 1) } else { RS_ROWS_U(OPV, 4) }
+#define RS_ROWS(OPV) RS_ROWS_U(OPV, kRowUnroll)
   switch (op) {
     case kCatchup: RS_ROWS(kCatchup) break;
     case kAdam: RS_ROWS(kAdam) break;

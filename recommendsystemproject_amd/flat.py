@@ -53,66 +53,20 @@ class LookupCall:
     keys[n] = row ids ascending (out-of-range ids last as 0xFFFFFFFF), vals[n] = lookup index
     r * bag + l, ascending within a row. Kept until the optimizer step (gradient segment sums,
     clip norm and Adam all walk the distinct rows of `keys`). Under data parallelism the backward
-    keeps the call's output gradient rows (dseg) for the exchange.
+    keeps the call's output gradient rows (dseg) for the exchange. keys, vals and the sort
+    workspace are allocated on the forward's stream and held here until the step ends."""
 
-    The sort may run on a side stream (LazyTable.lookup): `ready` is then that stream, and
-    reading `keys` / `vals` first makes the current stream wait for everything queued on it
-    (torch's wait_stream). Every backward joins its calls (functions._grad_lazy) even when it
-    does not read their keys: a graph capture must not end with the side stream unjoined. keys, vals
-    and the sort workspace are allocated on the forward's stream and held here, so their memory
-    is not reused before that join."""
-
-    __slots__ = ('_keys', '_vals', 'ws', 'ready', 'n', 'rows', 'bag', 'pad', 'mode', 'ids_ptr',
+    __slots__ = ('keys', 'vals', 'ws', 'n', 'rows', 'bag', 'pad', 'mode', 'ids_ptr',
                  'id_bytes', 'row_stride', 'keep', 'dseg', 'local_rows', 'a2a')
 
-    def __init__(self, keys, vals, n, rows, bag, pad, mode, ids_ptr, id_bytes, row_stride, keep,
-                 ws=None, ready=None):
-        self._keys, self._vals, self.n, self.rows, self.bag = keys, vals, n, rows, bag
+    def __init__(self, keys, vals, n, rows, bag, pad, mode, ids_ptr, id_bytes, row_stride, keep, ws=None):
+        self.keys, self.vals, self.n, self.rows, self.bag = keys, vals, n, rows, bag
         self.pad, self.mode = pad, mode
         self.ids_ptr, self.id_bytes, self.row_stride, self.keep = ids_ptr, id_bytes, row_stride, keep
-        self.ws, self.ready = ws, ready
+        self.ws = ws
         self.dseg = None
         self.local_rows = rows  # row-sharded call: the calling rank's rows (rows = world x local)
         self.a2a = None  # all-to-all row-sharded call: the requester side (A2ARequest)
-
-    def sync(self):
-        if self.ready is not None:
-            torch.cuda.current_stream(self._keys.device).wait_stream(self.ready)
-            self.ready = None
-
-    @property
-    def keys(self):
-        self.sync()
-        return self._keys
-
-    @property
-    def vals(self):
-        self.sync()
-        return self._vals
-
-
-_SORT_STREAMS = {}
-_BRANCH_STREAMS = set()  # stream handles already forked from the main one (the item tower's)
-
-
-def mark_branch_stream(stream):
-    """Register a stream the model forks from its main one (TwoTowerModel's item tower). Lookups
-    issued on it sort in line: a second-level fork (that stream joining the sort stream, then
-    the main stream joining both) makes hipStreamEndCapture crash on this ROCm
-    (tools/capture_fork_repro.py nested), and the branch already runs beside the main stream."""
-    _BRANCH_STREAMS.add(stream.cuda_stream)
-
-
-def _sort_stream(dev):
-    """The side stream the forward's lookup sorts run on (RSYS_SORT_STREAM=1; default in line)."""
-    if os.environ.get('RSYS_SORT_STREAM', '0') != '1':
-        return None
-    if torch.cuda.current_stream(dev).cuda_stream in _BRANCH_STREAMS:
-        return None
-    s = _SORT_STREAMS.get(dev)
-    if s is None:
-        s = _SORT_STREAMS[dev] = torch.cuda.Stream(device=dev)
-    return s
 
 
 # rs_segsum modes: one id per gradient row, mean bag, sum bag (max pooling: atomic scatter)
@@ -168,42 +122,35 @@ class LazyTable:
     def ptr(self, t):
         return t.data_ptr() + 4 * self.offset
 
-    def sort_call(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None, side=None):
-        """Sort a [rows, bag] id matrix by row (rs_lookup_sort) into a LookupCall; on stream
-        `side` (forked from the current one, joined when the call's keys are first read) if
-        given."""
+    def sort_call(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None):
+        """Sort a [rows, bag] id matrix by row (rs_lookup_sort) into a LookupCall."""
         dev = self.param.device
         n = rows * bag
         keys = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         vals = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         wsb = int(_hip.lib().rs_lookup_sort_ws_bytes(n, self.V))
         ws = torch.empty(wsb // 4 + 1, dtype=torch.int32, device=dev) if wsb else None
-        if side is not None:
-            side.wait_stream(torch.cuda.current_stream(dev))
-        st = _stream() if side is None else side.cuda_stream
         _hip.call('rs_lookup_sort', ids_ptr, id_bytes, rows, bag, row_stride, self.V, keys.data_ptr(),
-                  vals.data_ptr(), None if ws is None else ws.data_ptr(), st)
+                  vals.data_ptr(), None if ws is None else ws.data_ptr(), _stream())
         return LookupCall(keys, vals, n, rows, bag, -1 if pad is None else int(pad), mode, ids_ptr,
-                          id_bytes, row_stride, keep, ws, side)
+                          id_bytes, row_stride, keep, ws)
 
     def lookup(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None, record=True):
         """Forward hook: bring the call's rows to the current optimizer step before they are
         gathered and, when the step will train on this lookup (`record`), list it for the step
         with its ids sorted by row. Default: sort, then rs_sorted_catchup over the distinct rows.
         A lookup no backward follows (evaluation) is not sorted at all: rs_lookup_catchup works
-        in id order. RSYS_SORT_STREAM=1 moves the sort of recorded lookups to a side stream
-        (their catch-up then in id order too); measured at C3 it only trades the sort for a
-        slower catch-up (0.833 vs 0.839 ms/step), so it is off by default."""
+        in id order. (Measured and rejected: the sort of recorded lookups on a side stream with
+        their catch-up in id order -- 0.833 vs 0.839 ms per C3 step, within noise.)"""
         c = None
-        side = _sort_stream(self.param.device) if record else None
         if record:
-            c = self.sort_call(ids_ptr, rows, bag, row_stride, pad, mode, id_bytes, keep, side=side)
+            c = self.sort_call(ids_ptr, rows, bag, row_stride, pad, mode, id_bytes, keep)
             self.calls.append(c)
         opt = self.flat.lazy_opt
         if opt is None or rows * bag == 0:
             return c
         hyper = (opt['step_dev'].data_ptr(), opt['consts'].data_ptr(), *opt['hyper'], _stream())
-        if c is not None and side is None:
+        if c is not None:
             _hip.call('rs_sorted_catchup', c.keys.data_ptr(), c.n, self.D, self.ptr(self.flat.data),
                       self.ptr(opt['m']), self.ptr(opt['v']), self.last.data_ptr(), *hyper)
         else:
@@ -412,8 +359,6 @@ class LazyTable:
         return self.owner
 
     def end_step(self):
-        for c in self.calls + (self.exchanged or []):
-            c.sync()  # the memory of a call's sort is released on the forward's stream
         self.calls = []
         self.exchanged = None
 

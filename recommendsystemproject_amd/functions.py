@@ -93,10 +93,6 @@ def _grad_lazy(segs, calls, dout, tables):
             tables[i]._rs_lazy.segsum(c, ptr, dout.stride(0))
         else:
             rest.append(s)
-    for c in (calls or {}).values():
-        # join the side-stream sorts this backward did not read (atomic-scatter segments, the
-        # data-parallel path): a hipGraph capture must not end with a forked stream unjoined
-        c.sync()
     return rest
 
 
@@ -177,7 +173,7 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key):
             ops.dropout_bwd(dx, p, key, 0)
     lin = proc.feature_projection[0]
     # dx is final here (the dropout backward above ran in place before this point)
-    _wgrad_side(lambda: ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias)), dx, cat)
+    ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
     dcat = ops.linear_bwd_input(dx, lin.weight)
     for s, t in zip(segs, tables):
         s.grad = grad_of(t).data_ptr()
@@ -243,54 +239,6 @@ def layer_fwd_last(lyr, x, key_pad, last, B, L, d, H, p, key, site):
     return x2, (x, qkv, att, lse, h1, x1, m1, r1) + ff
 
 
-_WGRAD_STREAMS = {}
-_JOIN_QUEUED = set()  # side streams whose end-of-backward join is queued
-
-
-def _wgrad_side(fn, *reads, env='RSYS_WGRAD_STREAM', default='0'):
-    """Run fn (weight-gradient GEMMs: they feed parameter gradients only) on a second stream,
-    beside the backward's input-gradient chain (its critical path). The tensors fn reads are
-    recorded on that stream (their memory is not reused until it is done); the caller must not
-    modify them in place afterwards. SeqEncoderFn.backward joins the stream at its end, and the
-    current stream joins it once more when the whole backward is done (autograd callback).
-    Encoder: off by default (RSYS_WGRAD_STREAM=1 enables it): measured at C2, the weight gradients
-    compete with the HBM-bound input-gradient kernels and the step got slower (1.877 -> 1.972 ms).
-    DSSM towers (RSYS_TOWER_WGRAD_STREAM=1): at B = 4096 every tower kernel is a small,
-    latency-bound grid, but a third stream in the graph made the C2 step slower too (1.82 -> 1.945
-    ms, A/B on one box): off by default."""
-    if os.environ.get(env, default) != '1':
-        fn()
-        return
-    cur = torch.cuda.current_stream()
-    s = _WGRAD_STREAMS.get(cur.device)
-    if s is None:
-        s = _WGRAD_STREAMS[cur.device] = torch.cuda.Stream(device=cur.device)
-    s.wait_stream(cur)
-    with torch.cuda.stream(s):
-        fn()
-    for t in reads:
-        if t is not None:
-            t.record_stream(s)
-    if s not in _JOIN_QUEUED:
-        _JOIN_QUEUED.add(s)
-
-        def _join_at_end():
-            _JOIN_QUEUED.discard(s)
-            _wgrad_join()
-
-        try:
-            torch.autograd.Variable._execution_engine.queue_callback(_join_at_end)
-        except RuntimeError:  # called outside an autograd backward: join right away
-            _join_at_end()
-
-
-def _wgrad_join():
-    cur = torch.cuda.current_stream()
-    s = _WGRAD_STREAMS.get(cur.device)
-    if s is not None:
-        cur.wait_stream(s)
-
-
 def _post_attn_bwd(lyr, saved, dx2, p, key, site):
     """Backward of out-proj + LN1 + FFN + LN2 (any row count). Returns (dh1, datt): dh1 the
     gradient of the layer input through the residual, datt the gradient of the attention output."""
@@ -299,54 +247,22 @@ def _post_attn_bwd(lyr, saved, dx2, p, key, site):
     sa_mod = lyr.self_attn
     # x2 = LN2(x1 + drop2(ff))
     ln1_done = False
-    fused_ffn = isinstance(f1, tuple)
-    acts = fused_ffn and not ops.ffn_wgrad_fused()
-    if fused_ffn and not acts and not os.environ.get('RSYS_UNFUSED_FFN_LN') \
-            and not os.environ.get('RSYS_UNFUSED_FFN_LN2'):
-        # norm2 backward + FFN backward + norm1 backward in one pass (csrc/ffn.hip): dh2 and
-        # dx1 stay on chip; dff = drop2(dh2) is written for the fused weight gradients
+    if isinstance(f1, tuple):
+        # bf16 mode, fused feed-forward block: norm2 backward + FFN backward + norm1 backward in one
+        # pass (csrc/ffn.hip): dh2 and dx1 stay on chip; dff = drop2(dh2) is written for the fused
+        # weight gradients, which recompute f1 / dPre1 on chip
         dh1, dsa, dff = ops.ffn_bwd_ln2_bf16(
             x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, f1[1], dx2, h2, lyr.norm2.weight,
             m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias), h1, lyr.norm1.weight, m1, r1,
             g(lyr.norm1.weight), g(lyr.norm1.bias), p, key, site + 1, site + 3)
         ln1_done = True
-        def _ffn_wgrads2(dff=dff, mask=f1[1]):
-            ops.ffn_wgrad_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, mask, dff, p,
-                               g(lyr.linear1.weight), g(lyr.linear1.bias), g(lyr.linear2.weight),
-                               g(lyr.linear2.bias))
-        _wgrad_side(_ffn_wgrads2, dff, x1, f1[1])
+        ops.ffn_wgrad_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, f1[1], dff, p,
+                           g(lyr.linear1.weight), g(lyr.linear1.bias), g(lyr.linear2.weight), g(lyr.linear2.bias))
     else:
         dff = torch.empty_like(dx2) if p > 0 else None
         dh2 = ops.layernorm_bwd(h2, dx2, lyr.norm2.weight, m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias),
                                 da=dff, p=p, key=key, site=site + 3)
         dff = dh2 if dff is None else dff
-    if ln1_done:
-        pass
-    elif fused_ffn:  # fused feed-forward block (bf16 mode)
-        # fused weight gradients: f1 / dPre1 recomputed on chip, never written (csrc/ffn.hip)
-        if not os.environ.get('RSYS_UNFUSED_FFN_LN'):
-            # dx1 = dh2 + dPre1 W1 and norm1's backward in one pass: dx1 stays on chip
-            dh1, dsa, f1b, dpre = ops.ffn_bwd_ln_bf16(
-                x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, f1[1], dff, dh2, h1,
-                lyr.norm1.weight, m1, r1, g(lyr.norm1.weight), g(lyr.norm1.bias), p, key, site + 1,
-                acts=acts)
-            ln1_done = True
-        else:
-            # dx1 = dh2 + dPre1 W1 (out of place: dff may be dh2 itself and is read again below)
-            dh2, f1b, dpre = ops.ffn_bwd_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight,
-                                              f1[1], dff, dh2, p, acts=acts)
-
-        def _ffn_wgrads(dff=dff, f1b=f1b, dpre=dpre, mask=f1[1]):
-            if not acts:
-                ops.ffn_wgrad_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, mask, dff, p,
-                                   g(lyr.linear1.weight), g(lyr.linear1.bias), g(lyr.linear2.weight),
-                                   g(lyr.linear2.bias))
-                return
-            ops.wgrad_bf16(dff, f1b, g(lyr.linear2.weight), db=g(lyr.linear2.bias))
-            ops.wgrad_bf16(dpre, x1, g(lyr.linear1.weight), db=g(lyr.linear1.bias))
-        # dff (possibly the old dh2) and x1 are not written again below: dh2 is a new tensor
-        _wgrad_side(_ffn_wgrads, *[t for t in (dff, f1b, dpre, x1, f1[1]) if t is not None])
-    else:
         ops.linear_bwd_weight(dff, f1, g(lyr.linear2.weight), db=g(lyr.linear2.bias))
         # f1 holds relu(.) after dropout: (f1 > 0) == kept & positive, kept scale 1/(1-p)
         df1 = ops.linear_bwd_input(dff, lyr.linear2.weight, relu_mask_of=f1,
@@ -358,13 +274,9 @@ def _post_attn_bwd(lyr, saved, dx2, p, key, site):
         dsa = torch.empty_like(dh2) if p > 0 else None
         dh1 = ops.layernorm_bwd(h1, dh2, lyr.norm1.weight, m1, r1, g(lyr.norm1.weight), g(lyr.norm1.bias),
                                 da=dsa, p=p, key=key, site=site + 1)
-    def _out_wgrad(dsa=dsa):
-        ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
-    if dsa is None:  # p == 0: dsa IS dh1, which the in-proj backward accumulates into: inline
+    if dsa is None:  # p == 0: dsa IS dh1 (read here before the in-proj backward accumulates into it)
         dsa = dh1
-        _out_wgrad(dsa)
-    else:
-        _wgrad_side(_out_wgrad, dsa, att)
+    ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
     datt = ops.linear_bwd_input(dsa, sa_mod.out_proj.weight)
     return dh1, datt
 
@@ -373,12 +285,10 @@ def _in_proj_bwd(lyr, x, dqkv, dx=None):
     """in_proj weight gradient and dx (+)= dqkv W_in."""
     g = grad_of
     sa_mod = lyr.self_attn
-    def _in_wgrad():
-        if dqkv.dtype == torch.bfloat16:  # bf16 dqkv (RS_ATTN_QKV_BF16): bf16-MFMA weight gradient
-            ops.wgrad_bf16(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
-        else:
-            ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
-    _wgrad_side(_in_wgrad, dqkv, x)  # neither is written again (dx is the layer-input gradient)
+    if dqkv.dtype == torch.bfloat16:  # bf16 dqkv (RS_ATTN_QKV_BF16): bf16-MFMA weight gradient
+        ops.wgrad_bf16(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
+    else:
+        ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
     if dx is None:
         return ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight)
     return ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight, out=dx, beta=1.0)  # dx = dh1 + dqkv Win
@@ -477,7 +387,6 @@ class SeqEncoderFn(torch.autograd.Function):
             dx = layer_bwd(ctx.layers[i], ctx.layer_saved[i], dx, ctx.key_pad, B, L, d, H, p, key,
                            _layer_site(i))
         seq_input_bwd(proc, ctx.in_saved, dx, B, L, p, key)
-        _wgrad_join()  # the weight gradients complete before anything after the encoder backward
         ctx.layer_saved = ctx.in_saved = None
         return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
@@ -640,9 +549,8 @@ class BatchNormFn(torch.autograd.Function):
 
 # ================================================================================ MLP tower
 def _tower_wgrad(dz, h, lin):
-    """dW += dz^T h, db += colsum(dz) of one tower Linear, beside the input-gradient chain."""
-    _wgrad_side(lambda: ops.linear_bwd_weight(dz, h, grad_of(lin.weight), db=grad_of(lin.bias)), dz, h,
-                env='RSYS_TOWER_WGRAD_STREAM', default='0')
+    """dW += dz^T h, db += colsum(dz) of one tower Linear."""
+    ops.linear_bwd_weight(dz, h, grad_of(lin.weight), db=grad_of(lin.bias))
 
 
 class MLPFn(torch.autograd.Function):
@@ -901,8 +809,7 @@ class InBatchLossFn(torch.autograd.Function):
         B, D = int(U.shape[0]), int(U.shape[1])
         dev = U.device
         # bf16 mode: S tiles recomputed on the MFMA, never stored (csrc/ce_fused.hip)
-        fused = (precision.compute_dtype() == 'bf16' and D in (64, 128) and
-                 not os.environ.get('RSYS_UNFUSED_CE'))
+        fused = precision.compute_dtype() == 'bf16' and D in (64, 128)
         S = None
         if not fused:
             S = torch.empty(B, B, device=dev, dtype=torch.float32)

@@ -166,12 +166,6 @@ def ffn_wgrad_bf16(x, W1, b1, W2, mask, dff, p, dW1, db1, dW2, db2):
          P(dW2), P(db2), P(w), stream())
 
 
-def ffn_wgrad_fused() -> bool:
-    """RSYS_FFN_WGRAD=split keeps the activation round trip (rs_ffn_bwd_bf16 writes f1 / dPre1,
-    two rs_wgrad_bf16 passes read them) for A/B measurements."""
-    return os.environ.get('RSYS_FFN_WGRAD', 'fused') != 'split'
-
-
 def wgrad_bf16(dy, x, dW, *, db=None, beta=1.0):
     """dW[Mo,No] = beta*dW + dy[rows,Mo]^T x[rows,No] on bf16 MFMA; db += colsum(dy). dy / x may be
     fp32 or bf16 tensors."""

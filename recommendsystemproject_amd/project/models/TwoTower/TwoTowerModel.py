@@ -8,7 +8,7 @@ import torch
 import torch.nn as nn
 
 from recommendsystemproject_amd import _hip, library
-from recommendsystemproject_amd.flat import ensure_flat, mark_branch_stream
+from recommendsystemproject_amd.flat import ensure_flat
 
 
 class TwoTowerModel(nn.Module):
@@ -38,7 +38,6 @@ class TwoTowerModel(nn.Module):
         s = getattr(self, '_rs_side_stream', None)
         if s is None or s.device != dev:
             s = torch.cuda.Stream(device=dev)
-            mark_branch_stream(s)
             self._rs_side_stream = s
         return s
 

@@ -9,7 +9,7 @@ import torch.nn as nn
 
 from recommendsystemproject_amd import _hip, ops
 from recommendsystemproject_amd.flat import ensure_flat
-from recommendsystemproject_amd.functions import _wgrad_join, seq_input_bwd, seq_input_fwd
+from recommendsystemproject_amd.functions import seq_input_bwd, seq_input_fwd
 from recommendsystemproject_amd.rng import new_rng_state
 
 
@@ -31,7 +31,6 @@ class _SeqInputFn(torch.autograd.Function):
     def backward(ctx, dx):
         dx = dx.contiguous().view(ctx.B * ctx.L, -1).clone()
         seq_input_bwd(ctx.proc, ctx.saved, dx, ctx.B, ctx.L, ctx.p, ctx.key)
-        _wgrad_join()
         return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
 
