@@ -520,7 +520,9 @@ int rs_segsum(const uint32_t* keys, const uint32_t* vals, int64_t n, int bag, in
               void* stream);
 /* Row-sharded large tables under data parallelism (dist.py): rank r of W owns rows id % W == r
  * at local row id / W. Maps all-gathered int32 ids to int64 local rows (-1: owned elsewhere);
- * out-of-range ids set *err_flag (nullable) as rs_gather_fwd does (GenericTower.py:184-196). */
+ * out-of-range ids set *err_flag (nullable) as rs_gather_fwd does (GenericTower.py:184-196),
+ * except INT32_MIN: the empty pad slot of a ragged call's exchange (ranks' bags of different
+ * lengths padded to a common shape). */
 int rs_shard_map_ids(const int32_t* ids, int64_t n, int64_t vocab, int world, int rank, int64_t* local,
                      int* err_flag, void* stream);
 /* All-to-all row exchange of a one-id-per-row lookup of a row-sharded table (csrc/shard.hip;

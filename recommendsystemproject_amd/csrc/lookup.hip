@@ -1107,14 +1107,16 @@ __global__ void pack_rows_kernel(const float* __restrict__ src, int64_t ld, int6
 // Row-sharded tables (flat.py / dist.py): rank `rank` of `world` owns the rows id % world ==
 // rank, stored at local row id / world. Maps the all-gathered int32 ids of a lookup call to local
 // rows (int64, -1 where another rank owns the row: the gather reads it as 0 and the sort puts it
-// last); out-of-range ids raise the error flag as the gather would.
+// last); out-of-range ids raise the error flag as the gather would, except INT32_MIN, the pad
+// slot of a ragged call's exchange (dist.EMPTY_ID).
+constexpr int32_t kEmptyId = INT32_MIN;  // dist.EMPTY_ID
 __global__ void shard_map_kernel(const int32_t* __restrict__ ids, int64_t n, int64_t V, int world, int rank,
                                  int64_t* __restrict__ local, int* err) {
   bool bad = false;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t id = ids[i];
     const bool ok = id >= 0 && id < V;
-    bad |= !ok;
+    bad |= !ok && id != kEmptyId;  // kEmptyId: an exchange pad slot (ragged calls), not an id
     local[i] = ok && id % world == rank ? id / world : -1;
   }
   if (bad && err) atomicOr(err, 1);

@@ -29,7 +29,7 @@ import torch
 import torch.distributed as dist
 
 from . import _hip
-from .flat import ensure_flat, flat_of
+from .flat import SEG_MEAN, SEG_SUM, ensure_flat, flat_of
 
 
 def is_active() -> bool:
@@ -90,6 +90,38 @@ def sync_seed(src: int = 0) -> int:
     seed = int(broadcast_scalar(float(seed), src))
     torch.manual_seed(seed)
     return seed
+
+
+EMPTY_ID = -(1 << 31)  # the pad slot of a ragged call's id exchange (csrc/lookup.hip kEmptyId)
+
+
+def agree_max(*vals):
+    """The max over ranks of each host int (one tiny all-reduce + host sync). The ranks' lookup
+    calls can differ in shape -- the collate pads the history to each batch's longest -- and the
+    all-gathers / all-to-alls need one shape, so ragged calls are padded to the ranks' maxima.
+    Inside a hipGraph capture (bench.py) no sync is possible: the shapes are static there and
+    must be equal on every rank."""
+    if not is_active() or torch.cuda.is_current_stream_capturing():
+        return list(vals)
+    dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend() == 'nccl' else torch.device('cpu')
+    t = torch.tensor(vals, dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [int(x) for x in t.tolist()]
+
+
+def call_shape(rows, bag):
+    """(rows_max, bag_max, ragged) over the ranks for a [rows, bag] lookup call."""
+    rmax, rmin, bmax, bmin = agree_max(rows, -rows, bag, -bag)
+    return rmax, bmax, rmax != -rmin or bmax != -bmin
+
+
+def pad_ids(ids32, rows, bag, rmax, bmax):
+    """A [rows, bag] int32 id matrix padded to [rmax, bmax] with EMPTY_ID."""
+    if (rows, bag) == (rmax, bmax):
+        return ids32
+    out = torch.full((rmax, bmax), EMPTY_ID, dtype=torch.int32, device=ids32.device)
+    out[:rows, :bag] = ids32.view(rows, bag)
+    return out.view(-1)
 
 
 def allreduce_flat_grad(flat_grad: torch.Tensor):
@@ -226,14 +258,25 @@ def exchange_table(t):
         ids = bufs.get(('ids', i), (c.n,), torch.int32, dev)
         _hip.call('rs_pack_ids', c.ids_ptr, c.id_bytes, c.rows, c.bag, c.row_stride, ids.data_ptr(),
                   _stream())
-        all_ids = bufs.get(('all_ids', i), (world * c.n,), torch.int32, dev)
-        all_g = bufs.get(('all_g', i), (world * c.rows, t.D), torch.float32, dev)
+        rmax, bmax, ragged = call_shape(c.rows, c.bag)
+        g, mode = c.dseg, c.mode
+        if ragged:
+            # pad to the ranks' common shape: pad ids sort last (skipped), pad rows are zero; a
+            # mean bag's 1 / length is applied to this rank's rows here and the union sums
+            ids = pad_ids(ids, c.rows, c.bag, rmax, bmax)
+            g = torch.zeros(rmax, t.D, device=dev)
+            g[:c.rows] = c.dseg
+            if mode == SEG_MEAN:
+                _hip.call('rs_scale_inplace', g.data_ptr(), c.rows * t.D, 1.0 / c.bag, None, _stream())
+                mode = SEG_SUM
+        all_ids = bufs.get(('all_ids', i), (world * rmax * bmax,), torch.int32, dev)
+        all_g = bufs.get(('all_g', i), (world * rmax, t.D), torch.float32, dev)
         _all_gather(all_ids, ids)
-        _all_gather(all_g, c.dseg)
-        union.append((all_ids, all_g, c))
+        _all_gather(all_g, g)
+        union.append((all_ids, all_g, c, rmax, bmax, mode))
     calls = []
-    for all_ids, all_g, c in union:
-        u = t.sort_call(all_ids.data_ptr(), world * c.rows, c.bag, c.bag, c.pad, c.mode, id_bytes=4,
+    for all_ids, all_g, c, rmax, bmax, mode in union:
+        u = t.sort_call(all_ids.data_ptr(), world * rmax, bmax, bmax, c.pad, mode, id_bytes=4,
                         keep=(all_ids, all_g))
         calls.append((u, all_g))
     t.exchanged = [u for u, _ in calls]

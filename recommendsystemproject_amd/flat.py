@@ -57,7 +57,7 @@ class LookupCall:
     workspace are allocated on the forward's stream and held here until the step ends."""
 
     __slots__ = ('keys', 'vals', 'ws', 'n', 'rows', 'bag', 'pad', 'mode', 'ids_ptr',
-                 'id_bytes', 'row_stride', 'keep', 'dseg', 'local_rows', 'a2a')
+                 'id_bytes', 'row_stride', 'keep', 'dseg', 'local_rows', 'own_rows', 'prescale', 'a2a')
 
     def __init__(self, keys, vals, n, rows, bag, pad, mode, ids_ptr, id_bytes, row_stride, keep, ws=None):
         self.keys, self.vals, self.n, self.rows, self.bag = keys, vals, n, rows, bag
@@ -66,6 +66,8 @@ class LookupCall:
         self.ws = ws
         self.dseg = None
         self.local_rows = rows  # row-sharded call: the calling rank's rows (rows = world x local)
+        self.own_rows = None  # ragged row-sharded bags: this rank's rows of the padded local_rows
+        self.prescale = None  # ragged mean bags: 1 / this rank's bag length (union summed as SUM)
         self.a2a = None  # all-to-all row-sharded call: the requester side (A2ARequest)
 
 
@@ -181,7 +183,8 @@ class LazyTable:
         if n:
             _hip.call('rs_lookup_sort', seg.idx, 8, rows, 1, seg.idx_stride, self.V_full, keys.data_ptr(),
                       vals.data_ptr(), None if ws is None else ws.data_ptr(), _stream())
-        cap = shard_capacity(n, W)
+        from .dist import agree_max
+        cap = shard_capacity(agree_max(n)[0], W)  # one bucket shape on every rank (ragged calls)
         send_ids = torch.empty(W * cap, dtype=torch.int32, device=dev)
         counts = torch.empty(W, dtype=torch.int32, device=dev)
         ckey = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
@@ -233,7 +236,7 @@ class LazyTable:
         """Pooled bags: all-gather of the ids, per-requester partial bags of the owned rows, a
         reduce-scatter of the [W x rows, D] partial bags (module doc)."""
         from . import ops
-        from .dist import all_gather_into, reduce_scatter_sum
+        from .dist import all_gather_into, call_shape, pad_ids, reduce_scatter_sum
         W, r = self.shard
         dev = self.param.device
         bag = seg.bag
@@ -244,38 +247,47 @@ class LazyTable:
         ids32 = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         if n:
             _hip.call('rs_pack_ids', seg.idx, 8, rows, bag, seg.idx_stride, ids32.data_ptr(), _stream())
-        all32 = torch.empty(W * ids32.numel(), dtype=torch.int32, device=dev)
-        all_gather_into(all32, ids32)
-        if n == 0:
+        # ranks' calls of different shapes (the collate pads to each batch's longest bag): padded to
+        # the common [rmax, bmax] with empty slots (dist.EMPTY_ID: no row, no gradient)
+        rmax, bmax, ragged = call_shape(rows, bag)
+        if ragged and n:
+            ids32 = pad_ids(ids32, rows, bag, rmax, bmax)
+        nm = rmax * bmax
+        all32 = torch.empty(W * max(nm, 1), dtype=torch.int32, device=dev)
+        all_gather_into(all32, ids32 if nm else torch.empty(1, dtype=torch.int32, device=dev))
+        if nm == 0:
             res = torch.zeros(rows, self.D, device=dev)
             return None, _copy_seg(seg, res), (res,)
-        all32 = all32.view(W, -1)[:, :n].contiguous()
-        local = torch.empty(W * n, dtype=torch.int64, device=dev)
-        _hip.call('rs_shard_map_ids', all32.data_ptr(), W * n, self.V_full, W, r, local.data_ptr(), err_ptr,
+        all32 = all32.view(W, -1)[:, :nm].contiguous()
+        local = torch.empty(W * nm, dtype=torch.int64, device=dev)
+        _hip.call('rs_shard_map_ids', all32.data_ptr(), W * nm, self.V_full, W, r, local.data_ptr(), err_ptr,
                   _stream())
         opt = self.flat.lazy_opt
         if opt is not None:
-            _hip.call('rs_lookup_catchup', local.data_ptr(), 8, W * rows, bag, bag, self.V, self.D,
+            _hip.call('rs_lookup_catchup', local.data_ptr(), 8, W * rmax, bmax, bmax, self.V, self.D,
                       self.ptr(self.flat.data), self.ptr(opt['m']), self.ptr(opt['v']), self.last.data_ptr(),
                       opt['step_dev'].data_ptr(), opt['consts'].data_ptr(), *opt['hyper'], _stream())
         # per requesting rank and row: the sum of the owned rows of its bag (others read as 0)
-        part = torch.empty(W * rows, self.D, device=dev)
+        part = torch.empty(W * rmax, self.D, device=dev)
         ps = _hip.FeatureSeg()
         ps.kind, ps.dim, ps.out_col, ps.pool_mode, ps.bag, ps.pad_idx = (_hip.RS_SEG_POOL, self.D, 0,
-                                                                         _hip.RS_POOL['sum'], bag, -1)
-        ps.vocab, ps.idx_stride, ps.idx, ps.table = self.V, bag, local.data_ptr(), self.ptr(self.flat.data)
-        ops.gather_fwd([ps], W * rows, part, None)
-        out = torch.empty(rows, self.D, device=dev)
+                                                                         _hip.RS_POOL['sum'], bmax, -1)
+        ps.vocab, ps.idx_stride, ps.idx, ps.table = self.V, bmax, local.data_ptr(), self.ptr(self.flat.data)
+        ops.gather_fwd([ps], W * rmax, part, None)
+        out = torch.empty(rmax, self.D, device=dev)
         reduce_scatter_sum(out, part)
-        if mode == SEG_MEAN:
+        if mode == SEG_MEAN:  # this rank's own bag length
             _hip.call('rs_scale_inplace', out.data_ptr(), out.numel(), 1.0 / bag, None, _stream())
         c = None
         if record:
             pad = seg.pad_idx
             pad_local = pad // W if pad >= 0 and pad % W == r else -1
-            c = self.sort_call(local.data_ptr(), W * rows, bag, bag, pad_local if pad_local >= 0 else None,
-                               mode, id_bytes=8, keep=(local, all32))
-            c.local_rows = rows
+            c = self.sort_call(local.data_ptr(), W * rmax, bmax, bmax, pad_local if pad_local >= 0 else None,
+                               SEG_SUM if ragged and mode == SEG_MEAN else mode, id_bytes=8, keep=(local, all32))
+            c.local_rows = rmax
+            c.own_rows = rows
+            if ragged and mode == SEG_MEAN:
+                c.prescale = 1.0 / bag
             self.calls.append(c)
         return c, _copy_seg(seg, out), (out,)
 
@@ -291,9 +303,13 @@ class LazyTable:
             return
         if accumulate is None:
             if _dp_active():
-                # this rank's output gradient rows (a row-sharded call spans world x local_rows)
-                c.dseg = torch.empty(c.local_rows, self.D, dtype=torch.float32, device=dev)
-                _hip.call('rs_pack_rows', dout_ptr, ldo, c.local_rows, self.D, c.dseg.data_ptr(), _stream())
+                # this rank's output gradient rows (a row-sharded call spans world x local_rows;
+                # a ragged one pads them with zero rows and applies a mean bag's 1 / length here)
+                own = c.own_rows if c.own_rows is not None else c.local_rows
+                c.dseg = (torch.zeros if own != c.local_rows else torch.empty)(c.local_rows, self.D, device=dev)
+                _hip.call('rs_pack_rows', dout_ptr, ldo, own, self.D, c.dseg.data_ptr(), _stream())
+                if c.prescale is not None:
+                    _hip.call('rs_scale_inplace', c.dseg.data_ptr(), own * self.D, c.prescale, None, _stream())
                 return
             accumulate = len(self.calls) > 1
         ws = torch.empty(int(_hip.lib().rs_segsum_ws_bytes(c.n, self.D)) // 4 + 1, dtype=torch.int32,

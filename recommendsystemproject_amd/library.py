@@ -157,11 +157,13 @@ def _(grad, ticket, flat_grad):
 def _seq_encoder_setup(ctx, inputs, output):
     seq, params, stats, flat_grad = inputs[:4]
     ctx.shape = (len(seq), len(params), len(stats))
-    ctx.save_for_backward(output[1], flat_grad)
+    ctx.save_for_backward(output[1])
+    ctx.flat_grad = flat_grad  # not a saved tensor: every backward op bumps its version
 
 
 def _seq_encoder_bwd(ctx, gout, gticket):
-    ticket, flat_grad = ctx.saved_tensors
+    (ticket,) = ctx.saved_tensors
+    flat_grad = ctx.flat_grad
     torch.ops.rsys.seq_encoder_backward(gout.contiguous(), ticket, flat_grad)
     ns, npar, nst = ctx.shape
     return [None] * ns, [None] * npar, [None] * nst, None, None, None, None
@@ -227,11 +229,13 @@ def _tower_features_setup(ctx, inputs, output):
     sparse, dense, seq, seq_vec, params, flags, flat_grad = inputs[:7]
     ctx.n = (len(seq), len(params), len(flags))
     ctx.seq_shape = None if seq_vec is None else list(seq_vec.shape)
-    ctx.save_for_backward(output[1], flat_grad)
+    ctx.save_for_backward(output[1])
+    ctx.flat_grad = flat_grad  # not a saved tensor: every backward op bumps its version
 
 
 def _tower_features_bwd(ctx, gout, gticket):
-    ticket, flat_grad = ctx.saved_tensors
+    (ticket,) = ctx.saved_tensors
+    flat_grad = ctx.flat_grad
     dseq = torch.ops.rsys.tower_features_backward(gout.contiguous(), ticket, flat_grad, ctx.seq_shape or [0])
     ns, npar, nfl = ctx.n
     return None, None, [None] * ns, (dseq if ctx.seq_shape is not None else None), [None] * npar, \
@@ -299,12 +303,14 @@ def _x_setup(ctx, inputs, output):
     x, params, stats, flat_grad = inputs[:4]
     ctx.n = (len(params), len(stats))
     ctx.x_shape = list(x.shape)
-    ctx.save_for_backward(output[1], flat_grad)
+    ctx.save_for_backward(output[1])
+    ctx.flat_grad = flat_grad  # not a saved tensor: every backward op bumps its version
 
 
 def _make_x_bwd(opname):
     def bwd(ctx, gout, gticket):
-        ticket, flat_grad = ctx.saved_tensors
+        (ticket,) = ctx.saved_tensors
+        flat_grad = ctx.flat_grad
         dx = getattr(torch.ops.rsys, opname)(gout.contiguous(), ticket, flat_grad, ctx.x_shape)
         npar, nst = ctx.n
         return dx, [None] * npar, [None] * nst, None, None, None, None
