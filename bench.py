@@ -43,7 +43,9 @@ HBM_MEASURED_GBS = 6290.0  # MI355X_MICROARCH.md: measured float4 copy (79 % of 
 # v_exp_f32 issues in 8 cycles per wave on one SIMD (MI355X_MICROARCH.md cycle constants):
 # 64 lanes / 8 cycles x 4 SIMDs x 256 CUs x 2.4 GHz
 PEAK_EXP_PER_S = 64 / 8 * 4 * 256 * 2.4e9
-SOFTMAX_ENTRIES = ('rs_attn_fwd', 'rs_attn_bwd', 'rs_inbatch_ce_fused_fwd', 'rs_inbatch_ce_fused_bwd')
+CE_ENTRIES = ('rs_inbatch_ce_fused_fwd', 'rs_inbatch_ce_fused_bwd', 'rs_inbatch_ce_fused_f32_fwd',
+              'rs_inbatch_ce_fused_f32_bwd')
+SOFTMAX_ENTRIES = ('rs_attn_fwd', 'rs_attn_bwd') + CE_ENTRIES
 
 
 WORKLOADS = {
@@ -518,15 +520,16 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
                 if tr:
                     gather_roof[k]['traffic_detail'] = tr
 
-    # the batch similarity (U I^T inside the fused in-batch CE) against the bf16 MFMA peak
-    # (north_star: MFMA utilisation on the batch-dot)
+    # the batch similarity (U I^T inside the fused in-batch CE) against the MFMA peak of its
+    # operands (bf16, or f32 in fp32 mode) (north_star: MFMA utilisation on the batch-dot)
     batch_dot = {}
-    for k in ('rs_inbatch_ce_fused_fwd', 'rs_inbatch_ce_fused_bwd'):
+    for k in CE_ENTRIES:
         if k in summ and summ[k]['ms'] > 0:
             g = summ[k]
             tf = g['flops'] / (g['ms'] * 1e-3) / 1e12
-            batch_dot[k] = {'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
-                            'frac': round(tf / PEAK_BF16_TFLOPS, 4),
+            pk = PEAK_F32_TFLOPS if '_f32_' in k else PEAK_BF16_TFLOPS
+            batch_dot[k] = {'achieved': round(tf, 1), 'peak': pk, 'unit': 'TFLOP/s',
+                            'frac': round(tf / pk, 4),
                             'exp_frac': round(g['exps'] / (g['ms'] * 1e-3) / PEAK_EXP_PER_S, 4),
                             'flops_per_launch': round(g['flops'] / g['launches']),
                             'avg_launch_ms': round(g['ms'] / g['launches'], 4)}

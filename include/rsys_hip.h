@@ -326,13 +326,13 @@ int rs_tower_fwd(const float* A, int G, int Bg, int K, const float* in_mean, con
  * (db_i may be NULL). ws_i: rs_tower_wgrad_ws_floats(M, N_i, K_i) floats of scratch; sync_i:
  * rs_tower_wgrad_sync_ints(N_i, K_i) ints, zero on entry and again on exit. The row splits of a
  * tile are summed in a fixed order (deterministic). Host arrays (Ns, Ks, pointer arrays) are read
- * during the call only. */
+ * during the call only. bf16 != 0: products of bf16-rounded operands; 0: exact fp32 products. */
 int rs_tower_wgrad_split(int M, int N, int K);
 int64_t rs_tower_wgrad_ws_floats(int M, int N, int K);
 int rs_tower_wgrad_sync_ints(int N, int K);
 int rs_tower_wgrad(int nlayers, int M, const int* Ns, const int* Ks, const float* const* dz,
                    const float* const* h, float* const* dW, float* const* db, float* const* ws,
-                   int* const* sync, void* stream);
+                   int* const* sync, int bf16, void* stream);
 int rs_tower_bwd(const float* gin, int G, int Bg, int K, const float* y, const float* norm,
                  float l2_eps, const float* z, const float* mean, const float* rstd,
                  const float* bn_w, const float* mg, const float* mgx, float* dz, const float* W,
@@ -387,6 +387,16 @@ int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const float* Hn, int
                             int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
                             int N, int D, float T, const float* lse, const float* grad_out, float* dU,
                             float* dI, float* dhl, float* ws, void* stream);
+/* The same pair in fp32 compute mode: the tiles run on v_mfma_f32_32x32x2_f32 with fp32 operands
+ * (exact f32 products, no rounding of U, I); same arguments, workspace and outputs. */
+int rs_inbatch_ce_fused_f32_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
+                                int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
+                                int N, int D, float T, float* lse, float* row_loss, float* loss, float* ws,
+                                void* stream);
+int rs_inbatch_ce_fused_f32_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
+                                int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
+                                int N, int D, float T, const float* lse, const float* grad_out, float* dU,
+                                float* dI, float* dhl, float* ws, void* stream);
 /* dU[i] += sum_n dhl[i,n] H[i,n];  dH[i,n] = dhl[i,n] U[i]   (hard-negative bmm backward; dH in
  * the layout of H) */
 int rs_hardneg_bwd(const float* U, const float* Hn, int64_t h_row_stride, int64_t h_slot_stride,

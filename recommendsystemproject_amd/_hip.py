@@ -77,7 +77,7 @@ SIGNATURES = {
     'rs_tower_wgrad_split': (i32, [i32, i32, i32]),
     'rs_tower_wgrad_ws_floats': (i64, [i32, i32, i32]),
     'rs_tower_wgrad_sync_ints': (i32, [i32, i32]),
-    'rs_tower_wgrad': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    'rs_tower_wgrad': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp]),
     'rs_tower_sync_ints': (i32, [i32, i32]),
     'rs_tower_stats': (i32, [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, f32, vp]),
     'rs_tower_fwd': (i32, [vp, i32, i32, i32, vp, vp, vp, vp, i32, f32, vp, i32, vp, vp, vp, i32, vp, vp,
@@ -91,6 +91,9 @@ SIGNATURES = {
     'rs_inbatch_ce_fused_fwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp]),
     'rs_inbatch_ce_fused_bwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp,
                                       vp]),
+    'rs_inbatch_ce_fused_f32_fwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp]),
+    'rs_inbatch_ce_fused_f32_bwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp,
+                                          vp, vp]),
     'rs_inbatch_ce_fwd': (i32, [vp, i32, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp]),
     'rs_inbatch_ce_bwd': (i32, [vp, i32, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp]),
     'rs_inbatch_logits': (i32, [vp, i32, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, i64, vp]),

@@ -18,6 +18,13 @@
 // dI) whose bf16 fragments stay in registers, and streams 32-row tiles of the other matrix
 // through LDS. Column splits give >= 256 workgroups at B = 4096; their partials are reduced in
 // a fixed order (deterministic).
+//
+// fp32 compute mode runs the same kernels on v_mfma_f32_32x32x2_f32 (exact f32 products, a
+// k-ordered fma chain; 64 cycles per instruction and SIMD, 1/16 of the bf16 rate): the streamed
+// tiles are staged in LDS as fp32, the owned fragments are fp32 registers, and the dS^T
+// accumulator elements are the B operand of the gradient MFMA as they stand (no packing).
+#include <type_traits>
+
 #include "common.h"
 
 namespace rs {
@@ -79,24 +86,32 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* lo, const __bf16* hi) {
 // round trip (the loop ran at ~3,600 cycles per tile against ~600 of MFMA and exp work). The
 // backward stages kBT / 2 tiles per batch: its gradient accumulators leave no room for a 4-tile
 // register stage at two waves per SIMD.
+// fp32 tiles take twice the LDS: the forward stages 2 tiles per batch, the backward 1 (the LDS
+// image holds 2 x 2 tiles, 68 KB: two workgroups per CU).
 constexpr int kBT = 4;
-template <int MODE>
-constexpr int batch_tiles() { return MODE == 0 ? kBT : kBT / 2; }
+template <int MODE, bool F32>
+constexpr int batch_tiles() { return F32 ? (MODE == 0 ? kBT / 2 : kBT / 4) : (MODE == 0 ? kBT : kBT / 2); }
 
 // v_exp_f32 directly: exp2f() adds a denormal-range fix-up (compare, select, ldexp) per call
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-template <int D>
+template <int D, bool F32>
 struct CeLds {
-  __bf16 Ts[2][kBT * kTile * (D + 8)];
-  int64_t sid[2][kBT * kTile];
-  float slse[2][kBT * kTile];
+  using E = std::conditional_t<F32, float, __bf16>;
+  // row pitch: bf16 D + 8 (ds_read_b64_tr_b16 / b128 conflict-free), fp32 D + 4 (the b128 reads
+  // of 16 consecutive rows cover the 64 banks once)
+  static constexpr int PT = F32 ? D + 4 : D + 8;
+  static constexpr int NT = F32 ? kBT / 2 : kBT;  // tiles per LDS half
+  E Ts[2][NT * kTile * PT];
+  int64_t sid[2][NT * kTile];
+  float slse[2][NT * kTile];
 };
 
-template <int D, int MODE>
-__device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, CeLds<D>& L) {
-  constexpr int KS = D / 16;          // 32x32x16 k-steps over the embedding
-  constexpr int PT = D + 8;           // LDS pitch (bf16) of a streamed tile row
+template <int D, int MODE, bool F32>
+__device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, CeLds<D, F32>& L) {
+  using E = typename CeLds<D, F32>::E;
+  constexpr int KS = D / 16;          // 32x32x16 k-steps over the embedding (bf16)
+  constexpr int PT = CeLds<D, F32>::PT;
   constexpr int DB = D / 32;          // 32-wide blocks of the gradient
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = lane & 31, h = lane >> 5;
@@ -106,17 +121,29 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
   const int t_begin = split * a.split_rows;
   const int t_end = min(B, t_begin + a.split_rows);
 
-  // owned fragments: B operand of the S tile, lane (c, h) holds own[o][16 s + 8 h .. +7]
-  bf16x8 ob[KS];
+  // owned fragments: B operand of the S tile. bf16: lane (c, h) holds own[o][16 s + 8 h .. +7];
+  // fp32: own[o][h D/2 + s] for k-step s (k-steps pair embedding columns s and D/2 + s)
+  bf16x8 ob[F32 ? 1 : KS];
+  float obf[F32 ? D / 2 : 1];
+  if constexpr (F32) {
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    floatx4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = x0;
-    if (o_ok) {
-      const float* p = a.own + (int64_t)o * D + 16 * s + 8 * h;
-      x0 = *reinterpret_cast<const floatx4*>(p);
-      x1 = *reinterpret_cast<const floatx4*>(p + 4);
+    for (int s4 = 0; s4 < D / 8; ++s4) {
+      floatx4 x = {0.f, 0.f, 0.f, 0.f};
+      if (o_ok) x = *reinterpret_cast<const floatx4*>(a.own + (int64_t)o * D + h * (D / 2) + 4 * s4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) obf[4 * s4 + j] = x[j];
     }
-    ob[s] = cvt8(x0, x1);
+  } else {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      floatx4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = x0;
+      if (o_ok) {
+        const float* p = a.own + (int64_t)o * D + 16 * s + 8 * h;
+        x0 = *reinterpret_cast<const floatx4*>(p);
+        x1 = *reinterpret_cast<const floatx4*>(p + 4);
+      }
+      ob[s] = cvt8(x0, x1);
+    }
   }
   const int64_t id_o = (a.ids && o_ok) ? a.ids[(int64_t)o * a.id_stride] : 0;
   const int o_base = blockIdx.x * (kOwnW * kWaves) + __builtin_amdgcn_readfirstlane(wave) * kOwnW;
@@ -137,7 +164,7 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
   // batch staging: kBT tiles of 32 rows x D fp32 -> bf16 LDS, float4 per slot
   constexpr int NTHR = 64 * kWaves;
   constexpr int SL = kTile * D / 4 / NTHR;  // float4 slots per thread per tile
-  constexpr int BT = batch_tiles<MODE>();   // tiles per batch
+  constexpr int BT = batch_tiles<MODE, F32>();  // tiles per batch
   constexpr int BR = BT * kTile;            // rows per batch
   static_assert(BR <= NTHR, "one id / lse per thread and batch row");
   struct Stage {
@@ -170,10 +197,14 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
       for (int i = 0; i < SL; ++i) {
         const int slot = tid + NTHR * i;
         const int row = k * kTile + slot / (D / 4), col = (slot % (D / 4)) * 4;
-        bf16x4 v;
-        v[0] = (__bf16)R.v[k][i][0]; v[1] = (__bf16)R.v[k][i][1];
-        v[2] = (__bf16)R.v[k][i][2]; v[3] = (__bf16)R.v[k][i][3];
-        *reinterpret_cast<bf16x4*>(&L.Ts[hf][row * PT + col]) = v;
+        if constexpr (F32) {
+          *reinterpret_cast<floatx4*>(&L.Ts[hf][row * PT + col]) = R.v[k][i];
+        } else {
+          bf16x4 v;
+          v[0] = (__bf16)R.v[k][i][0]; v[1] = (__bf16)R.v[k][i][1];
+          v[2] = (__bf16)R.v[k][i][2]; v[3] = (__bf16)R.v[k][i][3];
+          *reinterpret_cast<bf16x4*>(&L.Ts[hf][row * PT + col]) = v;
+        }
       }
     if (tid < BR) {
       L.sid[hf][tid] = R.id;
@@ -183,21 +214,32 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
   float dg = 0.f;  // fwd: S_oo / T, captured by the lane that meets the diagonal
   bool has_dg = false;
   auto consume = [&](int hf, int k, int t0) {
-    const __bf16* T = &L.Ts[hf][k * kTile * PT];
+    const E* T = &L.Ts[hf][k * kTile * PT];
     const int64_t* sidk = &L.sid[hf][k * kTile];
     // S^T tile: C[t][o] = str[t] . own[o]; A = streamed rows (lane c: row t0 + c)
-    // two accumulator chains (even / odd k-steps) halve the dependent-MFMA latency
-    floatx16 acc, acc1;
+    floatx16 acc;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = acc1[e] = 0.f;
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    if constexpr (F32) {
+      // one chain: the f32 MFMA's dependent latency equals its issue interval (64 cycles)
 #pragma unroll
-    for (int s = 0; s < KS; s += 2) {
-      const bf16x8 af0 = *reinterpret_cast<const bf16x8*>(&T[c * PT + 16 * s + 8 * h]);
-      const bf16x8 af1 = *reinterpret_cast<const bf16x8*>(&T[c * PT + 16 * s + 16 + 8 * h]);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af0, ob[s], acc, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af1, ob[s + 1], acc1, 0, 0, 0);
+      for (int s4 = 0; s4 < D / 8; ++s4) {
+        const floatx4 a4 = *reinterpret_cast<const floatx4*>(&T[c * PT + h * (D / 2) + 4 * s4]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[j], obf[4 * s4 + j], acc, 0, 0, 0);
+      }
+    } else {
+      // two accumulator chains (even / odd k-steps) halve the dependent-MFMA latency
+      floatx16 acc1 = acc;
+#pragma unroll
+      for (int s = 0; s < KS; s += 2) {
+        const bf16x8 af0 = *reinterpret_cast<const bf16x8*>(&T[c * PT + 16 * s + 8 * h]);
+        const bf16x8 af1 = *reinterpret_cast<const bf16x8*>(&T[c * PT + 16 * s + 16 + 8 * h]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af0, ob[s], acc, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af1, ob[s + 1], acc1, 0, 0, 0);
+      }
+      acc += acc1;
     }
-    acc += acc1;
     // element e of this lane: streamed row t = t0 + 8(e>>2) + 4h + (e&3), owned column o.
     // The tile's ids are read up front as vectors and the masks are selects: a per-element
     // `if (ids && ...) sid[...]` became a divergent branch with its own LDS round trip.
@@ -250,8 +292,6 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
         run_m = nm;
       }
     } else {
-      // dS^T tile -> bf16 operand fragments (k-step 0: registers 0..7, k-step 1: 8..15)
-      bf16x8 xf[2];
       float lt[16];
       if constexpr (MODE == 2) {
 #pragma unroll
@@ -281,19 +321,34 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
           if (t >= B || !o_ok) dv[e] = 0.f;
         }
       }
+      if constexpr (F32) {
+        // grad^T[d][o] += sum_t str^T[d][t] dS^T[t][o], k-step s pairing tile rows
+        // 8(s>>2) + (s&3) (half 0) and that + 4 (half 1): B = this lane's dv[s] as it stands,
+        // A = the staged row's column 32 db + c
 #pragma unroll
-      for (int e = 0; e < 16; ++e) xf[e >> 3][e & 7] = (__bf16)dv[e];
-      // grad^T[d][o] += sum_t str^T[d][t] dS^T[t][o]: A = transposed streamed tile,
-      // element j of lane half h <-> tile row 16 kstep + 8 (j>>2) + 4 h + (j&3)
-      const int g16 = lane >> 4, lq = (lane & 15) >> 2, lp = lane & 3;
+        for (int s = 0; s < 16; ++s) {
+          const int tr = 8 * (s >> 2) + 4 * h + (s & 3);
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int r0 = 16 * k + 4 * (g16 >> 1) + lq;
+          for (int db = 0; db < DB; ++db)
+            gacc[db] = __builtin_amdgcn_mfma_f32_32x32x2f32(T[tr * PT + 32 * db + c], dv[s], gacc[db], 0, 0, 0);
+        }
+      } else {
+        // dS^T tile -> bf16 operand fragments (k-step 0: registers 0..7, k-step 1: 8..15)
+        bf16x8 xf[2];
 #pragma unroll
-        for (int db = 0; db < DB; ++db) {
-          const __bf16* p = &T[r0 * PT + 32 * db + 16 * (g16 & 1) + 4 * lp];
-          const bf16x8 af = tr_frag(p, p + 8 * PT);
-          gacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, xf[k], gacc[db], 0, 0, 0);
+        for (int e = 0; e < 16; ++e) xf[e >> 3][e & 7] = (__bf16)dv[e];
+        // grad^T[d][o] += sum_t str^T[d][t] dS^T[t][o]: A = transposed streamed tile,
+        // element j of lane half h <-> tile row 16 kstep + 8 (j>>2) + 4 h + (j&3)
+        const int g16 = lane >> 4, lq = (lane & 15) >> 2, lp = lane & 3;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int r0 = 16 * k + 4 * (g16 >> 1) + lq;
+#pragma unroll
+          for (int db = 0; db < DB; ++db) {
+            const __bf16* p = &T[r0 * PT + 32 * db + 16 * (g16 & 1) + 4 * lp];
+            const bf16x8 af = tr_frag(p, p + 8 * PT);
+            gacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, xf[k], gacc[db], 0, 0, 0);
+          }
         }
       }
     }
@@ -349,19 +404,19 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
   }
 }
 
-template <int D, int MODE>
+template <int D, int MODE, bool F32>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(2))) void ce_tile_kernel(CeArgs a) {
-  __shared__ __attribute__((aligned(16))) CeLds<D> lds;
-  ce_tile_body<D, MODE>(a, blockIdx.y, lds);
+  __shared__ __attribute__((aligned(16))) CeLds<D, F32> lds;
+  ce_tile_body<D, MODE, F32>(a, blockIdx.y, lds);
 }
 
 // dU and dI in one launch (blockIdx.z): the two halves are independent given lse, and 1,024
 // workgroups hide each other's tile latencies better than two back-to-back 512-workgroup grids
-template <int D>
+template <int D, bool F32>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(2))) void ce_bwd_pair_kernel(CeArgs aU, CeArgs aI) {
-  __shared__ __attribute__((aligned(16))) CeLds<D> lds;  // one image shared by both halves
-  if (blockIdx.z == 0) ce_tile_body<D, 1>(aU, blockIdx.y, lds);
-  else ce_tile_body<D, 2>(aI, blockIdx.y, lds);
+  __shared__ __attribute__((aligned(16))) CeLds<D, F32> lds;  // one image shared by both halves
+  if (blockIdx.z == 0) ce_tile_body<D, 1, F32>(aU, blockIdx.y, lds);
+  else ce_tile_body<D, 2, F32>(aI, blockIdx.y, lds);
 }
 
 // per user row: merge the split statistics with the hard-negative logits -> lse, row loss
@@ -466,11 +521,11 @@ int splits_for(int B, bool bwd) {
   return ns < 1 ? 1 : ns;
 }
 
-template <int MODE>
+template <int MODE, bool F32>
 int launch_tiles(const CeArgs& a, int D, int NS, hipStream_t st) {
   const dim3 grid(cdiv(a.B, kOwnW * kWaves), NS);
-  if (D == 128) ce_tile_kernel<128, MODE><<<grid, 64 * kWaves, 0, st>>>(a);
-  else ce_tile_kernel<64, MODE><<<grid, 64 * kWaves, 0, st>>>(a);
+  if (D == 128) ce_tile_kernel<128, MODE, F32><<<grid, 64 * kWaves, 0, st>>>(a);
+  else ce_tile_kernel<64, MODE, F32><<<grid, 64 * kWaves, 0, st>>>(a);
   return 0;
 }
 
@@ -485,16 +540,18 @@ extern "C" int64_t rs_inbatch_ce_fused_ws_bytes(int B, int D) {
   return (fwd > bwd ? fwd : bwd) * (int64_t)sizeof(float);
 }
 
-extern "C" int rs_inbatch_ce_fused_fwd(const float* U, const float* I, const float* Hn,
-                                       int64_t h_row_stride, int64_t h_slot_stride,
-                                       const int64_t* item_ids, int64_t id_stride, int B, int N,
-                                       int D, float T, float* lse, float* row_loss, float* loss,
-                                       float* ws, void* stream) {
-  RS_CHECK_ARG(U && I && lse && row_loss && loss && ws, "rs_inbatch_ce_fused_fwd: null pointer");
+namespace {
+
+template <bool F32>
+int ce_fused_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride, int64_t h_slot_stride,
+                 const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T, float* lse,
+                 float* row_loss, float* loss, float* ws, void* stream) {
+  const char* fn = F32 ? "rs_inbatch_ce_fused_f32_fwd" : "rs_inbatch_ce_fused_fwd";
+  RS_CHECK_ARG(U && I && lse && row_loss && loss && ws, "%s: null pointer", fn);
   RS_CHECK_ARG(B >= 1 && (D == 64 || D == 128) && N >= 0 && N <= 64,
-               "rs_inbatch_ce_fused_fwd: needs D in {64, 128}, N <= 64 (B=%d N=%d D=%d)", B, N, D);
-  RS_CHECK_ARG(N == 0 || Hn, "rs_inbatch_ce_fused_fwd: hard negatives need H");
-  RS_CHECK_ARG(aligned16(U) && aligned16(I), "rs_inbatch_ce_fused_fwd: U, I must be 16-byte aligned");
+               "%s: needs D in {64, 128}, N <= 64 (B=%d N=%d D=%d)", fn, B, N, D);
+  RS_CHECK_ARG(N == 0 || Hn, "%s: hard negatives need H", fn);
+  RS_CHECK_ARG(aligned16(U) && aligned16(I), "%s: U, I must be 16-byte aligned", fn);
   hipStream_t st = as_stream(stream);
   const int NS = splits_for(B, false);
   CeArgs a{};
@@ -502,25 +559,25 @@ extern "C" int rs_inbatch_ce_fused_fwd(const float* U, const float* I, const flo
   a.split_rows = cdiv(cdiv(B, NS), kTile) * kTile;
   a.part_m = ws; a.part_s = ws + (int64_t)NS * B; a.diag = ws + (int64_t)2 * NS * B;
   const int NSr = cdiv(B, a.split_rows);
-  launch_tiles<0>(a, D, NSr, st);
-  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_fwd tiles");
+  launch_tiles<0, F32>(a, D, NSr, st);
+  RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_fwd tiles" : "rs_inbatch_ce_fused_fwd tiles");
   const HStrideArgs hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
   ce_finish_fwd_kernel<<<cdiv(B, 4), 256, 0, st>>>(a.part_m, a.part_s, a.diag, NSr, U, Hn, hs.row, hs.slot, B,
                                                    N, D, a.invT, lse, row_loss);
-  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_fwd finish");
+  RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_fwd finish" : "rs_inbatch_ce_fused_fwd finish");
   return rs_sum(row_loss, B, 1.f / (float)B, loss, stream);
 }
 
-extern "C" int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const float* Hn,
-                                       int64_t h_row_stride, int64_t h_slot_stride,
-                                       const int64_t* item_ids, int64_t id_stride, int B, int N,
-                                       int D, float T, const float* lse, const float* grad_out,
-                                       float* dU, float* dI, float* dhl, float* ws, void* stream) {
-  RS_CHECK_ARG(U && I && lse && dU && dI && ws, "rs_inbatch_ce_fused_bwd: null pointer");
-  RS_CHECK_ARG(B >= 1 && (D == 64 || D == 128) && N >= 0 && N <= 64, "rs_inbatch_ce_fused_bwd: bad shape");
-  RS_CHECK_ARG(N == 0 || (Hn && dhl), "rs_inbatch_ce_fused_bwd: hard negatives need H, dhl");
+template <bool F32>
+int ce_fused_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride, int64_t h_slot_stride,
+                 const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T, const float* lse,
+                 const float* grad_out, float* dU, float* dI, float* dhl, float* ws, void* stream) {
+  const char* fn = F32 ? "rs_inbatch_ce_fused_f32_bwd" : "rs_inbatch_ce_fused_bwd";
+  RS_CHECK_ARG(U && I && lse && dU && dI && ws, "%s: null pointer", fn);
+  RS_CHECK_ARG(B >= 1 && (D == 64 || D == 128) && N >= 0 && N <= 64, "%s: bad shape", fn);
+  RS_CHECK_ARG(N == 0 || (Hn && dhl), "%s: hard negatives need H, dhl", fn);
   RS_CHECK_ARG(aligned16(U) && aligned16(I) && aligned16(dU) && aligned16(dI),
-               "rs_inbatch_ce_fused_bwd: operands must be 16-byte aligned");
+               "%s: operands must be 16-byte aligned", fn);
   hipStream_t st = as_stream(stream);
   const int NS = splits_for(B, true);
   CeArgs a{};
@@ -535,15 +592,49 @@ extern "C" int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const flo
   aI.own = I; aI.str = U;
   aI.part_d = ws + (int64_t)NSr * n;
   const dim3 grid(cdiv(B, kOwnW * kWaves), NSr, 2);
-  if (D == 128) ce_bwd_pair_kernel<128><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
-  else ce_bwd_pair_kernel<64><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
-  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd tiles");
+  if (D == 128) ce_bwd_pair_kernel<128, F32><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
+  else ce_bwd_pair_kernel<64, F32><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
+  RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_bwd tiles" : "rs_inbatch_ce_fused_bwd tiles");
   ce_reduce_kernel<<<(int)cdiv(2 * n / 4, 256), 256, 0, st>>>(ws, NSr, n, dU, dI, I, U, grad_out, B, a.invT);
-  RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd reduce");
+  RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_bwd reduce" : "rs_inbatch_ce_fused_bwd reduce");
   if (N) {
     const HStrideArgs hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
     ce_hard_bwd_kernel<<<cdiv(B, 4), 256, 0, st>>>(U, Hn, hs.row, hs.slot, B, N, D, a.invT, lse, grad_out, dhl);
-    RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd hard");
+    RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_bwd hard" : "rs_inbatch_ce_fused_bwd hard");
   }
   return 0;
+}
+
+}  // namespace
+
+extern "C" int rs_inbatch_ce_fused_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
+                                       int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
+                                       int N, int D, float T, float* lse, float* row_loss, float* loss, float* ws,
+                                       void* stream) {
+  return ce_fused_fwd<false>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, row_loss,
+                             loss, ws, stream);
+}
+
+extern "C" int rs_inbatch_ce_fused_f32_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
+                                           int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
+                                           int N, int D, float T, float* lse, float* row_loss, float* loss, float* ws,
+                                           void* stream) {
+  return ce_fused_fwd<true>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, row_loss,
+                            loss, ws, stream);
+}
+
+extern "C" int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
+                                       int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
+                                       int N, int D, float T, const float* lse, const float* grad_out, float* dU,
+                                       float* dI, float* dhl, float* ws, void* stream) {
+  return ce_fused_bwd<false>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, grad_out,
+                             dU, dI, dhl, ws, stream);
+}
+
+extern "C" int rs_inbatch_ce_fused_f32_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
+                                           int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
+                                           int N, int D, float T, const float* lse, const float* grad_out, float* dU,
+                                           float* dI, float* dhl, float* ws, void* stream) {
+  return ce_fused_bwd<true>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, grad_out,
+                            dU, dI, dhl, ws, stream);
 }

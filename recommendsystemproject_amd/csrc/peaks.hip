@@ -10,19 +10,13 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// dst[i] = src[i] over n float4s, 4 independent float4 loads per lane in flight per iteration
+// dst[i] = src[i] over n float4s, one float4 per lane and n / 256 workgroups: the shape that
+// measured best on the box (6.25 TB/s for 2 GiB, against 5.2-5.5 TB/s for grid-stride loops with
+// 4-16 float4s per lane, default or non-temporal policy; tools/copy_variants.hip)
 __global__ __launch_bounds__(256) void copy_f4_kernel(const floatx4* __restrict__ src, floatx4* __restrict__ dst,
                                                       int64_t n) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n; i += 4 * stride) {
-    const floatx4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    dst[i] = a;
-    dst[i + stride] = b;
-    dst[i + 2 * stride] = c;
-    dst[i + 3 * stride] = d;
-  }
-  for (; i < n; i += stride) dst[i] = src[i];
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) dst[i] = src[i];
 }
 
 // every wave: `iters` x 4 back-to-back 32x32x16 bf16 MFMAs (4 accumulators), operands from
@@ -57,8 +51,8 @@ extern "C" int rs_peak_copy(const void* src, void* dst, int64_t bytes, void* str
   RS_CHECK_ARG(src && dst && bytes >= 16 && bytes % 16 == 0 && aligned16(src) && aligned16(dst),
                "rs_peak_copy: needs 16-byte aligned buffers, bytes a multiple of 16");
   const int64_t n = bytes / 16;
-  // 8 workgroups of 256 lanes per CU (256 CUs): enough loads in flight to cover HBM latency
-  copy_f4_kernel<<<2048, 256, 0, as_stream(stream)>>>(reinterpret_cast<const floatx4*>(src),
+  RS_CHECK_ARG(n <= (int64_t)256 * 0x7fffffff, "rs_peak_copy: too large");
+  copy_f4_kernel<<<(unsigned)cdiv(n, (int64_t)256), 256, 0, as_stream(stream)>>>(reinterpret_cast<const floatx4*>(src),
                                                       reinterpret_cast<floatx4*>(dst), n);
   RS_CHECK_LAUNCH("rs_peak_copy");
   return 0;

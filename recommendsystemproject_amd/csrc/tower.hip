@@ -882,6 +882,8 @@ int bwd_dispatch(const TwArgs& a, hipStream_t st) {
 // column per lane) into v_mfma_f32_32x32x16_bf16. The S partial tiles meet in a fixed order: the
 // workgroup arriving last for a tile (write-through partials, one ticket per workgroup) sums them
 // s = 0..S-1 and adds the sum into dW (and db: fp32 column sums of the unrounded dz).
+// fp32 mode: the same kernel on v_mfma_f32_32x32x2_f32, chunks staged as fp32 (pitch 96 floats:
+// the two rows of a k-step fall in opposite bank halves) and read one element per lane.
 typedef short wshortx4 __attribute__((ext_vector_type(4)));
 typedef short wshortx8 __attribute__((ext_vector_type(8)));
 typedef float f16v __attribute__((ext_vector_type(16)));
@@ -911,10 +913,12 @@ __device__ __forceinline__ bf16x8t wtr_frag(const __bf16* lo, const __bf16* hi) 
   return __builtin_bit_cast(bf16x8t, v);
 }
 
+template <typename T>
 __global__ __launch_bounds__(256) void tower_wgrad_kernel(WgArgs a) {
   constexpr int D = 3;  // chunks of loads in flight per thread
-  __shared__ __attribute__((aligned(16))) __bf16 Ys[2][WCH][WPITCH];
-  __shared__ __attribute__((aligned(16))) __bf16 Xs[2][WCH][WPITCH];
+  constexpr bool F32 = sizeof(T) == 4;
+  __shared__ __attribute__((aligned(16))) T Ys[2][WCH][WPITCH];
+  __shared__ __attribute__((aligned(16))) T Xs[2][WCH][WPITCH];
   __shared__ float csum[16][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int ji = 0;
@@ -950,8 +954,8 @@ __global__ __launch_bounds__(256) void tower_wgrad_kernel(WgArgs a) {
       const f4 x = rok && k0 + lc < K ? rx[u] : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int e = 0; e < 4; ++e) ysum[e] += y[e];
-      lds_put4<__bf16>(&Ys[buf][row][lc], y);
-      lds_put4<__bf16>(&Xs[buf][row][lc], x);
+      lds_put4<T>(&Ys[buf][row][lc], y);
+      lds_put4<T>(&Xs[buf][row][lc], x);
     }
   };
   f16v acc;
@@ -971,13 +975,23 @@ __global__ __launch_bounds__(256) void tower_wgrad_kernel(WgArgs a) {
       stage(ch, buf, ry[st], rx[st]);
       lds_barrier();
       load(min(ch + D, nch - 1), ry[st], rx[st]);
+      if constexpr (F32) {
+        // k-step q: rows 2q (lanes 0-31) and 2q + 1 (lanes 32-63); A = dz[m][n0 + 32 wm + c],
+        // B = h[m][k0 + 32 wn + c]
+        const int c = lane & 31, hh = lane >> 5;
 #pragma unroll
-      for (int ks = 0; ks < WCH / 16; ++ks) {
-        const __bf16* py = &Ys[buf][16 * ks + trow][32 * wm + tcol];
-        const __bf16* px = &Xs[buf][16 * ks + trow][32 * wn + tcol];
-        const bf16x8t af = wtr_frag(py, py + 4 * WPITCH);
-        const bf16x8t bf = wtr_frag(px, px + 4 * WPITCH);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
+        for (int q = 0; q < WCH / 2; ++q)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ys[buf][2 * q + hh][32 * wm + c], Xs[buf][2 * q + hh][32 * wn + c],
+                                                     acc, 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < WCH / 16; ++ks) {
+          const __bf16* py = &Ys[buf][16 * ks + trow][32 * wm + tcol];
+          const __bf16* px = &Xs[buf][16 * ks + trow][32 * wn + tcol];
+          const bf16x8t af = wtr_frag(py, py + 4 * WPITCH);
+          const bf16x8t bf = wtr_frag(px, px + 4 * WPITCH);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
+        }
       }
     }
   }
@@ -1154,7 +1168,8 @@ extern "C" int rs_tower_bwd(const float* gin, int G, int Bg, int K, const float*
 // Weight gradients of up to 4 Linears in one launch (tower_wgrad_kernel). Per layer i: dz_i
 // [M][N_i], h_i [M][K_i], dW_i [N_i][K_i] += dz^T h, db_i [N_i] += colsum(dz) (may be NULL);
 // ws_i: rs_tower_wgrad_ws_floats(M, N_i, K_i) floats; sync_i: rs_tower_wgrad_sync_ints(N_i, K_i)
-// ints, zero on entry (zero again on exit). bf16 MFMA (bf16 compute mode only).
+// ints, zero on entry (zero again on exit). bf16 != 0: operands rounded to bf16 on
+// v_mfma_f32_32x32x16_bf16; 0: exact fp32 products on v_mfma_f32_32x32x2_f32.
 extern "C" int rs_tower_wgrad_split(int M, int N, int K) {
   const int tiles = cdiv(N, 64) * cdiv(K, 64);
   int S = (256 + tiles - 1) / tiles;
@@ -1171,7 +1186,7 @@ extern "C" int rs_tower_wgrad_sync_ints(int N, int K) { return cdiv(N, 64) * cdi
 
 extern "C" int rs_tower_wgrad(int nlayers, int M, const int* Ns, const int* Ks,
                               const float* const* dz, const float* const* h, float* const* dW,
-                              float* const* db, float* const* ws, int* const* sync, void* stream) {
+                              float* const* db, float* const* ws, int* const* sync, int bf16, void* stream) {
   RS_CHECK_ARG(nlayers >= 1 && nlayers <= WG_MAXJ && M >= 1, "rs_tower_wgrad: bad nlayers %d / M %d", nlayers, M);
   WgArgs a{};
   a.nj = nlayers;
@@ -1191,7 +1206,8 @@ extern "C" int rs_tower_wgrad(int nlayers, int M, const int* Ns, const int* Ks,
     j.wg0 = wg;
     wg += j.tn * j.tk * j.S;
   }
-  tower_wgrad_kernel<<<wg, 256, 0, as_stream(stream)>>>(a);
+  if (bf16) tower_wgrad_kernel<__bf16><<<wg, 256, 0, as_stream(stream)>>>(a);
+  else tower_wgrad_kernel<float><<<wg, 256, 0, as_stream(stream)>>>(a);
   RS_CHECK_LAUNCH("rs_tower_wgrad");
   return 0;
 }

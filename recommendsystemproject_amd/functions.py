@@ -640,9 +640,10 @@ def _tower_sync(mlp, dev, n):
     return t
 
 
-def _tower_wgrad_grouped(mlp, jobs, M):
-    """dW += dz^T h, db += colsum(dz) of every Linear of the tower in one launch (rs_tower_wgrad,
-    bf16 compute mode): 64 x 64 dW tiles x row splits, fixed-order reduction of the splits."""
+def _tower_wgrad_grouped(mlp, jobs, M, bf):
+    """dW += dz^T h, db += colsum(dz) of every Linear of the tower in one launch (rs_tower_wgrad;
+    bf16 or fp32 MFMA by the compute mode): 64 x 64 dW tiles x row splits, fixed-order reduction
+    of the splits."""
     import ctypes as C
     L = _hip.lib()
     dev = jobs[0][0].device
@@ -663,7 +664,7 @@ def _tower_wgrad_grouped(mlp, jobs, M):
             P(*[grad_of(lin.weight).data_ptr() for _, _, lin in jobs]),
             P(*[grad_of(lin.bias).data_ptr() if lin.bias is not None else None for _, _, lin in jobs]),
             P(*[ws[o:].data_ptr() for o in woff]), P(*[t[o:].data_ptr() for o in soff])]
-    ops.call('rs_tower_wgrad', n, M, *[C.addressof(a) for a in arrs], ops.stream())
+    ops.call('rs_tower_wgrad', n, M, *[C.addressof(a) for a in arrs], bf, ops.stream())
 
 
 class TowerChainFn(torch.autograd.Function):
@@ -753,7 +754,7 @@ class TowerChainFn(torch.autograd.Function):
         f32 = torch.float32
         off = ctx.sync_off
         gin, mg, mgx = dout, None, None
-        wjobs = []  # bf16 mode: every layer's weight gradient in one grouped launch at the end
+        wjobs = []  # every layer's weight gradient in one grouped launch at the end
         for j in range(n_hidden, -1, -1):
             lin = seq[4 * j]
             A, h, mean, rstd, bn_in, relu, dp, site = layers[j]
@@ -777,10 +778,7 @@ class TowerChainFn(torch.autograd.Function):
                      omgx.data_ptr(), grad_of(bn_in.weight).data_ptr(), grad_of(bn_in.bias).data_ptr(), bf,
                      ops.stream())
             off += L.rs_tower_sync_ints(G, N)
-            if bf:
-                wjobs.append((dz, h, lin))
-            else:
-                _tower_wgrad(dz, h, lin)
+            wjobs.append((dz, h, lin))
             gin, mg, mgx = g, omg, omgx
         # feature_bn's dx: the BatchNorm backward prologue with no GEMM
         x, _, m0, r0, fbn = layers[0][:5]
@@ -790,8 +788,8 @@ class TowerChainFn(torch.autograd.Function):
                  r0.data_ptr(), fbn.weight.data_ptr(), mg.data_ptr(), mgx.data_ptr(), dx.data_ptr(), None, 0,
                  None, None, None, None, None, 0, 0.0, None, 0, None, None, None, None, None, None, None, None,
                  bf, ops.stream())
-        if wjobs:
-            _tower_wgrad_grouped(ctx.mlp, wjobs, M)
+        for i in range(0, len(wjobs), 4):  # up to 4 Linears per launch (csrc/tower.hip WG_MAXJ)
+            _tower_wgrad_grouped(ctx.mlp, wjobs[i:i + 4], M, bf)
         ctx.layers = None
         return (None, None, None, dx, None) + (None,) * (len(ctx.needs_input_grad) - 5)
 
@@ -808,8 +806,9 @@ class InBatchLossFn(torch.autograd.Function):
         I = I.contiguous()
         B, D = int(U.shape[0]), int(U.shape[1])
         dev = U.device
-        # bf16 mode: S tiles recomputed on the MFMA, never stored (csrc/ce_fused.hip)
-        fused = precision.compute_dtype() == 'bf16' and D in (64, 128)
+        # S tiles recomputed on the MFMA (bf16 or f32 operands), never stored (csrc/ce_fused.hip)
+        fused = D in (64, 128)
+        sfx = '' if precision.compute_dtype() == 'bf16' else '_f32'
         S = None
         if not fused:
             S = torch.empty(B, B, device=dev, dtype=torch.float32)
@@ -836,7 +835,7 @@ class InBatchLossFn(torch.autograd.Function):
         loss = torch.empty((), device=dev, dtype=torch.float32)
         if fused:
             w = ops.ws(_hip.lib().rs_inbatch_ce_fused_ws_bytes(B, D), dev)
-            _hip.call('rs_inbatch_ce_fused_fwd', U.data_ptr(), I.data_ptr(), ops.P(Hc), hsr, hss, ops.P(ids), st,
+            _hip.call(f'rs_inbatch_ce_fused{sfx}_fwd', U.data_ptr(), I.data_ptr(), ops.P(Hc), hsr, hss, ops.P(ids), st,
                       B, N, D, float(temperature), lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(),
                       w.data_ptr(), ops.stream())
         else:
@@ -846,6 +845,7 @@ class InBatchLossFn(torch.autograd.Function):
         ctx.save_for_backward(U, I, Hc if Hc is not None else U)
         ctx.S, ctx.ids, ctx.st, ctx.N, ctx.T, ctx.lse = S, ids, st, N, float(temperature), lse
         ctx.fused = fused
+        ctx.sfx = sfx
         ctx.hs = (hsr, hss)
         return loss
 
@@ -862,7 +862,7 @@ class InBatchLossFn(torch.autograd.Function):
             dU = torch.empty_like(U)
             dI = torch.empty_like(I)
             w = ops.ws(_hip.lib().rs_inbatch_ce_fused_ws_bytes(B, D), U.device)
-            _hip.call('rs_inbatch_ce_fused_bwd', U.data_ptr(), I.data_ptr(), ops.P(Hc) if N else None,
+            _hip.call(f'rs_inbatch_ce_fused{ctx.sfx}_bwd', U.data_ptr(), I.data_ptr(), ops.P(Hc) if N else None,
                       ctx.hs[0], ctx.hs[1], ops.P(ctx.ids), ctx.st, B, N, D, ctx.T, ctx.lse.data_ptr(),
                       gout.data_ptr(), dU.data_ptr(), dI.data_ptr(), ops.P(dhl), w.data_ptr(), ops.stream())
             dH = None

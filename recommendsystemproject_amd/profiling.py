@@ -165,6 +165,8 @@ WORK = {
     'rs_ffn_bwd_ln2_bf16': _ffn_bwd_ln2_work,
     'rs_inbatch_ce_fused_fwd': _ce_fused_work,
     'rs_inbatch_ce_fused_bwd': lambda a: _ce_fused_work(a, True),
+    'rs_inbatch_ce_fused_f32_fwd': _ce_fused_work,
+    'rs_inbatch_ce_fused_f32_bwd': lambda a: _ce_fused_work(a, True),
     'rs_gemm_add_layernorm': _gemm_ln_work,
     'rs_ffn_fwd_bf16': _ffn_fwd_work,
     'rs_ffn_bwd_bf16': _ffn_bwd_work,
@@ -202,6 +204,8 @@ EXPS = {
     'rs_attn_bwd': lambda a: float(a[6] * a[9] * a[7] * a[7]),
     'rs_inbatch_ce_fused_fwd': lambda a: float(a[7]) * (a[7] + a[8]),
     'rs_inbatch_ce_fused_bwd': lambda a: 2.0 * a[7] * (a[7] + a[8]),
+    'rs_inbatch_ce_fused_f32_fwd': lambda a: float(a[7]) * (a[7] + a[8]),
+    'rs_inbatch_ce_fused_f32_bwd': lambda a: 2.0 * a[7] * (a[7] + a[8]),
 }
 
 

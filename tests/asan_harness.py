@@ -61,10 +61,10 @@ Ns, Ks = (C.c_int * n)(256, 128, 128), (C.c_int * n)(300, 256, 128)
 P = C.c_void_p * n
 ptrs = P(fake, fake, fake)
 rc = L.rs_tower_wgrad(n, 4096, C.addressof(Ns), C.addressof(Ks), C.addressof(ptrs), C.addressof(ptrs),
-                      C.addressof(ptrs), C.addressof(ptrs), C.addressof(ptrs), C.addressof(ptrs), None)
+                      C.addressof(ptrs), C.addressof(ptrs), C.addressof(ptrs), C.addressof(ptrs), 1, None)
 assert rc != 0
 expect_fail('rs_tower_wgrad', 9, 4096, C.addressof(Ns), C.addressof(Ks), C.addressof(ptrs), C.addressof(ptrs),
-            C.addressof(ptrs), C.addressof(ptrs), C.addressof(ptrs), C.addressof(ptrs), None)
+            C.addressof(ptrs), C.addressof(ptrs), C.addressof(ptrs), C.addressof(ptrs), 0, None)
 # assorted entry points with bad shapes
 expect_fail('rs_gemm_f32', 0, 0, -1, 4, 4, 1.0, None, 4, None, 4, 0.0, None, 4, 0, None, None,
             0, 0, 0.0, None, 0, 0, None, 1, None, None)

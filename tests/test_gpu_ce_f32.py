@@ -1,0 +1,114 @@
+"""The fused in-batch CE in fp32 compute mode (csrc/ce_fused.hip on v_mfma_f32_32x32x2_f32,
+rs_inbatch_ce_fused_f32_*): TwoTowerModel.compute_loss (TwoTowerModel.py:81-140: logits U I^T / T,
+off-diagonal id collisions at -1e9, hard negatives appended, mean cross-entropy) against float64
+torch on the same fp32 operands -- no operand rounding, so the bound is fp32 summation error only
+(loss within 2e-6 relative, gradients within 2e-5 of their largest entry) -- and against the
+unfused fp32 path (S stored, rs_inbatch_ce_fwd / bwd + three GEMMs)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from recommendsystemproject_amd import _hip, ops, precision
+from recommendsystemproject_amd.functions import InBatchLossFn
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+
+
+def rnd(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g).to(DEV)
+
+
+def _ref64(U, I, ids, H, T, gout):
+    Ud = U.double().requires_grad_(True)
+    Id = I.double().requires_grad_(True)
+    logits = Ud @ Id.t() / T
+    if ids is not None:
+        coll = (ids[:, None] == ids[None, :]) & ~torch.eye(len(ids), dtype=torch.bool, device=U.device)
+        logits = logits.masked_fill(coll, -1e9)
+    Hd = None
+    if H is not None:
+        Hd = H.double().requires_grad_(True)
+        logits = torch.cat([logits, torch.einsum('bd,bnd->bn', Ud, Hd) / T], 1)
+    loss = F.cross_entropy(logits, torch.arange(len(U), device=U.device))
+    (loss * gout).backward()
+    return loss.item(), Ud.grad.float(), Id.grad.float(), (Hd.grad.float() if H is not None else None)
+
+
+def _run(B, D, N, coll, T=0.15, gout=0.7, seed=0):
+    assert precision.compute_dtype() == 'fp32'
+    U = F.normalize(rnd(B, D, seed=21 + seed), dim=1).requires_grad_(True)
+    I = F.normalize(rnd(B, D, seed=22 + seed), dim=1).requires_grad_(True)
+    ids = torch.randint(0, B // 2 if coll else 10 ** 9, (B,), device=DEV)
+    H = F.normalize(rnd(B, N, D, seed=23 + seed), dim=2).requires_grad_(True) if N else None
+    loss = InBatchLossFn.apply(U, I, ids, H, T)
+    loss.backward(torch.tensor(gout, device=DEV))
+    return loss, U, I, ids, H
+
+
+@pytest.mark.parametrize('B,D,N,coll', [(4096, 128, 0, True), (1000, 128, 3, True), (300, 64, 0, False),
+                                        (33, 128, 2, True), (1, 64, 0, False), (4096, 64, 0, True)])
+def test_fused_f32_ce_vs_float64(B, D, N, coll):
+    loss, U, I, ids, H = _run(B, D, N, coll)
+    l_ref, dU, dI, dH = _ref64(U.detach(), I.detach(), ids, H.detach() if N else None, 0.15, 0.7)
+    assert abs(loss.item() - l_ref) <= 2e-6 * max(1.0, abs(l_ref)), (loss.item(), l_ref)
+    # + an absolute floor at the gradient's unit g = gout / (B T): at B = 1 the exact gradient is
+    # 0 (p = 1) and the kernel's fp32 p - 1 leaves ~1e-8 g
+    floor = 1e-7 * 0.7 / (B * 0.15)
+    for a, b_ in ((U.grad, dU), (I.grad, dI)) + (((H.grad, dH),) if N else ()):
+        sc = b_.abs().max().item()
+        assert (a - b_).abs().max().item() <= 2e-5 * sc + floor, ((a - b_).abs().max().item(), sc)
+
+
+@pytest.mark.parametrize('B,splits', [(4096, 3), (4096, 5), (2000, 2), (777, 1)])
+def test_fused_f32_ce_ragged_splits(B, splits, monkeypatch):
+    """Column splits whose tile count is not a multiple of the staged batch (2 tiles forward, 1
+    backward in fp32), and a last split shorter than the others."""
+    monkeypatch.setenv('RSYS_CE_SPLITS', str(splits))
+    test_fused_f32_ce_vs_float64(B, 128, 0, True)
+
+
+def test_fused_f32_ce_matches_unfused_path():
+    """The fused fp32 kernels against the S-stored fp32 path at the C3 shape (B = 4096, D = 128)."""
+    B, D, T = 4096, 128, 0.1
+    loss, U, I, ids, _ = _run(B, D, 0, True, T=T, gout=1.0, seed=5)
+    Ud, Id = U.detach(), I.detach()
+    S = torch.empty(B, B, device=DEV)
+    ops.gemm(Ud, Id, S, B, B, D, transA=0, transB=1, lda=D, ldb=D, ldc=B)
+    lse = torch.empty(B, device=DEV)
+    rl = torch.empty(B, device=DEV)
+    l2 = torch.empty((), device=DEV)
+    st = ops.stream()
+    _hip.call('rs_inbatch_ce_fwd', S.data_ptr(), B, Ud.data_ptr(), None, 0, 0, ids.data_ptr(), 1, B, 0, D, T,
+              lse.data_ptr(), rl.data_ptr(), l2.data_ptr(), st)
+    g = torch.ones((), device=DEV)
+    _hip.call('rs_inbatch_ce_bwd', S.data_ptr(), B, Ud.data_ptr(), None, 0, 0, ids.data_ptr(), 1, B, 0, D, T,
+              lse.data_ptr(), g.data_ptr(), None, st)
+    dU = torch.empty_like(Ud)
+    dI = torch.empty_like(Id)
+    ops.gemm(S, Id, dU, B, D, B, transA=0, transB=0, lda=B, ldb=D, ldc=D)
+    ops.gemm(S, Ud, dI, B, D, B, transA=1, transB=0, lda=B, ldb=D, ldc=D)
+    assert abs(loss.item() - l2.item()) <= 2e-6 * abs(l2.item())
+    for a, b_ in ((U.grad, dU), (I.grad, dI)):
+        assert (a - b_).abs().max().item() <= 2e-5 * b_.abs().max().item()
+
+
+def test_fused_f32_ce_deterministic():
+    B, D = 4096, 128
+    U = F.normalize(rnd(B, D, seed=31), dim=1).requires_grad_(True)
+    I = F.normalize(rnd(B, D, seed=32), dim=1).requires_grad_(True)
+    ids = torch.randint(0, 3000, (B,), device=DEV)
+    res = []
+    for _ in range(2):
+        U.grad = I.grad = None
+        loss = InBatchLossFn.apply(U, I, ids, None, 0.1)
+        loss.backward()
+        res.append((loss.item(), U.grad.clone(), I.grad.clone()))
+    assert res[0][0] == res[1][0] and torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+
+
+def test_fused_f32_ce_bad_args():
+    with pytest.raises(RuntimeError, match='rs_inbatch_ce_fused_f32_fwd'):
+        _hip.call('rs_inbatch_ce_fused_f32_fwd', None, None, None, 0, 0, None, 0, 16, 0, 128, 0.1, None, None, None,
+                  None, 0)
