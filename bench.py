@@ -18,7 +18,12 @@ import os
 import sys
 import time
 
-import torch
+# hardware queues per process, read when HIP initialises: the step forks up to 5 streams (the
+# item tower, and per tower the lazy tables' sort + catch-up chains, functions._lookup_lazy);
+# with HIP's default 4 two of them share a queue and run serially (HIP default: 4; at most 32)
+os.environ.setdefault('GPU_MAX_HW_QUEUES', '8')
+
+import torch  # noqa: E402
 import torch.distributed as dist
 import yaml
 
@@ -26,6 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from recommendsystemproject_amd import dist as rdist  # noqa: E402
+from recommendsystemproject_amd import _hip  # noqa: E402
 from recommendsystemproject_amd import synth  # noqa: E402
 from recommendsystemproject_amd import precision  # noqa: E402
 from recommendsystemproject_amd.flat import ensure_flat  # noqa: E402
@@ -237,17 +243,33 @@ def measure_peaks(dev, copy_bytes=1 << 31, reps=5):
                    'v_mfma_f32_32x32x16_bf16, 2048 x 256-thread workgroups, best of 5 (csrc/peaks.hip)'}
 
 
-def _copy_into(dst, src):
-    """Next resident batch -> the static input slot the captured graphs read (a device copy, as
-    a loader writing the next batch would)."""
+def _copy_pairs(dst, src, out):
     if isinstance(src, torch.Tensor):
-        dst.copy_(src, non_blocking=True)
+        out.append((dst, src))
     elif isinstance(src, dict):
         for k, v in src.items():
-            _copy_into(dst[k], v)
+            _copy_pairs(dst[k], v, out)
     elif isinstance(src, list):
         for d, v in zip(dst, src):
-            _copy_into(d, v)
+            _copy_pairs(d, v, out)
+
+
+def _copy_into(dst, src):
+    """Next resident batch -> the static input slot the captured graphs read (device copies, as
+    a loader writing the next batch would), all in one rs_copy_many launch."""
+    import ctypes as C
+    pairs = []
+    _copy_pairs(dst, src, pairs)
+    for k in range(0, len(pairs), 32):
+        part = pairs[k:k + 32]
+        for d, s in part:
+            assert d.is_contiguous() and s.is_contiguous() and d.nbytes == s.nbytes and d.dtype == s.dtype
+        n = len(part)
+        srcs = (C.c_void_p * n)(*[s.data_ptr() for _, s in part])
+        dsts = (C.c_void_p * n)(*[d.data_ptr() for d, _ in part])
+        nb = (C.c_int64 * n)(*[s.nbytes for _, s in part])
+        _hip.call('rs_copy_many', n, C.addressof(srcs), C.addressof(dsts), C.addressof(nb),
+                  torch.cuda.current_stream().cuda_stream)
 
 
 def _clone(b):
@@ -503,7 +525,7 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
     gather_roof = {}
     # the table gradient = the scatter of ordinary tables (rs_gather_bwd) + the sorted segment
     # sum of the large ones (rs_segsum); the sort itself runs in the forward (rs_lookup_sort)
-    groups = {'rs_gather_fwd': ('rs_gather_fwd',), 'table_grad': ('rs_gather_bwd', 'rs_segsum')}
+    groups = {'rs_gather_fwd': ('rs_gather_fwd', 'rs_gather_fwd_lazy'), 'table_grad': ('rs_gather_bwd', 'rs_segsum')}
     for k, members in groups.items():
         ms = [summ[m] for m in members if m in summ]
         g = {'ms': sum(x['ms'] for x in ms), 'bytes': sum(x['bytes'] for x in ms)}

@@ -123,10 +123,23 @@ typedef struct rs_feature_seg {
   const int* touch_count; /* kind 0/1, nullable: per-row lookup count of this optimizer step
                              (rs_sparse_touch); a row looked up once gets its gradient by a
                              plain store instead of an atomic add */
+  const int* lazy_last;   /* kind 0/1, nullable, rs_gather_fwd_lazy only: `last` of a lazy-Adam
+                             table (the optimizer step each row was last brought to); the rows are
+                             returned brought to the current step without being written */
 } rs_feature_seg_t;
 
 int rs_gather_fwd(const rs_feature_seg_t* segs, int nseg, int rows, float* out, int ldo,
                   int* err_flag, void* stream);
+/* The same gather with a read-through catch-up for the segments whose lazy_last is set (large
+ * lazy-Adam tables, sparse or sum / mean pooled, D % 4 == 0): each row is returned as
+ * rs_sorted_catchup would leave it -- the zero-gradient Adam steps last+1 .. *step replayed in
+ * registers from its exp_avg / exp_avg_sq, found m_off / v_off floats past the parameter element
+ * (one flat buffer per state) -- and nothing is written; rs_sorted_adam replays the same steps
+ * before its own. consts, beta1, beta2, eps, weight_decay: as rs_sorted_catchup. */
+int rs_gather_fwd_lazy(const rs_feature_seg_t* segs, int nseg, int rows, float* out, int ldo,
+                       int* err_flag, int64_t m_off, int64_t v_off, const int64_t* step,
+                       const float* consts, float beta1, float beta2, float eps, float weight_decay,
+                       void* stream);
 /* Backward: table grads by scatter-add (padding row skipped), dense grads via column
  * reductions (ws: rs_gather_ws_bytes), last-valid rows copied into a pre-zeroed src grad. */
 int64_t rs_gather_ws_bytes(const rs_feature_seg_t* segs_host, int nseg, int rows);
@@ -420,6 +433,9 @@ int rs_catalog_gather(const void* cat, int elem, int widen, int64_t V, int F, in
  * the longest selected list (the caller's batch maximum, as the reference pads to it). Row index
  * out of range: zeros, *err_flag |= 1; a list longer than Lb: truncated, *err_flag |= 2.
  * Fixed-width columns (sparse id matrix, dense matrix) use rs_catalog_gather with N = 1. */
+/* dst[i][0 .. bytes[i]) = src[i][...] for i < n <= 32 device buffers, one launch (host arrays read
+ * during the call only; the copies must not overlap). */
+int rs_copy_many(int n, const void* const* src, void* const* dst, const int64_t* bytes, void* stream);
 int rs_collate_ragged(const void* values, int elem, int tw, const int64_t* offsets, int64_t rows,
                       const int64_t* idx, int B, int Lb, int64_t* out, int* err_flag, void* stream);
 
@@ -515,6 +531,27 @@ int rs_lookup_catchup(const void* ids, int id_bytes, int rows, int bag, int64_t 
                       int64_t vocab, int D, float* p, float* m, float* v, int* last,
                       const int64_t* step, const float* consts, float beta1, float beta2, float eps,
                       float weight_decay, void* stream);
+/* Several sorted calls in one launch (at most 8, every D in one lanes-per-row class: D <= 16, 32,
+ * 64, 128, else). keys, n, D, call and owner as for the single-call entry points; p, m, v, last
+ * (Adam) and g are the call's table slices. rs_sorted_sqnorm_batch writes call c's
+ * rs_sorted_sqnorm_parts() partials at ws + c * parts. */
+typedef struct rs_sorted_call {
+  const uint32_t* keys;
+  int64_t n;
+  int D;
+  int call;
+  float* p;
+  float* g;
+  float* m;
+  float* v;
+  int* last;
+  int* owner;
+} rs_sorted_call_t;
+int rs_sorted_adam_batch(const rs_sorted_call_t* calls, int ncalls, const int64_t* step,
+                         const float* consts, float beta1, float beta2, float eps, float weight_decay,
+                         float scale, const float* coef, void* stream);
+int rs_sorted_sqnorm_batch(const rs_sorted_call_t* calls, int ncalls, float scale, double* ws,
+                           void* stream);
 int rs_sorted_adam(const uint32_t* keys, int64_t n, int D, float* p, float* g, float* m, float* v,
                    int* last, int* owner, int call, const int64_t* step, const float* consts,
                    float beta1, float beta2, float eps, float weight_decay, float scale,

@@ -28,7 +28,14 @@ class FeatureSeg(C.Structure):
     """Mirror of rs_feature_seg_t."""
     _fields_ = [('kind', i32), ('dim', i32), ('out_col', i32), ('pool_mode', i32), ('bag', i32),
                 ('pad_idx', i32), ('vocab', i64), ('idx_stride', i64), ('idx', vp), ('table', vp),
-                ('bias', vp), ('x', vp), ('grad', vp), ('grad_bias', vp), ('touch_count', vp)]
+                ('bias', vp), ('x', vp), ('grad', vp), ('grad_bias', vp), ('touch_count', vp),
+                ('lazy_last', vp)]
+
+
+class SortedCall(C.Structure):
+    """Mirror of rs_sorted_call_t."""
+    _fields_ = [('keys', vp), ('n', i64), ('D', i32), ('call', i32), ('p', vp), ('g', vp), ('m', vp), ('v', vp),
+                ('last', vp), ('owner', vp)]
 
 
 # name -> (restype, argtypes). Every symbol declared in include/rsys_hip.h.
@@ -59,6 +66,10 @@ SIGNATURES = {
     'rs_colsum_ws_bytes': (i64, [i32, i32]),
     'rs_colsum': (i32, [vp, i32, i32, i32, f32, f32, vp, vp, vp]),
     'rs_gather_fwd': (i32, [vp, i32, i32, vp, i32, vp, vp]),
+    'rs_sorted_adam_batch': (i32, [vp, i32, vp, vp, f32, f32, f32, f32, f32, vp, vp]),
+    'rs_sorted_sqnorm_batch': (i32, [vp, i32, f32, vp, vp]),
+    'rs_copy_many': (i32, [i32, vp, vp, vp, vp]),
+    'rs_gather_fwd_lazy': (i32, [vp, i32, i32, vp, i32, vp, i64, i64, vp, vp, f32, f32, f32, f32, vp]),
     'rs_gather_ws_bytes': (i64, [vp, i32, i32]),
     'rs_gather_bwd': (i32, [vp, i32, i32, vp, i32, vp, vp]),
     'rs_seq_mask': (i32, [vp, i64, i32, i32, i64, vp, vp, vp]),

@@ -29,6 +29,57 @@ __device__ __forceinline__ void adam_update(const AdamConst& h, float step_size,
   p = p - step_size * (m * __builtin_amdgcn_rcpf(denom));
 }
 
+// Steps from .. to (inclusive) with zero gradient of W <= 4 elements (a lazy table's catch-up),
+// bitwise equal to calling adam_update(h, consts[s].x, consts[s].y, 0.f, ...) per element and
+// step: with gs = 0 and wd == 0, (1 - b2) * gs * gs is +0 and v * b2 + (+0) == v * b2 exactly
+// (v >= 0), so that term is dropped; every other operation is the same IEEE operation in the same
+// order. The elements run interleaved (independent chains), two at a time as packed pairs
+// (v_pk_mul_f32 / v_pk_add_f32); an element whose moments are zero stays put exactly (m stays 0,
+// the update is p - step * (0 * rcp(eps)) = p). wd != 0 takes adam_update itself.
+template <int W>
+__device__ __forceinline__ void adam_replay_zero(const AdamConst& h, const float2* __restrict__ consts, int from,
+                                                 int to, float* p, float* m, float* v) {
+#pragma clang fp contract(off)
+  if (from > to) return;
+  if (h.wd != 0.f) {
+    for (int s = from; s <= to; ++s) {
+      const float2 c = consts[s];
+#pragma unroll
+      for (int j = 0; j < W; ++j) adam_update(h, c.x, c.y, 0.f, p[j], m[j], v[j]);
+    }
+    return;
+  }
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  constexpr int NP = (W + 1) / 2;
+  f2v pp[NP], mm[NP], vv[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    pp[q] = f2v{p[2 * q], 2 * q + 1 < W ? p[2 * q + 1] : 0.f};
+    mm[q] = f2v{m[2 * q], 2 * q + 1 < W ? m[2 * q + 1] : 0.f};
+    vv[q] = f2v{v[2 * q], 2 * q + 1 < W ? v[2 * q + 1] : 0.f};
+  }
+  const f2v omb1 = f2v{h.one_m_b1, h.one_m_b1}, b2 = f2v{h.b2, h.b2}, eps = f2v{h.eps, h.eps};
+  const f2v zero = f2v{0.f, 0.f};
+  for (int s = from; s <= to; ++s) {
+    const float2 c = consts[s];
+    const f2v ss = f2v{c.x, c.x}, ib = f2v{c.y, c.y};
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      mm[q] = mm[q] + omb1 * (zero - mm[q]);
+      vv[q] = vv[q] * b2;
+      f2v d = f2v{__builtin_amdgcn_sqrtf(vv[q][0]), __builtin_amdgcn_sqrtf(vv[q][1])};
+      d = d * ib + eps;
+      const f2v r = f2v{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+      pp[q] = pp[q] - ss * (mm[q] * r);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    p[2 * q] = pp[q][0]; m[2 * q] = mm[q][0]; v[2 * q] = vv[q][0];
+    if (2 * q + 1 < W) { p[2 * q + 1] = pp[q][1]; m[2 * q + 1] = mm[q][1]; v[2 * q + 1] = vv[q][1]; }
+  }
+}
+
 // per-step constants {lr / bc1(t), 1 / sqrt(bc2(t))}, computed in double then rounded once
 __host__ __device__ inline void adam_step_consts(double lr, double b1, double b2, double t,
                                                  float* step_size, float* inv_bc2_sqrt) {

@@ -11,6 +11,14 @@
 // Backward: dense [V, D] table gradients (the reference uses sparse=False embeddings, T16) by
 // float atomics, skipping the padding row as embedding_dense_backward does; Linear(1, D) dense
 // features by a deterministic column reduction; last-valid rows by a plain copy-add.
+//
+// Read-through catch-up (rs_gather_fwd_lazy): a large lazy-Adam table's segment (lazy_last set)
+// returns each row as rs_sorted_catchup would leave it -- the zero-gradient Adam steps the row
+// missed replayed in registers from its exp_avg / exp_avg_sq -- without writing the row, its
+// moments or `last`. The optimizer step replays the same steps before its own (lookup.hip
+// kAdam), so the stored state is the same bits; the forward's separate catch-up pass (read p, m,
+// v and write them back: 6 row transfers per distinct row) becomes 2 extra row reads per lookup.
+#include "adam.h"
 #include "common.h"
 
 namespace rs {
@@ -24,10 +32,20 @@ constexpr int64_t kSmallTableBytes = 48 * 1024;
 
 constexpr int kRowsPerLane = 4;            // forward sparse rows per lane on token-sized launches
 constexpr int kBagBatch = 16;              // bag ids (and rows) loaded per batch
+constexpr int kLazyBagBatch = 8;           // the same with exp_avg / exp_avg_sq rows beside them
 // forward: a table of at most this size whose workgroup reads at least as many row bytes as the
 // table holds is staged whole into LDS first (every row of such a table is hot: the genre / age /
 // occupation tables are read thousands of times per step), and its lookups are served from LDS
 constexpr int kStageBytes = 16 * 1024;
+
+// read-through catch-up of lazy-Adam segments: the moments sit at fixed element offsets from the
+// parameters (one flat buffer each), the step counter and per-step constants are the optimizer's
+struct LazyLaunch {
+  int64_t moff, voff;     // floats from a table element to its exp_avg / exp_avg_sq element
+  const int64_t* step;    // optimizer steps taken: rows are returned as of this step
+  const float2* consts;   // {lr / bc1(s), 1 / sqrt(bc2(s))}; consts[0] = {capacity, overflow}
+  AdamConst h;
+};
 
 struct SegLaunch {
   rs_feature_seg_t segs[kMaxSeg];
@@ -64,6 +82,7 @@ struct SegLaunch {
   int64_t ws_floats;
   int range_lds;
   float* ws;
+  LazyLaunch lz;  // rs_gather_fwd_lazy only
 };
 static_assert(sizeof(SegLaunch) <= 4096, "SegLaunch must fit the kernel-argument segment");
 
@@ -97,37 +116,78 @@ __device__ __forceinline__ void store_row(float* p, const float* v) {
   else p[0] = v[0];
 }
 
+// The optimizer step a lazy row is returned at (sparse.hip clamp_step: past the constants'
+// capacity the last slot is reused and the optimizer raises its overflow flag).
+__device__ __forceinline__ int lazy_target(const LazyLaunch& z) {
+  const int cap = __float_as_int(z.consts[0].x);
+  const int64_t t = *z.step;
+  return t < cap ? (int)t : cap - 1;
+}
+
+// Row values p (4 columns) with the row's moments mv / vv and `last`: replay the zero-gradient
+// steps last + 1 .. t as rs_sorted_catchup does (nothing to replay, or a row never stepped with
+// weight_decay == 0 -- its moments are zero and the replay is the identity; per element, zero
+// moments likewise).
+template <int W = 4>
+__device__ __forceinline__ void lazy_replay(const LazyLaunch& z, int last, int t, float* p, const float* mv,
+                                            const float* vv) {
+  if (last + 1 > t || (last == 0 && z.h.wd == 0.f)) return;
+  float m[W], v[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    m[j] = mv[j];
+    v[j] = vv[j];
+  }
+  adam_replay_zero<W>(z.h, z.consts, last + 1, t, p, m, v);
+}
+
 // Pooled bag: the (un-normalised) sum or max of positions [lbeg, lend) of row `row`'s bag.
-template <bool VEC>
+// LAZY: the rows read through the catch-up.
+template <bool VEC, bool LAZY = false>
 __device__ __forceinline__ void pool_acc(const SegLaunch& a, const rs_feature_seg_t& sg, int row,
                                          int c, int lbeg, int lend, float* acc) {
   constexpr int W = VEC ? 4 : 1;
+  constexpr int NB = LAZY ? kLazyBagBatch : kBagBatch;
   const int64_t* ids = sg.idx + (int64_t)row * sg.idx_stride;
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = sg.pool_mode == RS_POOL_MAX ? -INFINITY : 0.f;
   // Straight-line code only (no per-row branch or error atomic inside the batch): a branch
   // around each load makes the compiler wait for it before issuing the next.
   const bool is_max = sg.pool_mode == RS_POOL_MAX;
+  const int t = LAZY ? lazy_target(a.lz) : 0;
   bool bad = false;
-  int64_t raw[kBagBatch];
+  int64_t raw[NB];
 #pragma unroll
-  for (int u = 0; u < kBagBatch; ++u) raw[u] = lbeg + u < lend ? ids[lbeg + u] : 0;
-  for (int l0 = lbeg; l0 < lend; l0 += kBagBatch) {
-    const int nb = lend - l0 < kBagBatch ? lend - l0 : kBagBatch;
-    bool ok[kBagBatch];
-    float v[kBagBatch][4];
+  for (int u = 0; u < NB; ++u) raw[u] = lbeg + u < lend ? ids[lbeg + u] : 0;
+  for (int l0 = lbeg; l0 < lend; l0 += NB) {
+    const int nb = lend - l0 < NB ? lend - l0 : NB;
+    bool ok[NB];
+    float v[NB][4];
+    float mv[LAZY ? NB : 1][4], vv[LAZY ? NB : 1][4];
+    int lst[LAZY ? NB : 1];
 #pragma unroll
-    for (int u = 0; u < kBagBatch; ++u) {
+    for (int u = 0; u < NB; ++u) {
       const bool valid = raw[u] >= 0 && raw[u] < sg.vocab;
       bad |= u < nb && !valid;
       ok[u] = u < nb && valid;
-      load_row<VEC>(sg.table + (ok[u] ? raw[u] : 0) * sg.dim + c, v[u]);
+      const int64_t r = ok[u] ? raw[u] : 0;
+      load_row<VEC>(sg.table + r * sg.dim + c, v[u]);
+      if constexpr (LAZY) {
+        lst[u] = sg.lazy_last[r];
+        load_row<VEC>(sg.table + r * sg.dim + c + a.lz.moff, mv[u]);
+        load_row<VEC>(sg.table + r * sg.dim + c + a.lz.voff, vv[u]);
+      }
     }
-    const int n2 = l0 + kBagBatch;
+    const int n2 = l0 + NB;
 #pragma unroll
-    for (int u = 0; u < kBagBatch; ++u) raw[u] = n2 + u < lend ? ids[n2 + u] : 0;
+    for (int u = 0; u < NB; ++u) raw[u] = n2 + u < lend ? ids[n2 + u] : 0;
+    if constexpr (LAZY) {
 #pragma unroll
-    for (int u = 0; u < kBagBatch; ++u) {
+      for (int u = 0; u < NB; ++u)
+        if (ok[u]) lazy_replay<W>(a.lz, lst[u], t, v[u], mv[u], vv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
 #pragma unroll
       for (int j = 0; j < W; ++j) {
         const float x = ok[u] ? v[u][j] : 0.f;
@@ -139,7 +199,7 @@ __device__ __forceinline__ void pool_acc(const SegLaunch& a, const rs_feature_se
   if (bad && a.err) atomicOr(a.err, 1);
 }
 
-template <bool VEC>
+template <bool VEC, bool LAZY = false>
 __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int row, int chunk) {
   constexpr int W = VEC ? 4 : 1;
   const int c = chunk * W;
@@ -147,9 +207,19 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
   float* o = a.out + (int64_t)row * a.ldo + sg.out_col + c;
   if (sg.kind == RS_SEG_SPARSE) {
     const int64_t id = sg.idx[(int64_t)row * sg.idx_stride];
-    if (id_ok(id, sg.vocab, a.err)) load_row<VEC>(sg.table + id * sg.dim + c, acc);
+    if (id_ok(id, sg.vocab, a.err)) {
+      const float* pr = sg.table + id * sg.dim + c;
+      load_row<VEC>(pr, acc);
+      if constexpr (LAZY) {
+        float mv[4], vv[4];
+        const int l = sg.lazy_last[id];
+        load_row<VEC>(pr + a.lz.moff, mv);
+        load_row<VEC>(pr + a.lz.voff, vv);
+        lazy_replay<W>(a.lz, l, lazy_target(a.lz), acc, mv, vv);
+      }
+    }
   } else if (sg.kind == RS_SEG_POOL) {
-    pool_acc<VEC>(a, sg, row, c, 0, sg.bag, acc);
+    pool_acc<VEC, LAZY>(a, sg, row, c, 0, sg.bag, acc);
     if (sg.pool_mode == RS_POOL_MEAN) {
       const float n = (float)sg.bag;
 #pragma unroll
@@ -176,7 +246,7 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
 // workgroups of one float4 per lane, each a serial id -> row -> store chain). The workgroup owns
 // rows [lb R rpb, (lb + 1) R rpb); all R ids are loaded, then all R rows, then the R stores, so a
 // lane has R independent chains in flight. Same values as gather_seg (bad ids: zeros + err flag).
-template <int R>
+template <int R, bool LAZY = false>
 __device__ void gather_sparse_rows(const SegLaunch& a, const rs_feature_seg_t& sg, int rpb, int lb,
                                    int r, int chunk) {
   const int c = chunk * 4;
@@ -187,15 +257,34 @@ __device__ void gather_sparse_rows(const SegLaunch& a, const rs_feature_seg_t& s
     id[k] = row < a.rows ? sg.idx[(int64_t)row * sg.idx_stride] : 0;
   }
   float v[R][4];
+  float mv[LAZY ? R : 1][4], vv[LAZY ? R : 1][4];
+  int lst[LAZY ? R : 1];
+  bool okk[R];
   bool bad = false;
 #pragma unroll
   for (int k = 0; k < R; ++k) {
     const int row = (lb * R + k) * rpb + r;
     const bool ok = id[k] >= 0 && id[k] < sg.vocab;
+    okk[k] = ok;
     bad |= row < a.rows && !ok;
-    load_row<true>(sg.table + (ok ? id[k] : 0) * sg.dim + c, v[k]);
+    const float* pr = sg.table + (ok ? id[k] : 0) * sg.dim + c;
+    load_row<true>(pr, v[k]);
+    if constexpr (LAZY) {
+      lst[k] = sg.lazy_last[ok ? id[k] : 0];
+      load_row<true>(pr + a.lz.moff, mv[k]);
+      load_row<true>(pr + a.lz.voff, vv[k]);
+    }
+  }
+  if constexpr (LAZY) {
+    const int t = lazy_target(a.lz);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[k][j] = ok ? v[k][j] : 0.f;
+    for (int k = 0; k < R; ++k)
+      if (okk[k]) lazy_replay(a.lz, lst[k], t, v[k], mv[k], vv[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[k][j] = okk[k] ? v[k][j] : 0.f;
   }
 #pragma unroll
   for (int k = 0; k < R; ++k) {
@@ -208,7 +297,7 @@ __device__ void gather_sparse_rows(const SegLaunch& a, const rs_feature_seg_t& s
 // Pooled bag split over S row groups (small batches: more loads in flight per bag). Row group
 // g = r * S + p sums positions [p * per, (p + 1) * per) of bag r; the S partial sums are added
 // in p order through LDS by group p = 0.
-template <bool VEC>
+template <bool VEC, bool LAZY = false>
 __device__ void gather_pool_split(const SegLaunch& a, const rs_feature_seg_t& sg, int s, int lb) {
   constexpr int W = VEC ? 4 : 1;
   __shared__ float4 red[256];
@@ -221,7 +310,7 @@ __device__ void gather_pool_split(const SegLaunch& a, const rs_feature_seg_t& sg
   const int lbeg = p * per < sg.bag ? p * per : sg.bag;
   const int lend = lbeg + per < sg.bag ? lbeg + per : sg.bag;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if (active) pool_acc<VEC>(a, sg, row, chunk * W, lbeg, lend, acc);
+  if (active) pool_acc<VEC, LAZY>(a, sg, row, chunk * W, lbeg, lend, acc);
   red[threadIdx.x] = make_float4(acc[0], acc[1], acc[2], acc[3]);
   __syncthreads();
   if (!active || p != 0) return;
@@ -238,11 +327,33 @@ __device__ void gather_pool_split(const SegLaunch& a, const rs_feature_seg_t& sg
   store_row<VEC>(o, acc);
 }
 
+// LAZY launches (rs_gather_fwd_lazy): segments with lazy_last read through the catch-up (float4
+// rows, never staged: the plan checks); the others as in a plain launch
+template <bool LAZY>
 __global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
   extern __shared__ float4 stage_lds[];
   const int s = find_seg(a, blockIdx.x);
   rs_feature_seg_t sg = a.segs[s];
   const int lb = blockIdx.x - a.block_start[s];
+  if (LAZY && sg.lazy_last) {  // uniform per workgroup
+    if (a.split[s] > 1) {
+      if (a.vec[s]) gather_pool_split<true, true>(a, sg, s, lb);
+      else gather_pool_split<false, true>(a, sg, s, lb);
+      return;
+    }
+    const int C = a.chunks[s];
+    const int r = threadIdx.x / C, chunk = threadIdx.x % C;
+    if (r >= a.rpb[s]) return;
+    if (a.rpt[s] == kRowsPerLane) {
+      gather_sparse_rows<kRowsPerLane, true>(a, sg, a.rpb[s], lb, r, chunk);
+      return;
+    }
+    const int row = lb * a.rpb[s] + r;
+    if (row >= a.rows) return;
+    if (a.vec[s]) gather_seg<true, true>(a, sg, row, chunk);
+    else gather_seg<false, true>(a, sg, row, chunk);
+    return;
+  }
   if (a.stage[s]) {  // uniform per workgroup: the whole table into LDS, then read it from there
     const float4* src = reinterpret_cast<const float4*>(sg.table);
     for (int i = threadIdx.x; i < a.stage[s] / 16; i += 256) stage_lds[i] = src[i];
@@ -788,7 +899,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     if (!bwd && table_kind && vec) {
       const int64_t tbytes = g.vocab * g.dim * 4;
       const int64_t read = (int64_t)a.rpb[s] * (g.kind == RS_SEG_POOL ? g.bag : 1) * g.dim * 4;
-      if (tbytes <= kStageBytes && tbytes <= read && !getenv_flag("RSYS_NO_LDS_STAGE")) {
+      if (tbytes <= kStageBytes && tbytes <= read && !g.lazy_last && !getenv_flag("RSYS_NO_LDS_STAGE")) {
         a.stage[s] = (int)tbytes;
         if (a.stage[s] > a.stage_lds) a.stage_lds = a.stage[s];
       }
@@ -898,8 +1009,34 @@ extern "C" int rs_gather_fwd(const rs_feature_seg_t* segs, int nseg, int rows, f
   RS_RET_IF(plan(a, segs_host, nseg, rows, ldo, out));
   for (int i = 0; i < nseg; ++i) a.segs[i] = segs[i];
   a.out = out; a.dout = nullptr; a.err = err_flag;
-  gather_fwd_kernel<<<a.block_start[nseg], 256, a.stage_lds, as_stream(stream)>>>(a);
+  gather_fwd_kernel<false><<<a.block_start[nseg], 256, a.stage_lds, as_stream(stream)>>>(a);
   RS_CHECK_LAUNCH("rs_gather_fwd");
+  return 0;
+}
+
+extern "C" int rs_gather_fwd_lazy(const rs_feature_seg_t* segs, int nseg, int rows, float* out, int ldo,
+                                  int* err_flag, int64_t m_off, int64_t v_off, const int64_t* step,
+                                  const float* consts, float beta1, float beta2, float eps, float weight_decay,
+                                  void* stream) {
+  RS_CHECK_ARG(segs && out && step && consts, "rs_gather_fwd_lazy: null pointer");
+  if (rows == 0) return 0;
+  SegLaunch a;
+  RS_RET_IF(plan(a, segs, nseg, rows, ldo, out));
+  for (int i = 0; i < nseg; ++i) {
+    const rs_feature_seg_t& g = segs[i];
+    if (!g.lazy_last) continue;
+    RS_CHECK_ARG(g.kind == RS_SEG_SPARSE || (g.kind == RS_SEG_POOL && g.pool_mode != RS_POOL_MAX),
+                 "rs_gather_fwd_lazy: seg %d: read-through needs a sparse or sum / mean pooled lookup", i);
+    RS_CHECK_ARG(!a.stage[i], "rs_gather_fwd_lazy: seg %d: a read-through table cannot be staged", i);
+  }
+  for (int i = 0; i < nseg; ++i) a.segs[i] = segs[i];
+  a.out = out; a.dout = nullptr; a.err = err_flag;
+  a.lz.moff = m_off; a.lz.voff = v_off; a.lz.step = step;
+  a.lz.consts = reinterpret_cast<const float2*>(consts);
+  a.lz.h.one_m_b1 = 1.f - beta1; a.lz.h.b2 = beta2; a.lz.h.one_m_b2 = 1.f - beta2;
+  a.lz.h.eps = eps; a.lz.h.wd = weight_decay;
+  gather_fwd_kernel<true><<<a.block_start[nseg], 256, a.stage_lds, as_stream(stream)>>>(a);
+  RS_CHECK_LAUNCH("rs_gather_fwd_lazy");
   return 0;
 }
 

@@ -32,10 +32,14 @@
 namespace rs {
 namespace {
 
-constexpr int kSortThreads = 1024;
-constexpr int kSortWaves = kSortThreads / 64;
+// multi-tile radix sort: 1,024-lookup tiles of 256 threads (a 204,800-lookup call is 200 tiles:
+// 4,096-lookup tiles of 1,024 threads gave 50 workgroups and a 16-wave prefix per ranking round)
+constexpr int kSortThreads = 256;
 constexpr int kSortRounds = 4;
-constexpr int kSortTile = kSortThreads * kSortRounds;  // 4096 lookups per tile
+constexpr int kSortTile = kSortThreads * kSortRounds;  // 1,024 lookups per tile
+// one-workgroup sort of calls of at most kTileMax lookups (4 keys per thread)
+constexpr int kTileThreads = 1024;
+constexpr int kTileMax = 4096;
 constexpr int kMaxDigitBits = 9;
 constexpr int kMaxRadix = 1 << kMaxDigitBits;
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;
@@ -75,16 +79,19 @@ __device__ __forceinline__ uint32_t raw_key(const void* ids, int id_bytes, int b
   return id >= 0 && id < vocab ? (uint32_t)id : kSentinel;
 }
 
+template <int NT>
 struct RankLds {
-  uint16_t wc[kSortWaves][kMaxRadix];   // per-wave digit counts of the current round (leaders)
-  uint16_t pre[kSortWaves][kMaxRadix];  // tile-local start of each wave's group of a digit
-  int run[kMaxRadix];                   // tile-local count of each digit before this round
+  static constexpr int NW = NT / 64;
+  uint16_t wc[NW][kMaxRadix];   // per-wave digit counts of the current round (leaders)
+  uint16_t pre[NW][kMaxRadix];  // tile-local start of each wave's group of a digit
+  int run[kMaxRadix];           // tile-local count of each digit before this round
 };
 
 // Stable rank of this lane's digit within the tile, for one round of kSortThreads keys (key
 // order = round, wave, lane). Returns the tile-local position among keys of the same digit
 // (counting earlier rounds through lds.run). Two barriers.
-__device__ __forceinline__ int rank_round(RankLds& lds, uint32_t d, bool valid, int dbits,
+template <int NT>
+__device__ __forceinline__ int rank_round(RankLds<NT>& lds, uint32_t d, bool valid, int dbits,
                                           int radix) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint64_t peers = __ballot(valid);
@@ -98,10 +105,10 @@ __device__ __forceinline__ int rank_round(RankLds& lds, uint32_t d, bool valid, 
   const int lrank = __popcll(peers & lt);
   if (valid && lrank == 0) lds.wc[w][d] = (uint16_t)__popcll(peers);
   __syncthreads();
-  for (int t = threadIdx.x; t < radix; t += kSortThreads) {
+  for (int t = threadIdx.x; t < radix; t += NT) {
     int r = lds.run[t];
 #pragma unroll
-    for (int ww = 0; ww < kSortWaves; ++ww) {
+    for (int ww = 0; ww < RankLds<NT>::NW; ++ww) {
       const int c = lds.wc[ww][t];
       lds.wc[ww][t] = 0;
       lds.pre[ww][t] = (uint16_t)r;
@@ -113,9 +120,10 @@ __device__ __forceinline__ int rank_round(RankLds& lds, uint32_t d, bool valid, 
   return valid ? (int)lds.pre[w][d] + lrank : 0;
 }
 
-__device__ __forceinline__ void rank_reset(RankLds& lds, int radix) {
-  for (int t = threadIdx.x; t < radix; t += kSortThreads) lds.run[t] = 0;
-  for (int i = threadIdx.x; i < kSortWaves * kMaxRadix; i += kSortThreads)
+template <int NT>
+__device__ __forceinline__ void rank_reset(RankLds<NT>& lds, int radix) {
+  for (int t = threadIdx.x; t < radix; t += NT) lds.run[t] = 0;
+  for (int i = threadIdx.x; i < RankLds<NT>::NW * kMaxRadix; i += NT)
     (&lds.wc[0][0])[i] = 0;
 }
 
@@ -174,7 +182,7 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter_kernel(
     const uint32_t* __restrict__ ksrc, const uint32_t* __restrict__ vsrc, int64_t n, int shift,
     int dbits, const int* __restrict__ hist, const int* __restrict__ tot,
     uint32_t* __restrict__ kdst, uint32_t* __restrict__ vdst) {
-  __shared__ RankLds lds;
+  __shared__ RankLds<kSortThreads> lds;
   __shared__ int gbase[kMaxRadix];
   const int radix = 1 << dbits;
   rank_reset(lds, radix);
@@ -222,27 +230,31 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter_kernel(
 }
 
 // ---------------------------------------------------------------- one-tile sort (n <= 4096)
-__global__ __launch_bounds__(kSortThreads) void sort_tile_kernel(
+// One workgroup, the keys in registers (4 per thread) and exchanged through LDS between the
+// radix passes. (Measured and rejected: a bitonic sort of key/index pairs -- 39 us with an LDS
+// barrier per step, 47 us with the short distances in registers and shuffles: 78 steps of 4,096
+// compare-exchanges on one CU are VALU-bound; this sort takes ~23 us.)
+__global__ __launch_bounds__(kTileThreads) void sort_tile_kernel(
     const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab, int n,
     SortPlan plan, uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
-  __shared__ RankLds lds;
+  __shared__ RankLds<kTileThreads> lds;
   __shared__ int tbase[kMaxRadix];
-  __shared__ uint32_t xchg[kSortTile];
+  __shared__ uint32_t xchg[kTileMax];
   uint32_t key[kSortRounds], val[kSortRounds];
 #pragma unroll
   for (int r = 0; r < kSortRounds; ++r) {
-    const int e = r * kSortThreads + threadIdx.x;
+    const int e = r * kTileThreads + threadIdx.x;
     key[r] = e < n ? raw_key(ids, id_bytes, bag, stride, vocab, e) : kSentinel;
     val[r] = (uint32_t)e;
   }
   for (int p = 0; p < plan.passes; ++p) {
     const int radix = 1 << plan.dbits[p], shift = plan.shift[p];
     rank_reset(lds, radix);
-    for (int t = threadIdx.x; t < radix; t += kSortThreads) tbase[t] = 0;
+    for (int t = threadIdx.x; t < radix; t += kTileThreads) tbase[t] = 0;
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSortRounds; ++r)
-      if (r * kSortThreads + (int)threadIdx.x < n) atomicAdd(&tbase[(key[r] >> shift) & (radix - 1)], 1);
+      if (r * kTileThreads + (int)threadIdx.x < n) atomicAdd(&tbase[(key[r] >> shift) & (radix - 1)], 1);
     __syncthreads();
     if (threadIdx.x < 64) {  // exclusive scan of the digit counts
       int carry = 0;
@@ -262,7 +274,7 @@ __global__ __launch_bounds__(kSortThreads) void sort_tile_kernel(
     int pos[kSortRounds];
 #pragma unroll
     for (int r = 0; r < kSortRounds; ++r) {
-      const bool valid = r * kSortThreads + (int)threadIdx.x < n;
+      const bool valid = r * kTileThreads + (int)threadIdx.x < n;
       const uint32_t d = (key[r] >> shift) & (radix - 1);
       const int lp = rank_round(lds, d, valid, plan.dbits[p], radix);
       pos[r] = valid ? tbase[d] + lp : -1;
@@ -273,7 +285,7 @@ __global__ __launch_bounds__(kSortThreads) void sort_tile_kernel(
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSortRounds; ++r) {
-      const int e = r * kSortThreads + threadIdx.x;
+      const int e = r * kTileThreads + threadIdx.x;
       if (e < n) key[r] = xchg[e];
     }
     __syncthreads();
@@ -282,14 +294,14 @@ __global__ __launch_bounds__(kSortThreads) void sort_tile_kernel(
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSortRounds; ++r) {
-      const int e = r * kSortThreads + threadIdx.x;
+      const int e = r * kTileThreads + threadIdx.x;
       if (e < n) val[r] = xchg[e];
     }
     __syncthreads();
   }
 #pragma unroll
   for (int r = 0; r < kSortRounds; ++r) {
-    const int e = r * kSortThreads + threadIdx.x;
+    const int e = r * kTileThreads + threadIdx.x;
     if (e < n) {
       kout[e] = key[r];
       vout[e] = val[r];
@@ -341,8 +353,10 @@ struct RowArgs {
 // resident waves: tools/lazy_bench.py), so U = 1.
 constexpr int kRowUnroll = 1;
 
+// bid / nblocks: this workgroup's index and count among the workgroups working on `a` (a batched
+// launch deals one contiguous block range to each call)
 template <int OP, int G, int U>
-__global__ __launch_bounds__(256) void sorted_rows_kernel(RowArgs a) {
+__device__ __forceinline__ void sorted_rows_body(const RowArgs& a, int bid, int nblocks) {
   __shared__ double red[4];
   const int gl = threadIdx.x & (G - 1);
   double acc = 0.0;
@@ -354,11 +368,11 @@ __global__ __launch_bounds__(256) void sorted_rows_kernel(RowArgs a) {
     ct = a.consts[t];
     s = a.scale * (a.coef ? *a.coef : 1.f);
   }
-  const int64_t ngroups = (int64_t)gridDim.x * (256 / G);
+  const int64_t ngroups = (int64_t)nblocks * (256 / G);
   const int c0 = gl * 4;
   const int w = c0 < a.D ? (a.D - c0 < 4 ? a.D - c0 : 4) : 0;  // columns of this lane
   const bool vec = (a.D & 3) == 0;
-  for (int64_t i0 = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G; i0 < a.n; i0 += ngroups * U) {
+  for (int64_t i0 = (int64_t)bid * (256 / G) + threadIdx.x / G; i0 < a.n; i0 += ngroups * U) {
     int64_t row[U];
     bool act[U];
 #pragma unroll
@@ -422,16 +436,24 @@ __global__ __launch_bounds__(256) void sorted_rows_kernel(RowArgs a) {
       if (w > 0) {
         const int64_t o = row[u] * a.D + c0;
         if (OP == kCatchup) {
+          if (w == 4) {
+            adam_replay_zero<4>(a.h, a.consts, from[u], t, pp[u], mm[u], vv[u]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (j < w) replay(a.h, a.consts, from[u], t, pp[u][j], mm[u][j], vv[u][j]);
+          }
+        } else if (OP == kAdam) {
+          if (w == 4) {
+            adam_replay_zero<4>(a.h, a.consts, from[u], t - 1, pp[u], mm[u], vv[u]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (j < w && from[u] <= t - 1) replay(a.h, a.consts, from[u], t - 1, pp[u][j], mm[u][j], vv[u][j]);
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (j < w) replay(a.h, a.consts, from[u], t, pp[u][j], mm[u][j], vv[u][j]);
-        } else if (OP == kAdam) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (j >= w) continue;
-            if (from[u] <= t - 1) replay(a.h, a.consts, from[u], t - 1, pp[u][j], mm[u][j], vv[u][j]);
-            adam_update(a.h, ct.x, ct.y, gg[u][j] * s, pp[u][j], mm[u][j], vv[u][j]);
-          }
+            if (j < w) adam_update(a.h, ct.x, ct.y, gg[u][j] * s, pp[u][j], mm[u][j], vv[u][j]);
         } else if (OP == kSqnorm) {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
@@ -464,8 +486,29 @@ __global__ __launch_bounds__(256) void sorted_rows_kernel(RowArgs a) {
     acc = wave_sum(acc);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) a.ws[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    if (threadIdx.x == 0) a.ws[bid] = red[0] + red[1] + red[2] + red[3];
   }
+}
+
+template <int OP, int G, int U>
+__global__ __launch_bounds__(256) void sorted_rows_kernel(RowArgs a) {
+  sorted_rows_body<OP, G, U>(a, blockIdx.x, gridDim.x);
+}
+
+// several calls in one launch (the optimizer's per-call Adam steps / clip partials: one dispatch
+// instead of one per call); call c owns workgroups [first[c], first[c + 1])
+constexpr int kRowBatchMax = 8;
+struct RowBatch {
+  RowArgs a[kRowBatchMax];
+  int first[kRowBatchMax + 1];
+  int n;
+};
+
+template <int OP, int G, int U>
+__global__ __launch_bounds__(256) void sorted_rows_batch_kernel(RowBatch b) {
+  int c = 0;
+  while (c + 1 < b.n && (int)blockIdx.x >= b.first[c + 1]) ++c;
+  sorted_rows_body<OP, G, U>(b.a[c], blockIdx.x - b.first[c], b.first[c + 1] - b.first[c]);
 }
 
 constexpr int kRowGrid = 2048;
@@ -526,9 +569,13 @@ __global__ __launch_bounds__(256) void lookup_catchup_kernel(IdCatchArgs a) {
     } else {
       for (int j = 0; j < w; ++j) { pp[j] = a.p[o + j]; mm[j] = a.m[o + j]; vv[j] = a.v[o + j]; }
     }
+    if (w == 4) {
+      adam_replay_zero<4>(a.h, a.consts, l + 1, t, pp, mm, vv);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (j < w) replay(a.h, a.consts, l + 1, t, pp[j], mm[j], vv[j]);
+      for (int j = 0; j < 4; ++j)
+        if (j < w) replay(a.h, a.consts, l + 1, t, pp[j], mm[j], vv[j]);
+    }
     if (vec) {
       *reinterpret_cast<float4*>(a.p + o) = make_float4(pp[0], pp[1], pp[2], pp[3]);
       *reinterpret_cast<float4*>(a.m + o) = make_float4(mm[0], mm[1], mm[2], mm[3]);
@@ -873,7 +920,7 @@ AdamConst make_hyper(float b1, float b2, float eps, float wd) {
 }
 
 int64_t sort_ws_bytes(int64_t n, int64_t vocab) {
-  if (n <= kSortTile) return 0;
+  if (n <= kTileMax) return 0;
   const SortPlan p = make_plan(n, vocab);
   return 2 * n * 4 + ((int64_t)kMaxRadix * p.ntiles + kMaxRadix) * 4 + 256;
 }
@@ -895,9 +942,8 @@ extern "C" int rs_lookup_sort(const void* ids, int id_bytes, int rows, int bag, 
   if (n == 0) return 0;
   hipStream_t st = as_stream(stream);
   const SortPlan p = make_plan(n, vocab);
-  if (n <= kSortTile) {
-    sort_tile_kernel<<<1, kSortThreads, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, (int)n, p,
-                                                keys, vals);
+  if (n <= kTileMax) {
+    sort_tile_kernel<<<1, kTileThreads, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, (int)n, p, keys, vals);
     RS_CHECK_LAUNCH("rs_lookup_sort tile");
     return 0;
   }
@@ -1009,6 +1055,64 @@ extern "C" int rs_sorted_adam(const uint32_t* keys, int64_t n, int D, float* p, 
                "rs_sorted_adam: bad args");
   return sorted_rows(kAdam, keys, n, D, p, g, m, v, last, owner, call, step, consts, beta1, beta2,
                      eps, weight_decay, scale, coef, nullptr, as_stream(stream));
+}
+
+static int lanes_per_row(int D) { return D <= 16 ? 4 : D <= 32 ? 8 : D <= 64 ? 16 : D <= 128 ? 32 : 64; }
+
+static int sorted_rows_batch(int op, const rs_sorted_call_t* calls, int ncalls, const int64_t* step,
+                             const float* consts, float b1, float b2, float eps, float wd, float scale,
+                             const float* coef, double* ws, hipStream_t st) {
+  RS_CHECK_ARG(calls && ncalls >= 1 && ncalls <= kRowBatchMax, "rs_sorted_*_batch: 1 .. %d calls (got %d)",
+               kRowBatchMax, ncalls);
+  RowBatch b{};
+  b.n = ncalls;
+  const int G = lanes_per_row(calls[0].D);
+  int wg = 0;
+  for (int c = 0; c < ncalls; ++c) {
+    const rs_sorted_call_t& k = calls[c];
+    RS_CHECK_ARG(k.keys && k.g && k.D >= 1 && k.n >= 0 && lanes_per_row(k.D) == G,
+                 "rs_sorted_*_batch: call %d: bad args or another row width class than call 0", c);
+    RS_CHECK_ARG(op != kAdam || (k.p && k.m && k.v && k.last), "rs_sorted_adam_batch: call %d: null state", c);
+    RowArgs& a = b.a[c];
+    a.keys = k.keys; a.n = k.n; a.D = k.D; a.p = k.p; a.g = k.g; a.m = k.m; a.v = k.v; a.last = k.last;
+    a.owner = k.owner; a.call = k.call; a.step = step;
+    a.consts = reinterpret_cast<const float2*>(consts); a.h = make_hyper(b1, b2, eps, wd);
+    a.scale = scale; a.coef = coef; a.ws = ws ? ws + (int64_t)c * kRowGrid : nullptr;
+    b.first[c] = wg;
+    wg += op == kSqnorm ? kRowGrid : (int)std::max<int64_t>(1, std::min<int64_t>(kRowGrid * 4, cdiv(k.n, 256 / G)));
+  }
+  b.first[ncalls] = wg;
+#define RS_BATCH(OPV)                                                                        \
+  switch (G) {                                                                               \
+    case 4: sorted_rows_batch_kernel<OPV, 4, 1><<<wg, 256, 0, st>>>(b); break;               \
+    case 8: sorted_rows_batch_kernel<OPV, 8, 1><<<wg, 256, 0, st>>>(b); break;               \
+    case 16: sorted_rows_batch_kernel<OPV, 16, 1><<<wg, 256, 0, st>>>(b); break;             \
+    case 32: sorted_rows_batch_kernel<OPV, 32, 1><<<wg, 256, 0, st>>>(b); break;             \
+    default: sorted_rows_batch_kernel<OPV, 64, 1><<<wg, 256, 0, st>>>(b); break;             \
+  }
+  if (op == kAdam) {
+    RS_BATCH(kAdam)
+  } else {
+    RS_BATCH(kSqnorm)
+  }
+#undef RS_BATCH
+  RS_CHECK_LAUNCH("rs_sorted_rows_batch");
+  return 0;
+}
+
+extern "C" int rs_sorted_adam_batch(const rs_sorted_call_t* calls, int ncalls, const int64_t* step,
+                                    const float* consts, float beta1, float beta2, float eps, float weight_decay,
+                                    float scale, const float* coef, void* stream) {
+  RS_CHECK_ARG(step && consts, "rs_sorted_adam_batch: null pointer");
+  return sorted_rows_batch(kAdam, calls, ncalls, step, consts, beta1, beta2, eps, weight_decay, scale, coef,
+                           nullptr, as_stream(stream));
+}
+
+extern "C" int rs_sorted_sqnorm_batch(const rs_sorted_call_t* calls, int ncalls, float scale, double* ws,
+                                      void* stream) {
+  RS_CHECK_ARG(ws, "rs_sorted_sqnorm_batch: null ws");
+  return sorted_rows_batch(kSqnorm, calls, ncalls, nullptr, nullptr, 0.f, 0.f, 0.f, 0.f, scale, nullptr, ws,
+                           as_stream(stream));
 }
 
 extern "C" int rs_sorted_sqnorm_parts(void) { return kRowGrid; }

@@ -6,7 +6,7 @@
 // every table every step: a row whose exp_avg is non-zero keeps drifting after it was last
 // looked up. At 10M-100M rows that is a 75-360 GB sweep per step. Here a large table keeps
 // per-row `last` (the optimizer step the row was last brought to); a row is brought current
-// (the skipped zero-gradient steps replayed) before it is read, and rs_sparse_flush brings every
+// (the skipped zero-gradient steps replayed, adam.h adam_replay_zero) before it is read, and rs_sparse_flush brings every
 // row to step t (before state_dict / checkpoint). The replay runs the same fp32 operation
 // sequence as the dense kernel (adam.h adam_update) with the same per-step constants
 // (consts[s] = {lr/bc1(s), 1/sqrt(bc2(s))}, written once per step by rs_adam_prepare), so lazy and
@@ -20,16 +20,6 @@
 
 namespace rs {
 namespace {
-
-// replay zero-gradient steps s = from .. to (inclusive)
-__device__ __forceinline__ void replay(const AdamConst& h, const float2* __restrict__ consts, int from,
-                                       int to, float& p, float& m, float& v) {
-  if (h.wd == 0.f && m == 0.f && v == 0.f) return;  // exact: such an element does not move
-  for (int s = from; s <= to; ++s) {
-    const float2 c = consts[s];
-    adam_update(h, c.x, c.y, 0.f, p, m, v);
-  }
-}
 
 // consts[0] (step 0 never runs) holds {cap as int bits, overflow flag as int bits}: every reader
 // clamps its step index to cap - 1, so a graph replayed past the capacity reads no memory past the
@@ -66,7 +56,7 @@ __global__ void flush_kernel(float* __restrict__ p, float* __restrict__ m, float
     for (int c = lane; c < D; c += 64) {
       const int64_t o = row * D + c;
       float pp = p[o], mm = m[o], vv = v[o];
-      replay(h, consts, from, target, pp, mm, vv);
+      adam_replay_zero<1>(h, consts, from, target, &pp, &mm, &vv);
       p[o] = pp; m[o] = mm; v[o] = vv;
     }
     if (lane == 0) last[row] = target;

@@ -137,10 +137,13 @@ class LazyTable:
         return LookupCall(keys, vals, n, rows, bag, -1 if pad is None else int(pad), mode, ids_ptr,
                           id_bytes, row_stride, keep, ws)
 
-    def lookup(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None, record=True):
+    def lookup(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None, record=True,
+               read_through=False):
         """Forward hook: bring the call's rows to the current optimizer step before they are
         gathered and, when the step will train on this lookup (`record`), list it for the step
         with its ids sorted by row. Default: sort, then rs_sorted_catchup over the distinct rows.
+        `read_through`: sort only -- the gather brings the rows current in registers
+        (rs_gather_fwd_lazy, read_through_args) and the optimizer step replays the same steps.
         A lookup no backward follows (evaluation) is not sorted at all: rs_lookup_catchup works
         in id order. (Measured and rejected: the sort of recorded lookups on a side stream with
         their catch-up in id order -- 0.833 vs 0.839 ms per C3 step, within noise.)"""
@@ -149,7 +152,7 @@ class LazyTable:
             c = self.sort_call(ids_ptr, rows, bag, row_stride, pad, mode, id_bytes, keep)
             self.calls.append(c)
         opt = self.flat.lazy_opt
-        if opt is None or rows * bag == 0:
+        if opt is None or rows * bag == 0 or (c is not None and read_through):
             return c
         hyper = (opt['step_dev'].data_ptr(), opt['consts'].data_ptr(), *opt['hyper'], _stream())
         if c is not None:
@@ -160,6 +163,16 @@ class LazyTable:
                       self.ptr(self.flat.data), self.ptr(opt['m']), self.ptr(opt['v']), self.last.data_ptr(),
                       *hyper)
         return c
+
+    def read_through_args(self):
+        """rs_gather_fwd_lazy's launch arguments (m_off, v_off, step, consts, b1, b2, eps, wd), or
+        None before the first optimizer step (every row is current then)."""
+        opt = self.flat.lazy_opt
+        if opt is None:
+            return None
+        base = self.flat.data.data_ptr()
+        return ((opt['m'].data_ptr() - base) // 4, (opt['v'].data_ptr() - base) // 4, opt['step_dev'].data_ptr(),
+                opt['consts'].data_ptr(), *opt['hyper'])
 
     def shard_lookup(self, seg, rows, record=True, err_ptr=None):
         """Forward of a lookup of a row-sharded table (module doc) -> (LookupCall or None, the
@@ -644,14 +657,14 @@ def gather_shards(local, t):
     return unshard(parts, t.V_full)
 
 
-def lookup_table(weight, ids_ptr, rows, bag, row_stride, pad, mode, keep=None, record=True):
+def lookup_table(weight, ids_ptr, rows, bag, row_stride, pad, mode, keep=None, record=True, read_through=False):
     """Forward-side hook of the custom ops for a table lookup: a LookupCall for large
     (lazy-Adam) tables (None for ordinary ones, and for a lookup no backward follows: `record`
     False, the rows are only brought current)."""
     t = getattr(weight, '_rs_lazy', None)
     if t is None or flat_of(weight) is not t.flat:
         return None
-    return t.lookup(ids_ptr, rows, bag, row_stride, pad, mode, keep=keep, record=record)
+    return t.lookup(ids_ptr, rows, bag, row_stride, pad, mode, keep=keep, record=record, read_through=read_through)
 
 
 def grad_of(p):

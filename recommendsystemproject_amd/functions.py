@@ -39,16 +39,47 @@ def _pad(v):
     return -1 if v is None else int(v)
 
 
+def _read_through():
+    """RSYS_READ_THROUGH=1: recorded lookups of lazy tables read their rows through the catch-up
+    inside the gather (rs_gather_fwd_lazy) instead of a catch-up pass that writes them back first.
+    Off by default: the replay is VALU work (~14 operations per element and skipped step), and
+    read-through does it twice (gather, then the optimizer step) where the pass does it once --
+    measured at C3 (rows 7 steps stale): gather 0.194 ms + Adam 0.160 against catch-up 0.154 +
+    gather 0.036 + Adam 0.095. It pays off only when the rows are mostly current."""
+    return os.environ.get('RSYS_READ_THROUGH', '0') == '1'
+
+
+_CALL_STREAMS = {}
+
+
+def _call_stream(parent, k):
+    """The k-th side stream of `parent` for the per-table lookup work of one gather."""
+    key = (parent.device.index, parent.cuda_stream, k)
+    st = _CALL_STREAMS.get(key)
+    if st is None:
+        st = _CALL_STREAMS[key] = torch.cuda.Stream(device=parent.device)
+    return st
+
+
 def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
     """Large (lazy-Adam) tables, flat.py: bring this call's rows to the current optimizer step
-    before the gather reads them and (`record`: a backward follows) sort its ids by row
-    (csrc/lookup.hip). Returns {segment index: LookupCall}; ordinary tables are not listed.
+    before the gather reads them -- or, recorded lookups, have the gather read them through the
+    catch-up (segment lazy_last) -- and (`record`: a backward follows) sort its ids by row
+    (csrc/lookup.hip). Returns ({segment index: LookupCall}, the gather's lazy launch arguments or
+    None); ordinary tables are not listed.
     `keep` (the id tensors the segments point into) stays referenced by the calls until the
     optimizer step (the data-parallel exchange re-reads the ids after the backward).
     A row-sharded table (flat.py module doc) is looked up here: its segment is replaced by one
     reading this rank's rows as the exchange returned them (the all-to-all's row buckets, or
-    the reduce-scatter's pooled bags), kept alive through `keep`."""
+    the reduce-scatter's pooled bags), kept alive through `keep`.
+    The sort + catch-up of different tables are independent chains of small, latency-bound
+    kernels (C3: the user-id table's 35 us beside the history table's 200 us): the second and later
+    tables run on side streams forked from and joined back into the current one (a table's own
+    calls stay in order on one stream: their catch-ups touch the same rows). RSYS_TOWER_STREAMS=0
+    keeps everything on the current stream."""
     calls = {}
+    lazy = None
+    groups = {}  # table -> segment indices, first-seen order
     for i, (s, t) in enumerate(zip(segs, tables)):
         if s.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL) and hasattr(t, '_rs_lazy'):
             lt = t._rs_lazy
@@ -59,16 +90,58 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
                 if c is not None:
                     calls[i] = c
                 continue
-            pool = s.kind == _hip.RS_SEG_POOL
-            bag = s.bag if pool else 1
-            mode = SEG_ONE
-            if pool:
-                mode = {_hip.RS_POOL['mean']: SEG_MEAN, _hip.RS_POOL['sum']: SEG_SUM}.get(s.pool_mode)
-            c = lookup_table(t, s.idx, rows, bag, s.idx_stride, None if s.pad_idx < 0 else s.pad_idx,
-                             -1 if mode is None else mode, keep=keep, record=record)
-            if c is not None:
-                calls[i] = c
-    return calls
+            groups.setdefault(id(t), []).append(i)
+
+    def one(i):
+        nonlocal lazy
+        s, t = segs[i], tables[i]
+        lt = t._rs_lazy
+        pool = s.kind == _hip.RS_SEG_POOL
+        bag = s.bag if pool else 1
+        mode = SEG_ONE
+        if pool:
+            mode = {_hip.RS_POOL['mean']: SEG_MEAN, _hip.RS_POOL['sum']: SEG_SUM}.get(s.pool_mode)
+        args = lt.read_through_args() if record and mode is not None and _read_through() else None
+        c = lookup_table(t, s.idx, rows, bag, s.idx_stride, None if s.pad_idx < 0 else s.pad_idx,
+                         -1 if mode is None else mode, keep=keep, record=record, read_through=args is not None)
+        if c is not None:
+            calls[i] = c
+        if args is not None and flat_of(t) is lt.flat:
+            if lazy is not None and lazy != args:
+                raise RuntimeError('lazy tables of one gather must share one flat buffer and optimizer')
+            lazy = args
+            s.lazy_last = lt.last.data_ptr()
+        return c
+
+    order = list(groups.values())
+    fork = len(order) > 1 and os.environ.get('RSYS_TOWER_STREAMS', '1') != '0'
+    if not fork:
+        for idxs in order:
+            for i in idxs:
+                one(i)
+        return calls, lazy
+    # the largest table's work stays on the current stream, the others fork
+    order.sort(key=lambda idxs: -sum(int(segs[i].vocab) for i in idxs))
+    main = torch.cuda.current_stream()
+    sides = []
+    for k, idxs in enumerate(order):
+        if k == 0:
+            for i in idxs:
+                one(i)
+            continue
+        st = _call_stream(main, k)
+        st.wait_stream(main)
+        with torch.cuda.stream(st):
+            for i in idxs:
+                c = one(i)
+                if c is not None:  # made on the side stream, read on the main one until the step ends
+                    for x in (c.keys, c.vals, c.ws):
+                        if isinstance(x, torch.Tensor):
+                            x.record_stream(main)
+        sides.append(st)
+    for st in sides:
+        main.wait_stream(st)
+    return calls, lazy
 
 
 def _grad_lazy(segs, calls, dout, tables):
@@ -147,8 +220,8 @@ def seq_input_fwd(proc, seqd, B, L, p, key, err, need=True):
     M = B * L
     dev = proc.pos_emb.weight.device
     cat = torch.empty(M, dcat, device=dev, dtype=torch.float32)
-    calls = _lookup_lazy(segs, tables, M, keep, record=need, err=err)
-    ops.gather_fwd(segs, M, cat, err)
+    calls, lazy = _lookup_lazy(segs, tables, M, keep, record=need, err=err)
+    ops.gather_fwd(segs, M, cat, err, lazy=lazy)
     lin = proc.feature_projection[0]
     pos = proc.pos_emb.weight
     # drop_b(drop_a(cat W^T + b) + pos[l]) in the GEMM epilogue (sites 0, 1 = rs_dropout masks)
@@ -492,8 +565,8 @@ class TowerFeatureFn(torch.autograd.Function):
             raise RuntimeError(f'too many features in one tower ({len(segs)} > {_hip.MAX_SEGMENTS})')
         dev = tower.feature_bn.weight.device
         out = torch.empty(B, col, device=dev, dtype=torch.float32)
-        calls = _lookup_lazy(segs, [w for w, _ in pp], B, keep, record=need, err=tower.err_flag)
-        ops.gather_fwd(segs, B, out, tower.err_flag)
+        calls, lazy = _lookup_lazy(segs, [w for w, _ in pp], B, keep, record=need, err=tower.err_flag)
+        ops.gather_fwd(segs, B, out, tower.err_flag, lazy=lazy)
         if need:
             ctx.segs, ctx.pp, ctx.keep, ctx.B, ctx.calls = segs, pp, keep, B, calls
             ctx.has_seq = seq_vec is not None

@@ -200,9 +200,14 @@ def segments_array(segs):
     return arr
 
 
-def gather_fwd(segs, rows, out, err_flag=None):
+def gather_fwd(segs, rows, out, err_flag=None, lazy=None):
+    """rs_gather_fwd; with `lazy` = (m_off, v_off, step, consts, b1, b2, eps, wd) the segments
+    whose lazy_last is set read their rows through the lazy-Adam catch-up (rs_gather_fwd_lazy)."""
     arr = segments_array(segs)
-    call('rs_gather_fwd', arr, len(segs), rows, P(out), out.stride(0), P(err_flag), stream())
+    if lazy is not None and any(s.lazy_last for s in segs):
+        call('rs_gather_fwd_lazy', arr, len(segs), rows, P(out), out.stride(0), P(err_flag), *lazy, stream())
+    else:
+        call('rs_gather_fwd', arr, len(segs), rows, P(out), out.stride(0), P(err_flag), stream())
     return out
 
 

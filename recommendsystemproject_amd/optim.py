@@ -8,6 +8,8 @@ total norm and the clip coefficient kept on the device.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 
 from . import _hip, ops
@@ -26,6 +28,38 @@ def _flat_cover(params):
         if all(p.data_ptr() == base + 4 * p._rs_offset for p in params):
             return f
     return None
+
+
+def _row_class(D):
+    """rs_sorted_*_batch lanes-per-row class of a table width."""
+    return 0 if D <= 16 else 1 if D <= 32 else 2 if D <= 64 else 3 if D <= 128 else 4
+
+
+def _sorted_batches(items):
+    """[(rs_sorted_call_t, extra)] -> launches of at most 8 calls of one row class, in order."""
+    out, cur, cls = [], [], None
+    for sc, extra in items:
+        k = _row_class(sc.D)
+        if cur and (k != cls or len(cur) == 8):
+            out.append(cur)
+            cur = []
+        cls = k
+        cur.append((sc, extra))
+    if cur:
+        out.append(cur)
+    return out
+
+
+def _sorted_call(t, c, i, p=None, g=None, m=None, v=None, owner=None):
+    sc = _hip.SortedCall()
+    sc.keys, sc.n, sc.D, sc.call = c.keys.data_ptr(), c.n, t.D, i
+    sc.p = None if p is None else t.ptr(p)
+    sc.g = None if g is None else t.ptr(g)
+    sc.m = None if m is None else t.ptr(m)
+    sc.v = None if v is None else t.ptr(v)
+    sc.last = t.last.data_ptr() if p is not None else None
+    sc.owner = None if owner is None else owner.data_ptr()
+    return sc
 
 
 class _DeviceClip:
@@ -50,10 +84,12 @@ class _DeviceClip:
                 work.append((t, c, owner, i))
         ws = torch.empty(nd + ns * len(work) + 2, dtype=torch.float64, device=g.device)
         _hip.call('rs_grad_sqnorm', g.data_ptr(), n, float(scale), ws.data_ptr(), ops.stream())
-        for k, (t, c, owner, i) in enumerate(work):
-            _hip.call('rs_sorted_sqnorm', c.keys.data_ptr(), c.n, t.D, t.ptr(g),
-                      None if owner is None else owner.data_ptr(), i, float(scale),
-                      ws.data_ptr() + 8 * (nd + k * ns), ops.stream())
+        # every call's partials in one launch per row class (call k's at nd + k * ns)
+        items = [(_sorted_call(t, c, i, g=g, owner=owner), k) for k, (t, c, owner, i) in enumerate(work)]
+        for batch in _sorted_batches(items):
+            arr = (_hip.SortedCall * len(batch))(*[sc for sc, _ in batch])
+            _hip.call('rs_sorted_sqnorm_batch', C.addressof(arr), len(batch), float(scale),
+                      ws.data_ptr() + 8 * (nd + batch[0][1] * ns), ops.stream())
         first = next((k for k, w in enumerate(work) if getattr(w[0], 'shard', None) is not None), None)
         if first is not None:
             torch.distributed.all_reduce(ws[nd + first * ns:nd + len(work) * ns])
@@ -187,17 +223,22 @@ class Adam(torch.optim.Optimizer):
                     hyper = (float(b1), float(b2), eps, wd)
                     f.lazy_opt = dict(m=st['m'], v=st['v'], step_dev=st['step_dev'],
                                       consts=st['consts'], hyper=hyper)
+                    # every table's calls in one launch per row class (a row is stepped by exactly
+                    # one call: the lowest holding it, rs_sorted_owner, when a table has several)
+                    items = []
                     for t in f.lazy:
                         owner = t.mark_owners() if coef is None else t.owner
                         calls = t.step_calls()
                         for i, c in enumerate(calls):
                             if c.n == 0:
                                 continue
-                            _hip.call('rs_sorted_adam', c.keys.data_ptr(), c.n, t.D, t.ptr(f.data),
-                                      t.ptr(f.grad), t.ptr(st['m']), t.ptr(st['v']), t.last.data_ptr(),
-                                      None if owner is None or len(calls) <= 1 else owner.data_ptr(), i,
-                                      st['step_dev'].data_ptr(), st['consts'].data_ptr(), *hyper,
-                                      float(self.grad_scale), coef, ops.stream())
+                            items.append((_sorted_call(t, c, i, p=f.data, g=f.grad, m=st['m'], v=st['v'],
+                                                       owner=None if len(calls) <= 1 else owner), None))
+                    for batch in _sorted_batches(items):
+                        arr = (_hip.SortedCall * len(batch))(*[sc for sc, _ in batch])
+                        _hip.call('rs_sorted_adam_batch', C.addressof(arr), len(batch), st['step_dev'].data_ptr(),
+                                  st['consts'].data_ptr(), *hyper, float(self.grad_scale), coef, ops.stream())
+                    for t in f.lazy:
                         t.end_step()
                 continue
             if clip_max_norm is not None and clip_max_norm > 0:

@@ -46,8 +46,10 @@ def _gather_work(a, bwd=False):
         s = segs[i]
         if s.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL):
             bag = s.bag if s.kind == _hip.RS_SEG_POOL else 1
-            # table rows read (fwd) / scattered (bwd) + int64 ids
-            byts += rows * bag * (s.dim * 4 + 8)
+            # table rows read (fwd) / scattered (bwd) + int64 ids; a read-through
+            # lazy segment (rs_gather_fwd_lazy) also reads the row's two moment rows and `last`
+            rt = not bwd and len(a) > 7 and bool(s.lazy_last)
+            byts += rows * bag * (s.dim * 4 * (3 if rt else 1) + 8 + (4 if rt else 0))
         elif s.kind == _hip.RS_SEG_DENSE:
             byts += rows * 4
         else:
@@ -177,6 +179,7 @@ WORK = {
     'rs_attn_fwd': _attn_fwd_work,
     'rs_attn_bwd': _attn_bwd_work,
     'rs_gather_fwd': _gather_work,
+    'rs_gather_fwd_lazy': _gather_work,
     'rs_gather_bwd': lambda a: _gather_work(a, True),
     'rs_add_layernorm_fwd': _ln_fwd_work,
     'rs_layernorm_bwd': _ln_bwd_work,

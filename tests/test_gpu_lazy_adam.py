@@ -160,12 +160,35 @@ def _sorted_rows(keys):
     return sorted(set(int(x) for x in k if x != SENT))
 
 
-@pytest.mark.parametrize('catch', ['sorted', 'ids'])
+def _gather_pair(ids_d, D, V, pad, table, lazy=None, lazy_last=None):
+    """The call's rows gathered two ways: mean bags of 3 and one id per row (rs_gather_fwd, or
+    rs_gather_fwd_lazy reading through the catch-up when `lazy` is given)."""
+    rows = ids_d.shape[0]
+    outs = []
+    for kind in (_hip.RS_SEG_POOL, _hip.RS_SEG_SPARSE):
+        s = _hip.FeatureSeg()
+        s.kind, s.dim, s.out_col, s.vocab, s.pad_idx, s.table = kind, D, 0, V, pad, table.data_ptr()
+        if kind == _hip.RS_SEG_POOL:
+            s.pool_mode, s.bag, s.idx_stride, s.idx, n = _hip.RS_POOL['mean'], 3, 3, ids_d.data_ptr(), rows
+        else:
+            s.idx_stride, s.idx, n = 1, ids_d.data_ptr(), rows * 3
+        if lazy_last is not None:
+            s.lazy_last = lazy_last.data_ptr()
+        out = torch.full((n, D), 7.0, device=DEV)
+        err = torch.zeros(1, dtype=torch.int32, device=DEV)
+        ops.gather_fwd([s], n, out, err, lazy=lazy)
+        outs.append(out)
+    return outs
+
+
+@pytest.mark.parametrize('catch', ['sorted', 'ids', 'read'])
 @pytest.mark.parametrize('D,wd,clip,calls', [(40, 0.0, False, 1), (128, 0.0, True, 1), (16, 0.0, False, 1),
                                              (64, 0.01, True, 1), (32, 0.0, True, 2), (6, 0.01, False, 2)])
 def test_lazy_adam_bitwise_equals_dense(D, wd, clip, calls, catch):
-    """Forward catch-up either over the sorted keys (rs_sorted_catchup) or straight from the id
-    matrix (rs_lookup_catchup: one compare-and-swap per row picks the replaying lookup)."""
+    """Forward catch-up either over the sorted keys (rs_sorted_catchup), straight from the id
+    matrix (rs_lookup_catchup: one compare-and-swap per row picks the replaying lookup), or read
+    through inside the gather (rs_gather_fwd_lazy: nothing written; the gathered bags and rows
+    equal the dense weights' bitwise, and the optimizer step's replay stores the same state)."""
     V, pad, steps, cap = 3000, 7, 9, 64
     gen = torch.Generator().manual_seed(D + calls)
     p0 = torch.randn(V, D, generator=gen).to(DEV)
@@ -197,7 +220,13 @@ def test_lazy_adam_bitwise_equals_dense(D, wd, clip, calls, catch):
             ids_d = ids.to(DEV)
             keys, _ = _sort(ids_d, V)
             sorted_calls.append(keys)
-            if catch == 'sorted':
+            if catch == 'read':
+                lz = ((ml.data_ptr() - pl.data_ptr()) // 4, (vl.data_ptr() - pl.data_ptr()) // 4, step_l.data_ptr(),
+                      consts.data_ptr(), *hyper)
+                got = _gather_pair(ids_d, D, V, pad, pl, lazy=lz, lazy_last=last)
+                want = _gather_pair(ids_d, D, V, pad, pd)
+                assert all(torch.equal(a, b) for a, b in zip(got, want)), t
+            elif catch == 'sorted':
                 _hip.call('rs_sorted_catchup', keys.data_ptr(), ids.numel(), D, pl.data_ptr(), ml.data_ptr(),
                           vl.data_ptr(), last.data_ptr(), step_l.data_ptr(), consts.data_ptr(), *hyper, S)
             else:
@@ -207,8 +236,8 @@ def test_lazy_adam_bitwise_equals_dense(D, wd, clip, calls, catch):
             rows |= set(_sorted_rows(keys))
         rows = sorted(rows)
         # what the forward reads: touched rows (pad included) equal the dense weights exactly
-        if rows:
-            r = torch.tensor(rows, device=DEV)
+        r = torch.tensor(rows, device=DEV) if rows else None
+        if rows and catch != 'read':
             assert torch.equal(pl[r], pd[r]), t
         # gradient of the touched rows except the pad row (what the segment sum leaves)
         g = torch.zeros(V, D)

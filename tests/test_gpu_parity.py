@@ -40,13 +40,16 @@ def zero_dropout(cfg):
     return cfg
 
 
-@pytest.mark.parametrize('lazy', [False, True], ids=['dense_adam', 'lazy_adam'])
+@pytest.mark.parametrize('lazy', [False, True, 'read'], ids=['dense_adam', 'lazy_adam', 'lazy_read_through'])
 @pytest.mark.parametrize('path', GOLD, ids=[os.path.basename(p)[:-4] for p in GOLD])
 def test_training_step_matches_reference_golden(path, lazy, monkeypatch):
     """lazy: every lookup table trained by lazy-exact Adam (flat.py), which must reproduce the
-    reference's dense-gradient torch.optim.Adam (trap T16) to the same tolerance."""
+    reference's dense-gradient torch.optim.Adam (trap T16) to the same tolerance; 'read': with the
+    forward's catch-up read through inside the gather (rs_gather_fwd_lazy)."""
     if lazy:
         monkeypatch.setenv('RSYS_LAZY_ROWS', '1')
+    if lazy == 'read':
+        monkeypatch.setenv('RSYS_READ_THROUGH', '1')
     cfg, meta, data = gu.load(path)
     shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
     state = synth.make_state(shapes, seed=meta['weight_seed'])

@@ -1,7 +1,8 @@
 """Phase timing of the fused tower kernels (profiling only): runs one C3-shaped user-tower chain
 forward + backward with rs_tower_debug_buffer set, one kernel at a time, and prints per-phase
 percentiles across workgroups (us since the kernel's first workgroup started).
-Phases: 0 start, 1 prologue done, 2 main loop done, 3 C stored, 4 column sums done, 5 hand-off done."""
+Phases: 0 start, 1 prologue done, 2 main loop done, 3 C stored, 4 column sums done, 5 hand-off done,
+6 first k chunk done, 7 second k chunk done."""
 import os
 import sys
 
@@ -42,7 +43,7 @@ def call(name, *args):
         t0 = t[:, 0].min()
         rel = (t - t0) / 100.0  # 100 MHz -> us
         ph = [f'p{i}:' + '/'.join(f'{np.percentile(rel[:, i][t[:, i] > 0], q):.1f}' for q in (0, 50, 100))
-              for i in range(6) if (t[:, i] > 0).any()]
+              for i in range(8) if (t[:, i] > 0).any()]
         print(f'{name:14s} wgs={len(t):4d} ' + ' '.join(ph))
         return r
     return orig(name, *args)
