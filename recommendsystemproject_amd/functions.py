@@ -52,9 +52,15 @@ def _read_through():
 _CALL_STREAMS = {}
 
 
+def _skey(s):
+    """A stream's identity (torch.cuda.Stream, or the generic torch.Stream dynamo hands out)."""
+    h = getattr(s, 'cuda_stream', None)
+    return h if h is not None else ('id', getattr(s, 'stream_id', id(s)), getattr(s, 'device_index', None))
+
+
 def _call_stream(parent, k):
     """The k-th side stream of `parent` for the per-table lookup work of one gather."""
-    key = (parent.device.index, parent.cuda_stream, k)
+    key = (parent.device.index, _skey(parent), k)
     st = _CALL_STREAMS.get(key)
     if st is None:
         st = _CALL_STREAMS[key] = torch.cuda.Stream(device=parent.device)
@@ -76,7 +82,9 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
     kernels (C3: the user-id table's 35 us beside the history table's 200 us): the second and later
     tables run on side streams forked from and joined back into the current one (a table's own
     calls stay in order on one stream: their catch-ups touch the same rows). RSYS_TOWER_STREAMS=0
-    keeps everything on the current stream."""
+    keeps everything on the current stream. (Measured: inside the replayed hipGraph the forked
+    chain still runs on the forking stream's queue; sending it to the item tower's stream instead
+    queued it behind that tower and made the C3 step slower, 0.718 -> 0.75 ms.)"""
     calls = {}
     lazy = None
     groups = {}  # table -> segment indices, first-seen order
