@@ -306,7 +306,8 @@ int rs_batchnorm_bwd(const float* x, const float* y, const float* dy, const floa
  *
  * rs_tower_stats: feature_bn's batch statistics of x [G*Bg, C] (GenericTower.py:234): mean /
  *   rstd [G*C] published, running statistics updated group by group (momentum, unbiased
- *   variance), num_batches_tracked += G.
+ *   variance), num_batches_tracked += G. rng_state non-NULL: also the MLP's dropout key of this
+ *   step, key_out[0..1] = rng_state[0..1], rng_state[1] += 1 (rs_rng_next folded in).
  * rs_tower_fwd: A [G*Bg, K] -> BN with the published in_mean / in_rstd and bn_w / bn_b (+ ReLU
  *   + dropout (key, site) when relu: the rs_dropout_fwd draw of element row*K + k, Tower.py:17-19)
  *   -> h (written to h_out when non-NULL: the weight-gradient operand) -> h W^T + bias (W [N][K],
@@ -327,7 +328,8 @@ int rs_tower_debug_buffer(unsigned long long* buf);
 int rs_tower_sync_ints(int G, int N);
 int rs_tower_stats(const float* x, int G, int Bg, int C, float* part, int* sync, double* scratch,
                    float* mean, float* rstd, float* running_mean, float* running_var,
-                   int64_t* num_batches, float momentum, float eps, void* stream);
+                   int64_t* num_batches, float momentum, float eps, int64_t* rng_state, int64_t* key_out,
+                   void* stream);
 int rs_tower_fwd(const float* A, int G, int Bg, int K, const float* in_mean, const float* in_rstd,
                  const float* bn_w, const float* bn_b, int relu, float drop_p, const int64_t* key,
                  int site, float* h_out, const float* W, const float* bias, int N, float* z,
@@ -484,7 +486,9 @@ int rs_counter_add(int64_t* counter, int64_t delta, void* stream);
 
 /* ---------------------------------------------------------------- lazy-exact Adam (large tables)
  * Dense-gradient Adam semantics (every row moves every step, T16) without sweeping the table:
- * rows carry last[] = the optimizer step they were last brought to; consts[s] =
+ * rows carry last[V][2] int32 = the optimizer step a row's moments (m, v) and its parameters (p)
+ * were last brought to (p can be ahead: with weight_decay == 0 the forward catch-up writes p
+ * alone and the optimizer step replays the moments again; otherwise the two are equal); consts[s] =
  * {lr/bc1(s), sqrt(bc2(s))} is written once per step by rs_adam_prepare (which also advances
  * the device step count; consts[0] holds {capacity, overflow flag} as int bits and every reader
  * clamps its step index to the capacity). rs_sparse_flush brings every row to the current step
@@ -617,6 +621,10 @@ int rs_sum(const float* x, int n, float scale, float* out, void* stream);
 /* *flag |= bit if x[0..n) holds a NaN (x 16-byte aligned). The loss inputs' NaN guard of
  * TwoTowerModel.compute_loss (TwoTowerModel.py:88-91, 99-100): checked on the device every step,
  * raised by the host at its log-point sync. */
+/* The same for up to 4 tensors in one launch: flag |= bits[i] if x[i][0 .. n[i]) holds a NaN
+ * (host arrays read during the call only). */
+int rs_nan_check_many(int k, const float* const* x, const int64_t* n, const int* bits, int* flag,
+                      void* stream);
 int rs_nan_check(const float* x, int64_t n, int* flag, int bit, void* stream);
 
 #ifdef __cplusplus

@@ -69,6 +69,7 @@ SIGNATURES = {
     'rs_sorted_adam_batch': (i32, [vp, i32, vp, vp, f32, f32, f32, f32, f32, vp, vp]),
     'rs_sorted_sqnorm_batch': (i32, [vp, i32, f32, vp, vp]),
     'rs_copy_many': (i32, [i32, vp, vp, vp, vp]),
+    'rs_nan_check_many': (i32, [i32, vp, vp, vp, vp, vp]),
     'rs_gather_fwd_lazy': (i32, [vp, i32, i32, vp, i32, vp, i64, i64, vp, vp, f32, f32, f32, f32, vp]),
     'rs_gather_ws_bytes': (i64, [vp, i32, i32]),
     'rs_gather_bwd': (i32, [vp, i32, i32, vp, i32, vp, vp]),
@@ -90,7 +91,7 @@ SIGNATURES = {
     'rs_tower_wgrad_sync_ints': (i32, [i32, i32]),
     'rs_tower_wgrad': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp]),
     'rs_tower_sync_ints': (i32, [i32, i32]),
-    'rs_tower_stats': (i32, [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, f32, vp]),
+    'rs_tower_stats': (i32, [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, vp, vp]),
     'rs_tower_fwd': (i32, [vp, i32, i32, i32, vp, vp, vp, vp, i32, f32, vp, i32, vp, vp, vp, i32, vp, vp,
                            vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, vp, f32, i32, vp]),
     'rs_tower_bwd': (i32, [vp, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp,

@@ -80,6 +80,45 @@ __device__ __forceinline__ void adam_replay_zero(const AdamConst& h, const float
   }
 }
 
+// The moments alone over zero-gradient steps from .. to (weight_decay == 0 only: then m and v do
+// not depend on p): the same m and v bits adam_replay_zero leaves. A lazy table whose forward
+// catch-up wrote p alone (its p is current to a later step than its moments, `last` [.., 1] vs
+// [.., 0]) brings the moments up to p's step with this before replaying on.
+template <int W>
+__device__ __forceinline__ void adam_replay_mv(const AdamConst& h, int from, int to, float* m, float* v) {
+#pragma clang fp contract(off)
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  constexpr int NP = (W + 1) / 2;
+  f2v mm[NP], vv[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    mm[q] = f2v{m[2 * q], 2 * q + 1 < W ? m[2 * q + 1] : 0.f};
+    vv[q] = f2v{v[2 * q], 2 * q + 1 < W ? v[2 * q + 1] : 0.f};
+  }
+  const f2v omb1 = f2v{h.one_m_b1, h.one_m_b1}, b2 = f2v{h.b2, h.b2}, zero = f2v{0.f, 0.f};
+  for (int s = from; s <= to; ++s) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      mm[q] = mm[q] + omb1 * (zero - mm[q]);
+      vv[q] = vv[q] * b2;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    m[2 * q] = mm[q][0]; v[2 * q] = vv[q][0];
+    if (2 * q + 1 < W) { m[2 * q + 1] = mm[q][1]; v[2 * q + 1] = vv[q][1]; }
+  }
+}
+
+// A lazy row's catch-up from its state -- moments at step lm, parameters at step lp >= lm (equal
+// when weight_decay != 0) -- to step `to`: the moments alone to lp, then full zero-gradient steps.
+template <int W>
+__device__ __forceinline__ void adam_catch_row(const AdamConst& h, const float2* __restrict__ consts, int lm, int lp,
+                                               int to, float* p, float* m, float* v) {
+  if (lp > lm) adam_replay_mv<W>(h, lm + 1, lp < to ? lp : to, m, v);
+  adam_replay_zero<W>(h, consts, (lp > lm ? lp : lm) + 1, to, p, m, v);
+}
+
 // per-step constants {lr / bc1(t), 1 / sqrt(bc2(t))}, computed in double then rounded once
 __host__ __device__ inline void adam_step_consts(double lr, double b1, double b2, double t,
                                                  float* step_size, float* inv_bc2_sqrt) {

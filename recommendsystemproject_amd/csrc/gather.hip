@@ -129,16 +129,16 @@ __device__ __forceinline__ int lazy_target(const LazyLaunch& z) {
 // weight_decay == 0 -- its moments are zero and the replay is the identity; per element, zero
 // moments likewise).
 template <int W = 4>
-__device__ __forceinline__ void lazy_replay(const LazyLaunch& z, int last, int t, float* p, const float* mv,
+__device__ __forceinline__ void lazy_replay(const LazyLaunch& z, int2 last, int t, float* p, const float* mv,
                                             const float* vv) {
-  if (last + 1 > t || (last == 0 && z.h.wd == 0.f)) return;
+  if (last.y >= t || (last.x == 0 && z.h.wd == 0.f)) return;
   float m[W], v[W];
 #pragma unroll
   for (int j = 0; j < W; ++j) {
     m[j] = mv[j];
     v[j] = vv[j];
   }
-  adam_replay_zero<W>(z.h, z.consts, last + 1, t, p, m, v);
+  adam_catch_row<W>(z.h, z.consts, last.x, last.y, t, p, m, v);
 }
 
 // Pooled bag: the (un-normalised) sum or max of positions [lbeg, lend) of row `row`'s bag.
@@ -164,7 +164,7 @@ __device__ __forceinline__ void pool_acc(const SegLaunch& a, const rs_feature_se
     bool ok[NB];
     float v[NB][4];
     float mv[LAZY ? NB : 1][4], vv[LAZY ? NB : 1][4];
-    int lst[LAZY ? NB : 1];
+    int2 lst[LAZY ? NB : 1];
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
       const bool valid = raw[u] >= 0 && raw[u] < sg.vocab;
@@ -173,7 +173,7 @@ __device__ __forceinline__ void pool_acc(const SegLaunch& a, const rs_feature_se
       const int64_t r = ok[u] ? raw[u] : 0;
       load_row<VEC>(sg.table + r * sg.dim + c, v[u]);
       if constexpr (LAZY) {
-        lst[u] = sg.lazy_last[r];
+        lst[u] = reinterpret_cast<const int2*>(sg.lazy_last)[r];
         load_row<VEC>(sg.table + r * sg.dim + c + a.lz.moff, mv[u]);
         load_row<VEC>(sg.table + r * sg.dim + c + a.lz.voff, vv[u]);
       }
@@ -212,7 +212,7 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
       load_row<VEC>(pr, acc);
       if constexpr (LAZY) {
         float mv[4], vv[4];
-        const int l = sg.lazy_last[id];
+        const int2 l = reinterpret_cast<const int2*>(sg.lazy_last)[id];
         load_row<VEC>(pr + a.lz.moff, mv);
         load_row<VEC>(pr + a.lz.voff, vv);
         lazy_replay<W>(a.lz, l, lazy_target(a.lz), acc, mv, vv);
@@ -258,7 +258,7 @@ __device__ void gather_sparse_rows(const SegLaunch& a, const rs_feature_seg_t& s
   }
   float v[R][4];
   float mv[LAZY ? R : 1][4], vv[LAZY ? R : 1][4];
-  int lst[LAZY ? R : 1];
+  int2 lst[LAZY ? R : 1];
   bool okk[R];
   bool bad = false;
 #pragma unroll
@@ -270,7 +270,7 @@ __device__ void gather_sparse_rows(const SegLaunch& a, const rs_feature_seg_t& s
     const float* pr = sg.table + (ok ? id[k] : 0) * sg.dim + c;
     load_row<true>(pr, v[k]);
     if constexpr (LAZY) {
-      lst[k] = sg.lazy_last[ok ? id[k] : 0];
+      lst[k] = reinterpret_cast<const int2*>(sg.lazy_last)[ok ? id[k] : 0];
       load_row<true>(pr + a.lz.moff, mv[k]);
       load_row<true>(pr + a.lz.voff, vv[k]);
     }

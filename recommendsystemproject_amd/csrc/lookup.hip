@@ -310,14 +310,6 @@ __global__ __launch_bounds__(kTileThreads) void sort_tile_kernel(
 }
 
 // ---------------------------------------------------------------- per distinct row
-__device__ __forceinline__ void replay(const AdamConst& h, const float2* __restrict__ consts, int from,
-                                       int to, float& p, float& m, float& v) {
-  if (h.wd == 0.f && m == 0.f && v == 0.f) return;  // exact: such an element does not move
-  for (int s = from; s <= to; ++s) {
-    const float2 c = consts[s];
-    adam_update(h, c.x, c.y, 0.f, p, m, v);
-  }
-}
 
 __device__ __forceinline__ int clamp_step(const float2* consts, int64_t t) {
   const int cap = __float_as_int(consts[0].x);
@@ -389,15 +381,21 @@ __device__ __forceinline__ void sorted_rows_body(const RowArgs& a, int bid, int 
         if (act[u] && gl == 0) atomicMin(&a.owner[row[u]], a.call);
       continue;
     }
-    int from[U];
+    // a row's state steps: lm = its moments', lp = its parameters' (lp > lm after a forward
+    // catch-up that wrote p alone, weight_decay == 0; equal otherwise)
+    int lm[U], lp[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      from[u] = 1;
+      lm[u] = lp[u] = 0;
       if (act[u] && OP != kCatchup && a.owner && a.owner[row[u]] != a.call) act[u] = false;
-      if (act[u] && (OP == kCatchup || OP == kAdam)) from[u] = a.last[row[u]] + 1;
-      // catch-up: nothing to replay, or a row never stepped (its m = v = 0 from the start: with
+      if (act[u] && (OP == kCatchup || OP == kAdam)) {
+        const int2 l2 = reinterpret_cast<const int2*>(a.last)[row[u]];
+        lm[u] = l2.x;
+        lp[u] = l2.y;
+      }
+      // catch-up: p already current, or a row never stepped (its m = v = 0 from the start: with
       // weight_decay == 0 the replay is the identity, exactly)
-      if (OP == kCatchup && act[u] && (from[u] > t || (from[u] == 1 && a.h.wd == 0.f))) act[u] = false;
+      if (OP == kCatchup && act[u] && (lp[u] >= t || (lm[u] == 0 && a.h.wd == 0.f))) act[u] = false;
     }
     float pp[U][4], mm[U][4], vv[U][4], gg[U][4];
 #pragma unroll
@@ -408,7 +406,7 @@ __device__ __forceinline__ void sorted_rows_body(const RowArgs& a, int bid, int 
         if (vec) {
           const float4 p4 = *reinterpret_cast<const float4*>(a.p + o);
           pp[u][0] = p4.x; pp[u][1] = p4.y; pp[u][2] = p4.z; pp[u][3] = p4.w;
-          if (from[u] == 1 && a.h.wd == 0.f && OP == kAdam) {  // never stepped: m = v = 0
+          if (lm[u] == 0 && a.h.wd == 0.f && OP == kAdam) {  // never stepped: m = v = 0
 #pragma unroll
             for (int j = 0; j < 4; ++j) { mm[u][j] = 0.f; vv[u][j] = 0.f; }
           } else {
@@ -417,8 +415,13 @@ __device__ __forceinline__ void sorted_rows_body(const RowArgs& a, int bid, int 
             mm[u][0] = m4.x; mm[u][1] = m4.y; mm[u][2] = m4.z; mm[u][3] = m4.w;
             vv[u][0] = v4.x; vv[u][1] = v4.y; vv[u][2] = v4.z; vv[u][3] = v4.w;
           }
-        } else {
-          for (int j = 0; j < w; ++j) { pp[u][j] = a.p[o + j]; mm[u][j] = a.m[o + j]; vv[u][j] = a.v[o + j]; }
+        } else {  // D % 4 != 0: the lane's columns past w are zeros (m = v = 0: they stay put)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pp[u][j] = j < w ? a.p[o + j] : 0.f;
+            mm[u][j] = j < w ? a.m[o + j] : 0.f;
+            vv[u][j] = j < w ? a.v[o + j] : 0.f;
+          }
         }
       }
       if (OP == kAdam || OP == kSqnorm) {
@@ -435,22 +438,9 @@ __device__ __forceinline__ void sorted_rows_body(const RowArgs& a, int bid, int 
       if (!act[u]) continue;
       if (w > 0) {
         const int64_t o = row[u] * a.D + c0;
-        if (OP == kCatchup) {
-          if (w == 4) {
-            adam_replay_zero<4>(a.h, a.consts, from[u], t, pp[u], mm[u], vv[u]);
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (j < w) replay(a.h, a.consts, from[u], t, pp[u][j], mm[u][j], vv[u][j]);
-          }
-        } else if (OP == kAdam) {
-          if (w == 4) {
-            adam_replay_zero<4>(a.h, a.consts, from[u], t - 1, pp[u], mm[u], vv[u]);
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (j < w && from[u] <= t - 1) replay(a.h, a.consts, from[u], t - 1, pp[u][j], mm[u][j], vv[u][j]);
-          }
+        if (OP == kCatchup || OP == kAdam)
+          adam_catch_row<4>(a.h, a.consts, lm[u], lp[u], OP == kCatchup ? t : t - 1, pp[u], mm[u], vv[u]);
+        if (OP == kAdam) {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             if (j < w) adam_update(a.h, ct.x, ct.y, gg[u][j] * s, pp[u][j], mm[u][j], vv[u][j]);
@@ -463,12 +453,20 @@ __device__ __forceinline__ void sorted_rows_body(const RowArgs& a, int bid, int 
             }
         }
         if (OP == kCatchup || OP == kAdam) {
+          // the forward catch-up writes p alone when weight_decay == 0 (the moments stay at their
+          // step and are replayed again by the optimizer step: two row writes per row saved)
+          const bool mv = OP == kAdam || a.h.wd != 0.f;
           if (vec) {
             *reinterpret_cast<float4*>(a.p + o) = make_float4(pp[u][0], pp[u][1], pp[u][2], pp[u][3]);
-            *reinterpret_cast<float4*>(a.m + o) = make_float4(mm[u][0], mm[u][1], mm[u][2], mm[u][3]);
-            *reinterpret_cast<float4*>(a.v + o) = make_float4(vv[u][0], vv[u][1], vv[u][2], vv[u][3]);
+            if (mv) {
+              *reinterpret_cast<float4*>(a.m + o) = make_float4(mm[u][0], mm[u][1], mm[u][2], mm[u][3]);
+              *reinterpret_cast<float4*>(a.v + o) = make_float4(vv[u][0], vv[u][1], vv[u][2], vv[u][3]);
+            }
           } else {
-            for (int j = 0; j < w; ++j) { a.p[o + j] = pp[u][j]; a.m[o + j] = mm[u][j]; a.v[o + j] = vv[u][j]; }
+            for (int j = 0; j < w; ++j) {
+              a.p[o + j] = pp[u][j];
+              if (mv) { a.m[o + j] = mm[u][j]; a.v[o + j] = vv[u][j]; }
+            }
           }
         }
         if (OP == kAdam || OP == kZero) {
@@ -477,7 +475,8 @@ __device__ __forceinline__ void sorted_rows_body(const RowArgs& a, int bid, int 
         }
       }
       if ((OP == kCatchup || OP == kAdam) && gl == 0) {
-        a.last[row[u]] = t;
+        const bool p_only = OP == kCatchup && a.h.wd == 0.f;
+        reinterpret_cast<int2*>(a.last)[row[u]] = make_int2(p_only ? lm[u] : t, t);
         if (OP == kAdam && a.owner) a.owner[row[u]] = 0x7fffffff;
       }
     }
@@ -549,12 +548,18 @@ __global__ __launch_bounds__(256) void lookup_catchup_kernel(IdCatchArgs a) {
   for (int64_t e = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G; e < a.n; e += ngroups) {
     const uint32_t k = raw_key(a.ids, a.id_bytes, a.bag, a.stride, a.vocab, e);
     if (k == kSentinel) continue;  // the gather flags it
-    const int l = a.last[k];
-    // nothing to replay, or a row never stepped (m = v = 0: with weight_decay == 0 the replay is
+    // the row's state steps (moments, parameters) as one 64-bit word: the compare-and-swap moves
+    // both together
+    unsigned long long* lw = reinterpret_cast<unsigned long long*>(a.last) + k;
+    const unsigned long long old = *lw;
+    const int lm = (int)(uint32_t)old, lp = (int)(uint32_t)(old >> 32);
+    // p already current, or a row never stepped (m = v = 0: with weight_decay == 0 the replay is
     // the identity, exactly)
-    if (l + 1 > t || (l == 0 && a.h.wd == 0.f)) continue;
+    if (lp >= t || (lm == 0 && a.h.wd == 0.f)) continue;
+    const bool p_only = a.h.wd == 0.f;  // as sorted_rows_body's catch-up: p written alone
+    const unsigned long long nw = ((unsigned long long)(uint32_t)t << 32) | (uint32_t)(p_only ? lm : t);
     int won = 0;
-    if (gl == 0) won = atomicCAS(&a.last[k], l, t) == l;
+    if (gl == 0) won = atomicCAS(lw, old, nw) == old;
     won = __shfl(won, 0, G);
     if (!won || w == 0) continue;
     const int64_t o = (int64_t)k * a.D + c0;
@@ -566,22 +571,26 @@ __global__ __launch_bounds__(256) void lookup_catchup_kernel(IdCatchArgs a) {
       pp[0] = p4.x; pp[1] = p4.y; pp[2] = p4.z; pp[3] = p4.w;
       mm[0] = m4.x; mm[1] = m4.y; mm[2] = m4.z; mm[3] = m4.w;
       vv[0] = v4.x; vv[1] = v4.y; vv[2] = v4.z; vv[3] = v4.w;
-    } else {
-      for (int j = 0; j < w; ++j) { pp[j] = a.p[o + j]; mm[j] = a.m[o + j]; vv[j] = a.v[o + j]; }
-    }
-    if (w == 4) {
-      adam_replay_zero<4>(a.h, a.consts, l + 1, t, pp, mm, vv);
-    } else {
+    } else {  // D % 4 != 0: columns past w are zeros (they stay put)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (j < w) replay(a.h, a.consts, l + 1, t, pp[j], mm[j], vv[j]);
+      for (int j = 0; j < 4; ++j) {
+        pp[j] = j < w ? a.p[o + j] : 0.f;
+        mm[j] = j < w ? a.m[o + j] : 0.f;
+        vv[j] = j < w ? a.v[o + j] : 0.f;
+      }
     }
+    adam_catch_row<4>(a.h, a.consts, lm, lp, t, pp, mm, vv);
     if (vec) {
       *reinterpret_cast<float4*>(a.p + o) = make_float4(pp[0], pp[1], pp[2], pp[3]);
-      *reinterpret_cast<float4*>(a.m + o) = make_float4(mm[0], mm[1], mm[2], mm[3]);
-      *reinterpret_cast<float4*>(a.v + o) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      if (!p_only) {
+        *reinterpret_cast<float4*>(a.m + o) = make_float4(mm[0], mm[1], mm[2], mm[3]);
+        *reinterpret_cast<float4*>(a.v + o) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      }
     } else {
-      for (int j = 0; j < w; ++j) { a.p[o + j] = pp[j]; a.m[o + j] = mm[j]; a.v[o + j] = vv[j]; }
+      for (int j = 0; j < w; ++j) {
+        a.p[o + j] = pp[j];
+        if (!p_only) { a.m[o + j] = mm[j]; a.v[o + j] = vv[j]; }
+      }
     }
   }
 }

@@ -159,8 +159,56 @@ __global__ __launch_bounds__(256) void nan_check_kernel(const float* __restrict_
     bad |= x[i] != x[i];
   if (__ballot(bad) != 0 && (threadIdx.x & 63) == 0) atomicOr(flag, bit);
 }
+
+// up to 4 tensors in one launch (the loss's U, I, H): workgroup b checks tensor i of block range
+// [first[i], first[i + 1])
+struct NanList {
+  const float* x[4];
+  int64_t n[4];
+  int bit[4];
+  int first[5];
+  int k;
+};
+
+__global__ __launch_bounds__(256) void nan_check_many_kernel(NanList l, int* __restrict__ flag) {
+  int i = 0;
+  while (i + 1 < l.k && (int)blockIdx.x >= l.first[i + 1]) ++i;
+  const int b = blockIdx.x - l.first[i], nb = l.first[i + 1] - l.first[i];
+  const float* x = l.x[i];
+  const int64_t n = l.n[i];
+  bool bad = false;
+  const int64_t n4 = n / 4;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (int64_t j = (int64_t)b * 256 + threadIdx.x; j < n4; j += (int64_t)nb * 256) {
+    const float4 v = x4[j];
+    bad |= (v.x != v.x) | (v.y != v.y) | (v.z != v.z) | (v.w != v.w);
+  }
+  for (int64_t j = n4 * 4 + (int64_t)b * 256 + threadIdx.x; j < n; j += (int64_t)nb * 256) bad |= x[j] != x[j];
+  if (__ballot(bad) != 0 && (threadIdx.x & 63) == 0) atomicOr(flag, l.bit[i]);
+}
 }  // namespace
 }  // namespace rs
+
+extern "C" int rs_nan_check_many(int k, const float* const* x, const int64_t* n, const int* bits, int* flag,
+                                 void* stream) {
+  RS_CHECK_ARG(k >= 1 && k <= 4 && x && n && bits && flag, "rs_nan_check_many: bad args (k=%d)", k);
+  rs::NanList l{};
+  l.k = k;
+  int wg = 0;
+  for (int i = 0; i < k; ++i) {
+    RS_CHECK_ARG(x[i] && n[i] >= 0 && rs::aligned16(x[i]), "rs_nan_check_many: tensor %d: bad args", i);
+    l.x[i] = x[i];
+    l.n[i] = n[i];
+    l.bit[i] = bits[i];
+    l.first[i] = wg;
+    int blocks = rs::cdiv(n[i] / 4 + 1, 256);
+    wg += blocks > 512 ? 512 : blocks;
+  }
+  l.first[k] = wg;
+  rs::nan_check_many_kernel<<<wg, 256, 0, rs::as_stream(stream)>>>(l, flag);
+  RS_CHECK_LAUNCH("rs_nan_check_many");
+  return 0;
+}
 
 extern "C" int rs_nan_check(const float* x, int64_t n, int* flag, int bit, void* stream) {
   RS_CHECK_ARG(x && flag && n >= 0 && rs::aligned16(x), "rs_nan_check: bad args");

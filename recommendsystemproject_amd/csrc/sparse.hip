@@ -51,15 +51,15 @@ __global__ void flush_kernel(float* __restrict__ p, float* __restrict__ m, float
   const int target = clamp_step(consts, *step);
   const int lane = threadIdx.x & 63;
   for (int64_t row = blockIdx.x * 4 + (threadIdx.x >> 6); row < V; row += (int64_t)gridDim.x * 4) {
-    const int from = last[row] + 1;
-    if (from > target) continue;
+    const int2 l2 = reinterpret_cast<const int2*>(last)[row];  // (moments' step, parameters' step)
+    if (l2.x >= target) continue;
     for (int c = lane; c < D; c += 64) {
       const int64_t o = row * D + c;
       float pp = p[o], mm = m[o], vv = v[o];
-      adam_replay_zero<1>(h, consts, from, target, &pp, &mm, &vv);
+      adam_catch_row<1>(h, consts, l2.x, l2.y, target, &pp, &mm, &vv);
       p[o] = pp; m[o] = mm; v[o] = vv;
     }
-    if (lane == 0) last[row] = target;
+    if (lane == 0) reinterpret_cast<int2*>(last)[row] = make_int2(target, target);
   }
 }
 

@@ -803,7 +803,15 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
 // feature_bn's input statistics: tile (mean, M2) per column of x [G*Bg, C] over TM_STATS rows,
 // handed to the last arriver of each (group, 64-column block) like a GEMM epilogue's
 __global__ __launch_bounds__(256) void tower_stats_kernel(const float* __restrict__ x, int Bg,
-                                                          int C, int G, int tiles, Fin fin) {
+                                                          int C, int G, int tiles, Fin fin,
+                                                          int64_t* __restrict__ rng_state,
+                                                          int64_t* __restrict__ key_out) {
+  // the MLP's dropout key of this step (rs_rng_next folded in: one dependent launch less)
+  if (rng_state && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    key_out[0] = rng_state[0];
+    key_out[1] = rng_state[1];
+    rng_state[1] = rng_state[1] + 1;
+  }
   constexpr int R = TM_STATS / 4;  // rows per thread
   __shared__ float red[4][64];
   __shared__ float tmean[64];
@@ -1072,8 +1080,9 @@ extern "C" int rs_tower_sync_ints(int G, int N) { return (G + 1) * cdiv(N, 64); 
 extern "C" int rs_tower_stats(const float* x, int G, int Bg, int C, float* part, int* sync,
                               double* scratch, float* mean, float* rstd, float* running_mean,
                               float* running_var, int64_t* num_batches, float momentum, float eps,
-                              void* stream) {
+                              int64_t* rng_state, int64_t* key_out, void* stream) {
   RS_CHECK_ARG(x && part && sync && scratch && mean && rstd, "rs_tower_stats: null pointer");
+  RS_CHECK_ARG(!rng_state == !key_out, "rs_tower_stats: rng_state and key_out come together");
   RS_CHECK_ARG(G >= 1 && Bg >= 1 && C >= 1, "rs_tower_stats: bad shape G=%d Bg=%d C=%d", G, Bg, C);
   RS_CHECK_ARG(!running_mean == !running_var, "rs_tower_stats: running stats must come together");
   Fin f{};
@@ -1081,7 +1090,8 @@ extern "C" int rs_tower_stats(const float* x, int G, int Bg, int C, float* part,
   f.run_mean = running_mean; f.run_var = running_var; f.nbt = num_batches;
   f.momentum = momentum; f.eps = eps; f.bwd = 0; f.nb = cdiv(C, 64);
   const int tiles = cdiv(Bg, TM_STATS);
-  tower_stats_kernel<<<dim3(f.nb, G * tiles), 256, 0, as_stream(stream)>>>(x, Bg, C, G, tiles, f);
+  tower_stats_kernel<<<dim3(f.nb, G * tiles), 256, 0, as_stream(stream)>>>(x, Bg, C, G, tiles, f, rng_state,
+                                                                          key_out);
   RS_CHECK_LAUNCH("rs_tower_stats");
   return 0;
 }

@@ -116,7 +116,8 @@ class LazyTable:
         self.shard = shard  # (world, rank) of a row-sharded table, else None
         self.V_full = int(vocab) if vocab is not None else self.V
         dev = param.device
-        self.last = torch.zeros(self.V, dtype=torch.int32, device=dev)
+        # (moments' step, parameters' step) per row: the forward catch-up may bring p alone ahead
+        self.last = torch.zeros(self.V, 2, dtype=torch.int32, device=dev)
         self.owner = None   # [V] lowest call index per row; allocated for multi-call steps
         self.calls = []     # this step's LookupCalls, in forward order
         self.exchanged = None  # data parallel: the union calls that replaced the local ones

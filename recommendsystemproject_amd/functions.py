@@ -762,7 +762,8 @@ class TowerChainFn(torch.autograd.Function):
         seq = mlp.mlp
         n_hidden = (len(seq) - 1) // 4
         p = mlp.dropout_p
-        key = ops.rng_next(mlp.rng_state) if p > 0 else None
+        # the dropout key is drawn by rs_tower_stats (rs_rng_next folded into its launch)
+        key = torch.empty(2, dtype=torch.int64, device=x.device) if p > 0 else None
         bf = int(precision.compute_dtype() == 'bf16')
         x = x.contiguous()
         dev = x.device
@@ -788,7 +789,8 @@ class TowerChainFn(torch.autograd.Function):
                 (part, scr, mean, rstd)
 
         hf, keep = handoff(widths[0], 0, feature_bn, 0)
-        ops.call('rs_tower_stats', x.data_ptr(), G, Bg, widths[0], *hf, ops.stream())
+        ops.call('rs_tower_stats', x.data_ptr(), G, Bg, widths[0], *hf, ops.P(mlp.rng_state) if p > 0 else None,
+                 ops.P(key), ops.stream())
         A, bn, relu, dp, site = x, feature_bn, 0, 0.0, 0
         mean, rstd = keep[2], keep[3]
         layers = []

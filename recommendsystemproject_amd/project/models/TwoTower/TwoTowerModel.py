@@ -41,6 +41,19 @@ class TwoTowerModel(nn.Module):
             self._rs_side_stream = s
         return s
 
+    def _user_stream(self, dev):
+        """RSYS_USER_STREAM_PRIORITY=1: the user tower (the step's critical path at C3: the history
+        table's sort and catch-up, then its tower) on a high-priority stream of its own, so the
+        item tower's kernels beside it do not delay its dispatches."""
+        if os.environ.get('RSYS_USER_STREAM_PRIORITY', '0') != '1':
+            return None
+        s = getattr(self, '_rs_user_stream', None)
+        if s is None or s.device != dev:
+            lo, hi = torch.cuda.Stream.priority_range()
+            s = torch.cuda.Stream(device=dev, priority=hi)
+            self._rs_user_stream = s
+        return s
+
     def forward(self, batch_data):
         """-> (user_emb [B,D], item_emb [B,D], hard_neg_emb [B,N,D] or None) (TwoTowerModel.py:35-62;
         T13: one item-tower pass per hard-negative slot, so BatchNorm statistics are per slot)."""
@@ -59,26 +72,47 @@ class TwoTowerModel(nn.Module):
         side.wait_stream(main)
         with torch.cuda.stream(side):
             item_emb, hard_neg_emb = self._item_side(batch_data)
-        user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
+        ustream = self._user_stream(dev)
+        if ustream is not None:
+            ustream.wait_stream(main)
+            with torch.cuda.stream(ustream):
+                user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
+            main.wait_stream(ustream)
+            user_emb.record_stream(main)
+        else:
+            user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
         main.wait_stream(side)
         outs = [t for t in (item_emb, hard_neg_emb) if t is not None]
         for t in outs:
             t.record_stream(main)  # made on the side stream, read by the loss on the main one
         if torch.is_grad_enabled() and item_emb.requires_grad:
-            joined = []
+            self._join_backward(main, [(side, outs)] + ([(ustream, [user_emb])] if ustream is not None else []))
+        return user_emb, item_emb, hard_neg_emb
 
-            def _to_side(g):
-                # the loss's gradient (main stream) is read by the item tower's backward (side);
-                # once per backward, the main stream waits for the side stream's last kernels
-                g.record_stream(side)
+    @staticmethod
+    def _join_backward(main, branches):
+        """The loss's gradient (main stream) is read by each tower's backward on its own stream; the
+        backward kernels write the flat gradient directly (no AccumulateGrad to synchronise on),
+        so once per backward the main stream waits for every branch stream's last kernels."""
+        joined = []
+
+        def hook_for(st):
+            def _to(g):
+                g.record_stream(st)
                 if not joined:
                     joined.append(True)
-                    torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_stream(side))
-                return g
 
-            for t in outs:
-                t.register_hook(_to_side)
-        return user_emb, item_emb, hard_neg_emb
+                    def _join():
+                        for s, _ in branches:
+                            main.wait_stream(s)
+                    torch.autograd.Variable._execution_engine.queue_callback(_join)
+                return g
+            return _to
+
+        for st, ts in branches:
+            for t in ts:
+                if t.requires_grad:
+                    t.register_hook(hook_for(st))
 
     def _item_side(self, batch_data):
         item_emb = self.item_tower(batch_data['item_tower'], self.item_feature_mapping)
@@ -108,15 +142,25 @@ class TwoTowerModel(nn.Module):
     _NAN_MSG = {1: 'Found NaN in User Embedding', 2: 'Found NaN in Item Embedding',
                 4: 'Found NaN in Hard Negative Embedding'}
 
-    def _flag_nan(self, t, bit):
-        if t.is_cuda and not t.is_contiguous() and t.dim() == 3 and t.transpose(0, 1).is_contiguous():
-            t = t.transpose(0, 1)  # the grouped hard-negative pass's [B, N, D] view of [N, B, D]
-        if not t.is_cuda or not t.is_contiguous() or t.data_ptr() % 16:
-            t = t.contiguous()
-        if self.nan_flag.device != t.device:
-            self.nan_flag = self.nan_flag.to(t.device)
-        _hip.call('rs_nan_check', t.data_ptr(), t.numel(), self.nan_flag.data_ptr(), bit,
-                  torch.cuda.current_stream(t.device).cuda_stream)
+    def _flag_nan(self, pairs):
+        """One rs_nan_check_many launch over [(tensor, bit)] (the loss inputs)."""
+        import ctypes as C
+        ts, bits = [], []
+        for t, bit in pairs:
+            if t.is_cuda and not t.is_contiguous() and t.dim() == 3 and t.transpose(0, 1).is_contiguous():
+                t = t.transpose(0, 1)  # the grouped hard-negative pass's [B, N, D] view of [N, B, D]
+            if not t.is_cuda or not t.is_contiguous() or t.data_ptr() % 16:
+                t = t.contiguous()
+            ts.append(t)
+            bits.append(bit)
+        if self.nan_flag.device != ts[0].device:
+            self.nan_flag = self.nan_flag.to(ts[0].device)
+        k = len(ts)
+        xs = (C.c_void_p * k)(*[t.data_ptr() for t in ts])
+        ns = (C.c_int64 * k)(*[t.numel() for t in ts])
+        bs = (C.c_int * k)(*bits)
+        _hip.call('rs_nan_check_many', k, C.addressof(xs), C.addressof(ns), C.addressof(bs),
+                  self.nan_flag.data_ptr(), torch.cuda.current_stream(ts[0].device).cuda_stream)
 
     def check_errors(self):
         """Raise what the reference would have raised since the last check: RuntimeError for NaN
@@ -160,10 +204,8 @@ class TwoTowerModel(nn.Module):
     def compute_loss(self, user_emb, item_emb, item_ids=None, hard_neg_emb=None, temperature=0.1):
         """In-batch softmax loss (TwoTowerModel.py:81-150)."""
         if not self.check_nan and user_emb.is_cuda and not library.is_fake(user_emb):
-            self._flag_nan(user_emb.detach(), 1)
-            self._flag_nan(item_emb.detach(), 2)
-            if hard_neg_emb is not None:
-                self._flag_nan(hard_neg_emb.detach(), 4)
+            self._flag_nan([(user_emb.detach(), 1), (item_emb.detach(), 2)] +
+                           ([(hard_neg_emb.detach(), 4)] if hard_neg_emb is not None else []))
         if self.check_nan:
             if torch.isnan(user_emb).any():
                 raise RuntimeError('Found NaN in User Embedding')

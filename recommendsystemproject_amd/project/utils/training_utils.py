@@ -55,6 +55,19 @@ def build_user_history(train_df, user_col='user_id_enc', item_col='movie_id_enc'
     return user_history
 
 
+_ONES = {}
+
+
+def backward_seed(loss):
+    """A persistent device 1.0 to seed loss.backward() with: autograd's implicit ones_like(loss) is
+    a fill launch per step on the step's critical path."""
+    key = (loss.device, loss.dtype)
+    one = _ONES.get(key)
+    if one is None:
+        one = _ONES[key] = torch.ones((), device=loss.device, dtype=loss.dtype)
+    return one
+
+
 def train_step(model, batch_data, optimizer, max_grad_norm=1.0, temperature=0.1,
                item_id_feature='movie_id_enc', item_id_type='sparse'):
     """One training step on a device-resident batch; returns the loss as a device scalar."""
@@ -63,7 +76,7 @@ def train_step(model, batch_data, optimizer, max_grad_norm=1.0, temperature=0.1,
     ids = extract_item_id(batch_data['item_tower'], feature_name=item_id_feature, feature_type=item_id_type)
     loss = model.compute_loss(user_emb, pos_item_emb, hard_neg_emb=hard_neg_emb, item_ids=ids,
                               temperature=temperature)
-    loss.backward()
+    loss.backward(backward_seed(loss))
     rdist.allreduce_gradients(model, optimizer)
     if isinstance(optimizer, Adam):
         optimizer.step(clip_max_norm=max_grad_norm if max_grad_norm > 0 else None)

@@ -195,7 +195,7 @@ def test_lazy_adam_bitwise_equals_dense(D, wd, clip, calls, catch):
     pd, md, vd = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
     pl, ml, vl = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
     gl = torch.zeros_like(p0)
-    last = torch.zeros(V, dtype=torch.int32, device=DEV)
+    last = torch.zeros(V, 2, dtype=torch.int32, device=DEV)  # (moments' step, parameters' step)
     owner = torch.full((V,), 0x7fffffff, dtype=torch.int32, device=DEV)
     step_d = torch.zeros((), dtype=torch.int64, device=DEV)
     step_l = torch.zeros((), dtype=torch.int64, device=DEV)
@@ -284,7 +284,7 @@ def test_consts_overflow_clamped():
     V, D = 10, 8
     p = torch.randn(V, D, device=DEV)
     m, v = torch.ones_like(p), torch.ones_like(p)
-    last = torch.zeros(V, dtype=torch.int32, device=DEV)
+    last = torch.zeros(V, 2, dtype=torch.int32, device=DEV)  # (moments' step, parameters' step)
     _hip.call('rs_sparse_flush', p.data_ptr(), m.data_ptr(), v.data_ptr(), last.data_ptr(), V, D,
               step.data_ptr(), consts.data_ptr(), B1, B2, EPS, 0.0, ops.stream())
     assert int(last.max().item()) == cap - 1

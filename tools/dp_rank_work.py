@@ -37,7 +37,9 @@ class Table:
         self.m = torch.randn(V, D, device=DEV, generator=gen) * 1e-3
         self.v = torch.rand(V, D, device=DEV, generator=gen) * 1e-6
         self.g = torch.zeros(V, D, device=DEV)
-        self.last0 = torch.randint(T_STEP - 7, T_STEP, (V,), device=DEV, generator=gen, dtype=torch.int32)
+        # last[V][2] = (moments' step, parameters' step), both the row's last Adam step here
+        self.last0 = torch.randint(T_STEP - 7, T_STEP, (V, 1), device=DEV, generator=gen,
+                                   dtype=torch.int32).expand(V, 2).contiguous()
         self.last = self.last0.clone()
 
 

@@ -66,7 +66,7 @@ def main():
     m = torch.randn(V, D, device=dev) * 1e-3
     v = torch.rand(V, D, device=dev) * 1e-6
     gr = torch.zeros(V, D, device=dev)
-    last = torch.zeros(V, dtype=torch.int32, device=dev)
+    last = torch.zeros(V, 2, dtype=torch.int32, device=dev)  # (moments' step, parameters' step)
     cap = 4096
     consts = torch.zeros(cap, 2, device=dev)
     consts.view(torch.int32)[0, 0] = cap
