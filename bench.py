@@ -352,7 +352,8 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
             batch['hard_negatives'] = catalog.materialize(neg_ids)
         U, I, H = model(batch)
         loss = model.compute_loss(U, I, item_ids=ids, hard_neg_emb=H, temperature=T)
-        loss.backward(backward_seed(loss))
+        with rdist.overlap(model):  # N > 1: each tower's all-reduce starts inside the backward
+            loss.backward(backward_seed(loss))
         return loss
 
     def opt_step():
@@ -401,6 +402,12 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
                               'run': run_key(args, B, name, dtype, zipf, hard_negatives)}))
         return None
     graphs = None
+    # N > 1 (RCCL): the gradient all-reduce and the large tables' exchange are captured with the
+    # backward -- their host-side bookkeeping (this step's lookup calls, the buckets started in
+    # the backward) runs once, at capture, and every replay re-runs all of their collectives.
+    # Host-staged gloo collectives (ranks sharing one GPU) cannot be captured: eager steps.
+    if world > 1 and dist.get_backend() != 'nccl':
+        args.no_graph = True
     if not args.no_graph:
         try:
             s = torch.cuda.Stream()
@@ -415,6 +422,7 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
             # this thread captures; a global-mode capture would be invalidated by those queries
             with torch.cuda.graph(g1, capture_error_mode='thread_local'):
                 loss_static = fwd_bwd()
+                allreduce()
             with torch.cuda.graph(g2, capture_error_mode='thread_local'):
                 opt_step()
             graphs = (g1, g2, loss_static)
@@ -426,7 +434,6 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
         next_batch()
         if graphs is not None:
             graphs[0].replay()
-            allreduce()
             graphs[1].replay()
             return graphs[2]
         loss = fwd_bwd()

@@ -1,8 +1,11 @@
 """Data parallelism over RCCL (torch.distributed 'nccl' backend = RCCL on ROCm), one process
 per GPU. The batch is sharded: each rank runs the full training step on its own
 B samples (own in-batch negatives, own BatchNorm statistics, as DDP applied to the reference),
-then ONE all-reduce of the flat gradient buffer (all parameters, ~3.5 MB for the demo schema)
-and an identical clip + Adam on every rank. Parameters are broadcast from rank 0 at start.
+then an all-reduce of the flat gradient buffer's dense part (~3.5 MB for the demo schema, 0.9 MB
+at C3) and an identical clip + Adam on every rank. Parameters are broadcast from rank 0 at start.
+The all-reduce is bucketed per tower and started inside the backward (GradBuckets, `overlap`):
+each tower's bucket goes as soon as its last gradient writer has queued its kernels, so it
+runs under the other tower's backward and the large-table segment sums.
 
 Below W = 4, large tables trained by lazy-exact Adam (flat.py) stay replicated (a 10M x 128 table
 with its Adam state is ~20 GB: it fits 288 GB of HBM many times over) but their gradient is NOT
@@ -129,20 +132,165 @@ def allreduce_flat_grad(flat_grad: torch.Tensor):
     dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM)
 
 
+class GradBuckets:
+    """The dense part of a flat gradient [0, dense_numel) split into buckets, one per tower: a
+    tower's non-lazy parameters are contiguous in the flat buffer (module.parameters() order).
+    Every op that writes a bucket's gradient in the backward registers itself in its forward
+    (`note_writer`) and reports in its backward once its dense-gradient kernels are queued
+    (`note_writer(..., written=True)`), before any large-table work. While armed (`overlap`), the last writer of a
+    bucket starts the bucket's all-reduce asynchronously: RCCL's stream waits for the writer's
+    stream and the all-reduce runs while the rest of the backward (the other tower, the
+    large-table sort / segment sums) does. allreduce_gradients then only waits for those
+    and all-reduces what no writer covered. The launch order is the autograd engine's node order,
+    the same on every rank (same graph), so the ranks' collectives match."""
+
+    def __init__(self, f, spans):
+        self.f = f
+        self.spans = spans       # [(lo, hi)] per bucket, disjoint, inside [0, dense_numel)
+        self.pending = [0] * len(spans)
+        self.armed = 0
+        self.works = []          # (bucket, async work) launched in this backward
+        self.launched = 0        # buckets started inside a backward, all steps (tests)
+
+    def reset(self):
+        self.pending = [0] * len(self.spans)
+        self.works = []
+
+    def _launch(self, b):
+        lo, hi = self.spans[b]
+        self.launched += 1
+        self.works.append((b, dist.all_reduce(self.f.grad[lo:hi], op=dist.ReduceOp.SUM, async_op=True)))
+
+    def writer(self, params, delta):
+        b = _bucket_of(params)
+        if b is None:
+            return
+        if delta > 0 and any(w[0] == b for w in self.works):
+            # a second forward before allreduce_gradients: its gradient would be added after
+            # the bucket's all-reduce (gradient accumulation needs the backward outside overlap)
+            raise RuntimeError('rsys data parallel: a forward writing an already all-reduced gradient '
+                               'bucket (call allreduce_gradients after each backward run under '
+                               'dist.overlap)')
+        self.pending[b] += delta
+        if delta < 0 and self.pending[b] == 0 and self.armed and all(w[0] != b for w in self.works):
+            self._launch(b)
+
+    def finish(self):
+        """Wait (stream order) for the buckets launched in the backward; -> their spans."""
+        done = []
+        for b, w in self.works:
+            w.wait()
+            done.append(self.spans[b])
+        self.reset()
+        return done
+
+
+def _bucket_of(params):
+    for p in params:
+        b = getattr(p, '_rs_dp_bucket', None)
+        if b is not None:
+            return b
+    return None
+
+
+def setup_buckets(model: torch.nn.Module, groups) -> GradBuckets | None:
+    """One gradient bucket per module of `groups` (the towers) over the model's flat buffer;
+    None if a group's dense parameters do not form one span of their own."""
+    f = flat_of(next(model.parameters()))
+    if f is None:
+        return None
+    gb = getattr(f, 'dp_buckets', None)
+    if gb is not None or getattr(f, 'dp_buckets_tried', False):
+        return gb
+    f.dp_buckets_tried = True
+    lazy = {id(t.param) for t in f.lazy}
+    off = {id(p): (o, o + p.numel()) for p, o in zip(f.params, f.offsets)}
+    owner, spans = {}, []
+    for b, m in enumerate(groups):
+        ps = [p for p in m.parameters() if id(p) not in lazy and id(p) in off]
+        if not ps or any(id(p) in owner for p in ps):
+            return None
+        for p in ps:
+            owner[id(p)] = b
+        spans.append((min(off[id(p)][0] for p in ps), max(off[id(p)][1] for p in ps)))
+    # a span may hold no other group's (or ungrouped) parameter: its all-reduce would sum a
+    # gradient some other writer is still producing
+    for p in f.params:
+        if id(p) in lazy:
+            continue
+        lo, hi = off[id(p)]
+        for b, (s0, s1) in enumerate(spans):
+            if lo < s1 and hi > s0 and owner.get(id(p)) != b:
+                return None
+    for p in f.params:
+        if id(p) in owner:
+            p._rs_dp_bucket = owner[id(p)]
+    f.dp_buckets = GradBuckets(f, spans)
+    return f.dp_buckets
+
+
+def note_writer(params, written=False):
+    """Forward (written=False) / backward (written=True) of an op writing dense gradients of
+    `params` (GradBuckets). No-op without data parallelism or buckets."""
+    if not params:
+        return
+    f = flat_of(params[0])
+    gb = getattr(f, 'dp_buckets', None) if f is not None else None
+    if gb is not None:
+        gb.writer(params, -1 if written else 1)
+
+
+class overlap:
+    """`with overlap(model): loss.backward()` -- start each tower's gradient all-reduce inside
+    the backward (GradBuckets). allreduce_gradients must follow, as without it."""
+
+    def __init__(self, model):
+        f = flat_of(next(model.parameters())) if is_active() else None
+        self.gb = getattr(f, 'dp_buckets', None) if f is not None else None
+        if os.environ.get('RSYS_DP_OVERLAP', '1') == '0':
+            self.gb = None
+        elif (self.gb is not None and dist.get_backend() != 'nccl' and torch.cuda.is_available()
+              and torch.cuda.is_current_stream_capturing()):
+            self.gb = None  # host-staged collectives (gloo) cannot be captured
+
+    def __enter__(self):
+        if self.gb is not None:
+            self.gb.armed += 1
+        return self
+
+    def __exit__(self, *exc):
+        if self.gb is not None:
+            self.gb.armed -= 1
+        return False
+
+
+def _complement(n, spans):
+    out, at = [], 0
+    for lo, hi in sorted(spans):
+        if lo > at:
+            out.append((at, lo))
+        at = max(at, hi)
+    if at < n:
+        out.append((at, n))
+    return out
+
+
 def allreduce_gradients(model: torch.nn.Module, optimizer=None):
-    """After backward: one RCCL all-reduce of the model's flat gradient; the optimizer scales by
-    1/world (so clip + Adam see the average gradient, as DDP)."""
+    """After backward: RCCL all-reduce of the model's flat gradient -- the buckets the backward
+    started (overlap) are waited for, the rest is reduced here, in as few calls as it spans;
+    the optimizer scales by 1/world (so clip + Adam see the average gradient, as DDP)."""
     if not is_active():
         return
     params = list(model.parameters())
     f = flat_of(params[0])
     if f is None:
         raise RuntimeError('model is not flattened')
+    gb = getattr(f, 'dp_buckets', None)
+    done = gb.finish() if gb is not None else []
+    for lo, hi in _complement(f.dense_numel, done):
+        allreduce_flat_grad(f.grad[lo:hi])
     if f.lazy:
-        allreduce_flat_grad(f.grad[:f.dense_numel])
         exchange_lazy_grads(f)
-    else:
-        allreduce_flat_grad(f.grad)
     from .optim import Adam
     world = dist.get_world_size()
     if isinstance(optimizer, Adam):

@@ -24,6 +24,7 @@ import torch
 from torch.autograd.function import once_differentiable
 
 from . import _hip, ops, precision
+from . import dist as _dp
 from .flat import SEG_MEAN, SEG_ONE, SEG_SUM, flat_of, grad_of, lookup_table
 
 
@@ -152,12 +153,14 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
     return calls, lazy
 
 
-def _grad_lazy(segs, calls, dout, tables):
-    """Backward of the large-table segments: rs_segsum per call (deterministic, no atomics).
-    Returns the segments left for rs_gather_bwd (ordinary tables, dense, copies, and max-pooled
-    large tables, whose arg-max gradient keeps the atomic scatter)."""
+def _grad_tables(segs, calls, dout, tables, rows, params=()):
+    """Backward of a gather: the ordinary segments (ordinary tables, dense, copies, and max-pooled
+    large tables, whose arg-max gradient keeps the atomic scatter) through rs_gather_bwd first;
+    then -- the op's dense gradients all queued, its data-parallel bucket may start its
+    all-reduce (dist.GradBuckets) -- the large-table segments: rs_segsum per call (deterministic,
+    no atomics)."""
     from .flat import _dp_active
-    rest = []
+    rest, big = [], []
     dp = _dp_active()
     for i, s in enumerate(segs):
         c = calls.get(i) if calls else None
@@ -171,10 +174,14 @@ def _grad_lazy(segs, calls, dout, tables):
         # under data parallelism a call only keeps its output gradient rows here (rs_pack_rows,
         # any alignment / row stride); the exchange segment-sums every rank's
         if sharded or (c is not None and c.mode >= 0 and (dp or (ptr % 16 == 0 and dout.stride(0) % 4 == 0))):
-            tables[i]._rs_lazy.segsum(c, ptr, dout.stride(0))
+            big.append((tables[i]._rs_lazy, c, ptr))
         else:
             rest.append(s)
-    return rest
+    if rest:
+        ops.gather_bwd(rest, rows, dout)
+    _dp.note_writer(params, written=True)
+    for t, c, ptr in big:
+        t.segsum(c, ptr, dout.stride(0))
 
 
 # ================================================================================ sequence input
@@ -238,8 +245,9 @@ def seq_input_fwd(proc, seqd, B, L, p, key, err, need=True):
     return x, (segs, tables, cat, keep, calls)
 
 
-def seq_input_bwd(proc, saved, dx, B, L, p, key):
-    """Backward of seq_input_fwd; dx [B*L, d] is consumed (modified in place)."""
+def seq_input_bwd(proc, saved, dx, B, L, p, key, params=()):
+    """Backward of seq_input_fwd; dx [B*L, d] is consumed (modified in place). `params`: the
+    calling op's parameters (its data-parallel bucket, dist.GradBuckets)."""
     segs, tables, cat, _, calls = saved
     d = proc.target_dim
     pos_g = grad_of(proc.pos_emb.weight)
@@ -258,9 +266,7 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key):
     dcat = ops.linear_bwd_input(dx, lin.weight)
     for s, t in zip(segs, tables):
         s.grad = grad_of(t).data_ptr()
-    rest = _grad_lazy(segs, calls, dcat, tables)
-    if rest:
-        ops.gather_bwd(rest, B * L, dcat)
+    _grad_tables(segs, calls, dcat, tables, B * L, params)
 
 
 # ================================================================================ encoder layer
@@ -445,6 +451,8 @@ class SeqEncoderFn(torch.autograd.Function):
             ctx.enc, ctx.B, ctx.L, ctx.p = enc, B, L, p
             ctx.key, ctx.key_pad, ctx.last = key, key_pad, last
             ctx.in_saved, ctx.layer_saved, ctx.layers = in_saved, saved, layers
+            ctx.params = params
+            _dp.note_writer(params)
         return out
 
     @staticmethod
@@ -467,8 +475,8 @@ class SeqEncoderFn(torch.autograd.Function):
         for i in reversed(range(n)):
             dx = layer_bwd(ctx.layers[i], ctx.layer_saved[i], dx, ctx.key_pad, B, L, d, H, p, key,
                            _layer_site(i))
-        seq_input_bwd(proc, ctx.in_saved, dx, B, L, p, key)
-        ctx.layer_saved = ctx.in_saved = None
+        seq_input_bwd(proc, ctx.in_saved, dx, B, L, p, key, ctx.params)
+        ctx.layer_saved = ctx.in_saved = ctx.params = None
         return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
 
@@ -579,6 +587,8 @@ class TowerFeatureFn(torch.autograd.Function):
             ctx.segs, ctx.pp, ctx.keep, ctx.B, ctx.calls = segs, pp, keep, B, calls
             ctx.has_seq = seq_vec is not None
             ctx.seq_shape = tuple(seq_vec.shape) if seq_vec is not None else None
+            ctx.params = params
+            _dp.note_writer(params)
         return out
 
     @staticmethod
@@ -596,10 +606,8 @@ class TowerFeatureFn(torch.autograd.Function):
             dseq = torch.empty(ctx.seq_shape, device=dout.device, dtype=torch.float32)
             segs[-1].grad = dseq.data_ptr()
         tables = [w for w, _ in ctx.pp] + [None] * (len(segs) - n_feat)
-        rest = _grad_lazy(segs, ctx.calls, dout, tables)
-        if rest:
-            ops.gather_bwd(rest, ctx.B, dout)
-        ctx.segs = ctx.keep = ctx.calls = None
+        _grad_tables(segs, ctx.calls, dout, tables, ctx.B, ctx.params)
+        ctx.segs = ctx.keep = ctx.calls = ctx.params = None
         return (None, None, None, None, dseq) + (None,) * (len(ctx.needs_input_grad) - 5)
 
 
@@ -615,6 +623,8 @@ class BatchNormFn(torch.autograd.Function):
         if need:
             ctx.bn, ctx.G, ctx.x, ctx.mean, ctx.rstd = bn, G, x, mean, rstd
             ctx.training = bn.training
+            ctx.params = params
+            _dp.note_writer(params)
         return y
 
     @staticmethod
@@ -625,6 +635,7 @@ class BatchNormFn(torch.autograd.Function):
         bn = ctx.bn
         dx = ops.batchnorm_bwd(ctx.x, None, dy.contiguous(), bn.weight, ctx.mean, ctx.rstd,
                                grad_of(bn.weight), grad_of(bn.bias), ctx.G, relu=False)
+        _dp.note_writer(ctx.params, written=True)
         return (None, None, dx, None) + (None,) * (len(ctx.needs_input_grad) - 4)
 
 
@@ -661,6 +672,8 @@ class MLPFn(torch.autograd.Function):
             ctx.mlp, ctx.G, ctx.p, ctx.key = mlp, G, p, key
             ctx.saved, ctx.h_last, ctx.out, ctx.norm = saved, h, out, norm
             ctx.training = mlp.training
+            ctx.params = params
+            _dp.note_writer(params)
         return out
 
     @staticmethod
@@ -684,6 +697,7 @@ class MLPFn(torch.autograd.Function):
             _tower_wgrad(dz, h, lin)
             dh = ops.linear_bwd_input(dz, lin.weight)
         ctx.saved = None
+        _dp.note_writer(ctx.params, written=True)
         return (None, None, dh, None) + (None,) * (len(ctx.needs_input_grad) - 4)
 
 
@@ -820,6 +834,8 @@ class TowerChainFn(torch.autograd.Function):
             ctx.mlp, ctx.feature_bn, ctx.G, ctx.key, ctx.bf = mlp, feature_bn, G, key, bf
             ctx.layers, ctx.out, ctx.norm = layers, out, norm
             ctx.sync, ctx.sync_off = sync, ctx_sync_off
+            ctx.params = params
+            _dp.note_writer(params)
         return out
 
     @staticmethod
@@ -874,6 +890,7 @@ class TowerChainFn(torch.autograd.Function):
         for i in range(0, len(wjobs), 4):  # up to 4 Linears per launch (csrc/tower.hip WG_MAXJ)
             _tower_wgrad_grouped(ctx.mlp, wjobs[i:i + 4], M, bf)
         ctx.layers = None
+        _dp.note_writer(ctx.params, written=True)
         return (None, None, None, dx, None) + (None,) * (len(ctx.needs_input_grad) - 5)
 
 

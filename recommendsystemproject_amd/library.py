@@ -84,7 +84,27 @@ class _Ctx:
         self.saved_tensors = ts
 
 
-def _keep(ctx) -> Tensor:
+def _alias_outputs(v, ids):
+    """v with every tensor in `ids` (the op's outputs) replaced by a detached alias."""
+    if isinstance(v, Tensor):
+        return v.detach() if id(v) in ids else v
+    if isinstance(v, list):
+        return [_alias_outputs(x, ids) for x in v]
+    if isinstance(v, tuple):
+        return tuple(_alias_outputs(x, ids) for x in v)
+    return v
+
+
+def _keep(ctx, *outs) -> Tensor:
+    """Park `ctx` until the backward (or until the ticket dies). The op's outputs it holds are
+    swapped for detached aliases first: the autograd layer attaches the op's node to those very
+    tensors, and ctx -> output -> node -> saved ticket -> ctx would be a cycle through C++ that
+    Python's collector cannot break (a forward with no backward would keep its graph, and
+    through the parameter edges the model, alive)."""
+    ids = {id(o) for o in outs if isinstance(o, Tensor)}
+    if ids:
+        for k, v in list(vars(ctx).items()):
+            setattr(ctx, k, _alias_outputs(v, ids))
     t = next(_NEXT_TICKET)
     _SAVED[t] = ctx
     ticket = torch.tensor([t], dtype=torch.int64)
@@ -133,7 +153,7 @@ def _seq_encoder(seq: List[Tensor], params: List[Tensor], stats: List[Tensor], f
     enc = module_of(handle)
     ctx = _Ctx(3 + len(params))
     out = fn.SeqEncoderFn.forward(ctx, need, enc, dict(zip(keys.split(','), seq)), *params)
-    return out, (_keep(ctx) if need else _no_ticket())
+    return out, (_keep(ctx, out) if need else _no_ticket())
 
 
 @_seq_encoder.register_fake
@@ -202,7 +222,7 @@ def _tower_features(sparse: Optional[Tensor], dense: Optional[Tensor], seq: List
     ctx = _Ctx(5 + len(params))
     out = fn.TowerFeatureFn.forward(ctx, need, tower, d, getattr(tower, '_rs_call_mapping', None), seq_vec,
                                     *params)
-    return out, (_keep(ctx) if need else _no_ticket())
+    return out, (_keep(ctx, out) if need else _no_ticket())
 
 
 @_tower_features.register_fake
@@ -279,7 +299,7 @@ def _tower_chain(x: Tensor, params: List[Tensor], stats: List[Tensor], flat_grad
     tower = module_of(handle)
     ctx = _Ctx(5 + len(params))
     out = fn.TowerChainFn.forward(ctx, need, tower.feature_bn, tower.mlp, x, groups, *params)
-    return out, (_keep(ctx) if need else _no_ticket())
+    return out, (_keep(ctx, out) if need else _no_ticket())
 
 
 @_tower_chain.register_fake
@@ -337,7 +357,7 @@ def _batch_norm(x: Tensor, params: List[Tensor], stats: List[Tensor], flat_grad:
     bn = module_of(handle)
     ctx = _Ctx(4 + len(params))
     y = fn.BatchNormFn.forward(ctx, need, bn, x, groups, *params)
-    return y, (_keep(ctx) if need else _no_ticket())
+    return y, (_keep(ctx, y) if need else _no_ticket())
 
 
 @_batch_norm.register_fake
@@ -374,7 +394,7 @@ def _mlp_tower(x: Tensor, params: List[Tensor], stats: List[Tensor], flat_grad: 
     mlp = module_of(handle)
     ctx = _Ctx(4 + len(params))
     out = fn.MLPFn.forward(ctx, need, mlp, x, groups, *params)
-    return out, (_keep(ctx) if need else _no_ticket())
+    return out, (_keep(ctx, out) if need else _no_ticket())
 
 
 @_mlp_tower.register_fake
@@ -412,7 +432,7 @@ def _inbatch_loss(U: Tensor, I: Tensor, item_ids: Optional[Tensor], H: Optional[
     equal-id collisions at -1e9, hard-negative logits appended, cross_entropy(arange(B)) mean."""
     ctx = _Ctx(5)
     loss = fn.InBatchLossFn.forward(ctx, U, I, item_ids, H, temperature)
-    return loss, _keep(ctx)
+    return loss, _keep(ctx, loss)
 
 
 @_inbatch_loss.register_fake

@@ -76,7 +76,8 @@ def train_step(model, batch_data, optimizer, max_grad_norm=1.0, temperature=0.1,
     ids = extract_item_id(batch_data['item_tower'], feature_name=item_id_feature, feature_type=item_id_type)
     loss = model.compute_loss(user_emb, pos_item_emb, hard_neg_emb=hard_neg_emb, item_ids=ids,
                               temperature=temperature)
-    loss.backward(backward_seed(loss))
+    with rdist.overlap(model):  # data parallel: each tower's all-reduce starts in the backward
+        loss.backward(backward_seed(loss))
     rdist.allreduce_gradients(model, optimizer)
     if isinstance(optimizer, Adam):
         optimizer.step(clip_max_norm=max_grad_norm if max_grad_norm > 0 else None)

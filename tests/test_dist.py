@@ -143,6 +143,8 @@ def _gpu_worker(rank, world, port, q, lazy=False):
         rdist.broadcast_model(model)
         opt = Adam(model.parameters(), lr=1e-3)
         train_step(model, batches[rank], opt, 1.0, 0.15)  # all-reduce inside (dist is active)
+        # both towers' gradient buckets were all-reduced inside the backward (dist.overlap)
+        assert ensure_flat(model).dp_buckets.launched == 2, ensure_flat(model).dp_buckets.launched
         ensure_flat(model).flush()
         dp_w = ensure_flat(model).data.detach().clone()
         # more steps: every rank must hold bitwise-identical weights (rows touched by one rank only
@@ -555,3 +557,101 @@ def test_row_sharded_tables_match_replicated_two_ranks_one_gpu(case):
     # 320,494 seen in two runs; a wrong gradient moves thousands), bounded at 2e-4
     assert dl < 1e-5, res
     assert off <= max(16, 2e-4 * n_el) and worst <= 2 * 1e-3 * 3 * 1.01, res
+
+
+def _overlap_cpu_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    from recommendsystemproject_amd import dist as rdist
+    from recommendsystemproject_amd.flat import FlatParams
+    from recommendsystemproject_amd.optim import Adam
+    try:
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world))
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        torch.manual_seed(0)
+        model = torch.nn.Module()
+        model.user_tower = torch.nn.ParameterList([torch.nn.Parameter(torch.randn(s)) for s in (5, (3, 7), 1)])
+        model.item_tower = torch.nn.ParameterList([torch.nn.Parameter(torch.randn(s)) for s in ((4, 4), 6)])
+        model.extra = torch.nn.Parameter(torch.randn(3))  # in no bucket: reduced at the end
+        f = FlatParams(list(model.parameters()), torch.device('cpu'))
+        gb = rdist.setup_buckets(model, [model.user_tower, model.item_tower])
+        assert gb is not None and len(gb.spans) == 2
+        user, item = list(model.user_tower), list(model.item_tower)
+        # forward: two ops write the user tower's gradient, one the item tower's
+        rdist.note_writer(user[:2])
+        rdist.note_writer(user[2:])
+        rdist.note_writer(item)
+        g = torch.Generator().manual_seed(100 + rank)
+        local = torch.randn(f.numel, generator=g)
+        with rdist.overlap(model):
+            f.grad.copy_(local)
+            rdist.note_writer(item, written=True)
+            n_item = len(gb.works)
+            rdist.note_writer(user[2:], written=True)
+            n_mid = len(gb.works)
+            rdist.note_writer(user[:2], written=True)
+            n_all = len(gb.works)
+        opt = Adam.__new__(Adam)
+        rdist.allreduce_gradients(model, opt)
+        total = torch.zeros_like(local)
+        for r in range(world):
+            total += torch.randn(f.numel, generator=torch.Generator().manual_seed(100 + r))
+        err = (f.grad - total).abs().max().item()
+        # a second forward after a bucket's launch (no allreduce_gradients between) is refused
+        rdist.note_writer(item)
+        with rdist.overlap(model):
+            rdist.note_writer(item, written=True)
+        refused = False
+        try:
+            rdist.note_writer(item)
+        except RuntimeError:
+            refused = True
+        rdist.allreduce_gradients(model, opt)
+        if rank == 0:
+            q.put(('ok', (n_item, n_mid, n_all, err, refused, opt.grad_scale)))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put(('err', traceback.format_exc()))
+
+
+def test_dp_overlap_buckets_gloo_cpu():
+    """dist.GradBuckets: each tower's all-reduce starts when its last gradient writer reports
+    (not before), the uncovered rest is reduced by allreduce_gradients, and the sum is exact."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_cpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+    assert res[0] == 'ok', res
+    n_item, n_mid, n_all, err, refused, scale = res[1]
+    assert (n_item, n_mid, n_all) == (1, 1, 2)
+    assert err < 1e-6 and refused and scale == 0.5
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo_one_gpu(tmp_path):
+    """bench.py's N > 1 path (one JSON line from rank 0, bucketed all-reduce started in the
+    backward, max-over-ranks timing), two gloo ranks sharing the GPU: eager steps (host-staged
+    gloo collectives cannot be captured; RCCL runs capture them)."""
+    import json
+    import subprocess
+    import sys
+    port = _free_port()
+    env = dict(os.environ, RSYS_DIST_BACKEND='gloo', MASTER_ADDR='127.0.0.1')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'bench.py'),
+           '--gpus', '2', '--steps', '3', '--warmup', '2', '--config', 'c2', '--no-cpu-baseline', '--extra=']
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == 2 and d['config']['parallelism'] == 'dp2' and d['value'] > 0
+    assert d['config']['hip_graph'] is False
