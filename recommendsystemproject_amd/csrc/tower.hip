@@ -406,7 +406,7 @@ __device__ __forceinline__ f4 pro_apply(const TwArgs& p, f4 a, f4 a2, int m, int
   return v;
 }
 
-template <typename T, int TM, int TN, int PRO, int EPI>
+template <typename T, int TM, int TN, int PRO, int EPI, int DCH = 1>
 __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
   constexpr int PITCH = OpT<T>::PITCH;
   constexpr int MT = TM / 64;      // 16-row m tiles per wave (4 waves stacked over the rows)
@@ -416,7 +416,9 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
   constexpr bool GEMM = EPI != EPI_NONE;
   constexpr bool SUMS = EPI == EPI_STATS || EPI == EPI_BWD;  // column sums + hand-off
   constexpr bool TWO = PRO == PRO_BNB || PRO == PRO_L2B;  // second A-shaped input
-  constexpr int D = TWO ? 2 : 3;  // k chunks of loads in flight per thread
+  // k chunks of loads in flight per thread: the host picks DCH >= the chunk count where the
+  // registers allow it, so every operand load of the workgroup goes out in one round trip
+  constexpr int D = DCH;
   constexpr int TP = TN + 1;      // epilogue tile pitch (floats)
 
   // one LDS buffer: the double-buffered operand stages, reused by the epilogue's column tile
@@ -614,14 +616,16 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
     // the chunk count is padded to a multiple of D (padding chunks stage zeros): no exit inside
     // the unrolled body, so the waitcnt pass sees straight-line code with D chunks in flight
     const int nkp = (nk + D - 1) / D * D;
-    for (int kc0 = 0; kc0 < nkp; kc0 += D) {
+    // the last group of D chunks issues no further loads (two straight-line bodies, chosen per
+    // group by a uniform branch: with D >= the chunk count every load went out before the loop)
+    auto group = [&](int kc0, bool more) {
 #pragma unroll
       for (int st = 0; st < D; ++st) {
         const int kc = kc0 + st;
         const int buf = kc & 1;
         store(kc, buf, ra[st], ra2[st], rw[st]);
         lds_barrier();
-        load(min(kc + D, nk - 1), ra[st], ra2[st], rw[st]);  // past the end: a cached re-read
+        if (more) load(min(kc + D, nk - 1), ra[st], ra2[st], rw[st]);
         if constexpr (sizeof(T) == 2) {
           bf16x8t af[MT], bfr[NTL];
 #pragma unroll
@@ -651,22 +655,38 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
           }
         }
       }
+    };
+    for (int kc0 = 0; kc0 < nkp; kc0 += D) {
+      if (kc0 + D < nkp) group(kc0, true);
+      else group(kc0, false);
     }
     TW_MARK(2);
 
     // h = pro(A) for the weight gradient, written by n-block 0 at the very end (a global store
-    // before a barrier makes the barrier wait for it): re-read from L2 and transformed again
+    // before a barrier makes the barrier wait for it): re-read from L2 and transformed again, HB
+    // float4 loads per thread issued before any of their stores (a load after a store to a
+    // possibly aliasing array is not hoisted above it: one round trip per float4 otherwise)
     auto write_h = [&]() {
       if (!hwrite) return;
-      const int k4n = K / 4;
-      for (int idx = tid; idx < nt * k4n; idx += 256) {
-        const int rl = idx / k4n, k = (idx % k4n) * 4;
-        const size_t o = (size_t)(mbase + rl) * K + k;
-        const f4 a = *reinterpret_cast<const f4*>(p.A + o);
-        f4 a2{};
-        if constexpr (TWO) a2 = *reinterpret_cast<const f4*>(p.A2 + o);
-        *reinterpret_cast<f4*>(p.h_out + o) =
-            pro_apply<PRO>(p, a, a2, mbase + rl, rl, k, c0, c1, c2, c3, c4, rdot, rden, rcl, dk, drop);
+      constexpr int HB = TWO ? 8 : 12;
+      const int k4n = K / 4, total = nt * k4n;
+      for (int base = 0; base < total; base += 256 * HB) {
+        f4 a[HB], a2[HB];
+#pragma unroll
+        for (int u = 0; u < HB; ++u) {
+          const int idx = min(base + tid + 256 * u, total - 1);
+          const size_t o = (size_t)(mbase + idx / k4n) * K + (idx % k4n) * 4;
+          a[u] = *reinterpret_cast<const f4*>(p.A + o);
+          if constexpr (TWO) a2[u] = *reinterpret_cast<const f4*>(p.A2 + o);
+        }
+#pragma unroll
+        for (int u = 0; u < HB; ++u) {
+          const int idx = base + tid + 256 * u;
+          if (idx >= total) break;
+          const int rl = idx / k4n, k = (idx % k4n) * 4;
+          *reinterpret_cast<f4*>(p.h_out + (size_t)(mbase + rl) * K + k) =
+              pro_apply<PRO>(p, a[u], a2[u], mbase + rl, rl, k, c0, c1, c2, c3, c4, rdot, rden, rcl, dk, drop);
+        }
       }
     };
     auto store_c = [&]() {
@@ -855,16 +875,48 @@ constexpr int TM = 64;  // row tile of every GEMM instance
 
 unsigned long long* g_dbg = nullptr;  // rs_tower_debug_buffer: profiling only
 
-template <typename T, int TN, int PRO, int EPI>
-int launch(const TwArgs& a, int nblocks, hipStream_t st, const char* name) {
+template <typename T, int TN, int PRO, int EPI, int DCH>
+int launch_d(const TwArgs& a, int nblocks, hipStream_t st, const char* name) {
   TwArgs b = a;
   b.dbg = g_dbg;
   b.tiles = cdiv(b.Bg, TM);
   b.nbx = nblocks;
   const int rts = cdiv(b.G * b.tiles, 8) * 8;  // row tiles padded to whole XCD groups
-  tower_kernel<T, TM, TN, PRO, EPI><<<dim3(nblocks * rts), 256, 0, st>>>(b);
+  tower_kernel<T, TM, TN, PRO, EPI, DCH><<<dim3(nblocks * rts), 256, 0, st>>>(b);
   RS_CHECK_LAUNCH(name);
   return 0;
+}
+
+// k chunks in flight: the smallest of 4 / 5 / 8 / 10 that covers the K extent, so every operand
+// load of a workgroup goes out in one round trip -- within the occupancy the grid needs (staged
+// registers: 16 VGPRs per chunk at TN = 64, 24 with a second A input or TN = 128; D = 10, a
+// two-input D = 8 and a TN = 128 D = 5 leave one workgroup per CU). Grids of more than two
+// workgroups per CU keep the short pipeline (3 chunks, 2 with a second input) at 2-3 per CU.
+template <typename T, int TN, int PRO, int EPI>
+int launch(const TwArgs& a, int nblocks, hipStream_t st, const char* name) {
+  constexpr bool TWO = PRO == PRO_BNB || PRO == PRO_L2B;
+  const int nk = cdiv(a.K, KC);
+  const int64_t grid = (int64_t)nblocks * (cdiv(a.G * cdiv(a.Bg, TM), 8) * 8);
+  const int per_cu = (int)((grid + 255) / 256);
+#define RS_TW_LAUNCH(DV) return launch_d<T, TN, PRO, EPI, DV>(a, nblocks, st, name)
+  if (per_cu > 2) {
+    if constexpr (TWO) RS_TW_LAUNCH(2);
+    else RS_TW_LAUNCH(3);
+  }
+  if (nk <= 4) RS_TW_LAUNCH(4);
+  if constexpr (TN > 64) {
+    if (per_cu == 1 && nk <= 5) RS_TW_LAUNCH(5);
+    RS_TW_LAUNCH(4);
+  } else if constexpr (TWO) {
+    if (per_cu == 1 && nk == 5) RS_TW_LAUNCH(5);
+    if (per_cu == 1 && nk <= 8) RS_TW_LAUNCH(8);
+    RS_TW_LAUNCH(4);
+  } else {
+    if (nk <= 5) RS_TW_LAUNCH(5);
+    if (nk <= 8 || per_cu == 2 || nk > 10) RS_TW_LAUNCH(8);
+    RS_TW_LAUNCH(10);
+  }
+#undef RS_TW_LAUNCH
 }
 
 template <typename T>
