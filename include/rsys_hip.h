@@ -403,15 +403,18 @@ int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const float* Hn, int
                             int N, int D, float T, const float* lse, const float* grad_out, float* dU,
                             float* dI, float* dhl, float* ws, void* stream);
 /* The same pair in fp32 compute mode: the tiles run on v_mfma_f32_32x32x2_f32 with fp32 operands
- * (exact f32 products, no rounding of U, I); same arguments, workspace and outputs. */
+ * (exact f32 products, no rounding of U, I); same arguments, workspace and outputs, plus S:
+ * [B][rs_inbatch_ce_s_ld(B)] fp32 scratch that the forward fills with U I^T (raw dot products)
+ * and the backward reads instead of recomputing the tiles (keep it from forward to backward). */
+int64_t rs_inbatch_ce_s_ld(int B);
 int rs_inbatch_ce_fused_f32_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
                                 int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
-                                int N, int D, float T, float* lse, float* row_loss, float* loss, float* ws,
-                                void* stream);
+                                int N, int D, float T, float* lse, float* row_loss, float* loss, float* S,
+                                float* ws, void* stream);
 int rs_inbatch_ce_fused_f32_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
                                 int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
                                 int N, int D, float T, const float* lse, const float* grad_out, float* dU,
-                                float* dI, float* dhl, float* ws, void* stream);
+                                float* dI, float* dhl, const float* S, float* ws, void* stream);
 /* dU[i] += sum_n dhl[i,n] H[i,n];  dH[i,n] = dhl[i,n] U[i]   (hard-negative bmm backward; dH in
  * the layout of H) */
 int rs_hardneg_bwd(const float* U, const float* Hn, int64_t h_row_stride, int64_t h_slot_stride,

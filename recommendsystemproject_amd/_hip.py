@@ -103,9 +103,11 @@ SIGNATURES = {
     'rs_inbatch_ce_fused_fwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp]),
     'rs_inbatch_ce_fused_bwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp,
                                       vp]),
-    'rs_inbatch_ce_fused_f32_fwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp]),
+    'rs_inbatch_ce_s_ld': (i64, [i32]),
+    'rs_inbatch_ce_fused_f32_fwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp,
+                                          vp]),
     'rs_inbatch_ce_fused_f32_bwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp,
-                                          vp, vp]),
+                                          vp, vp, vp]),
     'rs_inbatch_ce_fwd': (i32, [vp, i32, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp]),
     'rs_inbatch_ce_bwd': (i32, [vp, i32, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp]),
     'rs_inbatch_logits': (i32, [vp, i32, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, i64, vp]),

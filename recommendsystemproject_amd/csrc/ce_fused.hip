@@ -23,6 +23,11 @@
 // k-ordered fma chain; 64 cycles per instruction and SIMD, 1/16 of the bf16 rate): the streamed
 // tiles are staged in LDS as fp32, the owned fragments are fp32 registers, and the dS^T
 // accumulator elements are the B operand of the gradient MFMA as they stand (no packing).
+// At that rate recomputing S twice in the backward cost half of its MFMA time (64 of 128
+// instructions per tile), so the fp32 forward also stores S ([B][ldS] fp32, 64 MB at B = 4096,
+// written as the tiles are produced) and the backward reads each tile's 4 KB back one tile ahead
+// instead: the same bits as the recomputation (the products U[u][k] I[i][k] and their k order
+// are the same in all three modes), half the backward's flops for 2 x B^2 x 4 bytes of reads.
 #include <type_traits>
 
 #include "common.h"
@@ -62,6 +67,8 @@ struct CeArgs {
   float* part_s;        // fwd: [NS][B]
   float* diag;          // fwd: [B] S_ii / T
   float* part_d;        // bwd: [NS][B][D]
+  float* S;             // fp32 mode: [B][ldS] raw U I^T, written by the forward, read by the backward
+  int ldS;
 };
 
 __device__ __forceinline__ bf16x8 cvt8(const floatx4& a, const floatx4& b) {
@@ -123,9 +130,11 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
 
   // owned fragments: B operand of the S tile. bf16: lane (c, h) holds own[o][16 s + 8 h .. +7];
   // fp32: own[o][h D/2 + s] for k-step s (k-steps pair embedding columns s and D/2 + s)
+  constexpr bool SLOAD = F32 && MODE != 0;  // S tiles read back instead of recomputed
   bf16x8 ob[F32 ? 1 : KS];
-  float obf[F32 ? D / 2 : 1];
-  if constexpr (F32) {
+  float obf[F32 && !SLOAD ? D / 2 : 1];
+  if constexpr (SLOAD) {
+  } else if constexpr (F32) {
 #pragma unroll
     for (int s4 = 0; s4 < D / 8; ++s4) {
       floatx4 x = {0.f, 0.f, 0.f, 0.f};
@@ -213,6 +222,31 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
   };
   float dg = 0.f;  // fwd: S_oo / T, captured by the lane that meets the diagonal
   bool has_dg = false;
+  // fp32 backward: the S tile at streamed rows t0.. of this lane's element layout (row t = t0 +
+  // 8(e>>2) + 4h + (e&3), owned column o), loaded one tile ahead. dU (MODE 1): S[o][t], four
+  // float4 per lane; dI (MODE 2): S[t][o], 16 scalars, coalesced over the lanes' items. Rows and
+  // columns past B are clamped (those elements are masked where consumed).
+  const int o_c = min(o, B - 1);
+  auto load_s = [&](int t0, floatx16& sv) {
+    if constexpr (SLOAD) {
+      if constexpr (MODE == 1) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const floatx4 v = *reinterpret_cast<const floatx4*>(a.S + (int64_t)o_c * a.ldS + min(t0, a.ldS - kTile) + 8 * g4 + 4 * h);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sv[4 * g4 + j] = v[j];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int t = min(t0 + 8 * (e >> 2) + 4 * h + (e & 3), B - 1);
+          sv[e] = a.S[(int64_t)t * a.ldS + o_c];
+        }
+      }
+    }
+  };
+  floatx16 snx;
+  if constexpr (SLOAD) load_s(t_begin, snx);
   auto consume = [&](int hf, int k, int t0) {
     const E* T = &L.Ts[hf][k * kTile * PT];
     const int64_t* sidk = &L.sid[hf][k * kTile];
@@ -220,7 +254,10 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
     floatx16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-    if constexpr (F32) {
+    if constexpr (SLOAD) {
+      acc = snx;
+      load_s(t0 + kTile, snx);
+    } else if constexpr (F32) {
       // one chain: the f32 MFMA's dependent latency equals its issue interval (64 cycles)
 #pragma unroll
       for (int s4 = 0; s4 < D / 8; ++s4) {
@@ -264,6 +301,14 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
     }
     const bool rare = (t0 == o_base) | (t0 + kTile > B) | !wave_ok;  // wave-uniform
     if constexpr (MODE == 0) {
+      if constexpr (F32) {
+        if (o_ok) {
+          float* sp = a.S + (int64_t)o * a.ldS + t0 + 4 * h;
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4)
+            *reinterpret_cast<floatx4*>(sp + 8 * g4) = floatx4{acc[4 * g4], acc[4 * g4 + 1], acc[4 * g4 + 2], acc[4 * g4 + 3]};
+        }
+      }
       float v[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) v[e] = coll[e] ? kMasked : acc[e] * sc2;
@@ -534,6 +579,9 @@ int launch_tiles(const CeArgs& a, int D, int NS, hipStream_t st) {
 
 using namespace rs;
 
+// row pitch of the fp32 mode's stored S: whole 32-column tiles (the tiles past B stay in the row)
+extern "C" int64_t rs_inbatch_ce_s_ld(int B) { return (int64_t)cdiv(B, kTile) * kTile; }
+
 extern "C" int64_t rs_inbatch_ce_fused_ws_bytes(int B, int D) {
   const int64_t fwd = (int64_t)splits_for(B, false) * B * 2 + B;
   const int64_t bwd = (int64_t)2 * splits_for(B, true) * B * D;  // dU and dI partials side by side
@@ -545,9 +593,9 @@ namespace {
 template <bool F32>
 int ce_fused_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride, int64_t h_slot_stride,
                  const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T, float* lse,
-                 float* row_loss, float* loss, float* ws, void* stream) {
+                 float* row_loss, float* loss, float* S, float* ws, void* stream) {
   const char* fn = F32 ? "rs_inbatch_ce_fused_f32_fwd" : "rs_inbatch_ce_fused_fwd";
-  RS_CHECK_ARG(U && I && lse && row_loss && loss && ws, "%s: null pointer", fn);
+  RS_CHECK_ARG(U && I && lse && row_loss && loss && ws && (!F32 || S), "%s: null pointer", fn);
   RS_CHECK_ARG(B >= 1 && (D == 64 || D == 128) && N >= 0 && N <= 64,
                "%s: needs D in {64, 128}, N <= 64 (B=%d N=%d D=%d)", fn, B, N, D);
   RS_CHECK_ARG(N == 0 || Hn, "%s: hard negatives need H", fn);
@@ -556,6 +604,7 @@ int ce_fused_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_
   const int NS = splits_for(B, false);
   CeArgs a{};
   a.own = U; a.str = I; a.B = B; a.invT = 1.f / T; a.ids = item_ids; a.id_stride = id_stride;
+  a.S = S; a.ldS = (int)rs_inbatch_ce_s_ld(B);
   a.split_rows = cdiv(cdiv(B, NS), kTile) * kTile;
   a.part_m = ws; a.part_s = ws + (int64_t)NS * B; a.diag = ws + (int64_t)2 * NS * B;
   const int NSr = cdiv(B, a.split_rows);
@@ -571,9 +620,10 @@ int ce_fused_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_
 template <bool F32>
 int ce_fused_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride, int64_t h_slot_stride,
                  const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T, const float* lse,
-                 const float* grad_out, float* dU, float* dI, float* dhl, float* ws, void* stream) {
+                 const float* grad_out, float* dU, float* dI, float* dhl, const float* S, float* ws,
+                 void* stream) {
   const char* fn = F32 ? "rs_inbatch_ce_fused_f32_bwd" : "rs_inbatch_ce_fused_bwd";
-  RS_CHECK_ARG(U && I && lse && dU && dI && ws, "%s: null pointer", fn);
+  RS_CHECK_ARG(U && I && lse && dU && dI && ws && (!F32 || S), "%s: null pointer", fn);
   RS_CHECK_ARG(B >= 1 && (D == 64 || D == 128) && N >= 0 && N <= 64, "%s: bad shape", fn);
   RS_CHECK_ARG(N == 0 || (Hn && dhl), "%s: hard negatives need H, dhl", fn);
   RS_CHECK_ARG(aligned16(U) && aligned16(I) && aligned16(dU) && aligned16(dI),
@@ -582,6 +632,7 @@ int ce_fused_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_
   const int NS = splits_for(B, true);
   CeArgs a{};
   a.B = B; a.invT = 1.f / T; a.ids = item_ids; a.id_stride = id_stride; a.lse = lse; a.grad_out = grad_out;
+  a.S = const_cast<float*>(S); a.ldS = (int)rs_inbatch_ce_s_ld(B);
   a.split_rows = cdiv(cdiv(B, NS), kTile) * kTile;
   a.part_d = ws;
   const int NSr = cdiv(B, a.split_rows);
@@ -612,15 +663,15 @@ extern "C" int rs_inbatch_ce_fused_fwd(const float* U, const float* I, const flo
                                        int N, int D, float T, float* lse, float* row_loss, float* loss, float* ws,
                                        void* stream) {
   return ce_fused_fwd<false>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, row_loss,
-                             loss, ws, stream);
+                             loss, nullptr, ws, stream);
 }
 
 extern "C" int rs_inbatch_ce_fused_f32_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
                                            int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
-                                           int N, int D, float T, float* lse, float* row_loss, float* loss, float* ws,
-                                           void* stream) {
+                                           int N, int D, float T, float* lse, float* row_loss, float* loss, float* S,
+                                           float* ws, void* stream) {
   return ce_fused_fwd<true>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, row_loss,
-                            loss, ws, stream);
+                            loss, S, ws, stream);
 }
 
 extern "C" int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
@@ -628,13 +679,13 @@ extern "C" int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const flo
                                        int N, int D, float T, const float* lse, const float* grad_out, float* dU,
                                        float* dI, float* dhl, float* ws, void* stream) {
   return ce_fused_bwd<false>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, grad_out,
-                             dU, dI, dhl, ws, stream);
+                             dU, dI, dhl, nullptr, ws, stream);
 }
 
 extern "C" int rs_inbatch_ce_fused_f32_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
                                            int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
                                            int N, int D, float T, const float* lse, const float* grad_out, float* dU,
-                                           float* dI, float* dhl, float* ws, void* stream) {
+                                           float* dI, float* dhl, const float* S, float* ws, void* stream) {
   return ce_fused_bwd<true>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, grad_out,
-                            dU, dI, dhl, ws, stream);
+                            dU, dI, dhl, S, ws, stream);
 }

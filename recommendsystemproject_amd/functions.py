@@ -906,10 +906,13 @@ class InBatchLossFn(torch.autograd.Function):
         I = I.contiguous()
         B, D = int(U.shape[0]), int(U.shape[1])
         dev = U.device
-        # S tiles recomputed on the MFMA (bf16 or f32 operands), never stored (csrc/ce_fused.hip)
+        # bf16: S tiles recomputed on the MFMA, never stored; fp32: the forward stores S (raw
+        # U I^T, [B, ldS]) for the backward to read instead of recomputing (csrc/ce_fused.hip)
         fused = D in (64, 128)
         sfx = '' if precision.compute_dtype() == 'bf16' else '_f32'
         S = None
+        if fused and sfx:
+            S = torch.empty(B, int(_hip.lib().rs_inbatch_ce_s_ld(B)), device=dev, dtype=torch.float32)
         if not fused:
             S = torch.empty(B, B, device=dev, dtype=torch.float32)
             ops.gemm(U, I, S, B, B, D, transA=0, transB=1, lda=D, ldb=D, ldc=B)
@@ -935,9 +938,10 @@ class InBatchLossFn(torch.autograd.Function):
         loss = torch.empty((), device=dev, dtype=torch.float32)
         if fused:
             w = ops.ws(_hip.lib().rs_inbatch_ce_fused_ws_bytes(B, D), dev)
+            extra = (S.data_ptr(),) if sfx else ()
             _hip.call(f'rs_inbatch_ce_fused{sfx}_fwd', U.data_ptr(), I.data_ptr(), ops.P(Hc), hsr, hss, ops.P(ids), st,
                       B, N, D, float(temperature), lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(),
-                      w.data_ptr(), ops.stream())
+                      *extra, w.data_ptr(), ops.stream())
         else:
             _hip.call('rs_inbatch_ce_fwd', S.data_ptr(), B, U.data_ptr(), ops.P(Hc), hsr, hss, ops.P(ids), st,
                       B, N, D, float(temperature), lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(),
@@ -962,9 +966,11 @@ class InBatchLossFn(torch.autograd.Function):
             dU = torch.empty_like(U)
             dI = torch.empty_like(I)
             w = ops.ws(_hip.lib().rs_inbatch_ce_fused_ws_bytes(B, D), U.device)
+            extra = (S.data_ptr(),) if ctx.sfx else ()
             _hip.call(f'rs_inbatch_ce_fused{ctx.sfx}_bwd', U.data_ptr(), I.data_ptr(), ops.P(Hc) if N else None,
                       ctx.hs[0], ctx.hs[1], ops.P(ctx.ids), ctx.st, B, N, D, ctx.T, ctx.lse.data_ptr(),
-                      gout.data_ptr(), dU.data_ptr(), dI.data_ptr(), ops.P(dhl), w.data_ptr(), ops.stream())
+                      gout.data_ptr(), dU.data_ptr(), dI.data_ptr(), ops.P(dhl), *extra, w.data_ptr(), ops.stream())
+            ctx.S = None
             dH = None
             if N:
                 dH = torch.empty_strided(Hc.shape, Hc.stride(), device=Hc.device, dtype=Hc.dtype)

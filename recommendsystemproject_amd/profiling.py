@@ -148,6 +148,16 @@ def _ce_fused_work(a, bwd=False):
     return (8.0 if bwd else 2.0) * B * B * D, 4.0 * 2 * B * D * (2 if bwd else 1)
 
 
+def _ce_fused_f32_work(a, bwd=False):
+    B, D = a[7], a[9]
+    # fp32: the forward computes S once and stores it (B x B fp32 written); the backward reads it
+    # back in both halves (2 x B x B fp32) and runs only dU = dS I and dI = dS^T U
+    fl, by = _ce_fused_work(a, False)
+    if bwd:
+        return 4.0 * B * B * D, 2 * by + 8.0 * B * B
+    return fl, by + 4.0 * B * B
+
+
 def _ffn_bwd_ln_work(a):
     M, F = a[0], a[1]
     # the FFN backward's operands plus norm1's: h1 read, dh1 (+ dsa) written instead of dx1
@@ -167,8 +177,8 @@ WORK = {
     'rs_ffn_bwd_ln2_bf16': _ffn_bwd_ln2_work,
     'rs_inbatch_ce_fused_fwd': _ce_fused_work,
     'rs_inbatch_ce_fused_bwd': lambda a: _ce_fused_work(a, True),
-    'rs_inbatch_ce_fused_f32_fwd': _ce_fused_work,
-    'rs_inbatch_ce_fused_f32_bwd': lambda a: _ce_fused_work(a, True),
+    'rs_inbatch_ce_fused_f32_fwd': _ce_fused_f32_work,
+    'rs_inbatch_ce_fused_f32_bwd': lambda a: _ce_fused_f32_work(a, True),
     'rs_gemm_add_layernorm': _gemm_ln_work,
     'rs_ffn_fwd_bf16': _ffn_fwd_work,
     'rs_ffn_bwd_bf16': _ffn_bwd_work,

@@ -111,4 +111,4 @@ def test_fused_f32_ce_deterministic():
 def test_fused_f32_ce_bad_args():
     with pytest.raises(RuntimeError, match='rs_inbatch_ce_fused_f32_fwd'):
         _hip.call('rs_inbatch_ce_fused_f32_fwd', None, None, None, 0, 0, None, 0, 16, 0, 128, 0.1, None, None, None,
-                  None, 0)
+                  None, None, 0)
