@@ -184,8 +184,32 @@ __device__ __forceinline__ bool fin_publish(const Fin& f, int N, int tiles, int 
   return ticket(f.cnt + g * f.nb + nb, tiles - 1);
 }
 
+// What the last arriver read-modify-writes at the very end (the running statistics, or dgamma /
+// dbeta, of column n0 + tid; num_batches_tracked), loaded by every workgroup before its ticket so
+// that the merge's tail is not one more dependent round trip.
+struct FinPre {
+  float a = 0.f, b = 0.f;
+  int64_t nbt = 0;
+};
+__device__ __forceinline__ FinPre fin_preload(const Fin& f, int nb, int ncols) {
+  FinPre r;
+  const int tid = threadIdx.x;
+  if (tid < ncols) {
+    const int col = nb * 64 + tid;
+    if (f.bwd) {
+      r.a = f.dgamma[col];
+      r.b = f.dbeta[col];
+    } else if (f.run_mean) {
+      r.a = f.run_mean[col];
+      r.b = f.run_var[col];
+    }
+  }
+  if (tid == 0 && !f.bwd && nb == 0 && f.nbt) r.nbt = *f.nbt;
+  return r;
+}
+
 __device__ void fin_merge(const Fin& f, int N, int G, int Bg, int tiles, int tm, int g, int nb,
-                          int ncols) {
+                          int ncols, const FinPre& pre) {
   __shared__ double comb[3][4][64];
   const int tid = threadIdx.x;
   const int n0 = nb * 64;
@@ -203,19 +227,36 @@ __device__ void fin_merge(const Fin& f, int N, int G, int Bg, int tiles, int tm,
       av[u] = ld_sc1(pb + o);
       qv[u] = ld_sc1(pb + o + N);
     }
+    if (f.bwd) {
 #pragma unroll
-    for (int u = 0; u < MB; ++u) {
-      if (t0 + u >= t_end) break;
-      if (f.bwd) {
+      for (int u = 0; u < MB; ++u) {
+        if (t0 + u >= t_end) break;
         a += (double)av[u];
         q += (double)qv[u];
-      } else {  // Chan: merge tile (n_t, mean_t, M2_t) into (n_a, a, q)
-        const double nt = (double)min(tm, Bg - (t0 + u) * tm);
-        const double n = n_a + nt, d = (double)av[u] - a;
-        a += d * (nt / n);
-        q += (double)qv[u] + d * d * (n_a * nt / n);
-        n_a = n;
       }
+    } else {
+      // the batch's tiles combined in two passes (weighted mean, then M2 + n_t (mean_t - mean)^2:
+      // one fp64 division per batch -- the per-tile Chan update's two divisions per tile were a
+      // dependent chain of ~4 us in the last arriver), then merged into (n_a, a, q) by Chan
+      double nb = 0.0, sb = 0.0;
+#pragma unroll
+      for (int u = 0; u < MB; ++u) {
+        const double nt = t0 + u < t_end ? (double)min(tm, Bg - (t0 + u) * tm) : 0.0;
+        nb += nt;
+        sb += nt * (double)av[u];
+      }
+      const double mb = sb / nb;
+      double qb = 0.0;
+#pragma unroll
+      for (int u = 0; u < MB; ++u) {
+        const double nt = t0 + u < t_end ? (double)min(tm, Bg - (t0 + u) * tm) : 0.0;
+        const double d = (double)av[u] - mb;
+        qb += nt > 0.0 ? (double)qv[u] + nt * d * d : 0.0;
+      }
+      const double n = n_a + nb, d = mb - a;
+      a += d * (nb / n);
+      q += qb + d * d * (n_a * nb / n);
+      n_a = n;
     }
   }
   comb[0][tl][c] = n_a;
@@ -240,8 +281,8 @@ __device__ void fin_merge(const Fin& f, int N, int G, int Bg, int tiles, int tm,
       if (f.bwd) {
         f.o0[col] = (float)(A / (double)Bg);
         f.o1[col] = (float)(Q / (double)Bg);
-        f.dgamma[col] += (float)Q;
-        f.dbeta[col] += (float)A;
+        f.dgamma[col] = pre.a + (float)Q;
+        f.dbeta[col] = pre.b + (float)A;
       } else {
         double var = Q / (double)Bg;
         if (var < 0.0) var = 0.0;
@@ -249,13 +290,13 @@ __device__ void fin_merge(const Fin& f, int N, int G, int Bg, int tiles, int tm,
         f.o1[col] = (float)(1.0 / sqrt(var + (double)f.eps));
         if (f.run_mean) {
           const double unb = Bg > 1 ? Q / (double)(Bg - 1) : var;
-          f.run_mean[col] = (1.f - f.momentum) * f.run_mean[col] + f.momentum * (float)A;
-          f.run_var[col] = (1.f - f.momentum) * f.run_var[col] + f.momentum * (float)unb;
+          f.run_mean[col] = (1.f - f.momentum) * pre.a + f.momentum * (float)A;
+          f.run_var[col] = (1.f - f.momentum) * pre.b + f.momentum * (float)unb;
         }
       }
     }
     if (tid == 0) {
-      if (!f.bwd && nb == 0 && f.nbt) *f.nbt += 1;
+      if (!f.bwd && nb == 0 && f.nbt) *f.nbt = pre.nbt + 1;
       __hip_atomic_store(f.cnt + nb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
@@ -301,19 +342,22 @@ __device__ void fin_merge(const Fin& f, int N, int G, int Bg, int tiles, int tm,
         tb += ld_sc1(f.scratch + (size_t)gg * 2 * N + col);
         tw += ld_sc1(f.scratch + (size_t)gg * 2 * N + N + col);
       }
-      f.dgamma[col] += (float)tw;
-      f.dbeta[col] += (float)tb;
+      f.dgamma[col] = pre.a + (float)tw;
+      f.dbeta[col] = pre.b + (float)tb;
     } else if (f.run_mean) {
+      float rm = pre.a, rv = pre.b;
       for (int gg = 0; gg < G; ++gg) {
         const double mu = ld_sc1(f.scratch + (size_t)gg * 2 * N + col);
         const double unb = ld_sc1(f.scratch + (size_t)gg * 2 * N + N + col);
-        f.run_mean[col] = (1.f - f.momentum) * f.run_mean[col] + f.momentum * (float)mu;
-        f.run_var[col] = (1.f - f.momentum) * f.run_var[col] + f.momentum * (float)unb;
+        rm = (1.f - f.momentum) * rm + f.momentum * (float)mu;
+        rv = (1.f - f.momentum) * rv + f.momentum * (float)unb;
       }
+      f.run_mean[col] = rm;
+      f.run_var[col] = rv;
     }
   }
   if (tid == 0) {
-    if (!f.bwd && nb == 0 && f.nbt) *f.nbt += G;
+    if (!f.bwd && nb == 0 && f.nbt) *f.nbt = pre.nbt + G;
     __hip_atomic_store(cnt2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -729,7 +773,9 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
         for (int j = 0; j < NTL; ++j) acc[i][j] /= den;
       }
       store_c();
+      TW_MARK(6);
       write_h();
+      TW_MARK(7);
     } else {
       // EPI_STATS: z = acc + bias; EPI_BWD: g = mask(acc) of the BatchNorm below. Both go through
       // an LDS tile (value, and g * xhat) whose columns 256 threads sum over the valid rows
@@ -811,11 +857,15 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
       }
       TW_MARK(4);
       const int ncols = min(TN, N - n0);
+      const FinPre pre = fin_preload(p.fin, nblk, ncols);
       const bool last = fin_publish(p.fin, N, p.tiles, g, tile, nblk, ncols, v0, v1);
-      if (last) fin_merge(p.fin, N, p.G, p.Bg, p.tiles, TM, g, nblk, ncols);
       TW_MARK(5);
+      // the last arriver's own outputs go out before its merge (their latency under the merge's)
       store_c();
+      TW_MARK(6);
       write_h();
+      if (last) fin_merge(p.fin, N, p.G, p.Bg, p.tiles, TM, g, nblk, ncols, pre);
+      TW_MARK(7);
     }
   }
 }
@@ -866,8 +916,9 @@ __global__ __launch_bounds__(256) void tower_stats_kernel(const float* __restric
   __syncthreads();
   const float m2t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
   const int ncols = min(64, C - (int)blockIdx.x * 64);
+  const FinPre pre = fin_preload(fin, blockIdx.x, ncols);
   if (fin_publish(fin, C, tiles, g, tile, blockIdx.x, ncols, mu, m2t))
-    fin_merge(fin, C, G, Bg, tiles, TM_STATS, g, blockIdx.x, ncols);
+    fin_merge(fin, C, G, Bg, tiles, TM_STATS, g, blockIdx.x, ncols, pre);
 }
 
 // ---------------------------------------------------------------------------- host side

@@ -2,7 +2,7 @@
 forward + backward with rs_tower_debug_buffer set, one kernel at a time, and prints per-phase
 percentiles across workgroups (us since the kernel's first workgroup started).
 Phases: 0 start, 1 prologue done, 2 main loop done, 3 C stored, 4 column sums done, 5 hand-off done,
-6 first k chunk done, 7 second k chunk done."""
+6 C stored, 7 h written (the workgroup's end)."""
 import os
 import sys
 
