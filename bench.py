@@ -644,8 +644,16 @@ def main():
         key = name if ex_dtype == 'fp32' else f'{name}_{ex_dtype}'
         if (name, ex_dtype) == (args.config, args.dtype):
             continue
-        r = run_workload(args, name, ex_dtype, None, 10 if name == 'c5' else 0, rank, world, dev,
-                         0.0 if name in cpu_done else cpu_s / 2, peaks)
+        try:
+            r = run_workload(args, name, ex_dtype, None, 10 if name == 'c5' else 0, rank, world, dev,
+                             0.0 if name in cpu_done else cpu_s / 2, peaks)
+        except Exception as e:  # an extra workload must not cost the headline line
+            import traceback
+            traceback.print_exc(file=sys.stderr)
+            extras[key] = {'error': repr(e)[:400]}
+            r = None
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
         cpu_done.add(name)
         order.append(key)
         if r is not None:
