@@ -233,51 +233,88 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter_kernel(
 // One workgroup, the keys in registers (4 per thread) and exchanged through LDS between the
 // radix passes. (Measured and rejected: a bitonic sort of key/index pairs -- 39 us with an LDS
 // barrier per step, 47 us with the short distances in registers and shuffles: 78 steps of 4,096
-// compare-exchanges on one CU are VALU-bound; this sort takes ~23 us.)
+// compare-exchanges on one CU are VALU-bound.)
+// Wave-major ranking (round 3): wave w holds keys w*256 .. w*256+255 (4 rounds of 64 lanes), so a
+// key's rank among equal digits is (digit base) + (that digit's count in earlier waves) + (its
+// count in this wave's earlier rounds) + (its lane rank): each wave keeps running per-digit counts
+// in its own LDS row with no workgroup barrier inside the rounds, and one prefix over the 16
+// waves per digit replaces the per-round 16-wave prefix and its two barriers (4 per pass before:
+// the user_id sort, 4,096 keys, 3 passes, took ~23 us).
+constexpr int kTileWaves = kTileThreads / 64;
+constexpr int kTileKeys = kTileMax / kTileWaves;  // keys per wave (4 rounds of 64)
+static_assert(kTileKeys == kSortRounds * 64, "one-tile sort: 4 rounds of 64 keys per wave");
+
 __global__ __launch_bounds__(kTileThreads) void sort_tile_kernel(
     const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab, int n,
     SortPlan plan, uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
-  __shared__ RankLds<kTileThreads> lds;
-  __shared__ int tbase[kMaxRadix];
+  __shared__ uint16_t cnt[kTileWaves][kMaxRadix];  // per wave: running, then exclusive, digit counts
+  __shared__ int dbase[kMaxRadix];                  // exclusive scan of the digit totals
+  __shared__ int wsum[kTileWaves];
   __shared__ uint32_t xchg[kTileMax];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   uint32_t key[kSortRounds], val[kSortRounds];
 #pragma unroll
   for (int r = 0; r < kSortRounds; ++r) {
-    const int e = r * kTileThreads + threadIdx.x;
+    const int e = w * kTileKeys + r * 64 + lane;
     key[r] = e < n ? raw_key(ids, id_bytes, bag, stride, vocab, e) : kSentinel;
     val[r] = (uint32_t)e;
   }
   for (int p = 0; p < plan.passes; ++p) {
-    const int radix = 1 << plan.dbits[p], shift = plan.shift[p];
-    rank_reset(lds, radix);
-    for (int t = threadIdx.x; t < radix; t += kTileThreads) tbase[t] = 0;
+    const int radix = 1 << plan.dbits[p], shift = plan.shift[p], dbits = plan.dbits[p];
+    for (int t = threadIdx.x; t < kTileWaves * radix; t += kTileThreads) cnt[t / radix][t % radix] = 0;
     __syncthreads();
+    int pin[kSortRounds];  // rank among this wave's keys of the same digit
 #pragma unroll
-    for (int r = 0; r < kSortRounds; ++r)
-      if (r * kTileThreads + (int)threadIdx.x < n) atomicAdd(&tbase[(key[r] >> shift) & (radix - 1)], 1);
-    __syncthreads();
-    if (threadIdx.x < 64) {  // exclusive scan of the digit counts
-      int carry = 0;
-      const int lane = threadIdx.x;
-      for (int d0 = 0; d0 < radix; d0 += 64) {
-        const int x = d0 + lane < radix ? tbase[d0 + lane] : 0;
-        int y = x;
-        for (int o = 1; o < 64; o <<= 1) {
-          const int t = __shfl_up(y, o, 64);
-          if (lane >= o) y += t;
-        }
-        if (d0 + lane < radix) tbase[d0 + lane] = carry + y - x;
-        carry += __shfl(y, 63, 64);
+    for (int r = 0; r < kSortRounds; ++r) {
+      const bool valid = w * kTileKeys + r * 64 + lane < n;
+      const uint32_t d = (key[r] >> shift) & (radix - 1);
+      uint64_t peers = __ballot(valid);
+      for (int b = 0; b < dbits; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        peers &= bit ? bb : ~bb;
       }
+      const int lrank = __popcll(peers & lt);
+      // every lane reads its digit's count, then the group's first lane adds the group (the
+      // wave's LDS operations complete in program order; the store is after the load)
+      const int old = valid ? (int)cnt[w][d] : 0;
+      __builtin_amdgcn_wave_barrier();
+      if (valid && lrank == 0) cnt[w][d] = (uint16_t)(old + __popcll(peers));
+      __builtin_amdgcn_wave_barrier();
+      pin[r] = old + lrank;
+    }
+    __syncthreads();
+    // per digit: exclusive offsets over the waves, then the digit totals scanned
+    int tot = 0;
+    if ((int)threadIdx.x < radix) {
+#pragma unroll
+      for (int ww = 0; ww < kTileWaves; ++ww) {
+        const int c = cnt[ww][threadIdx.x];
+        cnt[ww][threadIdx.x] = (uint16_t)tot;
+        tot += c;
+      }
+    }
+    int y = tot;  // inclusive scan over the digits: lanes, then the waves' sums
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(y, o, 64);
+      if (lane >= o) y += t;
+    }
+    if (lane == 63) wsum[w] = y;
+    __syncthreads();
+    if ((int)threadIdx.x < radix) {
+      int pre = 0;
+      for (int ww = 0; ww < w; ++ww) pre += wsum[ww];
+      dbase[threadIdx.x] = pre + y - tot;
     }
     __syncthreads();
     int pos[kSortRounds];
 #pragma unroll
     for (int r = 0; r < kSortRounds; ++r) {
-      const bool valid = r * kTileThreads + (int)threadIdx.x < n;
+      const bool valid = w * kTileKeys + r * 64 + lane < n;
       const uint32_t d = (key[r] >> shift) & (radix - 1);
-      const int lp = rank_round(lds, d, valid, plan.dbits[p], radix);
-      pos[r] = valid ? tbase[d] + lp : -1;
+      pos[r] = valid ? dbase[d] + (int)cnt[w][d] + pin[r] : -1;
     }
     // exchange keys, then values, through LDS into the new order
 #pragma unroll
@@ -285,7 +322,7 @@ __global__ __launch_bounds__(kTileThreads) void sort_tile_kernel(
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSortRounds; ++r) {
-      const int e = r * kTileThreads + threadIdx.x;
+      const int e = w * kTileKeys + r * 64 + lane;
       if (e < n) key[r] = xchg[e];
     }
     __syncthreads();
@@ -294,14 +331,14 @@ __global__ __launch_bounds__(kTileThreads) void sort_tile_kernel(
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSortRounds; ++r) {
-      const int e = r * kTileThreads + threadIdx.x;
+      const int e = w * kTileKeys + r * 64 + lane;
       if (e < n) val[r] = xchg[e];
     }
     __syncthreads();
   }
 #pragma unroll
   for (int r = 0; r < kSortRounds; ++r) {
-    const int e = r * kTileThreads + threadIdx.x;
+    const int e = w * kTileKeys + r * 64 + lane;
     if (e < n) {
       kout[e] = key[r];
       vout[e] = val[r];

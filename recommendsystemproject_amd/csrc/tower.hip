@@ -1123,18 +1123,24 @@ __global__ __launch_bounds__(256) void tower_wgrad_kernel(WgArgs a) {
   float* pdb = J.part + (size_t)J.tn * J.tk * J.S * 4096 + ((size_t)tn * J.S) * 64;
   if (do_db && tid < 64) st_sc1(pdb + s * 64 + tid, dbv);
   if (!ticket(J.cnt + tile, J.S - 1)) return;
+  // the S partials (this workgroup's own included: its sc1 stores are drained) summed in split
+  // order, 4 splits' loads in flight at a time: one split per round trip made the last arriver's
+  // tail ~S x 1.5 us
   f16v sum;
 #pragma unroll
   for (int e = 0; e < 16; ++e) sum[e] = 0.f;
-  for (int q = 0; q < J.S; ++q) {
-    f16v v;
-    if (q == s) {
-      v = acc;
-    } else {
+  constexpr int QB = 4;
+  for (int q0 = 0; q0 < J.S; q0 += QB) {
+    f16v v[QB];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) v[e] = ld_sc1(pt + (size_t)q * 4096 + e * 256 + tid);
+    for (int u = 0; u < QB; ++u) {
+      const int q = min(q0 + u, J.S - 1);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[u][e] = ld_sc1(pt + (size_t)q * 4096 + e * 256 + tid);
     }
-    sum += v;
+#pragma unroll
+    for (int u = 0; u < QB; ++u)
+      if (q0 + u < J.S) sum += v[u];
   }
   // dW += sum: every old value loaded before any is stored (a load after a store to the same
   // array would wait for the store: 16 serial round trips)
@@ -1152,8 +1158,14 @@ __global__ __launch_bounds__(256) void tower_wgrad_kernel(WgArgs a) {
     if (nn < N && kk < K) dWp[(size_t)nn * K + kk] = old[e] + sum[e];
   }
   if (do_db && tid < 64 && n0 + tid < N) {
+    float dv[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dv[q] = ld_sc1(pdb + min(q, J.S - 1) * 64 + tid);
     float t = 0.f;
-    for (int q = 0; q < J.S; ++q) t += q == s ? dbv : ld_sc1(pdb + q * 64 + tid);
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (q < J.S) t += dv[q];
+    for (int q = 16; q < J.S; ++q) t += ld_sc1(pdb + q * 64 + tid);
     J.db[n0 + tid] += t;
   }
   if (tid == 0) __hip_atomic_store(J.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
