@@ -336,21 +336,44 @@ __device__ void fin_merge(const Fin& f, int N, int G, int Bg, int tiles, int tm,
   // ---- every group of column block nb is in: cross-group step, groups in order
   if (tid < ncols) {
     const int col = n0 + tid;
+    // the groups' values GB at a time (one round trip per batch, not per group: G = 11 item
+    // groups with 10 hard negatives), consumed in group order
+    constexpr int GB = 8;
     if (f.bwd) {
       double tw = 0.0, tb = 0.0;
-      for (int gg = 0; gg < G; ++gg) {
-        tb += ld_sc1(f.scratch + (size_t)gg * 2 * N + col);
-        tw += ld_sc1(f.scratch + (size_t)gg * 2 * N + N + col);
+      for (int g0 = 0; g0 < G; g0 += GB) {
+        double vb[GB], vw[GB];
+#pragma unroll
+        for (int u = 0; u < GB; ++u) {
+          const size_t o = (size_t)min(g0 + u, G - 1) * 2 * N + col;
+          vb[u] = ld_sc1(f.scratch + o);
+          vw[u] = ld_sc1(f.scratch + o + N);
+        }
+#pragma unroll
+        for (int u = 0; u < GB; ++u) {
+          if (g0 + u >= G) break;
+          tb += vb[u];
+          tw += vw[u];
+        }
       }
       f.dgamma[col] = pre.a + (float)tw;
       f.dbeta[col] = pre.b + (float)tb;
     } else if (f.run_mean) {
       float rm = pre.a, rv = pre.b;
-      for (int gg = 0; gg < G; ++gg) {
-        const double mu = ld_sc1(f.scratch + (size_t)gg * 2 * N + col);
-        const double unb = ld_sc1(f.scratch + (size_t)gg * 2 * N + N + col);
-        rm = (1.f - f.momentum) * rm + f.momentum * (float)mu;
-        rv = (1.f - f.momentum) * rv + f.momentum * (float)unb;
+      for (int g0 = 0; g0 < G; g0 += GB) {
+        double vm[GB], vu[GB];
+#pragma unroll
+        for (int u = 0; u < GB; ++u) {
+          const size_t o = (size_t)min(g0 + u, G - 1) * 2 * N + col;
+          vm[u] = ld_sc1(f.scratch + o);
+          vu[u] = ld_sc1(f.scratch + o + N);
+        }
+#pragma unroll
+        for (int u = 0; u < GB; ++u) {
+          if (g0 + u >= G) break;
+          rm = (1.f - f.momentum) * rm + f.momentum * (float)vm[u];
+          rv = (1.f - f.momentum) * rv + f.momentum * (float)vu[u];
+        }
       }
       f.run_mean[col] = rm;
       f.run_var[col] = rv;
