@@ -18,10 +18,9 @@ import os
 import sys
 import time
 
-# hardware queues per process, read when HIP initialises: the step forks up to 5 streams (the
-# item tower, and per tower the lazy tables' sort + catch-up chains, functions._lookup_lazy);
-# with HIP's default 4 two of them share a queue and run serially (HIP default: 4; at most 32)
-os.environ.setdefault('GPU_MAX_HW_QUEUES', '8')
+# Hardware queues per process (GPU_MAX_HW_QUEUES) are left at the box's setting, HIP's default 4,
+# which is also what the training entry runs with; the effective value is recorded in the line.
+# Measured (tools/gpu_hwq_ab.sh, round 4): 8 queues made the C2 step 1.42 -> 3.0-3.2 ms (C3 equal).
 
 import torch  # noqa: E402
 import torch.distributed as dist
@@ -615,7 +614,8 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
                    'hip_graph': used_graph, 'final_loss': round(final_loss, 5),
                    'host_issue_ms_per_step': round(t_issue / args.steps * 1e3, 3),
                    'ids': f'zipf({zipf})' if zipf else 'uniform',
-                   'hard_negatives': hard_negatives, 'resident_batches': K},
+                   'hard_negatives': hard_negatives, 'resident_batches': K,
+                   'gpu_max_hw_queues': os.environ.get('GPU_MAX_HW_QUEUES', 'unset (HIP default 4)')},
         'roofline': roof,
         'gather_roofline': gather_roof,
         'batch_dot_roofline': batch_dot or None,
