@@ -96,9 +96,17 @@ def parse():
     ap.add_argument('--traffic', default='auto',
                     help='PMC traffic summary (tools/pmc_traffic.py output) for roofline.traffic; '
                          'auto: profiles/traffic_<config>_<dtype>.json when it matches this run')
+    ap.add_argument('--cpu-worker', nargs=2, default=None, metavar=('SPEC', 'OUT'), help=argparse.SUPPRESS)
     a = ap.parse_args()
     if a.extra is None:
-        a.extra = 'c3:fp32,c3:bf16' if a.config == 'c2' and a.batch is None and not a.zipf else ''
+        if a.config == 'c2' and a.batch is None and not a.zipf:
+            # N = 1 (the driver's BENCH line): every BASELINE workload that fits one GPU -- C3 at fp32
+            # (credited) and bf16, C3 with Zipf(1.05) ids, C5 with 10 hard negatives; N > 1 (the
+            # scaling runs): C3 data-parallel = configs[3] (C4), both precisions
+            one = int(os.environ.get('WORLD_SIZE', '1')) == 1
+            a.extra = 'c3:fp32,c3:bf16' + (',c3_zipf:fp32,c5:bf16' if one else '')
+        else:
+            a.extra = ''
     return a
 
 
@@ -155,9 +163,10 @@ def _cap_vocab(cfg, cap):
     return cfg, capped
 
 
-def _oracle_rate(cfg, seconds, B, dropout):
+def _oracle_rate(cfg, seconds, B, dropout, min_steps=1):
     """Samples/s of the oracle's training step on the bench's own first batches (seed 1000 + i,
-    the GPU rank 0's), timed after one warm-up step, for about `seconds`."""
+    the GPU rank 0's), timed after one warm-up step, for about `seconds` and at least `min_steps`
+    steps."""
     from oracle.twotower_oracle import OracleTrainer, model_state_shapes
     import copy
     cfg = copy.deepcopy(cfg)
@@ -177,20 +186,22 @@ def _oracle_rate(cfg, seconds, B, dropout):
         tr.step(batches[n % 2], maps, temperature=T)
         n += 1
         el = time.perf_counter() - t0
-        if el >= seconds or n >= 200:
+        if (el >= seconds and n >= min_steps) or n >= 200:
             break
     return n * B / el, n, el
 
 
-def cpu_baseline(cfg, seconds, B):
+def cpu_baseline(cfg, seconds, B, min_steps=10, legs=('config', '0')):
     """The oracle (CPU restatement of the reference step, fp32) on a bounded sample of the same
     workload: the configured batch B and the GPU's own batches, dropout as configured and p = 0
     (half the time each), on the torch threads of the box's CPU share. Tables above CPU_VOCAB_CAP
     rows are capped (the oracle's dense Adam over a 100M x 64 table and its state exceed the
     box's host-memory limit); the sample says so."""
     cfg, capped = _cap_vocab(cfg, CPU_VOCAB_CAP)
-    rate, n, el = _oracle_rate(cfg, seconds / 2, B, 'config')
-    rate0, n0, el0 = _oracle_rate(cfg, seconds / 2, B, '0')
+    rate, n, el = _oracle_rate(cfg, seconds / len(legs), B, 'config', min_steps)
+    rate0 = n0 = el0 = None
+    if '0' in legs:
+        rate0, n0, el0 = _oracle_rate(cfg, seconds / len(legs), B, '0', min_steps)
     model = None
     try:
         for line in open('/proc/cpuinfo'):
@@ -200,11 +211,58 @@ def cpu_baseline(cfg, seconds, B):
     except OSError:
         pass
     return {'value': round(rate, 1), 'unit': 'samples/s', 'cores': torch.get_num_threads(),
-            'kind': 'port', 'value_p0': round(rate0, 1),
+            'kind': 'port', 'value_p0': None if rate0 is None else round(rate0, 1),
             'sample': f'{n} steps x batch {B} (the GPU run\'s first batches; oracle, fp32, dropout as '
-                      f'configured), {el:.1f} s; p = 0 leg: {n0} steps, {el0:.1f} s' +
-                      (f'; tables capped at {CPU_VOCAB_CAP:,} rows (host memory)' if capped else ''),
-            'nproc': os.cpu_count(), 'cpu_model': model}
+                      f'configured), {el:.1f} s' + ('' if rate0 is None else f'; p = 0 leg: {n0} steps, {el0:.1f} s') +
+                      (f'; tables capped at {CPU_VOCAB_CAP:,} rows (host memory)' if capped else '') +
+                      f'; {torch.get_num_threads()} torch threads of {os.cpu_count()} host cores (the '
+                      f'GPU box\'s CPU share is 16 threads)',
+            'threads': torch.get_num_threads(), 'nproc': os.cpu_count(), 'cpu_model': model}
+
+
+def cpu_worker(spec_path, out_path):
+    """The CPU baselines of one bench run, in a child process started before the GPU is touched:
+    it runs on the host cores while the parent times the GPU workloads, so the samples can be
+    long (>= 10 steps per leg) without lengthening the run. Writes {key: cpu_baseline} as each
+    finishes."""
+    spec = json.load(open(spec_path))
+    res = {}
+    for job in spec['jobs']:
+        cfg = yaml.safe_load(open(os.path.join(ROOT, 'configs', f"{job['config']}.yaml")))
+        if job.get('zipf'):
+            cfg.setdefault('synthetic', {})['zipf'] = job['zipf']
+        try:
+            res[job['key']] = cpu_baseline(cfg, job['seconds'], job['batch'], job['min_steps'], tuple(job['legs']))
+        except Exception as e:  # a baseline must not cost the line
+            res[job['key']] = {'error': repr(e)[:300]}
+        json.dump(res, open(out_path + '.tmp', 'w'))
+        os.replace(out_path + '.tmp', out_path)
+
+
+def start_cpu_worker(jobs):
+    """-> (process, result path). Started before any HIP call of this process: the child is a
+    plain CPU python (it never touches the GPU)."""
+    import subprocess
+    import tempfile
+    d = tempfile.mkdtemp(prefix='rsys_cpu_')
+    spec, out = os.path.join(d, 'spec.json'), os.path.join(d, 'out.json')
+    json.dump({'jobs': jobs}, open(spec, 'w'))
+    env = dict(os.environ, HIP_VISIBLE_DEVICES='', CUDA_VISIBLE_DEVICES='', ROCR_VISIBLE_DEVICES='')
+    proc = subprocess.Popen([sys.executable, os.path.abspath(__file__), '--cpu-worker', spec, out], env=env,
+                            stdout=subprocess.DEVNULL, stderr=open(os.path.join(d, 'err.log'), 'w'))
+    return proc, out
+
+
+def collect_cpu_worker(proc, out, timeout):
+    try:
+        proc.wait(timeout=timeout)
+    except Exception:
+        proc.kill()
+        proc.wait()
+    try:
+        return json.load(open(out))
+    except Exception:
+        return {}
 
 
 def measure_peaks(dev, copy_bytes=1 << 31, reps=5):
@@ -302,6 +360,66 @@ def load_cfg(name, args):
     return cfg
 
 
+# Lazy-exact Adam's per-row work (csrc/lookup.hip, sparse.hip; adam.h), priced per distinct row
+# of a sorted call (flat.profile_call_rows: [(D, lookups, distinct rows)] of the priced steps):
+#   catch-up: p, m, v read, p written (weight decay 0: the moments are replayed in registers),
+#             `last` read + written;
+#   Adam    : p, g, m, v read, p, m, v written, g re-zeroed, `last` read + written;
+#   sqnorm  : g read.
+LAZY_ROW_BYTES = {
+    'rs_sorted_catchup': lambda rows: sum(r * (16.0 * D + 16.0) for D, _, r in rows),
+    'rs_sorted_adam_batch': lambda rows: sum(r * (32.0 * D + 16.0) for D, _, r in rows),
+    'rs_sorted_sqnorm_batch': lambda rows: sum(r * 4.0 * D for D, _, r in rows),
+}
+LAZY_ENTRIES = ('rs_lookup_sort', 'rs_sorted_catchup', 'rs_segsum', 'rs_sorted_sqnorm_batch', 'rs_sorted_adam_batch')
+
+
+def optimizer_roofline(summ, rows, flat_numel, dense_numel, ms_step, args, B, name, dtype, zipf, hard_negatives):
+    """the reference's optimizer sweeps every parameter, 28 B/param/step ('dense
+    equivalent': C3 2.69B params -> 75 GB); lazy-exact Adam moves the touched rows only. Reports
+    both, and the lazy chain (sort, catch-up, segment sum, clip partials, sorted Adam) and the
+    dense Adam over the non-table parameters as bytes / event time against 8 TB/s, with the
+    PMC traffic of the catch-up and the Adam step where collected on this workload. None
+    without large tables."""
+    if not rows:
+        return None
+    steps = 3.0  # the instrumented pass
+    ent = {}
+    tot_ms = tot_by = 0.0
+    for k in LAZY_ENTRIES + ('rs_adam_step',):
+        if k not in summ:
+            continue
+        ms = summ[k]['ms'] / steps
+        by = (LAZY_ROW_BYTES[k](rows) if k in LAZY_ROW_BYTES else summ[k]['bytes']) / steps
+        if k == 'rs_adam_step':
+            by = 28.0 * dense_numel  # the dense Adam covers [0, dense_numel) only
+        ent[k] = {'ms_per_step': round(ms, 4), 'bytes_per_step': round(by),
+                  'GBs': round(by / (ms * 1e-3) / 1e9, 1) if ms > 0 else None,
+                  'frac': round(by / (ms * 1e-3) / (PEAK_HBM_GBS * 1e9), 4) if ms > 0 else None}
+        tr = load_traffic(args, B, k, name, dtype, zipf, hard_negatives, suffix='_' + k.replace('rs_', ''))
+        if tr:
+            ent[k]['traffic'] = tr['hbm_bytes_per_launch']
+            ent[k]['traffic_detail'] = tr
+        tot_ms += ms
+        tot_by += by
+    dense_eq = 28.0 * flat_numel
+    distinct = sum(r for _, _, r in rows) / steps
+    lookups = sum(n for _, n, _ in rows) / steps
+    return {'dense_equivalent_bytes_per_step': round(dense_eq),
+            'dense_equivalent_ms_at_8TBs': round(dense_eq / (PEAK_HBM_GBS * 1e9) * 1e3, 3),
+            'params': flat_numel,
+            'lazy_bytes_per_step': round(tot_by), 'lazy_ms_per_step': round(tot_ms, 4),
+            'lazy_GBs': round(tot_by / (tot_ms * 1e-3) / 1e9, 1) if tot_ms > 0 else None,
+            'frac': round(tot_by / (tot_ms * 1e-3) / (PEAK_HBM_GBS * 1e9), 4) if tot_ms > 0 else None,
+            'lazy_share_of_step': round(tot_ms / ms_step, 3),
+            'bytes_ratio_dense_over_lazy': round(dense_eq / max(tot_by, 1.0), 1),
+            'table_rows_stepped_per_step': round(distinct), 'table_lookups_per_step': round(lookups),
+            'entries': ent,
+            'model': '28 B/param dense (SURVEY 8d); per distinct row: catch-up 16D+16 B, Adam 32D+16 B, '
+                     'clip partials 4D B; sort and segment sum as profiling.WORK; event time with the '
+                     'towers serial (instrumented pass)'}
+
+
 def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_seconds, peaks=None):
     """Build the model of workload `name`, time args.steps steps (after args.warmup) cycling through
     args.batches distinct resident batches, profile one instrumented pass. Returns the result dict
@@ -326,7 +444,7 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
         model = TwoTowerModel(GenericTower(cfg, 'user_tower'), GenericTower(cfg, 'item_tower'),
                               maps['user'], maps['item']).to(dev)
     model.train()
-    ensure_flat(model)
+    n_sharded = sum(t.shard is not None for t in ensure_flat(model).lazy)  # W >= 4: row-sharded tables
     rdist.broadcast_model(model)
     opt = Adam(model.parameters(), lr=float(cfg['train']['learning_rate']))
     opt.grad_scale = 1.0 / world
@@ -401,11 +519,17 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
             target = max(kt.summary().items(), key=lambda kv: kv[1]['ms'])[0]
         torch.cuda.synchronize()
         next_batch()
+        from recommendsystemproject_amd import flat as _flat
+        _flat.PROFILE_CALLS = []
         with PmcBracket(target) as pb:
             fwd_bwd()
             allreduce()
             opt_step()
         torch.cuda.synchronize()
+        rows = _flat.profile_call_rows(_flat.PROFILE_CALLS)
+        _flat.PROFILE_CALLS = None
+        if target in LAZY_ROW_BYTES:  # per-row work: priced from this step's distinct-row counts
+            pb.bytes = LAZY_ROW_BYTES[target](rows)
         if rank == 0:
             print(json.dumps({'pmc_bracket': target, 'launches': pb.launches,
                               'alg_bytes_per_launch': pb.bytes / max(pb.launches, 1),
@@ -488,12 +612,19 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
     tower_streams = os.environ.get('RSYS_TOWER_STREAMS')
     os.environ['RSYS_TOWER_STREAMS'] = '0'
     torch.cuda._sleep(int(2.4e9 * 0.03))  # ~30 ms at the 2.4 GHz shader clock
+    from recommendsystemproject_amd import flat as _flat
+    _flat.PROFILE_CALLS = []  # the large tables' sorted calls of these steps (distinct-row counts)
     with KernelTimer() as kt:
         for _ in range(3):
             next_batch()
             fwd_bwd()
             allreduce()
             opt_step()
+    lazy_rows = _flat.profile_call_rows(_flat.PROFILE_CALLS)
+    _flat.PROFILE_CALLS = None
+    fl_ = ensure_flat(model)
+    flat_numel = sum(int(p.numel()) for p in fl_.params)  # every parameter (full tables)
+    dense_numel = fl_.dense_numel
     if tower_streams is None:
         del os.environ['RSYS_TOWER_STREAMS']
     else:
@@ -586,13 +717,13 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
                           'mfma_frac': round(g['flops'] / sec / 1e12 / (PEAK_BF16_TFLOPS if dtype == 'bf16' else PEAK_F32_TFLOPS), 4),
                           'exp_frac': round(g['exps'] / sec / PEAK_EXP_PER_S, 4)}
 
+    opt_roof = optimizer_roofline(summ, lazy_rows, flat_numel, dense_numel, ms_step=el / args.steps * 1e3,
+                                  args=args, B=B, name=name, dtype=dtype, zipf=zipf, hard_negatives=hard_negatives)
     used_graph = graphs is not None
     _COPY_PLANS.clear()  # the plans hold this workload's batch tensors (and key on their ids)
     del model, opt, batches, batch, graphs, catalog
     torch.cuda.empty_cache()
     cpu = None
-    if rank == 0 and world == 1 and cpu_seconds > 0:
-        cpu = cpu_baseline(cfg, cpu_seconds, B)
 
     if rank != 0:
         return None
@@ -615,20 +746,54 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
                    'host_issue_ms_per_step': round(t_issue / args.steps * 1e3, 3),
                    'ids': f'zipf({zipf})' if zipf else 'uniform',
                    'hard_negatives': hard_negatives, 'resident_batches': K,
-                   'gpu_max_hw_queues': os.environ.get('GPU_MAX_HW_QUEUES', 'unset (HIP default 4)')},
+                   'gpu_max_hw_queues': os.environ.get('GPU_MAX_HW_QUEUES', 'unset (HIP default 4)'),
+                   'row_sharded_tables': n_sharded},
         'roofline': roof,
         'gather_roofline': gather_roof,
         'batch_dot_roofline': batch_dot or None,
         'softmax_roofline': softmax or None,
         'step_roofline': step_roof,
+        'optimizer_roofline': opt_roof,
         'cpu_baseline': cpu,
         'kernel_ms_per_step': {k: round(v['ms'] / 3, 4) for k, v in sorted(summ.items(), key=lambda kv: -kv[1]['ms'])},
         '_gemm_shapes': kt.gemm_shapes() if os.environ.get('RSYS_BENCH_DETAIL') else None,
     }
 
 
+def _cpu_jobs(args):
+    """The CPU baselines of this run (rank 0, N = 1): the primary workload, each extra workload's
+    config once, and C1 (BASELINE configs[0]). >= 10 steps per leg (C5: 2 steps, one leg -- its
+    oracle step at L = 200 with 10M-row tables takes tens of seconds on the host)."""
+    jobs, seen = [], set()
+
+    def add(key, config, zipf=None):
+        if (config, zipf) in seen:
+            return
+        seen.add((config, zipf))
+        c = yaml.safe_load(open(os.path.join(ROOT, 'configs', f'{config}.yaml')))
+        B = args.batch or int(c['train']['batch_size'])
+        big = config == 'c5'
+        jobs.append({'key': key, 'config': config, 'zipf': zipf, 'batch': B,
+                     'seconds': 5.0 if big else args.cpu_baseline_seconds,
+                     'min_steps': 2 if big else 10, 'legs': ['config'] if big else ['config', '0']})
+    add(args.config, args.config, args.zipf)
+    for ex in [e for e in (args.extra or '').split(',') if e]:
+        nm = ex.partition(':')[0]
+        add(nm, 'c3' if nm == 'c3_zipf' else nm, 1.05 if nm == 'c3_zipf' else None)
+    add('c1', 'c1')
+    return jobs
+
+
 def main():
     args = parse()
+    if args.cpu_worker:
+        cpu_worker(*args.cpu_worker)
+        return
+    cpu_s = 0.0 if args.no_cpu_baseline else args.cpu_baseline_seconds
+    worker = None
+    if int(os.environ.get('WORLD_SIZE', '1')) == 1 and cpu_s > 0 and not args.pmc_bracket:
+        # before any HIP call of this process: the CPU baselines run beside the GPU timing
+        worker = start_cpu_worker(_cpu_jobs(args))
     rdist.init_from_env()
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
@@ -639,7 +804,6 @@ def main():
     torch.cuda.set_device(dev)
     if args.dtype == 'config':
         args.dtype = 'bf16' if args.config in ('c2', 'c3', 'c5') else 'fp32'
-    cpu_s = 0.0 if args.no_cpu_baseline else args.cpu_baseline_seconds
     peaks = None if args.pmc_bracket else measure_peaks(dev)
     out = run_workload(args, args.config, args.dtype, args.zipf, args.hard_negatives, rank, world, dev,
                        cpu_s, peaks)
@@ -649,7 +813,6 @@ def main():
         return
     extras = {}
     order = [args.config]
-    cpu_done = set()
     for ex in [e for e in (args.extra or '').split(',') if e]:
         # the other headline workloads in the same line (BASELINE configs[2] = C3; at N > 1 the
         # same run is configs[3] = C4, C3 data-parallel). NAME:DTYPE; the reference computes in
@@ -659,9 +822,11 @@ def main():
         key = name if ex_dtype == 'fp32' else f'{name}_{ex_dtype}'
         if (name, ex_dtype) == (args.config, args.dtype):
             continue
+        zipf = 1.05 if name == 'c3_zipf' else None  # C3 with Zipf(1.05) ids
+        cfg_name = 'c3' if name == 'c3_zipf' else name
         try:
-            r = run_workload(args, name, ex_dtype, None, 10 if name == 'c5' else 0, rank, world, dev,
-                             0.0 if name in cpu_done else cpu_s / 2, peaks)
+            r = run_workload(args, cfg_name, ex_dtype, zipf, 10 if name == 'c5' else 0, rank, world, dev, 0.0,
+                             peaks)
         except Exception as e:  # an extra workload must not cost the headline line
             import traceback
             traceback.print_exc(file=sys.stderr)
@@ -669,20 +834,26 @@ def main():
             r = None
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
-        cpu_done.add(name)
         order.append(key)
         if r is not None:
             extras[key] = {k: r[k] for k in ('value', 'unit', 'ms_per_step', 'dtype', 'config', 'roofline',
                                              'gather_roofline', 'batch_dot_roofline', 'softmax_roofline',
-                                             'step_roofline', 'cpu_baseline', 'kernel_ms_per_step')}
+                                             'step_roofline', 'optimizer_roofline', 'cpu_baseline',
+                                             'kernel_ms_per_step')}
             if ex_dtype != 'fp32':
                 extras[key]['note'] = (f'{ex_dtype} compute mode, beside the fp32 entry "{name}" (the '
                                        "reference's precision)")
-    if rank == 0 and world == 1 and cpu_s > 0:
-        # BASELINE configs[0] (C1): the reference's CPU-runnable case -- demo schema without the
-        # sequence encoder, batch 256 -- on the CPU restatement, beside the GPU numbers
-        c1 = load_cfg('c1', args)
-        out['c1_cpu_baseline'] = cpu_baseline(c1, min(cpu_s, 10.0), int(c1['train']['batch_size']))
+    if worker is not None:
+        # the CPU baselines ran beside the GPU timing; C1 = BASELINE configs[0], the reference's
+        # CPU-runnable case (demo schema without the sequence encoder, batch 256)
+        cpu = collect_cpu_worker(*worker, timeout=600)
+        if rank == 0:
+            out['cpu_baseline'] = cpu.get(args.config)
+            for key in extras:
+                nm = key.rsplit('_bf16', 1)[0] if key.endswith('_bf16') else key
+                if 'error' not in extras[key]:
+                    extras[key]['cpu_baseline'] = cpu.get(nm)
+            out['c1_cpu_baseline'] = cpu.get('c1')
     if rank == 0:
         out['peaks_measured'] = peaks
         if args.prof_markers:

@@ -302,7 +302,7 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
     const bool rare = (t0 == o_base) | (t0 + kTile > B) | !wave_ok;  // wave-uniform
     if constexpr (MODE == 0) {
       if constexpr (F32) {
-        if (o_ok) {
+        if (o_ok && a.S) {  // S is stored only when a backward will read it
           float* sp = a.S + (int64_t)o * a.ldS + t0 + 4 * h;
 #pragma unroll
           for (int g4 = 0; g4 < 4; ++g4)
@@ -595,7 +595,7 @@ int ce_fused_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_
                  const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T, float* lse,
                  float* row_loss, float* loss, float* S, float* ws, void* stream) {
   const char* fn = F32 ? "rs_inbatch_ce_fused_f32_fwd" : "rs_inbatch_ce_fused_fwd";
-  RS_CHECK_ARG(U && I && lse && row_loss && loss && ws && (!F32 || S), "%s: null pointer", fn);
+  RS_CHECK_ARG(U && I && lse && row_loss && loss && ws, "%s: null pointer", fn);  // S: optional
   RS_CHECK_ARG(B >= 1 && (D == 64 || D == 128) && N >= 0 && N <= 64,
                "%s: needs D in {64, 128}, N <= 64 (B=%d N=%d D=%d)", fn, B, N, D);
   RS_CHECK_ARG(N == 0 || Hn, "%s: hard negatives need H", fn);

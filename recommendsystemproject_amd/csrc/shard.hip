@@ -124,25 +124,28 @@ __device__ __forceinline__ int64_t run_head(const uint32_t* keys, int64_t hi, ui
 }
 
 // every sorted position: the gather index of its lookup (lookup order) and its segment-sum key
-// (sorted order; padding / out-of-range / overflowed -> sentinel, no gradient)
+// (sorted order; padding / out-of-range / overflowed -> sentinel, no gradient). A lookup whose id
+// is out of range or overflowed its owner's bucket reads `zrow`, the zero row the requester keeps
+// after the returned buckets -- never another id's row (both are flagged and raise at the next
+// check_errors)
 __global__ __launch_bounds__(256) void shard_fill_kernel(const uint32_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals, int64_t n,
-                                                         int64_t pad, const int* __restrict__ comp,
+                                                         int64_t pad, const int* __restrict__ comp, int64_t zrow,
                                                          int64_t* __restrict__ idx, uint32_t* __restrict__ ckey,
                                                          int* __restrict__ flag) {
   bool bad = false;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t k = keys[i];
     const uint32_t e = vals[i];
-    if (k == kSentinel) {  // out-of-range id: the reference's IndexError (flagged; reads row 0)
+    if (k == kSentinel) {  // out-of-range id: the reference's IndexError (flagged; reads zeros)
       bad = true;
-      idx[e] = 0;
+      idx[e] = zrow;
       ckey[i] = kSentinel;
       continue;
     }
     const int64_t h = is_head(keys, i, k) ? i : run_head(keys, i, k);
     const int c = comp[h];
-    idx[e] = c < 0 ? 0 : c;
+    idx[e] = c < 0 ? zrow : c;
     ckey[i] = (c < 0 || (int64_t)k == pad) ? kSentinel : (uint32_t)c;
   }
   if (bad && flag) atomicOr(flag, 1);
@@ -199,8 +202,8 @@ extern "C" int rs_shard_bucket(const uint32_t* keys, const uint32_t* vals, int64
   RS_CHECK_LAUNCH("rs_shard_bucket scan");
   shard_assign_kernel<<<nb, kBT, 0, st>>>(keys, n, world, cap, block_base, send_ids, comp);
   RS_CHECK_LAUNCH("rs_shard_bucket assign");
-  shard_fill_kernel<<<std::min<int64_t>(cdiv(n, 256), 8192), 256, 0, st>>>(keys, vals, n, pad, comp, idx, ckey,
-                                                                           flag);
+  shard_fill_kernel<<<std::min<int64_t>(cdiv(n, 256), 8192), 256, 0, st>>>(keys, vals, n, pad, comp,
+                                                                           (int64_t)world * cap, idx, ckey, flag);
   RS_CHECK_LAUNCH("rs_shard_bucket fill");
   return 0;
 }

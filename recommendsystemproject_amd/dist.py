@@ -27,6 +27,7 @@ reduce-scatter per-rank partial bags, their backward all-gathers the bag gradien
 from __future__ import annotations
 
 import os
+import threading
 
 import torch
 import torch.distributed as dist
@@ -36,7 +37,7 @@ from .flat import SEG_MEAN, SEG_SUM, ensure_flat, flat_of
 
 
 def is_active() -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1 and not _AGREE.local
 
 
 def init_from_env(backend=None):
@@ -98,22 +99,126 @@ def sync_seed(src: int = 0) -> int:
 EMPTY_ID = -(1 << 31)  # the pad slot of a ragged call's id exchange (csrc/lookup.hip kEmptyId)
 
 
+class _Agreement(threading.local):
+    """This forward's batch shapes agreed over the ranks (agree_batch): per batch tensor its
+    per-dimension maxima over the ranks and whether any rank's dimension differs."""
+
+    def __init__(self):
+        self.table = None   # {(data_ptr, shape): (max dims, ragged)} of this forward's batch
+        self.sig = None     # the local shape signature of the last agreed batch
+        self.static = False  # the last agreed batch had the same shapes on every rank
+        self.local = 0      # local_only() depth: this process steps alone (no collective)
+
+
+_AGREE = _Agreement()
+
+
+class local_only:
+    """`with local_only(): ...` -- the model steps alone inside a distributed job (a single-rank
+    emulation or evaluation on one rank): no collective is issued for its shapes or gradients."""
+
+    def __enter__(self):
+        _AGREE.local += 1
+        return self
+
+    def __exit__(self, *exc):
+        _AGREE.local -= 1
+        return False
+
+
+def _batch_tensors(b, out):
+    """The tensors of a batch dict in a fixed order (sorted keys; lists in order; a materialised
+    hard-negative list's stacked batch): the same order on every rank of one config."""
+    if isinstance(b, torch.Tensor):
+        out.append(b)
+    elif isinstance(b, dict):
+        for k in sorted(b, key=str):
+            _batch_tensors(b[k], out)
+    elif isinstance(b, (list, tuple)):
+        for v in b:
+            _batch_tensors(v, out)
+        st = getattr(b, 'stacked', None)
+        if st is not None:
+            _batch_tensors(st, out)
+    return out
+
+
+def agree_batch(batch) -> None:
+    """ONE all-reduce per forward (TwoTowerModel.forward) of every batch tensor's shape: the
+    lookup calls of the large tables then take their common shapes from it (agreed_dims) instead of
+    one blocking all-reduce per call. Ranks' batches of equal shapes (the bench's, a loader with
+    drop_last and equal list lengths) need nothing more; ragged ones (the collate pads each
+    batch's lists to its own longest) pad every call to the per-dimension maxima.
+    Inside a hipGraph capture nothing can be exchanged: the batch must have the shapes of the last
+    eagerly agreed one, and that one must have been equal on every rank; otherwise this raises
+    (the ranks' collectives would not match and the job would hang)."""
+    if not is_active() or _AGREE.local:
+        return
+    ts = _batch_tensors(batch, [])
+    sig = tuple(tuple(int(d) for d in t.shape) for t in ts)
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        if sig != _AGREE.sig or not _AGREE.static:
+            raise RuntimeError('rsys data parallel: a batch captured into a hipGraph must have the shapes '
+                               'of the last eager step, equal on every rank (run one eager step on the '
+                               'captured shapes first)')
+        _AGREE.table = {(t.data_ptr(), tuple(t.shape)): (tuple(t.shape), False) for t in ts}
+        return
+    flat = [len(sig)] + [len(x) for x in sig] + [d for x in sig for d in x]
+    dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend() == 'nccl' else torch.device('cpu')
+    v = torch.tensor(flat + [-x for x in flat], dtype=torch.int64, device=dev)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    v = v.tolist()
+    n = len(flat)
+    mx, mn = v[:n], [-x for x in v[n:]]
+    if mx[:1 + len(sig)] != mn[:1 + len(sig)]:
+        raise RuntimeError('rsys data parallel: the ranks\' batches hold different tensors (same config?)')
+    table, at = {}, 1 + len(sig)
+    for t, shp in zip(ts, sig):
+        k = len(shp)
+        dims_max = tuple(mx[at:at + k])
+        table[(t.data_ptr(), shp)] = (dims_max, dims_max != tuple(mn[at:at + k]))
+        at += k
+    _AGREE.table = table
+    _AGREE.sig = sig
+    _AGREE.static = all(not r for _, r in table.values())
+
+
+def agreed_dims(t):
+    """(per-dimension maxima over the ranks, ragged?) of batch tensor t as this forward's
+    agree_batch saw it, or None (not a batch tensor, or no agreement this step)."""
+    if _AGREE.table is None or t is None:
+        return None
+    return _AGREE.table.get((t.data_ptr(), tuple(int(d) for d in t.shape)))
+
+
+def clear_agreement():
+    """End of the step's collectives (allreduce_gradients): later lookups outside a
+    TwoTowerModel forward agree per call again."""
+    _AGREE.table = None
+
+
 def agree_max(*vals):
-    """The max over ranks of each host int (one tiny all-reduce + host sync). The ranks' lookup
-    calls can differ in shape -- the collate pads the history to each batch's longest -- and the
-    all-gathers / all-to-alls need one shape, so ragged calls are padded to the ranks' maxima.
-    Inside a hipGraph capture (bench.py) no sync is possible: the shapes are static there and
-    must be equal on every rank."""
-    if not is_active() or torch.cuda.is_current_stream_capturing():
+    """The max over ranks of each host int (one tiny all-reduce + host sync): the fallback for a
+    lookup call whose shape agree_batch did not cover (a tower called outside TwoTowerModel).
+    Inside a hipGraph capture no exchange is possible: raises unless this step's batch was
+    agreed equal on every rank (then the local values are everyone's)."""
+    if not is_active() or _AGREE.local:
         return list(vals)
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        if _AGREE.table is not None and _AGREE.static:
+            return list(vals)
+        raise RuntimeError('rsys data parallel: a lookup shape cannot be agreed inside a hipGraph capture')
     dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend() == 'nccl' else torch.device('cpu')
     t = torch.tensor(vals, dtype=torch.int64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [int(x) for x in t.tolist()]
 
 
-def call_shape(rows, bag):
-    """(rows_max, bag_max, ragged) over the ranks for a [rows, bag] lookup call."""
+def call_shape(rows, bag, agreed=None):
+    """(rows_max, bag_max, ragged) over the ranks for a [rows, bag] lookup call; `agreed`: the
+    same triple derived from agree_batch (no collective)."""
+    if agreed is not None:
+        return agreed
     rmax, rmin, bmax, bmin = agree_max(rows, -rows, bag, -bag)
     return rmax, bmax, rmax != -rmin or bmax != -bmin
 
@@ -291,6 +396,7 @@ def allreduce_gradients(model: torch.nn.Module, optimizer=None):
         allreduce_flat_grad(f.grad[lo:hi])
     if f.lazy:
         exchange_lazy_grads(f)
+    clear_agreement()
     from .optim import Adam
     world = dist.get_world_size()
     if isinstance(optimizer, Adam):
@@ -406,7 +512,7 @@ def exchange_table(t):
         ids = bufs.get(('ids', i), (c.n,), torch.int32, dev)
         _hip.call('rs_pack_ids', c.ids_ptr, c.id_bytes, c.rows, c.bag, c.row_stride, ids.data_ptr(),
                   _stream())
-        rmax, bmax, ragged = call_shape(c.rows, c.bag)
+        rmax, bmax, ragged = call_shape(c.rows, c.bag, c.agreed)
         g, mode = c.dseg, c.mode
         if ragged:
             # pad to the ranks' common shape: pad ids sort last (skipped), pad rows are zero; a

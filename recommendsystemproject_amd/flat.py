@@ -44,6 +44,25 @@ from . import _hip
 ALIGN = 16  # floats (64 B)
 
 
+PROFILE_CALLS = None  # profiling only (bench.py): a list receiving (D, keys, n) of every sorted call
+
+
+def profile_call_rows(calls):
+    """[(D, lookups, distinct rows)] of recorded sorted calls (keys ascending; out-of-range ids
+    sort last as 0xFFFFFFFF and are not rows). One host sync: profiling passes only."""
+    out = []
+    for D, keys, n in calls or ():
+        if n == 0:
+            out.append((D, 0, 0))
+            continue
+        k = keys[:n]
+        valid = k != -1
+        heads = torch.ones_like(k, dtype=torch.bool)
+        heads[1:] = k[1:] != k[:-1]
+        out.append((D, n, int((heads & valid).sum())))
+    return out
+
+
 def lazy_rows_threshold() -> int:
     return int(os.environ.get('RSYS_LAZY_ROWS', 1 << 16))
 
@@ -57,7 +76,8 @@ class LookupCall:
     workspace are allocated on the forward's stream and held here until the step ends."""
 
     __slots__ = ('keys', 'vals', 'ws', 'n', 'rows', 'bag', 'pad', 'mode', 'ids_ptr',
-                 'id_bytes', 'row_stride', 'keep', 'dseg', 'local_rows', 'own_rows', 'prescale', 'a2a')
+                 'id_bytes', 'row_stride', 'keep', 'dseg', 'local_rows', 'own_rows', 'prescale', 'a2a',
+                 'agreed')
 
     def __init__(self, keys, vals, n, rows, bag, pad, mode, ids_ptr, id_bytes, row_stride, keep, ws=None):
         self.keys, self.vals, self.n, self.rows, self.bag = keys, vals, n, rows, bag
@@ -69,6 +89,7 @@ class LookupCall:
         self.own_rows = None  # ragged row-sharded bags: this rank's rows of the padded local_rows
         self.prescale = None  # ragged mean bags: 1 / this rank's bag length (union summed as SUM)
         self.a2a = None  # all-to-all row-sharded call: the requester side (A2ARequest)
+        self.agreed = None  # data parallel: (rows, bag, ragged) over the ranks (dist.agree_batch)
 
 
 # rs_segsum modes: one id per gradient row, mean bag, sum bag (max pooling: atomic scatter)
@@ -135,11 +156,13 @@ class LazyTable:
         ws = torch.empty(wsb // 4 + 1, dtype=torch.int32, device=dev) if wsb else None
         _hip.call('rs_lookup_sort', ids_ptr, id_bytes, rows, bag, row_stride, self.V, keys.data_ptr(),
                   vals.data_ptr(), None if ws is None else ws.data_ptr(), _stream())
+        if PROFILE_CALLS is not None:
+            PROFILE_CALLS.append((self.D, keys, n))
         return LookupCall(keys, vals, n, rows, bag, -1 if pad is None else int(pad), mode, ids_ptr,
                           id_bytes, row_stride, keep, ws)
 
     def lookup(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None, record=True,
-               read_through=False):
+               read_through=False, agreed=None):
         """Forward hook: bring the call's rows to the current optimizer step before they are
         gathered and, when the step will train on this lookup (`record`), list it for the step
         with its ids sorted by row. Default: sort, then rs_sorted_catchup over the distinct rows.
@@ -151,6 +174,7 @@ class LazyTable:
         c = None
         if record:
             c = self.sort_call(ids_ptr, rows, bag, row_stride, pad, mode, id_bytes, keep)
+            c.agreed = agreed
             self.calls.append(c)
         opt = self.flat.lazy_opt
         if opt is None or rows * bag == 0 or (c is not None and read_through):
@@ -198,7 +222,9 @@ class LazyTable:
             _hip.call('rs_lookup_sort', seg.idx, 8, rows, 1, seg.idx_stride, self.V_full, keys.data_ptr(),
                       vals.data_ptr(), None if ws is None else ws.data_ptr(), _stream())
         from .dist import agree_max
-        cap = shard_capacity(agree_max(n)[0], W)  # one bucket shape on every rank (ragged calls)
+        agreed = getattr(seg, 'agreed', None)
+        # one bucket shape on every rank (ragged calls): from the forward's batch agreement
+        cap = shard_capacity(agreed[0] if agreed is not None else agree_max(n)[0], W)
         send_ids = torch.empty(W * cap, dtype=torch.int32, device=dev)
         counts = torch.empty(W, dtype=torch.int32, device=dev)
         ckey = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
@@ -230,13 +256,15 @@ class LazyTable:
         gs.kind, gs.dim, gs.out_col, gs.pool_mode, gs.bag, gs.pad_idx = _hip.RS_SEG_SPARSE, self.D, 0, 0, 1, -1
         gs.vocab, gs.idx_stride, gs.idx, gs.table = self.V, 1, ids64.data_ptr(), self.ptr(self.flat.data)
         ops.gather_fwd([gs], W * cap, send_rows, None)
-        recv_rows = torch.empty_like(send_rows)
-        all_to_all(recv_rows, send_rows)
+        # the returned buckets, then one zero row: the row an out-of-range or overflowed lookup reads
+        recv_rows = torch.empty(W * cap + 1, self.D, device=dev)
+        recv_rows[W * cap].zero_()
+        all_to_all(recv_rows[:W * cap], send_rows)
         # this rank's lookups read their rows out of the returned buckets
         out = _hip.FeatureSeg()
         out.kind, out.dim, out.out_col, out.pool_mode, out.bag, out.pad_idx = (_hip.RS_SEG_SPARSE, self.D,
                                                                                  seg.out_col, 0, 1, -1)
-        out.vocab, out.idx_stride, out.idx, out.table = W * cap, 1, idx.data_ptr(), recv_rows.data_ptr()
+        out.vocab, out.idx_stride, out.idx, out.table = W * cap + 1, 1, idx.data_ptr(), recv_rows.data_ptr()
         keep = (idx, recv_rows)
         if not record:
             return None, out, keep
@@ -263,7 +291,7 @@ class LazyTable:
             _hip.call('rs_pack_ids', seg.idx, 8, rows, bag, seg.idx_stride, ids32.data_ptr(), _stream())
         # ranks' calls of different shapes (the collate pads to each batch's longest bag): padded to
         # the common [rmax, bmax] with empty slots (dist.EMPTY_ID: no row, no gradient)
-        rmax, bmax, ragged = call_shape(rows, bag)
+        rmax, bmax, ragged = call_shape(rows, bag, getattr(seg, 'agreed', None))
         if ragged and n:
             ids32 = pad_ids(ids32, rows, bag, rmax, bmax)
         nm = rmax * bmax
@@ -416,8 +444,8 @@ def _stream():
 
 
 def _dp_active():
-    d = torch.distributed
-    return d.is_available() and d.is_initialized() and d.get_world_size() > 1
+    from .dist import is_active  # a rank stepping alone (dist.local_only) is not data parallel
+    return is_active()
 
 
 def _is_lazy(p, lazy_ids):
@@ -658,14 +686,16 @@ def gather_shards(local, t):
     return unshard(parts, t.V_full)
 
 
-def lookup_table(weight, ids_ptr, rows, bag, row_stride, pad, mode, keep=None, record=True, read_through=False):
+def lookup_table(weight, ids_ptr, rows, bag, row_stride, pad, mode, keep=None, record=True, read_through=False,
+                 agreed=None):
     """Forward-side hook of the custom ops for a table lookup: a LookupCall for large
     (lazy-Adam) tables (None for ordinary ones, and for a lookup no backward follows: `record`
     False, the rows are only brought current)."""
     t = getattr(weight, '_rs_lazy', None)
     if t is None or flat_of(weight) is not t.flat:
         return None
-    return t.lookup(ids_ptr, rows, bag, row_stride, pad, mode, keep=keep, record=record, read_through=read_through)
+    return t.lookup(ids_ptr, rows, bag, row_stride, pad, mode, keep=keep, record=record, read_through=read_through,
+                    agreed=agreed)
 
 
 def grad_of(p):

@@ -40,6 +40,19 @@ def _pad(v):
     return -1 if v is None else int(v)
 
 
+def _agreed(x, tokens=False):
+    """Data parallel: (rows, bag, ragged) over the ranks of the lookup call reading batch tensor x,
+    from this forward's one shape agreement (dist.agree_batch), or None. tokens: a [B, L] / [B, L, T]
+    sequence feature read as one call of B * L rows."""
+    h = _dp.agreed_dims(x)
+    if h is None:
+        return None
+    dims, ragged = h
+    if tokens:
+        return dims[0] * dims[1], (dims[2] if len(dims) == 3 else 1), ragged
+    return dims[0], (dims[1] if len(dims) >= 2 else 1), ragged
+
+
 def _read_through():
     """RSYS_READ_THROUGH=1: recorded lookups of lazy tables read their rows through the catch-up
     inside the gather (rs_gather_fwd_lazy) instead of a catch-up pass that writes them back first.
@@ -112,7 +125,8 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
             mode = {_hip.RS_POOL['mean']: SEG_MEAN, _hip.RS_POOL['sum']: SEG_SUM}.get(s.pool_mode)
         args = lt.read_through_args() if record and mode is not None and _read_through() else None
         c = lookup_table(t, s.idx, rows, bag, s.idx_stride, None if s.pad_idx < 0 else s.pad_idx,
-                         -1 if mode is None else mode, keep=keep, record=record, read_through=args is not None)
+                         -1 if mode is None else mode, keep=keep, record=record, read_through=args is not None,
+                         agreed=getattr(s, 'agreed', None))
         if c is not None:
             calls[i] = c
         if args is not None and flat_of(t) is lt.flat:
@@ -196,6 +210,7 @@ def seq_feature_segments(proc, seqd, B, L):
             print(f'Configuration Error: Unable to find {name} in the input dictionary, {name} has skipped')
             continue
         x = seqd[name]
+        agreed = _agreed(x, tokens=True)
         x = (x if x.dtype == torch.int64 else x.long()).contiguous()
         keep.append(x)
         emb = proc.embeddings[name]
@@ -217,6 +232,7 @@ def seq_feature_segments(proc, seqd, B, L):
                              table=emb.weight.data_ptr(), pad_idx=pad))
         else:
             raise RuntimeError(f'sequence feature {name}: unsupported rank {x.dim()}')
+        segs[-1].agreed = agreed
         tables.append(emb.weight)
         col += D
     if not segs:
@@ -267,6 +283,35 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key, params=()):
     for s, t in zip(segs, tables):
         s.grad = grad_of(t).data_ptr()
     _grad_tables(segs, calls, dcat, tables, B * L, params)
+
+
+class SeqFeaturesFn(torch.autograd.Function):
+    """SequenceFeatureProcessor.forward on its own (SequenceFeatureProcessor.py:38-85): the
+    per-token gather, tag pooling, projection, positional embedding and dropouts of
+    seq_input_fwd -> [B, L, d]."""
+
+    @staticmethod
+    def forward(ctx, need, proc, seqd, *params):
+        first = next(v for v in seqd.values())
+        B, L = int(first.shape[0]), int(first.shape[1])
+        if L > proc.pos_emb.num_embeddings:
+            raise IndexError('index out of range in self')
+        p = proc.dropout if proc.training else 0.0
+        key = ops.rng_next(proc.rng_state) if p > 0 else None
+        x, saved = seq_input_fwd(proc, seqd, B, L, p, key, proc.err_flag, need)
+        if need:
+            ctx.proc, ctx.saved, ctx.B, ctx.L, ctx.p, ctx.key = proc, saved, B, L, p, key
+            ctx.params = params
+            _dp.note_writer(params)
+        return x.view(B, L, proc.target_dim)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dx):
+        dx = dx.contiguous().view(ctx.B * ctx.L, -1).clone()  # consumed in place below
+        seq_input_bwd(ctx.proc, ctx.saved, dx, ctx.B, ctx.L, ctx.p, ctx.key, ctx.params)
+        ctx.saved = ctx.params = None
+        return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
 
 # ================================================================================ encoder layer
@@ -500,6 +545,7 @@ def tower_segments(tower, input_dict, mapping):
                     print(f'Warning: Pooled feature {name} missing from sequence dict')
                     continue
                 x = seqd[name]
+                agreed = _agreed(x)
                 x = (x if x.dtype == torch.int64 else x.long())
                 if x.dim() == 1:
                     x = x.unsqueeze(1)
@@ -512,6 +558,7 @@ def tower_segments(tower, input_dict, mapping):
                                  pool_mode=_hip.RS_POOL[mode], bag=int(x.shape[1]),
                                  vocab=emb.num_embeddings, idx_stride=int(x.stride(0)),
                                  idx=x.data_ptr(), table=emb.weight.data_ptr(), pad_idx=_pad(emb.padding_idx)))
+                segs[-1].agreed = agreed
             else:
                 if sparse is None:
                     continue
@@ -527,6 +574,8 @@ def tower_segments(tower, input_dict, mapping):
                                  vocab=emb.num_embeddings, idx_stride=int(sp.stride(0)),
                                  idx=sp.data_ptr() + 8 * c * int(sp.stride(1)),
                                  table=emb.weight.data_ptr(), pad_idx=_pad(emb.padding_idx)))
+                ag = _agreed(sparse)
+                segs[-1].agreed = None if ag is None else (ag[0], 1, ag[2])
             params.append((emb.weight, None))
             col += emb.embedding_dim
     if dense_cfg and 'dense' in input_dict:
@@ -901,7 +950,7 @@ class InBatchLossFn(torch.autograd.Function):
     cross_entropy(labels = arange(B)), mean."""
 
     @staticmethod
-    def forward(ctx, U, I, item_ids, H, temperature):
+    def forward(ctx, U, I, item_ids, H, temperature, need=True):
         U = U.contiguous()
         I = I.contiguous()
         B, D = int(U.shape[0]), int(U.shape[1])
@@ -911,7 +960,7 @@ class InBatchLossFn(torch.autograd.Function):
         fused = D in (64, 128)
         sfx = '' if precision.compute_dtype() == 'bf16' else '_f32'
         S = None
-        if fused and sfx:
+        if fused and sfx and need:  # no backward (evaluation, no_grad): S is not stored
             S = torch.empty(B, int(_hip.lib().rs_inbatch_ce_s_ld(B)), device=dev, dtype=torch.float32)
         if not fused:
             S = torch.empty(B, B, device=dev, dtype=torch.float32)
@@ -976,7 +1025,7 @@ class InBatchLossFn(torch.autograd.Function):
                 dH = torch.empty_strided(Hc.shape, Hc.stride(), device=Hc.device, dtype=Hc.dtype)
                 _hip.call('rs_hardneg_bwd', U.data_ptr(), Hc.data_ptr(), ctx.hs[0], ctx.hs[1], dhl.data_ptr(),
                           dU.data_ptr(), dH.data_ptr(), B, N, D, ops.stream())
-            return dU, dI, None, dH, None
+            return dU, dI, None, dH, None, None
         _hip.call('rs_inbatch_ce_bwd', S.data_ptr(), B, U.data_ptr(), ops.P(Hc) if N else None,
                   ctx.hs[0], ctx.hs[1], ops.P(ctx.ids), ctx.st, B, N, D, ctx.T, ctx.lse.data_ptr(),
                   gout.data_ptr(), ops.P(dhl), ops.stream())
@@ -990,4 +1039,4 @@ class InBatchLossFn(torch.autograd.Function):
             _hip.call('rs_hardneg_bwd', U.data_ptr(), Hc.data_ptr(), ctx.hs[0], ctx.hs[1], dhl.data_ptr(),
                       dU.data_ptr(), dH.data_ptr(), B, N, D, ops.stream())
         ctx.S = None
-        return dU, dI, None, dH, None
+        return dU, dI, None, dH, None, None

@@ -20,13 +20,20 @@ nodes). Conventions:
 * `flat_grad`: the flat fp32 gradient buffer (flat.py) the parameters' .grad are views of. The
   backward kernels accumulate the weight gradients into it directly (no AccumulateGrad adds), so
   every backward op declares it mutated; the autograd formula returns None for the parameters.
-* `stats`: buffers a training-mode forward updates in place (BatchNorm running statistics and
-  num_batches_tracked, the dropout RNG state, the id-range error flag). They are passed so the
-  op's dependencies are explicit, but NOT declared mutated: torch.library refuses an autograd
-  formula on a mutating op, and a functional form (new statistics as outputs copied back by the
-  caller) would add a dozen copy launches per step. The kernels update them in place, as
-  before; under torch.compile the ops are opaque calls in program order, which keeps that
-  correct.
+* `stats` / `flags`: buffers a training-mode forward updates in place (BatchNorm running
+  statistics and num_batches_tracked, the dropout RNG state, the id-range error flag). They are
+  DECLARED mutated (mutates_args): custom_op's ADInplaceOrView kernel bumps their version
+  counters and functionalisation (torch.compile's AOT path) sees the writes. None of them ever
+  requires grad. torch.library.register_autograd refuses every op whose schema mutates an
+  argument, so the backward formula is installed by `_register_autograd` where register_autograd
+  puts it for a functional op: the Autograd kernel custom_op generates (torch/_library/
+  autograd.py) runs it. The wrappers below refuse a stats buffer that requires grad.
+* Large (lazy-Adam) embedding tables: a forward's catch-up replays the zero-gradient Adam steps a
+  row skipped before the row is read (flat.py). The value a row logically holds (what dense Adam
+  would hold) does not change, so the tables are not declared mutated -- they are parameters,
+  which autograd forbids an op to mutate in place; the optimizer and state_dict() read rows only
+  after bringing them current the same way (tests/test_gpu_lazy_adam.py, bitwise equal to dense
+  Adam).
 * `ticket` (a one-element int64 CPU tensor output): the activations a backward needs stay on
   the device in a per-call record (the kernels' saved tensors: per-layer activations, sorted
   lookups of the large tables, BatchNorm statistics); the ticket names it. The backward op takes
@@ -145,8 +152,26 @@ def _fake_ticket() -> Tensor:
     return torch.empty(1, dtype=torch.int64)
 
 
+def _register_autograd(op, backward, setup_context):
+    """op.register_autograd(backward, setup_context=...), also for an op that declares mutated
+    buffers (see the module doc): custom_op's generated Autograd kernel calls the formula; the
+    mutated arguments never require grad (_check_stats), so no gradient flows through them."""
+    if op._opoverload._schema.is_mutable:
+        op._backward_fn = backward
+        op._setup_context_fn = setup_context
+    else:
+        op.register_autograd(backward, setup_context=setup_context)
+
+
+def _check_stats(ts):
+    for t in ts:
+        if t.requires_grad:
+            raise RuntimeError('rsys op: a buffer the op updates in place requires grad')
+    return ts
+
+
 # ------------------------------------------------------------------------------ sequence encoder
-@torch.library.custom_op('rsys::seq_encoder', mutates_args=())
+@torch.library.custom_op('rsys::seq_encoder', mutates_args=('stats',))
 def _seq_encoder(seq: List[Tensor], params: List[Tensor], stats: List[Tensor], flat_grad: Tensor, handle: int,
                  keys: str, need: bool) -> Tuple[Tensor, Tensor]:
     """SequenceEncoder.forward (SequenceEncoder.py:32-56) -> ([B, d_model], ticket)."""
@@ -189,20 +214,70 @@ def _seq_encoder_bwd(ctx, gout, gticket):
     return [None] * ns, [None] * npar, [None] * nst, None, None, None, None
 
 
-_seq_encoder.register_autograd(_seq_encoder_bwd, setup_context=_seq_encoder_setup)
+_register_autograd(_seq_encoder, _seq_encoder_bwd, _seq_encoder_setup)
 
 
 def seq_encoder(enc, input_dict) -> Tensor:
     """SequenceEncoder.forward through rsys::seq_encoder."""
     params = list(enc.parameters())
     keys = [k for k in input_dict]
-    out, _ = _seq_encoder([input_dict[k] for k in keys], params, [enc.rng_state, enc.err_flag], flat_of(params[0]).grad,
+    out, _ = _seq_encoder([input_dict[k] for k in keys], params, _check_stats([enc.rng_state, enc.err_flag]),
+                          flat_of(params[0]).grad,
                           handle_of(enc), ','.join(keys), torch.is_grad_enabled())
     return out
 
 
+# ------------------------------------------------------------------------------ sequence features
+@torch.library.custom_op('rsys::seq_features', mutates_args=('stats',))
+def _seq_features(seq: List[Tensor], params: List[Tensor], stats: List[Tensor], flat_grad: Tensor, handle: int,
+                  keys: str, need: bool) -> Tuple[Tensor, Tensor]:
+    """SequenceFeatureProcessor.forward (SequenceFeatureProcessor.py:38-85) on its own: per-token
+    gather + tag pooling + projection + positional embedding + the two dropouts -> [B, L, d]."""
+    proc = module_of(handle)
+    ctx = _Ctx(3 + len(params))
+    out = fn.SeqFeaturesFn.forward(ctx, need, proc, dict(zip(keys.split(','), seq)), *params)
+    return out, (_keep(ctx, out) if need else _no_ticket())
+
+
+@_seq_features.register_fake
+def _(seq, params, stats, flat_grad, handle, keys, need):
+    proc = module_of(handle)
+    first = seq[0]
+    return first.new_empty((first.shape[0], first.shape[1], proc.target_dim), dtype=torch.float32), _fake_ticket()
+
+
+@torch.library.custom_op('rsys::seq_features_backward', mutates_args=('flat_grad',))
+def _seq_features_backward(grad: Tensor, ticket: Tensor, flat_grad: Tensor) -> None:
+    ctx = _take(ticket)
+    _raw(fn.SeqFeaturesFn.backward)(ctx, grad)
+
+
+@_seq_features_backward.register_fake
+def _(grad, ticket, flat_grad):
+    return None
+
+
+def _seq_features_bwd(ctx, gout, gticket):
+    (ticket,) = ctx.saved_tensors
+    torch.ops.rsys.seq_features_backward(gout.contiguous(), ticket, ctx.flat_grad)
+    ns, npar, nst = ctx.shape
+    return [None] * ns, [None] * npar, [None] * nst, None, None, None, None
+
+
+_register_autograd(_seq_features, _seq_features_bwd, _seq_encoder_setup)
+
+
+def seq_features(proc, input_dict) -> Tensor:
+    """SequenceFeatureProcessor.forward through rsys::seq_features."""
+    params = list(proc.parameters())
+    keys = [k for k in input_dict]
+    out, _ = _seq_features([input_dict[k] for k in keys], params, _check_stats([proc.rng_state, proc.err_flag]),
+                           flat_of(params[0]).grad, handle_of(proc), ','.join(keys), torch.is_grad_enabled())
+    return out
+
+
 # ------------------------------------------------------------------------------ tower features
-@torch.library.custom_op('rsys::tower_features', mutates_args=())
+@torch.library.custom_op('rsys::tower_features', mutates_args=('flags',))
 def _tower_features(sparse: Optional[Tensor], dense: Optional[Tensor], seq: List[Tensor], seq_vec: Optional[Tensor],
                     params: List[Tensor], flags: List[Tensor], flat_grad: Tensor, handle: int, keys: str,
                     need: bool) -> Tuple[Tensor, Tensor]:
@@ -262,7 +337,7 @@ def _tower_features_bwd(ctx, gout, gticket):
         [None] * nfl, None, None, None, None
 
 
-_tower_features.register_autograd(_tower_features_bwd, setup_context=_tower_features_setup)
+_register_autograd(_tower_features, _tower_features_bwd, _tower_features_setup)
 
 
 def tower_features(tower, input_dict, mapping, seq_vec) -> Tensor:
@@ -272,7 +347,8 @@ def tower_features(tower, input_dict, mapping, seq_vec) -> Tensor:
     keys = [k for k in seqd]
     tower._rs_call_mapping = mapping
     out, _ = _tower_features(input_dict.get('sparse'), input_dict.get('dense'), [seqd[k] for k in keys], seq_vec,
-                             params, [tower.err_flag], flat_of(tower.feature_bn.weight).grad, handle_of(tower),
+                             params, _check_stats([tower.err_flag]), flat_of(tower.feature_bn.weight).grad,
+                             handle_of(tower),
                              ','.join(keys), torch.is_grad_enabled())
     return out
 
@@ -291,7 +367,7 @@ def _mlp_bns(mlp):
     return [seq[4 * j + 1] for j in range((len(seq) - 1) // 4)]
 
 
-@torch.library.custom_op('rsys::tower_chain', mutates_args=())
+@torch.library.custom_op('rsys::tower_chain', mutates_args=('stats',))
 def _tower_chain(x: Tensor, params: List[Tensor], stats: List[Tensor], flat_grad: Tensor, handle: int, groups: int,
                  need: bool) -> Tuple[Tensor, Tensor]:
     """feature_bn + MLP_Tower in training mode (GenericTower.py:229-236; Tower.py:16-41) as one
@@ -337,19 +413,19 @@ def _make_x_bwd(opname):
     return bwd
 
 
-_tower_chain.register_autograd(_make_x_bwd('tower_chain_backward'), setup_context=_x_setup)
+_register_autograd(_tower_chain, _make_x_bwd('tower_chain_backward'), _x_setup)
 
 
 def tower_chain(tower, x, groups) -> Tensor:
     params = list(tower.feature_bn.parameters()) + list(tower.mlp.parameters())
-    stats = _bn_stats([tower.feature_bn] + _mlp_bns(tower.mlp)) + [tower.mlp.rng_state]
+    stats = _check_stats(_bn_stats([tower.feature_bn] + _mlp_bns(tower.mlp)) + [tower.mlp.rng_state])
     out, _ = _tower_chain(x, params, stats, flat_of(params[0]).grad, handle_of(tower), int(groups),
                           torch.is_grad_enabled())
     return out
 
 
 # ------------------------------------------------------------------------------ BatchNorm1d, MLP_Tower
-@torch.library.custom_op('rsys::batch_norm', mutates_args=())
+@torch.library.custom_op('rsys::batch_norm', mutates_args=('stats',))
 def _batch_norm(x: Tensor, params: List[Tensor], stats: List[Tensor], flat_grad: Tensor, handle: int, groups: int,
                 need: bool) -> Tuple[Tensor, Tensor]:
     """nn.BatchNorm1d (GenericTower.py:234): batch statistics and running-stat update in
@@ -376,17 +452,17 @@ def _(grad, ticket, flat_grad, x_shape):
     return grad.new_empty(x_shape)
 
 
-_batch_norm.register_autograd(_make_x_bwd('batch_norm_backward'), setup_context=_x_setup)
+_register_autograd(_batch_norm, _make_x_bwd('batch_norm_backward'), _x_setup)
 
 
 def batch_norm(bn, x, groups) -> Tensor:
     params = [bn.weight, bn.bias]
-    y, _ = _batch_norm(x, params, _bn_stats([bn]), flat_of(bn.weight).grad, handle_of(bn), int(groups),
+    y, _ = _batch_norm(x, params, _check_stats(_bn_stats([bn])), flat_of(bn.weight).grad, handle_of(bn), int(groups),
                        torch.is_grad_enabled())
     return y
 
 
-@torch.library.custom_op('rsys::mlp_tower', mutates_args=())
+@torch.library.custom_op('rsys::mlp_tower', mutates_args=('stats',))
 def _mlp_tower(x: Tensor, params: List[Tensor], stats: List[Tensor], flat_grad: Tensor, handle: int, groups: int,
                need: bool) -> Tuple[Tensor, Tensor]:
     """MLP_Tower.forward (Tower.py:16-41): [Linear -> BatchNorm1d -> ReLU -> Dropout] x n, Linear,
@@ -414,12 +490,12 @@ def _(grad, ticket, flat_grad, x_shape):
     return grad.new_empty(x_shape)
 
 
-_mlp_tower.register_autograd(_make_x_bwd('mlp_tower_backward'), setup_context=_x_setup)
+_register_autograd(_mlp_tower, _make_x_bwd('mlp_tower_backward'), _x_setup)
 
 
 def mlp_tower(mlp, x, groups) -> Tensor:
     params = list(mlp.parameters())
-    out, _ = _mlp_tower(x, params, _bn_stats(_mlp_bns(mlp)) + [mlp.rng_state], flat_of(params[0]).grad,
+    out, _ = _mlp_tower(x, params, _check_stats(_bn_stats(_mlp_bns(mlp)) + [mlp.rng_state]), flat_of(params[0]).grad,
                         handle_of(mlp), int(groups), torch.is_grad_enabled())
     return out
 
@@ -427,16 +503,17 @@ def mlp_tower(mlp, x, groups) -> Tensor:
 # ------------------------------------------------------------------------------ in-batch loss
 @torch.library.custom_op('rsys::inbatch_softmax_loss', mutates_args=())
 def _inbatch_loss(U: Tensor, I: Tensor, item_ids: Optional[Tensor], H: Optional[Tensor],
-                  temperature: float) -> Tuple[Tensor, Tensor]:
+                  temperature: float, need: bool) -> Tuple[Tensor, Tensor]:
     """TwoTowerModel.compute_loss (TwoTowerModel.py:81-140): logits U I^T / T, off-diagonal
-    equal-id collisions at -1e9, hard-negative logits appended, cross_entropy(arange(B)) mean."""
+    equal-id collisions at -1e9, hard-negative logits appended, cross_entropy(arange(B)) mean.
+    `need`: a backward follows (the fp32 form then keeps S = U I^T for it)."""
     ctx = _Ctx(5)
-    loss = fn.InBatchLossFn.forward(ctx, U, I, item_ids, H, temperature)
-    return loss, _keep(ctx, loss)
+    loss = fn.InBatchLossFn.forward(ctx, U, I, item_ids, H, temperature, need)
+    return loss, (_keep(ctx, loss) if need else _no_ticket())
 
 
 @_inbatch_loss.register_fake
-def _(U, I, item_ids, H, temperature):
+def _(U, I, item_ids, H, temperature, need):
     return U.new_empty(()), _fake_ticket()
 
 
@@ -456,7 +533,7 @@ def _(grad, ticket, u_shape, h_shape, h_stride):
 
 
 def _inbatch_setup(ctx, inputs, output):
-    U, I, item_ids, H, _ = inputs
+    U, I, item_ids, H = inputs[:4]
     ctx.u_shape = list(U.shape)
     if H is None:
         ctx.h = ([0], [1])
@@ -470,12 +547,13 @@ def _inbatch_setup(ctx, inputs, output):
 def _inbatch_bwd(ctx, gloss, gticket):
     (ticket,) = ctx.saved_tensors
     dU, dI, dH = torch.ops.rsys.inbatch_softmax_loss_backward(gloss.contiguous(), ticket, ctx.u_shape, *ctx.h)
-    return dU, dI, None, (dH if ctx.has_h else None), None
+    return dU, dI, None, (dH if ctx.has_h else None), None, None
 
 
-_inbatch_loss.register_autograd(_inbatch_bwd, setup_context=_inbatch_setup)
+_register_autograd(_inbatch_loss, _inbatch_bwd, _inbatch_setup)
 
 
 def inbatch_softmax_loss(U, I, item_ids=None, H=None, temperature=0.1) -> Tensor:
-    loss, _ = _inbatch_loss(U, I, item_ids, H, float(temperature))
+    need = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (U, I, H))
+    loss, _ = _inbatch_loss(U, I, item_ids, H, float(temperature), need)
     return loss

@@ -64,6 +64,9 @@ class TwoTowerModel(nn.Module):
         if rdist.is_active():
             # one gradient bucket per tower, all-reduced inside the backward (dist.overlap)
             rdist.setup_buckets(self, [self.user_tower, self.item_tower])
+            # the batch's shapes over the ranks, in one all-reduce: the large tables' lookup calls
+            # take their common shapes from it (no collective per call)
+            rdist.agree_batch(batch_data)
         side = self._side_stream(dev)
         if side is None or library.is_fake(self.user_tower.feature_bn.weight) or library.fake_mode_active():
             user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)

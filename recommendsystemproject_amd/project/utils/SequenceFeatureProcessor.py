@@ -2,36 +2,15 @@
 
 Same constructor, attributes and state_dict keys (embeddings.<name>.weight,
 feature_projection.0.{weight,bias}, pos_emb.weight); forward runs the fused HIP path
-(per-token gather + tag pooling + projection + positional embedding + dropouts) on MI355X.
+(per-token gather + tag pooling + projection + positional embedding + dropouts) on MI355X as
+the custom op rsys::seq_features (library.py; kernels in functions.SeqFeaturesFn).
 """
 import torch
 import torch.nn as nn
 
-from recommendsystemproject_amd import _hip, ops
+from recommendsystemproject_amd import _hip, library
 from recommendsystemproject_amd.flat import ensure_flat
-from recommendsystemproject_amd.functions import seq_input_bwd, seq_input_fwd
 from recommendsystemproject_amd.rng import new_rng_state
-
-
-class _SeqInputFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, need, proc, seqd, *params):
-        first = next(v for v in seqd.values())
-        B, L = int(first.shape[0]), int(first.shape[1])
-        if L > proc.pos_emb.num_embeddings:
-            raise IndexError('index out of range in self')
-        p = proc.dropout if proc.training else 0.0
-        key = ops.rng_next(proc.rng_state) if p > 0 else None
-        x, saved = seq_input_fwd(proc, seqd, B, L, p, key, proc.err_flag)
-        if need:
-            ctx.proc, ctx.saved, ctx.B, ctx.L, ctx.p, ctx.key = proc, saved, B, L, p, key
-        return x.view(B, L, proc.target_dim)
-
-    @staticmethod
-    def backward(ctx, dx):
-        dx = dx.contiguous().view(ctx.B * ctx.L, -1).clone()
-        seq_input_bwd(ctx.proc, ctx.saved, dx, ctx.B, ctx.L, ctx.p, ctx.key)
-        return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
 
 class SequenceFeatureProcessor(nn.Module):
@@ -57,4 +36,4 @@ class SequenceFeatureProcessor(nn.Module):
         """[B, L, target_dim] (SequenceFeatureProcessor.py:38-85)."""
         _hip.require_device(self.pos_emb.weight)
         ensure_flat(self)
-        return _SeqInputFn.apply(torch.is_grad_enabled(), self, input_dict, *self.parameters())
+        return library.seq_features(self, input_dict)

@@ -152,9 +152,11 @@ def test_custom_ops_registered_with_fake_impls():
     import torch
     from torch._subclasses.fake_tensor import FakeTensorMode
     from recommendsystemproject_amd import library  # noqa: F401  (registers torch.ops.rsys.*)
-    for n in ('seq_encoder', 'tower_features', 'tower_chain', 'batch_norm', 'mlp_tower', 'inbatch_softmax_loss'):
+    for n in ('seq_encoder', 'seq_features', 'tower_features', 'tower_chain', 'batch_norm', 'mlp_tower',
+              'inbatch_softmax_loss'):
         assert hasattr(torch.ops.rsys, n) and hasattr(torch.ops.rsys, n + '_backward'), n
     with FakeTensorMode():
         U, I = torch.empty(64, 128), torch.empty(64, 128)
-        loss, ticket = torch.ops.rsys.inbatch_softmax_loss(U, I, torch.empty(64, dtype=torch.int64), None, 0.15)
+        loss, ticket = torch.ops.rsys.inbatch_softmax_loss(U, I, torch.empty(64, dtype=torch.int64), None, 0.15,
+                                                          True)
         assert loss.shape == () and ticket.dtype == torch.int64

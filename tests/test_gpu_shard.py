@@ -43,7 +43,8 @@ def _bucket_ref(ids, W, cap, pad, vocab):
             slot_of[int(u)] = o * cap + s
         else:
             over = True
-    idx = np.array([slot_of.get(int(i), 0) if v else 0 for i, v in zip(ids, valid)], np.int64)
+    # an out-of-range or overflowed id reads the zero row after the buckets (W * cap)
+    idx = np.array([slot_of.get(int(i), W * cap) if v else W * cap for i, v in zip(ids, valid)], np.int64)
     return send, np.minimum(counts, cap), idx, slot_of, over
 
 
@@ -101,6 +102,10 @@ def test_shard_bucket_overflow_flag():
     assert counts.tolist() == [cap, 0]
     c = ckey.cpu().numpy().astype(np.uint32)
     assert (c[cap:] == SENT).all() and (c[:cap] != SENT).all()  # past the capacity: no gradient
+    # and no other id's row: the overflowed lookups read the zero row after the buckets
+    ix = idx.cpu().numpy()
+    ov = np.argsort(ids.cpu().numpy())[cap:]
+    assert (ix[ov] == W * cap).all() and (ix[np.argsort(ids.cpu().numpy())[:cap]] < cap).all()
 
 
 def test_shard_recv_masks_invalid_slots():
