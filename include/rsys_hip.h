@@ -598,6 +598,13 @@ int rs_shard_recv(const int32_t* recv_ids, const int* recv_counts, int world, in
 int rs_pack_ids(const void* ids, int id_bytes, int64_t rows, int bag, int64_t row_stride,
                 int32_t* out, void* stream);
 int rs_pack_rows(const float* src, int64_t ld, int64_t rows, int D, float* dst, void* stream);
+/* rs_pool_max_grad: a max-pooled [rows, bag] lookup's backward as per-lookup gradient rows
+ * out [rows * bag, D]: dout[r] at the first arg-max position of each column of bag r (torch.max(dim)
+ * backward), zero elsewhere (and for the padding id / invalid ids) -- the data-parallel exchange
+ * then treats the call as rows * bag single-id lookups. Replaces the arg-max scatter of
+ * GenericTower.py:159-160's pooled max under data parallelism. */
+int rs_pool_max_grad(const float* table, const void* ids, int id_bytes, int64_t rows, int bag, int64_t row_stride,
+                     int64_t vocab, int D, int64_t pad, const float* dout, int64_t ldo, float* out, void* stream);
 
 /* ---------------------------------------------------------------- dropout
  * Counter-based masks: element i of site `site` is kept iff hash(key[0], key[1], site, i) >= p,

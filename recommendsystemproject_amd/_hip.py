@@ -152,6 +152,7 @@ SIGNATURES = {
     'rs_shard_recv': (i32, [vp, vp, i32, i32, i64, vp, vp, vp, vp]),
     'rs_pack_ids': (i32, [vp, i32, i64, i32, i64, vp, vp]),
     'rs_pack_rows': (i32, [vp, i64, i64, i32, vp, vp]),
+    'rs_pool_max_grad': (i32, [vp, vp, i32, i64, i32, i64, i64, i32, i64, vp, i64, vp, vp]),
     'rs_dropout_fwd': (i32, [vp, i64, i32, vp, i32, i32, f32, vp, i32, vp]),
     'rs_seq_input_dropout_bwd_ws_bytes': (i64, [i32, i32]),
     'rs_seq_input_dropout_bwd': (i32, [vp, i32, i32, f32, vp, i32, i32, vp, vp, vp]),

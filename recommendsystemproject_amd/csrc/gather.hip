@@ -32,6 +32,8 @@ constexpr int64_t kSmallTableBytes = 48 * 1024;
 
 constexpr int kRowsPerLane = 4;            // forward sparse rows per lane on token-sized launches
 constexpr int kBagBatch = 16;              // bag ids (and rows) loaded per batch
+constexpr int kBagBatchNt = 8;             // the same for rows of large tables (non-temporal loads)
+constexpr int64_t kNtTableBytes = 64ll << 20;  // tables from this size: rows read once, nt loads
 constexpr int kLazyBagBatch = 8;           // the same with exp_avg / exp_avg_sq rows beside them
 // forward: a table of at most this size whose workgroup reads at least as many row bytes as the
 // table holds is staged whole into LDS first (every row of such a table is hot: the genre / age /
@@ -74,6 +76,7 @@ struct SegLaunch {
   int rblock_start[kMaxSeg + 1];
   uint8_t tiny[kMaxSeg];   // bwd: tiny table by the register-accumulator kernel
   uint8_t rpt[kMaxSeg];    // fwd sparse segments: rows per lane (kRowsPerLane on token-sized launches)
+  uint8_t nt[kMaxSeg];     // fwd: rows of a large table -- non-temporal loads, shorter bag batches
   int16_t tblocks[kMaxSeg];
   int tblock_start[kMaxSeg + 1];
   // bwd partials (small and ranged tables): [pchunks][vocab][dim] floats at ws + pws_off
@@ -100,13 +103,14 @@ __device__ __forceinline__ bool id_ok(int64_t id, int64_t vocab, int* err) {
   return true;
 }
 
-template <bool VEC>
+template <bool VEC, bool NT = false>
 __device__ __forceinline__ void load_row(const float* p, float* v) {
   if (VEC) {
-    float4 t = *reinterpret_cast<const float4*>(p);
-    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v t = NT ? __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p)) : *reinterpret_cast<const f4v*>(p);
+    v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
   } else {
-    v[0] = p[0];
+    v[0] = NT ? __builtin_nontemporal_load(p) : p[0];
   }
 }
 
@@ -143,11 +147,14 @@ __device__ __forceinline__ void lazy_replay(const LazyLaunch& z, int2 last, int 
 
 // Pooled bag: the (un-normalised) sum or max of positions [lbeg, lend) of row `row`'s bag.
 // LAZY: the rows read through the catch-up.
-template <bool VEC, bool LAZY = false>
+// NT (rows of a large table, read once per step): non-temporal row loads and 8 rows in flight per
+// lane group instead of 16 (tools/gather_sweep.hip, C3's history shape from HBM: 16 rows default
+// policy 4.7 TB/s, 8 rows nt 5.4 TB/s)
+template <bool VEC, bool LAZY = false, bool NT = false>
 __device__ __forceinline__ void pool_acc(const SegLaunch& a, const rs_feature_seg_t& sg, int row,
                                          int c, int lbeg, int lend, float* acc) {
   constexpr int W = VEC ? 4 : 1;
-  constexpr int NB = LAZY ? kLazyBagBatch : kBagBatch;
+  constexpr int NB = LAZY ? kLazyBagBatch : (NT ? kBagBatchNt : kBagBatch);
   const int64_t* ids = sg.idx + (int64_t)row * sg.idx_stride;
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = sg.pool_mode == RS_POOL_MAX ? -INFINITY : 0.f;
@@ -171,7 +178,7 @@ __device__ __forceinline__ void pool_acc(const SegLaunch& a, const rs_feature_se
       bad |= u < nb && !valid;
       ok[u] = u < nb && valid;
       const int64_t r = ok[u] ? raw[u] : 0;
-      load_row<VEC>(sg.table + r * sg.dim + c, v[u]);
+      load_row<VEC, NT && !LAZY>(sg.table + r * sg.dim + c, v[u]);
       if constexpr (LAZY) {
         lst[u] = reinterpret_cast<const int2*>(sg.lazy_last)[r];
         load_row<VEC>(sg.table + r * sg.dim + c + a.lz.moff, mv[u]);
@@ -246,7 +253,7 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
 // workgroups of one float4 per lane, each a serial id -> row -> store chain). The workgroup owns
 // rows [lb R rpb, (lb + 1) R rpb); all R ids are loaded, then all R rows, then the R stores, so a
 // lane has R independent chains in flight. Same values as gather_seg (bad ids: zeros + err flag).
-template <int R, bool LAZY = false>
+template <int R, bool LAZY = false, bool NT = false>
 __device__ void gather_sparse_rows(const SegLaunch& a, const rs_feature_seg_t& sg, int rpb, int lb,
                                    int r, int chunk) {
   const int c = chunk * 4;
@@ -268,7 +275,7 @@ __device__ void gather_sparse_rows(const SegLaunch& a, const rs_feature_seg_t& s
     okk[k] = ok;
     bad |= row < a.rows && !ok;
     const float* pr = sg.table + (ok ? id[k] : 0) * sg.dim + c;
-    load_row<true>(pr, v[k]);
+    load_row<true, NT && !LAZY>(pr, v[k]);
     if constexpr (LAZY) {
       lst[k] = reinterpret_cast<const int2*>(sg.lazy_last)[ok ? id[k] : 0];
       load_row<true>(pr + a.lz.moff, mv[k]);
@@ -297,7 +304,7 @@ __device__ void gather_sparse_rows(const SegLaunch& a, const rs_feature_seg_t& s
 // Pooled bag split over S row groups (small batches: more loads in flight per bag). Row group
 // g = r * S + p sums positions [p * per, (p + 1) * per) of bag r; the S partial sums are added
 // in p order through LDS by group p = 0.
-template <bool VEC, bool LAZY = false>
+template <bool VEC, bool LAZY = false, bool NT = false>
 __device__ void gather_pool_split(const SegLaunch& a, const rs_feature_seg_t& sg, int s, int lb) {
   constexpr int W = VEC ? 4 : 1;
   __shared__ float4 red[256];
@@ -310,7 +317,7 @@ __device__ void gather_pool_split(const SegLaunch& a, const rs_feature_seg_t& sg
   const int lbeg = p * per < sg.bag ? p * per : sg.bag;
   const int lend = lbeg + per < sg.bag ? lbeg + per : sg.bag;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if (active) pool_acc<VEC, LAZY>(a, sg, row, chunk * W, lbeg, lend, acc);
+  if (active) pool_acc<VEC, LAZY, NT>(a, sg, row, chunk * W, lbeg, lend, acc);
   red[threadIdx.x] = make_float4(acc[0], acc[1], acc[2], acc[3]);
   __syncthreads();
   if (!active || p != 0) return;
@@ -361,7 +368,8 @@ __global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
     sg.table = reinterpret_cast<const float*>(stage_lds);
   }
   if (a.split[s] > 1) {  // uniform per workgroup: the barrier inside is reached by every thread
-    if (a.vec[s]) gather_pool_split<true>(a, sg, s, lb);
+    if (a.vec[s] && a.nt[s]) gather_pool_split<true, false, true>(a, sg, s, lb);
+    else if (a.vec[s]) gather_pool_split<true>(a, sg, s, lb);
     else gather_pool_split<false>(a, sg, s, lb);
     return;
   }
@@ -369,7 +377,8 @@ __global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
   const int r = threadIdx.x / C, chunk = threadIdx.x % C;
   if (r >= a.rpb[s]) return;
   if (a.rpt[s] == kRowsPerLane) {  // plan: sparse, vec only
-    gather_sparse_rows<kRowsPerLane>(a, sg, a.rpb[s], lb, r, chunk);
+    if (a.nt[s]) gather_sparse_rows<kRowsPerLane, false, true>(a, sg, a.rpb[s], lb, r, chunk);
+    else gather_sparse_rows<kRowsPerLane>(a, sg, a.rpb[s], lb, r, chunk);
     return;
   }
   const int row = lb * a.rpb[s] + r;
@@ -895,6 +904,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.rpt[s] = (!bwd && vec && g.kind == RS_SEG_SPARSE && (int64_t)rows * C >= (int64_t)2048 * 256)
                    ? kRowsPerLane : 1;
     a.rpb[s] = 256 / (C * S);
+    a.nt[s] = !bwd && vec && table_kind && g.vocab * g.dim * 4 >= kNtTableBytes && !getenv_flag("RSYS_GATHER_NO_NT");
     a.stage[s] = 0;
     if (!bwd && table_kind && vec) {
       const int64_t tbytes = g.vocab * g.dim * 4;

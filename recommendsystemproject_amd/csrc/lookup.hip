@@ -229,6 +229,118 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter_kernel(
   }
 }
 
+// ---------------------------------------------------------------- single-launch passes (round 4)
+// Every pass's global digit totals come from one histogram launch over the pass-0 keys (a digit's
+// total does not depend on the order), and each pass is then ONE launch: a tile takes the next
+// tile index from a counter (so every lower tile is already running), ranks its keys in the tile
+// (rank_round, as above), publishes its per-digit counts, and finds the count of each digit in
+// all lower tiles by decoupled look-back (status word per (tile, digit): FLAG_AGG + the tile's own
+// count as soon as it is known, FLAG_PRE + the inclusive prefix once the look-back is done).
+// 1 + passes launches (+ one memset) instead of 3 x passes: C3's 204,800-lookup history call went
+// through 9 dependent launches. Same stable order, same bits.
+constexpr uint64_t kFlagAgg = 1ull << 62, kFlagPre = 2ull << 62, kFlagMask = 3ull << 62;
+
+__global__ __launch_bounds__(kSortThreads) void sort_hist_all_kernel(
+    const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab, int64_t n,
+    SortPlan plan, int* __restrict__ tot) {
+  __shared__ int h[4][kMaxRadix];
+  for (int t = threadIdx.x; t < 4 * kMaxRadix; t += kSortThreads) (&h[0][0])[t] = 0;
+  __syncthreads();
+  for (int64_t e = (int64_t)blockIdx.x * kSortThreads + threadIdx.x; e < n; e += (int64_t)gridDim.x * kSortThreads) {
+    const uint32_t k = raw_key(ids, id_bytes, bag, stride, vocab, e);
+    for (int q = 0; q < plan.passes; ++q) atomicAdd(&h[q][(k >> plan.shift[q]) & ((1 << plan.dbits[q]) - 1)], 1);
+  }
+  __syncthreads();
+  for (int q = 0; q < plan.passes; ++q) {
+    const int radix = 1 << plan.dbits[q];
+    for (int t = threadIdx.x; t < radix; t += kSortThreads)
+      if (h[q][t]) atomicAdd(&tot[q * kMaxRadix + t], h[q][t]);
+  }
+}
+
+__global__ __launch_bounds__(kSortThreads) void sort_onesweep_kernel(
+    const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab,
+    const uint32_t* __restrict__ ksrc, const uint32_t* __restrict__ vsrc, int64_t n, int shift,
+    int dbits, const int* __restrict__ tot, unsigned long long* __restrict__ status, int* __restrict__ counter,
+    uint32_t* __restrict__ kdst, uint32_t* __restrict__ vdst) {
+  __shared__ RankLds<kSortThreads> lds;
+  __shared__ int gbase[kMaxRadix];
+  __shared__ int s_tile;
+  const int radix = 1 << dbits;
+  rank_reset(lds, radix);
+  if (threadIdx.x == 0) s_tile = atomicAdd(counter, 1);
+  // global base of each digit: keys of smaller digits
+  if (threadIdx.x < 64) {
+    int carry = 0;
+    const int lane = threadIdx.x;
+    for (int d0 = 0; d0 < radix; d0 += 64) {
+      const int x = d0 + lane < radix ? tot[d0 + lane] : 0;
+      int y = x;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(y, o, 64);
+        if (lane >= o) y += t;
+      }
+      if (d0 + lane < radix) gbase[d0 + lane] = carry + y - x;
+      carry += __shfl(y, 63, 64);
+    }
+  }
+  __syncthreads();
+  const int tile = s_tile;
+  const int64_t base = (int64_t)tile * kSortTile;
+  uint32_t key[kSortRounds], val[kSortRounds];
+  int lp[kSortRounds];
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int64_t e = base + r * kSortThreads + threadIdx.x;
+    key[r] = kSentinel;
+    val[r] = 0;
+    if (e < n) {
+      key[r] = ksrc ? ksrc[e] : raw_key(ids, id_bytes, bag, stride, vocab, e);
+      val[r] = vsrc ? vsrc[e] : (uint32_t)e;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int64_t e = base + r * kSortThreads + threadIdx.x;
+    const uint32_t d = (key[r] >> shift) & (radix - 1);
+    lp[r] = rank_round(lds, d, e < n, dbits, radix);
+  }
+  // lds.run[d] = this tile's count of digit d: publish it, then look back over the lower tiles
+  unsigned long long* my = status + (int64_t)tile * kMaxRadix;
+  for (int d = threadIdx.x; d < radix; d += kSortThreads)
+    __hip_atomic_store(my + d, kFlagAgg | (unsigned long long)lds.run[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int d = threadIdx.x; d < radix; d += kSortThreads) {
+    unsigned long long excl = 0;
+    for (int j = tile - 1; j >= 0;) {
+      const unsigned long long w =
+          __hip_atomic_load(status + (int64_t)j * kMaxRadix + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long f = w & kFlagMask;
+      if (f == 0) {  // tile j has not published yet (it is running: it took its index earlier)
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      excl += w & ~kFlagMask;
+      if (f == kFlagPre) break;
+      --j;
+    }
+    __hip_atomic_store(my + d, kFlagPre | (excl + (unsigned long long)lds.run[d]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    gbase[d] += (int)excl;
+  }
+  __syncthreads();
+  // rank_round's positions count from the tile's start of each digit (lds.pre per round)
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int64_t e = base + r * kSortThreads + threadIdx.x;
+    if (e < n) {
+      const uint32_t d = (key[r] >> shift) & (radix - 1);
+      const int64_t pos = (int64_t)gbase[d] + lp[r];
+      kdst[pos] = key[r];
+      vdst[pos] = val[r];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- one-tile sort (n <= 4096)
 // One workgroup, the keys in registers (4 per thread) and exchanged through LDS between the
 // radix passes. (Measured and rejected: a bitonic sort of key/index pairs -- 39 us with an LDS
@@ -965,10 +1077,20 @@ AdamConst make_hyper(float b1, float b2, float eps, float wd) {
   return h;
 }
 
+bool sort_onesweep() {
+  static const bool v = !getenv_flag("RSYS_SORT_MULTILAUNCH");
+  return v;
+}
+
+// workspace: ping-pong keys + vals, then the multi-launch path's [radix][tiles] histogram and digit
+// totals, or the single-launch path's status words [passes][tiles][radix] (u64), tile counters and
+// per-pass digit totals
 int64_t sort_ws_bytes(int64_t n, int64_t vocab) {
   if (n <= kTileMax) return 0;
   const SortPlan p = make_plan(n, vocab);
-  return 2 * n * 4 + ((int64_t)kMaxRadix * p.ntiles + kMaxRadix) * 4 + 256;
+  const int64_t multi = ((int64_t)kMaxRadix * p.ntiles + kMaxRadix) * 4;
+  const int64_t one = (int64_t)p.passes * p.ntiles * kMaxRadix * 8 + 64 + (int64_t)4 * kMaxRadix * 4;
+  return 2 * n * 4 + (multi > one ? multi : one) + 256;
 }
 
 }  // namespace
@@ -996,6 +1118,30 @@ extern "C" int rs_lookup_sort(const void* ids, int id_bytes, int rows, int bag, 
   RS_CHECK_ARG(ws, "rs_lookup_sort: workspace needed for %lld lookups", (long long)n);
   uint32_t* tk = static_cast<uint32_t*>(ws);
   uint32_t* tv = tk + n;
+  if (sort_onesweep()) {
+    // status words (8-byte aligned after the ping-pong buffers), tile counters, digit totals
+    const int64_t off = ((2 * n * 4 + 7) / 8) * 8;
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(static_cast<char*>(ws) + off);
+    const int64_t nstatus = (int64_t)p.passes * p.ntiles * kMaxRadix;
+    int* counters = reinterpret_cast<int*>(status + nstatus);
+    int* tot = counters + 16;
+    RS_RET_IF((int)hipMemsetAsync(status, 0, nstatus * 8 + 64 + (int64_t)4 * kMaxRadix * 4, st));
+    const int hb = (int)std::min<int64_t>(cdiv(n, kSortThreads), 256);
+    sort_hist_all_kernel<<<hb, kSortThreads, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, n, p, tot);
+    RS_CHECK_LAUNCH("rs_lookup_sort hist");
+    for (int q = 0; q < p.passes; ++q) {
+      const bool to_out = ((p.passes - 1 - q) & 1) == 0;
+      uint32_t* kd = to_out ? keys : tk;
+      uint32_t* vd = to_out ? vals : tv;
+      const uint32_t* ks = q == 0 ? nullptr : (to_out ? tk : keys);
+      const uint32_t* vs = q == 0 ? nullptr : (to_out ? tv : vals);
+      sort_onesweep_kernel<<<p.ntiles, kSortThreads, 0, st>>>(
+          ids, id_bytes, bag, row_stride, vocab, ks, vs, n, p.shift[q], p.dbits[q], tot + q * kMaxRadix,
+          status + (int64_t)q * p.ntiles * kMaxRadix, counters + q, kd, vd);
+      RS_CHECK_LAUNCH("rs_lookup_sort pass");
+    }
+    return 0;
+  }
   int* hist = reinterpret_cast<int*>(tv + n);
   int* tot = hist + (int64_t)kMaxRadix * p.ntiles;
   // ping-pong so that the last pass lands in (keys, vals)
@@ -1280,6 +1426,55 @@ extern "C" int rs_shard_map_ids(const int32_t* ids, int64_t n, int64_t vocab, in
   shard_map_kernel<<<std::min<int64_t>(cdiv(n, 256), 8192), 256, 0, as_stream(stream)>>>(ids, n, vocab, world,
                                                                                             rank, local, err_flag);
   RS_CHECK_LAUNCH("rs_shard_map_ids");
+  return 0;
+}
+
+// max-pooled bag backward as per-lookup gradient rows (data parallel: the arg-max scatter's
+// contributions exchanged like single-id lookups): out[r * bag + l][c] = dout[r][c] where l is
+// the first position of bag r whose row holds the bag's maximum in column c (torch.max(dim)'s
+// backward, as gather_bwd's RS_POOL_MAX scatter), 0 elsewhere and for the padding row / invalid
+// ids. One thread per (bag, column).
+__global__ __launch_bounds__(256) void pool_max_grad_kernel(const float* __restrict__ table, const void* ids,
+                                                            int id_bytes, int64_t rows, int bag, int64_t stride,
+                                                            int64_t vocab, int D, int64_t pad,
+                                                            const float* __restrict__ dout, int64_t ldo,
+                                                            float* __restrict__ out) {
+  const int64_t n = rows * D;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / D;
+    const int c = (int)(i - r * D);
+    float best = -INFINITY;
+    int arg = -1;
+    for (int l = 0; l < bag; ++l) {
+      const int64_t e = r * stride + l;
+      const int64_t id = id_bytes == 8 ? static_cast<const int64_t*>(ids)[e] : static_cast<const int32_t*>(ids)[e];
+      const float v = id >= 0 && id < vocab ? table[id * D + c] : 0.f;
+      if (v > best || arg < 0) {
+        best = v;
+        arg = l;
+      }
+    }
+    const float g = dout[r * ldo + c];
+    for (int l = 0; l < bag; ++l) {
+      const int64_t e = r * stride + l;
+      const int64_t id = id_bytes == 8 ? static_cast<const int64_t*>(ids)[e] : static_cast<const int32_t*>(ids)[e];
+      const bool take = l == arg && id >= 0 && id < vocab && id != pad;
+      out[(r * bag + l) * D + c] = take ? g : 0.f;
+    }
+  }
+}
+
+extern "C" int rs_pool_max_grad(const float* table, const void* ids, int id_bytes, int64_t rows, int bag,
+                                int64_t row_stride, int64_t vocab, int D, int64_t pad, const float* dout,
+                                int64_t ldo, float* out, void* stream) {
+  RS_CHECK_ARG(table && ids && dout && out && rows >= 0 && bag >= 1 && row_stride >= bag && vocab >= 1 &&
+                   D >= 1 && ldo >= D && (id_bytes == 4 || id_bytes == 8),
+               "rs_pool_max_grad: bad args");
+  const int64_t n = rows * D;
+  if (n == 0) return 0;
+  pool_max_grad_kernel<<<std::min<int64_t>(cdiv(n, 256), 8192), 256, 0, as_stream(stream)>>>(
+      table, ids, id_bytes, rows, bag, row_stride, vocab, D, pad, dout, ldo, out);
+  RS_CHECK_LAUNCH("rs_pool_max_grad");
   return 0;
 }
 

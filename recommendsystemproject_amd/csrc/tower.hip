@@ -208,8 +208,30 @@ __device__ __forceinline__ FinPre fin_preload(const Fin& f, int nb, int ncols) {
   return r;
 }
 
-__device__ void fin_merge(const Fin& f, int N, int G, int Bg, int tiles, int tm, int g, int nb,
-                          int ncols, const FinPre& pre) {
+// The last arriver's first batch of tile values, loaded right after its ticket so that the
+// round trip runs under its own output stores (fin_merge consumes them)
+struct MergeFirst {
+  float av[MB], qv[MB];
+};
+
+__device__ __forceinline__ void fin_merge_load(const Fin& f, int N, int tiles, int g, int nb, int ncols,
+                                               MergeFirst& mf) {
+  const int tid = threadIdx.x;
+  const int c = tid & 63, tl = tid >> 6;
+  const int R = (tiles + 3) / 4, t_begin = tl * R, t_end = min(tiles, t_begin + R);
+  const int cc = nb * 64 + min(c, max(ncols - 1, 0));
+  const float* pb = f.part + (size_t)g * tiles * 2 * N + cc;
+#pragma unroll
+  for (int u = 0; u < MB; ++u) {
+    const size_t o = (size_t)max(min(t_begin + u, t_end - 1), 0) * 2 * N;
+    mf.av[u] = ld_sc1(pb + o);
+    mf.qv[u] = ld_sc1(pb + o + N);
+  }
+}
+
+template <bool PRE>
+__device__ __forceinline__ void fin_merge(const Fin& f, int N, int G, int Bg, int tiles, int tm, int g, int nb,
+                                          int ncols, const FinPre& pre, const MergeFirst& first) {
   __shared__ double comb[3][4][64];
   const int tid = threadIdx.x;
   const int n0 = nb * 64;
@@ -221,11 +243,19 @@ __device__ void fin_merge(const Fin& f, int N, int G, int Bg, int tiles, int tm,
   double n_a = 0.0, a = 0.0, q = 0.0;  // forward: (n, mean, M2); backward: (-, sum g, sum g xhat)
   for (int t0 = t_begin; t0 < t_end; t0 += MB) {
     float av[MB], qv[MB];
+    if (PRE && t0 == t_begin) {
 #pragma unroll
-    for (int u = 0; u < MB; ++u) {
-      const size_t o = (size_t)min(t0 + u, t_end - 1) * 2 * N;
-      av[u] = ld_sc1(pb + o);
-      qv[u] = ld_sc1(pb + o + N);
+      for (int u = 0; u < MB; ++u) {
+        av[u] = first.av[u];
+        qv[u] = first.qv[u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < MB; ++u) {
+        const size_t o = (size_t)min(t0 + u, t_end - 1) * 2 * N;
+        av[u] = ld_sc1(pb + o);
+        qv[u] = ld_sc1(pb + o + N);
+      }
     }
     if (f.bwd) {
 #pragma unroll
@@ -476,9 +506,14 @@ __device__ __forceinline__ f4 pro_apply(const TwArgs& p, f4 a, f4 a2, int m, int
 template <typename T, int TM, int TN, int PRO, int EPI, int DCH = 1>
 __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
   constexpr int PITCH = OpT<T>::PITCH;
-  constexpr int MT = TM / 64;      // 16-row m tiles per wave (4 waves stacked over the rows)
-  constexpr int NTL = TN / 16;     // 16-column n tiles per wave
-  constexpr int LA = (TM * (KC / 4) + 255) / 256;  // A float4 loads per thread per chunk
+  // the 4 waves tile the TM x TN output as WR row groups of 16 rows x WC column groups of TN / WC
+  // columns (TM = 64: 4 x 1, 32: 2 x 2, 16: 1 x 4)
+  static_assert(TM == 16 || TM == 32 || TM == 64, "row tile");
+  constexpr int WR = TM / 16, WC = 4 / WR;
+  constexpr int MT = 1;                 // 16-row m tiles per wave
+  constexpr int NTL = TN / (16 * WC);   // 16-column n tiles per wave
+  constexpr int AR = TM * (KC / 4);     // A float4 slots per chunk
+  constexpr int LA = (AR + 255) / 256;  // A float4 loads per thread per chunk
   constexpr int LW = (TN * (KC / 4) + 255) / 256;
   constexpr bool GEMM = EPI != EPI_NONE;
   constexpr bool SUMS = EPI == EPI_STATS || EPI == EPI_BWD;  // column sums + hand-off
@@ -560,7 +595,7 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
     }
     return;
   } else {
-    static_assert(LA * 256 == TM * 8 && LW * 256 == TN * 8, "tile loads must cover whole threads");
+    static_assert((LA * 256 == AR || (LA == 1 && AR < 256)) && LW * 256 == TN * 8, "tile loads");
     f4 ra[D][LA], ra2[D][LA], rw[D][LW];
     // Loads are unconditional (clamped to a valid address) and the chunk index is clamped, so the
     // pipelined body is straight-line code; out-of-range values are zeroed by selects where the
@@ -594,12 +629,16 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
 #pragma unroll
       for (int u = 0; u < LA; ++u) {
         const int idx = tid + 256 * u;
-        const int rl = idx >> 3, kl = (idx & 7) * 4, k = kc * KC + kl;
-        const bool ok = rl < nt && k < K;
+        const int rl = min(idx >> 3, TM - 1), kl = (idx & 7) * 4, k = kc * KC + kl;
+        const bool ok = (AR % 256 == 0 || idx < AR) && rl < nt && k < K;
         const int kt = min(k, K - 4);  // tables are read in range even for padding columns
         f4 v = pro_apply<PRO>(p, ra[u], ra2[u], mbase + rl, rl, kt, c0, c1, c2, c3, c4, rdot, rden, rcl, dk, drop);
         v = ok ? v : zero4;
-        lds_put4<T>(&As[buf][rl][kl], v);
+        // h = pro(A) (the weight gradient's operand, fp32) stored by n-block 0 as it is staged:
+        // every load of the workgroup was issued before the loop (D >= the chunk count) or is
+        // older than these stores, so no wait for them is needed before the kernel's end
+        if (hwrite && ok) *reinterpret_cast<f4*>(p.h_out + (size_t)(mbase + rl) * K + k) = v;
+        if (AR % 256 == 0 || idx < AR) lds_put4<T>(&As[buf][rl][kl], v);
       }
 #pragma unroll
       for (int u = 0; u < LW; ++u) {
@@ -623,7 +662,7 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
 #pragma unroll
     for (int st = 0; st < D; ++st) load(min(st, nk - 1), ra[st], ra2[st], rw[st]);
 
-    const int wrow = wave * (TM / 4);
+    const int wrow = (wave % WR) * 16, wcol = (wave / WR) * (TN / WC);
     const int r16 = lane & 15, q = lane >> 4;
     // epilogue operands of this tile, issued now and consumed after the loop: the pre-BN z of the
     // BatchNorm below (EPI_BWD), and the output-column constants (LDS)
@@ -634,7 +673,7 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
 #pragma unroll
         for (int j = 0; j < NTL; ++j)
           ez[i][j] = *reinterpret_cast<const f4*>(p.eZ + (size_t)(mbase + min(wrow + 16 * i + r16, nt - 1)) * N +
-                                                  min(n0 + 16 * j + 4 * q, N - 4));
+                                                  min(n0 + wcol + 16 * j + 4 * q, N - 4));
     }
     if (tid < TN) {
       const int n = min(n0 + tid, N - 1);
@@ -698,7 +737,7 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
 #pragma unroll
           for (int i = 0; i < MT; ++i) af[i] = *reinterpret_cast<const bf16x8t*>(&As[buf][wrow + 16 * i + r16][q * 8]);
 #pragma unroll
-          for (int j = 0; j < NTL; ++j) bfr[j] = *reinterpret_cast<const bf16x8t*>(&Bs[buf][16 * j + r16][q * 8]);
+          for (int j = 0; j < NTL; ++j) bfr[j] = *reinterpret_cast<const bf16x8t*>(&Bs[buf][wcol + 16 * j + r16][q * 8]);
 #pragma unroll
           for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -711,7 +750,7 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
 #pragma unroll
             for (int i = 0; i < MT; ++i) a4[i] = *reinterpret_cast<const f4*>(&As[buf][wrow + 16 * i + r16][16 * t + 4 * q]);
 #pragma unroll
-            for (int j = 0; j < NTL; ++j) b4[j] = *reinterpret_cast<const f4*>(&Bs[buf][16 * j + r16][16 * t + 4 * q]);
+            for (int j = 0; j < NTL; ++j) b4[j] = *reinterpret_cast<const f4*>(&Bs[buf][wcol + 16 * j + r16][16 * t + 4 * q]);
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -729,33 +768,6 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
     }
     TW_MARK(2);
 
-    // h = pro(A) for the weight gradient, written by n-block 0 at the very end (a global store
-    // before a barrier makes the barrier wait for it): re-read from L2 and transformed again, HB
-    // float4 loads per thread issued before any of their stores (a load after a store to a
-    // possibly aliasing array is not hoisted above it: one round trip per float4 otherwise)
-    auto write_h = [&]() {
-      if (!hwrite) return;
-      constexpr int HB = TWO ? 8 : 12;
-      const int k4n = K / 4, total = nt * k4n;
-      for (int base = 0; base < total; base += 256 * HB) {
-        f4 a[HB], a2[HB];
-#pragma unroll
-        for (int u = 0; u < HB; ++u) {
-          const int idx = min(base + tid + 256 * u, total - 1);
-          const size_t o = (size_t)(mbase + idx / k4n) * K + (idx % k4n) * 4;
-          a[u] = *reinterpret_cast<const f4*>(p.A + o);
-          if constexpr (TWO) a2[u] = *reinterpret_cast<const f4*>(p.A2 + o);
-        }
-#pragma unroll
-        for (int u = 0; u < HB; ++u) {
-          const int idx = base + tid + 256 * u;
-          if (idx >= total) break;
-          const int rl = idx / k4n, k = (idx % k4n) * 4;
-          *reinterpret_cast<f4*>(p.h_out + (size_t)(mbase + rl) * K + k) =
-              pro_apply<PRO>(p, a[u], a2[u], mbase + rl, rl, k, c0, c1, c2, c3, c4, rdot, rden, rcl, dk, drop);
-        }
-      }
-    };
     auto store_c = [&]() {
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
@@ -763,12 +775,12 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
         if (rl >= nt) continue;
 #pragma unroll
         for (int j = 0; j < NTL; ++j) {
-          const int n = n0 + 16 * j + 4 * q;
+          const int n = n0 + wcol + 16 * j + 4 * q;
           if (n < N) *reinterpret_cast<f4*>(p.C + (size_t)(mbase + rl) * N + n) = acc[i][j];
         }
       }
     };
-    // ---- epilogue: lane holds rows wrow + 16 i + r16, columns n0 + 16 j + 4 q + (0..3)
+    // ---- epilogue: lane holds rows wrow + 16 i + r16, columns n0 + wcol + 16 j + 4 q + (0..3)
     if constexpr (EPI == EPI_L2) {
       float ss[MT];
 #pragma unroll
@@ -778,7 +790,7 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
         for (int j = 0; j < NTL; ++j) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int nl = 16 * j + 4 * q + e;
+            const int nl = wcol + 16 * j + 4 * q + e;
             acc[i][j][e] += n0 + nl < N ? ctab[0][nl] : 0.f;
             ss[i] += acc[i][j][e] * acc[i][j][e];
           }
@@ -786,18 +798,29 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
         ss[i] += __shfl_xor(ss[i], 16, 64);
         ss[i] += __shfl_xor(ss[i], 32, 64);
       }
+      if constexpr (WC > 1) {
+        // the row's column groups sit in WC waves: their partial sums of squares meet in LDS and
+        // are added in column-group order (the same bits in every wave)
+        __shared__ float l2red[WC][TM];
+        lds_barrier();
+        if (q == 0) l2red[wave / WR][wrow + r16] = ss[0];
+        lds_barrier();
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WC; ++w) t += l2red[w][wrow + r16];
+        ss[0] = t;
+      }
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const int rl = wrow + 16 * i + r16;
         const float nrm = sqrtf(ss[i]);
         const float den = fmaxf(nrm, p.l2eps);
-        if (rl < nt && q == 0) p.norm_out[mbase + rl] = nrm;
+        if (rl < nt && q == 0 && wcol == 0) p.norm_out[mbase + rl] = nrm;
 #pragma unroll
         for (int j = 0; j < NTL; ++j) acc[i][j] /= den;
       }
       store_c();
       TW_MARK(6);
-      write_h();
       TW_MARK(7);
     } else {
       // EPI_STATS: z = acc + bias; EPI_BWD: g = mask(acc) of the BatchNorm below. Both go through
@@ -815,7 +838,7 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
         const int m = mbase + rl;
 #pragma unroll
         for (int j = 0; j < NTL; ++j) {
-          const int nl = 16 * j + 4 * q;
+          const int nl = wcol + 16 * j + 4 * q;
           float mk[4] = {1.f, 1.f, 1.f, 1.f};
           if constexpr (EPI == EPI_BWD) {
             if (edrop) {  // m*N + n even: two pair hashes
@@ -883,11 +906,13 @@ __global__ __launch_bounds__(256) void tower_kernel(TwArgs p) {
       const FinPre pre = fin_preload(p.fin, nblk, ncols);
       const bool last = fin_publish(p.fin, N, p.tiles, g, tile, nblk, ncols, v0, v1);
       TW_MARK(5);
-      // the last arriver's own outputs go out before its merge (their latency under the merge's)
+      // the last arriver issues its merge's first loads, then its own output stores (their
+      // latency under the loads'), then merges
+      MergeFirst mf;
+      if (last) fin_merge_load(p.fin, N, p.tiles, g, nblk, ncols, mf);
       store_c();
       TW_MARK(6);
-      write_h();
-      if (last) fin_merge(p.fin, N, p.G, p.Bg, p.tiles, TM, g, nblk, ncols, pre);
+      if (last) fin_merge<true>(p.fin, N, p.G, p.Bg, p.tiles, TM, g, nblk, ncols, pre, mf);
       TW_MARK(7);
     }
   }
@@ -941,15 +966,15 @@ __global__ __launch_bounds__(256) void tower_stats_kernel(const float* __restric
   const int ncols = min(64, C - (int)blockIdx.x * 64);
   const FinPre pre = fin_preload(fin, blockIdx.x, ncols);
   if (fin_publish(fin, C, tiles, g, tile, blockIdx.x, ncols, mu, m2t))
-    fin_merge(fin, C, G, Bg, tiles, TM_STATS, g, blockIdx.x, ncols, pre);
+    fin_merge<false>(fin, C, G, Bg, tiles, TM_STATS, g, blockIdx.x, ncols, pre, MergeFirst{});
 }
 
 // ---------------------------------------------------------------------------- host side
-constexpr int TM = 64;  // row tile of every GEMM instance
+constexpr int TM_MIN = 16;  // smallest GEMM row tile: rs_tower_part_floats sizes the partials for it
 
 unsigned long long* g_dbg = nullptr;  // rs_tower_debug_buffer: profiling only
 
-template <typename T, int TN, int PRO, int EPI, int DCH>
+template <typename T, int TM, int TN, int PRO, int EPI, int DCH>
 int launch_d(const TwArgs& a, int nblocks, hipStream_t st, const char* name) {
   TwArgs b = a;
   b.dbg = g_dbg;
@@ -961,36 +986,64 @@ int launch_d(const TwArgs& a, int nblocks, hipStream_t st, const char* name) {
   return 0;
 }
 
-// k chunks in flight: the smallest of 4 / 5 / 8 / 10 that covers the K extent, so every operand
-// load of a workgroup goes out in one round trip -- within the occupancy the grid needs (staged
-// registers: 16 VGPRs per chunk at TN = 64, 24 with a second A input or TN = 128; D = 10, a
-// two-input D = 8 and a TN = 128 D = 5 leave one workgroup per CU). Grids of more than two
-// workgroups per CU keep the short pipeline (3 chunks, 2 with a second input) at 2-3 per CU.
-template <typename T, int TN, int PRO, int EPI>
-int launch(const TwArgs& a, int nblocks, hipStream_t st, const char* name) {
+// k chunks in flight: the smallest of 2 / 3 / 4 / 5 / 8 / 10 that covers the K extent, so every
+// operand load of a workgroup goes out in one round trip, within a register budget for the staged
+// chunks set by the residency the grid needs (one or two workgroups per CU: ~160 VGPRs; more:
+// ~64). A chunk stages LA (x2 with a second A input) + LW float4 per thread.
+template <typename T, int TM, int TN, int PRO, int EPI>
+int launch_tm(const TwArgs& a, int nblocks, hipStream_t st, const char* name) {
   constexpr bool TWO = PRO == PRO_BNB || PRO == PRO_L2B;
+  constexpr int LA = (TM * (KC / 4) + 255) / 256, LW = (TN * (KC / 4) + 255) / 256;
+  constexpr int regs = 4 * (LA * (TWO ? 2 : 1) + LW);
   const int nk = cdiv(a.K, KC);
   const int64_t grid = (int64_t)nblocks * (cdiv(a.G * cdiv(a.Bg, TM), 8) * 8);
   const int per_cu = (int)((grid + 255) / 256);
-#define RS_TW_LAUNCH(DV) return launch_d<T, TN, PRO, EPI, DV>(a, nblocks, st, name)
-  if (per_cu > 2) {
-    if constexpr (TWO) RS_TW_LAUNCH(2);
-    else RS_TW_LAUNCH(3);
+  const int budget = per_cu > 2 ? 64 : (TN > 64 || TM == 64 ? 160 : 176);
+  static const int opts[] = {2, 3, 4, 5, 8, 10};
+  int d = 2;
+  for (int o : opts) {
+    if (o * regs > budget) break;
+    d = o;
+    if (o >= nk) break;
   }
-  if (nk <= 4) RS_TW_LAUNCH(4);
-  if constexpr (TN > 64) {
-    if (per_cu == 1 && nk <= 5) RS_TW_LAUNCH(5);
-    RS_TW_LAUNCH(4);
-  } else if constexpr (TWO) {
-    if (per_cu == 1 && nk == 5) RS_TW_LAUNCH(5);
-    if (per_cu == 1 && nk <= 8) RS_TW_LAUNCH(8);
-    RS_TW_LAUNCH(4);
-  } else {
-    if (nk <= 5) RS_TW_LAUNCH(5);
-    if (nk <= 8 || per_cu == 2 || nk > 10) RS_TW_LAUNCH(8);
-    RS_TW_LAUNCH(10);
+#define RS_TW_LAUNCH(DV) return launch_d<T, TM, TN, PRO, EPI, DV>(a, nblocks, st, name)
+  switch (d) {
+    case 2: RS_TW_LAUNCH(2);
+    case 3: RS_TW_LAUNCH(3);
+    case 4: RS_TW_LAUNCH(4);
+    case 5: RS_TW_LAUNCH(5);
+    case 8: RS_TW_LAUNCH(8);
+    default: RS_TW_LAUNCH(10);
   }
 #undef RS_TW_LAUNCH
+}
+
+int tower_tm_override() {
+  static const int v = [] {
+    const char* e = getenv("RSYS_TOWER_TM");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+// Row tile per launch (round 4): 64 rows when the grid already holds >= 2 workgroups per CU,
+// else 32 (the small-batch towers: B = 4096 gives 64 row tiles, so a 256-column Linear was 256
+// workgroups, one wave per SIMD with the staging VALU never under another wave's MFMA); the
+// final Linear (whole rows per workgroup for F.normalize, no statistics hand-off) goes to 16 rows
+// when 32 still leave CUs idle. RSYS_TOWER_TM=16/32/64 forces one (A/B).
+template <typename T, int TN, int PRO, int EPI>
+int launch(const TwArgs& a, int nblocks, hipStream_t st, const char* name) {
+  auto wgs = [&](int tm) { return (int64_t)nblocks * (cdiv(a.G * cdiv(a.Bg, tm), 8) * 8); };
+  int tm = tower_tm_override();
+  if (tm != 16 && tm != 32 && tm != 64) {
+    tm = wgs(64) >= 512 ? 64 : 32;
+    if (EPI == EPI_L2 && wgs(32) < 256) tm = 16;
+  }
+  if constexpr (EPI == EPI_L2) {
+    if (tm == 16) return launch_tm<T, 16, TN, PRO, EPI>(a, nblocks, st, name);
+  }
+  if (tm == 64) return launch_tm<T, 64, TN, PRO, EPI>(a, nblocks, st, name);
+  return launch_tm<T, 32, TN, PRO, EPI>(a, nblocks, st, name);
 }
 
 template <typename T>
@@ -1209,7 +1262,7 @@ extern "C" int rs_tower_debug_buffer(unsigned long long* buf) {
 }
 
 extern "C" int64_t rs_tower_part_floats(int G, int Bg, int N, int kind) {
-  const int tm = kind == 0 ? TM_STATS : TM;
+  const int tm = kind == 0 ? TM_STATS : TM_MIN;
   return (int64_t)G * cdiv(Bg, tm) * 2 * N;
 }
 

@@ -504,9 +504,6 @@ def exchange_table(t):
         return
     union = []
     for i, c in enumerate(t.calls):
-        if c.mode < 0:
-            raise NotImplementedError('data-parallel max-pooled large tables (arg-max scatter) '
-                                      'are not supported')
         if c.dseg is None:  # looked up without a backward (e.g. under no_grad)
             continue
         ids = bufs.get(('ids', i), (c.n,), torch.int32, dev)

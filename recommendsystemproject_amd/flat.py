@@ -283,7 +283,9 @@ class LazyTable:
         dev = self.param.device
         bag = seg.bag
         if seg.pool_mode not in (_hip.RS_POOL['mean'], _hip.RS_POOL['sum']):
-            raise NotImplementedError('row-sharded tables: max pooling is not supported')
+            # lazy_tables() keeps max-pooled tables replicated (their arg-max gradient is exchanged
+            # as per-lookup rows): a sharded one here means the table is also max-pooled elsewhere
+            raise RuntimeError('row-sharded table looked up with max pooling (mark it _rs_no_shard)')
         mode = SEG_MEAN if seg.pool_mode == _hip.RS_POOL['mean'] else SEG_SUM
         n = rows * bag
         ids32 = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
@@ -471,7 +473,7 @@ def shard_spec(param):
         return None
     d = torch.distributed
     thr = shard_threshold(d.get_world_size())
-    if thr <= 0 or int(param.shape[0]) < thr:
+    if thr <= 0 or int(param.shape[0]) < thr or getattr(param, '_rs_no_shard', False):
         return None
     return d.get_world_size(), d.get_rank()
 
@@ -628,8 +630,17 @@ def lazy_tables(module: torch.nn.Module):
     out = []
     # only lookup tables read through the gather (GenericTower.embeddings,
     # SequenceFeatureProcessor.embeddings); pos_emb is read whole by a GEMM epilogue
-    tables = [m for owner in module.modules() if isinstance(getattr(owner, 'embeddings', None), torch.nn.ModuleDict)
-              for m in owner.embeddings.values()]
+    tables = []
+    for owner in module.modules():
+        if not isinstance(getattr(owner, 'embeddings', None), torch.nn.ModuleDict):
+            continue
+        pooling = getattr(owner, 'pooling_config', None) or {}
+        for name, m in owner.embeddings.items():
+            if pooling.get(name) == 'max' and isinstance(m, torch.nn.Embedding):
+                # the arg-max backward has no partial-bag form: a max-pooled table stays replicated
+                # under data parallelism (dist.exchange_table, functions._max_as_single)
+                m.weight._rs_no_shard = True
+            tables.append(m)
     for m in tables:
         # the per-row kernels cover a row with at most 64 lanes x 4 columns (csrc/lookup.hip) and
         # the segment sum works on float4 rows: other widths stay ordinary (dense-Adam) tables

@@ -181,10 +181,11 @@ def _grad_tables(segs, calls, dout, tables, rows, params=()):
         ptr = dout.data_ptr() + 4 * s.out_col
         sharded = c is not None and getattr(tables[i]._rs_lazy, 'shard', None) is not None
         if c is not None and dp and c.mode < 0:
-            # the arg-max scatter below would write this rank's gradient into the local rows only:
-            # the data-parallel exchange has no max-pooled form
-            raise NotImplementedError('data-parallel max-pooled large tables (arg-max scatter) are not '
-                                      'supported')
+            # max pooling under data parallelism: the arg-max scatter's contributions as per-lookup
+            # gradient rows (rs_pool_max_grad), exchanged like rows x bag single-id lookups
+            # (GenericTower.py:159-160; max-pooled tables are never row-sharded, flat.lazy_tables)
+            big.append((tables[i]._rs_lazy, _max_as_single(c, s, dout), None))
+            continue
         # under data parallelism a call only keeps its output gradient rows here (rs_pack_rows,
         # any alignment / row stride); the exchange segment-sums every rank's
         if sharded or (c is not None and c.mode >= 0 and (dp or (ptr % 16 == 0 and dout.stride(0) % 4 == 0))):
@@ -195,7 +196,29 @@ def _grad_tables(segs, calls, dout, tables, rows, params=()):
         ops.gather_bwd(rest, rows, dout)
     _dp.note_writer(params, written=True)
     for t, c, ptr in big:
+        if ptr is None:  # max-pooled: its per-lookup gradient rows are already the call's dseg
+            continue
         t.segsum(c, ptr, dout.stride(0))
+
+
+def _max_as_single(c, s, dout):
+    """A max-pooled large-table call under data parallelism, turned into rows x bag single-id
+    lookups whose gradient rows (kept for the exchange, c.dseg) are the arg-max scatter's
+    contributions: dout[r] at each column's first arg-max position of bag r, zeros elsewhere. The
+    call's sorted values (r * bag + l) already index those rows."""
+    if s.idx_stride != s.bag:
+        raise RuntimeError('max-pooled large table: the id matrix must be contiguous')
+    n = c.rows * c.bag
+    g = torch.empty(n, s.dim, device=dout.device, dtype=torch.float32)
+    _hip.call('rs_pool_max_grad', s.table, s.idx, 8, c.rows, c.bag, s.idx_stride, s.vocab, s.dim, s.pad_idx,
+              dout.data_ptr() + 4 * s.out_col, dout.stride(0), g.data_ptr(), ops.stream())
+    if c.agreed is not None:
+        rmax, bmax, ragged = c.agreed
+        c.agreed = (rmax * bmax, 1, ragged)
+    c.rows, c.bag, c.row_stride, c.mode = n, 1, 1, SEG_ONE
+    c.local_rows = n
+    c.dseg = g
+    return c
 
 
 # ================================================================================ sequence input

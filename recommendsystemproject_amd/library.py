@@ -522,7 +522,7 @@ def _inbatch_loss_backward(grad: Tensor, ticket: Tensor, u_shape: List[int], h_s
                            h_stride: List[int]) -> Tuple[Tensor, Tensor, Tensor]:
     """-> dU, dI (U's shape), dH (H's shape and strides; [0] without hard negatives)."""
     ctx = _take(ticket)
-    dU, dI, _, dH, _ = _raw(fn.InBatchLossFn.backward)(ctx, grad)
+    dU, dI, _, dH = _raw(fn.InBatchLossFn.backward)(ctx, grad)[:4]
     return dU, dI, (dH if dH is not None else dU.new_empty(0))
 
 
