@@ -254,11 +254,24 @@ def start_cpu_worker(jobs):
 
 
 def collect_cpu_worker(proc, out, timeout):
-    try:
-        proc.wait(timeout=timeout)
-    except Exception:
-        proc.kill()
-        proc.wait()
+    """Wait for the CPU baselines (a progress line every 30 s: a silent run looks hung)."""
+    t0 = time.time()
+    while True:
+        try:
+            proc.wait(timeout=30)
+            break
+        except Exception:
+            pass
+        if time.time() - t0 > timeout:
+            proc.kill()
+            proc.wait()
+            break
+        try:
+            done = sorted(json.load(open(out)))
+        except Exception:
+            done = []
+        print(f'[bench] waiting for the CPU baselines ({time.time() - t0:.0f} s; done: {done})', file=sys.stderr,
+              flush=True)
     try:
         return json.load(open(out))
     except Exception:
@@ -425,6 +438,8 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
     args.batches distinct resident batches, profile one instrumented pass. Returns the result dict
     on rank 0 (None elsewhere); with args.pmc_bracket, prints the bracket line and returns None."""
     cfg = load_cfg(name, args)
+    if rank == 0:
+        print(f'[bench] {name} {dtype}: setting up', file=sys.stderr, flush=True)
     if zipf:
         cfg.setdefault('synthetic', {})['zipf'] = zipf
     precision.set_compute_dtype(dtype)
@@ -600,6 +615,9 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = float(el_t.item())
     final_loss = float(loss.item())
+    if rank == 0:
+        print(f'[bench] {name} {dtype}: {1e3 * el / args.steps:.3f} ms/step; instrumented passes next',
+              file=sys.stderr, flush=True)
     model.check_errors()  # device error flags (bad ids, NaN embeddings) of the timed steps
 
     # roofline of the dominant kernel: HIP events on the launch stream, eager instrumented steps.
@@ -761,25 +779,27 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
 
 
 def _cpu_jobs(args):
-    """The CPU baselines of this run (rank 0, N = 1): the primary workload, each extra workload's
-    config once, and C1 (BASELINE configs[0]). >= 10 steps per leg (C5: 2 steps, one leg -- its
-    oracle step at L = 200 with 10M-row tables takes tens of seconds on the host)."""
+    """The CPU baselines of this run (rank 0, N = 1): the primary workload (dropout as configured
+    and a p = 0 leg), each extra workload's config once (one leg), and C1 (BASELINE configs[0]).
+    >= 10 steps per leg (C5: 2 steps -- its oracle step at L = 200 with 10M-row tables takes tens
+    of seconds on the host). C3-Zipf reuses C3's: the oracle's dense step costs the same for any
+    ids. The legs run one after another in one child process, beside the GPU timing (~3 min)."""
     jobs, seen = [], set()
 
-    def add(key, config, zipf=None):
-        if (config, zipf) in seen:
+    def add(key, config, primary=False):
+        if config in seen:
             return
-        seen.add((config, zipf))
+        seen.add(config)
         c = yaml.safe_load(open(os.path.join(ROOT, 'configs', f'{config}.yaml')))
         B = args.batch or int(c['train']['batch_size'])
         big = config == 'c5'
-        jobs.append({'key': key, 'config': config, 'zipf': zipf, 'batch': B,
+        jobs.append({'key': key, 'config': config, 'zipf': args.zipf if primary else None, 'batch': B,
                      'seconds': 5.0 if big else args.cpu_baseline_seconds,
-                     'min_steps': 2 if big else 10, 'legs': ['config'] if big else ['config', '0']})
-    add(args.config, args.config, args.zipf)
+                     'min_steps': 2 if big else 10, 'legs': ['config', '0'] if primary and not big else ['config']})
+    add(args.config, args.config, primary=True)
     for ex in [e for e in (args.extra or '').split(',') if e]:
         nm = ex.partition(':')[0]
-        add(nm, 'c3' if nm == 'c3_zipf' else nm, 1.05 if nm == 'c3_zipf' else None)
+        add('c3' if nm == 'c3_zipf' else nm, 'c3' if nm == 'c3_zipf' else nm)
     add('c1', 'c1')
     return jobs
 
@@ -851,6 +871,7 @@ def main():
             out['cpu_baseline'] = cpu.get(args.config)
             for key in extras:
                 nm = key.rsplit('_bf16', 1)[0] if key.endswith('_bf16') else key
+                nm = 'c3' if nm == 'c3_zipf' else nm
                 if 'error' not in extras[key]:
                     extras[key]['cpu_baseline'] = cpu.get(nm)
             out['c1_cpu_baseline'] = cpu.get('c1')

@@ -828,7 +828,7 @@ __device__ __forceinline__ void keep_col4(const DropKey& dk, bool leven, uint32_
 }
 
 #ifndef RS_LONG_FWD_MINW
-#define RS_LONG_FWD_MINW 1
+#define RS_LONG_FWD_MINW 2  // two waves per SIMD (<= 256 VGPRs): the shared-tile merge pushed it to 276
 #endif
 template <int NT, bool DROP, bool QB>
 __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kernel(
@@ -862,7 +862,10 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
   for (int t = 0; t < NT; ++t) kb[t] = bf4(ld4(&Ks[t * 16 + r][4 * q]));
   col_frags<NT, kRowP>(&Vs[0][0], r, q, vb);
   float* T = Tsm[wave];
-  for (int tq = wave; tq < NT; tq += 4) {
+  // query tiles below NTF = 4 floor(NT / 4) go round-robin to the waves; the NT % 4 tiles past
+  // them are shared (see the end)
+  constexpr int NTF = 4 * (NT / 4), NR = NT - NTF;
+  for (int tq = wave; tq < NTF; tq += 4) {
     const int i = tq * 16 + r;
     const f4 z = {0.f, 0.f, 0.f, 0.f};
     const s4v qb = bf4(ld4(&Qs[i][4 * q]));
@@ -901,6 +904,92 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
     const int row = tq * 16 + (lane >> 2);
     if (row < L) st4q(out + ((int64_t)b * L + row) * d + h * 16 + 4 * (lane & 3), v);
   }
+  if constexpr (NR > 0) {
+    // Shared query tiles (C5, L = 200: tile 12 of 13, which made wave 0 do 4 tiles against 3):
+    // wave w takes key tiles tk = w mod 4 of each, the partial (max, sum, P V) of the four waves
+    // are merged through LDS in wave order (the online-softmax rescale), and wave x writes tile
+    // NTF + x.
+    __shared__ float mlp[4][NR][2][16];
+    __shared__ __attribute__((aligned(16))) f4 olp[4][NR][64];
+#pragma unroll
+    for (int x = 0; x < NR; ++x) {
+      const int tq = NTF + x;
+      const int i = tq * 16 + r;
+      const f4 z = {0.f, 0.f, 0.f, 0.f};
+      const s4v qb = bf4(ld4(&Qs[i][4 * q]));
+      f4 sv[NT];
+      float m = -INFINITY;
+#pragma unroll
+      for (int tk = 0; tk < NT; ++tk) {
+        if ((tk & 3) != wave) continue;  // wave-uniform
+        sv[tk] = mfma16(kb[tk], qb, z);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if ((kbits >> (4 * tk + e)) & 1ull) m = fmaxf(m, sv[tk][e] * scale2);
+      }
+      m = xmax(m);
+      float l = 0.f;
+      const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
+      f4 o = z;
+#pragma unroll
+      for (int tk = 0; tk < NT; ++tk) {
+        if ((tk & 3) != wave) continue;
+        float mk[4] = {1.f, 1.f, 1.f, 1.f};
+        if (DROP) attn_keep4(dk, leven, rowbase + tk * 16 + 4 * q, mk);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float pv = ((kbits >> (4 * tk + e)) & 1ull) ? __builtin_amdgcn_exp2f(sv[tk][e] * scale2 - m) : 0.f;
+          l += pv;
+          sv[tk][e] = DROP ? pv * mk[e] : pv;
+        }
+        o = mfma16(bf4(sv[tk]), vb[tk], o);
+      }
+      l = xsum(l);
+      if (q == 0) {
+        mlp[wave][x][0][r] = m;
+        mlp[wave][x][1][r] = l;
+      }
+      olp[wave][x][lane] = o;
+    }
+    __syncthreads();
+    if (wave < NR) {
+      const int x = wave, tq = NTF + x;
+      // this lane's rows: queries 4q + e (the MFMA output layout); the lse of query r (q == 0)
+      f4 on;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int qi = 4 * q + e;
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) M = fmaxf(M, mlp[w][x][0][qi]);
+        float lt = 0.f, ot = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float mw = mlp[w][x][0][qi];
+          const float f = mw == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw - M);
+          lt += f * mlp[w][x][1][qi];
+          ot += f * olp[w][x][lane][e];
+        }
+        on[e] = ot * __builtin_amdgcn_rcpf(lt);
+      }
+      const int i = tq * 16 + r;
+      if (q == 0 && i < L) {
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) M = fmaxf(M, mlp[w][x][0][r]);
+        float lt = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float mw = mlp[w][x][0][r];
+          lt += (mw == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw - M)) * mlp[w][x][1][r];
+        }
+        lse[(int64_t)bh * L + i] = (M + __builtin_amdgcn_logf(lt)) * kLn2;
+      }
+      const f4 v = tile_rows<kRowP>(T, on, r, q, lane);
+      const int row = tq * 16 + (lane >> 2);
+      if (row < L) st4q(out + ((int64_t)b * L + row) * d + h * 16 + 4 * (lane & 3), v);
+    }
+  }
 }
 
 // Single-pass backward: key-parallel (the lane's query-on-row tiles feed dV and dK), plus dQ.
@@ -908,6 +997,10 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
 // the wave's LDS image into an A fragment; each wave keeps partial dQ tiles for every query tile
 // in registers and the four partials are summed in wave order at the end (deterministic). P and
 // dP are computed once per (query, key) pair instead of twice (one exp, half a hash per pair).
+// Balance: wave w owns key tiles w, w + 4, ... below NTF = 4 floor(NT / 4); the NT % 4 tiles past
+// them are shared, wave w taking their pairs with query tiles tq = w mod 4, and their dK / dV
+// partials are summed in wave order at the end. (C5, L = 200, NT = 13: the busiest wave had 4 key
+// tiles = 52 (query, key) tile pairs against 39 for the others; now 43 / 42 / 42 / 42.)
 template <int NT, bool DROP, bool QB>
 __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
     const void* __restrict__ qkv_, const uint8_t* __restrict__ key_pad,
@@ -915,9 +1008,14 @@ __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
     void* __restrict__ dqkv_, int B, int L, int d, int H, float scale, float pdrop,
     const int64_t* __restrict__ key, int site) {
   constexpr int LP = NT * 16;
-  constexpr int NW = (NT + 3) / 4;  // key tiles per wave
+  constexpr int NW0 = NT / 4;       // key tiles owned by each wave
+  constexpr int NTF = 4 * NW0;      // the first shared key tile
+  constexpr int NR = NT - NTF;      // shared key tiles
+  constexpr int NW = NW0 + NR;      // key tiles a wave visits
   constexpr int TP = 20;
-  __shared__ __attribute__((aligned(16))) float img[4][LP][kRowP];  // Q, K, V, dO; then dQ partials
+  // Q, K, V, dO; then the shared tiles' dK / dV partials; then the dQ partials
+  __shared__ __attribute__((aligned(16))) float img[4][LP][kRowP];
+  static_assert(4 * NR * 2 * 256 <= 4 * LP * kRowP, "shared-tile partials fit the image");
   __shared__ __attribute__((aligned(16))) float L2s[LP];  // lse * log2(e)
   __shared__ __attribute__((aligned(16))) float Ds[LP];   // D_i = dO_i . O_i
   __shared__ float Kv[LP];                                // 1: key j is valid
@@ -974,7 +1072,7 @@ __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
   f4 dk_acc[NW], dv_acc[NW], dq_acc[NT];
 #pragma unroll
   for (int u = 0; u < NW; ++u) {
-    const int tk = wave + 4 * u < NT ? wave + 4 * u : NT - 1;
+    const int tk = u < NW0 ? wave + 4 * u : NTF + (u - NW0);
     kr[u] = bf4(ld4(&Ks[tk * 16 + r][4 * q]));
     vr[u] = bf4(ld4(&Vs[tk * 16 + r][4 * q]));
     s4v c1[1];
@@ -995,8 +1093,8 @@ __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
     dq_acc[tq] = z;
 #pragma unroll
     for (int u = 0; u < NW; ++u) {
-      const int tk = wave + 4 * u;
-      if (tk >= NT) break;
+      const int tk = u < NW0 ? wave + 4 * u : NTF + (u - NW0);
+      if (u >= NW0 && (tq & 3) != wave) continue;  // a shared tile: this query tile's wave only
       const f4 sacc = mfma16(qr, kr[u], z);  // S[query 16 tq + 4q + e][key 16 tk + r]
       const f4 pacc = mfma16(gr, vr[u], z);  // dP[query][key] = dO_i . V_j
       float mk[4] = {1.f, 1.f, 1.f, 1.f};
@@ -1022,11 +1120,10 @@ __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
       dq_acc[tq] = mfma16(bf4(dst), kc[u], dq_acc[tq]);  // dS K: [query 4q + e][c = r]
     }
   }
-  // dK / dV rows of this wave's key tiles
+  // dK / dV rows of this wave's own key tiles
 #pragma unroll
-  for (int u = 0; u < NW; ++u) {
+  for (int u = 0; u < NW0; ++u) {
     const int tk = wave + 4 * u;
-    if (tk >= NT) break;
     const f4 vk = tile_rows<TP>(T, dk_acc[u] * scale, r, q, lane);
     const f4 vv = tile_rows<TP>(T, dv_acc[u], r, q, lane);
     const int row = tk * 16 + (lane >> 2);
@@ -1035,8 +1132,36 @@ __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
       st4q(dbase + (int64_t)row * ld + 2 * d + 4 * (lane & 3), vv);
     }
   }
+  __syncthreads();  // the images are free
+  if constexpr (NR > 0) {
+    // shared key tiles: the four waves' dK / dV partials (MFMA layout, one f4 per lane) summed in
+    // wave order; wave x < NR finishes shared tile NTF + x
+    f4* part = reinterpret_cast<f4*>(&img[0][0][0]);  // [wave][x][dk, dv][lane]
+#pragma unroll
+    for (int x = 0; x < NR; ++x) {
+      part[((wave * NR + x) * 2 + 0) * 64 + lane] = dk_acc[NW0 + x];
+      part[((wave * NR + x) * 2 + 1) * 64 + lane] = dv_acc[NW0 + x];
+    }
+    __syncthreads();
+    if (wave < NR) {
+      const int x = wave;
+      f4 sk = part[(x * 2 + 0) * 64 + lane], sv = part[(x * 2 + 1) * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        sk += part[((w * NR + x) * 2 + 0) * 64 + lane];
+        sv += part[((w * NR + x) * 2 + 1) * 64 + lane];
+      }
+      const f4 vk = tile_rows<TP>(T, sk * scale, r, q, lane);
+      const f4 vv = tile_rows<TP>(T, sv, r, q, lane);
+      const int row = (NTF + x) * 16 + (lane >> 2);
+      if (row < L) {
+        st4q(dbase + (int64_t)row * ld + d + 4 * (lane & 3), vk);
+        st4q(dbase + (int64_t)row * ld + 2 * d + 4 * (lane & 3), vv);
+      }
+    }
+    __syncthreads();
+  }
   // dQ: the four waves' partial tiles summed in wave order through the (now free) images
-  __syncthreads();
   float* part = &img[0][0][0] + wave * LP * 16;
 #pragma unroll
   for (int tq = 0; tq < NT; ++tq)

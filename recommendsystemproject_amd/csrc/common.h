@@ -68,6 +68,12 @@ inline bool getenv_flag(const char* name) {
   return v && v[0] && !(v[0] == '0' && v[1] == 0);
 }
 
+// the same for a switch that defaults on: true iff set to exactly "0"
+inline bool getenv_flag0(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] == '0' && v[1] == 0;
+}
+
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 

@@ -32,7 +32,7 @@ constexpr int64_t kSmallTableBytes = 48 * 1024;
 
 constexpr int kRowsPerLane = 4;            // forward sparse rows per lane on token-sized launches
 constexpr int kBagBatch = 16;              // bag ids (and rows) loaded per batch
-constexpr int kBagBatchNt = 8;             // the same for rows of large tables (non-temporal loads)
+constexpr int kBagBatchNt = 4;             // the same for rows of large tables (non-temporal loads)
 constexpr int64_t kNtTableBytes = 64ll << 20;  // tables from this size: rows read once, nt loads
 constexpr int kLazyBagBatch = 8;           // the same with exp_avg / exp_avg_sq rows beside them
 // forward: a table of at most this size whose workgroup reads at least as many row bytes as the
@@ -74,7 +74,9 @@ struct SegLaunch {
   int16_t rranges[kMaxSeg];
   int16_t rchunks[kMaxSeg];
   int rblock_start[kMaxSeg + 1];
-  uint8_t tiny[kMaxSeg];   // bwd: tiny table by the register-accumulator kernel
+  uint8_t tiny[kMaxSeg];   // bwd: small table by the slot-image kernel (gather_bwd_slot_kernel)
+  int16_t slots[kMaxSeg];  // bwd: its row slots per workgroup (private [V][D] LDS images)
+  int slot_lds;            // bwd: dynamic LDS bytes of the slot kernel
   uint8_t rpt[kMaxSeg];    // fwd sparse segments: rows per lane (kRowsPerLane on token-sized launches)
   uint8_t nt[kMaxSeg];     // fwd: rows of a large table -- non-temporal loads, shorter bag batches
   int16_t tblocks[kMaxSeg];
@@ -147,9 +149,9 @@ __device__ __forceinline__ void lazy_replay(const LazyLaunch& z, int2 last, int 
 
 // Pooled bag: the (un-normalised) sum or max of positions [lbeg, lend) of row `row`'s bag.
 // LAZY: the rows read through the catch-up.
-// NT (rows of a large table, read once per step): non-temporal row loads and 8 rows in flight per
-// lane group instead of 16 (tools/gather_sweep.hip, C3's history shape from HBM: 16 rows default
-// policy 4.7 TB/s, 8 rows nt 5.4 TB/s)
+// NT (rows of a large table, read once per step): non-temporal row loads and 4 rows in flight per
+// lane group instead of 16, bags not split (tools/gather_sweep.hip, C3's history shape from HBM,
+// 8 rotating id sets: 16 rows split 4 ways, default policy, 4.7 TB/s; 4 rows unsplit nt 5.5 TB/s)
 template <bool VEC, bool LAZY = false, bool NT = false>
 __device__ __forceinline__ void pool_acc(const SegLaunch& a, const rs_feature_seg_t& sg, int row,
                                          int c, int lbeg, int lend, float* acc) {
@@ -206,7 +208,7 @@ __device__ __forceinline__ void pool_acc(const SegLaunch& a, const rs_feature_se
   if (bad && a.err) atomicOr(a.err, 1);
 }
 
-template <bool VEC, bool LAZY = false>
+template <bool VEC, bool LAZY = false, bool NT = false>
 __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int row, int chunk) {
   constexpr int W = VEC ? 4 : 1;
   const int c = chunk * W;
@@ -216,7 +218,7 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
     const int64_t id = sg.idx[(int64_t)row * sg.idx_stride];
     if (id_ok(id, sg.vocab, a.err)) {
       const float* pr = sg.table + id * sg.dim + c;
-      load_row<VEC>(pr, acc);
+      load_row<VEC, NT && !LAZY>(pr, acc);
       if constexpr (LAZY) {
         float mv[4], vv[4];
         const int2 l = reinterpret_cast<const int2*>(sg.lazy_last)[id];
@@ -226,7 +228,7 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
       }
     }
   } else if (sg.kind == RS_SEG_POOL) {
-    pool_acc<VEC, LAZY>(a, sg, row, c, 0, sg.bag, acc);
+    pool_acc<VEC, LAZY, NT>(a, sg, row, c, 0, sg.bag, acc);
     if (sg.pool_mode == RS_POOL_MEAN) {
       const float n = (float)sg.bag;
 #pragma unroll
@@ -383,7 +385,8 @@ __global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
   }
   const int row = lb * a.rpb[s] + r;
   if (row >= a.rows) return;
-  if (a.vec[s]) gather_seg<true>(a, sg, row, chunk);
+  if (a.vec[s] && a.nt[s]) gather_seg<true, false, true>(a, sg, row, chunk);
+  else if (a.vec[s]) gather_seg<true>(a, sg, row, chunk);
   else gather_seg<false>(a, sg, row, chunk);
 }
 
@@ -532,70 +535,63 @@ __global__ __launch_bounds__(256) void gather_bwd_small_kernel(SegLaunch a) {
   }
 }
 
-// Tiny tables (<= 32 rows, D | 64, bags of <= 4 ids: C2's genre / age / occupation / gender
-// tables): per-lane register accumulators instead of LDS float atomics (which run at ~0.5
-// lane-adds per clock per CU: C2's 30 x 8 genre table, 614,400 bag ids per step, took 33 us in
-// the small-table kernel). Lane (stream, c) owns column c of a stream of lookup rows and keeps
-// acc[v] for every table row v: each bag id adds its row's dout column to acc[id] by 32
-// compare-selects (VALU is idle here; 147 M selects at C2 are ~1 us of the chip). Rows are taken
-// 8 at a time with their ids and dout columns loaded together. The streams of a workgroup are
-// summed in stream order through LDS, the workgroup's [V, D] tile goes to ws[block], and
-// reduce_partials_kernel adds the blocks in order: bitwise reproducible, unlike the small-table
-// kernel's atomics. Opt-in (RSYS_TINY_GRAD=1): at C2's genre table it measured 46 + 8 us against
-// the small-table kernel's 33 us (a one-hot f32-MFMA variant, Cnt^T dout on 32x32x2 tiles, 45 us:
-// both latency-bound at ~100 lookup rows per wave).
-constexpr int kTinyRows = 32;
-constexpr int kTinyBag = 4;
-constexpr int kTinyUnroll = 8;
+// Small tables (<= 48 KB: C2 / C3's gender, age, occupation, zip, genre, release-year tables,
+// and the per-token genre bags of the history: 614,400 bag ids per step into a 30 x 8 table):
+// slot-private LDS images, no atomics, bitwise reproducible. A workgroup owns a contiguous run of
+// lookup rows; its lanes form `slots` groups of D (lane = slot * D + column) and slot k takes
+// rows k, k + slots, ... of the run, adding each bag id's dout column into ITS OWN [V][D] image
+// by a plain LDS read-modify-write (no two lanes ever touch one word, so no atomics and one fixed
+// order per word). The slot images are then summed in slot order into the workgroup's partial,
+// and reduce_partials_kernel adds the workgroup partials in order. Per bag id that is two LDS
+// operations per column lane -- the earlier kernels compared every id with every table row
+// (register accumulators: V compare-selects per id and column, 46 us at C2's genre table) or
+// used LDS / global float atomics (33 us, order-dependent bits).
+constexpr int kSlotRowsInFlight = 4;
 
-__global__ __launch_bounds__(256) void gather_bwd_tiny_kernel(SegLaunch a) {
-  __shared__ float red[256][kTinyRows + 1];
+__global__ __launch_bounds__(256) void gather_bwd_slot_kernel(SegLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) float img[];  // [slots][V][D]
   int s = 0;
   while (s + 1 < a.nseg && (int)blockIdx.x >= a.tblock_start[s + 1]) ++s;
   const rs_feature_seg_t& sg = a.segs[s];
   const int lb = blockIdx.x - a.tblock_start[s];
-  const int nblk = a.tblocks[s];
+  const int nblk = a.tblocks[s], nsl = a.slots[s];
   const int D = sg.dim;
-  const int c = threadIdx.x % D, str = threadIdx.x / D, nstr = 256 / D;
-  const int bag = sg.kind == RS_SEG_POOL ? sg.bag : 1;
-  const float sc = sg.kind == RS_SEG_POOL && sg.pool_mode == RS_POOL_MEAN ? 1.f / (float)bag : 1.f;
-  const int64_t pad = sg.pad_idx;
-  const int64_t step = (int64_t)nblk * nstr;
-  float acc[kTinyRows];
+  const int E = (int)(sg.vocab * D);
+  for (int e = threadIdx.x; e < nsl * E; e += 256) img[e] = 0.f;
+  __syncthreads();
+  const int sl = threadIdx.x / D, c = threadIdx.x - sl * D;
+  const int per = (a.rows + nblk - 1) / nblk;
+  const int r0 = lb * per, r1 = r0 + per < a.rows ? r0 + per : a.rows;
+  if (sl < nsl) {
+    const bool pool = sg.kind == RS_SEG_POOL;
+    const int bag = pool ? sg.bag : 1;
+    const float sc = pool && sg.pool_mode == RS_POOL_MEAN ? 1.f / (float)bag : 1.f;
+    const int64_t pad = sg.pad_idx, V = sg.vocab;
+    float* my = img + sl * E + c;
+    for (int r = r0 + sl; r < r1; r += kSlotRowsInFlight * nsl) {
+      float g[kSlotRowsInFlight];
+      int64_t row[kSlotRowsInFlight];
 #pragma unroll
-  for (int v = 0; v < kTinyRows; ++v) acc[v] = 0.f;
-  for (int64_t r0 = (int64_t)lb * nstr + str; r0 < a.rows; r0 += step * kTinyUnroll) {
-    float gv[kTinyUnroll];
-    int id[kTinyUnroll][kTinyBag];
+      for (int u = 0; u < kSlotRowsInFlight; ++u) {
+        row[u] = r + u * nsl;
+        g[u] = row[u] < r1 ? a.dout[row[u] * a.ldo + sg.out_col + c] * sc : 0.f;
+      }
+      for (int l = 0; l < bag; ++l) {
+        int64_t id[kSlotRowsInFlight];
 #pragma unroll
-    for (int u = 0; u < kTinyUnroll; ++u) {
-      const int64_t row = r0 + u * step;
-      const bool ok = row < a.rows;
-      const int64_t rr = ok ? row : 0;
-      gv[u] = ok ? a.dout[rr * a.ldo + sg.out_col + c] * sc : 0.f;
+        for (int u = 0; u < kSlotRowsInFlight; ++u) id[u] = row[u] < r1 ? sg.idx[row[u] * sg.idx_stride + l] : -1;
 #pragma unroll
-      for (int l = 0; l < kTinyBag; ++l) {
-        const int64_t x = ok && l < bag ? sg.idx[rr * sg.idx_stride + l] : -1;
-        id[u][l] = (x == pad || x < 0 || x >= kTinyRows) ? -1 : (int)x;
+        for (int u = 0; u < kSlotRowsInFlight; ++u)
+          if (id[u] >= 0 && id[u] < V && id[u] != pad) my[id[u] * D] += g[u];
       }
     }
-#pragma unroll
-    for (int u = 0; u < kTinyUnroll; ++u)
-#pragma unroll
-      for (int l = 0; l < kTinyBag; ++l)
-#pragma unroll
-        for (int v = 0; v < kTinyRows; ++v) acc[v] += id[u][l] == v ? gv[u] : 0.f;
   }
-#pragma unroll
-  for (int v = 0; v < kTinyRows; ++v) red[threadIdx.x][v] = acc[v];
   __syncthreads();
-  const int n = (int)(sg.vocab * D);
-  float* dst = a.ws + a.pws_off[s] + (int64_t)lb * n;
-  for (int i = threadIdx.x; i < n; i += 256) {
-    const int v = i / D, cc = i - v * D;
-    float t = 0.f;
-    for (int k = 0; k < nstr; ++k) t += red[k * D + cc][v];
-    dst[i] = t;
+  float* dst = a.ws + a.pws_off[s] + (int64_t)lb * E;
+  for (int e = threadIdx.x; e < E; e += 256) {
+    float t = img[e];
+    for (int k = 1; k < nsl; ++k) t += img[k * E + e];
+    dst[e] = t;
   }
 }
 
@@ -837,10 +833,12 @@ __global__ __launch_bounds__(1024) void dense_bwd_kernel(SegLaunch a) {
 }
 
 // Ranged table-gradient plan of one segment (0 ranges: the atomic scatter). Sparse ids and sum /
-// mean bags of a table of 48 KB - 4 MB (smaller ones: the small-table kernel) hit >= 8 times per
-// row on average, D in {16, 32, 64, 128, 256} (D/4 lanes per lookup divide a wave into <= 16
-// groups); ranges of 64 KB; chunks of >= 2 x vocab lookups (the [vocab, dim] partial of a chunk
-// costs no more than its dout rows), a multiple of 8 (XCD mapping), at most 1024 / ranges.
+// mean bags of a table of 48 KB - 4 MB (smaller ones: the slot kernel), D in {16, 32, 64, 128,
+// 256} (D/4 lanes per lookup divide a wave into <= 16 groups); ranges of 64 KB; chunks of >= 2 x
+// vocab lookups (the [vocab, dim] partial of a chunk costs no more than its dout rows), a multiple
+// of 8 (XCD mapping), at most 1024 / ranges. Round 4: also the tables hit < 8 times per row (C2's
+// 6,060-row user and 3,500-row item tables at 4,096 lookups), which took the atomic scatter: every
+// table of this size now gets a bitwise-reproducible gradient.
 struct RangePlan { int rows, ranges, chunks; };
 
 RangePlan range_plan(const rs_feature_seg_t& g, int rows, bool vec) {
@@ -849,8 +847,8 @@ RangePlan range_plan(const rs_feature_seg_t& g, int rows, bool vec) {
   const bool dim_ok = g.dim >= 16 && g.dim <= 256 && 256 % g.dim == 0;
   const int64_t tbytes = g.vocab * g.dim * 4;
   const int64_t n = (int64_t)rows * (g.kind == RS_SEG_POOL ? g.bag : 1);
-  if (!table_kind || !vec || !dim_ok || tbytes <= kSmallTableBytes || tbytes > (4 << 20) ||
-      n < 8 * g.vocab || getenv_flag("RSYS_NO_RANGE_GRAD"))
+  if (!table_kind || !vec || !dim_ok || tbytes <= kSmallTableBytes || tbytes > (4 << 20) || n == 0 ||
+      getenv_flag("RSYS_NO_RANGE_GRAD"))
     return r;
   int R = kRangeBytes / (g.dim * 4);
   const int nr = (int)((g.vocab + R - 1) / R);
@@ -887,14 +885,16 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.vec[s] = vec;
     a.chunks[s] = C;
     const bool table_kind = g.kind == RS_SEG_SPARSE || g.kind == RS_SEG_POOL;
+    // small tables: the slot-image kernel (deterministic); a max-pooled one (its arg-max needs the
+    // table rows) keeps the small-table kernel's atomics, as does RSYS_SLOT_GRAD=0 (A/B)
     a.tiny[s] = bwd && table_kind && !(g.kind == RS_SEG_POOL && g.pool_mode == RS_POOL_MAX) &&
-               g.vocab <= kTinyRows && g.dim <= 64 && 64 % g.dim == 0 &&
-               (g.kind == RS_SEG_SPARSE || g.bag <= kTinyBag) && getenv_flag("RSYS_TINY_GRAD");
+               g.vocab * g.dim * 4 <= kSmallTableBytes && g.dim <= 64 && !getenv_flag0("RSYS_SLOT_GRAD");
     a.small[s] = bwd && table_kind && g.vocab * g.dim * 4 <= kSmallTableBytes && !a.tiny[s];
     // Split long sum/mean bags over S row groups while the launch is short of ~8 waves per SIMD
     // and every group keeps >= 8 positions (C3: B = 4096, L = 50, D = 128 -> S = 4).
     int S = 1;
-    if (g.kind == RS_SEG_POOL && g.pool_mode != RS_POOL_MAX && !a.small[s]) {
+    const bool nt = !bwd && vec && table_kind && g.vocab * g.dim * 4 >= kNtTableBytes && !getenv_flag("RSYS_GATHER_NO_NT");
+    if (g.kind == RS_SEG_POOL && g.pool_mode != RS_POOL_MAX && !a.small[s] && !nt) {
       while (2 * S * C <= 256 && (g.bag + 2 * S - 1) / (2 * S) >= 8 &&
              (int64_t)rows * C * S < 8192 * 64)
         S *= 2;
@@ -904,7 +904,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.rpt[s] = (!bwd && vec && g.kind == RS_SEG_SPARSE && (int64_t)rows * C >= (int64_t)2048 * 256)
                    ? kRowsPerLane : 1;
     a.rpb[s] = 256 / (C * S);
-    a.nt[s] = !bwd && vec && table_kind && g.vocab * g.dim * 4 >= kNtTableBytes && !getenv_flag("RSYS_GATHER_NO_NT");
+    a.nt[s] = nt;
     a.stage[s] = 0;
     if (!bwd && table_kind && vec) {
       const int64_t tbytes = g.vocab * g.dim * 4;
@@ -939,13 +939,26 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
   }
   a.rblock_start[nseg] = rb;
   int ob = 0;
+  a.slot_lds = 0;
   for (int s = 0; s < nseg; ++s) {
     a.tblock_start[s] = ob;
     a.tblocks[s] = 0;
-    if (a.tiny[s]) {  // >= 16 lookup rows per stream, at most 256 workgroups
-      int nb = cdiv(rows, 16 * (256 / segs_host[s].dim));
-      a.tblocks[s] = (int16_t)(nb > 256 ? 256 : nb);
+    a.slots[s] = 0;
+    if (a.tiny[s]) {
+      // slots: as many D-lane groups as a workgroup holds, within 64 KB of images; workgroups:
+      // >= kSlotRowsInFlight rows per slot, <= 256, and <= 4 MB of partials in all
+      const int64_t E = segs_host[s].vocab * segs_host[s].dim;
+      int nsl = 256 / segs_host[s].dim;
+      const int fit = (int)((64 * 1024) / (E * 4));
+      nsl = nsl < fit ? nsl : fit;
+      nsl = nsl < 1 ? 1 : nsl;
+      int64_t nb = cdiv(rows, nsl * kSlotRowsInFlight);
+      const int64_t cap = std::max<int64_t>(8, (4ll << 20) / (E * 4));
+      nb = std::min<int64_t>(std::min<int64_t>(nb, 256), cap);
+      a.slots[s] = (int16_t)nsl;
+      a.tblocks[s] = (int16_t)(nb < 1 ? 1 : nb);
       ob += a.tblocks[s];
+      a.slot_lds = std::max<int>(a.slot_lds, (int)(nsl * E * 4));
     }
   }
   a.tblock_start[nseg] = ob;
@@ -1094,8 +1107,8 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
     RS_CHECK_LAUNCH("rs_gather_bwd range");
   }
   if (a.tblock_start[nseg] > 0) {
-    gather_bwd_tiny_kernel<<<a.tblock_start[nseg], 256, 0, st>>>(a);
-    RS_CHECK_LAUNCH("rs_gather_bwd tiny");
+    gather_bwd_slot_kernel<<<a.tblock_start[nseg], 256, a.slot_lds, st>>>(a);
+    RS_CHECK_LAUNCH("rs_gather_bwd slot");
   }
   if (a.ws_floats > 0) {
     int64_t nel = 0;

@@ -1026,17 +1026,23 @@ int tower_tm_override() {
   return v;
 }
 
-// Row tile per launch (round 4): 64 rows when the grid already holds >= 2 workgroups per CU,
-// else 32 (the small-batch towers: B = 4096 gives 64 row tiles, so a 256-column Linear was 256
-// workgroups, one wave per SIMD with the staging VALU never under another wave's MFMA); the
-// final Linear (whole rows per workgroup for F.normalize, no statistics hand-off) goes to 16 rows
-// when 32 still leave CUs idle. RSYS_TOWER_TM=16/32/64 forces one (A/B).
+// Row tile per launch (round 4): 64 rows when that grid fills the chip (193..256 workgroups, or
+// >= 512), else 32 (B = 4096 gives 64 row tiles: a 128-column Linear was 128 workgroups on 256 CUs); the final
+// Linear (whole rows per workgroup for F.normalize, no statistics hand-off) goes to 16 rows when
+// 32 still leave CUs idle. Measured (tools/tower_phases.py, C3 user tower): the 128-column
+// forward 22 -> 17 us, the final Linear 14 -> 6 us, the 128-column backward 19 -> 17 us; 32-row
+// tiles on grids that were already >= 256 workgroups were slower (their last arriver merges twice
+// the tiles). RSYS_TOWER_TM=16/32/64 forces one (A/B).
 template <typename T, int TN, int PRO, int EPI>
 int launch(const TwArgs& a, int nblocks, hipStream_t st, const char* name) {
   auto wgs = [&](int tm) { return (int64_t)nblocks * (cdiv(a.G * cdiv(a.Bg, tm), 8) * 8); };
   int tm = tower_tm_override();
   if (tm != 16 && tm != 32 && tm != 64) {
-    tm = wgs(64) >= 512 ? 64 : 32;
+    // 64 rows fill the chip once (193..256 workgroups) or at two and more per CU; between, a
+    // 64-row grid runs a second partial wave of workgroups (C3's 320-workgroup first-layer
+    // backward: 40 us at 64 rows, 25 us at 32)
+    const int64_t w64 = wgs(64);
+    tm = (w64 > 192 && w64 <= 256) || w64 >= 512 ? 64 : 32;
     if (EPI == EPI_L2 && wgs(32) < 256) tm = 16;
   }
   if constexpr (EPI == EPI_L2) {

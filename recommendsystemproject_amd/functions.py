@@ -1010,7 +1010,7 @@ class InBatchLossFn(torch.autograd.Function):
         loss = torch.empty((), device=dev, dtype=torch.float32)
         if fused:
             w = ops.ws(_hip.lib().rs_inbatch_ce_fused_ws_bytes(B, D), dev)
-            extra = (S.data_ptr(),) if sfx else ()
+            extra = (S.data_ptr() if S is not None else None,) if sfx else ()
             _hip.call(f'rs_inbatch_ce_fused{sfx}_fwd', U.data_ptr(), I.data_ptr(), ops.P(Hc), hsr, hss, ops.P(ids), st,
                       B, N, D, float(temperature), lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(),
                       *extra, w.data_ptr(), ops.stream())

@@ -159,9 +159,14 @@ def _gpu_worker(rank, world, port, q, lazy=False, pool_max=False, shard=False):
         assert ensure_flat(model).dp_buckets.launched == 2, ensure_flat(model).dp_buckets.launched
         ensure_flat(model).flush()
 
-        def state_vec(m):  # every float tensor of the state dict (sharded tables gathered: a collective)
-            return torch.cat([v.detach().reshape(-1).float() for k, v in sorted(m.state_dict().items())
-                              if v.is_floating_point()])
+        def state_vec(m):  # every parameter of the state dict (sharded tables gathered: a collective);
+            # not the BatchNorm running statistics (the emulation's model ran one forward per rank
+            # batch), nor the biases whose exact gradient is 0 (a training-mode BatchNorm follows:
+            # Adam on fp32 noise, as in test_row_sharded_tables_match_replicated_two_ranks_one_gpu)
+            names = {n for n, _ in m.named_parameters()}
+            sd = m.state_dict()
+            return torch.cat([v.detach().reshape(-1).float() for k, v in sorted(sd.items())
+                              if k in names and not k.endswith('feature_bn.bias') and not _bn_invariant_bias(k, sd)])
         dp_w = state_vec(model) if shard else ensure_flat(model).data.detach().clone()
         # more steps: every rank must hold bitwise-identical weights (rows touched by one rank only
         # included: the lazy tables replay them from the exchanged gradient); sharded: the
@@ -192,7 +197,8 @@ def _gpu_worker(rank, world, port, q, lazy=False, pool_max=False, shard=False):
             if lazy:
                 assert len(f.lazy) >= 3
             d = (ref_w - dp_w).abs()
-            q.put(('diverged', 0.0) if diverged else ('ok', d.max().item(), int((d > 1e-5).sum()), d.numel()))
+            tol = 1e-4 if shard else 1e-5
+            q.put(('diverged', 0.0) if diverged else ('ok', d.max().item(), int((d > tol).sum()), d.numel()))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover

@@ -22,7 +22,8 @@ def main():
     qkv = torch.randn(B * L, 3 * d, device=dev)
     if ops.qkv_bf16_ok(L, d, H, B * L):
         qkv = qkv.to(torch.bfloat16)
-    lens = torch.randint(0, L + 1, (B,), device=dev)
+    lens = (torch.full((B,), L, device=dev) if os.environ.get('FULL') == '1'
+            else torch.randint(0, L + 1, (B,), device=dev))
     seq = (torch.arange(L, device=dev)[None, :] < lens[:, None]).long()
     key_pad, _ = ops.seq_mask(seq, 0)
     key = torch.tensor([5, 1], dtype=torch.int64, device=dev)

@@ -6,7 +6,7 @@ import re
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
-names = ('gather_bwd_range_kernel', 'gather_bwd_tiny_kernel', 'gather_bwd_small_kernel', 'reduce_partials_kernel',
+names = ('gather_bwd_range_kernel', 'gather_bwd_slot_kernel', 'gather_bwd_small_kernel', 'reduce_partials_kernel',
          'gather_bwd_kernel')
 per = {n: [] for n in names}
 for r in rows:
