@@ -844,6 +844,15 @@ def main():
             continue
         zipf = 1.05 if name == 'c3_zipf' else None  # C3 with Zipf(1.05) ids
         cfg_name = 'c3' if name == 'c3_zipf' else name
+        # the previous workload's model, optimizer state, batches and graph pools are released
+        # before this one allocates (C5's 100M-row tables need ~200 GB of the 288)
+        import gc
+        gc.collect()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        if rank == 0:
+            print(f'[bench] {torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB still allocated before {key}',
+                  file=sys.stderr, flush=True)
         try:
             r = run_workload(args, cfg_name, ex_dtype, zipf, 10 if name == 'c5' else 0, rank, world, dev, 0.0,
                              peaks)

@@ -141,10 +141,19 @@ int rs_gather_fwd_lazy(const rs_feature_seg_t* segs, int nseg, int rows, float* 
                        const float* consts, float beta1, float beta2, float eps, float weight_decay,
                        void* stream);
 /* Backward: table grads by scatter-add (padding row skipped), dense grads via column
- * reductions (ws: rs_gather_ws_bytes), last-valid rows copied into a pre-zeroed src grad. */
+ * reductions (ws: rs_gather_ws_bytes), last-valid rows copied into a pre-zeroed src grad.
+ * Replaces the embedding backward of the reference's nn.Embedding lookups (GenericTower.py:153-
+ * 184, SequenceFeatureProcessor.py:57-66; torch's embedding_dense_backward). */
 int64_t rs_gather_ws_bytes(const rs_feature_seg_t* segs_host, int nseg, int rows);
 int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, const float* dout, int ldo,
                   float* ws, void* stream);
+/* Deterministic table gradients for every later rs_gather_bwd / rs_gather_ws_bytes (on != 0; also
+ * RSYS_DETERMINISTIC=1): the small tables through slot-private LDS images and the tables of up to
+ * 4 MB through the ranged LDS-image kernel, partials summed in fixed orders -- bitwise
+ * reproducible, slower than the float-atomic default at B = 4096 (torch.use_deterministic_
+ * algorithms(True) in the caller switches it on, as it does for torch's own index_add / embedding
+ * backward). Returns the previous setting. */
+int rs_set_deterministic(int on);
 
 /* h = dropout(A W^T + bias) + resid; y = LayerNorm(h)*gamma + beta; per-row mean / rstd.
  * The post-LN residual block of nn.TransformerEncoderLayer (x + dropout(sublayer(x)) -> norm,

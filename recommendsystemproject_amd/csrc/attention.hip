@@ -1019,7 +1019,13 @@ __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
   __shared__ __attribute__((aligned(16))) float L2s[LP];  // lse * log2(e)
   __shared__ __attribute__((aligned(16))) float Ds[LP];   // D_i = dO_i . O_i
   __shared__ float Kv[LP];                                // 1: key j is valid
-  __shared__ __attribute__((aligned(16))) float Tsm[4][16 * TP];
+  // per wave: the NW dS tiles of one query tile staged as bf16 (the dQ product's operand rounding,
+  // so the same bits) for the transpose, all written before one barrier and read after it -- the
+  // key tiles' chains overlap instead of meeting a barrier pair each; then the fp32 [16][TP]
+  // image of tile_rows. (79 KB in all: two workgroups per CU)
+  constexpr int TPB = 20;
+  constexpr int TB_HALFS = NW * 16 * TPB > 2 * 16 * TP ? NW * 16 * TPB : 2 * 16 * TP;
+  __shared__ __attribute__((aligned(16))) __bf16 Tbs[4][TB_HALFS];
   float(*Qs)[kRowP] = img[0];
   float(*Ks)[kRowP] = img[1];
   float(*Vs)[kRowP] = img[2];
@@ -1063,7 +1069,8 @@ __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
   const bool leven = (L & 1) == 0;
   const float scale2 = scale * kLog2e;
   const f4 z = {0.f, 0.f, 0.f, 0.f};
-  float* T = Tsm[wave];
+  float* T = reinterpret_cast<float*>(Tbs[wave]);
+  __bf16* Tb = Tbs[wave];
   QT* dbase = reinterpret_cast<QT*>(dqkv_) + (int64_t)b * L * ld + h * 16;
   __syncthreads();
 
@@ -1110,15 +1117,21 @@ __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
         ds[e] = pv * (mk[e] * pacc[e] - Dq[e]);
       }
       dv_acc[u] = mfma16(bf4(pz), gc[0], dv_acc[u]);  // (P∘Z)^T dO
-      dk_acc[u] = mfma16(bf4(ds), qc[0], dk_acc[u]);  // dS^T Q
-      // dS with the key on the k side: T[query][key] -> lane (r, q) reads row r, keys 4q..4q+3
+      const s4v dsb = bf4(ds);
+      dk_acc[u] = mfma16(dsb, qc[0], dk_acc[u]);  // dS^T Q
+      // dS with the key on the k side: Tb[u][query][key] -> lane (r, q) reads row r, keys 4q..4q+3
+      const bf4v dh = __builtin_bit_cast(bf4v, dsb);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) T[(4 * q + e) * TP + r] = ds[e];
-      __builtin_amdgcn_wave_barrier();
-      const f4 dst = ld4(&T[r * TP + 4 * q]);
-      __builtin_amdgcn_wave_barrier();
-      dq_acc[tq] = mfma16(bf4(dst), kc[u], dq_acc[tq]);  // dS K: [query 4q + e][c = r]
+      for (int e = 0; e < 4; ++e) Tb[u * 16 * TPB + (4 * q + e) * TPB + r] = dh[e];
     }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      if (u >= NW0 && (tq & 3) != wave) continue;
+      const s4v dst = *reinterpret_cast<const s4v*>(&Tb[u * 16 * TPB + r * TPB + 4 * q]);
+      dq_acc[tq] = mfma16(dst, kc[u], dq_acc[tq]);  // dS K: [query 4q + e][c = r]
+    }
+    __builtin_amdgcn_wave_barrier();
   }
   // dK / dV rows of this wave's own key tiles
 #pragma unroll

@@ -18,11 +18,16 @@
 // moments or `last`. The optimizer step replays the same steps before its own (lookup.hip
 // kAdam), so the stored state is the same bits; the forward's separate catch-up pass (read p, m,
 // v and write them back: 6 row transfers per distinct row) becomes 2 extra row reads per lookup.
+#include <atomic>
+
 #include "adam.h"
 #include "common.h"
 
 namespace rs {
 namespace {
+
+std::atomic<int> g_deterministic{0};  // rs_set_deterministic
+bool deterministic() { return g_deterministic.load(std::memory_order_relaxed) || getenv_flag("RSYS_DETERMINISTIC"); }
 
 constexpr int kMaxSeg = 24;  // segments travel by value in the kernel arguments (~2.6 KB)
 // tables up to this size get their gradient accumulated in LDS first (privatised per workgroup,
@@ -535,7 +540,8 @@ __global__ __launch_bounds__(256) void gather_bwd_small_kernel(SegLaunch a) {
   }
 }
 
-// Small tables (<= 48 KB: C2 / C3's gender, age, occupation, zip, genre, release-year tables,
+// Small tables in deterministic mode (rs_set_deterministic; <= 16 KB, or up to 48 KB when the
+// ranged kernel cannot take them: C2 / C3's gender, age, occupation, genre, release-year tables,
 // and the per-token genre bags of the history: 614,400 bag ids per step into a 30 x 8 table):
 // slot-private LDS images, no atomics, bitwise reproducible. A workgroup owns a contiguous run of
 // lookup rows; its lanes form `slots` groups of D (lane = slot * D + column) and slot k takes
@@ -546,7 +552,8 @@ __global__ __launch_bounds__(256) void gather_bwd_small_kernel(SegLaunch a) {
 // operations per column lane -- the earlier kernels compared every id with every table row
 // (register accumulators: V compare-selects per id and column, 46 us at C2's genre table) or
 // used LDS / global float atomics (33 us, order-dependent bits).
-constexpr int kSlotRowsInFlight = 4;
+constexpr int kSlotRows = 8;  // rows per slot per batch: their dout columns and ids load together
+constexpr int kSlotBag = 8;   // bags up to this long load all their ids at once
 
 __global__ __launch_bounds__(256) void gather_bwd_slot_kernel(SegLaunch a) {
   extern __shared__ __attribute__((aligned(16))) float img[];  // [slots][V][D]
@@ -568,21 +575,38 @@ __global__ __launch_bounds__(256) void gather_bwd_slot_kernel(SegLaunch a) {
     const float sc = pool && sg.pool_mode == RS_POOL_MEAN ? 1.f / (float)bag : 1.f;
     const int64_t pad = sg.pad_idx, V = sg.vocab;
     float* my = img + sl * E + c;
-    for (int r = r0 + sl; r < r1; r += kSlotRowsInFlight * nsl) {
-      float g[kSlotRowsInFlight];
-      int64_t row[kSlotRowsInFlight];
+    for (int r = r0 + sl; r < r1; r += kSlotRows * nsl) {
+      float g[kSlotRows];
+      int64_t row[kSlotRows];
 #pragma unroll
-      for (int u = 0; u < kSlotRowsInFlight; ++u) {
+      for (int u = 0; u < kSlotRows; ++u) {
         row[u] = r + u * nsl;
         g[u] = row[u] < r1 ? a.dout[row[u] * a.ldo + sg.out_col + c] * sc : 0.f;
       }
-      for (int l = 0; l < bag; ++l) {
-        int64_t id[kSlotRowsInFlight];
+      if (bag <= kSlotBag) {
+        // every id of the batch in flight with the dout columns: one round trip per batch
+        int id[kSlotRows][kSlotBag];  // table row, or -1 (no contribution)
 #pragma unroll
-        for (int u = 0; u < kSlotRowsInFlight; ++u) id[u] = row[u] < r1 ? sg.idx[row[u] * sg.idx_stride + l] : -1;
+        for (int u = 0; u < kSlotRows; ++u)
 #pragma unroll
-        for (int u = 0; u < kSlotRowsInFlight; ++u)
-          if (id[u] >= 0 && id[u] < V && id[u] != pad) my[id[u] * D] += g[u];
+          for (int l = 0; l < kSlotBag; ++l) {
+            const int64_t x = (row[u] < r1 && l < bag) ? sg.idx[row[u] * sg.idx_stride + l] : -1;
+            id[u][l] = (x >= 0 && x < V && x != pad) ? (int)x : -1;
+          }
+#pragma unroll
+        for (int u = 0; u < kSlotRows; ++u)
+#pragma unroll
+          for (int l = 0; l < kSlotBag; ++l)
+            if (id[u][l] >= 0) my[id[u][l] * D] += g[u];
+      } else {
+        for (int l = 0; l < bag; ++l) {
+          int64_t id[kSlotRows];
+#pragma unroll
+          for (int u = 0; u < kSlotRows; ++u) id[u] = row[u] < r1 ? sg.idx[row[u] * sg.idx_stride + l] : -1;
+#pragma unroll
+          for (int u = 0; u < kSlotRows; ++u)
+            if (id[u] >= 0 && id[u] < V && id[u] != pad) my[id[u] * D] += g[u];
+        }
       }
     }
   }
@@ -836,9 +860,10 @@ __global__ __launch_bounds__(1024) void dense_bwd_kernel(SegLaunch a) {
 // mean bags of a table of 48 KB - 4 MB (smaller ones: the slot kernel), D in {16, 32, 64, 128,
 // 256} (D/4 lanes per lookup divide a wave into <= 16 groups); ranges of 64 KB; chunks of >= 2 x
 // vocab lookups (the [vocab, dim] partial of a chunk costs no more than its dout rows), a multiple
-// of 8 (XCD mapping), at most 1024 / ranges. Round 4: also the tables hit < 8 times per row (C2's
-// 6,060-row user and 3,500-row item tables at 4,096 lookups), which took the atomic scatter: every
-// table of this size now gets a bitwise-reproducible gradient.
+// of 8 (XCD mapping), at most 1024 / ranges. Deterministic mode (round 4) also takes the tables hit
+// < 8 times per row (C2's 6,060-row user and 3,500-row item tables at 4,096 lookups) and the
+// small ones the slot kernel leaves to it: measured at C2 (tools/gather_bwd_time.py) the user
+// tower's table gradients 25 -> 53-65 us, so the atomic scatter stays the default for them.
 struct RangePlan { int rows, ranges, chunks; };
 
 RangePlan range_plan(const rs_feature_seg_t& g, int rows, bool vec) {
@@ -847,8 +872,11 @@ RangePlan range_plan(const rs_feature_seg_t& g, int rows, bool vec) {
   const bool dim_ok = g.dim >= 16 && g.dim <= 256 && 256 % g.dim == 0;
   const int64_t tbytes = g.vocab * g.dim * 4;
   const int64_t n = (int64_t)rows * (g.kind == RS_SEG_POOL ? g.bag : 1);
-  if (!table_kind || !vec || !dim_ok || tbytes <= kSmallTableBytes || tbytes > (4 << 20) || n == 0 ||
-      getenv_flag("RSYS_NO_RANGE_GRAD"))
+  // default: tables hit >= 8 times per row on average (the atomic scatter is faster below that);
+  // deterministic mode: every table of 4 MB or less that the kernel takes, small ones included
+  const bool det = deterministic();
+  if (!table_kind || !vec || !dim_ok || (tbytes <= kSmallTableBytes && !det) || tbytes > (4 << 20) || n == 0 ||
+      (n < 8 * g.vocab && !det) || getenv_flag("RSYS_NO_RANGE_GRAD"))
     return r;
   int R = kRangeBytes / (g.dim * 4);
   const int nr = (int)((g.vocab + R - 1) / R);
@@ -885,15 +913,24 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.vec[s] = vec;
     a.chunks[s] = C;
     const bool table_kind = g.kind == RS_SEG_SPARSE || g.kind == RS_SEG_POOL;
-    // small tables: the slot-image kernel (deterministic); a max-pooled one (its arg-max needs the
-    // table rows) keeps the small-table kernel's atomics, as does RSYS_SLOT_GRAD=0 (A/B)
-    a.tiny[s] = bwd && table_kind && !(g.kind == RS_SEG_POOL && g.pool_mode == RS_POOL_MAX) &&
-               g.vocab * g.dim * 4 <= kSmallTableBytes && g.dim <= 64 && !getenv_flag0("RSYS_SLOT_GRAD");
-    a.small[s] = bwd && table_kind && g.vocab * g.dim * 4 <= kSmallTableBytes && !a.tiny[s];
+    // small tables: the float-atomic small-table kernel by default; deterministic mode
+    // (rs_set_deterministic): the slot-image kernel where >= 4 slots fit (images <= 16 KB), the
+    // ranged kernel for the larger ones it takes (D >= 16, float4 rows: C2 / C3's zip table),
+    // else slots anyway. A max-pooled table (its arg-max needs the table rows) keeps the atomics.
+    const bool det = bwd && deterministic();
+    const int64_t tb = g.vocab * g.dim * 4;
+    const bool rangeable = vec && g.dim >= 16 && g.dim <= 256 && 256 % g.dim == 0;
+    a.tiny[s] = det && table_kind && !(g.kind == RS_SEG_POOL && g.pool_mode == RS_POOL_MAX) &&
+               tb <= kSmallTableBytes && g.dim <= 64 && (tb <= 16 * 1024 || !rangeable);
+    a.small[s] = bwd && table_kind && tb <= kSmallTableBytes && !a.tiny[s] && !(det && rangeable &&
+               !(g.kind == RS_SEG_POOL && g.pool_mode == RS_POOL_MAX));
     // Split long sum/mean bags over S row groups while the launch is short of ~8 waves per SIMD
     // and every group keeps >= 8 positions (C3: B = 4096, L = 50, D = 128 -> S = 4).
     int S = 1;
-    const bool nt = !bwd && vec && table_kind && g.vocab * g.dim * 4 >= kNtTableBytes && !getenv_flag("RSYS_GATHER_NO_NT");
+    // opt-in (RSYS_GATHER_NT=1): faster from HBM in isolation (tools/gather_sweep.hip), slower in
+    // the step (C3 fp32 0.037 -> 0.043 ms): there the catch-up has just brought the rows on chip,
+    // and rows not kept in the Infinity Cache cost the optimizer's later read of them
+    const bool nt = !bwd && vec && table_kind && g.vocab * g.dim * 4 >= kNtTableBytes && getenv_flag("RSYS_GATHER_NT");
     if (g.kind == RS_SEG_POOL && g.pool_mode != RS_POOL_MAX && !a.small[s] && !nt) {
       while (2 * S * C <= 256 && (g.bag + 2 * S - 1) / (2 * S) >= 8 &&
              (int64_t)rows * C * S < 8192 * 64)
@@ -917,7 +954,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.rranges[s] = 0;
     a.rchunks[s] = 0;
     a.rrows[s] = 0;
-    if (bwd && !a.small[s]) {
+    if (bwd && !a.small[s] && !a.tiny[s]) {
       const RangePlan rp = range_plan(g, rows, vec);
       a.rrows[s] = rp.rows;
       a.rranges[s] = rp.ranges;
@@ -952,9 +989,11 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
       const int fit = (int)((64 * 1024) / (E * 4));
       nsl = nsl < fit ? nsl : fit;
       nsl = nsl < 1 ? 1 : nsl;
-      int64_t nb = cdiv(rows, nsl * kSlotRowsInFlight);
-      const int64_t cap = std::max<int64_t>(8, (4ll << 20) / (E * 4));
-      nb = std::min<int64_t>(std::min<int64_t>(nb, 256), cap);
+      // one batch of kSlotRows rows per slot where the grid allows (<= 2048 workgroups, <= 8 MB
+      // of partials): the kernel is a single round trip of loads per workgroup
+      int64_t nb = cdiv(rows, nsl * kSlotRows);
+      const int64_t cap = std::max<int64_t>(8, (8ll << 20) / (E * 4));
+      nb = std::min<int64_t>(std::min<int64_t>(nb, 2048), cap);
       a.slots[s] = (int16_t)nsl;
       a.tblocks[s] = (int16_t)(nb < 1 ? 1 : nb);
       ob += a.tblocks[s];
@@ -1065,6 +1104,10 @@ extern "C" int rs_gather_fwd_lazy(const rs_feature_seg_t* segs, int nseg, int ro
 
 // rs_gather_bwd's workspace: the small and ranged tables' partials. Planned with float4-aligned
 // dout rows (the condition under which a segment is ranged at all): an upper bound.
+extern "C" int rs_set_deterministic(int on) {
+  return g_deterministic.exchange(on ? 1 : 0);
+}
+
 extern "C" int64_t rs_gather_ws_bytes(const rs_feature_seg_t* segs_host, int nseg, int rows) {
   if (!segs_host || nseg < 1 || nseg > kMaxSeg || rows <= 0) return 0;
   int ldo = 4;

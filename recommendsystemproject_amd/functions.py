@@ -301,10 +301,13 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key, params=()):
             ops.dropout_bwd(dx, p, key, 0)
     lin = proc.feature_projection[0]
     # dx is final here (the dropout backward above ran in place before this point)
-    ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
+    with _WgradBranch(dx, cat):
+        ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
     dcat = ops.linear_bwd_input(dx, lin.weight)
     for s, t in zip(segs, tables):
         s.grad = grad_of(t).data_ptr()
+    # the encoder's weight gradients (side stream) are in before the op reports its gradients
+    _WgradBranch.join()
     _grad_tables(segs, calls, dcat, tables, B * L, params)
 
 
@@ -338,6 +341,60 @@ class SeqFeaturesFn(torch.autograd.Function):
 
 
 # ================================================================================ encoder layer
+class _WgradBranch:
+    """The encoder backward's weight gradients on a side stream (round 4): a layer's dW / db
+    kernels only read activations and the layer's output gradient, and nothing on the input-
+    gradient chain reads what they write (the flat gradient), so they run beside the chain
+    instead of in it -- forked from the current stream once their inputs are queued, joined back
+    before the op reports its gradients (seq_input_bwd). The fork / join is captured into the
+    step's hipGraph as parallel branches. RSYS_WGRAD_STREAM=0 (and RSYS_TOWER_STREAMS=0, the
+    bench's serial instrumented pass) keeps them on the current stream."""
+
+    _streams = {}
+
+    def __init__(self, *tensors):
+        self.on = (os.environ.get('RSYS_WGRAD_STREAM', '1') != '0' and
+                   os.environ.get('RSYS_TOWER_STREAMS', '1') != '0' and
+                   all(t.is_cuda for t in tensors) and not any(_is_fake(t) for t in tensors))
+        self.tensors = tensors
+
+    def __enter__(self):
+        if not self.on:
+            return self
+        main = torch.cuda.current_stream()
+        side = self._streams.get(main.device)
+        if side is None:
+            side = self._streams[main.device] = torch.cuda.Stream(device=main.device)
+        side.wait_stream(main)
+        for t in self.tensors:  # made on the main stream, read on the side one
+            t.record_stream(side)
+        _WgradBranch._pending[main.device] = side
+        self._ctx = torch.cuda.stream(side)
+        self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            self._ctx.__exit__(*exc)
+
+    _pending = {}
+
+    @classmethod
+    def join(cls):
+        """The current stream waits for the weight gradients forked so far."""
+        if not cls._pending:
+            return
+        main = torch.cuda.current_stream()
+        side = cls._pending.pop(main.device, None)
+        if side is not None:
+            main.wait_stream(side)
+
+
+def _is_fake(t):
+    from torch._subclasses.fake_tensor import FakeTensor
+    return isinstance(t, FakeTensor)
+
+
 def _ffn_fwd(lyr, x1, p, key, site):
     """x2 = norm2(x1 + dropout2(linear2(dropout(relu(linear1(x1)))))) on any row count."""
     if ops.ffn_supported(x1, lyr.linear1.weight):
@@ -411,8 +468,10 @@ def _post_attn_bwd(lyr, saved, dx2, p, key, site):
             m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias), h1, lyr.norm1.weight, m1, r1,
             g(lyr.norm1.weight), g(lyr.norm1.bias), p, key, site + 1, site + 3)
         ln1_done = True
-        ops.ffn_wgrad_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, f1[1], dff, p,
-                           g(lyr.linear1.weight), g(lyr.linear1.bias), g(lyr.linear2.weight), g(lyr.linear2.bias))
+        with _WgradBranch(x1, f1[1], dff):
+            ops.ffn_wgrad_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, f1[1], dff, p,
+                               g(lyr.linear1.weight), g(lyr.linear1.bias), g(lyr.linear2.weight),
+                               g(lyr.linear2.bias))
     else:
         dff = torch.empty_like(dx2) if p > 0 else None
         dh2 = ops.layernorm_bwd(h2, dx2, lyr.norm2.weight, m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias),
@@ -431,7 +490,12 @@ def _post_attn_bwd(lyr, saved, dx2, p, key, site):
                                 da=dsa, p=p, key=key, site=site + 1)
     if dsa is None:  # p == 0: dsa IS dh1 (read here before the in-proj backward accumulates into it)
         dsa = dh1
-    ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
+        # the in-proj backward then accumulates into dh1 on the main stream: this weight gradient
+        # reads it first, on the main stream too
+        ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
+    else:
+        with _WgradBranch(dsa, att):
+            ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
     datt = ops.linear_bwd_input(dsa, sa_mod.out_proj.weight)
     return dh1, datt
 
@@ -440,10 +504,11 @@ def _in_proj_bwd(lyr, x, dqkv, dx=None):
     """in_proj weight gradient and dx (+)= dqkv W_in."""
     g = grad_of
     sa_mod = lyr.self_attn
-    if dqkv.dtype == torch.bfloat16:  # bf16 dqkv (RS_ATTN_QKV_BF16): bf16-MFMA weight gradient
-        ops.wgrad_bf16(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
-    else:
-        ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
+    with _WgradBranch(dqkv, x):
+        if dqkv.dtype == torch.bfloat16:  # bf16 dqkv (RS_ATTN_QKV_BF16): bf16-MFMA weight gradient
+            ops.wgrad_bf16(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
+        else:
+            ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
     if dx is None:
         return ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight)
     return ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight, out=dx, beta=1.0)  # dx = dh1 + dqkv Win

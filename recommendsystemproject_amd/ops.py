@@ -211,7 +211,21 @@ def gather_fwd(segs, rows, out, err_flag=None, lazy=None):
     return out
 
 
+_DETERMINISTIC = [None]
+
+
+def sync_deterministic():
+    """Mirror torch.are_deterministic_algorithms_enabled() into the library (rs_set_deterministic):
+    deterministic table gradients (slot-image / ranged kernels) instead of the float-atomic
+    scatter. RSYS_DETERMINISTIC=1 turns it on regardless."""
+    on = bool(torch.are_deterministic_algorithms_enabled())
+    if on != _DETERMINISTIC[0]:
+        _hip.lib().rs_set_deterministic(int(on))
+        _DETERMINISTIC[0] = on
+
+
 def gather_bwd(segs, rows, dout):
+    sync_deterministic()
     arr = segments_array(segs)
     # hot mid-size tables (C2's 3,500-row history table) reduce per-chunk partials from ws
     w = ws(_hip.lib().rs_gather_ws_bytes(arr, len(segs), rows), dout.device)

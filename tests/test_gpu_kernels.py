@@ -209,10 +209,11 @@ def test_gather_backward_ranged_hot_tables(monkeypatch, V, D, rows, Lb, mode):
     """Mid-size tables (48 KB - 4 MB, D in 16..256: C2's 3,500 x 32
     history table at 204,800 token lookups) take the ranged LDS path (gather.hip
     gather_bwd_range_kernel: row-owner waves, chunk partials reduced in order; bitwise
-    reproducible); tables of <= 48 KB the slot-image kernel (gather_bwd_slot_kernel: slot-private
-    LDS images, no atomics; bitwise reproducible); RSYS_SLOT_GRAD=0 the small-table kernel and
-    RSYS_NO_RANGE_GRAD=1 the atomic scatter: against the embedding backward, padding row skipped,
-    out-of-range ids ignored, grad accumulated (+=)."""
+    reproducible) when hit >= 8 times per row; smaller ones the float-atomic small-table kernel.
+    Deterministic mode (rs_set_deterministic, torch.use_deterministic_algorithms): the slot-image
+    kernel (slot-private LDS images, no atomics) or the ranged kernel for every table of <= 4 MB,
+    bitwise reproducible. RSYS_NO_RANGE_GRAD=1: the atomic scatter. All against the embedding
+    backward, padding row skipped, out-of-range ids ignored, grad accumulated (+=)."""
     t = rnd(V, D, seed=31).requires_grad_(True)
     shape = (rows,) if mode is None else (rows, Lb)
     ids = torch.randint(0, V, shape, device=DEV)
@@ -230,25 +231,33 @@ def test_gather_backward_ranged_hot_tables(monkeypatch, V, D, rows, Lb, mode):
         seg.update(pool_mode=_hip.RS_POOL[mode], bag=Lb)
     arr = ops.segments_array([_seg(**seg)])
     n = rows * Lb
-    ranged = 48 * 1024 < V * D * 4 <= 4 << 20 and D >= 16
-    slot = V * D * 4 <= 48 * 1024 and D <= 64  # the slot-image kernel
-    assert (_hip.lib().rs_gather_ws_bytes(arr, 1, rows) > 0) == (ranged or slot)  # partials in ws
+    L = _hip.lib()
+    ranged = 48 * 1024 < V * D * 4 <= 4 << 20 and D >= 16 and n >= 8 * V
+    assert (L.rs_gather_ws_bytes(arr, 1, rows) > 0) == ranged  # partials in ws
+    det_ok = V * D * 4 <= 4 << 20 and (D >= 16 or V * D * 4 <= 48 * 1024)  # slot or ranged
     grads = []
-    # the planned path twice, the small-table kernel (RSYS_SLOT_GRAD=0), the atomic scatter
-    for off, sk in (('', ''), ('', ''), ('', '0'), ('1', '')):
+    # the planned path, deterministic mode twice, the atomic scatter
+    for off, det in (('', 0), ('', 1), ('', 1), ('1', 0)):
         monkeypatch.setenv('RSYS_NO_RANGE_GRAD', off)
-        monkeypatch.setenv('RSYS_SLOT_GRAD', sk)
-        g = torch.full((V, D), 0.25, device=DEV)
-        ops.gather_bwd([_seg(**seg, grad=g.data_ptr())], rows, dout)
+        torch.use_deterministic_algorithms(bool(det), warn_only=True)
+        try:
+            ops.sync_deterministic()
+            if det:
+                assert (L.rs_gather_ws_bytes(arr, 1, rows) > 0) == det_ok
+            g = torch.full((V, D), 0.25, device=DEV)
+            ops.gather_bwd([_seg(**seg, grad=g.data_ptr())], rows, dout)
+            torch.cuda.synchronize()
+        finally:
+            torch.use_deterministic_algorithms(False)
+            ops.sync_deterministic()
         grads.append(g)
     monkeypatch.setenv('RSYS_NO_RANGE_GRAD', '')
-    monkeypatch.setenv('RSYS_SLOT_GRAD', '')
     scale = max(1.0, t.grad.abs().max().item())
     for gr in grads:
         assert (gr - 0.25 - t.grad).abs().max().item() <= 2e-5 * scale
         assert (gr[0] == 0.25).all()
-    if ranged or slot:  # ranged and slot-image gradients are bitwise reproducible
-        assert torch.equal(grads[0], grads[1])
+    if det_ok:  # slot-image and ranged gradients are bitwise reproducible
+        assert torch.equal(grads[1], grads[2])
     # out-of-range / negative ids contribute nothing and do not fault
     bad = ids.clone()
     bad.view(-1)[5] = V + 100

@@ -41,9 +41,9 @@ def timeit(segs, n=50):
     return e0.elapsed_time(e1) / n * 1e3
 
 
-KEYS = ('RSYS_NO_RANGE_GRAD', 'RSYS_SLOT_GRAD')
+KEYS = ('RSYS_NO_RANGE_GRAD', 'RSYS_DETERMINISTIC')
 for segs, label in (([seg_m], 'hist_movie_ids'), ([seg_g], 'hist_genre_ids'), ([seg_m, seg_g], 'both')):
-    for name, env in [('default', {}), ('small', {'RSYS_SLOT_GRAD': '0'}), ('atomic', {'RSYS_NO_RANGE_GRAD': '1'})]:
+    for name, env in [('default', {}), ('determ', {'RSYS_DETERMINISTIC': '1'}), ('atomic', {'RSYS_NO_RANGE_GRAD': '1'})]:
         for k in KEYS:
             os.environ.pop(k, None)
         os.environ.update(env)
