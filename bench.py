@@ -517,7 +517,13 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
             neg_ids.copy_(neg_sets[i], non_blocking=True)
 
     # eager warm-up (also allocates Adam state), then capture
-    for _ in range(max(2, min(args.warmup, 3))):
+    # eager warm-up; a PMC bracket step comes after every resident batch has been stepped once, so
+    # its large-table rows are (batches - 1) steps stale like the timed steps' (the catch-up's
+    # replay, its reads of the moments, are then those of the timed run)
+    n_warm = max(2, min(args.warmup, 3))
+    if args.pmc_bracket:
+        n_warm = max(n_warm, args.batches)
+    for _ in range(n_warm):
         next_batch()
         fwd_bwd()
         allreduce()

@@ -347,13 +347,15 @@ class _WgradBranch:
     gradient chain reads what they write (the flat gradient), so they run beside the chain
     instead of in it -- forked from the current stream once their inputs are queued, joined back
     before the op reports its gradients (seq_input_bwd). The fork / join is captured into the
-    step's hipGraph as parallel branches. RSYS_WGRAD_STREAM=0 (and RSYS_TOWER_STREAMS=0, the
-    bench's serial instrumented pass) keeps them on the current stream."""
+    step's hipGraph as parallel branches. Opt-in (RSYS_WGRAD_STREAM=1; never with
+    RSYS_TOWER_STREAMS=0, the bench's serial instrumented pass): measured at C2 (bf16, replayed
+    graphs) 1.425 -> 1.46 ms per step -- the branches' cross-queue waits cost more than the
+    overlap gains, the weight-gradient kernels being full-chip launches themselves."""
 
     _streams = {}
 
     def __init__(self, *tensors):
-        self.on = (os.environ.get('RSYS_WGRAD_STREAM', '1') != '0' and
+        self.on = (os.environ.get('RSYS_WGRAD_STREAM', '0') == '1' and
                    os.environ.get('RSYS_TOWER_STREAMS', '1') != '0' and
                    all(t.is_cuda for t in tensors) and not any(_is_fake(t) for t in tensors))
         self.tensors = tensors
