@@ -573,14 +573,23 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
                 allreduce()
                 opt_step()
             torch.cuda.current_stream().wait_stream(s)
-            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             # thread_local: the RCCL process group's watchdog thread polls its work events while
-            # this thread captures; a global-mode capture would be invalidated by those queries
-            with torch.cuda.graph(g1, capture_error_mode='thread_local'):
-                loss_static = fwd_bwd()
-                allreduce()
-            with torch.cuda.graph(g2, capture_error_mode='thread_local'):
-                opt_step()
+            # this thread captures; a global-mode capture would be invalidated by those queries.
+            # One graph for the whole step (RSYS_BENCH_GRAPHS=2: forward+backward and the optimizer
+            # as two, round 3's split, which left ~10 us between them)
+            if os.environ.get('RSYS_BENCH_GRAPHS', '1') == '2':
+                g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g1, capture_error_mode='thread_local'):
+                    loss_static = fwd_bwd()
+                    allreduce()
+                with torch.cuda.graph(g2, capture_error_mode='thread_local'):
+                    opt_step()
+            else:
+                g1, g2 = torch.cuda.CUDAGraph(), None
+                with torch.cuda.graph(g1, capture_error_mode='thread_local'):
+                    loss_static = fwd_bwd()
+                    allreduce()
+                    opt_step()
             graphs = (g1, g2, loss_static)
         except Exception as e:  # eager fallback keeps the same kernels
             print(f'[bench] graph capture failed ({e!r}); running eagerly', file=sys.stderr)
@@ -590,7 +599,8 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
         next_batch()
         if graphs is not None:
             graphs[0].replay()
-            graphs[1].replay()
+            if graphs[1] is not None:
+                graphs[1].replay()
             return graphs[2]
         loss = fwd_bwd()
         allreduce()

@@ -193,12 +193,41 @@ def _grad_tables(segs, calls, dout, tables, rows, params=()):
         else:
             rest.append(s)
     if rest:
-        ops.gather_bwd(rest, rows, dout)
+        _gather_bwd_split(rest, rows, dout)
     _dp.note_writer(params, written=True)
     for t, c, ptr in big:
         if ptr is None:  # max-pooled: its per-lookup gradient rows are already the call's dseg
             continue
         t.segsum(c, ptr, dout.stride(0))
+
+
+_HEAVY_LOOKUPS = 65536
+
+
+def _gather_bwd_split(segs, rows, dout):
+    """rs_gather_bwd of a gather's ordinary segments. Token-sized segments (>= 64K lookups: C2's
+    per-token history tables, 204,800 ids into 3,500 x 32 and 614,400 tag ids into 30 x 8) each
+    take a latency-bound kernel that leaves most of the chip idle, and one launch runs its kernels
+    back to back: the heavy segments after the first go to side streams, forked from the current
+    one and joined back before the caller reports its gradients. RSYS_GRAD_STREAMS=0 (and the
+    bench's serial instrumented pass, RSYS_TOWER_STREAMS=0) keeps one launch."""
+    heavy = [sg for sg in segs if sg.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL) and
+             rows * (sg.bag if sg.kind == _hip.RS_SEG_POOL else 1) >= _HEAVY_LOOKUPS]
+    if (len(heavy) < 2 or os.environ.get('RSYS_GRAD_STREAMS', '1') == '0' or
+            os.environ.get('RSYS_TOWER_STREAMS', '1') == '0' or not dout.is_cuda):
+        ops.gather_bwd(segs, rows, dout)
+        return
+    main = torch.cuda.current_stream()
+    side = [_call_stream(main, 8 + k) for k in range(len(heavy) - 1)]
+    moved = {id(sg) for sg in heavy[1:]}
+    for st, sg in zip(side, heavy[1:]):
+        st.wait_stream(main)
+        dout.record_stream(st)
+        with torch.cuda.stream(st):
+            ops.gather_bwd([sg], rows, dout)
+    ops.gather_bwd([sg for sg in segs if id(sg) not in moved], rows, dout)
+    for st in side:
+        main.wait_stream(st)
 
 
 def _max_as_single(c, s, dout):
