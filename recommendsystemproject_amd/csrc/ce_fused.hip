@@ -69,6 +69,8 @@ struct CeArgs {
   float* part_d;        // bwd: [NS][B][D]
   float* S;             // fp32 mode: [B][ldS] raw U I^T, written by the forward, read by the backward
   int ldS;
+  const __bf16* strb;   // bf16 backward: the streamed rows pre-rounded to bf16 (the same bits the
+                        // staging rounds to), half the bytes per tile: twice the tiles per batch
 };
 
 __device__ __forceinline__ bf16x8 cvt8(const floatx4& a, const floatx4& b) {
@@ -96,8 +98,10 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* lo, const __bf16* hi) {
 // fp32 tiles take twice the LDS: the forward stages 2 tiles per batch, the backward 1 (the LDS
 // image holds 2 x 2 tiles, 68 KB: two workgroups per CU).
 constexpr int kBT = 4;
-template <int MODE, bool F32>
-constexpr int batch_tiles() { return F32 ? (MODE == 0 ? kBT / 2 : kBT / 4) : (MODE == 0 ? kBT : kBT / 2); }
+template <int MODE, bool F32, bool SB = false>
+constexpr int batch_tiles() {
+  return F32 ? (MODE == 0 ? kBT / 2 : kBT / 4) : ((MODE == 0 || SB) ? kBT : kBT / 2);
+}
 
 // v_exp_f32 directly: exp2f() adds a denormal-range fix-up (compare, select, ldexp) per call
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -114,8 +118,9 @@ struct CeLds {
   float slse[2][NT * kTile];
 };
 
-template <int D, int MODE, bool F32>
+template <int D, int MODE, bool F32, bool SB = false>
 __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, CeLds<D, F32>& L) {
+  static_assert(!SB || (!F32 && MODE != 0), "bf16-streamed tiles: the bf16 backward");
   using E = typename CeLds<D, F32>::E;
   constexpr int KS = D / 16;          // 32x32x16 k-steps over the embedding (bf16)
   constexpr int PT = CeLds<D, F32>::PT;
@@ -173,11 +178,13 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
   // batch staging: kBT tiles of 32 rows x D fp32 -> bf16 LDS, float4 per slot
   constexpr int NTHR = 64 * kWaves;
   constexpr int SL = kTile * D / 4 / NTHR;  // float4 slots per thread per tile
-  constexpr int BT = batch_tiles<MODE, F32>();  // tiles per batch
+  constexpr int SLB = kTile * D / 8 / NTHR;  // bf16x8 slots per thread per tile (SB)
+  constexpr int BT = batch_tiles<MODE, F32, SB>();  // tiles per batch
   constexpr int BR = BT * kTile;            // rows per batch
   static_assert(BR <= NTHR, "one id / lse per thread and batch row");
   struct Stage {
-    floatx4 v[BT][SL];
+    floatx4 v[SB ? 1 : BT][SB ? 1 : SL];
+    bf16x8 vb[SB ? BT : 1][SB ? SLB : 1];
     int64_t id;
     float l;
   };
@@ -186,22 +193,44 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
   // a guarded load would sit in its own branch, and the waitcnt pass then drains vmcnt(0) at the
   // join -- waiting for the prefetch it was meant to overlap
   auto load_batch = [&](int t0) {
+    if constexpr (SB) {
 #pragma unroll
-    for (int k = 0; k < BT; ++k)
+      for (int k = 0; k < BT; ++k)
 #pragma unroll
-      for (int i = 0; i < SL; ++i) {
-        const int slot = tid + NTHR * i;
-        const int row = slot / (D / 4), col = (slot % (D / 4)) * 4;
-        const int t = min(t0 + k * kTile + row, B - 1);
-        R.v[k][i] = *reinterpret_cast<const floatx4*>(a.str + (int64_t)t * D + col);
-      }
+        for (int i = 0; i < SLB; ++i) {
+          const int slot = tid + NTHR * i;
+          const int row = slot / (D / 8), col = (slot % (D / 8)) * 8;
+          const int t = min(t0 + k * kTile + row, B - 1);
+          R.vb[k][i] = *reinterpret_cast<const bf16x8*>(a.strb + (int64_t)t * D + col);
+        }
+    } else {
+#pragma unroll
+      for (int k = 0; k < BT; ++k)
+#pragma unroll
+        for (int i = 0; i < SL; ++i) {
+          const int slot = tid + NTHR * i;
+          const int row = slot / (D / 4), col = (slot % (D / 4)) * 4;
+          const int t = min(t0 + k * kTile + row, B - 1);
+          R.v[k][i] = *reinterpret_cast<const floatx4*>(a.str + (int64_t)t * D + col);
+        }
+    }
     const int t = min(t0 + (tid & (BR - 1)), B - 1);
     R.id = a.ids ? a.ids[(int64_t)t * a.id_stride] : 0;
     if constexpr (MODE == 2) R.l = a.lse[t] * kLog2e;  // staged in the log2 domain
   };
   auto store_batch = [&](int hf) {
+    if constexpr (SB) {
 #pragma unroll
-    for (int k = 0; k < BT; ++k)
+      for (int k = 0; k < BT; ++k)
+#pragma unroll
+        for (int i = 0; i < SLB; ++i) {
+          const int slot = tid + NTHR * i;
+          const int row = k * kTile + slot / (D / 8), col = (slot % (D / 8)) * 8;
+          *reinterpret_cast<bf16x8*>(&L.Ts[hf][row * PT + col]) = R.vb[k][i];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < (SB ? 0 : BT); ++k)
 #pragma unroll
       for (int i = 0; i < SL; ++i) {
         const int slot = tid + NTHR * i;
@@ -457,11 +486,25 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(2))
 
 // dU and dI in one launch (blockIdx.z): the two halves are independent given lse, and 1,024
 // workgroups hide each other's tile latencies better than two back-to-back 512-workgroup grids
-template <int D, bool F32>
+template <int D, bool F32, bool SB = false>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(2))) void ce_bwd_pair_kernel(CeArgs aU, CeArgs aI) {
   __shared__ __attribute__((aligned(16))) CeLds<D, F32> lds;  // one image shared by both halves
-  if (blockIdx.z == 0) ce_tile_body<D, 1, F32>(aU, blockIdx.y, lds);
-  else ce_tile_body<D, 2, F32>(aI, blockIdx.y, lds);
+  if (blockIdx.z == 0) ce_tile_body<D, 1, F32, SB>(aU, blockIdx.y, lds);
+  else ce_tile_body<D, 2, F32, SB>(aI, blockIdx.y, lds);
+}
+
+// the bf16 backward's streamed operands: U and I rounded to bf16 once (n elements each)
+__global__ __launch_bounds__(256) void ce_round_bf16_kernel(const float* __restrict__ U, const float* __restrict__ I,
+                                                            int64_t n, __bf16* __restrict__ Ub, __bf16* __restrict__ Ib) {
+  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4;
+  if (i >= 2 * n) return;
+  const bool second = i >= n;
+  const float* src = second ? I + (i - n) : U + i;
+  __bf16* dst = second ? Ib + (i - n) : Ub + i;
+  const floatx4 v = *reinterpret_cast<const floatx4*>(src);
+  bf16x4 h;
+  h[0] = (__bf16)v[0]; h[1] = (__bf16)v[1]; h[2] = (__bf16)v[2]; h[3] = (__bf16)v[3];
+  *reinterpret_cast<bf16x4*>(dst) = h;
 }
 
 // per user row: merge the split statistics with the hard-negative logits -> lse, row loss
@@ -584,7 +627,8 @@ extern "C" int64_t rs_inbatch_ce_s_ld(int B) { return (int64_t)cdiv(B, kTile) * 
 
 extern "C" int64_t rs_inbatch_ce_fused_ws_bytes(int B, int D) {
   const int64_t fwd = (int64_t)splits_for(B, false) * B * 2 + B;
-  const int64_t bwd = (int64_t)2 * splits_for(B, true) * B * D;  // dU and dI partials side by side
+  // dU and dI partials side by side, then the bf16 copies of U and I (B * D floats hold both)
+  const int64_t bwd = (int64_t)2 * splits_for(B, true) * B * D + (int64_t)B * D + 8;
   return (fwd > bwd ? fwd : bwd) * (int64_t)sizeof(float);
 }
 
@@ -643,6 +687,31 @@ int ce_fused_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_
   aI.own = I; aI.str = U;
   aI.part_d = ws + (int64_t)NSr * n;
   const dim3 grid(cdiv(B, kOwnW * kWaves), NSr, 2);
+  if constexpr (!F32) {
+    // bf16: U and I rounded once (one small launch), so every workgroup streams half the bytes
+    // and stages twice the tiles per batch with the same registers (RSYS_CE_STREAM_F32=1: the
+    // fp32 rows, rounded as staged)
+    if (!getenv_flag("RSYS_CE_STREAM_F32")) {
+      float* wb = ws + (int64_t)2 * NSr * n;
+      __bf16* Ub = reinterpret_cast<__bf16*>(wb);
+      __bf16* Ib = Ub + n;
+      ce_round_bf16_kernel<<<(int)cdiv(2 * n / 4, 256), 256, 0, st>>>(U, I, n, Ub, Ib);
+      RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd round");
+      aU.strb = Ib;
+      aI.strb = Ub;
+      if (D == 128) ce_bwd_pair_kernel<128, false, true><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
+      else ce_bwd_pair_kernel<64, false, true><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
+      RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd tiles");
+      ce_reduce_kernel<<<(int)cdiv(2 * n / 4, 256), 256, 0, st>>>(ws, NSr, n, dU, dI, I, U, grad_out, B, a.invT);
+      RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd reduce");
+      if (N) {
+        const HStrideArgs hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
+        ce_hard_bwd_kernel<<<cdiv(B, 4), 256, 0, st>>>(U, Hn, hs.row, hs.slot, B, N, D, a.invT, lse, grad_out, dhl);
+        RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd hard");
+      }
+      return 0;
+    }
+  }
   if (D == 128) ce_bwd_pair_kernel<128, F32><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
   else ce_bwd_pair_kernel<64, F32><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
   RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_bwd tiles" : "rs_inbatch_ce_fused_bwd tiles");

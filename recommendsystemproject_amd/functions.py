@@ -137,7 +137,8 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
         return c
 
     order = list(groups.values())
-    fork = len(order) > 1 and os.environ.get('RSYS_TOWER_STREAMS', '1') != '0'
+    fork = (len(order) > 1 and os.environ.get('RSYS_TOWER_STREAMS', '1') != '0' and
+            os.environ.get('RSYS_LOOKUP_STREAMS', '1') != '0')
     if not fork:
         for idxs in order:
             for i in idxs:
@@ -209,11 +210,14 @@ def _gather_bwd_split(segs, rows, dout):
     per-token history tables, 204,800 ids into 3,500 x 32 and 614,400 tag ids into 30 x 8) each
     take a latency-bound kernel that leaves most of the chip idle, and one launch runs its kernels
     back to back: the heavy segments after the first go to side streams, forked from the current
-    one and joined back before the caller reports its gradients. RSYS_GRAD_STREAMS=0 (and the
-    bench's serial instrumented pass, RSYS_TOWER_STREAMS=0) keeps one launch."""
+    one and joined back before the caller reports its gradients. Opt-in (RSYS_GRAD_STREAMS=1;
+    never with RSYS_TOWER_STREAMS=0, the bench's serial instrumented pass): measured at C2 (bf16,
+    replayed graphs) 1.40 -> 1.48 ms per step, like the weight-gradient branches (_WgradBranch):
+    on this ROCm the replayed graph pays more for the extra cross-queue waits than the two
+    latency-bound kernels gain by overlapping."""
     heavy = [sg for sg in segs if sg.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL) and
              rows * (sg.bag if sg.kind == _hip.RS_SEG_POOL else 1) >= _HEAVY_LOOKUPS]
-    if (len(heavy) < 2 or os.environ.get('RSYS_GRAD_STREAMS', '1') == '0' or
+    if (len(heavy) < 2 or os.environ.get('RSYS_GRAD_STREAMS', '0') != '1' or
             os.environ.get('RSYS_TOWER_STREAMS', '1') == '0' or not dout.is_cuda):
         ops.gather_bwd(segs, rows, dout)
         return
