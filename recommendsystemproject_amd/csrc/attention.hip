@@ -1001,8 +1001,33 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
 // them are shared, wave w taking their pairs with query tiles tq = w mod 4, and their dK / dV
 // partials are summed in wave order at the end. (C5, L = 200, NT = 13: the busiest wave had 4 key
 // tiles = 52 (query, key) tile pairs against 39 for the others; now 43 / 42 / 42 / 42.)
+// bf16 images of the long backward: Q, K, V and dO are MFMA operands only (rounded to bf16
+// wherever they are used), so they are staged once as bf16 -- half the LDS of the fp32 images,
+// which lets three workgroups share a CU -- and their fragments are read as they stand
+constexpr int kRowPB = 24;  // bf16 image row pitch (48 B)
+template <int LP, typename QT>
+__device__ __forceinline__ void load_head_image16(const QT* __restrict__ base, int ld, int L, int off,
+                                                  __bf16 (*X)[kRowPB]) {
+  for (int e = threadIdx.x; e < LP * 4; e += 256) {
+    const int row = e >> 2, c4 = (e & 3) * 4;
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < L) v = ldq(base + (int64_t)row * ld + off + c4);
+    *reinterpret_cast<s4v*>(&X[row][c4]) = bf4(v);
+  }
+}
+__device__ __forceinline__ s4v row_frag16(const __bf16 (*X)[kRowPB], int row, int q) {
+  return *reinterpret_cast<const s4v*>(&X[row][4 * q]);
+}
+// column r, rows t0 + 4q + j of a bf16 image: the B operand fragment
+__device__ __forceinline__ s4v col_frag16(const __bf16 (*X)[kRowPB], int t0, int r, int q) {
+  s4v o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = __builtin_bit_cast(short, X[t0 + 4 * q + j][r]);
+  return o;
+}
+
 template <int NT, bool DROP, bool QB>
-__global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
+__global__ __launch_bounds__(256, 3) void attn_bwd_long1_bf16_kernel(
     const void* __restrict__ qkv_, const uint8_t* __restrict__ key_pad,
     const float* __restrict__ out, const float* __restrict__ dout, const float* __restrict__ lse,
     void* __restrict__ dqkv_, int B, int L, int d, int H, float scale, float pdrop,
@@ -1013,23 +1038,23 @@ __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
   constexpr int NR = NT - NTF;      // shared key tiles
   constexpr int NW = NW0 + NR;      // key tiles a wave visits
   constexpr int TP = 20;
-  // Q, K, V, dO; then the shared tiles' dK / dV partials; then the dQ partials
-  __shared__ __attribute__((aligned(16))) float img[4][LP][kRowP];
-  static_assert(4 * NR * 2 * 256 <= 4 * LP * kRowP, "shared-tile partials fit the image");
+  // Q, K, V, dO as bf16; then the wave-ordered dQ and shared-tile dK / dV accumulators (fp32)
+  __shared__ __attribute__((aligned(16))) __bf16 img[4][LP][kRowPB];
+  static_assert((LP * 16 + NR * 2 * 256) * 4 <= 4 * LP * kRowPB * 2, "accumulators fit the image");
   __shared__ __attribute__((aligned(16))) float L2s[LP];  // lse * log2(e)
   __shared__ __attribute__((aligned(16))) float Ds[LP];   // D_i = dO_i . O_i
   __shared__ float Kv[LP];                                // 1: key j is valid
   // per wave: the NW dS tiles of one query tile staged as bf16 (the dQ product's operand rounding,
   // so the same bits) for the transpose, all written before one barrier and read after it -- the
   // key tiles' chains overlap instead of meeting a barrier pair each; then the fp32 [16][TP]
-  // image of tile_rows. (79 KB in all: two workgroups per CU)
+  // image of tile_rows. (52 KB in all: three workgroups per CU)
   constexpr int TPB = 20;
   constexpr int TB_HALFS = NW * 16 * TPB > 2 * 16 * TP ? NW * 16 * TPB : 2 * 16 * TP;
   __shared__ __attribute__((aligned(16))) __bf16 Tbs[4][TB_HALFS];
-  float(*Qs)[kRowP] = img[0];
-  float(*Ks)[kRowP] = img[1];
-  float(*Vs)[kRowP] = img[2];
-  float(*Gs)[kRowP] = img[3];
+  __bf16(*Qs)[kRowPB] = img[0];
+  __bf16(*Ks)[kRowPB] = img[1];
+  __bf16(*Vs)[kRowPB] = img[2];
+  __bf16(*Gs)[kRowPB] = img[3];
   int b, h;
   if (!map_bh(B, H, b, h)) return;  // uniform over the workgroup
   const int bh = b * H + h;
@@ -1038,15 +1063,10 @@ __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
   const int ld = 3 * d;
   typedef typename std::conditional<QB, __bf16, float>::type QT;
   const QT* base = reinterpret_cast<const QT*>(qkv_) + (int64_t)b * L * ld + h * 16;
-  load_head_image<LP>(base, ld, L, 0, Qs);
-  load_head_image<LP>(base, ld, L, d, Ks);
-  load_head_image<LP>(base, ld, L, 2 * d, Vs);
-  for (int e = threadIdx.x; e < LP * 4; e += 256) {
-    const int row = e >> 2, c4 = (e & 3) * 4;
-    f4 v = {0.f, 0.f, 0.f, 0.f};
-    if (row < L) v = ld4(dout + ((int64_t)b * L + row) * d + h * 16 + c4);
-    *reinterpret_cast<f4*>(&Gs[row][c4]) = v;
-  }
+  load_head_image16<LP>(base, ld, L, 0, Qs);
+  load_head_image16<LP>(base, ld, L, d, Ks);
+  load_head_image16<LP>(base, ld, L, 2 * d, Vs);
+  load_head_image16<LP>(dout + (int64_t)b * L * d + h * 16, d, L, 0, Gs);
   for (int i = threadIdx.x; i < LP; i += 256) {
     float Di = 0.f, li = 0.f, kv = 0.f;
     if (i < L) {
@@ -1080,21 +1100,18 @@ __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
 #pragma unroll
   for (int u = 0; u < NW; ++u) {
     const int tk = u < NW0 ? wave + 4 * u : NTF + (u - NW0);
-    kr[u] = bf4(ld4(&Ks[tk * 16 + r][4 * q]));
-    vr[u] = bf4(ld4(&Vs[tk * 16 + r][4 * q]));
-    s4v c1[1];
-    col_frags<1, kRowP>(&Ks[tk * 16][0], r, q, c1);
-    kc[u] = c1[0];
+    kr[u] = row_frag16(Ks, tk * 16 + r, q);
+    vr[u] = row_frag16(Vs, tk * 16 + r, q);
+    kc[u] = col_frag16(Ks, tk * 16, r, q);
     kval[u] = Kv[tk * 16 + r];
     dk_acc[u] = dv_acc[u] = z;
   }
 #pragma unroll
   for (int tq = 0; tq < NT; ++tq) {
-    const s4v qr = bf4(ld4(&Qs[tq * 16 + r][4 * q]));
-    const s4v gr = bf4(ld4(&Gs[tq * 16 + r][4 * q]));
-    s4v qc[1], gc[1];
-    col_frags<1, kRowP>(&Qs[tq * 16][0], r, q, qc);
-    col_frags<1, kRowP>(&Gs[tq * 16][0], r, q, gc);
+    const s4v qr = row_frag16(Qs, tq * 16 + r, q);
+    const s4v gr = row_frag16(Gs, tq * 16 + r, q);
+    const s4v qc[1] = {col_frag16(Qs, tq * 16, r, q)};
+    const s4v gc[1] = {col_frag16(Gs, tq * 16, r, q)};
     const f4 l2 = ld4(&L2s[tq * 16 + 4 * q]);
     const f4 Dq = ld4(&Ds[tq * 16 + 4 * q]);
     dq_acc[tq] = z;
@@ -1145,50 +1162,46 @@ __global__ __launch_bounds__(256) void attn_bwd_long1_bf16_kernel(
       st4q(dbase + (int64_t)row * ld + 2 * d + 4 * (lane & 3), vv);
     }
   }
+  // dQ partials (every query tile) and the shared key tiles' dK / dV partials summed in wave order
+  // through one fp32 accumulator in the (now free) images: ((w0 + w1) + w2) + w3
   __syncthreads();  // the images are free
-  if constexpr (NR > 0) {
-    // shared key tiles: the four waves' dK / dV partials (MFMA layout, one f4 per lane) summed in
-    // wave order; wave x < NR finishes shared tile NTF + x
-    f4* part = reinterpret_cast<f4*>(&img[0][0][0]);  // [wave][x][dk, dv][lane]
+  float* accq = reinterpret_cast<float*>(&img[0][0][0]);  // [LP][16]
+  f4* accs = reinterpret_cast<f4*>(accq + LP * 16);       // [NR][dk, dv][lane]
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
 #pragma unroll
-    for (int x = 0; x < NR; ++x) {
-      part[((wave * NR + x) * 2 + 0) * 64 + lane] = dk_acc[NW0 + x];
-      part[((wave * NR + x) * 2 + 1) * 64 + lane] = dv_acc[NW0 + x];
+      for (int tq = 0; tq < NT; ++tq)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float* pp = accq + (tq * 16 + 4 * q + e) * 16 + r;
+          *pp = (w == 0 ? 0.f : *pp) + dq_acc[tq][e];
+        }
+#pragma unroll
+      for (int x = 0; x < NR; ++x) {
+        f4* pk = accs + (x * 2 + 0) * 64 + lane;
+        f4* pv = accs + (x * 2 + 1) * 64 + lane;
+        *pk = (w == 0 ? z : *pk) + dk_acc[NW0 + x];
+        *pv = (w == 0 ? z : *pv) + dv_acc[NW0 + x];
+      }
     }
     __syncthreads();
-    if (wave < NR) {
+  }
+  if constexpr (NR > 0) {
+    if (wave < NR) {  // wave x finishes shared key tile NTF + x
       const int x = wave;
-      f4 sk = part[(x * 2 + 0) * 64 + lane], sv = part[(x * 2 + 1) * 64 + lane];
-#pragma unroll
-      for (int w = 1; w < 4; ++w) {
-        sk += part[((w * NR + x) * 2 + 0) * 64 + lane];
-        sv += part[((w * NR + x) * 2 + 1) * 64 + lane];
-      }
-      const f4 vk = tile_rows<TP>(T, sk * scale, r, q, lane);
-      const f4 vv = tile_rows<TP>(T, sv, r, q, lane);
+      const f4 vk = tile_rows<TP>(T, accs[(x * 2 + 0) * 64 + lane] * scale, r, q, lane);
+      const f4 vv = tile_rows<TP>(T, accs[(x * 2 + 1) * 64 + lane], r, q, lane);
       const int row = (NTF + x) * 16 + (lane >> 2);
       if (row < L) {
         st4q(dbase + (int64_t)row * ld + d + 4 * (lane & 3), vk);
         st4q(dbase + (int64_t)row * ld + 2 * d + 4 * (lane & 3), vv);
       }
     }
-    __syncthreads();
   }
-  // dQ: the four waves' partial tiles summed in wave order through the (now free) images
-  float* part = &img[0][0][0] + wave * LP * 16;
-#pragma unroll
-  for (int tq = 0; tq < NT; ++tq)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) part[(tq * 16 + 4 * q + e) * 16 + r] = dq_acc[tq][e];
-  __syncthreads();
-  const float* p0 = &img[0][0][0];
   for (int e = threadIdx.x; e < LP * 4; e += 256) {
     const int row = e >> 2, c4 = (e & 3) * 4;
     if (row >= L) continue;
-    f4 v = ld4(p0 + row * 16 + c4);
-#pragma unroll
-    for (int w = 1; w < 4; ++w) v += ld4(p0 + w * LP * 16 + row * 16 + c4);
-    st4q(dbase + (int64_t)row * ld + c4, v * scale);
+    st4q(dbase + (int64_t)row * ld + c4, ld4(accq + row * 16 + c4) * scale);
   }
 }
 

@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 VARS=$1; CFGS=${2:-c3:fp32}
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
 for cd in $CFGS; do
   cfg=${cd%%:*}; dt=${cd#*:}
   for v in $VARS; do
