@@ -827,8 +827,33 @@ __device__ __forceinline__ void keep_col4(const DropKey& dk, bool leven, uint32_
   }
 }
 
+// bf16 images of the long kernels: Q, K, V and dO are MFMA operands only (rounded to bf16
+// wherever they are used), so they are staged once as bf16 -- half the LDS of the fp32 images,
+// which lets three workgroups share a CU -- and their fragments are read as they stand
+constexpr int kRowPB = 24;  // bf16 image row pitch (48 B)
+template <int LP, typename QT>
+__device__ __forceinline__ void load_head_image16(const QT* __restrict__ base, int ld, int L, int off,
+                                                  __bf16 (*X)[kRowPB]) {
+  for (int e = threadIdx.x; e < LP * 4; e += 256) {
+    const int row = e >> 2, c4 = (e & 3) * 4;
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < L) v = ldq(base + (int64_t)row * ld + off + c4);
+    *reinterpret_cast<s4v*>(&X[row][c4]) = bf4(v);
+  }
+}
+__device__ __forceinline__ s4v row_frag16(const __bf16 (*X)[kRowPB], int row, int q) {
+  return *reinterpret_cast<const s4v*>(&X[row][4 * q]);
+}
+// column r, rows t0 + 4q + j of a bf16 image: the B operand fragment
+__device__ __forceinline__ s4v col_frag16(const __bf16 (*X)[kRowPB], int t0, int r, int q) {
+  s4v o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = __builtin_bit_cast(short, X[t0 + 4 * q + j][r]);
+  return o;
+}
+
 #ifndef RS_LONG_FWD_MINW
-#define RS_LONG_FWD_MINW 2  // two waves per SIMD (<= 256 VGPRs): the shared-tile merge pushed it to 276
+#define RS_LONG_FWD_MINW 3  // three workgroups per CU: bf16 images (LDS) and V re-read (VGPRs)
 #endif
 template <int NT, bool DROP, bool QB>
 __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kernel(
@@ -836,9 +861,9 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
     float* __restrict__ lse, int B, int L, int d, int H, float scale, float pdrop,
     const int64_t* __restrict__ key, int site) {
   constexpr int LP = NT * 16;
-  __shared__ __attribute__((aligned(16))) float Qs[LP][kRowP];
-  __shared__ __attribute__((aligned(16))) float Ks[LP][kRowP];
-  __shared__ __attribute__((aligned(16))) float Vs[LP][kRowP];
+  __shared__ __attribute__((aligned(16))) __bf16 Qs[LP][kRowPB];
+  __shared__ __attribute__((aligned(16))) __bf16 Ks[LP][kRowPB];
+  __shared__ __attribute__((aligned(16))) __bf16 Vs[LP][kRowPB];
   __shared__ __attribute__((aligned(16))) float Tsm[4][16 * kRowP];
   int b, h;
   if (!map_bh(B, H, b, h)) return;  // uniform over the workgroup
@@ -848,19 +873,20 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
   const int ld = 3 * d;
   typedef typename std::conditional<QB, __bf16, float>::type QT;
   const QT* base = reinterpret_cast<const QT*>(qkv_) + (int64_t)b * L * ld + h * 16;
-  load_head_image<LP>(base, ld, L, 0, Qs);  // Q too: no global load inside the tile loop
-  load_head_image<LP>(base, ld, L, d, Ks);
-  load_head_image<LP>(base, ld, L, 2 * d, Vs);
+  load_head_image16<LP>(base, ld, L, 0, Qs);  // Q too: no global load inside the tile loop
+  load_head_image16<LP>(base, ld, L, d, Ks);
+  load_head_image16<LP>(base, ld, L, 2 * d, Vs);
   const uint64_t kbits = key_bits_long<NT>(key_pad, b, L, lane, q);
   DropKey dk;
   if (DROP) dk = make_key(key, site, pdrop);
   const bool leven = (L & 1) == 0;
   const float scale2 = scale * kLog2e;
   __syncthreads();
-  s4v kb[NT], vb[NT];
+  // K fragments in registers; V's column fragments re-read from the bf16 image where the P V
+  // products need them (their registers kept the kernel at two waves per SIMD)
+  s4v kb[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) kb[t] = bf4(ld4(&Ks[t * 16 + r][4 * q]));
-  col_frags<NT, kRowP>(&Vs[0][0], r, q, vb);
+  for (int t = 0; t < NT; ++t) kb[t] = row_frag16(Ks, t * 16 + r, q);
   float* T = Tsm[wave];
   // query tiles below NTF = 4 floor(NT / 4) go round-robin to the waves; the NT % 4 tiles past
   // them are shared (see the end)
@@ -868,34 +894,54 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
   for (int tq = wave; tq < NTF; tq += 4) {
     const int i = tq * 16 + r;
     const f4 z = {0.f, 0.f, 0.f, 0.f};
-    const s4v qb = bf4(ld4(&Qs[i][4 * q]));
-    f4 sv[NT];
-#pragma unroll
-    for (int tk = 0; tk < NT; ++tk) sv[tk] = mfma16(kb[tk], qb, z);
-    float m = -INFINITY;
-#pragma unroll
-    for (int tk = 0; tk < NT; ++tk)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if ((kbits >> (4 * tk + e)) & 1ull) m = fmaxf(m, sv[tk][e] * scale2);
-    m = xmax(m);
-    float l = 0.f;
+    const s4v qb = row_frag16(Qs, i, q);
+    // online softmax over chunks of CH key tiles (flash-style rescale of the running sum and of
+    // the P V accumulator when the max grows): only CH score tiles live at a time -- all NT of
+    // them held the kernel at two waves per SIMD
+    constexpr int CH = 4;
+    float m = -INFINITY, l = 0.f;
+    f4 o = z;
     const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
 #pragma unroll
-    for (int tk = 0; tk < NT; ++tk) {
-      float mk[4] = {1.f, 1.f, 1.f, 1.f};
-      if (DROP) attn_keep4(dk, leven, rowbase + tk * 16 + 4 * q, mk);
+    for (int c0 = 0; c0 < NT; c0 += CH) {
+      f4 sv[CH];
+      float cm = -INFINITY;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float pv = ((kbits >> (4 * tk + e)) & 1ull) ? __builtin_amdgcn_exp2f(sv[tk][e] * scale2 - m) : 0.f;
-        l += pv;
-        sv[tk][e] = DROP ? pv * mk[e] : pv;
+      for (int u = 0; u < CH; ++u) {
+        const int tk = c0 + u;
+        if (tk >= NT) break;
+        sv[u] = mfma16(kb[tk], qb, z);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if ((kbits >> (4 * tk + e)) & 1ull) cm = fmaxf(cm, sv[u][e] * scale2);
+      }
+      cm = xmax(cm);
+      const float mn = fmaxf(m, cm);
+      if (c0 > 0) {
+        // rescale by 2^(m - mn) (0 while no key was valid); rows 4q + e of o need query 4q + e's
+        const float al = (m == -INFINITY || mn == -INFINITY) ? (mn == -INFINITY ? 1.f : 0.f)
+                                                              : __builtin_amdgcn_exp2f(m - mn);
+        l *= al;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] *= __shfl(al, 4 * q + e, 64);
+      }
+      m = mn;
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int tk = c0 + u;
+        if (tk >= NT) break;
+        float mk[4] = {1.f, 1.f, 1.f, 1.f};
+        if (DROP) attn_keep4(dk, leven, rowbase + tk * 16 + 4 * q, mk);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float pv = ((kbits >> (4 * tk + e)) & 1ull) ? __builtin_amdgcn_exp2f(sv[u][e] * scale2 - m) : 0.f;
+          l += pv;
+          sv[u][e] = DROP ? pv * mk[e] : pv;
+        }
+        o = mfma16(bf4(sv[u]), col_frag16(Vs, tk * 16, r, q), o);
       }
     }
     l = xsum(l);
-    f4 o = z;
-#pragma unroll
-    for (int tk = 0; tk < NT; ++tk) o = mfma16(bf4(sv[tk]), vb[tk], o);
     if (q == 0 && i < L) lse[(int64_t)bh * L + i] = (m + __builtin_amdgcn_logf(l)) * kLn2;
     f4 on;
 #pragma unroll
@@ -916,7 +962,7 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
       const int tq = NTF + x;
       const int i = tq * 16 + r;
       const f4 z = {0.f, 0.f, 0.f, 0.f};
-      const s4v qb = bf4(ld4(&Qs[i][4 * q]));
+      const s4v qb = row_frag16(Qs, i, q);
       f4 sv[NT];
       float m = -INFINITY;
 #pragma unroll
@@ -942,7 +988,7 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
           l += pv;
           sv[tk][e] = DROP ? pv * mk[e] : pv;
         }
-        o = mfma16(bf4(sv[tk]), vb[tk], o);
+        o = mfma16(bf4(sv[tk]), col_frag16(Vs, tk * 16, r, q), o);
       }
       l = xsum(l);
       if (q == 0) {
@@ -1001,31 +1047,6 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
 // them are shared, wave w taking their pairs with query tiles tq = w mod 4, and their dK / dV
 // partials are summed in wave order at the end. (C5, L = 200, NT = 13: the busiest wave had 4 key
 // tiles = 52 (query, key) tile pairs against 39 for the others; now 43 / 42 / 42 / 42.)
-// bf16 images of the long backward: Q, K, V and dO are MFMA operands only (rounded to bf16
-// wherever they are used), so they are staged once as bf16 -- half the LDS of the fp32 images,
-// which lets three workgroups share a CU -- and their fragments are read as they stand
-constexpr int kRowPB = 24;  // bf16 image row pitch (48 B)
-template <int LP, typename QT>
-__device__ __forceinline__ void load_head_image16(const QT* __restrict__ base, int ld, int L, int off,
-                                                  __bf16 (*X)[kRowPB]) {
-  for (int e = threadIdx.x; e < LP * 4; e += 256) {
-    const int row = e >> 2, c4 = (e & 3) * 4;
-    f4 v = {0.f, 0.f, 0.f, 0.f};
-    if (row < L) v = ldq(base + (int64_t)row * ld + off + c4);
-    *reinterpret_cast<s4v*>(&X[row][c4]) = bf4(v);
-  }
-}
-__device__ __forceinline__ s4v row_frag16(const __bf16 (*X)[kRowPB], int row, int q) {
-  return *reinterpret_cast<const s4v*>(&X[row][4 * q]);
-}
-// column r, rows t0 + 4q + j of a bf16 image: the B operand fragment
-__device__ __forceinline__ s4v col_frag16(const __bf16 (*X)[kRowPB], int t0, int r, int q) {
-  s4v o;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) o[j] = __builtin_bit_cast(short, X[t0 + 4 * q + j][r]);
-  return o;
-}
-
 template <int NT, bool DROP, bool QB>
 __global__ __launch_bounds__(256, 3) void attn_bwd_long1_bf16_kernel(
     const void* __restrict__ qkv_, const uint8_t* __restrict__ key_pad,
