@@ -489,6 +489,10 @@ int rs_grad_sqnorm(const float* g, int64_t n, float scale, double* ws, void* str
 /* sums nparts double partials (dense + sparse-table contributions) into norm and coef */
 int rs_clip_coef(const double* ws, int nparts, float max_norm, float* total_norm, float* coef,
                  void* stream);
+/* the same, and *counter += 1 in the same launch (the optimizer's device step count, which
+ * rs_adam_step's step_dev then reads: the step that clips needs no separate counter launch) */
+int rs_clip_coef_step(const double* ws, int nparts, float max_norm, float* total_norm, float* coef,
+                      int64_t* counter, void* stream);
 int rs_scale_inplace(float* g, int64_t n, float scale, const float* coef, void* stream);
 int rs_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, float beta1,
                  float beta2, float eps, float weight_decay, int step, const int64_t* step_dev,

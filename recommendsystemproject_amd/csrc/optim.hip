@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g
 // fixed-order (deterministic) sum of nb partials: strided per-thread sums, then a fixed tree
 __global__ __launch_bounds__(1024) void clip_coef_kernel(const double* __restrict__ ws, int nb,
                                                          float max_norm, float* total_norm,
-                                                         float* coef) {
+                                                         float* coef, int64_t* counter) {
   __shared__ double red[16];
   double t = 0.0;
   for (int i = threadIdx.x; i < nb; i += 1024) t += ws[i];
@@ -66,6 +66,7 @@ __global__ __launch_bounds__(1024) void clip_coef_kernel(const double* __restric
   if (total_norm) *total_norm = norm;
   float c = max_norm / (norm + 1e-6f);
   *coef = c < 1.f ? c : 1.f;
+  if (counter) *counter += 1;  // the optimizer's step count (rs_clip_coef_step): one launch less
 }
 
 __global__ void scale_kernel(float* __restrict__ g, int64_t n, float scale,
@@ -148,8 +149,16 @@ extern "C" int rs_sqnorm_parts(int64_t n) { return sq_blocks(n); }
 extern "C" int rs_clip_coef(const double* ws, int nparts, float max_norm, float* total_norm,
                             float* coef, void* stream) {
   RS_CHECK_ARG(ws && coef && nparts >= 1, "rs_clip_coef: bad args");
-  clip_coef_kernel<<<1, 1024, 0, as_stream(stream)>>>(ws, nparts, max_norm, total_norm, coef);
+  clip_coef_kernel<<<1, 1024, 0, as_stream(stream)>>>(ws, nparts, max_norm, total_norm, coef, nullptr);
   RS_CHECK_LAUNCH("rs_clip_coef");
+  return 0;
+}
+
+extern "C" int rs_clip_coef_step(const double* ws, int nparts, float max_norm, float* total_norm,
+                                 float* coef, int64_t* counter, void* stream) {
+  RS_CHECK_ARG(ws && coef && counter && nparts >= 1, "rs_clip_coef_step: bad args");
+  clip_coef_kernel<<<1, 1024, 0, as_stream(stream)>>>(ws, nparts, max_norm, total_norm, coef, counter);
+  RS_CHECK_LAUNCH("rs_clip_coef_step");
   return 0;
 }
 

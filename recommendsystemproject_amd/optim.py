@@ -69,9 +69,10 @@ class _DeviceClip:
         self.norm = torch.zeros((), device=device, dtype=torch.float32)
         self.coef = torch.ones((), device=device, dtype=torch.float32)
 
-    def compute(self, g, n, max_norm, scale=1.0, lazy=()):
+    def compute(self, g, n, max_norm, scale=1.0, lazy=(), counter=None):
         """2-norm of g[:n] plus the distinct rows of every lazy table's step calls (their other
-        rows hold no gradient), one double partial per block, summed in one fixed order."""
+        rows hold no gradient), one double partial per block, summed in one fixed order.
+        `counter` (a device int64 step count): advanced by the same launch (rs_clip_coef_step)."""
         L = _hip.lib()
         nd = int(L.rs_sqnorm_parts(n))
         ns = int(L.rs_sorted_sqnorm_parts())
@@ -93,8 +94,12 @@ class _DeviceClip:
         first = next((k for k, w in enumerate(work) if getattr(w[0], 'shard', None) is not None), None)
         if first is not None:
             torch.distributed.all_reduce(ws[nd + first * ns:nd + len(work) * ns])
-        _hip.call('rs_clip_coef', ws.data_ptr(), nd + ns * len(work), float(max_norm),
-                  self.norm.data_ptr(), self.coef.data_ptr(), ops.stream())
+        if counter is not None:
+            _hip.call('rs_clip_coef_step', ws.data_ptr(), nd + ns * len(work), float(max_norm),
+                      self.norm.data_ptr(), self.coef.data_ptr(), counter.data_ptr(), ops.stream())
+        else:
+            _hip.call('rs_clip_coef', ws.data_ptr(), nd + ns * len(work), float(max_norm),
+                      self.norm.data_ptr(), self.coef.data_ptr(), ops.stream())
 
 
 def clip_grad_norm_(parameters, max_norm, norm_type=2.0, error_if_nonfinite=False, foreach=None):
@@ -203,10 +208,14 @@ class Adam(torch.optim.Optimizer):
                 st['step'] += 1
                 lr, eps, wd = float(group['lr']), float(group['eps']), float(group['weight_decay'])
                 coef = None
+                counted = False
                 if clip_max_norm is not None and clip_max_norm > 0:
                     if self._clip is None:
                         self._clip = _DeviceClip(f.data.device)
-                    self._clip.compute(f.grad, f.dense_numel, clip_max_norm, self.grad_scale, f.lazy)
+                    # dense step count advanced by the clip's own launch (no rs_counter_add)
+                    counted = not f.lazy
+                    self._clip.compute(f.grad, f.dense_numel, clip_max_norm, self.grad_scale, f.lazy,
+                                       counter=st['step_dev'] if counted else None)
                     coef = self._clip.coef.data_ptr()
                 # device-side step count: the same launch replays correctly inside a hipGraph
                 if f.lazy:
@@ -214,7 +223,7 @@ class Adam(torch.optim.Optimizer):
                         raise RuntimeError(f'lazy Adam: more than {CONSTS_CAP - 2} steps; raise optim.CONSTS_CAP')
                     _hip.call('rs_adam_prepare', st['step_dev'].data_ptr(), st['consts'].data_ptr(),
                               CONSTS_CAP, lr, float(b1), float(b2), ops.stream())
-                else:
+                elif not counted:
                     _hip.call('rs_counter_add', st['step_dev'].data_ptr(), 1, ops.stream())
                 _hip.call('rs_adam_step', f.data.data_ptr(), f.grad.data_ptr(), st['m'].data_ptr(),
                           st['v'].data_ptr(), f.dense_numel, lr, float(b1), float(b2), eps, wd, 0,

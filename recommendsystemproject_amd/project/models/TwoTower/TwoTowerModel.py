@@ -42,19 +42,6 @@ class TwoTowerModel(nn.Module):
             self._rs_side_stream = s
         return s
 
-    def _user_stream(self, dev):
-        """RSYS_USER_STREAM_PRIORITY=1: the user tower (the step's critical path at C3: the history
-        table's sort and catch-up, then its tower) on a high-priority stream of its own, so the
-        item tower's kernels beside it do not delay its dispatches."""
-        if os.environ.get('RSYS_USER_STREAM_PRIORITY', '0') != '1':
-            return None
-        s = getattr(self, '_rs_user_stream', None)
-        if s is None or s.device != dev:
-            lo, hi = torch.cuda.Stream.priority_range()
-            s = torch.cuda.Stream(device=dev, priority=hi)
-            self._rs_user_stream = s
-        return s
-
     def forward(self, batch_data):
         """-> (user_emb [B,D], item_emb [B,D], hard_neg_emb [B,N,D] or None) (TwoTowerModel.py:35-62;
         T13: one item-tower pass per hard-negative slot, so BatchNorm statistics are per slot)."""
@@ -79,21 +66,13 @@ class TwoTowerModel(nn.Module):
         side.wait_stream(main)
         with torch.cuda.stream(side):
             item_emb, hard_neg_emb = self._item_side(batch_data)
-        ustream = self._user_stream(dev)
-        if ustream is not None:
-            ustream.wait_stream(main)
-            with torch.cuda.stream(ustream):
-                user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
-            main.wait_stream(ustream)
-            user_emb.record_stream(main)
-        else:
-            user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
+        user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
         main.wait_stream(side)
         outs = [t for t in (item_emb, hard_neg_emb) if t is not None]
         for t in outs:
             t.record_stream(main)  # made on the side stream, read by the loss on the main one
         if torch.is_grad_enabled() and item_emb.requires_grad:
-            self._join_backward(main, [(side, outs)] + ([(ustream, [user_emb])] if ustream is not None else []))
+            self._join_backward(main, [(side, outs)])
         return user_emb, item_emb, hard_neg_emb
 
     @staticmethod
