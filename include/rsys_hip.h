@@ -250,12 +250,17 @@ int rs_seq_mask(const int64_t* seq, int64_t ld_seq, int B, int L, int64_t pad_va
  * RS_ATTN_QKV_BF16 (with RS_GEMM_BF16, on that path only): qkv is bf16 storage and rs_attn_bwd
  * writes dqkv as bf16 (RNE); Q, K, V are MFMA operands only, so the products are unchanged. */
 #define RS_ATTN_QKV_BF16 2048
+/* zbits (optional, may be NULL; after stream so that callers of the earlier signature stay
+ * valid): on the bf16 path with L <= 64 and p > 0, rs_attn_fwd stores the dropout keep decisions
+ * there -- B*H*ceil(L/16)*64 uint16 words, bit 4 tk + e of word (b H + h, tq, lane) -- and
+ * rs_attn_bwd given the same buffer reads them instead of drawing them again (identical draws).
+ * Pass NULL to both, or the same buffer to both; elsewhere it is ignored. */
 int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out, float* lse,
                 int B, int L, int d, int H, float scale, float p, const int64_t* key, int site,
-                int flags, void* stream);
+                int flags, void* stream, uint16_t* zbits);
 int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float* out, const float* dout,
                 const float* lse, float* dqkv, int B, int L, int d, int H, float scale, float p,
-                const int64_t* key, int site, int flags, void* stream);
+                const int64_t* key, int site, int flags, void* stream, const uint16_t* zbits);
 
 /* Attention for ONE query row per sample, i_b = last[b] (the final encoder layer: the encoder
  * returns context[b, last[b]] only, SequenceEncoder.py:58-74 (T7), so the final layer's other

@@ -75,8 +75,8 @@ SIGNATURES = {
     'rs_gather_bwd': (i32, [vp, i32, i32, vp, i32, vp, vp]),
     'rs_set_deterministic': (i32, [i32]),
     'rs_seq_mask': (i32, [vp, i64, i32, i32, i64, vp, vp, vp]),
-    'rs_attn_fwd': (i32, [vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, vp]),
-    'rs_attn_bwd': (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, vp]),
+    'rs_attn_fwd': (i32, [vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, vp, vp]),
+    'rs_attn_bwd': (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, vp, vp]),
     'rs_attn_rows_fwd': (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, vp]),
     'rs_attn_rows_bwd': (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, vp]),
     'rs_add_layernorm_fwd': (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, vp, i32, vp]),

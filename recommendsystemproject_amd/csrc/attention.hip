@@ -460,10 +460,14 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef __bf16 bf4v __attribute__((ext_vector_type(4)));
 
+// two v_cvt_pk_bf16_f32 (round to nearest even, as the element-wise casts; those compiled to four
+// single-element converts and two v_perm_b32)
 __device__ __forceinline__ s4v bf4(const f4& v) {
-  bf4v h;
-  h[0] = (__bf16)v[0]; h[1] = (__bf16)v[1]; h[2] = (__bf16)v[2]; h[3] = (__bf16)v[3];
-  return __builtin_bit_cast(s4v, h);
+  typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  const bf2v lo = __builtin_convertvector(f2v{v[0], v[1]}, bf2v);
+  const bf2v hi = __builtin_convertvector(f2v{v[2], v[3]}, bf2v);
+  return __builtin_bit_cast(s4v, __builtin_shufflevector(lo, hi, 0, 1, 2, 3));
 }
 __device__ __forceinline__ f4 mfma16(const s4v& a, const s4v& b, const f4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
@@ -515,6 +519,47 @@ __device__ __forceinline__ void attn_keep4(const DropKey& dk, bool leven, uint32
   }
 }
 
+// the same draws as keep decisions (kept <-> multiplier 1/(1-p)): the kernels below fold the
+// 1/(1-p) into one product per output element and select instead of multiplying
+__device__ __forceinline__ void attn_keep4b(const DropKey& dk, bool leven, uint32_t idx0, bool (&kp)[4]) {
+  if (leven) {
+    const uint32_t h0 = pair_hash32(dk, idx0 >> 1), h1 = pair_hash32(dk, (idx0 >> 1) + 1);
+    kp[0] = (h0 & 0xffffu) >= dk.thresh;
+    kp[1] = (h0 >> 16) >= dk.thresh;
+    kp[2] = (h1 & 0xffffu) >= dk.thresh;
+    kp[3] = (h1 >> 16) >= dk.thresh;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t x = idx0 + i, hh = pair_hash32(dk, x >> 1);
+      kp[i] = ((x & 1) ? (hh >> 16) : (hh & 0xffffu)) >= dk.thresh;
+    }
+  }
+}
+
+// Score-tile accumulator init: 0 for valid keys, -inf for padded ones (bit 4t + e of the lane's
+// key bits), so the MFMA itself masks the scores: no per-element select in the max or the exp.
+template <int NT>
+__device__ __forceinline__ void key_bias(uint32_t kbits, f4 (&kbias)[NT]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) kbias[t][e] = ((kbits >> (4 * t + e)) & 1u) ? 0.f : -INFINITY;
+}
+// IEEE maximum (v_maximum3_f32 on gfx950): unlike fmaxf it needs no canonicalising v_max_f32
+// of every MFMA result first
+__device__ __forceinline__ float vmax(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+
+// transposed bf16 fragment of a per-wave [16][WP] image W (row = query, 16-bit elements): lane
+// (r, q) receives W[4q + j][16 tk + r], j < 4 -- the A operand [key r][query 4q + j] of a product
+// that sums over the tile's queries (ds_read_b64_tr_b16; EXEC must be full: the callers' waves
+// exit whole or not at all)
+__device__ __forceinline__ s4v tr_col(const __bf16* W, int wp, int tk, int lane) {
+  typedef __attribute__((address_space(3))) s4v* lptr;
+  const int g = lane >> 4, l16 = lane & 15;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lptr)(W + (4 * g + (l16 >> 2)) * wp + 16 * tk + 4 * (l16 & 3)));
+}
+
 // 16x16 tile held as acc[e] = X[row 4q + e][col r] -> rows of 4 consecutive columns per lane
 // through the wave's LDS image T (pitch TP): lane l gets row l >> 2, columns 4 (l & 3) .. + 3
 template <int TP>
@@ -533,11 +578,14 @@ __device__ __forceinline__ void st4q(__bf16* p, const f4& v) {
   *reinterpret_cast<bf4v*>(p) = h;
 }
 
-template <int NT, bool DROP, bool QB>
+// ZB (with DROP): the keep decisions of the lane's 4 NT (query, key) elements of query tile tq are
+// also stored, bit 4 tk + e, as zbits[(bh NT + tq) 64 + lane] (16 bits, NT <= 4) for the backward,
+// which then reads them instead of drawing them again
+template <int NT, bool DROP, bool QB, bool ZB = false>
 __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
     const void* __restrict__ qkv_, const uint8_t* __restrict__ key_pad, float* __restrict__ out,
     float* __restrict__ lse, int B, int L, int d, int H, float scale, float pdrop,
-    const int64_t* __restrict__ key, int site) {
+    const int64_t* __restrict__ key, int site, uint16_t* __restrict__ zbits = nullptr) {
   constexpr int LP = NT * 16;
   __shared__ __attribute__((aligned(16))) float Vsm[4][LP][kRowP];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -559,6 +607,8 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
     *reinterpret_cast<f4*>(&Vs[row][4 * q]) = row < L ? ldq(base + (int64_t)row * ld + 2 * d + 4 * q) : z;
   }
   const uint32_t kbits = key_bits<NT>(key_pad, b, L, lane, q);
+  f4 kbias[NT];
+  key_bias<NT>(kbits, kbias);
   DropKey dk;
   if (DROP) dk = make_key(key, site, pdrop);
   const bool leven = (L & 1) == 0;
@@ -571,57 +621,67 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(
   for (int tq = 0; tq < NT; ++tq) {
     f4 sv[NT];
 #pragma unroll
-    for (int tk = 0; tk < NT; ++tk) sv[tk] = mfma16(kb[tk], qb[tq], f4{0.f, 0.f, 0.f, 0.f});
+    for (int tk = 0; tk < NT; ++tk) sv[tk] = mfma16(kb[tk], qb[tq], kbias[tk]);  // masked: -inf
+    // max of the raw scores, scaled once (scale2 > 0 and rounding is monotonic: bitwise the max
+    // of the scaled scores); a row with every key masked uses 0 (P = 0, l = 0, as before)
     float m = -INFINITY;
 #pragma unroll
-    for (int tk = 0; tk < NT; ++tk)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if ((kbits >> (4 * tk + e)) & 1u) m = fmaxf(m, sv[tk][e] * scale2);
+    for (int tk = 0; tk < NT; ++tk) m = vmax(vmax(vmax(m, sv[tk][0]), sv[tk][1]), vmax(sv[tk][2], sv[tk][3]));
     m = xmax(m);
+    const float ms = m == -INFINITY ? 0.f : m * scale2;
     float l = 0.f;
     const int i = tq * 16 + r;
     const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
+    uint32_t zw = 0;
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk) {
-      float mk[4] = {1.f, 1.f, 1.f, 1.f};
-      if (DROP) attn_keep4(dk, leven, rowbase + tk * 16 + 4 * q, mk);
+      bool kp[4] = {true, true, true, true};
+      if (DROP) attn_keep4b(dk, leven, rowbase + tk * 16 + 4 * q, kp);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float pv = ((kbits >> (4 * tk + e)) & 1u) ? __builtin_amdgcn_exp2f(sv[tk][e] * scale2 - m) : 0.f;
+        const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sv[tk][e], scale2, -ms));
         l += pv;
-        sv[tk][e] = DROP ? pv * mk[e] : pv;
+        sv[tk][e] = kp[e] ? pv : 0.f;  // P∘Z (1/(1-p) applied to the output row below)
+        if (ZB) zw |= kp[e] ? (1u << (4 * tk + e)) : 0u;
       }
     }
+    if (ZB) zbits[((int64_t)bh * NT + tq) * 64 + lane] = (uint16_t)zw;
     l = xsum(l);
     f4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk) o = mfma16(bf4(sv[tk]), vb[tk], o);
-    if (q == 0 && i < L) lse[(int64_t)bh * L + i] = (m + __builtin_amdgcn_logf(l)) * kLn2;
+    if (q == 0 && i < L) lse[(int64_t)bh * L + i] = (ms + __builtin_amdgcn_logf(l)) * kLn2;
     // rows 4q + e of the tile need the 1/l of query 4q + e (lane 4q + e)
+    const float rl = DROP ? __builtin_amdgcn_rcpf(l) * dk.scale : __builtin_amdgcn_rcpf(l);
     f4 on;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) on[e] = o[e] * __builtin_amdgcn_rcpf(__shfl(l, 4 * q + e, 64));
+    for (int e = 0; e < 4; ++e) on[e] = o[e] * __shfl(rl, 4 * q + e, 64);
     const f4 v = tile_rows<kRowP>(T, on, r, q, lane);
     const int row = tq * 16 + (lane >> 2);
     if (row < L) st4q(out + ((int64_t)b * L + row) * d + h * 16 + 4 * (lane & 3), v);
   }
 }
 
-template <int NT, bool DROP, bool QB>
-// 3 waves per SIMD (<= 168 VGPRs, a few spilled words): 10 % faster than the unbounded 236
+// 3 waves per SIMD (<= 168 VGPRs). ZB (with DROP): the keep decisions come from the forward's
+// zbits (attn_fwd_bf16_kernel) instead of the hash -- the same draws, none of the hash's VALU work
+template <int NT, bool DROP, bool QB, bool ZB = false>
 __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(
     const void* __restrict__ qkv_, const uint8_t* __restrict__ key_pad,
     const float* __restrict__ out, const float* __restrict__ dout, const float* __restrict__ lse,
     void* __restrict__ dqkv_, int B, int L, int d, int H, float scale, float pdrop,
-    const int64_t* __restrict__ key, int site) {
+    const int64_t* __restrict__ key, int site, const uint16_t* __restrict__ zbits = nullptr) {
   constexpr int LP = NT * 16;
   // pitch 24: the transpose's ds_read_b128 (rows r, columns 4q) is conflict-free; its b32 writes
   // are 2-way, which costs nothing for ds_write_b32 (MI355X_MICROARCH.md §LDS)
   constexpr int TP = 24;
-  // one 6 KB image per wave: Q, K and dO pass through it once (column fragments), then it is the
-  // transpose buffer of P∘Z, dS and the output tiles
-  __shared__ __attribute__((aligned(16))) float Xsm[4][LP * TP];
+  // bf16 [16 queries][WP] images of one query tile's P∘Z and dS (row = query, 4 keys per 8-byte
+  // store), read back transposed (tr_col); WP = LP + 16: 80 at LP = 64 puts the eight rows of a
+  // 32-lane half's transposed reads on disjoint banks
+  constexpr int WP = LP + 16;
+  constexpr int XW = (LP * TP > 16 * TP + 16 * WP) ? LP * TP : 16 * TP + 16 * WP;
+  // one image per wave (6.5 KB at LP = 64): Q, K and dO pass through it once (column
+  // fragments), then rows [0, 16) are the output transposes and the rest the P∘Z / dS images
+  __shared__ __attribute__((aligned(16))) float Xsm[4][XW];
   // the Q and dO column fragments (each used once per query tile) wait in LDS, one 8-byte slot
   // per lane (conflict-free b64 accesses): held in registers they pushed the kernel past its
   // 168-VGPR budget (3 waves per SIMD) and the spill stores were ~56 MB of scratch writes per
@@ -652,7 +712,10 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(
       kf[t] = ok ? ldq(base + (int64_t)row * ld + d + 4 * q) : z;
       vb[t] = bf4(ok ? ldq(base + (int64_t)row * ld + 2 * d + 4 * q) : z);
       gf[t] = ok ? ld4(gbase + (int64_t)row * d + 4 * q) : z;
-      lsei[t] = ok ? lse[(int64_t)bh * L + row] * kLog2e : 0.f;
+      // base-2 log-sum-exp; +inf past L and 0 for a row with every key masked (lse = -inf): the
+      // exp below then gives P = 0 for those rows as the masked selects used to
+      const float ls = ok ? lse[(int64_t)bh * L + row] : 0.f;
+      lsei[t] = !ok ? INFINITY : (ls == -INFINITY ? 0.f : ls * kLog2e);
     }
 #pragma unroll
     for (int pass = 0; pass < 3; ++pass) {
@@ -677,12 +740,21 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(
       gb[t] = bf4(gf[t]);
     }
   }
+  uint32_t zw[NT];
+  if (ZB)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) zw[t] = zbits[((int64_t)bh * NT + t) * 64 + lane];
   const uint32_t kbits = key_bits<NT>(key_pad, b, L, lane, q);
+  f4 kbias[NT];
+  key_bias<NT>(kbits, kbias);
   DropKey dk;
   if (DROP) dk = make_key(key, site, pdrop);
   const bool leven = (L & 1) == 0;
   const float scale2 = scale * kLog2e;
+  const float zs = DROP ? dk.scale : 1.f;  // the kept elements' 1/(1-p), applied per output
   QT* dbase = reinterpret_cast<QT*>(dqkv_) + (int64_t)b * L * ld + h * 16;
+  __bf16* Wpz = reinterpret_cast<__bf16*>(T + 16 * TP);  // [16][WP] P∘Z / zs
+  __bf16* Wds = Wpz + 16 * WP;                            // [16][WP] dS
   f4 dv_acc[NT], dk_acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) dv_acc[t] = dk_acc[t] = f4{0.f, 0.f, 0.f, 0.f};
@@ -690,67 +762,63 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(
   for (int tq = 0; tq < NT; ++tq) {
     const int i = tq * 16 + r;
     const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
-    f4 pvs[NT], ds[NT];  // ds holds z * dP^T until D is known
-    uint32_t zb = 0;      // kept-element bits (dropout), bit 4 tk + e
+    f4 pvs[NT], dpz[NT];  // P and dP∘Z / zs of the lane's (query i, keys 16 tk + 4q + e)
     float Dp = 0.f;
 #pragma unroll
     for (int tk = 0; tk < NT; ++tk) {
-      const f4 sacc = mfma16(kb[tk], qb[tq], f4{0.f, 0.f, 0.f, 0.f});  // S^T[key][query]
+      const f4 sacc = mfma16(kb[tk], qb[tq], kbias[tk]);               // S^T[key][query], masked -inf
       const f4 pacc = mfma16(vb[tk], gb[tq], f4{0.f, 0.f, 0.f, 0.f});  // dP^T = V dO^T
-      float mk[4] = {1.f, 1.f, 1.f, 1.f};
-      if (DROP) attn_keep4(dk, leven, rowbase + tk * 16 + 4 * q, mk);
+      bool kp[4] = {true, true, true, true};
+      if (ZB) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) kp[e] = (zw[tq] >> (4 * tk + e)) & 1u;
+      } else if (DROP) {
+        attn_keep4b(dk, leven, rowbase + tk * 16 + 4 * q, kp);
+      }
+      f4 pz;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float pv = (((kbits >> (4 * tk + e)) & 1u) && i < L)
-                             ? __builtin_amdgcn_exp2f(sacc[e] * scale2 - lsei[tq]) : 0.f;
+        // lsei is +inf past L and 0 for a row with no valid key: P = 0 there without a select
+        const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[e], scale2, -lsei[tq]));
         pvs[tk][e] = pv;
-        ds[tk][e] = DROP ? mk[e] * pacc[e] : pacc[e];
-        if (DROP) zb |= (mk[e] != 0.f ? 1u : 0u) << (4 * tk + e);
-        Dp += pv * ds[tk][e];
+        dpz[tk][e] = kp[e] ? pacc[e] : 0.f;
+        pz[e] = kp[e] ? pv : 0.f;
+        Dp = __builtin_fmaf(pv, dpz[tk][e], Dp);
       }
+      // P∘Z row slice -> W (A operand of dV = (P∘Z)^T dO after the transposed read)
+      *reinterpret_cast<s4v*>(&Wpz[r * WP + 16 * tk + 4 * q]) = bf4(pz);
     }
-    // D_i = sum_j P_ij dP_ij (= dO_i . O_i): from the register tiles, no O read
-    const float Di = xsum(Dp);
-#pragma unroll
-    for (int tk = 0; tk < NT; ++tk)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) ds[tk][e] = pvs[tk][e] * (ds[tk][e] - Di);
+    // D_i = sum_j P_ij (dP∘Z)_ij (= dO_i . O_i): from the register tiles, no O read
+    const float Di = xsum(Dp) * zs;
     f4 dq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int tk = 0; tk < NT; ++tk) dq = mfma16(bf4(ds[tk]), kc[tk], dq);  // dS[query][key] K
+    for (int tk = 0; tk < NT; ++tk) {
+      f4 ds;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ds[e] = pvs[tk][e] * __builtin_fmaf(dpz[tk][e], zs, -Di);
+      const s4v dsb = bf4(ds);
+      *reinterpret_cast<s4v*>(&Wds[r * WP + 16 * tk + 4 * q]) = dsb;
+      dq = mfma16(dsb, kc[tk], dq);  // dS[query][key] K
+    }
+    __builtin_amdgcn_wave_barrier();
+    // dV[key][c] += (P∘Z)^T dO and dK[key][c] += dS^T Q: A = [key = lane & 15][query 4q + j]
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) {
+      dv_acc[tk] = mfma16(tr_col(Wpz, WP, tk, lane), Fsm[wave][1][tq][lane], dv_acc[tk]);
+      dk_acc[tk] = mfma16(tr_col(Wds, WP, tk, lane), Fsm[wave][0][tq][lane], dk_acc[tk]);
+    }
     {
       const f4 v = tile_rows<TP>(T, dq * scale, r, q, lane);
       const int row = tq * 16 + (lane >> 2);
       if (row < L) st4q(dbase + (int64_t)row * ld + 4 * (lane & 3), v);
     }
-    // dV[key][c] += PZ^T dO and dK[key][c] += dS^T Q: A = [key = lane & 15][query], i.e. the
-    // transpose of this lane's tiles, through T (T[key][query])
-#pragma unroll
-    for (int tk = 0; tk < NT; ++tk)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)  // P∘Z (kept: P * 1/(1-p), the forward's product)
-        T[(tk * 16 + 4 * q + e) * TP + r] =
-            DROP ? (((zb >> (4 * tk + e)) & 1u) ? pvs[tk][e] * dk.scale : 0.f) : pvs[tk][e];
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int tk = 0; tk < NT; ++tk)
-      dv_acc[tk] = mfma16(bf4(ld4(&T[(tk * 16 + r) * TP + 4 * q])), Fsm[wave][1][tq][lane], dv_acc[tk]);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int tk = 0; tk < NT; ++tk)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) T[(tk * 16 + 4 * q + e) * TP + r] = ds[tk][e];
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int tk = 0; tk < NT; ++tk)
-      dk_acc[tk] = mfma16(bf4(ld4(&T[(tk * 16 + r) * TP + 4 * q])), Fsm[wave][0][tq][lane], dk_acc[tk]);
     __builtin_amdgcn_wave_barrier();
   }
   // dK / dV rows: acc[e] = X[key 16 tk + 4 q + e][c = r]
 #pragma unroll
   for (int tk = 0; tk < NT; ++tk) {
     const f4 vk = tile_rows<TP>(T, dk_acc[tk] * scale, r, q, lane);
-    const f4 vv = tile_rows<TP>(T, dv_acc[tk], r, q, lane);
+    const f4 vv = tile_rows<TP>(T, dv_acc[tk] * zs, r, q, lane);
     const int row = tk * 16 + (lane >> 2);
     if (row < L) {
       st4q(dbase + (int64_t)row * ld + d + 4 * (lane & 3), vk);
@@ -865,6 +933,8 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
   __shared__ __attribute__((aligned(16))) __bf16 Ks[LP][kRowPB];
   __shared__ __attribute__((aligned(16))) __bf16 Vs[LP][kRowPB];
   __shared__ __attribute__((aligned(16))) float Tsm[4][16 * kRowP];
+  // score-tile accumulator init per key: 0 (valid) or -inf (padded, or past L): the MFMA masks
+  __shared__ __attribute__((aligned(16))) float Kb[LP];
   int b, h;
   if (!map_bh(B, H, b, h)) return;  // uniform over the workgroup
   const int bh = b * H + h;
@@ -876,7 +946,7 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
   load_head_image16<LP>(base, ld, L, 0, Qs);  // Q too: no global load inside the tile loop
   load_head_image16<LP>(base, ld, L, d, Ks);
   load_head_image16<LP>(base, ld, L, 2 * d, Vs);
-  const uint64_t kbits = key_bits_long<NT>(key_pad, b, L, lane, q);
+  for (int j = threadIdx.x; j < LP; j += 256) Kb[j] = (j < L && key_pad[(int64_t)b * L + j] == 0) ? 0.f : -INFINITY;
   DropKey dk;
   if (DROP) dk = make_key(key, site, pdrop);
   const bool leven = (L & 1) == 0;
@@ -899,7 +969,8 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
     // the P V accumulator when the max grows): only CH score tiles live at a time -- all NT of
     // them held the kernel at two waves per SIMD
     constexpr int CH = 4;
-    float m = -INFINITY, l = 0.f;
+    // m: running max of the raw (masked) scores; ms = m * scale2, or 0 while no key was valid
+    float m = -INFINITY, ms = 0.f, l = 0.f;
     f4 o = z;
     const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
 #pragma unroll
@@ -910,42 +981,43 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
       for (int u = 0; u < CH; ++u) {
         const int tk = c0 + u;
         if (tk >= NT) break;
-        sv[u] = mfma16(kb[tk], qb, z);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if ((kbits >> (4 * tk + e)) & 1ull) cm = fmaxf(cm, sv[u][e] * scale2);
+        sv[u] = mfma16(kb[tk], qb, ld4(&Kb[tk * 16 + 4 * q]));
+        cm = vmax(vmax(vmax(cm, sv[u][0]), sv[u][1]), vmax(sv[u][2], sv[u][3]));
       }
       cm = xmax(cm);
-      const float mn = fmaxf(m, cm);
+      const float mn = vmax(m, cm);
+      const float msn = mn == -INFINITY ? 0.f : mn * scale2;
       if (c0 > 0) {
-        // rescale by 2^(m - mn) (0 while no key was valid); rows 4q + e of o need query 4q + e's
-        const float al = (m == -INFINITY || mn == -INFINITY) ? (mn == -INFINITY ? 1.f : 0.f)
-                                                              : __builtin_amdgcn_exp2f(m - mn);
+        // rescale by 2^(ms - msn) (l and o are 0 while no key was valid); rows 4q + e of o need
+        // query 4q + e's factor
+        const float al = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - msn);
         l *= al;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] *= __shfl(al, 4 * q + e, 64);
       }
       m = mn;
+      ms = msn;
 #pragma unroll
       for (int u = 0; u < CH; ++u) {
         const int tk = c0 + u;
         if (tk >= NT) break;
-        float mk[4] = {1.f, 1.f, 1.f, 1.f};
-        if (DROP) attn_keep4(dk, leven, rowbase + tk * 16 + 4 * q, mk);
+        bool kp[4] = {true, true, true, true};
+        if (DROP) attn_keep4b(dk, leven, rowbase + tk * 16 + 4 * q, kp);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float pv = ((kbits >> (4 * tk + e)) & 1ull) ? __builtin_amdgcn_exp2f(sv[u][e] * scale2 - m) : 0.f;
+          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sv[u][e], scale2, -ms));
           l += pv;
-          sv[u][e] = DROP ? pv * mk[e] : pv;
+          sv[u][e] = kp[e] ? pv : 0.f;  // P∘Z / (1/(1-p)): the factor goes on the output row
         }
         o = mfma16(bf4(sv[u]), col_frag16(Vs, tk * 16, r, q), o);
       }
     }
     l = xsum(l);
-    if (q == 0 && i < L) lse[(int64_t)bh * L + i] = (m + __builtin_amdgcn_logf(l)) * kLn2;
+    if (q == 0 && i < L) lse[(int64_t)bh * L + i] = (ms + __builtin_amdgcn_logf(l)) * kLn2;
+    const float rl = DROP ? __builtin_amdgcn_rcpf(l) * dk.scale : __builtin_amdgcn_rcpf(l);
     f4 on;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) on[e] = o[e] * __builtin_amdgcn_rcpf(__shfl(l, 4 * q + e, 64));
+    for (int e = 0; e < 4; ++e) on[e] = o[e] * __shfl(rl, 4 * q + e, 64);
     const f4 v = tile_rows<kRowP>(T, on, r, q, lane);
     const int row = tq * 16 + (lane >> 2);
     if (row < L) st4q(out + ((int64_t)b * L + row) * d + h * 16 + 4 * (lane & 3), v);
@@ -968,25 +1040,25 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
 #pragma unroll
       for (int tk = 0; tk < NT; ++tk) {
         if ((tk & 3) != wave) continue;  // wave-uniform
-        sv[tk] = mfma16(kb[tk], qb, z);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if ((kbits >> (4 * tk + e)) & 1ull) m = fmaxf(m, sv[tk][e] * scale2);
+        sv[tk] = mfma16(kb[tk], qb, ld4(&Kb[tk * 16 + 4 * q]));
+        m = vmax(vmax(vmax(m, sv[tk][0]), sv[tk][1]), vmax(sv[tk][2], sv[tk][3]));
       }
       m = xmax(m);
+      m = m == -INFINITY ? -INFINITY : m * scale2;  // the merge below reads -inf as "no valid key"
+      const float ms = m == -INFINITY ? 0.f : m;
       float l = 0.f;
       const uint32_t rowbase = ((uint32_t)bh * (uint32_t)L + (uint32_t)i) * (uint32_t)L;
       f4 o = z;
 #pragma unroll
       for (int tk = 0; tk < NT; ++tk) {
         if ((tk & 3) != wave) continue;
-        float mk[4] = {1.f, 1.f, 1.f, 1.f};
-        if (DROP) attn_keep4(dk, leven, rowbase + tk * 16 + 4 * q, mk);
+        bool kp[4] = {true, true, true, true};
+        if (DROP) attn_keep4b(dk, leven, rowbase + tk * 16 + 4 * q, kp);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float pv = ((kbits >> (4 * tk + e)) & 1ull) ? __builtin_amdgcn_exp2f(sv[tk][e] * scale2 - m) : 0.f;
+          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sv[tk][e], scale2, -ms));
           l += pv;
-          sv[tk][e] = DROP ? pv * mk[e] : pv;
+          sv[tk][e] = kp[e] ? pv : 0.f;
         }
         o = mfma16(bf4(sv[tk]), col_frag16(Vs, tk * 16, r, q), o);
       }
@@ -1016,7 +1088,7 @@ __global__ __launch_bounds__(256, RS_LONG_FWD_MINW) void attn_fwd_long_bf16_kern
           lt += f * mlp[w][x][1][qi];
           ot += f * olp[w][x][lane][e];
         }
-        on[e] = ot * __builtin_amdgcn_rcpf(lt);
+        on[e] = ot * (DROP ? __builtin_amdgcn_rcpf(lt) * dk.scale : __builtin_amdgcn_rcpf(lt));
       }
       const int i = tq * 16 + r;
       if (q == 0 && i < L) {
@@ -1098,8 +1170,11 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_long1_bf16_kernel(
         const f4 ov = ld4(o + c), gv = ld4(g + c);
         Di += ov[0] * gv[0] + ov[1] * gv[1] + ov[2] * gv[2] + ov[3] * gv[3];
       }
-      li = lse[(int64_t)bh * L + i] * kLog2e;
+      const float ls = lse[(int64_t)bh * L + i];
+      li = ls == -INFINITY ? 0.f : ls * kLog2e;  // a row with no valid key: P = 0 below
       kv = key_pad[(int64_t)b * L + i] == 0 ? 1.f : 0.f;
+    } else {
+      li = INFINITY;  // query rows past L: P = 0 without a select
     }
     Ds[i] = Di;
     L2s[i] = li;
@@ -1149,15 +1224,18 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_long1_bf16_kernel(
       f4 pz, ds;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int i = tq * 16 + 4 * q + e;
-        const float pv = (kval[u] != 0.f && i < L) ? __builtin_amdgcn_exp2f(sacc[e] * scale2 - l2[e]) : 0.f;
+        // l2 is +inf past L and 0 for a row with no valid key; the key's validity is lane-uniform
+        float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[e], scale2, -l2[e]));
+        pv = kval[u] != 0.f ? pv : 0.f;
         pz[e] = pv * mk[e];
-        ds[e] = pv * (mk[e] * pacc[e] - Dq[e]);
+        ds[e] = pv * __builtin_fmaf(mk[e], pacc[e], -Dq[e]);
       }
       dv_acc[u] = mfma16(bf4(pz), gc[0], dv_acc[u]);  // (P∘Z)^T dO
       const s4v dsb = bf4(ds);
       dk_acc[u] = mfma16(dsb, qc[0], dk_acc[u]);  // dS^T Q
       // dS with the key on the k side: Tb[u][query][key] -> lane (r, q) reads row r, keys 4q..4q+3
+      // (measured: an 8-byte [key][query] row store read back with tr_col spilled at this
+      // kernel's 168-VGPR budget)
       const bf4v dh = __builtin_bit_cast(bf4v, dsb);
 #pragma unroll
       for (int e = 0; e < 4; ++e) Tb[u * 16 * TPB + (4 * q + e) * TPB + r] = dh[e];
@@ -1267,7 +1345,7 @@ static bool long_bf16_ok(int hd, int L, int B, int H, int flags) {
 
 extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out, float* lse,
                            int B, int L, int d, int H, float scale, float p, const int64_t* key,
-                           int site, int flags, void* stream) {
+                           int site, int flags, void* stream, uint16_t* zbits) {
   RS_CHECK_ARG(qkv && key_pad && out && lse, "rs_attn_fwd: null pointer");
   RS_CHECK_ARG(B >= 0 && L >= 1 && H >= 1 && d % H == 0, "rs_attn_fwd: bad shape");
   RS_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || key), "rs_attn_fwd: bad dropout p=%f", p);
@@ -1288,7 +1366,9 @@ extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out,
     const bool qb = (flags & RS_ATTN_QKV_BF16) != 0;
 #define RS_AF(NTV)                                                                                  \
   if (nt == NTV) {                                                                                  \
-    if (qb && p > 0.f) attn_fwd_bf16_kernel<NTV, true, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
+    if (qb && p > 0.f && zbits) attn_fwd_bf16_kernel<NTV, true, true, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site, zbits); \
+    else if (bf && !qb && p > 0.f && zbits) attn_fwd_bf16_kernel<NTV, true, false, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site, zbits); \
+    else if (qb && p > 0.f) attn_fwd_bf16_kernel<NTV, true, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
     else if (qb) attn_fwd_bf16_kernel<NTV, false, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
     else if (bf && p > 0.f) attn_fwd_bf16_kernel<NTV, true, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
     else if (bf) attn_fwd_bf16_kernel<NTV, false, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, lse, B, L, d, H, scale, p, key, site); \
@@ -1327,7 +1407,7 @@ extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out,
 extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float* out,
                            const float* dout, const float* lse, float* dqkv, int B, int L, int d,
                            int H, float scale, float p, const int64_t* key, int site, int flags,
-                           void* stream) {
+                           void* stream, const uint16_t* zbits) {
   RS_CHECK_ARG(qkv && key_pad && out && dout && lse && dqkv, "rs_attn_bwd: null pointer");
   RS_CHECK_ARG(B >= 0 && L >= 1 && H >= 1 && d % H == 0, "rs_attn_bwd: bad shape");
   RS_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || key), "rs_attn_bwd: bad dropout p=%f", p);
@@ -1349,7 +1429,9 @@ extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float
     const bool qb = (flags & RS_ATTN_QKV_BF16) != 0;
 #define RS_AB(NTV)                                                                                  \
   if (nt == NTV) {                                                                                  \
-    if (qb && p > 0.f) attn_bwd_bf16_kernel<NTV, true, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
+    if (qb && p > 0.f && zbits) attn_bwd_bf16_kernel<NTV, true, true, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site, zbits); \
+    else if (bf && !qb && p > 0.f && zbits) attn_bwd_bf16_kernel<NTV, true, false, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site, zbits); \
+    else if (qb && p > 0.f) attn_bwd_bf16_kernel<NTV, true, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
     else if (qb) attn_bwd_bf16_kernel<NTV, false, true><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
     else if (bf && p > 0.f) attn_bwd_bf16_kernel<NTV, true, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \
     else if (bf) attn_bwd_bf16_kernel<NTV, false, false><<<g4, 256, 0, st>>>(qkv, key_pad, out, dout, lse, dqkv, B, L, d, H, scale, p, key, site); \

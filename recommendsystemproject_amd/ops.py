@@ -248,19 +248,47 @@ def _attn_flags(qkv):
     return precision.gemm_flags() | (_hip.RS_ATTN_QKV_BF16 if qkv.dtype == torch.bfloat16 else 0)
 
 
+def _zbits_words(B, L, d, H, p, flags):
+    """uint16 words of rs_attn_fwd's saved dropout keep bits (include/rsys_hip.h): the bf16 MFMA
+    path with L <= 64 and p > 0 (the dispatch condition of attention.hip), else 0."""
+    if not (p > 0 and flags & _hip.RS_GEMM_BF16 and d // H == 16 and L <= 64 and B * H * L * L < 2 ** 32
+            and not os.environ.get('RSYS_ATTN_VALU') and not os.environ.get('RSYS_ATTN_NO_ZBITS')):
+        return 0
+    return B * H * ((L + 15) // 16) * 64
+
+
 def attn_fwd(qkv, key_pad, B, L, d, H, p=0.0, key=None, site=0):
+    """-> out [B*L, d], lse [B*H*L]. Where the kernel saves its dropout keep bits for the backward
+    (_zbits_words), they live in lse's storage past its B*H*L floats, so whoever keeps lse for
+    attn_bwd keeps them too; an lse without that tail makes attn_bwd draw them again."""
     out = torch.empty(B * L, d, device=qkv.device, dtype=torch.float32)
-    lse = torch.empty(B * H * L, device=qkv.device, dtype=torch.float32)
+    flags = _attn_flags(qkv)
+    n, zw = B * H * L, _zbits_words(B, L, d, H, p, flags)
+    if zw:
+        buf = torch.empty(n + (zw + 1) // 2 + 4, device=qkv.device, dtype=torch.float32)
+        lse, zb = buf[:n], _zbits_ptr(buf, n)
+    else:
+        lse, zb = torch.empty(n, device=qkv.device, dtype=torch.float32), None
     call('rs_attn_fwd', P(qkv), P(key_pad), P(out), P(lse), B, L, d, H,
-         float((d // H) ** -0.5), float(p), P(key), site, _attn_flags(qkv), stream())
+         float((d // H) ** -0.5), float(p), P(key), site, flags, stream(), zb)
     return out, lse
+
+
+def _zbits_ptr(lse, n):
+    return (lse.data_ptr() + 4 * n + 15) // 16 * 16  # 16-byte aligned start past the lse floats
 
 
 def attn_bwd(qkv, key_pad, out, dout, lse, B, L, d, H, p=0.0, key=None, site=0):
     """dqkv has qkv's storage dtype (bf16 with RS_ATTN_QKV_BF16)."""
     dqkv = torch.empty(B * L, 3 * d, device=qkv.device, dtype=qkv.dtype)
+    flags = _attn_flags(qkv)
+    n, zw = B * H * L, _zbits_words(B, L, d, H, p, flags)
+    zb = None
+    if zw and lse.storage_offset() == 0 and lse.numel() == n and \
+            lse.untyped_storage().nbytes() >= 4 * (n + (zw + 1) // 2 + 4):
+        zb = _zbits_ptr(lse, n)  # attn_fwd's tail (its docstring)
     call('rs_attn_bwd', P(qkv), P(key_pad), P(out), P(dout), P(lse), P(dqkv), B, L, d, H,
-         float((d // H) ** -0.5), float(p), P(key), site, _attn_flags(qkv), stream())
+         float((d // H) ** -0.5), float(p), P(key), site, flags, stream(), zb)
     return dqkv
 
 

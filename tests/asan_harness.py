@@ -68,7 +68,7 @@ expect_fail('rs_tower_wgrad', 9, 4096, C.addressof(Ns), C.addressof(Ks), C.addre
 # assorted entry points with bad shapes
 expect_fail('rs_gemm_f32', 0, 0, -1, 4, 4, 1.0, None, 4, None, 4, 0.0, None, 4, 0, None, None,
             0, 0, 0.0, None, 0, 0, None, 1, None, None)
-expect_fail('rs_attn_fwd', 1, 1, 1, 1, 2, 5, 60, 4, 1.0, 0.0, None, 0, 0, None)
+expect_fail('rs_attn_fwd', 1, 1, 1, 1, 2, 5, 60, 4, 1.0, 0.0, None, 0, 0, None, None)
 expect_fail('rs_tower_stats', None, 1, 1, 1, None, None, None, None, None, None, None, None, 0.1, 1e-5, None, None,
             None)
 print('asan harness ok')

@@ -46,7 +46,7 @@ def test_bad_arguments_report_errors_without_gpu():
         _hip.call('rs_gemm_f32', 0, 0, -1, 4, 4, 1.0, None, 4, None, 4, 0.0, None, 4, 0, None, None,
                   0, 0, 0.0, None, 0, 0, None, 1, None, None)
     with pytest.raises(_hip.HipError, match='head_dim'):
-        _hip.call('rs_attn_fwd', 1, 1, 1, 1, 2, 5, 60, 4, 1.0, 0.0, None, 0, 0, None)
+        _hip.call('rs_attn_fwd', 1, 1, 1, 1, 2, 5, 60, 4, 1.0, 0.0, None, 0, 0, None, None)
 
 
 @pytest.mark.parametrize('name', CONFIGS)

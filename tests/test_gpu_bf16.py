@@ -449,6 +449,29 @@ def test_bf16_attention_dropout_matches_fp32_masks(L, bf16_mode):
     assert (g16 - g32).abs().max().item() < 3e-2 * g32.abs().max().item()
 
 
+@pytest.mark.parametrize('L', [50, 33, 64, 7])
+def test_bf16_attention_saved_keep_bits(L, bf16_mode):
+    """L <= 64: the forward saves its dropout keep bits in lse's storage tail (ops.attn_fwd) and
+    the backward reads them instead of hashing again -- the same draws, so dqkv is bitwise the
+    one an lse without the tail (re-drawn) gives; fp32 and bf16 qkv storage, odd and even L."""
+    B, d, H, p = 5, 64, 4, 0.3
+    lens = torch.randint(1, L + 1, (B,))
+    seq = (torch.arange(L)[None, :] < lens[:, None]).long().to(DEV)
+    key_pad, _ = ops.seq_mask(seq, 0)
+    key = torch.tensor([123, 4], dtype=torch.int64, device=DEV)
+    dout = rnd(B * L, d, seed=16)
+    q32 = rnd(B * L, 3 * d, seed=15)
+    for q in (q32, q32.to(torch.bfloat16)):
+        assert ops._zbits_words(B, L, d, H, p, ops._attn_flags(q)) > 0
+        o, lse = ops.attn_fwd(q, key_pad, B, L, d, H, p, key, 7)
+        assert lse.numel() == B * H * L and lse.untyped_storage().nbytes() > 4 * lse.numel()
+        g_bits = ops.attn_bwd(q, key_pad, o, dout, lse, B, L, d, H, p, key, 7)
+        g_hash = ops.attn_bwd(q, key_pad, o, dout, lse.clone(), B, L, d, H, p, key, 7)
+        assert torch.equal(g_bits, g_hash)
+        o2, _ = ops.attn_fwd(q, key_pad, B, L, d, H, p, key, 8)  # another site: other draws
+        assert not torch.equal(o, o2)
+
+
 def _ce_ref(U, I, ids, H, T, gout=1.0):
     """compute_loss (TwoTowerModel.py:81-140) in float64 on bf16-rounded U, I (the fused kernel's
     products); hard-negative logits from the fp32 embeddings as in the kernel."""
