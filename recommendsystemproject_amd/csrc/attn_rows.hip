@@ -34,6 +34,33 @@ __device__ __forceinline__ float wmax(float v) {
 }
 __device__ __forceinline__ float r16(float x) { return (float)(__bf16)x; }
 
+// Wave totals of HD per-lane channels, transposed: each butterfly step halves the channels a lane
+// carries (it keeps the half its partner does not), so HD + log2(64 / HD) - 1 shuffles replace
+// wsum's 6 HD (96 at head_dim 16). Lane l ends with the total of channel l >> RowShift<HD>.
+template <int HD>
+struct RowShift { static constexpr int v = HD == 8 ? 3 : (HD == 16 ? 2 : (HD == 32 ? 1 : 0)); };
+template <int HD>
+__device__ __forceinline__ float wsum_t(float (&x)[HD], int lane) {
+  constexpr int NS = 6 - RowShift<HD>::v;  // log2(HD) halving steps over lane bits 5, 4, ...
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int M = 32 >> s, h = HD >> (s + 1);
+    const bool hi = (lane & M) != 0;
+#pragma unroll
+    for (int j = 0; j < h; ++j) {
+      float a = x[j], b = x[j + h];
+      // (empty asm: keeps the two selects on values -- folded into one select of the array index,
+      // they became a compare/select chain over all HD registers per access)
+      asm("" : "+v"(a), "+v"(b));
+      x[j] = (hi ? b : a) + __shfl_xor(hi ? a : b, M, 64);
+    }
+  }
+  float v = x[0];
+#pragma unroll
+  for (int s = 0; s < RowShift<HD>::v; ++s) v += __shfl_xor(v, (32 / HD) >> s, 64);
+  return v;
+}
+
 // HD consecutive elements of a qkv row slice, fp32 or bf16 storage (HD % 4 == 0)
 template <int HD>
 __device__ __forceinline__ void ldrow(const float* p, float (&x)[HD]) {
@@ -125,12 +152,10 @@ __global__ __launch_bounds__(256) void attn_rows_fwd_kernel(
   }
   l = wsum(l);
   const float inv = 1.f / l;
-#pragma unroll
-  for (int c = 0; c < HD; ++c) o[c] = wsum(o[c]) * inv;
-  if (lane == 0) {
-    strow<HD>(out + (int64_t)b * d + h * HD, o);
-    lse[bh] = m + logf(l);
-  }
+  const float oc = wsum_t<HD>(o, lane) * inv;  // channel lane >> RowShift
+  constexpr int SH = RowShift<HD>::v;
+  if ((lane & ((1 << SH) - 1)) == 0) out[(int64_t)b * d + h * HD + (lane >> SH)] = oc;
+  if (lane == 0) lse[bh] = m + logf(l);
 }
 
 template <int HD, bool DROP, bool BF, bool QB>
@@ -185,6 +210,14 @@ __global__ __launch_bounds__(256) void attn_rows_bwd_kernel(
   float dq[HD];
 #pragma unroll
   for (int c = 0; c < HD; ++c) dq[c] = 0.f;
+  // H == 4 (the encoder's four heads, d = 4 HD <= 64): the workgroup's waves are the four heads of
+  // sample b, so each chunk's rows of dqkv are staged in LDS and the workgroup stores them as
+  // whole rows (3d contiguous elements, 16-byte stores) -- per lane, the 8-byte pieces of 64
+  // different rows per store instruction were the kernel's cost (C5: 0.175 ms per step)
+  constexpr bool CO = HD <= 16;
+  constexpr int SP = 12 * HD + 16 / (int)sizeof(QT);  // staged row pitch: 3d elements + 16 B
+  __shared__ __attribute__((aligned(16))) QT St[CO ? 64 : 1][CO ? SP : 1];
+  const bool coop = CO && H == 4;  // uniform over the workgroup (B H is a multiple of 4)
 #pragma unroll
   for (int ch = 0; ch < kMaxChunks; ++ch) {
     const int j = ch * 64 + lane;
@@ -201,15 +234,36 @@ __global__ __launch_bounds__(256) void attn_rows_bwd_kernel(
         dv[c] = pz * g[c];
         zero[c] = 0.f;
       }
-      QT* row = dbase + (int64_t)j * ld;
-      if (j != i) strow<HD>(row, zero);  // dead query rows: zero gradient
-      strow<HD>(row + d, dk_);
-      strow<HD>(row + 2 * d, dv);
+      if (coop) {
+        QT* sr = &St[lane][h * HD];
+        strow<HD>(sr, zero);  // dead query rows: zero gradient (the selected row's is not stored)
+        strow<HD>(sr + d, dk_);
+        strow<HD>(sr + 2 * d, dv);
+      } else {
+        QT* row = dbase + (int64_t)j * ld;
+        if (j != i) strow<HD>(row, zero);  // dead query rows: zero gradient
+        strow<HD>(row + d, dk_);
+        strow<HD>(row + 2 * d, dv);
+      }
+    }
+    if (CO && coop && ch < nch) {
+      __syncthreads();
+      constexpr int CPR = 12 * HD * (int)sizeof(QT) / 16;  // 16-byte chunks per row
+      constexpr int QCH = CPR / 3;                          // ... of its dQ part
+      const int r0 = ch * 64, nr = min(64, L - r0);
+      QT* orow = reinterpret_cast<QT*>(dqkv_) + ((int64_t)b * L + r0) * ld;
+      for (int e = threadIdx.x; e < nr * CPR; e += 256) {
+        const int r = e / CPR, kc = e - r * CPR;
+        if (r0 + r == i && kc < QCH) continue;  // the selected row's dQ: stored below
+        *reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(orow + (int64_t)r * ld) + 16 * kc) =
+            *reinterpret_cast<const uint4*>(reinterpret_cast<const unsigned char*>(&St[r][0]) + 16 * kc);
+      }
+      __syncthreads();
     }
   }
-#pragma unroll
-  for (int c = 0; c < HD; ++c) dq[c] = wsum(dq[c]) * scale;
-  if (lane == 0) strow<HD>(dbase + (int64_t)i * ld, dq);
+  const float dqc = wsum_t<HD>(dq, lane) * scale;  // channel lane >> RowShift
+  constexpr int SH = RowShift<HD>::v;
+  if ((lane & ((1 << SH) - 1)) == 0) dbase[(int64_t)i * ld + (lane >> SH)] = (QT)dqc;
 }
 
 }  // namespace

@@ -405,7 +405,7 @@ def _bf16_attention_ref(qkv, key_pad, dout, B, L, d, H):
 def test_bf16_attention(B, L, bf16_mode):
     d, H = 64, 4
     qkv = rnd(B * L, 3 * d, seed=11)
-    lens = torch.randint(1, L + 1, (B,))
+    lens = torch.randint(1, L + 1, (B,), generator=torch.Generator().manual_seed(L))  # fixed padding
     seq = (torch.arange(L)[None, :] < lens[:, None]).long().to(DEV)
     key_pad, _ = ops.seq_mask(seq, 0)
     dout = rnd(B * L, d, seed=12)
@@ -414,11 +414,12 @@ def test_bf16_attention(B, L, bf16_mode):
     ro, rd = _bf16_attention_ref(qkv, key_pad, dout, B, L, d, H)
     # an fp32 value next to a bf16 rounding boundary may round the other way than in float64:
     # single-ulp (2^-8) flips of a probability bound the worst element; the mean stays tight
+    # (1.5e-4: with unseeded padding a draw at L = 100 measured 1.04e-4; a wrong product is ~1e-2)
     for a, b_ in ((out, ro), (dqkv, rd)):
         sc = b_.abs().max().item()
         err = (a - b_).abs()
         assert err.max().item() < 5e-3 * sc, (err.max().item(), sc)
-        assert err.mean().item() < 1e-4 * sc, (err.mean().item(), sc)
+        assert err.mean().item() < 1.5e-4 * sc, (err.mean().item(), sc)
     # and it is not the fp32 kernel
     precision.set_compute_dtype('fp32')
     out32, _ = ops.attn_fwd(qkv, key_pad, B, L, d, H)

@@ -35,7 +35,8 @@ def _mask(B, L, seed):
 
 
 @pytest.mark.parametrize('L,d,H,p', [(50, 64, 4, 0.0), (50, 64, 4, 0.1), (7, 32, 4, 0.0),
-                                     (1, 64, 4, 0.0), (200, 64, 4, 0.1), (33, 64, 2, 0.0)])
+                                     (1, 64, 4, 0.0), (200, 64, 4, 0.1), (33, 64, 2, 0.0),
+                                     (50, 64, 1, 0.1), (70, 64, 8, 0.1)])
 def test_attn_rows_matches_full_fp32(L, d, H, p):
     B = 37
     qkv = rnd(B * L, 3 * d, seed=1)
