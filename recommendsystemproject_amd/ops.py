@@ -285,8 +285,8 @@ def attn_bwd(qkv, key_pad, out, dout, lse, B, L, d, H, p=0.0, key=None, site=0):
     n, zw = B * H * L, _zbits_words(B, L, d, H, p, flags)
     zb = None
     if zw and lse.storage_offset() == 0 and lse.numel() == n and \
-            lse.untyped_storage().nbytes() >= 4 * (n + (zw + 1) // 2 + 4):
-        zb = _zbits_ptr(lse, n)  # attn_fwd's tail (its docstring)
+            lse.untyped_storage().nbytes() == 4 * (n + (zw + 1) // 2 + 4):
+        zb = _zbits_ptr(lse, n)  # attn_fwd's tail (its docstring; exactly its allocation's size)
     call('rs_attn_bwd', P(qkv), P(key_pad), P(out), P(dout), P(lse), P(dqkv), B, L, d, H,
          float((d // H) ** -0.5), float(p), P(key), site, flags, stream(), zb)
     return dqkv
