@@ -796,6 +796,9 @@ __global__ __launch_bounds__(1024) void ffn_wgrad_reduce_kernel(const float* __r
 int wgrad_fused_grid(int M) {
   const int chunks = cdiv(M, WG_ROWS);
   int g = cdiv(chunks, 4);  // >= 4 chunks per workgroup: the partials stay well below the reads
+  // small batches (the last encoder layer's B rows: 64 chunks at B = 4096) ran 16 workgroups of 4
+  // chunks one after another; one chunk per workgroup there, the partials (64 x 130 KB) are cheap
+  if (g < 64) g = chunks < 64 ? chunks : 64;
   return g < 1 ? 1 : (g > 256 ? 256 : g);
 }
 
@@ -813,6 +816,9 @@ size_t bwd_ln2_lds(int F) { return bwd_lds(F, false) + (size_t)D * 4 + (size_t)8
 int grid_for(int M, size_t lds) {
   const int per_cu = lds > 80 * 1024 ? 1 : 2;
   int bx = cdiv(M / 16, 16);
+  // small batches (the last encoder layer's B rows): one 16-row group per wave instead of 16 per
+  // workgroup, while that stays under one workgroup per CU (B = 4096: 32 workgroups, not 16)
+  if (bx < 256) bx = cdiv(M / 16, 8) < 256 ? cdiv(M / 16, 8) : 256;
   if (bx > 256 * per_cu) bx = 256 * per_cu;
   return bx < 1 ? 1 : bx;
 }
