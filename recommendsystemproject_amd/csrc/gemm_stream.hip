@@ -862,18 +862,15 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
   int g = blockIdx.x * 8 + wave;
   typedef const __attribute__((address_space(1))) floatx4* gptr4;
   typedef const __attribute__((address_space(1))) bf16x8* gptrb8;
-  // PF row groups of A in flight per wave (PF - 1 ahead of the one being consumed): one group
-  // (4 KB at K = 64) per wave at two waves per SIMD kept too few bytes in flight for HBM
-  constexpr int PF = (ABF || KC <= 2) ? 3 : 2;
-  floatx4 araw[PF][ABF ? 1 : KC][4];
-  bf16x8 abraw[PF][ABF ? KC : 1][2];
-  auto load_raw = [&](int gg, floatx4 (*dst)[4], bf16x8 (*dstb)[2]) {
+  floatx4 araw[ABF ? 1 : KC][4];
+  bf16x8 abraw[ABF ? KC : 1][2];
+  auto load_raw = [&](int gg, floatx4 (*dst)[4]) {
     if constexpr (ABF) {
       const __bf16* row = reinterpret_cast<const __bf16*>(a.A) + (int64_t)(gg * 16 + r) * a.lda + 16 * q;
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
-        dstb[c][0] = *(gptrb8)(row + 64 * c);
-        dstb[c][1] = *(gptrb8)(row + 64 * c + 8);
+        abraw[c][0] = *(gptrb8)(row + 64 * c);
+        abraw[c][1] = *(gptrb8)(row + 64 * c + 8);
       }
     } else {
       const float* row = a.A + (int64_t)(gg * 16 + r) * a.lda + 16 * q;
@@ -885,11 +882,7 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
                                                                       : floatx4{0.f, 0.f, 0.f, 0.f};
     }
   };
-#pragma unroll
-  for (int i = 0; i < PF - 1; ++i) {
-    const int gi = g + i * stride;
-    if (g < groups) load_raw(gi < groups ? gi : g, araw[i], abraw[i]);
-  }
+  if (g < groups) load_raw(g, araw);
   constexpr bool EPRE = !LN && (EPI & (RS_EPI_AUX_MASK | kEpiBeta)) != 0;
   for (; g < groups; g += stride) {
     const int m = g * 16 + r;
@@ -908,34 +901,18 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
         else epre[t] = *(gptr4)(a.C + (int64_t)m * a.ldc + n0);
       }
     }
-    // the group PF - 1 ahead goes out first (no branch: clamped to this group past the end)
-    {
-      const int gn = g + (PF - 1) * stride;
-      load_raw(gn < groups ? gn : g, araw[PF - 1], abraw[PF - 1]);
-    }
     bf16x8 af[KC][2];
 #pragma unroll
     for (int c = 0; c < KC; ++c) {
       if constexpr (ABF) {
-        af[c][0] = abraw[0][c][0];
-        af[c][1] = abraw[0][c][1];
+        af[c][0] = abraw[c][0];
+        af[c][1] = abraw[c][1];
       } else {
-        af[c][0] = cvt8(araw[0][c][0], araw[0][c][1]);
-        af[c][1] = cvt8(araw[0][c][2], araw[0][c][3]);
+        af[c][0] = cvt8(araw[c][0], araw[c][1]);
+        af[c][1] = cvt8(araw[c][2], araw[c][3]);
       }
     }
-#pragma unroll
-    for (int i = 0; i < PF - 1; ++i) {
-#pragma unroll
-      for (int c = 0; c < (ABF ? 1 : KC); ++c)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) araw[i][c][u] = araw[i + 1][c][u];
-#pragma unroll
-      for (int c = 0; c < (ABF ? KC : 1); ++c) {
-        abraw[i][c][0] = abraw[i + 1][c][0];
-        abraw[i][c][1] = abraw[i + 1][c][1];
-      }
-    }
+    load_raw(g + stride < groups ? g + stride : g, araw);  // next group, no branch
     floatx4 lnacc[LN ? NT : 1];
     constexpr int TG = NT % 4 == 0 ? 4 : (NT % 2 == 0 ? 2 : 1);
 #pragma unroll
