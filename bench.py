@@ -13,6 +13,7 @@ Prints ONE JSON line (rank 0).
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import sys
@@ -27,6 +28,7 @@ import torch.distributed as dist
 import yaml
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+T_START = time.time()
 sys.path.insert(0, ROOT)
 
 from recommendsystemproject_amd import dist as rdist  # noqa: E402
@@ -104,7 +106,7 @@ def parse():
             # (credited) and bf16, C3 with Zipf(1.05) ids, C5 with 10 hard negatives; N > 1 (the
             # scaling runs): C3 data-parallel = configs[3] (C4), both precisions
             one = int(os.environ.get('WORLD_SIZE', '1')) == 1
-            a.extra = 'c3:fp32,c3:bf16' + (',c3_zipf:fp32,c5:bf16' if one else '')
+            a.extra = 'c3:fp32,c3:bf16' + (',c3_zipf:fp32,c5:fp32,c5:bf16' if one else '')
         else:
             a.extra = ''
     return a
@@ -200,8 +202,8 @@ def cpu_baseline(cfg, seconds, B, min_steps=10, legs=('config', '0')):
     cfg, capped = _cap_vocab(cfg, CPU_VOCAB_CAP)
     rate, n, el = _oracle_rate(cfg, seconds / len(legs), B, 'config', min_steps)
     rate0 = n0 = el0 = None
-    if '0' in legs:
-        rate0, n0, el0 = _oracle_rate(cfg, seconds / len(legs), B, '0', min_steps)
+    if '0' in legs:  # the p = 0 leg: half the steps
+        rate0, n0, el0 = _oracle_rate(cfg, seconds / len(legs), B, '0', max(3, min_steps // 2))
     model = None
     try:
         for line in open('/proc/cpuinfo'):
@@ -217,15 +219,17 @@ def cpu_baseline(cfg, seconds, B, min_steps=10, legs=('config', '0')):
                       (f'; tables capped at {CPU_VOCAB_CAP:,} rows (host memory)' if capped else '') +
                       f'; {torch.get_num_threads()} torch threads of {os.cpu_count()} host cores (the '
                       f'GPU box\'s CPU share is 16 threads)',
-            'threads': torch.get_num_threads(), 'nproc': os.cpu_count(), 'cpu_model': model}
+            'threads': torch.get_num_threads(), 'nproc': os.cpu_count(), 'cpu_model': model, 'steps': n,
+            'seconds': round(el, 1), 'batch': B}
 
 
 def cpu_worker(spec_path, out_path):
-    """The CPU baselines of one bench run, in a child process started before the GPU is touched:
-    it runs on the host cores while the parent times the GPU workloads, so the samples can be
-    long (>= 10 steps per leg) without lengthening the run. Writes {key: cpu_baseline} as each
-    finishes."""
+    """The CPU baselines of one bench run, in a child process started before the GPU is touched
+    (a plain CPU python: it never initialises HIP). It waits for the parent's 'go' on stdin,
+    sent once every GPU workload has been timed, so the two legs never share the host cores.
+    Writes {key: cpu_baseline} as each finishes."""
     spec = json.load(open(spec_path))
+    sys.stdin.readline()  # the parent's go (or EOF: the parent is gone, run anyway)
     res = {}
     for job in spec['jobs']:
         cfg = yaml.safe_load(open(os.path.join(ROOT, 'configs', f"{job['config']}.yaml")))
@@ -249,8 +253,18 @@ def start_cpu_worker(jobs):
     json.dump({'jobs': jobs}, open(spec, 'w'))
     env = dict(os.environ, HIP_VISIBLE_DEVICES='', CUDA_VISIBLE_DEVICES='', ROCR_VISIBLE_DEVICES='')
     proc = subprocess.Popen([sys.executable, os.path.abspath(__file__), '--cpu-worker', spec, out], env=env,
-                            stdout=subprocess.DEVNULL, stderr=open(os.path.join(d, 'err.log'), 'w'))
+                            stdin=subprocess.PIPE, stdout=subprocess.DEVNULL,
+                            stderr=open(os.path.join(d, 'err.log'), 'w'))
     return proc, out
+
+
+def release_cpu_worker(proc):
+    """The GPU timing is over: the CPU baselines may start."""
+    try:
+        proc.stdin.write(b'go\n')
+        proc.stdin.close()
+    except OSError:
+        pass
 
 
 def collect_cpu_worker(proc, out, timeout):
@@ -263,6 +277,7 @@ def collect_cpu_worker(proc, out, timeout):
         except Exception:
             pass
         if time.time() - t0 > timeout:
+            print('[bench] CPU baselines timed out', file=sys.stderr, flush=True)
             proc.kill()
             proc.wait()
             break
@@ -529,6 +544,9 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
         allreduce()
         opt_step()
     torch.cuda.synchronize()
+    if rank == 0:
+        print(f'[bench] {name} {dtype}: {n_warm} eager warm-up steps done ({time.time() - T_START:.0f} s)',
+              file=sys.stderr, flush=True)
     if args.pmc_bracket:
         target = args.pmc_bracket
         if target == 'auto':
@@ -591,6 +609,8 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
                     allreduce()
                     opt_step()
             graphs = (g1, g2, loss_static)
+            if rank == 0:
+                print(f'[bench] {name} {dtype}: step captured', file=sys.stderr, flush=True)
         except Exception as e:  # eager fallback keeps the same kernels
             print(f'[bench] graph capture failed ({e!r}); running eagerly', file=sys.stderr)
             graphs = None
@@ -709,8 +729,19 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
     gather_roof = {}
     # the table gradient = the scatter of ordinary tables (rs_gather_bwd) + the sorted segment
     # sum of the large ones (rs_segsum); the sort itself runs in the forward (rs_lookup_sort)
-    groups = {'rs_gather_fwd': ('rs_gather_fwd', 'rs_gather_fwd_lazy'), 'table_grad': ('rs_gather_bwd', 'rs_segsum')}
+    # catchup_gather: the lazy tables' forward unit -- the catch-up that brings a call's distinct rows
+    # current, then the gather that reads them (priced by their own algorithmic bytes, both kernels'
+    # event time)
+    groups = {'rs_gather_fwd': ('rs_gather_fwd', 'rs_gather_fwd_lazy'), 'table_grad': ('rs_gather_bwd', 'rs_segsum'),
+              'catchup_gather': ('rs_sorted_catchup', 'rs_gather_fwd', 'rs_gather_fwd_lazy')}
+    if lazy_rows:
+        summ = dict(summ)
+        if 'rs_sorted_catchup' in summ:  # priced per distinct row (LAZY_ROW_BYTES), as optimizer_roofline
+            summ['rs_sorted_catchup'] = dict(summ['rs_sorted_catchup'],
+                                             bytes=LAZY_ROW_BYTES['rs_sorted_catchup'](lazy_rows))
     for k, members in groups.items():
+        if k == 'catchup_gather' and 'rs_sorted_catchup' not in summ:
+            continue
         ms = [summ[m] for m in members if m in summ]
         g = {'ms': sum(x['ms'] for x in ms), 'bytes': sum(x['bytes'] for x in ms)}
         if g['ms'] > 0:
@@ -797,9 +828,9 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
 def _cpu_jobs(args):
     """The CPU baselines of this run (rank 0, N = 1): the primary workload (dropout as configured
     and a p = 0 leg), each extra workload's config once (one leg), and C1 (BASELINE configs[0]).
-    >= 10 steps per leg (C5: 2 steps -- its oracle step at L = 200 with 10M-row tables takes tens
-    of seconds on the host). C3-Zipf reuses C3's: the oracle's dense step costs the same for any
-    ids. The legs run one after another in one child process, beside the GPU timing (~3 min)."""
+    >= 10 steps per leg (the p = 0 leg 5; C5 5 -- its oracle step at L = 200 with 10M-row tables
+    takes ~25 s on the host). C3-Zipf reuses C3's: the oracle's dense step costs the same for any
+    ids. The legs run one after another in one child process, after the GPU timing (~4 min)."""
     jobs, seen = [], set()
 
     def add(key, config, primary=False):
@@ -811,7 +842,7 @@ def _cpu_jobs(args):
         big = config == 'c5'
         jobs.append({'key': key, 'config': config, 'zipf': args.zipf if primary else None, 'batch': B,
                      'seconds': 5.0 if big else args.cpu_baseline_seconds,
-                     'min_steps': 2 if big else 10, 'legs': ['config', '0'] if primary and not big else ['config']})
+                     'min_steps': 5 if big else 10, 'legs': ['config', '0'] if primary and not big else ['config']})
     add(args.config, args.config, primary=True)
     for ex in [e for e in (args.extra or '').split(',') if e]:
         nm = ex.partition(':')[0]
@@ -820,7 +851,65 @@ def _cpu_jobs(args):
     return jobs
 
 
+def _frac(d, *path):
+    for k in path:
+        if not isinstance(d, dict) or d.get(k) is None:
+            return None
+        d = d[k]
+    return d
+
+
+def _cpu_short(c):
+    if not c or 'error' in c:
+        return c
+    return {k: c.get(k) for k in ('value', 'unit', 'cores', 'kind', 'threads', 'nproc', 'steps', 'seconds',
+                                  'batch', 'value_p0', 'sample')}
+
+
+def _extra_short(r):
+    if 'error' in r:
+        return {'error': r['error'][:200]}
+    g = r.get('gather_roofline') or {}
+    return {'value': r['value'], 'ms_per_step': r['ms_per_step'], 'dtype': r['dtype'],
+            'workload': r['config']['workload'].split(':')[0],
+            'roofline_frac': _frac(r, 'roofline', 'frac'), 'roofline_kernel': _frac(r, 'roofline', 'kernel'),
+            'gather_frac': _frac(g, 'rs_gather_fwd', 'frac'),
+            'catchup_gather_frac': _frac(g, 'catchup_gather', 'frac'),
+            'step_roofline_frac': _frac(r, 'step_roofline', 'frac'),
+            'cpu_baseline_value': _frac(r, 'cpu_baseline', 'value')}
+
+
+def compact_line(out):
+    """The stdout line: the contract's fields, the dominant kernel's roofline without its PMC
+    detail, the CPU baseline's numbers, and per extra workload its headline numbers only (the
+    whole record is the stderr 'bench_detail' object). Kept well under 8 KB."""
+    keys = ('metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup', 'ms_per_step', 'higher_is_better', 'scaling',
+            'vs_baseline', 'dtype', 'data')
+    line = {k: out[k] for k in keys}
+    cfg = out['config']
+    line['config'] = {k: cfg.get(k) for k in ('workload', 'global_batch', 'per_gpu_batch', 'seq_len', 'dropout',
+                                             'parallelism', 'hip_graph', 'ids', 'hard_negatives',
+                                             'resident_batches', 'row_sharded_tables')}
+    line['roofline'] = {k: v for k, v in out['roofline'].items() if k not in ('traffic_detail', 'valu_exp')}
+    g = out.get('gather_roofline') or {}
+    line['gather_roofline'] = {k: {'frac': v.get('frac'), 'achieved': v.get('achieved'), 'ms_per_step': v.get('ms_per_step'),
+                                   'traffic': v.get('traffic')} for k, v in g.items()}
+    line['step_roofline'] = out.get('step_roofline')
+    line['cpu_baseline'] = _cpu_short(out.get('cpu_baseline'))
+    c1 = out.get('c1_cpu_baseline')
+    line['c1_cpu_baseline'] = {'value': c1.get('value'), 'steps': c1.get('steps'), 'batch': c1.get('batch')} \
+        if c1 and 'error' not in c1 else c1
+    pk = out.get('peaks_measured') or {}
+    line['peaks_measured'] = {k: pk.get(k) for k in ('hbm_copy_GBs', 'bf16_mfma_TFLOPs')}
+    if out.get('extra'):
+        line['extra'] = {k: _extra_short(v) for k, v in out['extra'].items()}
+    line['wall_s'] = out.get('wall_s')
+    line['detail'] = 'stderr: {"bench_detail": ...}'
+    return line
+
+
 def main():
+    faulthandler.enable()  # a crash prints the Python stack of every thread
     args = parse()
     if args.cpu_worker:
         cpu_worker(*args.cpu_worker)
@@ -889,9 +978,13 @@ def main():
                 extras[key]['note'] = (f'{ex_dtype} compute mode, beside the fp32 entry "{name}" (the '
                                        "reference's precision)")
     if worker is not None:
-        # the CPU baselines ran beside the GPU timing; C1 = BASELINE configs[0], the reference's
-        # CPU-runnable case (demo schema without the sequence encoder, batch 256)
-        cpu = collect_cpu_worker(*worker, timeout=600)
+        # every GPU workload is timed: the CPU baselines run now, alone on the host cores; C1 =
+        # BASELINE configs[0], the reference's CPU-runnable case (demo schema without the sequence
+        # encoder, batch 256)
+        print(f'[bench] GPU legs done ({time.time() - T_START:.0f} s); CPU baselines next', file=sys.stderr,
+              flush=True)
+        release_cpu_worker(worker[0])
+        cpu = collect_cpu_worker(*worker, timeout=900)
         if rank == 0:
             out['cpu_baseline'] = cpu.get(args.config)
             for key in extras:
@@ -912,7 +1005,11 @@ def main():
                 for k, v in shp[:24]]}), file=sys.stderr)
         if extras:
             out['extra'] = extras
-        print(json.dumps(out))
+        out['wall_s'] = round(time.time() - T_START, 1)
+        # the full record (per-kernel times, every roofline object, PMC traffic details) on stderr;
+        # stdout carries ONE compact line the driver parses (round 4's 23 KB line was not parsed)
+        print(json.dumps({'bench_detail': out}), file=sys.stderr, flush=True)
+        print(json.dumps(compact_line(out)), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 

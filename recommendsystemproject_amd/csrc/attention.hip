@@ -1315,18 +1315,9 @@ int threads_for(int L) {
 using namespace rs;
 
 // bf16 compute mode, head_dim 16, 64 < L <= 256 (fp32 or bf16 qkv): the long-history MFMA kernels
-// RSYS_ATTN_LONG_MIN=N (A/B): the workgroup-per-(b, h) kernels from L > N instead of L > 64
-static int long_min_L() {
-  static const int v = [] {
-    const char* e = getenv("RSYS_ATTN_LONG_MIN");
-    const int x = e ? atoi(e) : 64;
-    return x < 32 ? 32 : (x > 64 ? 64 : x);
-  }();
-  return v;
-}
-
+// (L <= 64 takes the wave-per-(b, h) kernels above them in the dispatch)
 static bool long_bf16_ok(int hd, int L, int B, int H, int flags) {
-  return hd == 16 && L > long_min_L() && L <= 256 && (flags & RS_GEMM_BF16) &&
+  return hd == 16 && L > 64 && L <= 256 && (flags & RS_GEMM_BF16) &&
          (int64_t)B * H * L * L < ((int64_t)1 << 32) && !getenv_flag("RSYS_ATTN_VALU");
 }
 
@@ -1391,7 +1382,7 @@ extern "C" int rs_attn_fwd(const float* qkv, const uint8_t* key_pad, float* out,
   }
     const int nt = (L + 15) / 16;
     const bool qb = (flags & RS_ATTN_QKV_BF16) != 0;
-    RS_AFL(3) RS_AFL(4) RS_AFL(5) RS_AFL(6) RS_AFL(7) RS_AFL(8) RS_AFL(9) RS_AFL(10) RS_AFL(11)
+    RS_AFL(5) RS_AFL(6) RS_AFL(7) RS_AFL(8) RS_AFL(9) RS_AFL(10) RS_AFL(11)
     RS_AFL(12) RS_AFL(13) RS_AFL(14) RS_AFL(15) RS_AFL(16)
 #undef RS_AFL
     RS_CHECK_LAUNCH("rs_attn_fwd long bf16");
@@ -1455,7 +1446,7 @@ extern "C" int rs_attn_bwd(const float* qkv, const uint8_t* key_pad, const float
   }
     const int nt = (L + 15) / 16;
     const bool qb = (flags & RS_ATTN_QKV_BF16) != 0;
-    RS_ABL(3) RS_ABL(4) RS_ABL(5) RS_ABL(6) RS_ABL(7) RS_ABL(8) RS_ABL(9) RS_ABL(10) RS_ABL(11)
+    RS_ABL(5) RS_ABL(6) RS_ABL(7) RS_ABL(8) RS_ABL(9) RS_ABL(10) RS_ABL(11)
     RS_ABL(12) RS_ABL(13) RS_ABL(14) RS_ABL(15) RS_ABL(16)
 #undef RS_ABL
     RS_CHECK_LAUNCH("rs_attn_bwd long bf16");

@@ -104,9 +104,11 @@ class _Agreement(threading.local):
     per-dimension maxima over the ranks and whether any rank's dimension differs."""
 
     def __init__(self):
-        self.table = None   # {(data_ptr, shape): (max dims, ragged)} of this forward's batch
+        self.table = None   # {(data_ptr, shape): (max dims, ragged)} of this forward's batch; dropped
+                            # when the forward ends (end_forward): its keys are allocator addresses
         self.sig = None     # the local shape signature of the last agreed batch
         self.static = False  # the last agreed batch had the same shapes on every rank
+        self.step = False   # a batch was agreed since the last allreduce_gradients (clear_agreement)
         self.local = 0      # local_only() depth: this process steps alone (no collective)
 
 
@@ -144,9 +146,11 @@ def _batch_tensors(b, out):
 
 
 def agree_batch(batch) -> None:
-    """ONE all-reduce per forward (TwoTowerModel.forward) of every batch tensor's shape: the
-    lookup calls of the large tables then take their common shapes from it (agreed_dims) instead of
-    one blocking all-reduce per call. Ranks' batches of equal shapes (the bench's, a loader with
+    """One agreement per forward (TwoTowerModel.forward) of every batch tensor's shape -- a
+    fixed-size header all-reduce (tensor count, total rank: batches of different structure raise
+    before any variable-length collective), then one all-reduce of every dimension: the lookup
+    calls of the large tables take their common shapes from it (agreed_dims, valid until the
+    forward ends: end_forward) instead of one blocking all-reduce per call. Ranks' batches of equal shapes (the bench's, a loader with
     drop_last and equal list lengths) need nothing more; ragged ones (the collate pads each
     batch's lists to its own longest) pad every call to the per-dimension maxima.
     Inside a hipGraph capture nothing can be exchanged: the batch must have the shapes of the last
@@ -162,9 +166,18 @@ def agree_batch(batch) -> None:
                                'of the last eager step, equal on every rank (run one eager step on the '
                                'captured shapes first)')
         _AGREE.table = {(t.data_ptr(), tuple(t.shape)): (tuple(t.shape), False) for t in ts}
+        _AGREE.step = True
         return
-    flat = [len(sig)] + [len(x) for x in sig] + [d for x in sig for d in x]
     dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend() == 'nccl' else torch.device('cpu')
+    # a fixed-size header first (tensor count, total rank of the tensors): batches of different
+    # structure would otherwise all-reduce vectors of different lengths (a hang, or garbage)
+    head = [len(sig), sum(len(x) for x in sig)]
+    h = torch.tensor(head + [-x for x in head], dtype=torch.int64, device=dev)
+    dist.all_reduce(h, op=dist.ReduceOp.MAX)
+    h = h.tolist()
+    if h[:2] != [-x for x in h[2:]]:
+        raise RuntimeError('rsys data parallel: the ranks\' batches hold different tensors (same config?)')
+    flat = [len(sig)] + [len(x) for x in sig] + [d for x in sig for d in x]
     v = torch.tensor(flat + [-x for x in flat], dtype=torch.int64, device=dev)
     dist.all_reduce(v, op=dist.ReduceOp.MAX)
     v = v.tolist()
@@ -181,6 +194,16 @@ def agree_batch(batch) -> None:
     _AGREE.table = table
     _AGREE.sig = sig
     _AGREE.static = all(not r for _, r in table.values())
+    _AGREE.step = True
+
+
+def end_forward():
+    """The forward that agreed its batch is over (TwoTowerModel.forward): its table keyed by batch
+    tensor addresses is dropped, so a later lookup outside a TwoTowerModel forward (validate()'s
+    item indexing through get_item_embeddings, a tower called on its own) can never match a
+    reused allocator address of the same shape and take another batch's dims; it agrees per call
+    (agree_max) instead. The step's `static` verdict stays until clear_agreement."""
+    _AGREE.table = None
 
 
 def agreed_dims(t):
@@ -195,6 +218,7 @@ def clear_agreement():
     """End of the step's collectives (allreduce_gradients): later lookups outside a
     TwoTowerModel forward agree per call again."""
     _AGREE.table = None
+    _AGREE.step = False
 
 
 def agree_max(*vals):
@@ -205,7 +229,7 @@ def agree_max(*vals):
     if not is_active() or _AGREE.local:
         return list(vals)
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
-        if _AGREE.table is not None and _AGREE.static:
+        if _AGREE.step and _AGREE.static:
             return list(vals)
         raise RuntimeError('rsys data parallel: a lookup shape cannot be agreed inside a hipGraph capture')
     dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend() == 'nccl' else torch.device('cpu')

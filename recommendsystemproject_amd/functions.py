@@ -194,12 +194,55 @@ def _grad_tables(segs, calls, dout, tables, rows, params=()):
         else:
             rest.append(s)
     if rest:
+        rest = _sorted_ordinary(rest, rows, dout)
+    if rest:
         _gather_bwd_split(rest, rows, dout)
     _dp.note_writer(params, written=True)
     for t, c, ptr in big:
         if ptr is None:  # max-pooled: its per-lookup gradient rows are already the call's dseg
             continue
         t.segsum(c, ptr, dout.stride(0))
+
+
+_SORTED_ORDINARY_BYTES = 4 << 20
+
+
+def _sorted_ordinary(segs, rows, dout):
+    """Deterministic mode (torch.use_deterministic_algorithms / RSYS_DETERMINISTIC): the gradient
+    of an ORDINARY (dense-Adam) table above 4 MB -- too large for the LDS-image kernels, so the
+    default is the float-atomic scatter -- through the large tables' sorted path instead: sort the
+    call's ids by row (rs_lookup_sort), then the segment sum (rs_segsum, accumulate), each row's
+    contributions added in lookup order with plain stores. The same two kernels and inputs as a
+    lazy table's call, so a model trained with RSYS_LAZY_ROWS=0 (dense Adam over every row) gets
+    bitwise the lazy path's table gradients. Returns the segments left to rs_gather_bwd."""
+    ops.sync_deterministic()
+    if not ops.deterministic_enabled() or not dout.is_cuda:
+        return segs
+    rest = []
+    for sg in segs:
+        pooled = sg.kind == _hip.RS_SEG_POOL
+        mode = SEG_ONE if sg.kind == _hip.RS_SEG_SPARSE else \
+            {_hip.RS_POOL['mean']: SEG_MEAN, _hip.RS_POOL['sum']: SEG_SUM}.get(sg.pool_mode) if pooled else None
+        ptr = dout.data_ptr() + 4 * sg.out_col
+        if (mode is None or not sg.grad or int(sg.vocab) * sg.dim * 4 <= _SORTED_ORDINARY_BYTES or
+                sg.dim % 4 or sg.dim > 256 or ptr % 16 or dout.stride(0) % 4):
+            rest.append(sg)
+            continue
+        bag = sg.bag if pooled else 1
+        n = rows * bag
+        if n == 0:
+            continue
+        L = _hip.lib()
+        keys = torch.empty(n, dtype=torch.int32, device=dout.device)
+        vals = torch.empty(n, dtype=torch.int32, device=dout.device)
+        wsb = int(L.rs_lookup_sort_ws_bytes(n, int(sg.vocab)))
+        sws = torch.empty(wsb // 4 + 1, dtype=torch.int32, device=dout.device) if wsb else None
+        _hip.call('rs_lookup_sort', sg.idx, 8, rows, bag, sg.idx_stride, int(sg.vocab), keys.data_ptr(),
+                  vals.data_ptr(), None if sws is None else sws.data_ptr(), ops.stream())
+        ws = torch.empty(int(L.rs_segsum_ws_bytes(n, sg.dim)) // 4 + 1, dtype=torch.int32, device=dout.device)
+        _hip.call('rs_segsum', keys.data_ptr(), vals.data_ptr(), n, bag, mode, sg.pad_idx, ptr,
+                  dout.stride(0), sg.dim, sg.grad, 1, ws.data_ptr(), ops.stream())
+    return rest
 
 
 _HEAVY_LOOKUPS = 65536
@@ -368,7 +411,10 @@ class SeqFeaturesFn(torch.autograd.Function):
     @once_differentiable
     def backward(ctx, dx):
         dx = dx.contiguous().view(ctx.B * ctx.L, -1).clone()  # consumed in place below
-        seq_input_bwd(ctx.proc, ctx.saved, dx, ctx.B, ctx.L, ctx.p, ctx.key, ctx.params)
+        try:
+            seq_input_bwd(ctx.proc, ctx.saved, dx, ctx.B, ctx.L, ctx.p, ctx.key, ctx.params)
+        finally:
+            _WgradBranch.join()
         ctx.saved = ctx.params = None
         return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
@@ -423,6 +469,13 @@ class _WgradBranch:
         side = cls._pending.pop(main.device, None)
         if side is not None:
             main.wait_stream(side)
+
+    @classmethod
+    def assert_joined(cls):
+        """The optimizer reads the flat gradient: no forked weight-gradient branch may be pending."""
+        if cls._pending:
+            cls._pending.clear()
+            raise RuntimeError('rsys: an encoder weight-gradient branch was forked and never joined')
 
 
 def _is_fake(t):
@@ -631,19 +684,24 @@ class SeqEncoderFn(torch.autograd.Function):
         d, H = proc.target_dim, enc.n_head
         dout = dout.contiguous()
         n = len(ctx.layers)
-        if ctx.prune:
-            dx = layer_bwd_last(ctx.layers[n - 1], ctx.layer_saved[n - 1], dout.clone(), ctx.key_pad,
-                                ctx.last, B, L, d, H, p, key, _layer_site(n - 1))
-            n -= 1
-        else:
-            dx = torch.zeros(B * L, d, device=dout.device, dtype=torch.float32)
-            seg = _seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=ctx.last.data_ptr(),
-                       grad=dx.data_ptr())
-            ops.gather_bwd([seg], B, dout)
-        for i in reversed(range(n)):
-            dx = layer_bwd(ctx.layers[i], ctx.layer_saved[i], dx, ctx.key_pad, B, L, d, H, p, key,
-                           _layer_site(i))
-        seq_input_bwd(proc, ctx.in_saved, dx, B, L, p, key, ctx.params)
+        try:
+            if ctx.prune:
+                dx = layer_bwd_last(ctx.layers[n - 1], ctx.layer_saved[n - 1], dout.clone(), ctx.key_pad,
+                                    ctx.last, B, L, d, H, p, key, _layer_site(n - 1))
+                n -= 1
+            else:
+                dx = torch.zeros(B * L, d, device=dout.device, dtype=torch.float32)
+                seg = _seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=ctx.last.data_ptr(),
+                           grad=dx.data_ptr())
+                ops.gather_bwd([seg], B, dout)
+            for i in reversed(range(n)):
+                dx = layer_bwd(ctx.layers[i], ctx.layer_saved[i], dx, ctx.key_pad, B, L, d, H, p, key,
+                               _layer_site(i))
+            seq_input_bwd(proc, ctx.in_saved, dx, B, L, p, key, ctx.params)
+        finally:
+            # structural join of any weight-gradient branch this backward forked (seq_input_bwd
+            # joins on its normal path; an exception or a path that never reaches it joins here)
+            _WgradBranch.join()
         ctx.layer_saved = ctx.in_saved = ctx.params = None
         return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 

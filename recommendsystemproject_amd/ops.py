@@ -224,6 +224,12 @@ def sync_deterministic():
         _DETERMINISTIC[0] = on
 
 
+def deterministic_enabled() -> bool:
+    """Deterministic table gradients requested (torch.use_deterministic_algorithms or
+    RSYS_DETERMINISTIC=1)."""
+    return bool(torch.are_deterministic_algorithms_enabled()) or os.environ.get('RSYS_DETERMINISTIC', '0') == '1'
+
+
 def gather_bwd(segs, rows, dout):
     sync_deterministic()
     arr = segments_array(segs)

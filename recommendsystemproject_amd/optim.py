@@ -199,6 +199,8 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        from .functions import _WgradBranch
+        _WgradBranch.assert_joined()
         for group in self.param_groups:
             b1, b2 = group['betas']
             f = self._group_flat(group)

@@ -42,9 +42,32 @@ class TwoTowerModel(nn.Module):
             self._rs_side_stream = s
         return s
 
+    def _user_stream(self, dev):
+        """RSYS_USER_STREAM=1 (or 'high': the highest stream priority): the user tower on a stream of
+        its own instead of the current one -- the current stream then only forks the two towers
+        and joins them before the loss. Off by default (measured no faster: DESIGN.md §5)."""
+        mode = os.environ.get('RSYS_USER_STREAM', '0')
+        if mode not in ('1', 'high'):
+            return None
+        s = getattr(self, '_rs_user_stream', None)
+        if s is None or s.device != dev or getattr(self, '_rs_user_stream_mode', None) != mode:
+            if mode == 'high':
+                _, hi = torch.cuda.Stream.priority_range()
+                s = torch.cuda.Stream(device=dev, priority=hi)
+            else:
+                s = torch.cuda.Stream(device=dev)
+            self._rs_user_stream, self._rs_user_stream_mode = s, mode
+        return s
+
     def forward(self, batch_data):
         """-> (user_emb [B,D], item_emb [B,D], hard_neg_emb [B,N,D] or None) (TwoTowerModel.py:35-62;
         T13: one item-tower pass per hard-negative slot, so BatchNorm statistics are per slot)."""
+        try:
+            return self._forward(batch_data)
+        finally:
+            rdist.end_forward()  # the batch agreement is this forward's only (dist.end_forward)
+
+    def _forward(self, batch_data):
         dev = self.user_tower.feature_bn.weight.device
         _hip.require_device(self.user_tower.feature_bn.weight)
         ensure_flat(self)
@@ -66,13 +89,21 @@ class TwoTowerModel(nn.Module):
         side.wait_stream(main)
         with torch.cuda.stream(side):
             item_emb, hard_neg_emb = self._item_side(batch_data)
-        user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
+        ustream = self._user_stream(dev)
+        if ustream is not None:
+            ustream.wait_stream(main)
+            with torch.cuda.stream(ustream):
+                user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
+            main.wait_stream(ustream)
+            user_emb.record_stream(main)
+        else:
+            user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
         main.wait_stream(side)
         outs = [t for t in (item_emb, hard_neg_emb) if t is not None]
         for t in outs:
             t.record_stream(main)  # made on the side stream, read by the loss on the main one
         if torch.is_grad_enabled() and item_emb.requires_grad:
-            self._join_backward(main, [(side, outs)])
+            self._join_backward(main, [(side, outs)] + ([(ustream, [user_emb])] if ustream is not None else []))
         return user_emb, item_emb, hard_neg_emb
 
     @staticmethod

@@ -109,3 +109,71 @@ def test_rccl_exchange_world_size_one(monkeypatch):
             (f.data - ensure_flat(ref).data).abs().max().item() < 1e-6
     finally:
         dist.destroy_process_group()
+
+
+def _copy_batch(dst, src):
+    if isinstance(src, torch.Tensor):
+        dst.copy_(src)
+    elif isinstance(src, dict):
+        for k, v in src.items():
+            _copy_batch(dst[k], v)
+
+
+def _clone_batch(b):
+    if isinstance(b, torch.Tensor):
+        return b.clone()
+    return {k: _clone_batch(v) for k, v in b.items()} if isinstance(b, dict) else b
+
+
+def test_rccl_captured_step_row_sharded_world_size_one(monkeypatch):
+    """bench.py's N > 1 step exactly as the driver's RCCL scaling run executes it, on one GPU: the
+    'nccl' backend at world_size 1 with the exchange forced on and every lookup table row-sharded
+    (RSYS_SHARD_ROWS=1: the single-id / per-token lookups through the all-to-all row exchange,
+    pooled bags through all-gather + reduce-scatter), forward + backward with the bucketed
+    all-reduces started inside it + the shard exchange + clip + Adam captured into ONE hipGraph
+    (thread_local capture, as bench.py) and replayed for 3 steps on new batches. Deterministic
+    mode; the weights after the replays equal an eager run of the same 5 steps bitwise."""
+    from recommendsystemproject_amd import ops
+    monkeypatch.setenv('RSYS_LAZY_ROWS', '1')
+    monkeypatch.setenv('RSYS_SHARD_ROWS', '1')
+    monkeypatch.setenv('MASTER_ADDR', '127.0.0.1')
+    monkeypatch.setenv('MASTER_PORT', str(_free_port()))
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=DEV)
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        monkeypatch.setattr(rdist, 'is_active', lambda: True)
+        import recommendsystemproject_amd.flat as flat
+        monkeypatch.setattr(flat, '_dp_active', lambda: True)
+        _, cfg = _model()
+        b = _batches(cfg, 5)
+        losses = {}
+        datas = {}
+        for mode in ('eager', 'graph'):
+            model, _ = _model()
+            opt = Adam(model.parameters(), lr=1e-3)
+            f = ensure_flat(model)
+            assert sum(t.shard is not None for t in f.lazy) >= 3
+            if mode == 'eager':
+                losses[mode] = [float(train_step(model, x, opt, 1.0, 0.15)) for x in b]
+            else:
+                ls = [float(train_step(model, x, opt, 1.0, 0.15)) for x in b[:2]]  # eager warm-up
+                slot = _clone_batch(b[1])
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode='thread_local'):
+                    loss_static = train_step(model, slot, opt, 1.0, 0.15)
+                for x in b[2:]:
+                    _copy_batch(slot, x)
+                    g.replay()
+                    ls.append(float(loss_static))
+                losses[mode] = ls
+            f.flush()
+            torch.cuda.synchronize()
+            datas[mode] = f.data.clone()
+            assert all(t.calls == [] and t.exchanged is None for t in f.lazy)
+        assert losses['graph'] == losses['eager'], losses
+        assert torch.equal(datas['graph'], datas['eager']), (datas['graph'] - datas['eager']).abs().max().item()
+    finally:
+        torch.use_deterministic_algorithms(False)
+        ops.sync_deterministic()
+        dist.destroy_process_group()

@@ -232,9 +232,25 @@ def _c3_steps(cfg, model, batches, T):
     return [train_step(model, synth.batch_to_torch(b, DEV), opt, 1.0, T).item() for b in batches]
 
 
-def test_c3_real_tables_lazy_matches_dense_adam(monkeypatch):
+@pytest.fixture
+def deterministic():
+    """torch.use_deterministic_algorithms(True): every table gradient through a fixed-order kernel
+    (slot-image / ranged LDS images, sorted segment sums for the large ones, lazy or not:
+    functions._sorted_ordinary), so two runs that compute the same sums agree bitwise."""
+    from recommendsystemproject_amd import ops
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    ops.sync_deterministic()
+    yield
+    torch.use_deterministic_algorithms(False)
+    ops.sync_deterministic()
+
+
+def test_c3_real_tables_lazy_matches_dense_adam(monkeypatch, deterministic):
     """C3 at its real sizes: lazy-exact Adam over sorted lookups (1M / 10M / 10M rows) against
-    the same model trained with dense Adam over every row, 5 steps of distinct batches."""
+    the same model trained with dense Adam over every row, 5 steps of distinct batches, in
+    deterministic mode: the table gradients are the same fixed-order sums in both runs, so the
+    losses and the tables agree bitwise (up to 1e-6 where the clip coefficient's last bit may
+    differ: the dense run's norm sums 2.69B squares, the lazy one only the touched rows')."""
     cfg = cfg_of('c3')
     T = float(cfg['train']['temperature'])
     batches = [synth.make_batch(cfg, 4096, seed=300 + s) for s in range(5)]
@@ -250,20 +266,12 @@ def test_c3_real_tables_lazy_matches_dense_adam(monkeypatch):
         dense.load_state_dict({k: v for k, v in init.items()}, strict=False)
     assert not ensure_flat(dense).lazy
     l_dense = _c3_steps(cfg, dense, batches, T)
-    np.testing.assert_allclose(l_lazy, l_dense, rtol=0, atol=1e-5)
+    np.testing.assert_allclose(l_lazy, l_dense, rtol=0, atol=1e-6)
     sl, sd = lazy.state_dict(), dense.state_dict()  # lazy: flushed to the current step
-    lr = float(cfg['train']['learning_rate'])
     for k, w0 in init.items():
         a, b = sl[k], sd[k]
-        # The small tables' gradients are scattered with float atomics in both runs, so they
-        # differ in the last bits between the runs; from step 2 on, Adam turns that noise on
-        # near-zero gradient elements into up to +-lr steps (the golden tests' BN-invariant
-        # parameters, same cause). One step alone is bitwise equal (tools/diag_c3.py).
         d = (a - b).abs()
-        assert d.max().item() <= 2 * lr * len(batches), (k, d.max().item())
-        moved = (a != w0).any(1) | (b != w0).any(1)
-        frac = (d[moved] <= 1e-6).float().mean().item()
-        assert frac >= 0.999, (k, frac)
+        assert d.max().item() <= 1e-6, (k, d.max().item(), int((d > 0).sum()))
         # rows no batch looked up moved by neither (their Adam state is zero)
         rows = torch.randint(0, a.shape[0], (4096,), device=DEV)
         touched = torch.zeros(a.shape[0], dtype=torch.bool, device=DEV)

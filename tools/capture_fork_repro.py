@@ -65,6 +65,21 @@ def body():
         y2 = y2 + 1
         cur.wait_stream(tower)
         return y1, y2, h1, h2
+    if v in ('chain', 'chain_fresh'):
+        # a fork of a fork: cur -> A, A -> B, B joined into A, A joined into cur (the user tower on
+        # its own stream forking its per-table lookup stream: TwoTowerModel RSYS_USER_STREAM=1)
+        a_st = tower if v == 'chain' else torch.cuda.Stream()
+        a_st.wait_stream(cur)
+        with torch.cuda.stream(a_st):
+            y1 = x * 2
+            b_st = side if v == 'chain' else torch.cuda.Stream()
+            b_st.wait_stream(a_st)
+            with torch.cuda.stream(b_st):
+                y2 = x * 3
+            a_st.wait_stream(b_st)
+            y1 = y1 + y2
+        cur.wait_stream(a_st)
+        return y1, y2
     if v == 'autograd':
         y = Fn.apply(w)
         y.sum().backward()
