@@ -90,7 +90,7 @@ int rs_colsum(const float* X, int M, int N, int ldx, float scale, float beta, fl
  * Descriptor-driven multi-table gather into a row-major concat buffer out[rows, ldo].
  * One segment per feature (kind: 0 single sparse id, 1 pooled bag, 2 dense Linear(1,D),
  * 3 last-valid row of a [rows*L, D] sequence, 4 plain [rows, D] slice copy). Segments are
- * passed by value into the kernel arguments (at most 24 per call). Replaces GenericTower.forward feature loop (GenericTower.py:133-233,
+ * passed by value into the kernel arguments (at most 20 per call). Replaces GenericTower.forward feature loop (GenericTower.py:133-233,
  * K1/K2/K11 + torch.cat), SequenceFeatureProcessor.forward gather/tag-pool/cat
  * (SequenceFeatureProcessor.py:57-76, K3) and SequenceEncoder._gather_last_valid
  * (SequenceEncoder.py:58-74, K10). Segment layout: rs_feature_seg_t below. */
@@ -126,6 +126,13 @@ typedef struct rs_feature_seg {
   const int* lazy_last;   /* kind 0/1, nullable, rs_gather_fwd_lazy only: `last` of a lazy-Adam
                              table (the optimizer step each row was last brought to); the rows are
                              returned brought to the current step without being written */
+  const uint32_t* hot_keys; /* kind 1 (mean / sum), nullable, forward only: this call's ids sorted
+                             by row (rs_lookup_sort keys, hot_n of them). The rows looked up at
+                             least 2 x 256 times (the padding row, Zipf-hot rows; up to 64 of them)
+                             are found from the sorted keys and staged once per workgroup into LDS,
+                             and their lookups are served from there (same values, same order:
+                             the result is bitwise the plain gather's) */
+  int64_t hot_n;
 } rs_feature_seg_t;
 
 int rs_gather_fwd(const rs_feature_seg_t* segs, int nseg, int rows, float* out, int ldo,
@@ -525,7 +532,8 @@ int rs_sparse_flush(float* p, float* m, float* v, int* last, int64_t V, int D, c
  * One forward lookup of a large table (a [rows, bag] id matrix, int64 or int32, row stride
  * row_stride) is sorted by row id: keys[n] ascending (ids outside [0, vocab) last, as
  * 0xFFFFFFFF), vals[n] = the lookup index r * bag + l, ascending within a row (stable LSD radix
- * sort; n <= 4096 in one launch without workspace, else rs_lookup_sort_ws_bytes of workspace).
+ * sort of rs_lookup_sort_ws_bytes of workspace; n <= 8192: a counting sort over the whole chip,
+ * two launches; n <= 4096 also runs without a workspace, one workgroup's radix passes).
  * Every per-row operation then walks the distinct rows (run heads) of keys:
  *   rs_sorted_catchup  replay skipped zero-gradient Adam steps before the gather reads the rows
  *                      (bitwise equal to dense Adam); rs_lookup_catchup does the same straight

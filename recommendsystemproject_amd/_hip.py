@@ -19,7 +19,7 @@ RS_ATTN_QKV_BF16 = 2048
 RS_EPI_DROP_A, RS_EPI_DROP_B = 16, 32
 RS_SEG_SPARSE, RS_SEG_POOL, RS_SEG_DENSE, RS_SEG_LASTVALID, RS_SEG_COPY = 0, 1, 2, 3, 4
 RS_POOL = {'mean': 0, 'sum': 1, 'max': 2}
-MAX_SEGMENTS = 24
+MAX_SEGMENTS = 20
 
 vp, i32, i64, f32 = C.c_void_p, C.c_int, C.c_int64, C.c_float
 
@@ -29,7 +29,7 @@ class FeatureSeg(C.Structure):
     _fields_ = [('kind', i32), ('dim', i32), ('out_col', i32), ('pool_mode', i32), ('bag', i32),
                 ('pad_idx', i32), ('vocab', i64), ('idx_stride', i64), ('idx', vp), ('table', vp),
                 ('bias', vp), ('x', vp), ('grad', vp), ('grad_bias', vp), ('touch_count', vp),
-                ('lazy_last', vp)]
+                ('lazy_last', vp), ('hot_keys', vp), ('hot_n', i64)]
 
 
 class SortedCall(C.Structure):

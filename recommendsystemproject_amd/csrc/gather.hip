@@ -29,7 +29,7 @@ namespace {
 std::atomic<int> g_deterministic{0};  // rs_set_deterministic
 bool deterministic() { return g_deterministic.load(std::memory_order_relaxed) || getenv_flag("RSYS_DETERMINISTIC"); }
 
-constexpr int kMaxSeg = 24;  // segments travel by value in the kernel arguments (~2.6 KB)
+constexpr int kMaxSeg = 20;  // segments travel by value in the kernel arguments (~2.4 KB)
 // tables up to this size get their gradient accumulated in LDS first (privatised per workgroup,
 // then one global atomic per touched element): a 30-row genre table hit 600k times per step
 // would otherwise serialise on a few hundred addresses
@@ -44,6 +44,14 @@ constexpr int kLazyBagBatch = 8;           // the same with exp_avg / exp_avg_sq
 // table holds is staged whole into LDS first (every row of such a table is hot: the genre / age /
 // occupation tables are read thousands of times per step), and its lookups are served from LDS
 constexpr int kStageBytes = 16 * 1024;
+// forward, pooled (mean / sum) lookups of a large table with its sorted call (seg.hot_keys): the
+// hot rows -- runs of >= 2 kHotQ equal sorted keys, found by sampling every kHotQ-th key -- are
+// staged once per workgroup into LDS (up to kHotMax rows) and served from there through flat
+// loads; the segment runs kHotBlocks persistent workgroups (the staging is paid per workgroup)
+constexpr int kHotQ = 256;
+constexpr int kHotMax = 64;
+constexpr int kHotHash = 256;
+constexpr int kHotBlocks = 256;
 
 // read-through catch-up of lazy-Adam segments: the moments sit at fixed element offsets from the
 // parameters (one flat buffer each), the step counter and per-step constants are the optimizer's
@@ -84,6 +92,7 @@ struct SegLaunch {
   int slot_lds;            // bwd: dynamic LDS bytes of the slot kernel
   uint8_t rpt[kMaxSeg];    // fwd sparse segments: rows per lane (kRowsPerLane on token-sized launches)
   uint8_t nt[kMaxSeg];     // fwd: rows of a large table -- non-temporal loads, shorter bag batches
+  uint8_t hot[kMaxSeg];    // fwd: pooled lookups with their hot rows staged in LDS (gather_pool_hot)
   int16_t tblocks[kMaxSeg];
   int tblock_start[kMaxSeg + 1];
   // bwd partials (small and ranged tables): [pchunks][vocab][dim] floats at ws + pws_off
@@ -341,6 +350,146 @@ __device__ void gather_pool_split(const SegLaunch& a, const rs_feature_seg_t& sg
   store_row<VEC>(o, acc);
 }
 
+// The hot rows of a pooled call (seg.hot_keys: its ids sorted by row): sample every kHotQ-th
+// sorted position p; p starts the first sample of a run of at least kHotQ keys when key[p] ==
+// key[p + kHotQ - 1] and key[p - kHotQ] differs, so every run of >= 2 kHotQ - 1 lookups (and some
+// shorter ones) is listed once. Up to kHotMax rows are staged into `rows` (LDS) and entered into an
+// open-addressing table id -> slot. Returns the number staged. Which rows make the list (LDS
+// atomics) does not change any value: a staged row is a copy of the table row.
+struct HotLds {
+  int count;
+  int ids[kHotMax];
+  int tab[kHotHash];
+  uint8_t slot[kHotHash];
+};
+
+__device__ __forceinline__ int hot_hash(uint32_t id) { return (int)((id * 2654435761u) >> 24); }
+
+__device__ int hot_stage(const rs_feature_seg_t& sg, HotLds& h, float4* rows) {
+  if (threadIdx.x == 0) h.count = 0;
+  for (int i = threadIdx.x; i < kHotHash; i += 256) h.tab[i] = -1;
+  __syncthreads();
+  const uint32_t* keys = sg.hot_keys;
+  const int64_t n = sg.hot_n;
+  for (int64_t p = (int64_t)threadIdx.x * kHotQ; p + kHotQ - 1 < n; p += (int64_t)256 * kHotQ) {
+    const uint32_t k = keys[p];
+    if (k == 0xFFFFFFFFu || keys[p + kHotQ - 1] != k || (p >= kHotQ && keys[p - kHotQ] == k)) continue;
+    const int i = atomicAdd(&h.count, 1);
+    if (i < kHotMax) h.ids[i] = (int)k;
+  }
+  __syncthreads();
+  const int cnt = h.count < kHotMax ? h.count : kHotMax;
+  if ((int)threadIdx.x < cnt) {
+    const int id = h.ids[threadIdx.x];
+    int b = hot_hash((uint32_t)id);
+    while (atomicCAS(&h.tab[b], -1, id) != -1) b = (b + 1) & (kHotHash - 1);
+    h.slot[b] = (uint8_t)threadIdx.x;
+  }
+  const int q = sg.dim / 4;
+  for (int i = threadIdx.x; i < cnt * q; i += 256) {
+    const int r = i / q;
+    rows[i] = reinterpret_cast<const float4*>(sg.table + (int64_t)h.ids[r] * sg.dim)[i - r * q];
+  }
+  __syncthreads();
+  return cnt;
+}
+
+// slot of row id among the staged hot rows, or -1
+__device__ __forceinline__ int hot_find(const HotLds& h, int64_t id) {
+  int b = hot_hash((uint32_t)id);
+  for (;;) {
+    const int t = h.tab[b];
+    if (t == (int)id) return h.slot[b];
+    if (t < 0) return -1;
+    b = (b + 1) & (kHotHash - 1);
+  }
+}
+
+// pool_acc (VEC, plain rows) with the staged hot rows: a lookup of a hot row reads its LDS copy
+// through the same flat load (no branch around the load), in the same order -- the same sums
+__device__ __forceinline__ void pool_acc_hot(const rs_feature_seg_t& sg, const HotLds& h, int cnt,
+                                             const float4* hrows, int row, int c, int lbeg, int lend,
+                                             float* acc, bool& bad) {
+  constexpr int NB = kBagBatch;
+  const int64_t* ids = sg.idx + (int64_t)row * sg.idx_stride;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = 0.f;
+  int64_t raw[NB];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) raw[u] = lbeg + u < lend ? ids[lbeg + u] : 0;
+  for (int l0 = lbeg; l0 < lend; l0 += NB) {
+    const int nb = lend - l0 < NB ? lend - l0 : NB;
+    bool ok[NB];
+    float v[NB][4];
+    int sl[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const bool valid = raw[u] >= 0 && raw[u] < sg.vocab;
+      bad |= u < nb && !valid;
+      ok[u] = u < nb && valid;
+      sl[u] = cnt ? hot_find(h, ok[u] ? raw[u] : 0) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int64_t r = ok[u] ? raw[u] : 0;
+      const float* src = sl[u] >= 0 ? reinterpret_cast<const float*>(hrows + sl[u] * (sg.dim / 4)) + c
+                                    : sg.table + r * sg.dim + c;
+      load_row<true>(src, v[u]);
+    }
+    const int n2 = l0 + NB;
+#pragma unroll
+    for (int u = 0; u < NB; ++u) raw[u] = n2 + u < lend ? ids[n2 + u] : 0;
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float x = ok[u] ? v[u][j] : 0.f;
+        const float y = acc[j] + x;
+        acc[j] = u < nb ? y : acc[j];
+      }
+    }
+  }
+}
+
+// gather_pool_split over persistent workgroups with the hot rows in LDS: workgroup lb of nblk
+// takes row groups lb, lb + nblk, ...
+__device__ void gather_pool_hot(const SegLaunch& a, const rs_feature_seg_t& sg, int s, int lb, int nblk,
+                                float4* dyn) {
+  __shared__ float4 red[256];
+  __shared__ HotLds h;
+  const int cnt = hot_stage(sg, h, dyn);
+  const int C = a.chunks[s], S = a.split[s];
+  const int grp = threadIdx.x / C, chunk = threadIdx.x % C;
+  const int r = grp / S, p = grp % S;
+  const int per = (sg.bag + S - 1) / S;
+  const int lbeg = p * per < sg.bag ? p * per : sg.bag;
+  const int lend = lbeg + per < sg.bag ? lbeg + per : sg.bag;
+  const int ngroups = (a.rows + a.rpb[s] - 1) / a.rpb[s];
+  bool bad = false;
+  for (int g = lb; g < ngroups; g += nblk) {
+    const int row = g * a.rpb[s] + r;
+    const bool active = r < a.rpb[s] && row < a.rows;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (active) pool_acc_hot(sg, h, cnt, dyn, row, chunk * 4, lbeg, lend, acc, bad);
+    red[threadIdx.x] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    __syncthreads();
+    if (active && p == 0) {
+      for (int q = 1; q < S; ++q) {
+        const float4 t = red[threadIdx.x + q * C];
+        acc[0] += t.x; acc[1] += t.y; acc[2] += t.z; acc[3] += t.w;
+      }
+      if (sg.pool_mode == RS_POOL_MEAN) {
+        const float n = (float)sg.bag;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = acc[j] / n;
+      }
+      store_row<true>(a.out + (int64_t)row * a.ldo + sg.out_col + chunk * 4, acc);
+    }
+    __syncthreads();
+  }
+  if (bad && a.err) atomicOr(a.err, 1);
+}
+
 // LAZY launches (rs_gather_fwd_lazy): segments with lazy_last read through the catch-up (float4
 // rows, never staged: the plan checks); the others as in a plain launch
 template <bool LAZY>
@@ -366,6 +515,10 @@ __global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
     if (row >= a.rows) return;
     if (a.vec[s]) gather_seg<true, true>(a, sg, row, chunk);
     else gather_seg<false, true>(a, sg, row, chunk);
+    return;
+  }
+  if (a.hot[s]) {  // uniform per workgroup: persistent workgroups with the hot rows in LDS
+    gather_pool_hot(a, sg, s, lb, a.block_start[s + 1] - a.block_start[s], stage_lds);
     return;
   }
   if (a.stage[s]) {  // uniform per workgroup: the whole table into LDS, then read it from there
@@ -942,8 +1095,14 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
                    ? kRowsPerLane : 1;
     a.rpb[s] = 256 / (C * S);
     a.nt[s] = nt;
+    a.hot[s] = !bwd && vec && g.kind == RS_SEG_POOL && g.pool_mode != RS_POOL_MAX && g.hot_keys &&
+               g.hot_n >= 2 * kHotQ && !nt && !g.lazy_last && g.dim <= 256 && !getenv_flag("RSYS_NO_HOT_ROWS");
+    if (a.hot[s]) {
+      const int hb = kHotMax * g.dim * 4;
+      if (hb > a.stage_lds) a.stage_lds = hb;
+    }
     a.stage[s] = 0;
-    if (!bwd && table_kind && vec) {
+    if (!bwd && table_kind && vec && !a.hot[s]) {
       const int64_t tbytes = g.vocab * g.dim * 4;
       const int64_t read = (int64_t)a.rpb[s] * (g.kind == RS_SEG_POOL ? g.bag : 1) * g.dim * 4;
       if (tbytes <= kStageBytes && tbytes <= read && !g.lazy_last && !getenv_flag("RSYS_NO_LDS_STAGE")) {
@@ -961,7 +1120,12 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
       a.rchunks[s] = rp.chunks;
     }
     a.block_start[s] = blocks;
-    if (!a.small[s] && !a.rranges[s] && !a.tiny[s]) blocks += cdiv(rows, a.rpb[s] * a.rpt[s]);
+    if (a.hot[s]) {
+      const int ng = cdiv(rows, a.rpb[s]);
+      blocks += ng < kHotBlocks ? ng : kHotBlocks;
+    } else if (!a.small[s] && !a.rranges[s] && !a.tiny[s]) {
+      blocks += cdiv(rows, a.rpb[s] * a.rpt[s]);
+    }
   }
   a.block_start[nseg] = blocks;
   int rb = 0;

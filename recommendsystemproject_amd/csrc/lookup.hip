@@ -458,6 +458,209 @@ __global__ __launch_bounds__(kTileThreads) void sort_tile_kernel(
   }
 }
 
+// ---------------------------------------------------------------- big-tile passes (round 5)
+// Calls above kRankMax lookups (C3's 204,800-id history call): tiles of 4,096 keys, one 1,024-thread
+// workgroup each, TWO launches per pass instead of three:
+//   sort_bhist_kernel    per-tile digit counts -> hist[digit][tile];
+//   sort_bscatter_kernel every tile computes its digits' global bases itself from hist (the keys of
+//                        smaller digits, plus this digit's keys in earlier tiles: ntiles loads per
+//                        digit, 50 at C3), ranks its keys wave-major as sort_tile_kernel does, puts
+//                        them into tile order (by digit) through LDS and stores them from there, so
+//                        a digit's keys leave the tile as one contiguous run (coalesced stores).
+// Stable (tile order, then wave-major key order within a tile): the same keys and values as the
+// 1,024-key tiles (RSYS_SORT_SMALL_TILES=1 keeps those for A/B).
+__global__ __launch_bounds__(kTileThreads) void sort_bhist_kernel(
+    const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab,
+    const uint32_t* __restrict__ src, int64_t n, int shift, int dbits, int* __restrict__ hist) {
+  __shared__ int h[kMaxRadix];
+  const int radix = 1 << dbits;
+  for (int t = threadIdx.x; t < radix; t += kTileThreads) h[t] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kTileMax;
+#pragma unroll
+  for (int r = 0; r < kTileMax / kTileThreads; ++r) {
+    const int64_t e = base + r * kTileThreads + threadIdx.x;
+    if (e < n) {
+      const uint32_t k = src ? src[e] : raw_key(ids, id_bytes, bag, stride, vocab, e);
+      atomicAdd(&h[(k >> shift) & (radix - 1)], 1);
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < radix; t += kTileThreads) hist[(int64_t)t * gridDim.x + blockIdx.x] = h[t];
+}
+
+__global__ __launch_bounds__(kTileThreads) void sort_bscatter_kernel(
+    const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab,
+    const uint32_t* __restrict__ ksrc, const uint32_t* __restrict__ vsrc, int64_t n, int shift, int dbits,
+    const int* __restrict__ hist, uint32_t* __restrict__ kdst, uint32_t* __restrict__ vdst) {
+  __shared__ uint16_t cnt[kTileWaves][kMaxRadix];  // per wave: running, then exclusive, digit counts
+  __shared__ int tbase[kMaxRadix];                  // the tile's exclusive digit scan
+  __shared__ int gbase[kMaxRadix];                  // global start of the tile's run of each digit
+  __shared__ int wsum[kTileWaves], wsum2[kTileWaves];
+  __shared__ uint32_t xk[kTileMax], xv[kTileMax];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const int radix = 1 << dbits;
+  const int tile = blockIdx.x, ntiles = gridDim.x;
+  const int64_t base = (int64_t)tile * kTileMax;
+  const int nt = (int)(n - base < kTileMax ? n - base : kTileMax);
+  uint32_t key[kSortRounds], val[kSortRounds];
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int e = w * kTileKeys + r * 64 + lane;
+    key[r] = kSentinel;
+    val[r] = 0;
+    if (e < nt) {
+      key[r] = ksrc ? ksrc[base + e] : raw_key(ids, id_bytes, bag, stride, vocab, base + e);
+      val[r] = vsrc ? vsrc[base + e] : (uint32_t)(base + e);
+    }
+  }
+  // this digit's keys in earlier tiles and in all tiles (thread d)
+  int before = 0, total = 0;
+  if ((int)threadIdx.x < radix) {
+    const int* hd = hist + (int64_t)threadIdx.x * ntiles;
+    for (int t = 0; t < ntiles; ++t) {
+      const int c = hd[t];
+      before += t < tile ? c : 0;
+      total += c;
+    }
+  }
+  for (int t = threadIdx.x; t < kTileWaves * radix; t += kTileThreads) cnt[t / radix][t % radix] = 0;
+  __syncthreads();
+  int pin[kSortRounds];
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const bool valid = w * kTileKeys + r * 64 + lane < nt;
+    const uint32_t d = (key[r] >> shift) & (radix - 1);
+    uint64_t peers = __ballot(valid);
+    for (int b = 0; b < dbits; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      peers &= bit ? bb : ~bb;
+    }
+    const int lrank = __popcll(peers & lt);
+    const int old = valid ? (int)cnt[w][d] : 0;
+    __builtin_amdgcn_wave_barrier();
+    if (valid && lrank == 0) cnt[w][d] = (uint16_t)(old + __popcll(peers));
+    __builtin_amdgcn_wave_barrier();
+    pin[r] = old + lrank;
+  }
+  __syncthreads();
+  // per digit: exclusive offsets over the waves; the tile's digit counts and the global totals
+  // scanned over the digits (two inclusive scans: lanes, then the waves' sums)
+  int tot = 0;
+  if ((int)threadIdx.x < radix) {
+#pragma unroll
+    for (int ww = 0; ww < kTileWaves; ++ww) {
+      const int c = cnt[ww][threadIdx.x];
+      cnt[ww][threadIdx.x] = (uint16_t)tot;
+      tot += c;
+    }
+  }
+  int y = tot, g = total;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t1 = __shfl_up(y, o, 64), t2 = __shfl_up(g, o, 64);
+    if (lane >= o) { y += t1; g += t2; }
+  }
+  if (lane == 63) { wsum[w] = y; wsum2[w] = g; }
+  __syncthreads();
+  if ((int)threadIdx.x < radix) {
+    int pre = 0, pre2 = 0;
+    for (int ww = 0; ww < w; ++ww) { pre += wsum[ww]; pre2 += wsum2[ww]; }
+    tbase[threadIdx.x] = pre + y - tot;
+    gbase[threadIdx.x] = pre2 + g - total + before;
+  }
+  __syncthreads();
+  // keys into tile order (by digit) through LDS
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const bool valid = w * kTileKeys + r * 64 + lane < nt;
+    if (valid) {
+      const uint32_t d = (key[r] >> shift) & (radix - 1);
+      const int pl = tbase[d] + (int)cnt[w][d] + pin[r];
+      xk[pl] = key[r];
+      xv[pl] = val[r];
+    }
+  }
+  __syncthreads();
+  // store from tile order: position j of the tile holds a key of digit d at tile offset j - tbase[d]
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int j = r * kTileThreads + (int)threadIdx.x;
+    if (j < nt) {
+      const uint32_t k = xk[j];
+      const uint32_t d = (k >> shift) & (radix - 1);
+      const int64_t pos = (int64_t)gbase[d] + (j - tbase[d]);
+      kdst[pos] = k;
+      vdst[pos] = xv[j];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- counting sort (n <= kRankMax)
+// A small call (C3's user-id and item-id calls: 4,096 ids) sorted by counting ranks spread over
+// the whole chip instead of one workgroup's radix passes (sort_tile_kernel: 3 passes of 4,096 keys
+// on one CU, ~19 us). The stable rank of lookup i is
+//   rank(i) = #{j : key_j < key_i} + #{j < i : key_j == key_i},
+// a permutation of 0 .. n-1. Pass 1: workgroup (ib, jb) counts, for the 256 keys of block ib, the
+// keys of block jb that precede them (j < i is decided per block: every j of a lower block
+// precedes i on a tie, no j of a higher block does; the diagonal block compares indices) -- 256 x
+// 256 compares, one broadcast LDS read per 4 keys; the partial counts go to the workspace. Pass 2:
+// one thread per lookup sums its nb partials and stores its key and lookup index at its rank.
+// n = 4,096: 256 workgroups of ~2 x 256 VALU operations per lane, then 16 workgroups.
+constexpr int kRankBlock = 256;
+constexpr int kRankMax = 8192;
+
+__global__ __launch_bounds__(kRankBlock) void rank_partial_kernel(const void* __restrict__ ids, int id_bytes,
+                                                                  int bag, int64_t stride, int64_t vocab, int n,
+                                                                  int* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) uint32_t kj[kRankBlock];
+  const int ib = blockIdx.x, jb = blockIdx.y, t = threadIdx.x;
+  const int i = ib * kRankBlock + t, j = jb * kRankBlock + t;
+  const uint32_t ki = i < n ? raw_key(ids, id_bytes, bag, stride, vocab, i) : kSentinel;
+  // past n: the sentinel, which precedes no key (never <, and == only on the diagonal block at
+  // an index above every valid one)
+  kj[t] = j < n ? raw_key(ids, id_bytes, bag, stride, vocab, j) : kSentinel;
+  __syncthreads();
+  int cnt = 0;
+  const uint4* q = reinterpret_cast<const uint4*>(kj);
+  if (jb < ib) {
+#pragma unroll 16
+    for (int c = 0; c < kRankBlock / 4; ++c) {
+      const uint4 k4 = q[c];
+      cnt += (k4.x <= ki) + (k4.y <= ki) + (k4.z <= ki) + (k4.w <= ki);
+    }
+  } else if (jb > ib) {
+#pragma unroll 16
+    for (int c = 0; c < kRankBlock / 4; ++c) {
+      const uint4 k4 = q[c];
+      cnt += (k4.x < ki) + (k4.y < ki) + (k4.z < ki) + (k4.w < ki);
+    }
+  } else {
+#pragma unroll 16
+    for (int c = 0; c < kRankBlock / 4; ++c) {
+      const uint4 k4 = q[c];
+      const int b = 4 * c;
+      cnt += (k4.x < ki || (k4.x == ki && b < t)) + (k4.y < ki || (k4.y == ki && b + 1 < t)) +
+             (k4.z < ki || (k4.z == ki && b + 2 < t)) + (k4.w < ki || (k4.w == ki && b + 3 < t));
+    }
+  }
+  if (i < n) part[(int64_t)jb * n + i] = cnt;
+}
+
+__global__ __launch_bounds__(256) void rank_scatter_kernel(const void* __restrict__ ids, int id_bytes, int bag,
+                                                           int64_t stride, int64_t vocab, int n, int nb,
+                                                           const int* __restrict__ part,
+                                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int r = 0;
+  for (int b = 0; b < nb; ++b) r += part[(int64_t)b * n + i];
+  keys[r] = raw_key(ids, id_bytes, bag, stride, vocab, i);
+  vals[r] = (uint32_t)i;
+}
+
 // ---------------------------------------------------------------- per distinct row
 
 __device__ __forceinline__ int clamp_step(const float2* consts, int64_t t) {
@@ -1088,7 +1291,7 @@ bool sort_onesweep() {
 // totals, or the single-launch path's status words [passes][tiles][radix] (u64), tile counters and
 // per-pass digit totals
 int64_t sort_ws_bytes(int64_t n, int64_t vocab) {
-  if (n <= kTileMax) return 0;
+  if (n <= kRankMax) return (int64_t)cdiv(n, kRankBlock) * n * 4 + 256;  // the counting sort's partials
   const SortPlan p = make_plan(n, vocab);
   const int64_t multi = ((int64_t)kMaxRadix * p.ntiles + kMaxRadix) * 4;
   const int64_t one = (int64_t)p.passes * p.ntiles * kMaxRadix * 8 + 64 + (int64_t)4 * kMaxRadix * 4;
@@ -1112,7 +1315,17 @@ extern "C" int rs_lookup_sort(const void* ids, int id_bytes, int rows, int bag, 
   if (n == 0) return 0;
   hipStream_t st = as_stream(stream);
   const SortPlan p = make_plan(n, vocab);
-  if (n <= kTileMax) {
+  if (n <= kRankMax && ws) {  // the counting sort (its partials in ws)
+    const int nb = (int)cdiv(n, kRankBlock);
+    rank_partial_kernel<<<dim3(nb, nb), kRankBlock, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, (int)n,
+                                                              static_cast<int*>(ws));
+    RS_CHECK_LAUNCH("rs_lookup_sort rank");
+    rank_scatter_kernel<<<nb, 256, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, (int)n, nb,
+                                            static_cast<const int*>(ws), keys, vals);
+    RS_CHECK_LAUNCH("rs_lookup_sort rank scatter");
+    return 0;
+  }
+  if (n <= kTileMax) {  // without a workspace: one workgroup's radix passes
     sort_tile_kernel<<<1, kTileThreads, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, (int)n, p, keys, vals);
     RS_CHECK_LAUNCH("rs_lookup_sort tile");
     return 0;
@@ -1145,6 +1358,23 @@ extern "C" int rs_lookup_sort(const void* ids, int id_bytes, int rows, int bag, 
     return 0;
   }
   int* hist = reinterpret_cast<int*>(tv + n);
+  if (!getenv_flag("RSYS_SORT_SMALL_TILES")) {  // 4,096-key tiles, two launches per pass
+    const int nt4 = (int)cdiv(n, kTileMax);
+    for (int q = 0; q < p.passes; ++q) {
+      const bool to_out = ((p.passes - 1 - q) & 1) == 0;
+      uint32_t* kd = to_out ? keys : tk;
+      uint32_t* vd = to_out ? vals : tv;
+      const uint32_t* ks = q == 0 ? nullptr : (to_out ? tk : keys);
+      const uint32_t* vs = q == 0 ? nullptr : (to_out ? tv : vals);
+      sort_bhist_kernel<<<nt4, kTileThreads, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, ks, n, p.shift[q],
+                                                      p.dbits[q], hist);
+      RS_CHECK_LAUNCH("rs_lookup_sort bhist");
+      sort_bscatter_kernel<<<nt4, kTileThreads, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, ks, vs, n,
+                                                         p.shift[q], p.dbits[q], hist, kd, vd);
+      RS_CHECK_LAUNCH("rs_lookup_sort bscatter");
+    }
+    return 0;
+  }
   int* tot = hist + (int64_t)kMaxRadix * p.ntiles;
   // ping-pong so that the last pass lands in (keys, vals)
   for (int q = 0; q < p.passes; ++q) {

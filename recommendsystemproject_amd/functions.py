@@ -129,6 +129,9 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
                          agreed=getattr(s, 'agreed', None))
         if c is not None:
             calls[i] = c
+            if pool and mode is not None and args is None:
+                # the gather stages this call's hot rows (runs of equal sorted keys) into LDS
+                s.hot_keys, s.hot_n = c.keys.data_ptr(), c.n
         if args is not None and flat_of(t) is lt.flat:
             if lazy is not None and lazy != args:
                 raise RuntimeError('lazy tables of one gather must share one flat buffer and optimizer')

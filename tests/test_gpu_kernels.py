@@ -2,6 +2,7 @@
 (index work bit-exact)."""
 import math
 
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -131,6 +132,43 @@ def test_gather_small_tables_staged_in_lds(monkeypatch):
     ops.gather_fwd([_seg(kind=_hip.RS_SEG_POOL, dim=8, out_col=0, pool_mode=0, bag=6, vocab=30, idx_stride=6,
                          idx=bad.data_ptr(), table=tb.data_ptr())], B, out, err)
     assert err.item() == 1
+
+
+@pytest.mark.parametrize('zipf,B,V,D,Lb', [(None, 4096, 1_000_000, 128, 50), (1.05, 4096, 1_000_000, 128, 50),
+                                            (1.05, 300, 200_000, 64, 30), (None, 64, 50_000, 32, 8)])
+def test_gather_hot_rows_bitwise(monkeypatch, zipf, B, V, D, Lb):
+    """Pooled (mean / sum) lookups with their sorted call (seg.hot_keys): the rows looked up >= 512
+    times -- the padding row, Zipf-hot rows -- are staged into LDS per workgroup and served from
+    there; the result is bitwise the plain gather's (RSYS_NO_HOT_ROWS=1) and matches torch."""
+    from recommendsystemproject_amd import synth
+    g = np.random.default_rng(B + D)
+    ids_np = synth._ids(g, V, (B, Lb), zipf)
+    k = g.integers(0, Lb + 1, size=B)
+    ids_np = np.where(np.arange(Lb)[None, :] < k[:, None], ids_np, 0)  # right-padded with row 0
+    ids = torch.from_numpy(ids_np).to(DEV)
+    t = rnd(V, D, seed=3)
+    n = B * Lb
+    keys = torch.empty(n, dtype=torch.int32, device=DEV)
+    vals = torch.empty(n, dtype=torch.int32, device=DEV)
+    ws = torch.empty(int(_hip.lib().rs_lookup_sort_ws_bytes(n, V)) // 4 + 1, dtype=torch.int32, device=DEV)
+    _hip.call('rs_lookup_sort', ids.data_ptr(), 8, B, Lb, Lb, V, keys.data_ptr(), vals.data_ptr(), ws.data_ptr(),
+              ops.stream())
+    for mode in ('mean', 'sum'):
+        outs = []
+        for off in ('', '1'):
+            monkeypatch.setenv('RSYS_NO_HOT_ROWS', off)
+            seg = _seg(kind=_hip.RS_SEG_POOL, dim=D, out_col=4, pool_mode=_hip.RS_POOL[mode], bag=Lb, vocab=V,
+                       idx_stride=Lb, idx=ids.data_ptr(), table=t.data_ptr())
+            seg.hot_keys, seg.hot_n = keys.data_ptr(), n
+            out = torch.zeros(B, D + 8, device=DEV)
+            err = torch.zeros(1, dtype=torch.int32, device=DEV)
+            ops.gather_fwd([seg], B, out, err)
+            assert err.item() == 0
+            outs.append(out)
+        assert torch.equal(outs[0], outs[1]), (zipf, mode, (outs[0] - outs[1]).abs().max().item())
+        ref = t[ids].sum(1) / (Lb if mode == 'mean' else 1)
+        assert torch.allclose(outs[0][:, 4:4 + D], ref, atol=1e-5)
+    monkeypatch.setenv('RSYS_NO_HOT_ROWS', '')
 
 
 def test_gather_bit_exact_all_kinds():

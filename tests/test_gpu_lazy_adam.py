@@ -25,15 +25,16 @@ LR, B1, B2, EPS = 1e-2, 0.9, 0.999, 1e-8
 SENT = 0xFFFFFFFF
 
 
-def _sort(ids, vocab, bag=None, stride=None):
-    """rs_lookup_sort of a [rows, bag] id tensor on the device -> (keys, vals) as numpy uint32."""
+def _sort(ids, vocab, bag=None, stride=None, no_ws=False):
+    """rs_lookup_sort of a [rows, bag] id tensor on the device -> (keys, vals) as numpy uint32.
+    no_ws: no workspace (n <= 4096: the one-workgroup radix sort instead of the counting sort)."""
     rows = ids.shape[0]
     bag = bag or (ids.shape[1] if ids.dim() == 2 else 1)
     stride = stride or (ids.stride(0) if ids.dim() == 2 else 1)
     n = rows * bag
     keys = torch.empty(max(n, 1), dtype=torch.int32, device=DEV)
     vals = torch.empty(max(n, 1), dtype=torch.int32, device=DEV)
-    wsb = int(_hip.lib().rs_lookup_sort_ws_bytes(n, vocab))
+    wsb = 0 if no_ws else int(_hip.lib().rs_lookup_sort_ws_bytes(n, vocab))
     ws = torch.empty(wsb // 4 + 1, dtype=torch.int32, device=DEV) if wsb else None
     _hip.call('rs_lookup_sort', ids.data_ptr(), ids.element_size(), rows, bag, stride, vocab,
               keys.data_ptr(), vals.data_ptr(), None if ws is None else ws.data_ptr(), ops.stream())
@@ -47,12 +48,15 @@ def _expect(ids_np, vocab):
     return key[order].astype(np.uint32), order.astype(np.uint32)
 
 
-@pytest.mark.parametrize('n,bag,vocab,dtype', [
-    (1, 1, 300, torch.int64), (4096, 1, 1_000_000, torch.int64), (3000, 3, 19, torch.int64),
-    (4097, 1, 10_000_000, torch.int64), (204_800, 50, 10_000_000, torch.int64),
-    (100_000, 1, 100_000_000, torch.int32), (65_536, 4, 65_536, torch.int64),
-    (819_200, 1, 100_000_000, torch.int64)])
-def test_lookup_sort_bit_exact(n, bag, vocab, dtype):
+@pytest.mark.parametrize('n,bag,vocab,dtype,no_ws', [
+    (1, 1, 300, torch.int64, False), (4096, 1, 1_000_000, torch.int64, False), (3000, 3, 19, torch.int64, False),
+    (4096, 1, 10_000_000, torch.int64, True), (3000, 3, 19, torch.int64, True), (257, 1, 1000, torch.int32, False),
+    (8192, 1, 10_000_000, torch.int64, False), (6000, 2, 1_000_000, torch.int32, False),
+    (8193, 1, 10_000_000, torch.int64, False),
+    (4097, 1, 10_000_000, torch.int64, False), (204_800, 50, 10_000_000, torch.int64, False),
+    (100_000, 1, 100_000_000, torch.int32, False), (65_536, 4, 65_536, torch.int64, False),
+    (819_200, 1, 100_000_000, torch.int64, False)])
+def test_lookup_sort_bit_exact(n, bag, vocab, dtype, no_ws):
     g = np.random.default_rng(n + bag)
     rows = max(n // bag, 1)
     ids = g.integers(0, vocab, size=(rows, bag))
@@ -62,7 +66,7 @@ def test_lookup_sort_bit_exact(n, bag, vocab, dtype):
         ids.reshape(-1)[3] = vocab + 5                       # out of range
         ids.reshape(-1)[7] = -2
     t = torch.from_numpy(ids).to(dtype).to(DEV)
-    keys, vals = _sort(t, vocab)
+    keys, vals = _sort(t, vocab, no_ws=no_ws)
     ek, ev = _expect(ids, vocab)
     assert np.array_equal(keys.cpu().numpy().view(np.uint32)[:ids.size], ek)
     assert np.array_equal(vals.cpu().numpy().view(np.uint32)[:ids.size], ev)
