@@ -126,8 +126,8 @@ def load_traffic(args, B, entry, name, dtype, zipf, hard_negatives, suffix=''):
     path = args.traffic
     if path == 'none':
         return None
-    if path == 'auto':
-        path = os.path.join(ROOT, 'profiles', f'traffic_{name}_{dtype}{suffix}.json')
+    if path == 'auto':  # Zipf-id runs of a config have their own files (traffic_c3_zipf_fp32_gather.json)
+        path = os.path.join(ROOT, 'profiles', f'traffic_{name}{"_zipf" if zipf else ""}_{dtype}{suffix}.json')
     if not os.path.exists(path):
         return None
     tr = json.load(open(path))
@@ -876,7 +876,9 @@ def _extra_short(r):
             'gather_frac': _frac(g, 'rs_gather_fwd', 'frac'),
             'catchup_gather_frac': _frac(g, 'catchup_gather', 'frac'),
             'step_roofline_frac': _frac(r, 'step_roofline', 'frac'),
-            'cpu_baseline_value': _frac(r, 'cpu_baseline', 'value')}
+            'cpu_baseline_value': _frac(r, 'cpu_baseline', 'value'),
+            'cpu_baseline_steps': _frac(r, 'cpu_baseline', 'steps'),
+            'cpu_baseline_of': r.get('cpu_baseline_of', r['config']['workload'].split(':')[0])}
 
 
 def compact_line(out):
@@ -991,7 +993,11 @@ def main():
                 nm = key.rsplit('_bf16', 1)[0] if key.endswith('_bf16') else key
                 nm = 'c3' if nm == 'c3_zipf' else nm
                 if 'error' not in extras[key]:
+                    # one oracle run per config: the oracle computes in fp32 with a dense step whose
+                    # cost does not depend on the ids, so the bf16 and Zipf entries share it
                     extras[key]['cpu_baseline'] = cpu.get(nm)
+                    if nm != key:
+                        extras[key]['cpu_baseline_of'] = nm
             out['c1_cpu_baseline'] = cpu.get('c1')
     if rank == 0:
         out['peaks_measured'] = peaks

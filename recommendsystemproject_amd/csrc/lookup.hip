@@ -1315,7 +1315,8 @@ extern "C" int rs_lookup_sort(const void* ids, int id_bytes, int rows, int bag, 
   if (n == 0) return 0;
   hipStream_t st = as_stream(stream);
   const SortPlan p = make_plan(n, vocab);
-  if (n <= kRankMax && ws) {  // the counting sort (its partials in ws)
+  // the counting sort (its partials in ws); RSYS_SORT_NO_RANK=1 (A/B): the radix paths below
+  if (n <= kRankMax && ws && !getenv_flag("RSYS_SORT_NO_RANK")) {
     const int nb = (int)cdiv(n, kRankBlock);
     rank_partial_kernel<<<dim3(nb, nb), kRankBlock, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, (int)n,
                                                               static_cast<int*>(ws));

@@ -32,7 +32,7 @@ import threading
 import torch
 import torch.distributed as dist
 
-from . import _hip
+from . import _hip, streams
 from .flat import SEG_MEAN, SEG_SUM, ensure_flat, flat_of
 
 
@@ -258,7 +258,8 @@ def pad_ids(ids32, rows, bag, rmax, bmax):
 
 def allreduce_flat_grad(flat_grad: torch.Tensor):
     """Sum the flat gradient over ranks (the mean is folded into the optimizer's grad_scale)."""
-    dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM)
+    with streams.on_root():
+        dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM)
 
 
 class GradBuckets:
@@ -288,7 +289,10 @@ class GradBuckets:
     def _launch(self, b):
         lo, hi = self.spans[b]
         self.launched += 1
-        self.works.append((b, dist.all_reduce(self.f.grad[lo:hi], op=dist.ReduceOp.SUM, async_op=True)))
+        # issued from the root stream when a tower's side stream is current (streams.on_root: RCCL's
+        # stream forked from a side stream breaks the captured step); waited for on the root
+        with streams.on_root(sync=False):
+            self.works.append((b, dist.all_reduce(self.f.grad[lo:hi], op=dist.ReduceOp.SUM, async_op=True)))
 
     def writer(self, params, delta):
         b = _bucket_of(params)
@@ -453,10 +457,11 @@ class _ExchangeBuffers:
 
 
 def _all_gather(out, inp):
-    if dist.get_backend() == 'nccl':
-        dist.all_gather_into_tensor(out, inp)
-    else:
-        dist.all_gather(list(out.chunk(dist.get_world_size())), inp)
+    with streams.on_root():
+        if dist.get_backend() == 'nccl':
+            dist.all_gather_into_tensor(out, inp)
+        else:
+            dist.all_gather(list(out.chunk(dist.get_world_size())), inp)
 
 
 all_gather_into = _all_gather
@@ -466,7 +471,8 @@ def all_to_all(out, inp):
     """out block s = rank s's inp block `rank` (equal splits along dim 0): RCCL's all-to-all; on
     other backends (gloo: ranks sharing one GPU in tests) through host copies."""
     if dist.get_backend() == 'nccl':
-        dist.all_to_all_single(out, inp)
+        with streams.on_root():
+            dist.all_to_all_single(out, inp)
         return
     o = torch.empty(out.shape, dtype=out.dtype)
     dist.all_to_all_single(o, inp.cpu())
@@ -478,7 +484,8 @@ def reduce_scatter_sum(out, inp):
     reduce-scatter; other backends (gloo sharing one GPU in tests): an all-reduce of inp and the
     block."""
     if dist.get_backend() == 'nccl':
-        dist.reduce_scatter_tensor(out, inp)
+        with streams.on_root():
+            dist.reduce_scatter_tensor(out, inp)
         return
     dist.all_reduce(inp)
     r = dist.get_rank()

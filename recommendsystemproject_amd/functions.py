@@ -23,7 +23,7 @@ import os
 import torch
 from torch.autograd.function import once_differentiable
 
-from . import _hip, ops, precision
+from . import _hip, ops, precision, streams
 from . import dist as _dp
 from .flat import SEG_MEAN, SEG_ONE, SEG_SUM, flat_of, grad_of, lookup_table
 
@@ -77,7 +77,7 @@ def _call_stream(parent, k):
     key = (parent.device.index, _skey(parent), k)
     st = _CALL_STREAMS.get(key)
     if st is None:
-        st = _CALL_STREAMS[key] = torch.cuda.Stream(device=parent.device)
+        st = _CALL_STREAMS[key] = streams.side_stream(parent.device)
     return st
 
 
@@ -140,8 +140,10 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
         return c
 
     order = list(groups.values())
+    # no fork from a side stream (the item tower's, or the user tower's own): a fork of a fork
+    # breaks hipGraph capture on this ROCm (streams.py)
     fork = (len(order) > 1 and os.environ.get('RSYS_TOWER_STREAMS', '1') != '0' and
-            os.environ.get('RSYS_LOOKUP_STREAMS', '1') != '0')
+            os.environ.get('RSYS_LOOKUP_STREAMS', '1') != '0' and torch.cuda.is_available() and streams.can_fork())
     if not fork:
         for idxs in order:
             for i in idxs:
@@ -264,7 +266,7 @@ def _gather_bwd_split(segs, rows, dout):
     heavy = [sg for sg in segs if sg.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL) and
              rows * (sg.bag if sg.kind == _hip.RS_SEG_POOL else 1) >= _HEAVY_LOOKUPS]
     if (len(heavy) < 2 or os.environ.get('RSYS_GRAD_STREAMS', '0') != '1' or
-            os.environ.get('RSYS_TOWER_STREAMS', '1') == '0' or not dout.is_cuda):
+            os.environ.get('RSYS_TOWER_STREAMS', '1') == '0' or not dout.is_cuda or not streams.can_fork()):
         ops.gather_bwd(segs, rows, dout)
         return
     main = torch.cuda.current_stream()
@@ -439,7 +441,8 @@ class _WgradBranch:
     def __init__(self, *tensors):
         self.on = (os.environ.get('RSYS_WGRAD_STREAM', '0') == '1' and
                    os.environ.get('RSYS_TOWER_STREAMS', '1') != '0' and
-                   all(t.is_cuda for t in tensors) and not any(_is_fake(t) for t in tensors))
+                   all(t.is_cuda for t in tensors) and not any(_is_fake(t) for t in tensors) and
+                   streams.can_fork())
         self.tensors = tensors
 
     def __enter__(self):
@@ -448,7 +451,7 @@ class _WgradBranch:
         main = torch.cuda.current_stream()
         side = self._streams.get(main.device)
         if side is None:
-            side = self._streams[main.device] = torch.cuda.Stream(device=main.device)
+            side = self._streams[main.device] = streams.side_stream(main.device)
         side.wait_stream(main)
         for t in self.tensors:  # made on the main stream, read on the side one
             t.record_stream(side)

@@ -65,10 +65,17 @@ def body():
         y2 = y2 + 1
         cur.wait_stream(tower)
         return y1, y2, h1, h2
-    if v in ('chain', 'chain_fresh'):
+    if v == 'fork_fresh':  # one level: a stream made here forks from the capturing stream and joins back
+        a_st = torch.cuda.Stream()
+        a_st.wait_stream(cur)
+        with torch.cuda.stream(a_st):
+            y1 = x * 2
+        cur.wait_stream(a_st)
+        return y1
+    if v in ('chain', 'chain_fresh', 'chain_dj'):
         # a fork of a fork: cur -> A, A -> B, B joined into A, A joined into cur (the user tower on
         # its own stream forking its per-table lookup stream: TwoTowerModel RSYS_USER_STREAM=1)
-        a_st = tower if v == 'chain' else torch.cuda.Stream()
+        a_st = tower if v == 'chain' else torch.cuda.Stream()  # chain_fresh / chain_dj: new streams
         a_st.wait_stream(cur)
         with torch.cuda.stream(a_st):
             y1 = x * 2
@@ -79,6 +86,8 @@ def body():
             a_st.wait_stream(b_st)
             y1 = y1 + y2
         cur.wait_stream(a_st)
+        if v == 'chain_dj':  # the grandchild also joined straight into the origin
+            cur.wait_stream(b_st)
         return y1, y2
     if v == 'autograd':
         y = Fn.apply(w)
