@@ -751,6 +751,19 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
                               'frac_of_measured_copy': round(gbs / (peaks or {}).get('hbm_copy_GBs', HBM_MEASURED_GBS), 4),
                               'bytes_per_step': round(g['bytes'] / 3),
                               'ms_per_step': round(g['ms'] / 3, 4), 'entries': list(members)}
+            if k == 'catchup_gather' and lazy_rows:
+                # the catch-up's other bound: its replay of the skipped zero-gradient Adam steps is VALU
+                # work (adam.h adam_replay_zero: per element pair and step 9 packed fp32 operations at 4
+                # cycles and 4 transcendentals at 8 -- MI355X_MICROARCH.md issue costs -- on 64 lanes),
+                # modelled with every distinct row (batches - 1) steps stale, the bench's cycle
+                el_steps = sum(D * r for D, _, r in lazy_rows) / 3 * max(args.batches - 1, 0)
+                valu_ms = el_steps * 34.0 / 64 / (1024 * 2.4e9) * 1e3
+                ms_c = summ['rs_sorted_catchup']['ms'] / 3
+                gather_roof[k]['catchup_valu_model'] = {
+                    'element_steps_per_step': round(el_steps), 'valu_bound_ms': round(valu_ms, 4),
+                    'catchup_ms_per_step': round(ms_c, 4), 'frac': round(valu_ms / ms_c, 4) if ms_c > 0 else None,
+                    'model': '34 SIMD cycles per element and replayed step, 1024 SIMDs x 2.4 GHz, '
+                             'rows (batches - 1) steps stale'}
             if k == 'rs_gather_fwd':  # PMC traffic of the gather (profiles/traffic_<cfg>_<dt>_gather.json)
                 tr = load_traffic(args, B, 'rs_gather_fwd', name, dtype, zipf, hard_negatives, suffix='_gather')
                 gather_roof[k]['traffic'] = tr['hbm_bytes_per_launch'] if tr else None
@@ -875,6 +888,7 @@ def _extra_short(r):
             'roofline_frac': _frac(r, 'roofline', 'frac'), 'roofline_kernel': _frac(r, 'roofline', 'kernel'),
             'gather_frac': _frac(g, 'rs_gather_fwd', 'frac'),
             'catchup_gather_frac': _frac(g, 'catchup_gather', 'frac'),
+            'catchup_valu_frac': _frac(g, 'catchup_gather', 'catchup_valu_model', 'frac'),
             'step_roofline_frac': _frac(r, 'step_roofline', 'frac'),
             'cpu_baseline_value': _frac(r, 'cpu_baseline', 'value'),
             'cpu_baseline_steps': _frac(r, 'cpu_baseline', 'steps'),
@@ -896,6 +910,9 @@ def compact_line(out):
     g = out.get('gather_roofline') or {}
     line['gather_roofline'] = {k: {'frac': v.get('frac'), 'achieved': v.get('achieved'), 'ms_per_step': v.get('ms_per_step'),
                                    'traffic': v.get('traffic')} for k, v in g.items()}
+    for k, v in g.items():
+        if v.get('catchup_valu_model'):
+            line['gather_roofline'][k]['catchup_valu_frac'] = v['catchup_valu_model']['frac']
     line['step_roofline'] = out.get('step_roofline')
     line['cpu_baseline'] = _cpu_short(out.get('cpu_baseline'))
     c1 = out.get('c1_cpu_baseline')

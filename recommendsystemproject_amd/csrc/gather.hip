@@ -44,10 +44,14 @@ constexpr int kLazyBagBatch = 8;           // the same with exp_avg / exp_avg_sq
 // table holds is staged whole into LDS first (every row of such a table is hot: the genre / age /
 // occupation tables are read thousands of times per step), and its lookups are served from LDS
 constexpr int kStageBytes = 16 * 1024;
-// forward, pooled (mean / sum) lookups of a large table with its sorted call (seg.hot_keys): the
-// hot rows -- runs of >= 2 kHotQ equal sorted keys, found by sampling every kHotQ-th key -- are
-// staged once per workgroup into LDS (up to kHotMax rows) and served from there through flat
-// loads; the segment runs kHotBlocks persistent workgroups (the staging is paid per workgroup)
+// forward, pooled (mean / sum) lookups of a large table with its sorted call (seg.hot_keys), opt-in
+// (RSYS_HOT_ROWS=1): the hot rows -- runs of >= 2 kHotQ equal sorted keys, found by sampling every
+// kHotQ-th key -- are staged once per workgroup into LDS (up to kHotMax rows) and served from there
+// through flat loads; the segment runs kHotBlocks persistent workgroups (the staging is paid per
+// workgroup). Measured slower (round 5, C3 fp32 in the step, two repetitions): the history
+// gather 0.039 -> 0.086 ms per step with uniform ids (the padding row is half the lookups) and
+// 0.038 -> 0.087 ms with Zipf(1.05) ids -- 256 persistent workgroups keep far fewer row loads in
+// flight than the 2,048 short ones, and the hot rows are already served by L2
 constexpr int kHotQ = 256;
 constexpr int kHotMax = 64;
 constexpr int kHotHash = 256;
@@ -1096,7 +1100,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.rpb[s] = 256 / (C * S);
     a.nt[s] = nt;
     a.hot[s] = !bwd && vec && g.kind == RS_SEG_POOL && g.pool_mode != RS_POOL_MAX && g.hot_keys &&
-               g.hot_n >= 2 * kHotQ && !nt && !g.lazy_last && g.dim <= 256 && !getenv_flag("RSYS_NO_HOT_ROWS");
+               g.hot_n >= 2 * kHotQ && !nt && !g.lazy_last && g.dim <= 256 && getenv_flag("RSYS_HOT_ROWS");
     if (a.hot[s]) {
       const int hb = kHotMax * g.dim * 4;
       if (hb > a.stage_lds) a.stage_lds = hb;

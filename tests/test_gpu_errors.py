@@ -133,7 +133,13 @@ def test_rccl_captured_step_row_sharded_world_size_one(monkeypatch):
     all-reduces started inside it + the shard exchange + clip + Adam captured into ONE hipGraph
     (thread_local capture, as bench.py) and replayed for 3 steps on new batches. Deterministic
     mode; the weights after the replays equal an eager run of the same 5 steps bitwise."""
+    import faulthandler
+    import sys
     from recommendsystemproject_amd import ops
+
+    def stage(msg):
+        print(f'[rccl-captured] {msg}', file=sys.stderr, flush=True)
+    faulthandler.dump_traceback_later(100, exit=True)  # a hang prints every thread's stack and ends
     monkeypatch.setenv('RSYS_LAZY_ROWS', '1')
     monkeypatch.setenv('RSYS_SHARD_ROWS', '1')
     monkeypatch.setenv('MASTER_ADDR', '127.0.0.1')
@@ -155,25 +161,39 @@ def test_rccl_captured_step_row_sharded_world_size_one(monkeypatch):
             assert sum(t.shard is not None for t in f.lazy) >= 3
             if mode == 'eager':
                 losses[mode] = [float(train_step(model, x, opt, 1.0, 0.15)) for x in b]
+                stage('eager steps done')
             else:
                 ls = [float(train_step(model, x, opt, 1.0, 0.15)) for x in b[:2]]  # eager warm-up
+                stage('graph mode: eager warm-up done')
                 slot = _clone_batch(b[1])
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, capture_error_mode='thread_local'):
                     loss_static = train_step(model, slot, opt, 1.0, 0.15)
+                stage('captured')
                 for x in b[2:]:
                     _copy_batch(slot, x)
                     g.replay()
                     ls.append(float(loss_static))
+                    stage('replayed')
                 losses[mode] = ls
+                # the graph holds RCCL kernels of the communicator: release it before the process
+                # group is destroyed (ncclCommDestroy waits for the graphs that use the communicator)
+                del g, loss_static
+                torch.cuda.synchronize()
             f.flush()
             torch.cuda.synchronize()
             datas[mode] = f.data.clone()
             assert all(t.calls == [] and t.exchanged is None for t in f.lazy)
+        stage(f"losses eager {losses['eager']} graph {losses['graph']}")
         assert losses['graph'] == losses['eager'], losses
         assert torch.equal(datas['graph'], datas['eager']), (datas['graph'] - datas['eager']).abs().max().item()
+        stage('bitwise equal')
     finally:
+        faulthandler.cancel_dump_traceback_later()
         torch.use_deterministic_algorithms(False)
         ops.sync_deterministic()
+        import gc
+        gc.collect()
+        torch.cuda.synchronize()
         dist.destroy_process_group()

@@ -137,9 +137,10 @@ def test_gather_small_tables_staged_in_lds(monkeypatch):
 @pytest.mark.parametrize('zipf,B,V,D,Lb', [(None, 4096, 1_000_000, 128, 50), (1.05, 4096, 1_000_000, 128, 50),
                                             (1.05, 300, 200_000, 64, 30), (None, 64, 50_000, 32, 8)])
 def test_gather_hot_rows_bitwise(monkeypatch, zipf, B, V, D, Lb):
-    """Pooled (mean / sum) lookups with their sorted call (seg.hot_keys): the rows looked up >= 512
-    times -- the padding row, Zipf-hot rows -- are staged into LDS per workgroup and served from
-    there; the result is bitwise the plain gather's (RSYS_NO_HOT_ROWS=1) and matches torch."""
+    """Pooled (mean / sum) lookups with their sorted call (seg.hot_keys), RSYS_HOT_ROWS=1 (opt-in:
+    measured slower in the step, gather.hip): the rows looked up >= 512 times -- the padding row,
+    Zipf-hot rows -- are staged into LDS per workgroup and served from there; the result is
+    bitwise the plain gather's and matches torch."""
     from recommendsystemproject_amd import synth
     g = np.random.default_rng(B + D)
     ids_np = synth._ids(g, V, (B, Lb), zipf)
@@ -155,8 +156,8 @@ def test_gather_hot_rows_bitwise(monkeypatch, zipf, B, V, D, Lb):
               ops.stream())
     for mode in ('mean', 'sum'):
         outs = []
-        for off in ('', '1'):
-            monkeypatch.setenv('RSYS_NO_HOT_ROWS', off)
+        for on in ('1', ''):
+            monkeypatch.setenv('RSYS_HOT_ROWS', on)
             seg = _seg(kind=_hip.RS_SEG_POOL, dim=D, out_col=4, pool_mode=_hip.RS_POOL[mode], bag=Lb, vocab=V,
                        idx_stride=Lb, idx=ids.data_ptr(), table=t.data_ptr())
             seg.hot_keys, seg.hot_n = keys.data_ptr(), n
@@ -168,7 +169,7 @@ def test_gather_hot_rows_bitwise(monkeypatch, zipf, B, V, D, Lb):
         assert torch.equal(outs[0], outs[1]), (zipf, mode, (outs[0] - outs[1]).abs().max().item())
         ref = t[ids].sum(1) / (Lb if mode == 'mean' else 1)
         assert torch.allclose(outs[0][:, 4:4 + D], ref, atol=1e-5)
-    monkeypatch.setenv('RSYS_NO_HOT_ROWS', '')
+    monkeypatch.setenv('RSYS_HOT_ROWS', '')
 
 
 def test_gather_bit_exact_all_kinds():

@@ -1,0 +1,15 @@
+#!/bin/bash
+# round-5 profile set: rocprofv3 kernel-trace summaries (C2 bf16, C3 fp32) with PMC traffic of each
+# line's dominant entry point; PMC traffic of the gather at C3 (uniform and Zipf ids) and of C5's
+# dominant entry (bf16 and fp32, 10 hard negatives); C3 fp32's one-step timeline.
+# Outputs: gpurun_out/prof_<tag>/ (traffic.json, summary.txt), gpurun_out/tl_c3_fp32/.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+bash tools/gpu_prof_all.sh \
+  "c2_bf16|auto|--config c2 --extra=" \
+  "c3_fp32|auto|--config c3 --dtype fp32 --extra=" \
+  "c3_fp32_gather|rs_gather_fwd|--config c3 --dtype fp32 --extra=|notrace" \
+  "c3z_fp32_gather|rs_gather_fwd|--config c3 --dtype fp32 --zipf 1.05 --extra=|notrace" \
+  "c5_bf16|auto|--config c5 --hard-negatives 10 --extra=|notrace" \
+  "c5_fp32|auto|--config c5 --dtype fp32 --hard-negatives 10 --extra=|notrace" || exit 1
+CONFIG=c3 DT=fp32 bash tools/gpu_timeline.sh
