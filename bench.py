@@ -399,7 +399,12 @@ LAZY_ROW_BYTES = {
     'rs_sorted_adam_batch': lambda rows: sum(r * (32.0 * D + 16.0) for D, _, r in rows),
     'rs_sorted_sqnorm_batch': lambda rows: sum(r * 4.0 * D for D, _, r in rows),
 }
-LAZY_ENTRIES = ('rs_lookup_sort', 'rs_sorted_catchup', 'rs_segsum', 'rs_sorted_sqnorm_batch', 'rs_sorted_adam_batch')
+# round 5: the dense region rides in the first sorted batch's launch (+ 28 B / 4 B per dense param)
+LAZY_ROW_BYTES['rs_sorted_adam_batch_dense'] = LAZY_ROW_BYTES['rs_sorted_adam_batch']
+LAZY_ROW_BYTES['rs_sorted_sqnorm_batch_dense'] = LAZY_ROW_BYTES['rs_sorted_sqnorm_batch']
+DENSE_BYTES_PER_PARAM = {'rs_adam_step': 28.0, 'rs_sorted_adam_batch_dense': 28.0, 'rs_sorted_sqnorm_batch_dense': 4.0}
+LAZY_ENTRIES = ('rs_lookup_sort', 'rs_sorted_catchup', 'rs_segsum', 'rs_sorted_sqnorm_batch', 'rs_sorted_adam_batch',
+                'rs_sorted_sqnorm_batch_dense', 'rs_sorted_adam_batch_dense')
 
 
 def optimizer_roofline(summ, rows, flat_numel, dense_numel, ms_step, args, B, name, dtype, zipf, hard_negatives):
@@ -420,7 +425,8 @@ def optimizer_roofline(summ, rows, flat_numel, dense_numel, ms_step, args, B, na
         ms = summ[k]['ms'] / steps
         by = (LAZY_ROW_BYTES[k](rows) if k in LAZY_ROW_BYTES else summ[k]['bytes']) / steps
         if k == 'rs_adam_step':
-            by = 28.0 * dense_numel  # the dense Adam covers [0, dense_numel) only
+            by = 0.0
+        by += DENSE_BYTES_PER_PARAM.get(k, 0.0) * dense_numel  # the dense region [0, dense_numel)
         ent[k] = {'ms_per_step': round(ms, 4), 'bytes_per_step': round(by),
                   'GBs': round(by / (ms * 1e-3) / 1e9, 1) if ms > 0 else None,
                   'frac': round(by / (ms * 1e-3) / (PEAK_HBM_GBS * 1e9), 4) if ms > 0 else None}
@@ -568,7 +574,8 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
         rows = _flat.profile_call_rows(_flat.PROFILE_CALLS)
         _flat.PROFILE_CALLS = None
         if target in LAZY_ROW_BYTES:  # per-row work: priced from this step's distinct-row counts
-            pb.bytes = LAZY_ROW_BYTES[target](rows)
+            pb.bytes = (LAZY_ROW_BYTES[target](rows) +
+                        DENSE_BYTES_PER_PARAM.get(target, 0.0) * ensure_flat(model).dense_numel)
         if rank == 0:
             print(json.dumps({'pmc_bracket': target, 'launches': pb.launches,
                               'alg_bytes_per_launch': pb.bytes / max(pb.launches, 1),

@@ -503,6 +503,11 @@ int rs_clip_coef(const double* ws, int nparts, float max_norm, float* total_norm
                  void* stream);
 /* the same, and *counter += 1 in the same launch (the optimizer's device step count, which
  * rs_adam_step's step_dev then reads: the step that clips needs no separate counter launch) */
+/* the same, and in the same launch the lazy tables' Adam constants of the next step (rs_adam_prepare:
+ * *step += 1, consts[*step] = {lr / bc1, 1 / sqrt(bc2)}); one launch instead of two (round 5) */
+int rs_clip_coef_prepare(const double* ws, int nparts, float max_norm, float* total_norm, float* coef,
+                         int64_t* step, float* consts, int cap, float lr, float beta1, float beta2,
+                         void* stream);
 int rs_clip_coef_step(const double* ws, int nparts, float max_norm, float* total_norm, float* coef,
                       int64_t* counter, void* stream);
 int rs_scale_inplace(float* g, int64_t n, float scale, const float* coef, void* stream);
@@ -532,8 +537,8 @@ int rs_sparse_flush(float* p, float* m, float* v, int* last, int64_t V, int D, c
  * One forward lookup of a large table (a [rows, bag] id matrix, int64 or int32, row stride
  * row_stride) is sorted by row id: keys[n] ascending (ids outside [0, vocab) last, as
  * 0xFFFFFFFF), vals[n] = the lookup index r * bag + l, ascending within a row (stable LSD radix
- * sort of rs_lookup_sort_ws_bytes of workspace; n <= 8192: a counting sort over the whole chip,
- * two launches; n <= 4096 also runs without a workspace, one workgroup's radix passes).
+ * sort of rs_lookup_sort_ws_bytes of workspace; n <= 4096: one workgroup's radix passes, one
+ * launch; 4096 < n <= 8192: a counting sort over the whole chip, two launches).
  * Every per-row operation then walks the distinct rows (run heads) of keys:
  *   rs_sorted_catchup  replay skipped zero-gradient Adam steps before the gather reads the rows
  *                      (bitwise equal to dense Adam); rs_lookup_catchup does the same straight
@@ -583,6 +588,16 @@ typedef struct rs_sorted_call {
 int rs_sorted_adam_batch(const rs_sorted_call_t* calls, int ncalls, const int64_t* step,
                          const float* consts, float beta1, float beta2, float eps, float weight_decay,
                          float scale, const float* coef, void* stream);
+/* The same two batches with the flat buffer's dense region [0, n) in the same launch (round 5):
+ * rs_grad_sqnorm's partials of g (rs_sqnorm_parts(n) of them) into ws_dense, and rs_adam_step's
+ * update of p, g, m, v (step constants from *step, lr) -- the same partitions, the same bits as the
+ * separate launches (clip_grad_norm_ + Adam.step, training_utils.py:53-56, train_twotower.py:111). */
+int rs_sorted_sqnorm_batch_dense(const rs_sorted_call_t* calls, int ncalls, float scale, double* ws,
+                                 const float* g, int64_t n, double* ws_dense, void* stream);
+int rs_sorted_adam_batch_dense(const rs_sorted_call_t* calls, int ncalls, const int64_t* step,
+                               const float* consts, float beta1, float beta2, float eps, float weight_decay,
+                               float scale, const float* coef, float* p, float* g, float* m, float* v,
+                               int64_t n, float lr, void* stream);
 int rs_sorted_sqnorm_batch(const rs_sorted_call_t* calls, int ncalls, float scale, double* ws,
                            void* stream);
 int rs_sorted_adam(const uint32_t* keys, int64_t n, int D, float* p, float* g, float* m, float* v,

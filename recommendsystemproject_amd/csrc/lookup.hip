@@ -468,7 +468,9 @@ __global__ __launch_bounds__(kTileThreads) void sort_tile_kernel(
 //                        them into tile order (by digit) through LDS and stores them from there, so
 //                        a digit's keys leave the tile as one contiguous run (coalesced stores).
 // Stable (tile order, then wave-major key order within a tile): the same keys and values as the
-// 1,024-key tiles (RSYS_SORT_SMALL_TILES=1 keeps those for A/B).
+// 1,024-key tiles. Opt-in (RSYS_SORT_BIG_TILES=1): measured slower in the C3 step (history call
+// 3 x (6.5 + 14.4) us against 3 x (hist + scan + scatter) ~ 55 us: the wave-major ranking of 4,096
+// keys on one workgroup costs more than the launch it saves).
 __global__ __launch_bounds__(kTileThreads) void sort_bhist_kernel(
     const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab,
     const uint32_t* __restrict__ src, int64_t n, int shift, int dbits, int* __restrict__ hist) {
@@ -849,17 +851,108 @@ __global__ __launch_bounds__(256) void sorted_rows_kernel(RowArgs a) {
 // several calls in one launch (the optimizer's per-call Adam steps / clip partials: one dispatch
 // instead of one per call); call c owns workgroups [first[c], first[c + 1])
 constexpr int kRowBatchMax = 8;
+
+// The dense region of the flat buffer riding in the same launch (round 5: one launch less each for
+// the clip partials and the Adam step of a step with lazy tables -- ~4.5 us of launch floor each on
+// this box): workgroups [0, blocks) do what rs_grad_sqnorm / rs_adam_step do, with the same
+// partition (the same partials, the same bits), the sorted calls the rest.
+struct DensePart {
+  float* p; float* g; float* m; float* v;  // Adam: all four; sqnorm: g
+  int64_t n;
+  int blocks;                              // 0: no dense part
+  float lr, b1, b2;                        // Adam: the step constants come from *step (as rs_adam_step)
+  AdamConst h;
+  double* ws;                              // sqnorm: one partial per dense workgroup
+};
+
 struct RowBatch {
   RowArgs a[kRowBatchMax];
   int first[kRowBatchMax + 1];
   int n;
+  DensePart d;
 };
+
+// rs_grad_sqnorm's and rs_adam_step's grids (optim.hip sq_blocks / adam blocks)
+static int dense_sq_blocks(int64_t n) {
+  int64_t b = (n + 256 * 16 - 1) / (256 * 16);
+  return (int)(b > 1024 ? 1024 : (b < 1 ? 1 : b));
+}
+static int dense_adam_blocks(int64_t n) {
+  int64_t b = (n / 4 + 255) / 256;
+  return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
+}
+
+template <int OP>
+__device__ __forceinline__ void dense_part(const DensePart& d, const int64_t* step, float scale, const float* coef,
+                                           int bid) {
+#pragma clang fp contract(off)
+  const int64_t stride = (int64_t)d.blocks * 256;
+  if constexpr (OP == kSqnorm) {
+    __shared__ double red[4];
+    double acc = 0.0;
+    const int64_t n4 = d.n / 4;
+    if ((reinterpret_cast<uintptr_t>(d.g) & 15) == 0) {
+      const float4* g4 = reinterpret_cast<const float4*>(d.g);
+      for (int64_t i = bid * 256 + threadIdx.x; i < n4; i += stride) {
+        const float4 v = g4[i];
+        const float a = v.x * scale, b = v.y * scale, c = v.z * scale, e = v.w * scale;
+        acc += (double)(a * a) + (double)(b * b) + (double)(c * c) + (double)(e * e);
+      }
+      for (int64_t i = n4 * 4 + bid * 256 + threadIdx.x; i < d.n; i += stride) {
+        const float a = d.g[i] * scale;
+        acc += (double)(a * a);
+      }
+    } else {
+      for (int64_t i = bid * 256 + threadIdx.x; i < d.n; i += stride) {
+        const float a = d.g[i] * scale;
+        acc += (double)(a * a);
+      }
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) d.ws[bid] = red[0] + red[1] + red[2] + red[3];
+  } else if constexpr (OP == kAdam) {
+    const float s = scale * (coef ? *coef : 1.f);
+    float step_size, inv_bc2;
+    adam_step_consts((double)d.lr, (double)d.b1, (double)d.b2, (double)*step, &step_size, &inv_bc2);
+    const bool vec = ((reinterpret_cast<uintptr_t>(d.p) | reinterpret_cast<uintptr_t>(d.g) |
+                       reinterpret_cast<uintptr_t>(d.m) | reinterpret_cast<uintptr_t>(d.v)) & 15) == 0;
+    int64_t done = 0;
+    if (vec) {
+      const int64_t n4 = d.n / 4;
+      float4* p4 = reinterpret_cast<float4*>(d.p);
+      float4* g4 = reinterpret_cast<float4*>(d.g);
+      float4* m4 = reinterpret_cast<float4*>(d.m);
+      float4* v4 = reinterpret_cast<float4*>(d.v);
+      for (int64_t i = bid * 256 + threadIdx.x; i < n4; i += stride) {
+        float4 p = p4[i], g = g4[i], m = m4[i], v = v4[i];
+        adam_update(d.h, step_size, inv_bc2, g.x * s, p.x, m.x, v.x);
+        adam_update(d.h, step_size, inv_bc2, g.y * s, p.y, m.y, v.y);
+        adam_update(d.h, step_size, inv_bc2, g.z * s, p.z, m.z, v.z);
+        adam_update(d.h, step_size, inv_bc2, g.w * s, p.w, m.w, v.w);
+        p4[i] = p; m4[i] = m; v4[i] = v;
+      }
+      done = n4 * 4;
+    }
+    for (int64_t i = done + bid * 256 + threadIdx.x; i < d.n; i += stride) {
+      float p = d.p[i], m = d.m[i], v = d.v[i];
+      adam_update(d.h, step_size, inv_bc2, d.g[i] * s, p, m, v);
+      d.p[i] = p; d.m[i] = m; d.v[i] = v;
+    }
+  }
+}
 
 template <int OP, int G, int U>
 __global__ __launch_bounds__(256) void sorted_rows_batch_kernel(RowBatch b) {
+  if ((int)blockIdx.x < b.d.blocks) {  // uniform per workgroup
+    dense_part<OP>(b.d, b.a[0].step, b.a[0].scale, b.a[0].coef, blockIdx.x);
+    return;
+  }
+  const int bid = (int)blockIdx.x - b.d.blocks;
   int c = 0;
-  while (c + 1 < b.n && (int)blockIdx.x >= b.first[c + 1]) ++c;
-  sorted_rows_body<OP, G, U>(b.a[c], blockIdx.x - b.first[c], b.first[c + 1] - b.first[c]);
+  while (c + 1 < b.n && bid >= b.first[c + 1]) ++c;
+  sorted_rows_body<OP, G, U>(b.a[c], bid - b.first[c], b.first[c + 1] - b.first[c]);
 }
 
 constexpr int kRowGrid = 2048;
@@ -970,7 +1063,24 @@ struct SegArgs {
   float* part;    // [nchunks][2][D]: head / tail partial of runs crossing chunk borders
   int* flags;     // [nchunks]: 1 = a run starts in this chunk and continues past it
   int nchunks;
+  int* cnt;       // the fix kernel's ticket (after the flags; zeroed by segsum_kernel)
 };
+
+// agent-scope (sc1) accesses for the fix kernel's hand-off to its last workgroup (the fence-free
+// form of MI355X_MICROARCH.md: sc1 stores, every storing wave drained, one agent-scope add per
+// workgroup after a barrier, sc1 loads by the last adder -- no L2 write-back fence)
+__device__ __forceinline__ float seg_ld(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int seg_ld(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void seg_st(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void seg_st(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 template <int NV>  // columns per lane (D <= 64 * NV)
 __device__ __forceinline__ void load_contrib(const SegArgs& a, uint32_t e, float inv, float* x) {
@@ -999,14 +1109,17 @@ __device__ __forceinline__ void put_row(const SegArgs& a, int64_t row, const flo
   }
 }
 
-template <int NV>
+template <int NV, bool SC1 = false>
 __device__ __forceinline__ void put_part(const SegArgs& a, int chunk, int which, const float* acc) {
   const int lane = threadIdx.x & 63;
   float* dst = a.part + ((int64_t)chunk * 2 + which) * a.D;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int c = lane + 64 * j;
-    if (c < a.D) dst[c] = acc[j];
+    if (c < a.D) {
+      if (SC1) seg_st(dst + c, acc[j]);
+      else dst[c] = acc[j];
+    }
   }
 }
 
@@ -1141,14 +1254,19 @@ __device__ __forceinline__ void segsum_chunk(const SegArgs& a, int chunk, int2* 
 constexpr int kFixBatch = 16;
 constexpr int kFixBlock = 16;  // chunks per level-1 block: one batch of loads per block wave
 
-template <int NV>
+template <int NV, bool SC1 = false>
 __device__ __forceinline__ void load_vec(const float* src, int D, float* v) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int j = 0; j < NV; ++j) v[j] = lane + 64 * j < D ? src[lane + 64 * j] : 0.f;
+  for (int j = 0; j < NV; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < D ? (SC1 ? seg_ld(src + c) : src[c]) : 0.f;
+  }
 }
 
-template <int NV>
+// SC1: the block partials and flags go out as agent-scope stores (the fused fix kernel's last
+// workgroup reads them)
+template <int NV, bool SC1 = false>
 __device__ __forceinline__ void fix_block(const SegArgs& a, int blk) {
   const int nblk = (a.nchunks + kFixBlock - 1) / kFixBlock;
   if (blk >= nblk) return;
@@ -1198,7 +1316,7 @@ __device__ __forceinline__ void fix_block(const SegArgs& a, int blk) {
           for (int j = 0; j < NV; ++j) acc[j] += hv[u][j];
           if (!(f & kThrough)) {  // ends in chunk c
             if (from_left) {
-              put_part<NV>(a, a.nchunks + blk, 0, acc);
+              put_part<NV, SC1>(a, a.nchunks + blk, 0, acc);
               bflag |= kHead;
             } else {
               put_row<NV>(a, key, acc);
@@ -1217,25 +1335,30 @@ __device__ __forceinline__ void fix_block(const SegArgs& a, int blk) {
     }
     if (open) {  // continues over the block's right border
       if (from_left) {
-        put_part<NV>(a, a.nchunks + blk, 0, acc);
+        put_part<NV, SC1>(a, a.nchunks + blk, 0, acc);
         bflag |= kHead | kThrough;
       } else {
-        put_part<NV>(a, a.nchunks + blk, 1, acc);
+        put_part<NV, SC1>(a, a.nchunks + blk, 1, acc);
         bflag |= kTail;
       }
     }
   }
-  if (lane == 0) a.flags[a.nchunks + blk] = bflag;
+  if (lane == 0) {
+    if (SC1) seg_st(a.flags + a.nchunks + blk, bflag);
+    else a.flags[a.nchunks + blk] = bflag;
+  }
 }
 
-template <int NV>
+template <int NV, bool SC1 = false>
 __device__ __forceinline__ void fix_run(const SegArgs& a, int blk) {
   const int nblk = (a.nchunks + kFixBlock - 1) / kFixBlock;
-  if (blk >= nblk || !(a.flags[a.nchunks + blk] & kTail)) return;
+  if (blk >= nblk) return;
+  const int bf = SC1 ? seg_ld(a.flags + a.nchunks + blk) : a.flags[a.nchunks + blk];
+  if (!(bf & kTail)) return;
   const int64_t lastpos = (int64_t)(blk * kFixBlock + kFixBlock - 1) * kChunk + kChunk - 1;
   const uint32_t key = a.keys[lastpos < a.n ? lastpos : a.n - 1];
   float acc[NV];
-  load_vec<NV>(a.part + ((int64_t)(a.nchunks + blk) * 2 + 1) * a.D, a.D, acc);
+  load_vec<NV, SC1>(a.part + ((int64_t)(a.nchunks + blk) * 2 + 1) * a.D, a.D, acc);
   bool done = false;
   for (int b = blk + 1; b < nblk && !done; b += kFixBatch) {
     float h[kFixBatch][NV];
@@ -1243,8 +1366,8 @@ __device__ __forceinline__ void fix_run(const SegArgs& a, int blk) {
 #pragma unroll
     for (int u = 0; u < kFixBatch; ++u) {
       const int bb = b + u < nblk ? b + u : nblk - 1;
-      f[u] = a.flags[a.nchunks + bb];
-      load_vec<NV>(a.part + ((int64_t)(a.nchunks + bb) * 2) * a.D, a.D, h[u]);
+      f[u] = SC1 ? seg_ld(a.flags + a.nchunks + bb) : a.flags[a.nchunks + bb];
+      load_vec<NV, SC1>(a.part + ((int64_t)(a.nchunks + bb) * 2) * a.D, a.D, h[u]);
     }
 #pragma unroll
     for (int u = 0; u < kFixBatch; ++u) {
@@ -1260,8 +1383,27 @@ __device__ __forceinline__ void fix_run(const SegArgs& a, int blk) {
 template <int NV, int G>
 __global__ __launch_bounds__(256) void segsum_kernel(SegArgs a) {
   __shared__ int2 slot[4][64];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.cnt = 0;  // the fix kernel's ticket
   const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (chunk < a.nchunks) segsum_chunk<NV, G>(a, chunk, slot[threadIdx.x >> 6]);
+}
+
+// Both fix levels in one launch (round 5): every wave runs level 1 for its block, the workgroups
+// hand their block partials and flags to the last one to finish (agent-scope stores, one ticket),
+// which runs level 2 for every block. Saves a launch per call (~4.5 us each on this box, three
+// calls on C3's critical path); RSYS_SEGSUM_TWO_FIX=1 keeps the two launches.
+template <int NV>
+__global__ __launch_bounds__(256) void segsum_fix_kernel(SegArgs a) {
+  __shared__ int s_last;
+  fix_block<NV, true>(a, blockIdx.x * 4 + (threadIdx.x >> 6));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(a.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  const int nblk = (a.nchunks + kFixBlock - 1) / kFixBlock;
+  for (int blk = threadIdx.x >> 6; blk < nblk; blk += 4) fix_run<NV, true>(a, blk);
 }
 
 template <int NV>
@@ -1315,8 +1457,10 @@ extern "C" int rs_lookup_sort(const void* ids, int id_bytes, int rows, int bag, 
   if (n == 0) return 0;
   hipStream_t st = as_stream(stream);
   const SortPlan p = make_plan(n, vocab);
-  // the counting sort (its partials in ws); RSYS_SORT_NO_RANK=1 (A/B): the radix paths below
-  if (n <= kRankMax && ws && !getenv_flag("RSYS_SORT_NO_RANK")) {
+  // opt-in (RSYS_SORT_RANK=1): the counting sort (its partials in ws) -- measured no faster than the
+  // one-tile radix sort (two launches of 10.4 + 6.6 us against one of ~18 us: the ~4.5 us launch
+  // floor of this box eats the gain)
+  if (n <= kRankMax && ws && (getenv_flag("RSYS_SORT_RANK") || n > kTileMax)) {
     const int nb = (int)cdiv(n, kRankBlock);
     rank_partial_kernel<<<dim3(nb, nb), kRankBlock, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, (int)n,
                                                               static_cast<int*>(ws));
@@ -1359,7 +1503,7 @@ extern "C" int rs_lookup_sort(const void* ids, int id_bytes, int rows, int bag, 
     return 0;
   }
   int* hist = reinterpret_cast<int*>(tv + n);
-  if (!getenv_flag("RSYS_SORT_SMALL_TILES")) {  // 4,096-key tiles, two launches per pass
+  if (getenv_flag("RSYS_SORT_BIG_TILES")) {  // opt-in: 4,096-key tiles, two launches per pass
     const int nt4 = (int)cdiv(n, kTileMax);
     for (int q = 0; q < p.passes; ++q) {
       const bool to_out = ((p.passes - 1 - q) & 1) == 0;
@@ -1486,11 +1630,15 @@ static int lanes_per_row(int D) { return D <= 16 ? 4 : D <= 32 ? 8 : D <= 64 ? 1
 
 static int sorted_rows_batch(int op, const rs_sorted_call_t* calls, int ncalls, const int64_t* step,
                              const float* consts, float b1, float b2, float eps, float wd, float scale,
-                             const float* coef, double* ws, hipStream_t st) {
+                             const float* coef, double* ws, hipStream_t st, const DensePart* dense = nullptr) {
   RS_CHECK_ARG(calls && ncalls >= 1 && ncalls <= kRowBatchMax, "rs_sorted_*_batch: 1 .. %d calls (got %d)",
                kRowBatchMax, ncalls);
   RowBatch b{};
   b.n = ncalls;
+  if (dense && dense->n > 0) {
+    b.d = *dense;
+    b.d.blocks = op == kSqnorm ? dense_sq_blocks(dense->n) : dense_adam_blocks(dense->n);
+  }
   const int G = lanes_per_row(calls[0].D);
   int wg = 0;
   for (int c = 0; c < ncalls; ++c) {
@@ -1507,6 +1655,7 @@ static int sorted_rows_batch(int op, const rs_sorted_call_t* calls, int ncalls, 
     wg += op == kSqnorm ? kRowGrid : (int)std::max<int64_t>(1, std::min<int64_t>(kRowGrid * 4, cdiv(k.n, 256 / G)));
   }
   b.first[ncalls] = wg;
+  wg += b.d.blocks;
 #define RS_BATCH(OPV)                                                                        \
   switch (G) {                                                                               \
     case 4: sorted_rows_batch_kernel<OPV, 4, 1><<<wg, 256, 0, st>>>(b); break;               \
@@ -1531,6 +1680,27 @@ extern "C" int rs_sorted_adam_batch(const rs_sorted_call_t* calls, int ncalls, c
   RS_CHECK_ARG(step && consts, "rs_sorted_adam_batch: null pointer");
   return sorted_rows_batch(kAdam, calls, ncalls, step, consts, beta1, beta2, eps, weight_decay, scale, coef,
                            nullptr, as_stream(stream));
+}
+
+extern "C" int rs_sorted_adam_batch_dense(const rs_sorted_call_t* calls, int ncalls, const int64_t* step,
+                                          const float* consts, float beta1, float beta2, float eps,
+                                          float weight_decay, float scale, const float* coef, float* p, float* g,
+                                          float* m, float* v, int64_t n, float lr, void* stream) {
+  RS_CHECK_ARG(step && consts && n >= 0 && (n == 0 || (p && g && m && v)), "rs_sorted_adam_batch_dense: bad args");
+  DensePart d{};
+  d.p = p; d.g = g; d.m = m; d.v = v; d.n = n; d.lr = lr; d.b1 = beta1; d.b2 = beta2;
+  d.h = make_hyper(beta1, beta2, eps, weight_decay);
+  return sorted_rows_batch(kAdam, calls, ncalls, step, consts, beta1, beta2, eps, weight_decay, scale, coef,
+                           nullptr, as_stream(stream), &d);
+}
+
+extern "C" int rs_sorted_sqnorm_batch_dense(const rs_sorted_call_t* calls, int ncalls, float scale, double* ws,
+                                            const float* g, int64_t n, double* ws_dense, void* stream) {
+  RS_CHECK_ARG(ws && n >= 0 && (n == 0 || (g && ws_dense)), "rs_sorted_sqnorm_batch_dense: bad args");
+  DensePart d{};
+  d.g = const_cast<float*>(g); d.n = n; d.ws = ws_dense;
+  return sorted_rows_batch(kSqnorm, calls, ncalls, nullptr, nullptr, 0.f, 0.f, 0.f, 0.f, scale, nullptr, ws,
+                           as_stream(stream), &d);
 }
 
 extern "C" int rs_sorted_sqnorm_batch(const rs_sorted_call_t* calls, int ncalls, float scale, double* ws,
@@ -1583,18 +1753,25 @@ extern "C" int rs_segsum(const uint32_t* keys, const uint32_t* vals, int64_t n, 
   a.part = static_cast<float*>(ws);
   const int64_t np = a.nchunks + (a.nchunks + kFixBlock - 1) / kFixBlock;
   a.flags = reinterpret_cast<int*>(a.part + np * 2 * D);
+  a.cnt = a.flags + np;  // inside rs_segsum_ws_bytes' 256-byte tail
   hipStream_t st = as_stream(stream);
   const int grid = cdiv(a.nchunks, 4);
   RS_CHECK_ARG(D % 4 == 0 && ldo % 4 == 0 && aligned16(dout) && aligned16(grad),
                "rs_segsum: D, ldo multiples of 4 and 16-byte aligned dout / grad required");
   const int bgrid = cdiv(cdiv(a.nchunks, kFixBlock), 4);
+  const bool two_fix = getenv_flag("RSYS_SEGSUM_TWO_FIX");
 #define RS_SEGSUM(NV, G)                                               \
   segsum_kernel<NV, G><<<grid, 256, 0, st>>>(a);                       \
   RS_CHECK_LAUNCH("rs_segsum");                                        \
-  segsum_fix_blocks_kernel<NV><<<bgrid, 256, 0, st>>>(a);              \
-  RS_CHECK_LAUNCH("rs_segsum blocks");                                 \
-  segsum_fix_runs_kernel<NV><<<bgrid, 256, 0, st>>>(a);                \
-  RS_CHECK_LAUNCH("rs_segsum runs");
+  if (two_fix) {                                                       \
+    segsum_fix_blocks_kernel<NV><<<bgrid, 256, 0, st>>>(a);            \
+    RS_CHECK_LAUNCH("rs_segsum blocks");                               \
+    segsum_fix_runs_kernel<NV><<<bgrid, 256, 0, st>>>(a);              \
+    RS_CHECK_LAUNCH("rs_segsum runs");                                 \
+  } else {                                                             \
+    segsum_fix_kernel<NV><<<bgrid, 256, 0, st>>>(a);                   \
+    RS_CHECK_LAUNCH("rs_segsum fix");                                  \
+  }
   if (D <= 16) { RS_SEGSUM(1, 4) }
   else if (D <= 32) { RS_SEGSUM(1, 8) }
   else if (D <= 64) { RS_SEGSUM(1, 16) }

@@ -69,6 +69,37 @@ __global__ __launch_bounds__(1024) void clip_coef_kernel(const double* __restric
   if (counter) *counter += 1;  // the optimizer's step count (rs_clip_coef_step): one launch less
 }
 
+// rs_clip_coef_prepare: the clip coefficient and, in the same launch, the lazy tables' Adam step
+// constants for the next step (sparse.hip adam_prepare_kernel's body, the same values)
+__global__ __launch_bounds__(1024) void clip_coef_prepare_kernel(const double* __restrict__ ws, int nb,
+                                                                 float max_norm, float* total_norm, float* coef,
+                                                                 int64_t* step, float2* consts, int cap, float lr,
+                                                                 float b1, float b2) {
+  __shared__ double red[16];
+  double t = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 1024) t += ws[i];
+  t = wave_sum(t);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  t = 0.0;
+  for (int w = 0; w < 16; ++w) t += red[w];
+  const float norm = (float)sqrt(t);
+  if (total_norm) *total_norm = norm;
+  float c = max_norm / (norm + 1e-6f);
+  *coef = c < 1.f ? c : 1.f;
+  const int64_t s = *step + 1;
+  *step = s;
+  if (s < cap) {
+    float2 k;
+    adam_step_consts((double)lr, (double)b1, (double)b2, (double)s, &k.x, &k.y);
+    consts[s] = k;
+    if (s == 1) consts[0] = make_float2(__int_as_float(cap), __int_as_float(0));
+  } else {
+    consts[0] = make_float2(__int_as_float(cap), __int_as_float(1));
+  }
+}
+
 __global__ void scale_kernel(float* __restrict__ g, int64_t n, float scale,
                              const float* __restrict__ coef) {
   const float s = scale * (coef ? *coef : 1.f);
@@ -159,6 +190,17 @@ extern "C" int rs_clip_coef_step(const double* ws, int nparts, float max_norm, f
   RS_CHECK_ARG(ws && coef && counter && nparts >= 1, "rs_clip_coef_step: bad args");
   clip_coef_kernel<<<1, 1024, 0, as_stream(stream)>>>(ws, nparts, max_norm, total_norm, coef, counter);
   RS_CHECK_LAUNCH("rs_clip_coef_step");
+  return 0;
+}
+
+extern "C" int rs_clip_coef_prepare(const double* ws, int nparts, float max_norm, float* total_norm, float* coef,
+                                    int64_t* step, float* consts, int cap, float lr, float beta1, float beta2,
+                                    void* stream) {
+  RS_CHECK_ARG(ws && coef && step && consts && nparts >= 1 && cap >= 2, "rs_clip_coef_prepare: bad args");
+  clip_coef_prepare_kernel<<<1, 1024, 0, as_stream(stream)>>>(ws, nparts, max_norm, total_norm, coef, step,
+                                                              reinterpret_cast<float2*>(consts), cap, lr, beta1,
+                                                              beta2);
+  RS_CHECK_LAUNCH("rs_clip_coef_prepare");
   return 0;
 }
 

@@ -149,16 +149,18 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
             for i in idxs:
                 one(i)
         return calls, lazy
-    # the largest table's work stays on the current stream, the others fork
+    # the largest table's work stays on the current stream, the others fork (onto the stream
+    # TwoTowerModel prefers -- the item tower's, ahead of its tower -- or a stream per table)
     order.sort(key=lambda idxs: -sum(int(segs[i].vocab) for i in idxs))
     main = torch.cuda.current_stream()
     sides = []
+    pref = streams.preferred_lookup_stream()
     for k, idxs in enumerate(order):
         if k == 0:
             for i in idxs:
                 one(i)
             continue
-        st = _call_stream(main, k)
+        st = pref if pref is not None and pref.device == main.device else _call_stream(main, k)
         st.wait_stream(main)
         with torch.cuda.stream(st):
             for i in idxs:
@@ -167,7 +169,8 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
                     for x in (c.keys, c.vals, c.ws):
                         if isinstance(x, torch.Tensor):
                             x.record_stream(main)
-        sides.append(st)
+        if st not in sides:
+            sides.append(st)
     for st in sides:
         main.wait_stream(st)
     return calls, lazy

@@ -9,6 +9,7 @@ total norm and the clip coefficient kept on the device.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -69,10 +70,13 @@ class _DeviceClip:
         self.norm = torch.zeros((), device=device, dtype=torch.float32)
         self.coef = torch.ones((), device=device, dtype=torch.float32)
 
-    def compute(self, g, n, max_norm, scale=1.0, lazy=(), counter=None):
+    def compute(self, g, n, max_norm, scale=1.0, lazy=(), counter=None, prepare=None):
         """2-norm of g[:n] plus the distinct rows of every lazy table's step calls (their other
         rows hold no gradient), one double partial per block, summed in one fixed order.
-        `counter` (a device int64 step count): advanced by the same launch (rs_clip_coef_step)."""
+        `counter` (a device int64 step count): advanced by the same launch (rs_clip_coef_step);
+        `prepare` = (step, consts, cap, lr, b1, b2): the lazy tables' next-step Adam constants
+        made by the same launch too (rs_clip_coef_prepare). The dense partials ride in the first
+        sorted batch's launch (rs_sorted_sqnorm_batch_dense)."""
         L = _hip.lib()
         nd = int(L.rs_sqnorm_parts(n))
         ns = int(L.rs_sorted_sqnorm_parts())
@@ -84,17 +88,29 @@ class _DeviceClip:
             for i, c in enumerate(t.step_calls()):
                 work.append((t, c, owner, i))
         ws = torch.empty(nd + ns * len(work) + 2, dtype=torch.float64, device=g.device)
-        _hip.call('rs_grad_sqnorm', g.data_ptr(), n, float(scale), ws.data_ptr(), ops.stream())
-        # every call's partials in one launch per row class (call k's at nd + k * ns)
+        # every call's partials in one launch per row class (call k's at nd + k * ns); the dense
+        # region's in the first of those launches
         items = [(_sorted_call(t, c, i, g=g, owner=owner), k) for k, (t, c, owner, i) in enumerate(work)]
-        for batch in _sorted_batches(items):
+        batches = _sorted_batches(items)
+        if not batches or os.environ.get('RSYS_OPT_FUSE', '1') == '0':
+            _hip.call('rs_grad_sqnorm', g.data_ptr(), n, float(scale), ws.data_ptr(), ops.stream())
+        for j, batch in enumerate(batches):
             arr = (_hip.SortedCall * len(batch))(*[sc for sc, _ in batch])
-            _hip.call('rs_sorted_sqnorm_batch', C.addressof(arr), len(batch), float(scale),
-                      ws.data_ptr() + 8 * (nd + batch[0][1] * ns), ops.stream())
+            if j == 0 and os.environ.get('RSYS_OPT_FUSE', '1') != '0':
+                _hip.call('rs_sorted_sqnorm_batch_dense', C.addressof(arr), len(batch), float(scale),
+                          ws.data_ptr() + 8 * (nd + batch[0][1] * ns), g.data_ptr(), n, ws.data_ptr(), ops.stream())
+            else:
+                _hip.call('rs_sorted_sqnorm_batch', C.addressof(arr), len(batch), float(scale),
+                          ws.data_ptr() + 8 * (nd + batch[0][1] * ns), ops.stream())
         first = next((k for k, w in enumerate(work) if getattr(w[0], 'shard', None) is not None), None)
         if first is not None:
             torch.distributed.all_reduce(ws[nd + first * ns:nd + len(work) * ns])
-        if counter is not None:
+        if prepare is not None:
+            step, consts, cap, lr, b1, b2 = prepare
+            _hip.call('rs_clip_coef_prepare', ws.data_ptr(), nd + ns * len(work), float(max_norm),
+                      self.norm.data_ptr(), self.coef.data_ptr(), step.data_ptr(), consts.data_ptr(), int(cap),
+                      float(lr), float(b1), float(b2), ops.stream())
+        elif counter is not None:
             _hip.call('rs_clip_coef_step', ws.data_ptr(), nd + ns * len(work), float(max_norm),
                       self.norm.data_ptr(), self.coef.data_ptr(), counter.data_ptr(), ops.stream())
         else:
@@ -210,26 +226,34 @@ class Adam(torch.optim.Optimizer):
                 st['step'] += 1
                 lr, eps, wd = float(group['lr']), float(group['eps']), float(group['weight_decay'])
                 coef = None
-                counted = False
+                counted = prepared = False
+                fuse = os.environ.get('RSYS_OPT_FUSE', '1') != '0'
+                if f.lazy and st['step'] >= CONSTS_CAP - 1:
+                    raise RuntimeError(f'lazy Adam: more than {CONSTS_CAP - 2} steps; raise optim.CONSTS_CAP')
                 if clip_max_norm is not None and clip_max_norm > 0:
                     if self._clip is None:
                         self._clip = _DeviceClip(f.data.device)
-                    # dense step count advanced by the clip's own launch (no rs_counter_add)
+                    # the device step count (and the lazy tables' step constants) advanced by the
+                    # clip coefficient's own launch (no rs_counter_add / rs_adam_prepare launch)
                     counted = not f.lazy
+                    prepared = bool(f.lazy) and fuse
                     self._clip.compute(f.grad, f.dense_numel, clip_max_norm, self.grad_scale, f.lazy,
-                                       counter=st['step_dev'] if counted else None)
+                                       counter=st['step_dev'] if counted else None,
+                                       prepare=(st['step_dev'], st['consts'], CONSTS_CAP, lr, b1, b2)
+                                       if prepared else None)
                     coef = self._clip.coef.data_ptr()
                 # device-side step count: the same launch replays correctly inside a hipGraph
-                if f.lazy:
-                    if st['step'] >= CONSTS_CAP - 1:
-                        raise RuntimeError(f'lazy Adam: more than {CONSTS_CAP - 2} steps; raise optim.CONSTS_CAP')
+                if f.lazy and not prepared:
                     _hip.call('rs_adam_prepare', st['step_dev'].data_ptr(), st['consts'].data_ptr(),
                               CONSTS_CAP, lr, float(b1), float(b2), ops.stream())
-                elif not counted:
+                elif not f.lazy and not counted:
                     _hip.call('rs_counter_add', st['step_dev'].data_ptr(), 1, ops.stream())
-                _hip.call('rs_adam_step', f.data.data_ptr(), f.grad.data_ptr(), st['m'].data_ptr(),
-                          st['v'].data_ptr(), f.dense_numel, lr, float(b1), float(b2), eps, wd, 0,
-                          st['step_dev'].data_ptr(), float(self.grad_scale), coef, 0, ops.stream())
+                dense_args = (f.data.data_ptr(), f.grad.data_ptr(), st['m'].data_ptr(), st['v'].data_ptr(),
+                              f.dense_numel)
+                dense_done = not (f.lazy and fuse)
+                if dense_done:
+                    _hip.call('rs_adam_step', *dense_args, lr, float(b1), float(b2), eps, wd, 0,
+                              st['step_dev'].data_ptr(), float(self.grad_scale), coef, 0, ops.stream())
                 if f.lazy:
                     hyper = (float(b1), float(b2), eps, wd)
                     f.lazy_opt = dict(m=st['m'], v=st['v'], step_dev=st['step_dev'],
@@ -247,8 +271,17 @@ class Adam(torch.optim.Optimizer):
                                                        owner=None if len(calls) <= 1 else owner), None))
                     for batch in _sorted_batches(items):
                         arr = (_hip.SortedCall * len(batch))(*[sc for sc, _ in batch])
-                        _hip.call('rs_sorted_adam_batch', C.addressof(arr), len(batch), st['step_dev'].data_ptr(),
-                                  st['consts'].data_ptr(), *hyper, float(self.grad_scale), coef, ops.stream())
+                        if not dense_done:  # the dense region's Adam in the first batch's launch
+                            _hip.call('rs_sorted_adam_batch_dense', C.addressof(arr), len(batch),
+                                      st['step_dev'].data_ptr(), st['consts'].data_ptr(), *hyper,
+                                      float(self.grad_scale), coef, *dense_args, lr, ops.stream())
+                            dense_done = True
+                        else:
+                            _hip.call('rs_sorted_adam_batch', C.addressof(arr), len(batch), st['step_dev'].data_ptr(),
+                                      st['consts'].data_ptr(), *hyper, float(self.grad_scale), coef, ops.stream())
+                    if not dense_done:
+                        _hip.call('rs_adam_step', *dense_args, lr, float(b1), float(b2), eps, wd, 0,
+                                  st['step_dev'].data_ptr(), float(self.grad_scale), coef, 0, ops.stream())
                     for t in f.lazy:
                         t.end_step()
                 continue

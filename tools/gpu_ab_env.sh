@@ -13,9 +13,10 @@ for cd in $CFGS; do
     python3 - "$rep" "$cfg" "$dt" "$lab" gpurun_out/ab_${lab}_${cfg}_${dt}.log <<'PY' | tee -a gpurun_out/ab_env.txt
 import json, sys
 rep, cfg, dt, lab, path = sys.argv[1:]
-d = [json.loads(l) for l in open(path) if l.startswith('{"metric')][-1]
+d = [json.loads(l)['bench_detail'] for l in open(path) if l.startswith('{"bench_detail"')][-1]
 k = d['kernel_ms_per_step']
-keys = ('rs_lookup_sort', 'rs_sorted_catchup', 'rs_gather_fwd', 'rs_gather_bwd', 'rs_sorted_adam_batch', 'rs_tower_fwd', 'rs_tower_bwd')
+keys = ('rs_lookup_sort', 'rs_sorted_catchup', 'rs_gather_fwd', 'rs_gather_bwd', 'rs_segsum', 'rs_sorted_adam_batch',
+        'rs_sorted_adam_batch_dense', 'rs_tower_fwd', 'rs_tower_bwd')
 print(rep, cfg, dt, lab, d['ms_per_step'], ' '.join(f'{x[3:]}={k.get(x, 0):.4f}' for x in keys), flush=True)
 PY
   done
