@@ -695,7 +695,10 @@ int ce_fused_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_
   a.part_m = ws; a.part_s = ws + (int64_t)NS * B; a.diag = ws + (int64_t)2 * NS * B;
   // the finish kernel's ticket, after diag (rs_inbatch_ce_fused_ws_bytes: the backward's larger
   // workspace leaves room); zeroed by the tile kernel's first workgroup, re-armed by the last adder
-  const bool fused_sum = !getenv_flag("RSYS_CE_SUM_LAUNCH");
+  // RSYS_CE_SUM_FUSED=1: the mean by the finish kernel's last workgroup (round 5) -- measured
+  // slower: ce_finish_fwd 5 -> 19.5 us against rs_sum's 4.8 (1,024 workgroups' tickets on one
+  // counter), C3 fp32 0.816 vs 0.813, so the separate launch stays the default
+  const bool fused_sum = getenv_flag("RSYS_CE_SUM_FUSED");
   a.cnt = fused_sum ? reinterpret_cast<int*>(ws + (int64_t)2 * NS * B + B) : nullptr;
   const int NSr = cdiv(B, a.split_rows);
   launch_tiles<0, F32>(a, D, NSr, st);

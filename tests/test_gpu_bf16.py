@@ -37,7 +37,8 @@ def bf16_mode():
 
 @pytest.mark.parametrize('N,K,kind', [(256, 64, 'fwd_relu'), (192, 64, 'fwd_bias'), (256, 64, 'fwd_plain'),
                                       (64, 256, 'dgrad_beta'), (64, 192, 'dgrad_beta'),
-                                      (256, 64, 'dgrad_mask'), (64, 64, 'dgrad')])
+                                      (256, 64, 'dgrad_mask'), (64, 64, 'dgrad'),
+                                      (64, 48, 'fwd_plain'), (48, 64, 'dgrad')])
 def test_bf16_streaming_gemm(N, K, kind, bf16_mode):
     M = 40960
     x = rnd(M, K, seed=1)
