@@ -36,14 +36,16 @@ __device__ __forceinline__ void adam_update(const AdamConst& h, float step_size,
 // order. The elements run interleaved (independent chains), two at a time as packed pairs
 // (v_pk_mul_f32 / v_pk_add_f32); an element whose moments are zero stays put exactly (m stays 0,
 // the update is p - step * (0 * rcp(eps)) = p). wd != 0 takes adam_update itself.
-template <int W>
-__device__ __forceinline__ void adam_replay_zero(const AdamConst& h, const float2* __restrict__ consts, int from,
-                                                 int to, float* p, float* m, float* v) {
+// CF: the step constants' accessor, s -> consts[s] (a global table, or a window of it staged in
+// LDS by the caller: the replay's one dependent load per step was the catch-up's latency chain)
+template <int W, class CF>
+__device__ __forceinline__ void adam_replay_zero(const AdamConst& h, CF cst, int from, int to, float* p, float* m,
+                                                 float* v) {
 #pragma clang fp contract(off)
   if (from > to) return;
   if (h.wd != 0.f) {
     for (int s = from; s <= to; ++s) {
-      const float2 c = consts[s];
+      const float2 c = cst(s);
 #pragma unroll
       for (int j = 0; j < W; ++j) adam_update(h, c.x, c.y, 0.f, p[j], m[j], v[j]);
     }
@@ -61,7 +63,7 @@ __device__ __forceinline__ void adam_replay_zero(const AdamConst& h, const float
   const f2v omb1 = f2v{h.one_m_b1, h.one_m_b1}, b2 = f2v{h.b2, h.b2}, eps = f2v{h.eps, h.eps};
   const f2v zero = f2v{0.f, 0.f};
   for (int s = from; s <= to; ++s) {
-    const float2 c = consts[s];
+    const float2 c = cst(s);
     const f2v ss = f2v{c.x, c.x}, ib = f2v{c.y, c.y};
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
@@ -112,12 +114,29 @@ __device__ __forceinline__ void adam_replay_mv(const AdamConst& h, int from, int
 
 // A lazy row's catch-up from its state -- moments at step lm, parameters at step lp >= lm (equal
 // when weight_decay != 0) -- to step `to`: the moments alone to lp, then full zero-gradient steps.
+template <int W, class CF>
+__device__ __forceinline__ void adam_catch_row_f(const AdamConst& h, CF cst, int lm, int lp, int to, float* p,
+                                                 float* m, float* v) {
+  if (lp > lm) adam_replay_mv<W>(h, lm + 1, lp < to ? lp : to, m, v);
+  adam_replay_zero<W>(h, cst, (lp > lm ? lp : lm) + 1, to, p, m, v);
+}
+
 template <int W>
 __device__ __forceinline__ void adam_catch_row(const AdamConst& h, const float2* __restrict__ consts, int lm, int lp,
                                                int to, float* p, float* m, float* v) {
-  if (lp > lm) adam_replay_mv<W>(h, lm + 1, lp < to ? lp : to, m, v);
-  adam_replay_zero<W>(h, consts, (lp > lm ? lp : lm) + 1, to, p, m, v);
+  adam_catch_row_f<W>(h, [consts](int s) { return consts[s]; }, lm, lp, to, p, m, v);
 }
+
+// The last kConstWin steps' constants staged in LDS by every workgroup of a row kernel (steps
+// t - kConstWin + 1 .. t; older steps read the global table): one load round trip per workgroup
+// instead of one per replayed step and row
+constexpr int kConstWin = 64;
+struct ConstWin {
+  const float2* g;
+  const float2* w;  // LDS window
+  int lo;           // step of w[0]
+  __device__ __forceinline__ float2 operator()(int s) const { return s >= lo ? w[s - lo] : g[s]; }
+};
 
 // per-step constants {lr / bc1(t), 1 / sqrt(bc2(t))}, computed in double then rounded once
 __host__ __device__ inline void adam_step_consts(double lr, double b1, double b2, double t,

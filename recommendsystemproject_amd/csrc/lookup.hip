@@ -704,14 +704,24 @@ constexpr int kRowUnroll = 1;
 template <int OP, int G, int U>
 __device__ __forceinline__ void sorted_rows_body(const RowArgs& a, int bid, int nblocks) {
   __shared__ double red[4];
+  __shared__ float2 cwin[(OP == kCatchup || OP == kAdam) ? kConstWin : 1];
   const int gl = threadIdx.x & (G - 1);
   double acc = 0.0;
   int t = 0;
   float2 ct = make_float2(0.f, 0.f);
   float s = 1.f;
-  if (OP == kCatchup || OP == kAdam) t = clamp_step(a.consts, *a.step);
+  ConstWin cw{a.consts, cwin, 0};
+  if (OP == kCatchup || OP == kAdam) {
+    t = clamp_step(a.consts, *a.step);
+    cw.lo = t - kConstWin + 1;
+    if (threadIdx.x < kConstWin) {
+      const int st = cw.lo + (int)threadIdx.x;
+      cwin[threadIdx.x] = a.consts[st > 0 ? st : 0];
+    }
+    __syncthreads();
+  }
   if (OP == kAdam) {
-    ct = a.consts[t];
+    ct = cwin[kConstWin - 1];
     s = a.scale * (a.coef ? *a.coef : 1.f);
   }
   const int64_t ngroups = (int64_t)nblocks * (256 / G);
@@ -793,7 +803,7 @@ __device__ __forceinline__ void sorted_rows_body(const RowArgs& a, int bid, int 
       if (w > 0) {
         const int64_t o = row[u] * a.D + c0;
         if (OP == kCatchup || OP == kAdam)
-          adam_catch_row<4>(a.h, a.consts, lm[u], lp[u], OP == kCatchup ? t : t - 1, pp[u], mm[u], vv[u]);
+          adam_catch_row_f<4>(a.h, cw, lm[u], lp[u], OP == kCatchup ? t : t - 1, pp[u], mm[u], vv[u]);
         if (OP == kAdam) {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
@@ -986,6 +996,13 @@ template <int G>
 __global__ __launch_bounds__(256) void lookup_catchup_kernel(IdCatchArgs a) {
   const int gl = threadIdx.x & (G - 1);
   const int t = clamp_step(a.consts, *a.step);
+  __shared__ float2 cwin[kConstWin];  // the recent steps' constants (ConstWin)
+  const ConstWin cw{a.consts, cwin, t - kConstWin + 1};
+  if (threadIdx.x < kConstWin) {
+    const int st = cw.lo + (int)threadIdx.x;
+    cwin[threadIdx.x] = a.consts[st > 0 ? st : 0];
+  }
+  __syncthreads();
   const int64_t ngroups = (int64_t)gridDim.x * (256 / G);
   const int c0 = gl * 4;
   const int w = c0 < a.D ? (a.D - c0 < 4 ? a.D - c0 : 4) : 0;
@@ -1024,7 +1041,7 @@ __global__ __launch_bounds__(256) void lookup_catchup_kernel(IdCatchArgs a) {
         vv[j] = j < w ? a.v[o + j] : 0.f;
       }
     }
-    adam_catch_row<4>(a.h, a.consts, lm, lp, t, pp, mm, vv);
+    adam_catch_row_f<4>(a.h, cw, lm, lp, t, pp, mm, vv);
     if (vec) {
       *reinterpret_cast<float4*>(a.p + o) = make_float4(pp[0], pp[1], pp[2], pp[3]);
       if (!p_only) {
