@@ -1419,8 +1419,24 @@ __global__ __launch_bounds__(256) void segsum_fix_kernel(SegArgs a) {
     s_last = __hip_atomic_fetch_add(a.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
+  // level 2 in the last workgroup: only blocks whose run continues past their right border have
+  // work. Their flags are read 256 at a time and the tail blocks listed in LDS first -- the waves
+  // walking every block (fix_run's flag load, then its early return) was ~50 dependent round
+  // trips per wave at C3's 200 history blocks. Each listed block writes its own run's row, so the
+  // order the waves take them in does not matter.
+  __shared__ int tails[256];
+  __shared__ int ntails;
   const int nblk = (a.nchunks + kFixBlock - 1) / kFixBlock;
-  for (int blk = threadIdx.x >> 6; blk < nblk; blk += 4) fix_run<NV, true>(a, blk);
+  for (int b0 = 0; b0 < nblk; b0 += 256) {
+    if (threadIdx.x == 0) ntails = 0;
+    __syncthreads();
+    const int b = b0 + (int)threadIdx.x;
+    const int bf = b < nblk ? seg_ld(a.flags + a.nchunks + b) : 0;
+    if (bf & kTail) tails[atomicAdd(&ntails, 1)] = b;
+    __syncthreads();
+    for (int i = threadIdx.x >> 6; i < ntails; i += 4) fix_run<NV, true>(a, tails[i]);
+    __syncthreads();
+  }
 }
 
 template <int NV>
