@@ -698,6 +698,11 @@ struct RowArgs {
 // per group iteration with their loads issued together; measured slower at U = 4 (168 VGPRs, fewer
 // resident waves: tools/lazy_bench.py), so U = 1.
 constexpr int kRowUnroll = 1;
+// The clip partials (kSqnorm) read one gradient row per position: 4 positions per group iteration
+// with their loads issued together (16 VGPRs of rows; the per-lane accumulation order is that of
+// U = 1: positions i0, i0 + ngroups, ...). Their grid is fixed at kRowGrid workgroups (one partial
+// each), so a group walks ~13 positions at C3 -- one key and one row round trip each at U = 1.
+constexpr int kSqUnroll = 4;
 
 // bid / nblocks: this workgroup's index and count among the workgroups working on `a` (a batched
 // launch deals one contiguous block range to each call)
@@ -1600,7 +1605,7 @@ static int sorted_rows(int op, const uint32_t* keys, int64_t n, int D, float* p,
   switch (op) {
     case kCatchup: RS_ROWS(kCatchup) break;
     case kAdam: RS_ROWS(kAdam) break;
-    case kSqnorm: RS_ROWS(kSqnorm) break;
+    case kSqnorm: RS_ROWS_U(kSqnorm, kSqUnroll) break;
     case kOwner: RS_ROWS(kOwner) break;
     default: RS_ROWS(kZero) break;
   }
@@ -1691,11 +1696,11 @@ static int sorted_rows_batch(int op, const rs_sorted_call_t* calls, int ncalls, 
   wg += b.d.blocks;
 #define RS_BATCH(OPV)                                                                        \
   switch (G) {                                                                               \
-    case 4: sorted_rows_batch_kernel<OPV, 4, 1><<<wg, 256, 0, st>>>(b); break;               \
-    case 8: sorted_rows_batch_kernel<OPV, 8, 1><<<wg, 256, 0, st>>>(b); break;               \
-    case 16: sorted_rows_batch_kernel<OPV, 16, 1><<<wg, 256, 0, st>>>(b); break;             \
-    case 32: sorted_rows_batch_kernel<OPV, 32, 1><<<wg, 256, 0, st>>>(b); break;             \
-    default: sorted_rows_batch_kernel<OPV, 64, 1><<<wg, 256, 0, st>>>(b); break;             \
+    case 4: sorted_rows_batch_kernel<OPV, 4, OPV == kSqnorm ? kSqUnroll : 1><<<wg, 256, 0, st>>>(b); break;               \
+    case 8: sorted_rows_batch_kernel<OPV, 8, OPV == kSqnorm ? kSqUnroll : 1><<<wg, 256, 0, st>>>(b); break;               \
+    case 16: sorted_rows_batch_kernel<OPV, 16, OPV == kSqnorm ? kSqUnroll : 1><<<wg, 256, 0, st>>>(b); break;             \
+    case 32: sorted_rows_batch_kernel<OPV, 32, OPV == kSqnorm ? kSqUnroll : 1><<<wg, 256, 0, st>>>(b); break;             \
+    default: sorted_rows_batch_kernel<OPV, 64, OPV == kSqnorm ? kSqUnroll : 1><<<wg, 256, 0, st>>>(b); break;             \
   }
   if (op == kAdam) {
     RS_BATCH(kAdam)

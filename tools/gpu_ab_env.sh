@@ -15,7 +15,7 @@ import json, sys
 rep, cfg, dt, lab, path = sys.argv[1:]
 d = [json.loads(l)['bench_detail'] for l in open(path) if l.startswith('{"bench_detail"')][-1]
 k = d['kernel_ms_per_step']
-keys = ('rs_lookup_sort', 'rs_sorted_catchup', 'rs_gather_fwd', 'rs_gather_bwd', 'rs_segsum', 'rs_sorted_adam_batch',
+keys = ('rs_lookup_sort', 'rs_sorted_catchup', 'rs_gather_fwd', 'rs_gather_bwd', 'rs_segsum', 'rs_sorted_sqnorm_batch_dense', 'rs_sorted_adam_batch',
         'rs_sorted_adam_batch_dense', 'rs_tower_fwd', 'rs_tower_bwd')
 print(rep, cfg, dt, lab, d['ms_per_step'], ' '.join(f'{x[3:]}={k.get(x, 0):.4f}' for x in keys), flush=True)
 PY
