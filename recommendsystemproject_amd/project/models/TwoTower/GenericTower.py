@@ -84,6 +84,11 @@ class GenericTower(nn.Module):
         L2-normalised [B, output_dims] (GenericTower.py:120-237). `groups` > 1: the batch is G
         blocks of B/G rows (e.g. the N hard-negative slots stacked) and every BatchNorm keeps
         per-block statistics -- identical to G separate passes (T13), in one pass."""
+        return self.head(self.features(input_dict, feature_column_mapping), groups)
+
+    def features(self, input_dict, feature_column_mapping=None):
+        """The forward's first half (GenericTower.py:120-228): the feature gathers, the sequence
+        encoder and the concatenation -> x [B, total input dims]."""
         _hip.require_device(self.feature_bn.weight)
         ensure_flat(self)
         seq_vec = None
@@ -91,7 +96,10 @@ class GenericTower(nn.Module):
             seqd = input_dict['sequence']
             if seqd:
                 seq_vec = self.seq_encoder(seqd)
-        x = library.tower_features(self, input_dict, feature_column_mapping, seq_vec)
+        return library.tower_features(self, input_dict, feature_column_mapping, seq_vec)
+
+    def head(self, x, groups=1):
+        """The forward's second half (GenericTower.py:229-237): feature_bn + MLP_Tower + L2 norm."""
         if tower_chain_supported(self.feature_bn, self.mlp, x, int(groups)):
             # feature_bn + MLP_Tower as one fused kernel chain (training mode)
             ensure_flat(self.mlp)
