@@ -30,19 +30,32 @@ def main():
     w = ops.ws(_hip.lib().rs_inbatch_ce_fused_ws_bytes(B, D), dev)
     st = ops.stream()
 
+    f32 = os.environ.get('CE_F32') == '1'  # the fp32 entry points (exact f32 products, stored S)
+    S = torch.empty(B * int(_hip.lib().rs_inbatch_ce_s_ld(B)), device=dev) if f32 else None
+
     def fwd():
+        if f32:
+            _hip.call('rs_inbatch_ce_fused_f32_fwd', U.data_ptr(), I.data_ptr(), None, 0, 0, ids.data_ptr(), 1,
+                      B, 0, D, 0.15, lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(), S.data_ptr(),
+                      w.data_ptr(), st)
+            return
         _hip.call('rs_inbatch_ce_fused_fwd', U.data_ptr(), I.data_ptr(), None, 0, 0, ids.data_ptr(), 1,
                   B, 0, D, 0.15, lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(), w.data_ptr(), st)
 
     def bwd():
+        if f32:
+            _hip.call('rs_inbatch_ce_fused_f32_bwd', U.data_ptr(), I.data_ptr(), None, 0, 0, ids.data_ptr(), 1,
+                      B, 0, D, 0.15, lse.data_ptr(), None, dU.data_ptr(), dI.data_ptr(), None, S.data_ptr(),
+                      w.data_ptr(), st)
+            return
         _hip.call('rs_inbatch_ce_fused_bwd', U.data_ptr(), I.data_ptr(), None, 0, 0, ids.data_ptr(), 1,
                   B, 0, D, 0.15, lse.data_ptr(), None, dU.data_ptr(), dI.data_ptr(), None, w.data_ptr(), st)
 
     fwd()
     bwd()
     torch.cuda.synchronize()
-    # reference on the same bf16-rounded operands
-    Ub, Ib = U.bfloat16().float(), I.bfloat16().float()
+    # reference on the same operands (bf16-rounded in the bf16 mode)
+    Ub, Ib = (U, I) if f32 else (U.bfloat16().float(), I.bfloat16().float())
     S = Ub @ Ib.T / 0.15
     coll = (ids[:, None] == ids[None, :]) & ~torch.eye(B, dtype=torch.bool, device=dev)
     S = S.masked_fill(coll, -1e9)
@@ -64,7 +77,8 @@ def main():
     tf = ev[0].elapsed_time(ev[1]) / n * 1e3
     tb = ev[1].elapsed_time(ev[2]) / n * 1e3
     fl = 2.0 * B * B * D
-    print(json.dumps({'splits': os.environ.get('RSYS_CE_SPLITS', 'auto'), 'B': B, 'D': D,
+    print(json.dumps({'f32': f32, 'occ': os.environ.get('RSYS_CE_F32_OCC', '0'),
+                      'splits': os.environ.get('RSYS_CE_SPLITS', 'auto'), 'B': B, 'D': D,
                       'fwd_us': round(tf, 1), 'bwd_us': round(tb, 1),
                       'fwd_tflops': round(fl / tf / 1e6, 1), 'bwd_tflops': round(4 * fl / tb / 1e6, 1),
                       'loss_err': abs(float(loss) - float(ref_loss)), 'dU_err': err_u, 'dI_err': err_i}))
