@@ -386,7 +386,12 @@ extern "C" int rs_gemm_add_layernorm(int M, int N, int K, const float* A, int ld
   RS_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || key), "rs_gemm_add_layernorm: bad dropout p");
   if (M == 0) return 0;
   hipStream_t st = as_stream(stream);
-  if (rowgemm_ln_supported(M, N, K, A, lda) && !getenv_flag("RSYS_UNFUSED_LN")) {
+  // bf16 mode, B-row calls (the pruned last encoder layer, M = 4,096): the fused bf16 kernel takes
+  // them too (round 5: one launch instead of the small-M fp32 GEMM + rs_add_layernorm_fwd)
+  const bool small_bf16 = (flags & RS_GEMM_BF16) && M >= 16 && M % 16 == 0 && N == 64 && K % 64 == 0 &&
+                          lda % 4 == 0 && ldw % 4 == 0 && aligned16(A) && aligned16(W) &&
+                          !getenv_flag("RSYS_SMALL_LN_UNFUSED");
+  if ((rowgemm_ln_supported(M, N, K, A, lda) || small_bf16) && !getenv_flag("RSYS_UNFUSED_LN")) {
     StreamArgs sa{};
     sa.M = M; sa.N = N; sa.K = K; sa.alpha = 1.f; sa.beta = 0.f; sa.A = A; sa.lda = lda;
     sa.B = W; sa.ldb = ldw; sa.transB = 1; sa.C = h; sa.ldc = N;
