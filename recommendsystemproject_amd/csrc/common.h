@@ -60,6 +60,9 @@ int partials_reduce(const float* ws, int P, int N, float scale, float beta, floa
 // the same with columns [0, split) -> out0 and [split, N) -> out1
 int partials_reduce2(const float* ws, int P, int N, int split, float scale, float beta, float* out0,
                      float* out1, hipStream_t st);
+// two partials_reduce2 jobs of one shape (ws0 -> a0 | a1, ws1 -> b0 | b1) in one launch
+int partials_reduce2x2(const float* ws0, const float* ws1, int P, int N, int split, float scale, float beta,
+                       float* a0, float* a1, float* b0, float* b1, hipStream_t st);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // debug / A-B switches read at launch time (host only): set and not "0"

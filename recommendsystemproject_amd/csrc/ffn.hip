@@ -937,8 +937,8 @@ extern "C" int rs_ffn_bwd_ln2_bf16(int M, int F, const float* x, const float* W1
   if (p > 0.f) ffn_bwd_bf16_kernel<256, true, true, false, true><<<nb, 512, lds, st>>>(a);
   else ffn_bwd_bf16_kernel<256, true, false, false, true><<<nb, 512, lds, st>>>(a);
   RS_CHECK_LAUNCH("rs_ffn_bwd_ln2_bf16");
-  RS_RET_IF(partials_reduce2(ws, nb, 128, 64, 1.f, 1.f, dgamma1, dbeta1, st));
-  return partials_reduce2(a.ln2_ws, nb, 128, 64, 1.f, 1.f, dgamma2, dbeta2, st);
+  // both LayerNorms' gamma / beta partials in one reduce launch (same order of operations per job)
+  return partials_reduce2x2(ws, a.ln2_ws, nb, 128, 64, 1.f, 1.f, dgamma1, dbeta1, dgamma2, dbeta2, st);
 }
 
 extern "C" int rs_ffn_bwd_bf16(int M, int F, const float* x, const float* W1, const float* b1,

@@ -47,6 +47,54 @@ __global__ __launch_bounds__(1024) void partials_reduce_kernel(const float* __re
   }
 }
 
+// Two independent partials_reduce2 jobs in one launch (blockIdx.y picks the job): the fused FFN
+// backward's LayerNorm 1 and LayerNorm 2 gamma / beta gradients (round 5: one launch less on the
+// C2 backward's critical path, ~4.7 us each)
+struct ReduceJob {
+  const float* ws;
+  int P, N, split;
+  float scale, beta;
+  float* out0;
+  float* out1;
+};
+
+__global__ __launch_bounds__(1024) void partials_reduce_jobs_kernel(ReduceJob j0, ReduceJob j1) {
+  const ReduceJob& j = blockIdx.y == 0 ? j0 : j1;
+  __shared__ float red[16][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if ((int)blockIdx.x * 64 >= j.N) return;  // whole workgroup
+  const int l = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (c < j.N) {
+    int p = l;
+    for (; p + 16 * 7 < j.P; p += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = j.ws[(int64_t)(p + 16 * u) * j.N + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; p < j.P; p += 16) acc += j.ws[(int64_t)p * j.N + c];
+  }
+  red[l][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (l == 0 && c < j.N) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
+    float* o = c < j.split ? j.out0 + c : j.out1 + (c - j.split);
+    *o = (j.beta != 0.f ? j.beta * *o : 0.f) + j.scale * t;
+  }
+}
+
+int partials_reduce2x2(const float* ws0, const float* ws1, int P, int N, int split, float scale, float beta,
+                       float* a0, float* a1, float* b0, float* b1, hipStream_t st) {
+  const ReduceJob j0{ws0, P, N, split, scale, beta, a0, a1}, j1{ws1, P, N, split, scale, beta, b0, b1};
+  partials_reduce_jobs_kernel<<<dim3(cdiv(N, 64), 2), 1024, 0, st>>>(j0, j1);
+  RS_CHECK_LAUNCH("partials_reduce2x2");
+  return 0;
+}
+
 int partials_reduce(const float* ws, int P, int N, float scale, float beta, float* out,
                     hipStream_t st) {
   partials_reduce_kernel<<<cdiv(N, 64), 1024, 0, st>>>(ws, P, N, scale, beta, out);
