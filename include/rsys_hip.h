@@ -667,6 +667,16 @@ int rs_seq_input_dropout_bwd(float* dx, int rows, int N, float p, const int64_t*
 int rs_dropout_bwd(float* dx, int64_t n, float p, const int64_t* key, int site, void* stream);
 
 /* ---------------------------------------------------------------- reductions */
+/* Deferred parameter-gradient reductions (round 5; no reference counterpart -- the optimizer step
+ * of training_utils.py:28-60 is the only reader of these gradients). After rs_reduce_defer(1) the
+ * weight-gradient entry points (rs_gemm_f32's transposed-A weight gradients, rs_wgrad_bf16,
+ * rs_ffn_wgrad_bf16), the fused FFN backward's LayerNorm partials and rs_seq_input_dropout_bwd's
+ * positional partials queue their final split reduction instead of launching it; rs_reduce_flush
+ * runs every queued reduction in one launch on `stream` (the bits of the immediate path) and
+ * rs_reduce_defer(0) ends the queueing. The caller keeps each call's workspace alive until the
+ * flush is queued, and reads none of those gradients before it. */
+int rs_reduce_defer(int on);
+int rs_reduce_flush(void* stream);
 /* out = scale * sum(x[0..n)) (deterministic; mean loss) */
 int rs_sum(const float* x, int n, float scale, float* out, void* stream);
 /* *flag |= bit if x[0..n) holds a NaN (x 16-byte aligned). The loss inputs' NaN guard of

@@ -135,6 +135,8 @@ SIGNATURES = {
     'rs_peak_mfma': (i32, [vp, i32, i32, vp]),
     'rs_peak_mfma_flops': (i64, [i32, i32]),
     'rs_sum': (i32, [vp, i32, f32, vp, vp]),
+    'rs_reduce_defer': (i32, [i32]),
+    'rs_reduce_flush': (i32, [vp]),
     'rs_nan_check': (i32, [vp, i64, vp, i32, vp]),
     'rs_rng_next': (i32, [vp, vp, vp]),
     'rs_adam_prepare': (i32, [vp, vp, i32, f32, f32, f32, vp]),

@@ -60,6 +60,13 @@ int partials_reduce(const float* ws, int P, int N, float scale, float beta, floa
 // the same with columns [0, split) -> out0 and [split, N) -> out1
 int partials_reduce2(const float* ws, int P, int N, int split, float scale, float beta, float* out0,
                      float* out1, hipStream_t st);
+// deferred reductions (reduce.hip): while deferring, reduce_defer_job queues a job for
+// rs_reduce_flush instead of a launch; partials_reduce_any is partials_reduce(2) or a queued job
+bool reduce_deferring();
+void reduce_defer_job(const float* ws, int P, int N, int nr, float* const* outs, const int* begins,
+                      const float* alphas, const float* betas);
+int partials_reduce_any(const float* ws, int P, int N, int split, float scale, float beta, float* out0,
+                        float* out1, hipStream_t st);
 // two partials_reduce2 jobs of one shape (ws0 -> a0 | a1, ws1 -> b0 | b1) in one launch
 int partials_reduce2x2(const float* ws0, const float* ws1, int P, int N, int split, float scale, float beta,
                        float* a0, float* a1, float* b0, float* b1, hipStream_t st);

@@ -136,7 +136,7 @@ extern "C" int rs_seq_input_dropout_bwd(float* dx, int rows, int N, float p, con
   hipStream_t st = as_stream(stream);
   seq_input_dropout_bwd_kernel<<<cdiv(rows, rpb), 256, 0, st>>>(dx, rows, N, rpb, p, key, site_a, site_b, ws);
   RS_CHECK_LAUNCH("rs_seq_input_dropout_bwd");
-  return partials_reduce(ws, cdiv(rows, rpb), N, 1.f, 1.f, pos_grad, st);
+  return partials_reduce_any(ws, cdiv(rows, rpb), N, N, 1.f, 1.f, pos_grad, nullptr, st);
 }
 
 extern "C" int rs_dropout_bwd(float* dx, int64_t n, float p, const int64_t* key, int site,

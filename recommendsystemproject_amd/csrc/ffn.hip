@@ -988,6 +988,14 @@ extern "C" int rs_ffn_wgrad_bf16(int M, int F, const float* x, const float* W1, 
   hipStream_t st = as_stream(stream);
   ffn_wgrad_bf16_kernel<<<cdiv(M, rpb), 512, wgrad_fused_lds(), st>>>(a, ws, rpb);
   RS_CHECK_LAUNCH("rs_ffn_wgrad_bf16");
+  if (reduce_deferring()) {  // queued for rs_reduce_flush: dW1 | dW2 | db1 | db2 += the column sums
+    constexpr int FD = WG_F * D;
+    float* outs[4] = {dW1, dW2, db1, db2};
+    const int begins[4] = {0, FD, 2 * FD, 2 * FD + WG_F};
+    const float al[4] = {1.f, 1.f, 1.f, 1.f}, be[4] = {1.f, 1.f, 1.f, 1.f};
+    reduce_defer_job(ws, cdiv(M, rpb), WG_OUT, 4, outs, begins, al, be);
+    return 0;
+  }
   ffn_wgrad_reduce_kernel<<<cdiv(WG_OUT, 64), 1024, 0, st>>>(ws, cdiv(M, rpb), dW1, dW2, db1, db2);
   RS_CHECK_LAUNCH("rs_ffn_wgrad_bf16 reduce");
   return 0;

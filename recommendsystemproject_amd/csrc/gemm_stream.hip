@@ -1159,6 +1159,22 @@ int64_t wgrad_ws_bytes(int M, int N, int K) {
   return (int64_t)wgrad_blocks(K) * ((int64_t)M * N + M) * (int64_t)sizeof(float);
 }
 
+// wgrad_reduce_kernel's work as deferred jobs (reduce.hip) while the library defers reductions:
+// C = alpha * sum + beta * C over the M x N partials (a contiguous C only), rowsum += alpha * sum
+bool wgrad_reduce_deferred(const StreamArgs& s, int P) {
+  if (!reduce_deferring() || s.ldc != s.N) return false;
+  const int total = s.M * s.N;
+  float* oc[1] = {s.C};
+  const int b0[1] = {0};
+  const float al[1] = {s.alpha}, bc[1] = {s.beta}, br[1] = {1.f};
+  reduce_defer_job(s.ws, P, total, 1, oc, b0, al, bc);
+  if (s.rowsum) {
+    float* orow[1] = {s.rowsum};
+    reduce_defer_job(s.ws + (int64_t)P * total, P, s.M, 1, orow, b0, al, br);
+  }
+  return true;
+}
+
 int wgrad_bf16_launch(const StreamArgs& s, bool y_bf16, bool x_bf16, hipStream_t st) {
   const int mo_pad = (s.M + 31) / 32 * 32, no_pad = (s.N + 31) / 32 * 32;
   const int nb = wgrad_blocks(s.K);
@@ -1187,6 +1203,7 @@ int wgrad_bf16_launch(const StreamArgs& s, bool y_bf16, bool x_bf16, hipStream_t
   }
 #undef RS_WB
   RS_CHECK_LAUNCH("wgrad bf16");
+  if (wgrad_reduce_deferred(s, nblk)) return 0;
   const int total = s.M * s.N + (s.rowsum ? s.M : 0);
   wgrad_reduce_kernel<<<cdiv(total, 64), 1024, 0, st>>>(s, nblk);
   RS_CHECK_LAUNCH("wgrad reduce");
@@ -1212,6 +1229,7 @@ int wgrad_launch(const StreamArgs& s, hipStream_t st) {
   }
 #undef RS_WG
   RS_CHECK_LAUNCH("wgrad");
+  if (wgrad_reduce_deferred(s, nblk)) return 0;
   const int total = s.M * s.N + (s.rowsum ? s.M : 0);
   wgrad_reduce_kernel<<<cdiv(total, 64), 1024, 0, st>>>(s, nblk);
   RS_CHECK_LAUNCH("wgrad reduce");

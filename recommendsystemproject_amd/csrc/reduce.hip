@@ -1,6 +1,9 @@
 // Deterministic column / full reductions (bias gradients, positional-embedding gradients,
 // LayerNorm gamma/beta gradients, mean loss). Two passes with a fixed summation order so that
 // repeated runs are bitwise identical (no float atomics).
+#include <algorithm>
+#include <vector>
+
 #include "common.h"
 
 namespace rs {
@@ -87,8 +90,15 @@ __global__ __launch_bounds__(1024) void partials_reduce_jobs_kernel(ReduceJob j0
   }
 }
 
+int partials_reduce_any(const float* ws, int P, int N, int split, float scale, float beta, float* out0,
+                        float* out1, hipStream_t st);
+
 int partials_reduce2x2(const float* ws0, const float* ws1, int P, int N, int split, float scale, float beta,
                        float* a0, float* a1, float* b0, float* b1, hipStream_t st) {
+  if (reduce_deferring()) {
+    partials_reduce_any(ws0, P, N, split, scale, beta, a0, a1, st);
+    return partials_reduce_any(ws1, P, N, split, scale, beta, b0, b1, st);
+  }
   const ReduceJob j0{ws0, P, N, split, scale, beta, a0, a1}, j1{ws1, P, N, split, scale, beta, b0, b1};
   partials_reduce_jobs_kernel<<<dim3(cdiv(N, 64), 2), 1024, 0, st>>>(j0, j1);
   RS_CHECK_LAUNCH("partials_reduce2x2");
@@ -108,6 +118,135 @@ int partials_reduce2(const float* ws, int P, int N, int split, float scale, floa
   partials_reduce_kernel<<<cdiv(N, 64), 1024, 0, st>>>(ws, P, N, scale, beta, out0, out1, split);
   RS_CHECK_LAUNCH("partials_reduce2");
   return 0;
+}
+
+// ---------------------------------------------------------------- deferred reductions (round 5)
+// A backward's parameter-gradient reductions (the weight gradients' split partials, the fused FFN
+// weight gradient's, the LayerNorm gamma / beta and positional-embedding partials) are only read
+// by the optimizer. Between rs_reduce_defer(1) and rs_reduce_flush the library queues them as jobs
+// instead of launching one small reduce kernel each (~4.5 us of launch floor apiece, nine of them
+// on the C2 backward's critical path), and the flush runs every queued job in ONE launch. Each job
+// sums its partials exactly as partials_reduce_kernel does (16 strided lanes with 8 loads in
+// flight, then the fixed 16-way LDS order) and writes out = beta * out + alpha * sum per column
+// range, so the deferred and the immediate paths give the same bits. The caller keeps every
+// partials buffer alive until the flush is queued (ops.deferred_reduce).
+namespace {
+
+constexpr int kJobRanges = 4;
+constexpr int kMaxJobs = 24;
+
+struct JobRange {
+  float* out;
+  int begin;  // first column of this range (ranges ascending, the first at 0)
+  float alpha, beta;
+};
+
+struct RedJob {
+  const float* ws;  // [P][N]
+  int P, N, nr, blk0;
+  JobRange r[kJobRanges];
+};
+
+struct RedJobs {
+  RedJob j[kMaxJobs];
+  int n;
+};
+
+__global__ __launch_bounds__(1024) void reduce_jobs_kernel(RedJobs js) {
+  int k = 0;
+  while (k + 1 < js.n && (int)blockIdx.x >= js.j[k + 1].blk0) ++k;
+  const RedJob& j = js.j[k];
+  __shared__ float red[16][64];
+  const int c = ((int)blockIdx.x - j.blk0) * 64 + (threadIdx.x & 63);
+  const int l = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (c < j.N) {
+    int p = l;
+    for (; p + 16 * 7 < j.P; p += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = j.ws[(int64_t)(p + 16 * u) * j.N + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; p < j.P; p += 16) acc += j.ws[(int64_t)p * j.N + c];
+  }
+  red[l][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (l == 0 && c < j.N) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
+    int q = 0;
+    while (q + 1 < j.nr && c >= j.r[q + 1].begin) ++q;
+    float* o = j.r[q].out + (c - j.r[q].begin);
+    // beta * out + alpha * sum (the partials_reduce / ffn_wgrad_reduce form), alpha * sum when
+    // beta == 0 (wgrad_reduce's: no read, and a -0 stays -0)
+    *o = j.r[q].beta != 0.f ? j.r[q].beta * *o + j.r[q].alpha * t : j.r[q].alpha * t;
+  }
+}
+
+bool g_defer = false;
+std::vector<RedJob> g_jobs;
+
+int launch_jobs(const RedJob* jobs, int n, hipStream_t st) {
+  for (int a = 0; a < n; a += kMaxJobs) {
+    RedJobs js{};
+    js.n = std::min(kMaxJobs, n - a);
+    int blk = 0;
+    for (int i = 0; i < js.n; ++i) {
+      js.j[i] = jobs[a + i];
+      js.j[i].blk0 = blk;
+      blk += cdiv(js.j[i].N, 64);
+    }
+    if (blk == 0) continue;
+    reduce_jobs_kernel<<<blk, 1024, 0, st>>>(js);
+    RS_CHECK_LAUNCH("rs_reduce_flush");
+  }
+  return 0;
+}
+
+}  // namespace
+
+bool reduce_deferring() { return g_defer; }
+
+// queue a job (deferring) -- the caller launches its own kernel otherwise; outs: up to 4 column
+// ranges {out, begin, alpha, beta}
+void reduce_defer_job(const float* ws, int P, int N, int nr, float* const* outs, const int* begins,
+                      const float* alphas, const float* betas) {
+  RedJob j{};
+  j.ws = ws; j.P = P; j.N = N; j.nr = nr;
+  for (int i = 0; i < nr; ++i) j.r[i] = JobRange{outs[i], begins[i], alphas[i], betas[i]};
+  g_jobs.push_back(j);
+}
+
+}  // namespace rs
+
+extern "C" int rs_reduce_defer(int on) {
+  rs::g_defer = on != 0;
+  return 0;
+}
+
+extern "C" int rs_reduce_flush(void* stream) {
+  std::vector<rs::RedJob> jobs;
+  jobs.swap(rs::g_jobs);
+  if (jobs.empty()) return 0;
+  return rs::launch_jobs(jobs.data(), (int)jobs.size(), rs::as_stream(stream));
+}
+
+namespace rs {
+
+int partials_reduce_any(const float* ws, int P, int N, int split, float scale, float beta, float* out0,
+                        float* out1, hipStream_t st) {
+  if (g_defer) {
+    float* outs[2] = {out0, out1};
+    const int begins[2] = {0, split};
+    const float al[2] = {scale, scale}, be[2] = {beta, beta};
+    reduce_defer_job(ws, P, N, out1 && split < N ? 2 : 1, outs, begins, al, be);
+    return 0;
+  }
+  return out1 && split < N ? partials_reduce2(ws, P, N, split, scale, beta, out0, out1, st)
+                           : partials_reduce(ws, P, N, scale, beta, out0, st);
 }
 
 namespace {

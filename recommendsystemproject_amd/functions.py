@@ -693,20 +693,26 @@ class SeqEncoderFn(torch.autograd.Function):
         d, H = proc.target_dim, enc.n_head
         dout = dout.contiguous()
         n = len(ctx.layers)
+        # the encoder's weight / LayerNorm / positional gradient reductions queued and run as one
+        # launch at the end (ops.deferred_reduce): not under data parallelism (the bucket's
+        # all-reduce starts inside seq_input_bwd) nor with the weight gradients on a side stream
+        from .flat import _dp_active
+        defer = not _dp_active() and os.environ.get('RSYS_WGRAD_STREAM', '0') != '1'
         try:
-            if ctx.prune:
-                dx = layer_bwd_last(ctx.layers[n - 1], ctx.layer_saved[n - 1], dout.clone(), ctx.key_pad,
-                                    ctx.last, B, L, d, H, p, key, _layer_site(n - 1))
-                n -= 1
-            else:
-                dx = torch.zeros(B * L, d, device=dout.device, dtype=torch.float32)
-                seg = _seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=ctx.last.data_ptr(),
-                           grad=dx.data_ptr())
-                ops.gather_bwd([seg], B, dout)
-            for i in reversed(range(n)):
-                dx = layer_bwd(ctx.layers[i], ctx.layer_saved[i], dx, ctx.key_pad, B, L, d, H, p, key,
-                               _layer_site(i))
-            seq_input_bwd(proc, ctx.in_saved, dx, B, L, p, key, ctx.params)
+            with ops.deferred_reduce(defer):
+                if ctx.prune:
+                    dx = layer_bwd_last(ctx.layers[n - 1], ctx.layer_saved[n - 1], dout.clone(), ctx.key_pad,
+                                        ctx.last, B, L, d, H, p, key, _layer_site(n - 1))
+                    n -= 1
+                else:
+                    dx = torch.zeros(B * L, d, device=dout.device, dtype=torch.float32)
+                    seg = _seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=ctx.last.data_ptr(),
+                               grad=dx.data_ptr())
+                    ops.gather_bwd([seg], B, dout)
+                for i in reversed(range(n)):
+                    dx = layer_bwd(ctx.layers[i], ctx.layer_saved[i], dx, ctx.key_pad, B, L, d, H, p, key,
+                                   _layer_site(i))
+                seq_input_bwd(proc, ctx.in_saved, dx, B, L, p, key, ctx.params)
         finally:
             # structural join of any weight-gradient branch this backward forked (seq_input_bwd
             # joins on its normal path; an exception or a path that never reaches it joins here)

@@ -5,6 +5,7 @@ current stream handle; all arithmetic runs in librsys_hip.so.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import numpy as np
@@ -24,9 +25,35 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+_DEFER_KEEP = []  # deferred_reduce: the workspaces of this scope, alive until its flush is queued
+
+
 def ws(nbytes: int, device) -> torch.Tensor:
     """Workspace from the caching allocator (capture-safe)."""
-    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+    t = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+    if _DEFER_KEEP:
+        _DEFER_KEEP[-1].append(t)  # a queued reduction reads it at the flush
+    return t
+
+
+@contextlib.contextmanager
+def deferred_reduce(on=True):
+    """The parameter-gradient reductions queued inside run as ONE launch at the end of the scope
+    (rs_reduce_defer / rs_reduce_flush, round 5): nothing inside may read those gradients. Off
+    (plain pass-through) when `on` is false, in a nested scope, or with RSYS_DEFER_REDUCE=0."""
+    if not on or _DEFER_KEEP or os.environ.get('RSYS_DEFER_REDUCE', '1') == '0':
+        yield
+        return
+    _DEFER_KEEP.append([])
+    call('rs_reduce_defer', 1)
+    try:
+        yield
+    finally:
+        call('rs_reduce_defer', 0)
+        try:
+            call('rs_reduce_flush', stream())
+        finally:
+            _DEFER_KEEP.pop()
 
 
 def gemm(A, B, C, M, N, K, *, transA, transB, lda, ldb, ldc, alpha=1.0, beta=0.0, epi=0,
