@@ -1321,7 +1321,18 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
     gather_bwd_slot_kernel<<<a.tblock_start[nseg], 256, a.slot_lds, st>>>(a);
     RS_CHECK_LAUNCH("rs_gather_bwd slot");
   }
-  if (a.ws_floats > 0) {
+  if (a.ws_floats > 0 && reduce_deferring()) {
+    // queued for rs_reduce_flush (reduce.hip): the same per-element order as reduce_partials_kernel
+    // (16 strided lanes over the chunks, then lanes 0..15), grad += the sum
+    for (int s = 0; s < nseg; ++s) {
+      if (!a.pchunks[s]) continue;
+      float* outs[1] = {segs_host[s].grad};
+      const int b0[1] = {0};
+      const float one[1] = {1.f};
+      reduce_defer_job(a.ws + a.pws_off[s], a.pchunks[s], (int)(segs_host[s].vocab * segs_host[s].dim), 1, outs, b0,
+                       one, one);
+    }
+  } else if (a.ws_floats > 0) {
     int64_t nel = 0;
     for (int s = 0; s < nseg; ++s)
       if (a.pchunks[s]) nel = std::max<int64_t>(nel, segs_host[s].vocab * segs_host[s].dim / 4 + 1);
