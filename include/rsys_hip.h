@@ -173,6 +173,16 @@ int rs_gemm_add_layernorm(int M, int N, int K, const float* A, int lda, const fl
                           const float* gamma, const float* beta, float* mean, float* rstd, float eps,
                           float p, const int64_t* key, int site, int flags, void* stream);
 /* flags: RS_GEMM_BF16 (bf16 operands for the GEMM part; LayerNorm stays fp32) or 0. */
+/* The same with the residual read in place (round 5): row m's residual is resid row
+ * m * resid_bag + resid_rows[m] -- the pruned last encoder layer's x[b, last[b]]
+ * (SequenceEncoder.py:58-74), no gathered copy. bf16 mode (flags & RS_GEMM_BF16), M % 16 == 0,
+ * N == 64, K in {64, 256}; anything else fails (the caller gathers the rows and calls
+ * rs_gemm_add_layernorm). */
+int rs_gemm_add_layernorm_rows(int M, int N, int K, const float* A, int lda, const float* W, int ldw,
+                               const float* bias, const float* resid, const int64_t* resid_rows,
+                               int resid_bag, float* h, float* y, const float* gamma, const float* beta,
+                               float* mean, float* rstd, float eps, float p, const int64_t* key, int site,
+                               int flags, void* stream);
 
 /* ---------------------------------------------------------------- fused feed-forward block (bf16 mode)
  * x2 = norm2(x1 + dropout2(linear2(dropout(relu(linear1(x1)))))) of nn.TransformerEncoderLayer

@@ -49,6 +49,8 @@ SIGNATURES = {
                           i32, i32, f32, vp, i32, i32, vp, i32, vp, vp]),
     'rs_gemm_add_layernorm': (i32, [i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp,
                                     f32, f32, vp, i32, i32, vp]),
+    'rs_gemm_add_layernorm_rows': (i32, [i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, i32, vp, vp, vp, vp,
+                                         vp, vp, f32, f32, vp, i32, i32, vp]),
     'rs_ffn_mask_words': (i64, [i32, i32]),
     'rs_ffn_fwd_bf16': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, f32, vp,
                               i32, i32, vp]),

@@ -375,6 +375,34 @@ extern "C" int rs_gemm_f32(int transA, int transB, int M, int N, int K, float al
 // h = dropout(A W^T + bias) + resid; y = LayerNorm(h) (TransformerEncoderLayer's
 // norm(x + dropout(sublayer(x))) with the sublayer's last Linear). One streaming kernel for the
 // encoder shape (N = d_model = 64); otherwise the GEMM followed by rs_add_layernorm_fwd.
+// rs_gemm_add_layernorm with the residual read in place: row m's residual is resid row
+// m * resid_bag + resid_rows[m] (round 5: the pruned last encoder layer's x[b, last[b]], no gathered
+// copy). bf16 mode, M % 16 == 0, N == 64, K % 64 == 0 only; -1 (rs_last_error) otherwise, and the
+// caller gathers and takes rs_gemm_add_layernorm.
+extern "C" int rs_gemm_add_layernorm_rows(int M, int N, int K, const float* A, int lda, const float* W, int ldw,
+                                          const float* bias, const float* resid, const int64_t* resid_rows,
+                                          int resid_bag, float* h, float* y, const float* gamma, const float* beta,
+                                          float* mean, float* rstd, float eps, float p, const int64_t* key, int site,
+                                          int flags, void* stream) {
+  RS_CHECK_ARG(A && W && resid && resid_rows && h && y && gamma && beta && mean && rstd && resid_bag >= 1,
+               "rs_gemm_add_layernorm_rows: null pointer / bad bag");
+  RS_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || key), "rs_gemm_add_layernorm_rows: bad dropout p");
+  RS_CHECK_ARG((flags & RS_GEMM_BF16) && M >= 16 && M % 16 == 0 && N == 64 && K % 64 == 0 && lda % 4 == 0 &&
+                   ldw % 4 == 0 && aligned16(A) && aligned16(W) && (K == 64 || K == 256),
+               "rs_gemm_add_layernorm_rows: bf16 mode, M %% 16 == 0, N == 64, K in {64, 256} only");
+  if (M == 0) return 0;
+  StreamArgs sa{};
+  sa.M = M; sa.N = N; sa.K = K; sa.alpha = 1.f; sa.beta = 0.f; sa.A = A; sa.lda = lda;
+  sa.B = W; sa.ldb = ldw; sa.transB = 1; sa.C = h; sa.ldc = N;
+  sa.epi = RS_EPI_AUX_ADD | (bias ? RS_EPI_BIAS : 0) | (p > 0.f ? RS_EPI_DROP_A : 0) | RS_GEMM_BF16;
+  sa.bias = bias; sa.aux = resid; sa.ld_aux = N; sa.aux_mod = M;
+  sa.aux_rows = resid_rows; sa.aux_bag = resid_bag;
+  sa.drop_p = p; sa.drop_key = key; sa.site_a = site;
+  sa.ln_gamma = gamma; sa.ln_beta = beta; sa.ln_y = y; sa.ln_mean = mean; sa.ln_rstd = rstd;
+  sa.ln_eps = eps;
+  return rowgemm_ln_launch(sa, as_stream(stream));
+}
+
 extern "C" int rs_gemm_add_layernorm(int M, int N, int K, const float* A, int lda, const float* W,
                                      int ldw, const float* bias, const float* resid, float* h,
                                      float* y, const float* gamma, const float* beta, float* mean,

@@ -29,6 +29,10 @@ struct StreamArgs {
   float* ln_mean;
   float* ln_rstd;
   float ln_eps;
+  // LN instances, optional: the residual row of output row m is aux row m * aux_bag + aux_rows[m]
+  // (the pruned last encoder layer reads x[b, last[b]] in place instead of a gathered copy)
+  const int64_t* aux_rows;
+  int aux_bag;
 };
 
 bool rowgemm_supported(int transA, int M, int N, int K, const float* A, int lda);

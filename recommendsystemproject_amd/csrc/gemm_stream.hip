@@ -889,8 +889,9 @@ __global__ __launch_bounds__(512) void rowgemm_bf16_kernel(StreamArgs a) {
     floatx4 lnres[LN ? NT : 1];
     floatx4 epre[EPRE ? NT : 1];
     if constexpr (LN) {
+      const int64_t rr = a.aux_rows ? (int64_t)m * a.aux_bag + a.aux_rows[m] : (int64_t)m;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) lnres[t] = *(gptr4)(a.aux + (int64_t)m * a.ld_aux + t * 16 + 4 * q);
+      for (int t = 0; t < NT; ++t) lnres[t] = *(gptr4)(a.aux + rr * a.ld_aux + t * 16 + 4 * q);
     }
     if constexpr (EPRE) {
 #pragma unroll

@@ -538,12 +538,16 @@ def layer_fwd_last(lyr, x, key_pad, last, B, L, d, H, p, key, site):
     qkv = ops.linear_fwd(x, sa_mod.in_proj_weight, sa_mod.in_proj_bias,
                          out_dtype=torch.bfloat16 if ops.qkv_bf16_ok(L, d, H, B * L) else torch.float32)
     att, lse = ops.attn_rows_fwd(qkv, key_pad, last, B, L, d, H, p, key, site)
-    xs = torch.empty(B, d, device=x.device, dtype=torch.float32)  # residual rows x[b, last[b]]
-    ops.gather_fwd([_seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=last.data_ptr(),
-                         table=x.data_ptr())], B, xs)
-    h1, x1, m1, r1 = ops.linear_add_layernorm(att, sa_mod.out_proj.weight, sa_mod.out_proj.bias, xs,
-                                              lyr.norm1.weight, lyr.norm1.bias, lyr.norm1.eps, p, key,
-                                              site + 1)
+    # the residual rows x[b, last[b]] read in place by the fused kernel (bf16 mode), else gathered
+    post = ops.linear_add_layernorm_rows(att, sa_mod.out_proj.weight, sa_mod.out_proj.bias, x, last, L,
+                                         lyr.norm1.weight, lyr.norm1.bias, lyr.norm1.eps, p, key, site + 1)
+    if post is None:
+        xs = torch.empty(B, d, device=x.device, dtype=torch.float32)
+        ops.gather_fwd([_seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=last.data_ptr(),
+                             table=x.data_ptr())], B, xs)
+        post = ops.linear_add_layernorm(att, sa_mod.out_proj.weight, sa_mod.out_proj.bias, xs,
+                                        lyr.norm1.weight, lyr.norm1.bias, lyr.norm1.eps, p, key, site + 1)
+    h1, x1, m1, r1 = post
     x2, ff = _ffn_fwd(lyr, x1, p, key, site)
     return x2, (x, qkv, att, lse, h1, x1, m1, r1) + ff
 

@@ -360,6 +360,28 @@ def linear_add_layernorm(x, W, bias, resid, gamma, beta, eps=1e-5, p=0.0, key=No
     return h, y, mean, rstd
 
 
+def linear_add_layernorm_rows(x, W, bias, table, rows, bag, gamma, beta, eps=1e-5, p=0.0, key=None, site=0):
+    """linear_add_layernorm with the residual rows read in place: row m's residual is
+    table[m * bag + rows[m]] (rs_gemm_add_layernorm_rows). None when the fused bf16 kernel does not
+    take the shape (the caller gathers the rows instead)."""
+    M, K = x.shape
+    N = W.shape[0]
+    if os.environ.get('RSYS_LN_ROWS') == '0':  # A/B: the gathered copy (round 4's path)
+        return None
+    if not (precision.gemm_flags() & _hip.RS_GEMM_BF16) or M % 16 or N != 64 or K not in (64, 256) or \
+            x.stride(0) % 4 or W.stride(0) % 4 or rows.dtype != torch.int64 or not table.is_contiguous():
+        return None
+    dev = x.device
+    h = torch.empty(M, N, device=dev, dtype=torch.float32)
+    y = torch.empty(M, N, device=dev, dtype=torch.float32)
+    mean = torch.empty(M, device=dev, dtype=torch.float32)
+    rstd = torch.empty(M, device=dev, dtype=torch.float32)
+    call('rs_gemm_add_layernorm_rows', M, N, K, P(x), x.stride(0), P(W), W.stride(0), P(bias), P(table), P(rows),
+         int(bag), P(h), P(y), P(gamma), P(beta), P(mean), P(rstd), float(eps), float(p), P(key), site,
+         precision.gemm_flags(), stream())
+    return h, y, mean, rstd
+
+
 def add_layernorm_fwd(a, b, gamma, beta, eps=1e-5, p=0.0, key=None, site=0):
     """h = dropout(a) + b (into a); returns y, mean, rstd."""
     M, N = a.shape
