@@ -152,16 +152,66 @@ struct RedJobs {
   int n;
 };
 
+// per job: columns in blocks of 256 (64 lanes x 4 columns, 16-byte loads) when N % 4 == 0, else
+// 64 scalar columns; wave w of the 16 sums partials w, w + 16, ... of its lane's columns with 8
+// loads in flight, then lanes' sums meet in the fixed 16-way LDS order -- per column exactly the
+// operations of partials_reduce_kernel (whose lane group w sums the same partials in the same order)
+__host__ __device__ __forceinline__ bool job_vec(const RedJob& j) {
+  return (j.N & 3) == 0 && (reinterpret_cast<uintptr_t>(j.ws) & 15) == 0;
+}
+__device__ __forceinline__ int job_cols(const RedJob& j) { return job_vec(j) ? 256 : 64; }
+
+__device__ __forceinline__ void job_out(const RedJob& j, int c, float t) {
+  int q = 0;
+  while (q + 1 < j.nr && c >= j.r[q + 1].begin) ++q;
+  float* o = j.r[q].out + (c - j.r[q].begin);
+  // beta * out + alpha * sum (the partials_reduce / ffn_wgrad_reduce form), alpha * sum when
+  // beta == 0 (wgrad_reduce's: no read, and a -0 stays -0)
+  *o = j.r[q].beta != 0.f ? j.r[q].beta * *o + j.r[q].alpha * t : j.r[q].alpha * t;
+}
+
 __global__ __launch_bounds__(1024) void reduce_jobs_kernel(RedJobs js) {
   int k = 0;
   while (k + 1 < js.n && (int)blockIdx.x >= js.j[k + 1].blk0) ++k;
   const RedJob& j = js.j[k];
-  __shared__ float red[16][64];
-  const int c = ((int)blockIdx.x - j.blk0) * 64 + (threadIdx.x & 63);
-  const int l = threadIdx.x >> 6;
+  __shared__ float4 red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (job_cols(j) == 256) {
+    const int c4 = ((int)blockIdx.x - j.blk0) * 64 + lane;  // float4 column index
+    const int n4 = j.N / 4;
+    const float4* src = reinterpret_cast<const float4*>(j.ws);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c4 < n4) {
+      int p = w;
+      for (; p + 16 * 7 < j.P; p += 16 * 8) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(p + 16 * u) * n4 + c4];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+      }
+      for (; p < j.P; p += 16) {
+        const float4 v = src[(int64_t)p * n4 + c4];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+    red[w][lane] = acc;
+    __syncthreads();
+    if (w == 0 && c4 < n4) {
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { const float4 r = red[i][lane]; t.x += r.x; t.y += r.y; t.z += r.z; t.w += r.w; }
+      job_out(j, 4 * c4, t.x);
+      job_out(j, 4 * c4 + 1, t.y);
+      job_out(j, 4 * c4 + 2, t.z);
+      job_out(j, 4 * c4 + 3, t.w);
+    }
+    return;
+  }
+  const int c = ((int)blockIdx.x - j.blk0) * 64 + lane;
   float acc = 0.f;
   if (c < j.N) {
-    int p = l;
+    int p = w;
     for (; p + 16 * 7 < j.P; p += 16 * 8) {
       float v[8];
 #pragma unroll
@@ -171,18 +221,13 @@ __global__ __launch_bounds__(1024) void reduce_jobs_kernel(RedJobs js) {
     }
     for (; p < j.P; p += 16) acc += j.ws[(int64_t)p * j.N + c];
   }
-  red[l][threadIdx.x & 63] = acc;
+  reinterpret_cast<float*>(&red[w][0])[lane] = acc;
   __syncthreads();
-  if (l == 0 && c < j.N) {
+  if (w == 0 && c < j.N) {
     float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
-    int q = 0;
-    while (q + 1 < j.nr && c >= j.r[q + 1].begin) ++q;
-    float* o = j.r[q].out + (c - j.r[q].begin);
-    // beta * out + alpha * sum (the partials_reduce / ffn_wgrad_reduce form), alpha * sum when
-    // beta == 0 (wgrad_reduce's: no read, and a -0 stays -0)
-    *o = j.r[q].beta != 0.f ? j.r[q].beta * *o + j.r[q].alpha * t : j.r[q].alpha * t;
+    for (int i = 0; i < 16; ++i) t += reinterpret_cast<const float*>(&red[i][0])[lane];
+    job_out(j, c, t);
   }
 }
 
@@ -197,7 +242,7 @@ int launch_jobs(const RedJob* jobs, int n, hipStream_t st) {
     for (int i = 0; i < js.n; ++i) {
       js.j[i] = jobs[a + i];
       js.j[i].blk0 = blk;
-      blk += cdiv(js.j[i].N, 64);
+      blk += cdiv(js.j[i].N, job_vec(js.j[i]) ? 256 : 64);
     }
     if (blk == 0) continue;
     reduce_jobs_kernel<<<blk, 1024, 0, st>>>(js);
@@ -231,6 +276,15 @@ extern "C" int rs_reduce_flush(void* stream) {
   std::vector<rs::RedJob> jobs;
   jobs.swap(rs::g_jobs);
   if (jobs.empty()) return 0;
+  static const bool dbg = rs::getenv_flag("RSYS_DEFER_DEBUG");
+  if (dbg) {
+    int64_t bytes = 0;
+    for (const auto& j : jobs) {
+      fprintf(stderr, "rs_reduce_flush job P=%d N=%d ranges=%d\n", j.P, j.N, j.nr);
+      bytes += (int64_t)(j.P + 1) * j.N * 4;
+    }
+    fprintf(stderr, "rs_reduce_flush %zu jobs, %.2f MB\n", jobs.size(), bytes / 1e6);
+  }
   return rs::launch_jobs(jobs.data(), (int)jobs.size(), rs::as_stream(stream));
 }
 

@@ -166,3 +166,31 @@ def test_pruned_last_layer_step(dtype, B, monkeypatch):
             if k not in skip and g2[k].norm() > 1e-3 * b.norm():
                 cs = cos(g1[k].flatten(), g2[k].flatten(), dim=0).item()
                 assert cs > 0.99, (k, cs)
+
+
+@pytest.mark.parametrize('dtype', ['bf16', 'fp32'])
+def test_deferred_reductions_bitwise(dtype, monkeypatch):
+    """The encoder backward's parameter-gradient reductions queued and run as one launch
+    (ops.deferred_reduce, rs_reduce_flush) against the immediate per-call reduce launches, in
+    deterministic mode: every gradient bitwise equal (the jobs keep each reduce's order)."""
+    from oracle.twotower_oracle import model_state_shapes
+    from recommendsystemproject_amd import ops, synth
+    cfg = yaml.safe_load(open(os.path.join(ROOT, 'configs', 'c2.yaml')))
+    for t in cfg['two_tower'].values():  # the dropout keys advance per step
+        t['dropout'] = 0.0
+        t.get('transformer_parameters', {})['dropout'] = 0.0
+    shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
+    state = synth.make_state(shapes, seed=5)
+    batch = synth.batch_to_torch(synth.make_batch(cfg, 512, seed=11, edge_cases=True), DEV)
+    torch.use_deterministic_algorithms(True)
+    try:
+        monkeypatch.setenv('RSYS_DEFER_REDUCE', '1')
+        l1, U1, g1 = _step(cfg, state, batch, False, monkeypatch, dtype)
+        monkeypatch.setenv('RSYS_DEFER_REDUCE', '0')
+        l2, U2, g2 = _step(cfg, state, batch, False, monkeypatch, dtype)
+    finally:
+        torch.use_deterministic_algorithms(False)
+        ops.sync_deterministic()
+    assert l1 == l2 and torch.equal(U1, U2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
