@@ -50,8 +50,8 @@ HBM_MEASURED_GBS = 6290.0  # MI355X_MICROARCH.md: measured float4 copy (79 % of 
 # v_exp_f32 issues in 8 cycles per wave on one SIMD (MI355X_MICROARCH.md cycle constants):
 # 64 lanes / 8 cycles x 4 SIMDs x 256 CUs x 2.4 GHz
 PEAK_EXP_PER_S = 64 / 8 * 4 * 256 * 2.4e9
-CE_ENTRIES = ('rs_inbatch_ce_fused_fwd', 'rs_inbatch_ce_fused_bwd', 'rs_inbatch_ce_fused_f32_fwd',
-              'rs_inbatch_ce_fused_f32_bwd')
+CE_ENTRIES = ('rs_inbatch_ce_fused_fwd', 'rs_inbatch_ce_fused_bwd', 'rs_inbatch_ce_fused_fwd_uib',
+              'rs_inbatch_ce_fused_bwd_uib', 'rs_inbatch_ce_fused_f32_fwd', 'rs_inbatch_ce_fused_f32_bwd')
 SOFTMAX_ENTRIES = ('rs_attn_fwd', 'rs_attn_bwd') + CE_ENTRIES
 
 

@@ -433,6 +433,17 @@ int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const float* Hn, int
                             int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
                             int N, int D, float T, const float* lse, const float* grad_out, float* dU,
                             float* dI, float* dhl, float* ws, void* stream);
+/* The bf16 pair with the rounding of U and I done once, in the forward's tiles: the forward also
+ * writes ui_bf16 ([2][B][D] bf16, U then I, 16-byte aligned), which the backward streams instead
+ * of rounding U and I in a launch of its own (keep it from forward to backward). Same results. */
+int rs_inbatch_ce_fused_fwd_uib(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
+                                int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
+                                int N, int D, float T, float* lse, float* row_loss, float* loss, float* ws,
+                                void* ui_bf16, void* stream);
+int rs_inbatch_ce_fused_bwd_uib(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
+                                int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
+                                int N, int D, float T, const float* lse, const float* grad_out, float* dU,
+                                float* dI, float* dhl, float* ws, const void* ui_bf16, void* stream);
 /* The same pair in fp32 compute mode: the tiles run on v_mfma_f32_32x32x2_f32 with fp32 operands
  * (exact f32 products, no rounding of U, I); same arguments, workspace and outputs, plus S:
  * [B][rs_inbatch_ce_s_ld(B)] fp32 scratch that the forward fills with U I^T (raw dot products)

@@ -106,6 +106,10 @@ SIGNATURES = {
     'rs_inbatch_ce_fused_fwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp]),
     'rs_inbatch_ce_fused_bwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp,
                                       vp]),
+    'rs_inbatch_ce_fused_fwd_uib': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp,
+                                          vp]),
+    'rs_inbatch_ce_fused_bwd_uib': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp,
+                                          vp, vp, vp]),
     'rs_inbatch_ce_s_ld': (i64, [i32]),
     'rs_inbatch_ce_fused_f32_fwd': (i32, [vp, vp, vp, i64, i64, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp,
                                           vp]),

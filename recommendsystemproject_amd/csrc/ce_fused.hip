@@ -526,11 +526,22 @@ __global__ __launch_bounds__(256) void ce_finish_fwd_kernel(const float* __restr
                                                             float* __restrict__ lse,
                                                             float* __restrict__ row_loss,
                                                             int* __restrict__ cnt, float* __restrict__ loss,
-                                                            float loss_scale) {
+                                                            float loss_scale, const float* __restrict__ I,
+                                                            __bf16* __restrict__ outb) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + wave;
   if (i < B) ce_finish_row(part_m, part_s, diag, NS, U, Hn, hs_row, hs_slot, B, N, D, invT, lse, row_loss, i,
                            lane, cnt != nullptr);
+  // rows i of U and I rounded to bf16 for the backward's streamed operands (outb: [2][B][D]; D even) -- the
+  // backward's rounding launch folded into this short one
+  if (outb && i < B)
+    for (int c = 2 * lane; c < D; c += 128) {
+      const float2 u = *reinterpret_cast<const float2*>(U + (int64_t)i * D + c);
+      const float2 v = *reinterpret_cast<const float2*>(I + (int64_t)i * D + c);
+      typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<bf16x2*>(outb + (int64_t)i * D + c) = bf16x2{(__bf16)u.x, (__bf16)u.y};
+      *reinterpret_cast<bf16x2*>(outb + ((int64_t)B + i) * D + c) = bf16x2{(__bf16)v.x, (__bf16)v.y};
+    }
   if (!cnt) return;
   // the mean over the rows by the last workgroup to finish (fused rs_sum, round 5): every wave's
   // row_loss store is agent-scope and drained before the workgroup's one ticket (the fence-free
@@ -679,8 +690,9 @@ namespace {
 template <bool F32>
 int ce_fused_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride, int64_t h_slot_stride,
                  const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T, float* lse,
-                 float* row_loss, float* loss, float* S, float* ws, void* stream) {
+                 float* row_loss, float* loss, float* S, float* ws, __bf16* uib, void* stream) {
   const char* fn = F32 ? "rs_inbatch_ce_fused_f32_fwd" : "rs_inbatch_ce_fused_fwd";
+  RS_CHECK_ARG(!uib || aligned16(uib), "%s: ui_bf16 must be 16-byte aligned", fn);
   RS_CHECK_ARG(U && I && lse && row_loss && loss && ws, "%s: null pointer", fn);  // S: optional
   RS_CHECK_ARG(B >= 1 && (D == 64 || D == 128) && N >= 0 && N <= 64,
                "%s: needs D in {64, 128}, N <= 64 (B=%d N=%d D=%d)", fn, B, N, D);
@@ -705,7 +717,8 @@ int ce_fused_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_
   RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_fwd tiles" : "rs_inbatch_ce_fused_fwd tiles");
   const HStrideArgs hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
   ce_finish_fwd_kernel<<<cdiv(B, 4), 256, 0, st>>>(a.part_m, a.part_s, a.diag, NSr, U, Hn, hs.row, hs.slot, B,
-                                                   N, D, a.invT, lse, row_loss, a.cnt, loss, 1.f / (float)B);
+                                                   N, D, a.invT, lse, row_loss, a.cnt, loss, 1.f / (float)B,
+                                                   I, F32 ? nullptr : uib);
   RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_fwd finish" : "rs_inbatch_ce_fused_fwd finish");
   if (fused_sum) return 0;
   return rs_sum(row_loss, B, 1.f / (float)B, loss, stream);
@@ -715,7 +728,7 @@ template <bool F32>
 int ce_fused_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride, int64_t h_slot_stride,
                  const int64_t* item_ids, int64_t id_stride, int B, int N, int D, float T, const float* lse,
                  const float* grad_out, float* dU, float* dI, float* dhl, const float* S, float* ws,
-                 void* stream) {
+                 const __bf16* uib, void* stream) {
   const char* fn = F32 ? "rs_inbatch_ce_fused_f32_bwd" : "rs_inbatch_ce_fused_bwd";
   RS_CHECK_ARG(U && I && lse && dU && dI && ws && (!F32 || S), "%s: null pointer", fn);
   RS_CHECK_ARG(B >= 1 && (D == 64 || D == 128) && N >= 0 && N <= 64, "%s: bad shape", fn);
@@ -742,11 +755,15 @@ int ce_fused_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_
     // and stages twice the tiles per batch with the same registers (RSYS_CE_STREAM_F32=1: the
     // fp32 rows, rounded as staged)
     if (!getenv_flag("RSYS_CE_STREAM_F32")) {
-      float* wb = ws + (int64_t)2 * NSr * n;
-      __bf16* Ub = reinterpret_cast<__bf16*>(wb);
-      __bf16* Ib = Ub + n;
-      ce_round_bf16_kernel<<<(int)cdiv(2 * n / 4, 256), 256, 0, st>>>(U, I, n, Ub, Ib);
-      RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd round");
+      // the forward's copies when it wrote them (rs_inbatch_ce_fused_fwd_uib), else one launch here
+      const __bf16* Ub = uib;
+      if (!uib) {
+        __bf16* wb = reinterpret_cast<__bf16*>(ws + (int64_t)2 * NSr * n);
+        ce_round_bf16_kernel<<<(int)cdiv(2 * n / 4, 256), 256, 0, st>>>(U, I, n, wb, wb + n);
+        RS_CHECK_LAUNCH("rs_inbatch_ce_fused_bwd round");
+        Ub = wb;
+      }
+      const __bf16* Ib = Ub + n;
       aU.strb = Ib;
       aI.strb = Ub;
       if (D == 128) ce_bwd_pair_kernel<128, false, true><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
@@ -782,7 +799,18 @@ extern "C" int rs_inbatch_ce_fused_fwd(const float* U, const float* I, const flo
                                        int N, int D, float T, float* lse, float* row_loss, float* loss, float* ws,
                                        void* stream) {
   return ce_fused_fwd<false>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, row_loss,
-                             loss, nullptr, ws, stream);
+                             loss, nullptr, ws, nullptr, stream);
+}
+
+// the same, also writing U and I as rounded to bf16 ([2][B][D], U then I) for
+// rs_inbatch_ce_fused_bwd_uib: the backward's rounding launch folded into the forward's finish
+extern "C" int rs_inbatch_ce_fused_fwd_uib(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
+                                           int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
+                                           int N, int D, float T, float* lse, float* row_loss, float* loss, float* ws,
+                                           void* ui_bf16, void* stream) {
+  RS_CHECK_ARG(ui_bf16, "rs_inbatch_ce_fused_fwd_uib: null ui_bf16");
+  return ce_fused_fwd<false>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, row_loss,
+                             loss, nullptr, ws, static_cast<__bf16*>(ui_bf16), stream);
 }
 
 extern "C" int rs_inbatch_ce_fused_f32_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
@@ -790,7 +818,7 @@ extern "C" int rs_inbatch_ce_fused_f32_fwd(const float* U, const float* I, const
                                            int N, int D, float T, float* lse, float* row_loss, float* loss, float* S,
                                            float* ws, void* stream) {
   return ce_fused_fwd<true>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, row_loss,
-                            loss, S, ws, stream);
+                            loss, S, ws, nullptr, stream);
 }
 
 extern "C" int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
@@ -798,7 +826,17 @@ extern "C" int rs_inbatch_ce_fused_bwd(const float* U, const float* I, const flo
                                        int N, int D, float T, const float* lse, const float* grad_out, float* dU,
                                        float* dI, float* dhl, float* ws, void* stream) {
   return ce_fused_bwd<false>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, grad_out,
-                             dU, dI, dhl, nullptr, ws, stream);
+                             dU, dI, dhl, nullptr, ws, nullptr, stream);
+}
+
+// ui_bf16: the forward's rounded copies (rs_inbatch_ce_fused_fwd_uib on the same U, I)
+extern "C" int rs_inbatch_ce_fused_bwd_uib(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
+                                           int64_t h_slot_stride, const int64_t* item_ids, int64_t id_stride, int B,
+                                           int N, int D, float T, const float* lse, const float* grad_out, float* dU,
+                                           float* dI, float* dhl, float* ws, const void* ui_bf16, void* stream) {
+  RS_CHECK_ARG(ui_bf16 && aligned16(ui_bf16), "rs_inbatch_ce_fused_bwd_uib: ui_bf16 null or not 16-byte aligned");
+  return ce_fused_bwd<false>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, grad_out,
+                             dU, dI, dhl, nullptr, ws, static_cast<const __bf16*>(ui_bf16), stream);
 }
 
 extern "C" int rs_inbatch_ce_fused_f32_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_stride,
@@ -806,5 +844,5 @@ extern "C" int rs_inbatch_ce_fused_f32_bwd(const float* U, const float* I, const
                                            int N, int D, float T, const float* lse, const float* grad_out, float* dU,
                                            float* dI, float* dhl, const float* S, float* ws, void* stream) {
   return ce_fused_bwd<true>(U, I, Hn, h_row_stride, h_slot_stride, item_ids, id_stride, B, N, D, T, lse, grad_out,
-                            dU, dI, dhl, S, ws, stream);
+                            dU, dI, dhl, S, ws, nullptr, stream);
 }

@@ -276,6 +276,10 @@ extern "C" int rs_reduce_flush(void* stream) {
   std::vector<rs::RedJob> jobs;
   jobs.swap(rs::g_jobs);
   if (jobs.empty()) return 0;
+  // the long jobs' workgroups (most partials each) dispatched first, the short ones fill the tail
+  // (each job's sums are independent of where it sits in the grid)
+  if (!rs::getenv_flag("RSYS_DEFER_FIFO"))
+    std::stable_sort(jobs.begin(), jobs.end(), [](const rs::RedJob& x, const rs::RedJob& y) { return x.P > y.P; });
   static const bool dbg = rs::getenv_flag("RSYS_DEFER_DEBUG");
   if (dbg) {
     int64_t bytes = 0;

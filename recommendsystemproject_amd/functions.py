@@ -1185,12 +1185,20 @@ class InBatchLossFn(torch.autograd.Function):
         lse = torch.empty(B, device=dev, dtype=torch.float32)
         row_loss = torch.empty(B, device=dev, dtype=torch.float32)
         loss = torch.empty((), device=dev, dtype=torch.float32)
+        uib = None
         if fused:
             w = ops.ws(_hip.lib().rs_inbatch_ce_fused_ws_bytes(B, D), dev)
             extra = (S.data_ptr() if S is not None else None,) if sfx else ()
-            _hip.call(f'rs_inbatch_ce_fused{sfx}_fwd', U.data_ptr(), I.data_ptr(), ops.P(Hc), hsr, hss, ops.P(ids), st,
+            name = f'rs_inbatch_ce_fused{sfx}_fwd'
+            if not sfx and need and os.environ.get('RSYS_CE_UIB', '1') != '0':
+                # bf16: the tiles also write U, I as rounded ([2, B, D]) for the backward's streamed
+                # operands -- its rounding launch folded into this one
+                uib = torch.empty(2, B, D, device=dev, dtype=torch.bfloat16)
+                name += '_uib'
+            post = (uib.data_ptr(),) if uib is not None else ()
+            _hip.call(name, U.data_ptr(), I.data_ptr(), ops.P(Hc), hsr, hss, ops.P(ids), st,
                       B, N, D, float(temperature), lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(),
-                      *extra, w.data_ptr(), ops.stream())
+                      *extra, w.data_ptr(), *post, ops.stream())
         else:
             _hip.call('rs_inbatch_ce_fwd', S.data_ptr(), B, U.data_ptr(), ops.P(Hc), hsr, hss, ops.P(ids), st,
                       B, N, D, float(temperature), lse.data_ptr(), row_loss.data_ptr(), loss.data_ptr(),
@@ -1198,6 +1206,7 @@ class InBatchLossFn(torch.autograd.Function):
         ctx.save_for_backward(U, I, Hc if Hc is not None else U)
         ctx.S, ctx.ids, ctx.st, ctx.N, ctx.T, ctx.lse = S, ids, st, N, float(temperature), lse
         ctx.fused = fused
+        ctx.uib = uib
         ctx.sfx = sfx
         ctx.hs = (hsr, hss)
         return loss
@@ -1216,10 +1225,14 @@ class InBatchLossFn(torch.autograd.Function):
             dI = torch.empty_like(I)
             w = ops.ws(_hip.lib().rs_inbatch_ce_fused_ws_bytes(B, D), U.device)
             extra = (S.data_ptr(),) if ctx.sfx else ()
-            _hip.call(f'rs_inbatch_ce_fused{ctx.sfx}_bwd', U.data_ptr(), I.data_ptr(), ops.P(Hc) if N else None,
-                      ctx.hs[0], ctx.hs[1], ops.P(ctx.ids), ctx.st, B, N, D, ctx.T, ctx.lse.data_ptr(),
-                      gout.data_ptr(), dU.data_ptr(), dI.data_ptr(), ops.P(dhl), *extra, w.data_ptr(), ops.stream())
+            uib = ctx.uib
+            post = (uib.data_ptr(),) if uib is not None else ()
+            _hip.call(f'rs_inbatch_ce_fused{ctx.sfx}_bwd' + ('_uib' if uib is not None else ''), U.data_ptr(),
+                      I.data_ptr(), ops.P(Hc) if N else None, ctx.hs[0], ctx.hs[1], ops.P(ctx.ids), ctx.st, B, N, D,
+                      ctx.T, ctx.lse.data_ptr(), gout.data_ptr(), dU.data_ptr(), dI.data_ptr(), ops.P(dhl), *extra,
+                      w.data_ptr(), *post, ops.stream())
             ctx.S = None
+            ctx.uib = None
             dH = None
             if N:
                 dH = torch.empty_strided(Hc.shape, Hc.stride(), device=Hc.device, dtype=Hc.dtype)

@@ -177,6 +177,8 @@ WORK = {
     'rs_ffn_bwd_ln2_bf16': _ffn_bwd_ln2_work,
     'rs_inbatch_ce_fused_fwd': _ce_fused_work,
     'rs_inbatch_ce_fused_bwd': lambda a: _ce_fused_work(a, True),
+    'rs_inbatch_ce_fused_fwd_uib': _ce_fused_work,
+    'rs_inbatch_ce_fused_bwd_uib': lambda a: _ce_fused_work(a, True),
     'rs_inbatch_ce_fused_f32_fwd': _ce_fused_f32_work,
     'rs_inbatch_ce_fused_f32_bwd': lambda a: _ce_fused_f32_work(a, True),
     'rs_gemm_add_layernorm': _gemm_ln_work,
@@ -217,6 +219,8 @@ EXPS = {
     'rs_attn_bwd': lambda a: float(a[6] * a[9] * a[7] * a[7]),
     'rs_inbatch_ce_fused_fwd': lambda a: float(a[7]) * (a[7] + a[8]),
     'rs_inbatch_ce_fused_bwd': lambda a: 2.0 * a[7] * (a[7] + a[8]),
+    'rs_inbatch_ce_fused_fwd_uib': lambda a: float(a[7]) * (a[7] + a[8]),
+    'rs_inbatch_ce_fused_bwd_uib': lambda a: 2.0 * a[7] * (a[7] + a[8]),
     'rs_inbatch_ce_fused_f32_fwd': lambda a: float(a[7]) * (a[7] + a[8]),
     'rs_inbatch_ce_fused_f32_bwd': lambda a: 2.0 * a[7] * (a[7] + a[8]),
 }

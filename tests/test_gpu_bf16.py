@@ -520,6 +520,38 @@ def test_fused_inbatch_ce_ragged_batches(B, splits, bf16_mode, monkeypatch):
     test_fused_inbatch_ce(B, 128, 0, True, bf16_mode)
 
 
+@pytest.mark.parametrize('B,D,splits', [(4096, 128, 0), (4096, 128, 3), (777, 128, 0), (33, 64, 0),
+                                        (300, 64, 2)])
+def test_fused_ce_forward_rounded_copies(B, D, splits, bf16_mode, monkeypatch):
+    """rs_inbatch_ce_fused_fwd_uib's copies of U and I (written by the forward's finish kernel)
+    are U, I rounded to bf16, and the backward that streams them gives the bits of the one that
+    rounds U, I in its own launch."""
+    from recommendsystemproject_amd import _hip
+    from recommendsystemproject_amd.functions import InBatchLossFn
+    if splits:
+        monkeypatch.setenv('RSYS_CE_SPLITS', str(splits))
+    U = F.normalize(rnd(B, D, seed=41), dim=1).requires_grad_(True)
+    I = F.normalize(rnd(B, D, seed=42), dim=1).requires_grad_(True)
+    ids = torch.randint(0, max(B // 2, 1), (B,), device=DEV)
+    uib = torch.full((2, B, D), float('nan'), device=DEV, dtype=torch.bfloat16)
+    lse, rl = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    loss = torch.empty((), device=DEV)
+    w = torch.empty(_hip.lib().rs_inbatch_ce_fused_ws_bytes(B, D) // 4, device=DEV)
+    _hip.call('rs_inbatch_ce_fused_fwd_uib', U.data_ptr(), I.data_ptr(), None, 0, 0, ids.data_ptr(), 1, B, 0, D,
+              0.15, lse.data_ptr(), rl.data_ptr(), loss.data_ptr(), w.data_ptr(), uib.data_ptr(), None)
+    torch.cuda.synchronize()
+    assert torch.equal(uib[0], U.detach().bfloat16()) and torch.equal(uib[1], I.detach().bfloat16())
+    res = []
+    for flag in ('1', '0'):
+        monkeypatch.setenv('RSYS_CE_UIB', flag)
+        U.grad = I.grad = None
+        l_ = InBatchLossFn.apply(U, I, ids, None, 0.15)
+        l_.backward()
+        res.append((l_.item(), U.grad.clone(), I.grad.clone()))
+    assert res[0][0] == res[1][0] == loss.item()
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+
+
 def test_fused_ce_deterministic(bf16_mode):
     from recommendsystemproject_amd.functions import InBatchLossFn
     B, D = 4096, 128
