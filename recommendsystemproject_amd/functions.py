@@ -384,9 +384,16 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key, params=()):
         if p > 0:
             ops.dropout_bwd(dx, p, key, 0)
     lin = proc.feature_projection[0]
-    # dx is final here (the dropout backward above ran in place before this point)
-    with _WgradBranch(dx, cat):
-        ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
+    # dx is final here (the dropout backward above ran in place before this point). Under the
+    # encoder's deferred reductions the projection's weight gradient and the flush of every
+    # reduction queued so far run on a side stream beside dcat and the tables' gradients below
+    # (ops.deferred_side; joined at the end of the encoder backward)
+    with ops.deferred_side(dx, cat) as forked:
+        if forked:
+            ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
+    if not forked:
+        with _WgradBranch(dx, cat):
+            ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
     dcat = ops.linear_bwd_input(dx, lin.weight)
     for s, t in zip(segs, tables):
         s.grad = grad_of(t).data_ptr()

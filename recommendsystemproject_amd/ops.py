@@ -26,6 +26,8 @@ def stream():
 
 
 _DEFER_KEEP = []  # deferred_reduce: the workspaces of this scope, alive until its flush is queued
+_DEFER_SIDE = []  # deferred_reduce: the side streams of this scope's early flushes (deferred_side)
+_SIDE_STREAMS = {}
 
 
 def ws(nbytes: int, device) -> torch.Tensor:
@@ -45,6 +47,7 @@ def deferred_reduce(on=True):
         yield
         return
     _DEFER_KEEP.append([])
+    _DEFER_SIDE.append([])
     call('rs_reduce_defer', 1)
     try:
         yield
@@ -53,7 +56,41 @@ def deferred_reduce(on=True):
         try:
             call('rs_reduce_flush', stream())
         finally:
+            # the early flushes' side streams joined before the workspaces they read are released
+            cur = torch.cuda.current_stream() if _DEFER_SIDE[-1] else None
+            for sd in _DEFER_SIDE.pop():
+                cur.wait_stream(sd)
             _DEFER_KEEP.pop()
+
+
+@contextlib.contextmanager
+def deferred_side(*tensors):
+    """Inside a deferred_reduce scope: the body runs on a side stream forked from the current one,
+    and the reductions queued so far (plus the body's) are flushed there at its end -- beside the
+    rest of the scope, which must not read those gradients; the scope's end joins it back
+    (round 5: the encoder's flush and input-projection weight gradient beside the sequence tables'
+    gradients). `tensors`: made on the current stream and read by the body. Yields whether it
+    forked (plain pass-through outside a scope, from a side stream, with RSYS_TOWER_STREAMS=0, the
+    bench's serial instrumented pass, and unless RSYS_FLUSH_SIDE=1). Opt-in: measured at C2 (bf16,
+    replayed graph) 1.27 -> 1.356 ms per step -- the graph's extra branch took the hardware queue
+    the item tower's backward chain runs on, which then waited behind the sequence tables'
+    gradient kernels; C3 fp32 0.759 -> 0.755."""
+    from . import streams
+    if (not _DEFER_SIDE or os.environ.get('RSYS_FLUSH_SIDE', '0') != '1' or not torch.cuda.is_available()
+            or os.environ.get('RSYS_TOWER_STREAMS', '1') == '0' or not streams.can_fork()):
+        yield False
+        return
+    main = torch.cuda.current_stream()
+    side = _SIDE_STREAMS.get(main.device)
+    if side is None:
+        side = _SIDE_STREAMS[main.device] = streams.side_stream(main.device)
+    side.wait_stream(main)
+    for t in tensors:
+        t.record_stream(side)
+    _DEFER_SIDE[-1].append(side)
+    with torch.cuda.stream(side):
+        yield True
+        call('rs_reduce_flush', stream())
 
 
 def gemm(A, B, C, M, N, K, *, transA, transB, lda, ldb, ldc, alpha=1.0, beta=0.0, epi=0,
