@@ -102,6 +102,12 @@ struct SegLaunch {
   // bwd partials (small and ranged tables): [pchunks][vocab][dim] floats at ws + pws_off
   int16_t pchunks[kMaxSeg];
   int64_t pws_off[kMaxSeg];
+  // bwd, tiny tables by the one-hot MFMA kernel (gather_bwd_onehot_kernel): lookup rows per wave,
+  // first block, dynamic LDS bytes
+  uint8_t oh[kMaxSeg];
+  int oh_rpw[kMaxSeg];
+  int oblock_start[kMaxSeg + 1];
+  int oh_lds;
   int64_t ws_floats;
   int range_lds;
   float* ws;
@@ -776,6 +782,115 @@ __global__ __launch_bounds__(256) void gather_bwd_slot_kernel(SegLaunch a) {
   }
 }
 
+// One-hot MFMA table gradient of tiny, heavily hit tables (round 5; V <= 64 rows, D <= 16 columns,
+// >= 65,536 lookups a call): grad[V][D] += sum over lookup rows r of count_r[V] (x) dout[r][D], a [V x rows] x
+// [rows x D] product on v_mfma_f32_16x16x4_f32 whose A operand -- the row's bag-id counts, scaled by
+// 1 / bag for mean pooling -- is built in registers from the ids: in k-step t, lane (i = l & 15,
+// k = l >> 4) holds A[v = 16 m + i][row 4 t + k] = sc * #{ids of the row == v} (four bag
+// positions per pass) and B[row 4 t + k][c = i] = dout[row][c]. The per-token genre bags of C2's
+// history (204,800 rows x 3 ids into a 30 x 8 table) were 25.7 us of LDS float atomics on 240
+// words in the C2 step (gather_bwd_small_kernel), 19.6 here; every row is one MFMA column whatever
+// its ids. The towers' tables (4,096 lookups) stay on the atomic kernel (see kOhMinLookups). Each wave sums a contiguous run
+// of rows in a fixed order, the 8 waves meet in a fixed LDS order, and the workgroup partials are
+// reduced in order (reduce_partials_kernel or the deferred flush): deterministic, in both modes.
+constexpr int kOhWaves = 8;   // 512 threads: 256 registers a lane (64 accumulators, 8 k-steps of ids)
+constexpr int kOhSteps = 8;   // k-steps (4 rows each) per batch: 32 rows' loads in flight per wave
+constexpr int kOhMaxM = 4;    // M tiles: V <= 64 (the MFMA chains grow with the tiles: at C2's
+                              // 152-row year table, 16 tiles, the atomic kernel was 2x faster)
+constexpr int kOhMaxE = 1024; // V x D: 4 LDS slices of 4 KB
+constexpr int64_t kOhMinLookups = 65536;  // below: the atomic kernel (one 4,096-row batch of the
+                                          // towers' tables: 12 us atomic, 16 us one-hot incl. launch)
+
+// MT: M tiles computed for every segment of the launch (the largest segment's, rounded up to a
+// power of two): tiles past a table's rows only ever add zeros, and no per-tile branch breaks the
+// MFMA chains
+template <int MT>
+__global__ __launch_bounds__(kOhWaves * 64) void gather_bwd_onehot_kernel(SegLaunch a) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][V * D]
+  int s = 0;
+  while (s + 1 < a.nseg && (int)blockIdx.x >= a.oblock_start[s + 1]) ++s;
+  const rs_feature_seg_t& sg = a.segs[s];
+  const int lb = blockIdx.x - a.oblock_start[s];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, k = lane >> 4;
+  const int D = sg.dim;
+  const int V = (int)sg.vocab;
+  const int E = V * D;
+  const bool pool = sg.kind == RS_SEG_POOL;
+  const int bag = pool ? sg.bag : 1;
+  const float sc = pool && sg.pool_mode == RS_POOL_MEAN ? 1.f / (float)bag : 1.f;
+  const int64_t pad = sg.pad_idx;
+  const int64_t rpw = a.oh_rpw[s];
+  const int64_t r0 = ((int64_t)lb * kOhWaves + w) * rpw;
+  const int64_t r1 = r0 + rpw < (int64_t)a.rows ? r0 + rpw : (int64_t)a.rows;
+  f4v acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = f4v{0.f, 0.f, 0.f, 0.f};
+  for (int64_t rb = r0; rb < r1; rb += 4 * kOhSteps) {
+    float bv[kOhSteps];
+    int64_t row[kOhSteps];
+#pragma unroll
+    for (int t = 0; t < kOhSteps; ++t) {
+      row[t] = rb + 4 * t + k;
+      bv[t] = (row[t] < r1 && i < D) ? a.dout[row[t] * a.ldo + sg.out_col + i] : 0.f;
+    }
+    for (int l0 = 0; l0 < bag; l0 += 4) {
+      int id[kOhSteps][4];  // table row, or -1 (no contribution)
+#pragma unroll
+      for (int t = 0; t < kOhSteps; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t x = (row[t] < r1 && l0 + u < bag) ? sg.idx[row[t] * sg.idx_stride + l0 + u] : -1;
+          id[t][u] = (x >= 0 && x < V && x != pad) ? (int)x : -1;
+        }
+#pragma unroll
+      for (int t = 0; t < kOhSteps; ++t)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int v = 16 * m + i;
+          const float cnt = (float)((id[t][0] == v) + (id[t][1] == v) + (id[t][2] == v) + (id[t][3] == v));
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(cnt * sc, bv[t], acc[m], 0, 0, 0);
+        }
+    }
+  }
+  // acc[m][j]: table row v = 16 m + 4 k + j, column c = i. Waves 4..7 hand theirs to waves 0..3,
+  // then each element is the fixed-order sum of the 4 slices
+  const int c = i;
+  if (w >= 4) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int v = 16 * m + 4 * k + j;
+        if (v < V && c < D) red[(w - 4) * E + v * D + c] = acc[m][j];
+      }
+    }
+  }
+  __syncthreads();
+  if (w < 4) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int v = 16 * m + 4 * k + j;
+        if (v < V && c < D) {
+          float* r = red + w * E + v * D + c;
+          *r = acc[m][j] + *r;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  float* dst = a.ws + a.pws_off[s] + (int64_t)lb * E;
+  for (int e = threadIdx.x; e < E; e += kOhWaves * 64) {
+    float t = red[e];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) t += red[q * E + e];
+    dst[e] = t;
+  }
+}
+
 // LDS-image table gradient of hot mid-size tables: no atomics, deterministic. C2's 3,500 x 32
 // hist_movie_ids table gets 204,800 token lookups per step (~58 per row); the atomic scatter
 // serialises on the hot rows' L2 lines (90 us per step). A workgroup owns one RANGE of table rows
@@ -1077,9 +1192,13 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     const bool det = bwd && deterministic();
     const int64_t tb = g.vocab * g.dim * 4;
     const bool rangeable = vec && g.dim >= 16 && g.dim <= 256 && 256 % g.dim == 0;
-    a.tiny[s] = det && table_kind && !(g.kind == RS_SEG_POOL && g.pool_mode == RS_POOL_MAX) &&
+    // tiny tables (both modes): the one-hot MFMA kernel (RSYS_NO_ONEHOT_GRAD=1: the kernels below)
+    a.oh[s] = bwd && table_kind && !(g.kind == RS_SEG_POOL && g.pool_mode == RS_POOL_MAX) && g.vocab <= 16 * kOhMaxM &&
+              g.dim <= 16 && g.vocab * g.dim <= kOhMaxE &&
+              (int64_t)rows * (g.kind == RS_SEG_POOL ? g.bag : 1) >= kOhMinLookups && !getenv_flag("RSYS_NO_ONEHOT_GRAD");
+    a.tiny[s] = det && table_kind && !(g.kind == RS_SEG_POOL && g.pool_mode == RS_POOL_MAX) && !a.oh[s] &&
                tb <= kSmallTableBytes && g.dim <= 64 && (tb <= 16 * 1024 || !rangeable);
-    a.small[s] = bwd && table_kind && tb <= kSmallTableBytes && !a.tiny[s] && !(det && rangeable &&
+    a.small[s] = bwd && table_kind && tb <= kSmallTableBytes && !a.tiny[s] && !a.oh[s] && !(det && rangeable &&
                !(g.kind == RS_SEG_POOL && g.pool_mode == RS_POOL_MAX));
     // Split long sum/mean bags over S row groups while the launch is short of ~8 waves per SIMD
     // and every group keeps >= 8 positions (C3: B = 4096, L = 50, D = 128 -> S = 4).
@@ -1117,7 +1236,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.rranges[s] = 0;
     a.rchunks[s] = 0;
     a.rrows[s] = 0;
-    if (bwd && !a.small[s] && !a.tiny[s]) {
+    if (bwd && !a.small[s] && !a.tiny[s] && !a.oh[s]) {
       const RangePlan rp = range_plan(g, rows, vec);
       a.rrows[s] = rp.rows;
       a.rranges[s] = rp.ranges;
@@ -1127,7 +1246,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     if (a.hot[s]) {
       const int ng = cdiv(rows, a.rpb[s]);
       blocks += ng < kHotBlocks ? ng : kHotBlocks;
-    } else if (!a.small[s] && !a.rranges[s] && !a.tiny[s]) {
+    } else if (!a.small[s] && !a.rranges[s] && !a.tiny[s] && !a.oh[s]) {
       blocks += cdiv(rows, a.rpb[s] * a.rpt[s]);
     }
   }
@@ -1169,6 +1288,26 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     }
   }
   a.tblock_start[nseg] = ob;
+  // one-hot tables: <= 256 workgroups of 8 waves, each wave a run of whole 32-row batches (C2's
+  // genre tokens: 200 workgroups of 4 batches a wave, 26.2 us a call against 27.3 at 400 x 2 and
+  // 35.0 at 800 x 1 -- the partials and workgroup launches cost more than the batch round trips)
+  int hb = 0;
+  a.oh_lds = 0;
+  for (int s = 0; s < nseg; ++s) {
+    a.oblock_start[s] = hb;
+    a.oh_rpw[s] = 0;
+    if (!a.oh[s]) continue;
+    const int64_t per_wave_min = 4 * kOhSteps;
+    int64_t nb = std::min<int64_t>(256, std::max<int64_t>(1, cdiv(rows, kOhWaves * per_wave_min)));
+    int64_t rpw = cdiv(cdiv(rows, nb * kOhWaves), per_wave_min) * per_wave_min;
+    if (const char* e = getenv("RSYS_OH_RPW")) rpw = std::max<int64_t>(per_wave_min, atoi(e) / per_wave_min * per_wave_min);  // tuning only
+    nb = std::max<int64_t>(1, cdiv(rows, rpw * kOhWaves));
+    a.oh_rpw[s] = (int)rpw;
+    a.tblocks[s] = (int16_t)nb;  // the partial count (pchunks)
+    hb += (int)nb;
+    a.oh_lds = std::max<int>(a.oh_lds, (int)(4 * segs_host[s].vocab * segs_host[s].dim * 4));
+  }
+  a.oblock_start[nseg] = hb;
   a.ws = nullptr;
 
   int sb = 0;
@@ -1192,7 +1331,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
   a.sblock_start[nseg] = sb;
   int64_t off = 0;
   for (int s = 0; s < nseg; ++s) {
-    a.pchunks[s] = a.rranges[s] ? a.rchunks[s] : (a.tiny[s] ? a.tblocks[s] : 0);
+    a.pchunks[s] = a.rranges[s] ? a.rchunks[s] : ((a.tiny[s] || a.oh[s]) ? a.tblocks[s] : 0);
     a.pws_off[s] = off;
     off += (int64_t)a.pchunks[s] * segs_host[s].vocab * segs_host[s].dim;
     off = (off + 3) / 4 * 4;  // float4-aligned partials
@@ -1320,6 +1459,18 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
   if (a.tblock_start[nseg] > 0) {
     gather_bwd_slot_kernel<<<a.tblock_start[nseg], 256, a.slot_lds, st>>>(a);
     RS_CHECK_LAUNCH("rs_gather_bwd slot");
+  }
+  if (a.oblock_start[nseg] > 0) {
+    int mt = 1;
+    for (int s = 0; s < nseg; ++s)
+      while (a.oh[s] && 16 * mt < segs_host[s].vocab) mt *= 2;
+    const int nb = a.oblock_start[nseg];
+    switch (mt) {
+      case 1: gather_bwd_onehot_kernel<1><<<nb, kOhWaves * 64, a.oh_lds, st>>>(a); break;
+      case 2: gather_bwd_onehot_kernel<2><<<nb, kOhWaves * 64, a.oh_lds, st>>>(a); break;
+      default: gather_bwd_onehot_kernel<4><<<nb, kOhWaves * 64, a.oh_lds, st>>>(a); break;
+    }
+    RS_CHECK_LAUNCH("rs_gather_bwd onehot");
   }
   if (a.ws_floats > 0 && reduce_deferring()) {
     // queued for rs_reduce_flush (reduce.hip): the same per-element order as reduce_partials_kernel

@@ -272,8 +272,9 @@ def test_gather_backward_ranged_hot_tables(monkeypatch, V, D, rows, Lb, mode):
     n = rows * Lb
     L = _hip.lib()
     ranged = 48 * 1024 < V * D * 4 <= 4 << 20 and D >= 16 and n >= 8 * V
-    assert (L.rs_gather_ws_bytes(arr, 1, rows) > 0) == ranged  # partials in ws
-    det_ok = V * D * 4 <= 4 << 20 and (D >= 16 or V * D * 4 <= 48 * 1024)  # slot or ranged
+    onehot = V <= 64 and D <= 16 and n >= 65536  # gather_bwd_onehot_kernel, both modes
+    assert (L.rs_gather_ws_bytes(arr, 1, rows) > 0) == (ranged or onehot)  # partials in ws
+    det_ok = V * D * 4 <= 4 << 20 and (D >= 16 or V * D * 4 <= 48 * 1024)  # slot, ranged or one-hot
     grads = []
     # the planned path, deterministic mode twice, the atomic scatter
     for off, det in (('', 0), ('', 1), ('', 1), ('1', 0)):
@@ -298,6 +299,55 @@ def test_gather_backward_ranged_hot_tables(monkeypatch, V, D, rows, Lb, mode):
     if det_ok:  # slot-image and ranged gradients are bitwise reproducible
         assert torch.equal(grads[1], grads[2])
     # out-of-range / negative ids contribute nothing and do not fault
+    bad = ids.clone()
+    bad.view(-1)[5] = V + 100
+    bad.view(-1)[6] = -3
+    g = torch.zeros(V, D, device=DEV)
+    ops.gather_bwd([_seg(**dict(seg, idx=bad.data_ptr()), grad=g.data_ptr())], rows, dout)
+    assert torch.isfinite(g).all()
+
+
+@pytest.mark.parametrize('V,D,rows,Lb,mode', [(30, 8, 204800, 3, 'mean'), (30, 8, 22000, 3, 'sum'),
+                                               (3, 4, 70000, 1, None), (25, 8, 65537, 1, None),
+                                               (64, 8, 70001, 1, None), (64, 16, 8000, 9, 'mean'),
+                                               (17, 3, 1333, 50, 'sum'), (1, 1, 65536, 1, None),
+                                               (50, 10, 70000, 5, 'mean')])
+def test_gather_backward_onehot_tiny_tables(monkeypatch, V, D, rows, Lb, mode):
+    """Tiny, heavily hit tables (V <= 64, D <= 16, >= 65,536 lookups a call: C2's per-token genre
+    bags of the history) take the one-hot MFMA kernel in both modes
+    (gather.hip gather_bwd_onehot_kernel): against the embedding backward (padding row skipped,
+    out-of-range ids ignored, grad accumulated), bitwise reproducible, and within fp32 summation
+    order of the atomic kernel (RSYS_NO_ONEHOT_GRAD=1). Odd row counts, bags longer than one pass
+    of four ids, D not a multiple of 4."""
+    t = rnd(V, D, seed=41).requires_grad_(True)
+    shape = (rows,) if mode is None else (rows, Lb)
+    ids = torch.randint(0, V, shape, device=DEV)
+    ids.view(-1)[::13] = 0  # padding row
+    ids.view(-1)[:100] = V - 1  # one row many times in one batch
+    kind = _hip.RS_SEG_SPARSE if mode is None else _hip.RS_SEG_POOL
+    ldo = D + 5
+    dout = rnd(rows, ldo, seed=42)
+    emb = F.embedding(ids, t, padding_idx=0)
+    ref = emb if mode is None else (emb.mean(1) if mode == 'mean' else emb.sum(1))
+    ref.backward(dout[:, 3:3 + D])
+    seg = dict(kind=kind, dim=D, out_col=3, vocab=V, idx_stride=1 if mode is None else Lb, idx=ids.data_ptr(),
+               table=t.data_ptr(), pad_idx=0)
+    if mode is not None:
+        seg.update(pool_mode=_hip.RS_POOL[mode], bag=Lb)
+    assert _hip.lib().rs_gather_ws_bytes(ops.segments_array([_seg(**seg)]), 1, rows) > 0
+    grads = []
+    for off in ('', '', '1'):
+        monkeypatch.setenv('RSYS_NO_ONEHOT_GRAD', off)
+        g = torch.full((V, D), 0.5, device=DEV)
+        ops.gather_bwd([_seg(**seg, grad=g.data_ptr())], rows, dout)
+        torch.cuda.synchronize()
+        grads.append(g)
+    monkeypatch.delenv('RSYS_NO_ONEHOT_GRAD')
+    assert torch.equal(grads[0], grads[1])
+    scale = max(1.0, t.grad.abs().max().item())
+    for gr in grads:
+        assert (gr - 0.5 - t.grad).abs().max().item() <= 2e-5 * scale * max(1, Lb // 8)
+        assert (gr[0] == 0.5).all() or V == 1
     bad = ids.clone()
     bad.view(-1)[5] = V + 100
     bad.view(-1)[6] = -3

@@ -2,7 +2,7 @@
 and C2's per-token sequence tables, per plan variant: default (atomic small-table kernel, ranged
 for hot 48 KB - 4 MB tables), RSYS_DETERMINISTIC=1 (slot-image / ranged kernels for every table),
 RSYS_NO_RANGE_GRAD=1 (atomic scatter for the mid tables too). Event time per call (host launch overhead included); run
-under rocprofv3 --kernel-trace --stats for the kernels.
+under rocprofv3 --kernel-trace --stats for the kernels. RSYS_NO_ONEHOT_GRAD=1 (round 5): the tiny tables back on the atomic / slot kernels.
 
     python tools/gather_bwd_time.py
 """
@@ -71,10 +71,10 @@ def timeit(segs, rows, ld, n=50):
     return e0.elapsed_time(e1) / n * 1e3
 
 
-KEYS = ('RSYS_NO_RANGE_GRAD', 'RSYS_DETERMINISTIC')
+KEYS = ('RSYS_NO_RANGE_GRAD', 'RSYS_DETERMINISTIC', 'RSYS_NO_ONEHOT_GRAD')
 for label, (segs, rows, ld) in cases.items():
     for name, env in [('default', {}), ('determ', {'RSYS_DETERMINISTIC': '1'}),
-                      ('atomic', {'RSYS_NO_RANGE_GRAD': '1'})]:
+                      ('atomic', {'RSYS_NO_RANGE_GRAD': '1'}), ('no_onehot', {'RSYS_NO_ONEHOT_GRAD': '1'})]:
         for k in KEYS:
             os.environ.pop(k, None)
         os.environ.update(env)
