@@ -1288,7 +1288,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     }
   }
   a.tblock_start[nseg] = ob;
-  // one-hot tables: <= 256 workgroups of 8 waves, each wave a run of whole 32-row batches (C2's
+  // one-hot tables: workgroups of 8 waves, each wave a run of whole 32-row batches (C2's
   // genre tokens: 200 workgroups of 4 batches a wave, 26.2 us a call against 27.3 at 400 x 2 and
   // 35.0 at 800 x 1 -- the partials and workgroup launches cost more than the batch round trips)
   int hb = 0;
@@ -1298,7 +1298,11 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.oh_rpw[s] = 0;
     if (!a.oh[s]) continue;
     const int64_t per_wave_min = 4 * kOhSteps;
-    int64_t nb = std::min<int64_t>(256, std::max<int64_t>(1, cdiv(rows, kOhWaves * per_wave_min)));
+    // <= 128 rows (4 batches) a wave once the grid is past 256 workgroups (C5's 819,200 history
+    // tokens: 800 workgroups rather than 13 serial batches a wave)
+    int64_t nb = std::max<int64_t>(std::min<int64_t>(256, cdiv(rows, kOhWaves * per_wave_min)),
+                                   std::min<int64_t>(1024, cdiv(rows, kOhWaves * 128)));
+    nb = std::max<int64_t>(1, nb);
     int64_t rpw = cdiv(cdiv(rows, nb * kOhWaves), per_wave_min) * per_wave_min;
     if (const char* e = getenv("RSYS_OH_RPW")) rpw = std::max<int64_t>(per_wave_min, atoi(e) / per_wave_min * per_wave_min);  // tuning only
     nb = std::max<int64_t>(1, cdiv(rows, rpw * kOhWaves));
