@@ -1087,6 +1087,10 @@ __global__ __launch_bounds__(kReduceWaves * 64) void reduce_partials_kernel(SegL
 // Linear(1, D) backward: dW[c] += sum_b dout[b,c]*x[b]; db[c] += sum_b dout[b,c].
 // One 1024-thread workgroup per dense segment: 1024/D row lanes, 8 rows in flight per lane,
 // then a fixed-order LDS reduction (deterministic).
+// One workgroup per dense segment (Linear(1, D) of one input column): dW[c] += sum_r dout[r][c] x[r],
+// db[c] += sum_r dout[r][c]. Row-lanes keep 16 rows' loads in flight; the row-lanes of a column
+// meet by wave shuffles, then across waves in a fixed LDS order (round 5: C2's D = 8 column was
+// 11.9 us -- four load round trips and a 128-long serial LDS sum per column)
 __global__ __launch_bounds__(1024) void dense_bwd_kernel(SegLaunch a) {
   const int s = blockIdx.x;
   const rs_feature_seg_t& sg = a.segs[s];
@@ -1095,18 +1099,19 @@ __global__ __launch_bounds__(1024) void dense_bwd_kernel(SegLaunch a) {
   const int D = sg.dim;
   const int lanes = 1024 / D;  // D <= 256
   const int c = threadIdx.x % D, rl = threadIdx.x / D;
+  constexpr int U = 16;
   float aw = 0.f, ab = 0.f;
   if (rl < lanes) {
     int row = rl;
-    for (; row + 7 * lanes < a.rows; row += 8 * lanes) {
-      float gv[8], xv[8];
+    for (; row + (U - 1) * lanes < a.rows; row += U * lanes) {
+      float gv[U], xv[U];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < U; ++u) {
         gv[u] = a.dout[(int64_t)(row + u * lanes) * a.ldo + sg.out_col + c];
         xv[u] = sg.x[(int64_t)(row + u * lanes) * sg.idx_stride];
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < U; ++u) {
         aw += gv[u] * xv[u];
         ab += gv[u];
       }
@@ -1117,14 +1122,30 @@ __global__ __launch_bounds__(1024) void dense_bwd_kernel(SegLaunch a) {
       ab += gv;
     }
   }
-  red_w[threadIdx.x] = aw;
-  red_b[threadIdx.x] = ab;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int np;  // partials per column in red_*[i * D + c]
+  if (D < 64 && 64 % D == 0) {
+    // the 64 / D row-lanes of a column inside one wave: butterfly (every lane ends with the sum)
+    for (int off = D; off < 64; off <<= 1) {
+      aw += __shfl_xor(aw, off, 64);
+      ab += __shfl_xor(ab, off, 64);
+    }
+    if (lane < D) {
+      red_w[w * D + c] = aw;
+      red_b[w * D + c] = ab;
+    }
+    np = 16;
+  } else {
+    red_w[threadIdx.x] = aw;
+    red_b[threadIdx.x] = ab;
+    np = lanes;
+  }
   __syncthreads();
   if (threadIdx.x < D) {
-    float w = 0.f, b = 0.f;
-    for (int i = 0; i < lanes; ++i) { w += red_w[i * D + c]; b += red_b[i * D + c]; }
-    sg.grad[c] += w;
-    sg.grad_bias[c] += b;
+    float sw = 0.f, sb = 0.f;
+    for (int i = 0; i < np; ++i) { sw += red_w[i * D + c]; sb += red_b[i * D + c]; }
+    sg.grad[c] += sw;
+    sg.grad_bias[c] += sb;
   }
 }
 

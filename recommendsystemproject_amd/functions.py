@@ -712,7 +712,11 @@ class SeqEncoderFn(torch.autograd.Function):
         try:
             with ops.deferred_reduce(defer):
                 if ctx.prune:
-                    dx = layer_bwd_last(ctx.layers[n - 1], ctx.layer_saved[n - 1], dout.clone(), ctx.key_pad,
+                    # the fused bf16 FFN backward only reads the output gradient; the fp32 path's
+                    # norm2 backward runs in place over it (autograd's buffer: give it a copy)
+                    ls = ctx.layer_saved[n - 1]
+                    d_last = dout if isinstance(ls[8], tuple) else dout.clone()
+                    dx = layer_bwd_last(ctx.layers[n - 1], ls, d_last, ctx.key_pad,
                                         ctx.last, B, L, d, H, p, key, _layer_site(n - 1))
                     n -= 1
                 else:
