@@ -656,11 +656,11 @@ __device__ void scatter_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int 
   }
 }
 
-__global__ __launch_bounds__(256) void gather_bwd_kernel(SegLaunch a) {
-  const int s = find_seg(a, blockIdx.x);
+__device__ __forceinline__ void gather_bwd_body(const SegLaunch& a, int bid) {
+  const int s = find_seg(a, bid);
   const rs_feature_seg_t& sg = a.segs[s];
   if (sg.kind == RS_SEG_DENSE || a.small[s]) return;
-  const int lb = blockIdx.x - a.block_start[s];
+  const int lb = bid - a.block_start[s];
   const int C = a.chunks[s], S = a.split[s];
   const int grp = threadIdx.x / C, chunk = threadIdx.x % C;
   const int r = grp / S, p = grp % S;
@@ -677,12 +677,13 @@ __global__ __launch_bounds__(256) void gather_bwd_kernel(SegLaunch a) {
   else scatter_seg<false>(a, sg, row, chunk, nullptr, lbeg, lend);
 }
 
-__global__ __launch_bounds__(256) void gather_bwd_small_kernel(SegLaunch a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+__global__ __launch_bounds__(256) void gather_bwd_kernel(SegLaunch a) { gather_bwd_body(a, blockIdx.x); }
+
+__device__ __forceinline__ void gather_bwd_small_body(const SegLaunch& a, int bid, float* lds) {
   int s = 0;
-  while (s + 1 < a.nseg && (int)blockIdx.x >= a.sblock_start[s + 1]) ++s;
+  while (s + 1 < a.nseg && bid >= a.sblock_start[s + 1]) ++s;
   const rs_feature_seg_t& sg = a.segs[s];
-  const int lb = blockIdx.x - a.sblock_start[s];
+  const int lb = bid - a.sblock_start[s];
   const int nblk = a.sblocks[s];
   const int n = (int)(sg.vocab * sg.dim);
   for (int e = threadIdx.x; e < n; e += 256) lds[e] = 0.f;
@@ -701,6 +702,90 @@ __global__ __launch_bounds__(256) void gather_bwd_small_kernel(SegLaunch a) {
     const float v = lds[e];
     if (v != 0.f) atomicAdd(sg.grad + e, v);
   }
+}
+
+__global__ __launch_bounds__(256) void gather_bwd_small_kernel(SegLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  gather_bwd_small_body(a, blockIdx.x, lds);
+}
+
+// dense segment s (Linear(1, D) of one input column) by one 256-thread workgroup: dW[c] +=
+// sum_r dout[r][c] x[r], db[c] += sum_r dout[r][c]; row-lanes with 16 rows' loads in flight, the
+// row-lanes of a column summed by wave shuffles and then in wave order (deterministic). red: 512
+// floats of LDS
+__device__ __forceinline__ void dense_bwd_body(const SegLaunch& a, int s, float* red) {
+  const rs_feature_seg_t& sg = a.segs[s];
+  const int D = sg.dim;
+  const int lanes = 256 / D;  // D <= 256
+  const int c = threadIdx.x % D, rl = threadIdx.x / D;
+  constexpr int U = 16;
+  float aw = 0.f, ab = 0.f;
+  if (rl < lanes) {
+    int row = rl;
+    for (; row + (U - 1) * lanes < a.rows; row += U * lanes) {
+      float gv[U], xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        gv[u] = a.dout[(int64_t)(row + u * lanes) * a.ldo + sg.out_col + c];
+        xv[u] = sg.x[(int64_t)(row + u * lanes) * sg.idx_stride];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        aw += gv[u] * xv[u];
+        ab += gv[u];
+      }
+    }
+    for (; row < a.rows; row += lanes) {
+      const float gv = a.dout[(int64_t)row * a.ldo + sg.out_col + c];
+      aw += gv * sg.x[(int64_t)row * sg.idx_stride];
+      ab += gv;
+    }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int np;  // partials per column at red[i * D + c] (weights) and red[256 + i * D + c] (bias)
+  if (D < 64 && 64 % D == 0) {
+    for (int off = D; off < 64; off <<= 1) {
+      aw += __shfl_xor(aw, off, 64);
+      ab += __shfl_xor(ab, off, 64);
+    }
+    if (lane < D) {
+      red[w * D + c] = aw;
+      red[256 + w * D + c] = ab;
+    }
+    np = 4;
+  } else {
+    red[threadIdx.x] = aw;
+    red[256 + threadIdx.x] = ab;
+    np = lanes;
+  }
+  __syncthreads();
+  if (threadIdx.x < D) {
+    float sw = 0.f, sb = 0.f;
+    for (int i = 0; i < np; ++i) { sw += red[i * D + c]; sb += red[256 + i * D + c]; }
+    sg.grad[c] += sw;
+    sg.grad_bias[c] += sb;
+  }
+}
+
+// the backward's scatter, small-table and dense work in ONE launch (round 5): blocks [0, nsmall)
+// the small-table kernel's, then one per dense segment, then the scatter's (C2's user tower: three
+// launches on the critical chain, 8.7 + 13.3 + 12.2 us)
+__global__ __launch_bounds__(256) void gather_bwd_fused_kernel(SegLaunch a, int nsmall, int ndense) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  int b = blockIdx.x;
+  if (b < nsmall) {
+    gather_bwd_small_body(a, b, lds);
+    return;
+  }
+  b -= nsmall;
+  if (b < ndense) {
+    int s = 0, k = 0;
+    for (; s < a.nseg; ++s)
+      if (a.segs[s].kind == RS_SEG_DENSE && k++ == b) break;
+    dense_bwd_body(a, s, lds);
+    return;
+  }
+  gather_bwd_body(a, b - ndense);
 }
 
 // Small tables in deterministic mode (rs_set_deterministic; <= 16 KB, or up to 48 KB when the
@@ -1267,7 +1352,7 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     if (a.hot[s]) {
       const int ng = cdiv(rows, a.rpb[s]);
       blocks += ng < kHotBlocks ? ng : kHotBlocks;
-    } else if (!a.small[s] && !a.rranges[s] && !a.tiny[s] && !a.oh[s]) {
+    } else if (!a.small[s] && !a.rranges[s] && !a.tiny[s] && !a.oh[s] && !(bwd && g.kind == RS_SEG_DENSE)) {
       blocks += cdiv(rows, a.rpb[s] * a.rpt[s]);
     }
   }
@@ -1469,11 +1554,19 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
   RS_CHECK_ARG(ws || a.ws_floats == 0,
                "rs_gather_bwd: small / ranged table gradients need ws (rs_gather_ws_bytes)");
   hipStream_t st = as_stream(stream);
-  if (a.block_start[nseg] > 0) {
+  int ndense = 0;
+  for (int s = 0; s < nseg; ++s) ndense += segs_host[s].kind == RS_SEG_DENSE;
+  const bool split = getenv_flag("RSYS_GATHER_BWD_SPLIT");  // A/B: three launches
+  if (!split && a.block_start[nseg] + a.sblock_start[nseg] + ndense > 0) {
+    gather_bwd_fused_kernel<<<a.sblock_start[nseg] + ndense + a.block_start[nseg], 256,
+                              std::max(a.small_lds, 512 * 4), st>>>(a, a.sblock_start[nseg], ndense);
+    RS_CHECK_LAUNCH("rs_gather_bwd");
+  }
+  if (split && a.block_start[nseg] > 0) {
     gather_bwd_kernel<<<a.block_start[nseg], 256, 0, st>>>(a);
     RS_CHECK_LAUNCH("rs_gather_bwd");
   }
-  if (a.sblock_start[nseg] > 0) {
+  if (split && a.sblock_start[nseg] > 0) {
     gather_bwd_small_kernel<<<a.sblock_start[nseg], 256, a.small_lds, st>>>(a);
     RS_CHECK_LAUNCH("rs_gather_bwd small");
   }
@@ -1515,9 +1608,7 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
     reduce_partials_kernel<<<(int)std::min<int64_t>(cdiv(nel, 64), 1024), kReduceWaves * 64, 0, st>>>(a);
     RS_CHECK_LAUNCH("rs_gather_bwd partials");
   }
-  bool any_dense = false;
-  for (int s = 0; s < nseg; ++s) any_dense |= segs_host[s].kind == RS_SEG_DENSE;
-  if (any_dense) {
+  if (split && ndense) {
     dense_bwd_kernel<<<nseg, 1024, 0, st>>>(a);
     RS_CHECK_LAUNCH("rs_gather_bwd dense");
   }
