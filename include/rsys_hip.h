@@ -531,6 +531,11 @@ int rs_clip_coef_prepare(const double* ws, int nparts, float max_norm, float* to
                          void* stream);
 int rs_clip_coef_step(const double* ws, int nparts, float max_norm, float* total_norm, float* coef,
                       int64_t* counter, void* stream);
+/* rs_grad_sqnorm + rs_clip_coef_step in one launch (round 5): the last workgroup of the partials
+ * makes the coefficient (same bits) and advances *counter (nullable). ticket: one int, zero
+ * before the first call; the call leaves it zero (clip_grad_norm_, training_utils.py:53-54) */
+int rs_grad_sqnorm_clip_step(const float* g, int64_t n, float scale, double* ws, int* ticket, float max_norm,
+                             float* total_norm, float* coef, int64_t* counter, void* stream);
 int rs_scale_inplace(float* g, int64_t n, float scale, const float* coef, void* stream);
 int rs_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, float beta1,
                  float beta2, float eps, float weight_decay, int step, const int64_t* step_dev,

@@ -129,6 +129,7 @@ SIGNATURES = {
     'rs_sqnorm_parts': (i32, [i64]),
     'rs_clip_coef': (i32, [vp, i32, f32, vp, vp, vp]),
     'rs_clip_coef_step': (i32, [vp, i32, f32, vp, vp, vp, vp]),
+    'rs_grad_sqnorm_clip_step': (i32, [vp, i64, f32, vp, vp, f32, vp, vp, vp, vp]),
     'rs_clip_coef_prepare': (i32, [vp, i32, f32, vp, vp, vp, vp, i32, f32, f32, f32, vp]),
     'rs_sorted_sqnorm_batch_dense': (i32, [vp, i32, f32, vp, vp, i64, vp, vp]),
     'rs_sorted_adam_batch_dense': (i32, [vp, i32, vp, vp, f32, f32, f32, f32, f32, vp, vp, vp, vp, vp, i64, f32,

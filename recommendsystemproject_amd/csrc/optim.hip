@@ -49,6 +49,76 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g
   if (threadIdx.x == 0) ws[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// rs_grad_sqnorm_clip_step: sqnorm_kernel's partials, and the last workgroup to finish turns them
+// into the clip coefficient exactly as clip_coef_kernel does (its 1,024 threads' strided sums
+// emulated as 4 per thread, the same wave trees, the same 16-way order: the same bits) and
+// advances the step counter -- one launch instead of two on the optimizer's chain (round 5). The
+// hand-off is fence-free (MI355X_MICROARCH.md): each workgroup's partial store is drained
+// (vmcnt(0)) before its agent-scope ticket; the last one reads the partials with agent-scope loads
+// and re-arms the ticket.
+__global__ __launch_bounds__(256) void sqnorm_clip_kernel(const float* __restrict__ g, int64_t n, float scale,
+                                                          double* __restrict__ ws, int* __restrict__ ticket,
+                                                          float max_norm, float* total_norm, float* coef,
+                                                          int64_t* counter) {
+  __shared__ double red[16];
+  __shared__ int s_last;
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t n4 = n / 4;
+  const bool vec = (reinterpret_cast<uintptr_t>(g) & 15) == 0;
+  if (vec) {
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+      const float4 v = g4[i];
+      const float a = v.x * scale, b = v.y * scale, c = v.z * scale, d = v.w * scale;
+      acc += (double)(a * a) + (double)(b * b) + (double)(c * c) + (double)(d * d);
+    }
+    for (int64_t i = n4 * 4 + blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+      const float a = g[i] * scale;
+      acc += (double)(a * a);
+    }
+  } else {
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+      const float a = g[i] * scale;
+      acc += (double)(a * a);
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(ws + blockIdx.x, red[0] + red[1] + red[2] + red[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const int nb = gridDim.x;
+  double t[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {  // virtual thread threadIdx.x + 256 q of clip_coef_kernel
+    t[q] = 0.0;
+    for (int i = threadIdx.x + 256 * q; i < nb; i += 1024)
+      t[q] += __hip_atomic_load(ws + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();  // red reused
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double v = wave_sum(t[q]);
+    if ((threadIdx.x & 63) == 0) red[4 * q + (threadIdx.x >> 6)] = v;  // virtual wave 4 q + wave
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double tt = 0.0;
+  for (int w = 0; w < 16; ++w) tt += red[w];
+  const float norm = (float)sqrt(tt);
+  if (total_norm) *total_norm = norm;
+  float c = max_norm / (norm + 1e-6f);
+  *coef = c < 1.f ? c : 1.f;
+  if (counter) *counter += 1;
+  *ticket = 0;
+}
+
 // fixed-order (deterministic) sum of nb partials: strided per-thread sums, then a fixed tree
 __global__ __launch_bounds__(1024) void clip_coef_kernel(const double* __restrict__ ws, int nb,
                                                          float max_norm, float* total_norm,
@@ -176,6 +246,16 @@ extern "C" int rs_grad_sqnorm(const float* g, int64_t n, float scale, double* ws
 }
 
 extern "C" int rs_sqnorm_parts(int64_t n) { return sq_blocks(n); }
+
+extern "C" int rs_grad_sqnorm_clip_step(const float* g, int64_t n, float scale, double* ws, int* ticket,
+                                        float max_norm, float* total_norm, float* coef, int64_t* counter,
+                                        void* stream) {
+  RS_CHECK_ARG(g && ws && ticket && coef && n >= 0, "rs_grad_sqnorm_clip_step: bad args");
+  sqnorm_clip_kernel<<<sq_blocks(n), 256, 0, as_stream(stream)>>>(g, n, scale, ws, ticket, max_norm, total_norm,
+                                                                  coef, counter);
+  RS_CHECK_LAUNCH("rs_grad_sqnorm_clip_step");
+  return 0;
+}
 
 extern "C" int rs_clip_coef(const double* ws, int nparts, float max_norm, float* total_norm,
                             float* coef, void* stream) {

@@ -69,6 +69,7 @@ class _DeviceClip:
     def __init__(self, device):
         self.norm = torch.zeros((), device=device, dtype=torch.float32)
         self.coef = torch.ones((), device=device, dtype=torch.float32)
+        self.ticket = torch.zeros((), device=device, dtype=torch.int32)  # rs_grad_sqnorm_clip_step
 
     def compute(self, g, n, max_norm, scale=1.0, lazy=(), counter=None, prepare=None):
         """2-norm of g[:n] plus the distinct rows of every lazy table's step calls (their other
@@ -92,6 +93,13 @@ class _DeviceClip:
         # region's in the first of those launches
         items = [(_sorted_call(t, c, i, g=g, owner=owner), k) for k, (t, c, owner, i) in enumerate(work)]
         batches = _sorted_batches(items)
+        if (not work and prepare is None and os.environ.get('RSYS_OPT_FUSE', '1') != '0'
+                and os.environ.get('RSYS_SQNORM_CLIP_FUSED', '1') != '0'):
+            # no lazy tables: the partials and the coefficient in one launch (same bits)
+            _hip.call('rs_grad_sqnorm_clip_step', g.data_ptr(), n, float(scale), ws.data_ptr(),
+                      self.ticket.data_ptr(), float(max_norm), self.norm.data_ptr(), self.coef.data_ptr(),
+                      counter.data_ptr() if counter is not None else None, ops.stream())
+            return
         if not batches or os.environ.get('RSYS_OPT_FUSE', '1') == '0':
             _hip.call('rs_grad_sqnorm', g.data_ptr(), n, float(scale), ws.data_ptr(), ops.stream())
         for j, batch in enumerate(batches):

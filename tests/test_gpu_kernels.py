@@ -692,6 +692,38 @@ def test_clip_coefficient():
     assert abs(coef.item() - min(1.0, 1.0 / (tn + 1e-6))) < 1e-6
 
 
+@pytest.mark.parametrize('n', [1, 4097, 100003, 1900000, 5000000])
+def test_sqnorm_clip_one_launch_bitwise(n):
+    """rs_grad_sqnorm_clip_step (the partials' last workgroup makes the coefficient, advances the
+    step counter, re-arms its ticket) against rs_grad_sqnorm + rs_clip_coef_step: the same bits,
+    twice in a row (the ticket is left at zero)."""
+    L = _hip.lib()
+    g = rnd(n, seed=7) * 0.01
+    nparts = int(L.rs_sqnorm_parts(n))
+    ws = torch.empty(nparts + 2, dtype=torch.float64, device=DEV)
+    out = []
+    for fused in (0, 1, 1):
+        norm = torch.zeros((), device=DEV)
+        coef = torch.zeros((), device=DEV)
+        cnt = torch.full((), 5, dtype=torch.int64, device=DEV)
+        if fused:
+            ticket = out[-1][3] if len(out) > 1 else torch.zeros((), dtype=torch.int32, device=DEV)
+            _hip.call('rs_grad_sqnorm_clip_step', g.data_ptr(), n, 0.5, ws.data_ptr(), ticket.data_ptr(), 0.3,
+                      norm.data_ptr(), coef.data_ptr(), cnt.data_ptr(), ops.stream())
+        else:
+            ticket = None
+            _hip.call('rs_grad_sqnorm', g.data_ptr(), n, 0.5, ws.data_ptr(), ops.stream())
+            _hip.call('rs_clip_coef_step', ws.data_ptr(), nparts, 0.3, norm.data_ptr(), coef.data_ptr(),
+                      cnt.data_ptr(), ops.stream())
+        torch.cuda.synchronize()
+        out.append((norm.clone(), coef.clone(), cnt.item(), ticket))
+    for o in out[1:]:
+        assert torch.equal(o[0], out[0][0]) and torch.equal(o[1], out[0][1]) and o[2] == 6
+        assert o[3].item() == 0
+    tn = (0.5 * g).double().norm().item()
+    assert abs(out[0][0].item() - tn) < 1e-5 * tn
+
+
 @pytest.mark.parametrize('B,L,d,p', [(4096, 50, 64, 0.15), (37, 7, 64, 0.3), (300, 20, 16, 0.5)])
 def test_seq_input_dropout_bwd_fused(B, L, d, p):
     """rs_seq_input_dropout_bwd (one pass: drop_b backward, positional-embedding colsum, drop_a
