@@ -58,12 +58,26 @@ __global__ __launch_bounds__(256) void seq_input_dropout_bwd_kernel(float* __res
   float4 acc[kSeqDropCols];
 #pragma unroll
   for (int u = 0; u < kSeqDropCols; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // the next row's loads are issued before this row's hashes and stores (one row in flight
+  // behind the other: the loop was a load round trip per row)
+  // (unconditional loads -- row and column clamped, the extra values unused: a guarded load
+  // would make the join wait for it)
+  float4 nx[kSeqDropCols];
+  if (r0 >= r1) return;
+#pragma unroll
+  for (int u = 0; u < kSeqDropCols; ++u) {
+    const int g = min(threadIdx.x + 256 * u, G4 - 1);
+    nx[u] = *reinterpret_cast<const float4*>(dx + (int64_t)r0 * N + 4 * g);
+  }
   for (int row = r0; row < r1; ++row) {
     float4 v[kSeqDropCols];
 #pragma unroll
-    for (int u = 0; u < kSeqDropCols; ++u) {  // loads first, then the hashes
-      const int g = threadIdx.x + 256 * u;
-      if (g < G4) v[u] = *reinterpret_cast<const float4*>(dx + (int64_t)row * N + 4 * g);
+    for (int u = 0; u < kSeqDropCols; ++u) v[u] = nx[u];
+    const int rn = min(row + 1, r1 - 1);
+#pragma unroll
+    for (int u = 0; u < kSeqDropCols; ++u) {
+      const int g = min(threadIdx.x + 256 * u, G4 - 1);
+      nx[u] = *reinterpret_cast<const float4*>(dx + (int64_t)rn * N + 4 * g);
     }
 #pragma unroll
     for (int u = 0; u < kSeqDropCols; ++u) {
