@@ -639,6 +639,23 @@ int64_t rs_segsum_ws_bytes(int64_t n, int D);
 int rs_segsum(const uint32_t* keys, const uint32_t* vals, int64_t n, int bag, int mode, int64_t pad,
               const float* dout, int64_t ldo, int D, float* grad, int accumulate, void* ws,
               void* stream);
+/* Up to 4 rs_segsum calls of one row width D on DIFFERENT tables (distinct grad) in one launch
+ * pair (round 5); each call's arguments as rs_segsum's, its own ws (rs_segsum_ws_bytes), n >= 1.
+ * Same results as the calls one by one. */
+typedef struct rs_segsum_call {
+  const uint32_t* keys;
+  const uint32_t* vals;
+  int64_t n;
+  int bag;
+  int mode;
+  int64_t pad;
+  const float* dout;
+  int64_t ldo;
+  float* grad;
+  int accumulate;
+  void* ws;
+} rs_segsum_call_t;
+int rs_segsum_batch(const rs_segsum_call_t* calls, int ncalls, int D, void* stream);
 /* Row-sharded large tables under data parallelism (dist.py): rank r of W owns rows id % W == r
  * at local row id / W. Maps all-gathered int32 ids to int64 local rows (-1: owned elsewhere);
  * out-of-range ids set *err_flag (nullable) as rs_gather_fwd does (GenericTower.py:184-196),

@@ -38,6 +38,12 @@ class SortedCall(C.Structure):
                 ('last', vp), ('owner', vp)]
 
 
+class SegsumCall(C.Structure):
+    """Mirror of rs_segsum_call_t."""
+    _fields_ = [('keys', vp), ('vals', vp), ('n', i64), ('bag', i32), ('mode', i32), ('pad', i64), ('dout', vp),
+                ('ldo', i64), ('grad', vp), ('accumulate', i32), ('ws', vp)]
+
+
 # name -> (restype, argtypes). Every symbol declared in include/rsys_hip.h.
 SIGNATURES = {
     'rs_version': (i32, []),
@@ -161,6 +167,7 @@ SIGNATURES = {
     'rs_sorted_zero_grad': (i32, [vp, i64, i32, vp, vp]),
     'rs_segsum_ws_bytes': (i64, [i64, i32]),
     'rs_segsum': (i32, [vp, vp, i64, i32, i32, i64, vp, i64, i32, vp, i32, vp, vp]),
+    'rs_segsum_batch': (i32, [vp, i32, i32, vp]),
     'rs_shard_map_ids': (i32, [vp, i64, i64, i32, i32, vp, vp, vp]),
     'rs_shard_bucket_ws_bytes': (i64, [i64, i32]),
     'rs_shard_bucket': (i32, [vp, vp, i64, i32, i32, i64, vp, vp, vp, vp, vp, vp, vp]),

@@ -1403,25 +1403,39 @@ __device__ __forceinline__ void fix_run(const SegArgs& a, int blk) {
 }
 
 template <int NV, int G>
+__device__ __forceinline__ void segsum_body(const SegArgs& a, int bid, int2 (*slot)[64]) {
+  if (bid == 0 && threadIdx.x == 0) *a.cnt = 0;  // the fix kernel's ticket
+  const int chunk = bid * 4 + (threadIdx.x >> 6);
+  if (chunk < a.nchunks) segsum_chunk<NV, G>(a, chunk, slot[threadIdx.x >> 6]);
+}
+
+template <int NV, int G>
 __global__ __launch_bounds__(256) void segsum_kernel(SegArgs a) {
   __shared__ int2 slot[4][64];
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.cnt = 0;  // the fix kernel's ticket
-  const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (chunk < a.nchunks) segsum_chunk<NV, G>(a, chunk, slot[threadIdx.x >> 6]);
+  segsum_body<NV, G>(a, blockIdx.x, slot);
 }
 
 // Both fix levels in one launch (round 5): every wave runs level 1 for its block, the workgroups
 // hand their block partials and flags to the last one to finish (agent-scope stores, one ticket),
 // which runs level 2 for every block. Saves a launch per call (~4.5 us each on this box, three
 // calls on C3's critical path); RSYS_SEGSUM_TWO_FIX=1 keeps the two launches.
+struct FixLds {
+  int s_last;
+  int tails[256];
+  int ntails;
+};
+
+// block bid of nb of one call's fix launch
 template <int NV>
-__global__ __launch_bounds__(256) void segsum_fix_kernel(SegArgs a) {
-  __shared__ int s_last;
-  fix_block<NV, true>(a, blockIdx.x * 4 + (threadIdx.x >> 6));
+__device__ __forceinline__ void segsum_fix_body(const SegArgs& a, int bid, int nb, FixLds& L) {
+  int& s_last = L.s_last;
+  int* tails = L.tails;
+  int& ntails = L.ntails;
+  fix_block<NV, true>(a, bid * 4 + (threadIdx.x >> 6));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(a.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+    s_last = __hip_atomic_fetch_add(a.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
   __syncthreads();
   if (!s_last) return;
   // level 2 in the last workgroup: only blocks whose run continues past their right border have
@@ -1429,8 +1443,6 @@ __global__ __launch_bounds__(256) void segsum_fix_kernel(SegArgs a) {
   // walking every block (fix_run's flag load, then its early return) was ~50 dependent round
   // trips per wave at C3's 200 history blocks. Each listed block writes its own run's row, so the
   // order the waves take them in does not matter.
-  __shared__ int tails[256];
-  __shared__ int ntails;
   const int nblk = (a.nchunks + kFixBlock - 1) / kFixBlock;
   for (int b0 = 0; b0 < nblk; b0 += 256) {
     if (threadIdx.x == 0) ntails = 0;
@@ -1442,6 +1454,39 @@ __global__ __launch_bounds__(256) void segsum_fix_kernel(SegArgs a) {
     for (int i = threadIdx.x >> 6; i < ntails; i += 4) fix_run<NV, true>(a, tails[i]);
     __syncthreads();
   }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void segsum_fix_kernel(SegArgs a) {
+  __shared__ FixLds L;
+  segsum_fix_body<NV>(a, blockIdx.x, gridDim.x, L);
+}
+
+// several calls (different tables) in one segment-sum launch and one fix launch (round 5: C3's
+// user tower, the 1M-row user-id table and the 10M-row history table, were two launch pairs back
+// to back on the chain); each call's blocks, ticket and summation order are its own
+constexpr int kSegCalls = 4;
+struct SegBatch {
+  SegArgs c[kSegCalls];
+  int blk0[kSegCalls + 1];   // segsum blocks
+  int fblk0[kSegCalls + 1];  // fix blocks
+  int n;
+};
+
+template <int NV, int G>
+__global__ __launch_bounds__(256) void segsum_batch_kernel(SegBatch b) {
+  __shared__ int2 slot[4][64];
+  int k = 0;
+  while (k + 1 < b.n && (int)blockIdx.x >= b.blk0[k + 1]) ++k;
+  segsum_body<NV, G>(b.c[k], blockIdx.x - b.blk0[k], slot);
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void segsum_fix_batch_kernel(SegBatch b) {
+  __shared__ FixLds L;
+  int k = 0;
+  while (k + 1 < b.n && (int)blockIdx.x >= b.fblk0[k + 1]) ++k;
+  segsum_fix_body<NV>(b.c[k], blockIdx.x - b.fblk0[k], b.fblk0[k + 1] - b.fblk0[k], L);
 }
 
 template <int NV>
@@ -1816,6 +1861,50 @@ extern "C" int rs_segsum(const uint32_t* keys, const uint32_t* vals, int64_t n, 
   else if (D <= 128) { RS_SEGSUM(2, 32) }
   else { RS_SEGSUM(4, 64) }
 #undef RS_SEGSUM
+  return 0;
+}
+
+extern "C" int rs_segsum_batch(const rs_segsum_call_t* calls, int ncalls, int D, void* stream) {
+  RS_CHECK_ARG(calls && ncalls >= 1 && ncalls <= kSegCalls && D >= 1 && D <= 256 && D % 4 == 0,
+               "rs_segsum_batch: bad args (ncalls %d, D %d)", ncalls, D);
+  SegBatch b{};
+  int blk = 0, fblk = 0;
+  for (int i = 0; i < ncalls; ++i) {
+    const rs_segsum_call_t& c = calls[i];
+    RS_CHECK_ARG(c.keys && c.vals && c.dout && c.grad && c.ws && c.n >= 1 && c.n < ((int64_t)1 << 31) &&
+                     c.bag >= 1 && c.mode >= 0 && c.mode <= 2 && c.ldo >= D && c.ldo % 4 == 0 &&
+                     aligned16(c.dout) && aligned16(c.grad),
+                 "rs_segsum_batch: bad call %d", i);
+    for (int j = 0; j < i; ++j)
+      RS_CHECK_ARG(calls[j].grad != c.grad, "rs_segsum_batch: calls %d and %d write one table", j, i);
+    SegArgs& a = b.c[i];
+    a.keys = c.keys; a.vals = c.vals; a.n = c.n; a.bag = c.bag; a.mode = c.mode; a.pad = c.pad; a.dout = c.dout;
+    a.ldo = c.ldo; a.D = D; a.grad = c.grad; a.accumulate = c.accumulate;
+    a.nchunks = cdiv(c.n, kChunk);
+    a.part = static_cast<float*>(c.ws);
+    const int64_t np = a.nchunks + (a.nchunks + kFixBlock - 1) / kFixBlock;
+    a.flags = reinterpret_cast<int*>(a.part + np * 2 * D);
+    a.cnt = a.flags + np;
+    b.blk0[i] = blk;
+    b.fblk0[i] = fblk;
+    blk += cdiv(a.nchunks, 4);
+    fblk += cdiv(cdiv(a.nchunks, kFixBlock), 4);
+  }
+  b.blk0[ncalls] = blk;
+  b.fblk0[ncalls] = fblk;
+  b.n = ncalls;
+  hipStream_t st = as_stream(stream);
+#define RS_SEGSUM_B(NV, G)                                     \
+  segsum_batch_kernel<NV, G><<<blk, 256, 0, st>>>(b);          \
+  RS_CHECK_LAUNCH("rs_segsum_batch");                          \
+  segsum_fix_batch_kernel<NV><<<fblk, 256, 0, st>>>(b);        \
+  RS_CHECK_LAUNCH("rs_segsum_batch fix");
+  if (D <= 16) { RS_SEGSUM_B(1, 4) }
+  else if (D <= 32) { RS_SEGSUM_B(1, 8) }
+  else if (D <= 64) { RS_SEGSUM_B(1, 16) }
+  else if (D <= 128) { RS_SEGSUM_B(2, 32) }
+  else { RS_SEGSUM_B(4, 64) }
+#undef RS_SEGSUM_B
   return 0;
 }
 

@@ -362,6 +362,19 @@ class LazyTable:
                   dout_ptr, ldo, self.D, self.ptr(self.flat.grad), int(accumulate), ws.data_ptr(),
                   _stream())
 
+    def segsum_call(self, c, dout_ptr, ldo):
+        """The plain (single-process) segsum of call c as an rs_segsum_call_t for rs_segsum_batch
+        (functions._grad_tables batches the calls of different tables): (call, ws), or None where
+        segsum() takes another path (empty call, all-to-all, data parallelism)."""
+        if c.n == 0 or c.a2a is not None or _dp_active():
+            return None
+        ws = torch.empty(int(_hip.lib().rs_segsum_ws_bytes(c.n, self.D)) // 4 + 1, dtype=torch.int32,
+                         device=self.param.device)
+        sc = _hip.SegsumCall(keys=c.keys.data_ptr(), vals=c.vals.data_ptr(), n=c.n, bag=c.bag, mode=c.mode,
+                             pad=c.pad, dout=dout_ptr, ldo=ldo, grad=self.ptr(self.flat.grad),
+                             accumulate=int(len(self.calls) > 1), ws=ws.data_ptr())
+        return sc, ws
+
     def _a2a_local_segsum(self, c, dout_ptr, ldo):
         """Backward, requester side of an all-to-all call: the call's output gradient summed per
         distinct id into its bucket slot (send_grad [W x cap, D]); dist.exchange_lazy_grads sends

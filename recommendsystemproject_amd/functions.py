@@ -18,6 +18,7 @@ Function.forward grad mode is always off, so the modules decide whether to keep 
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import torch
@@ -206,10 +207,30 @@ def _grad_tables(segs, calls, dout, tables, rows, params=()):
     if rest:
         _gather_bwd_split(rest, rows, dout)
     _dp.note_writer(params, written=True)
+    # calls of different tables of one row width share one launch pair (rs_segsum_batch, up to 4
+    # a launch); a table's calls keep their order (each its own launch after the first);
+    # RSYS_SEGSUM_BATCH=0: one rs_segsum per call
+    batch_on = os.environ.get('RSYS_SEGSUM_BATCH', '1') != '0'
+    pending = []
+
+    def flush():
+        if pending:
+            arr = (_hip.SegsumCall * len(pending))(*[sc for _, sc, _ in pending])
+            _hip.call('rs_segsum_batch', C.addressof(arr), len(pending), pending[0][0].D, ops.stream())
+            pending.clear()
+
     for t, c, ptr in big:
         if ptr is None:  # max-pooled: its per-lookup gradient rows are already the call's dseg
             continue
-        t.segsum(c, ptr, dout.stride(0))
+        args = t.segsum_call(c, ptr, dout.stride(0)) if batch_on else None
+        if args is None:
+            flush()
+            t.segsum(c, ptr, dout.stride(0))
+            continue
+        if len(pending) == 4 or any(pt is t for pt, _, _ in pending) or (pending and pending[0][0].D != t.D):
+            flush()
+        pending.append((t, args[0], args[1]))
+    flush()
 
 
 _SORTED_ORDINARY_BYTES = 4 << 20

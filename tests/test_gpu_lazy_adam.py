@@ -138,6 +138,41 @@ def test_segsum_matches_dense_backward(mode, bag, D, zipf):
     assert torch.allclose(acc, base + got, atol=1e-5)
 
 
+@pytest.mark.parametrize('D', [128, 64, 40])
+def test_segsum_batch_bitwise(D):
+    """rs_segsum_batch (several tables' calls in one launch pair, functions._grad_tables) gives
+    the bits of the calls one by one: single ids, a mean bag of 50 (C3's user side), a sum bag,
+    accumulate on and off, n from 1 to 204,800."""
+    g = np.random.default_rng(D)
+    specs = [(1_000_000, 4096, 1, 0, 0, 0), (300_000, 4096, 50, 1, 0, 1), (5000, 777, 3, 2, 2, 0), (10, 1, 1, 0, -1, 1)]
+    calls, singles, keep = [], [], []
+    for V, B, bag, mode, pad, acc in specs:
+        ids = g.integers(0, V, size=(B, bag))
+        ids[g.random((B, bag)) < 0.2] = max(pad, 0)
+        t = torch.from_numpy(ids).to(DEV)
+        dout = torch.randn(B, D + 8, device=DEV)[:, 4:4 + D]
+        keys, vals = _sort(t, V)
+        base = torch.randn(V, D, device=DEV)
+        n = B * bag
+        singles.append(_segsum(keys, vals, n, bag, mode, pad, dout, V, D, acc=acc, grad=base.clone()))
+        grad = base.clone()
+        ws = torch.empty(int(_hip.lib().rs_segsum_ws_bytes(n, D)) // 4 + 1, dtype=torch.int32, device=DEV)
+        keep += [t, dout, keys, vals, grad, ws]
+        calls.append(_hip.SegsumCall(keys=keys.data_ptr(), vals=vals.data_ptr(), n=n, bag=bag, mode=mode, pad=pad,
+                                     dout=dout.data_ptr(), ldo=dout.stride(0), grad=grad.data_ptr(), accumulate=acc,
+                                     ws=ws.data_ptr()))
+    arr = (_hip.SegsumCall * len(calls))(*calls)
+    import ctypes
+    _hip.call('rs_segsum_batch', ctypes.addressof(arr), len(calls), D, ops.stream())
+    torch.cuda.synchronize()
+    for i, want in enumerate(singles):
+        assert torch.equal(keep[6 * i + 4], want), i
+    # one table twice in a batch is refused
+    arr2 = (_hip.SegsumCall * 2)(calls[0], calls[0])
+    with pytest.raises(RuntimeError):
+        _hip.call('rs_segsum_batch', ctypes.addressof(arr2), 2, D, ops.stream())
+
+
 def test_segsum_equals_atomic_scatter():
     """rs_segsum == the atomic scatter of rs_gather_bwd (ordinary tables) up to summation order."""
     from recommendsystemproject_amd.functions import _seg
