@@ -3,6 +3,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--batch 4096]
     torchrun --nproc-per-node N bench.py --gpus N ...       (one process per GPU, RCCL)
 
+`python bench.py --gpus N` (N > 1, no torchrun) launches the N rank processes itself
+(launch_ranks) and forwards rank 0's line.
+
 Workload (BASELINE.json configs[1]): MovieLens-1M-schema DSSM + Transformer sequence encoder,
 seq_len 50, d_model 64, per-GPU batch 4096, dropout as configured, temperature from the config,
 Adam + clip_grad_norm_(1.0). Synthetic MovieLens-shaped batches (synth.py), resident in HBM
@@ -63,7 +66,10 @@ WORKLOADS = {
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None,
+                    help='ranks (one process per GPU). Without torchrun\'s WORLD_SIZE, N > 1 makes this '
+                         'process a launcher of N rank processes (launch_ranks); under torchrun it must '
+                         'equal WORLD_SIZE')
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--config', default='c2')
@@ -229,7 +235,8 @@ def cpu_worker(spec_path, out_path):
     sent once every GPU workload has been timed, so the two legs never share the host cores.
     Writes {key: cpu_baseline} as each finishes."""
     spec = json.load(open(spec_path))
-    sys.stdin.readline()  # the parent's go (or EOF: the parent is gone, run anyway)
+    if not sys.stdin.readline():  # EOF: the parent is gone (or failed) before its go -- no orphan run
+        return
     res = {}
     for job in spec['jobs']:
         cfg = yaml.safe_load(open(os.path.join(ROOT, 'configs', f"{job['config']}.yaml")))
@@ -806,6 +813,11 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
                                   args=args, B=B, name=name, dtype=dtype, zipf=zipf, hard_negatives=hard_negatives)
     used_graph = graphs is not None
     _COPY_PLANS.clear()  # the plans hold this workload's batch tensors (and key on their ids)
+    if graphs is not None:  # the graphs (and the RCCL kernels they hold at N > 1) go first
+        torch.cuda.synchronize()
+        for g in graphs[:2]:
+            if g is not None:
+                g.reset()
     del model, opt, batches, batch, graphs, catalog
     torch.cuda.empty_cache()
     cpu = None
@@ -934,12 +946,74 @@ def compact_line(out):
     return line
 
 
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, argv, cmd=None, poll_s=0.5):
+    """`bench.py --gpus N` without torchrun: this process starts N rank processes of itself (one
+    per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set as torchrun sets them)
+    and never touches the GPU itself -- it imports torch (no HIP call) and makes no torch.cuda
+    call, so no rank is a fork or exec of a process that initialised HIP. Rank 0's stdout (the
+    JSON line) is this process's stdout; the other ranks' stdout and every rank's stderr go to
+    stderr. If a rank fails, the others are stopped (their process groups) and the exit code is
+    the first failure's. `cmd`: the rank command (default: this script with `argv`)."""
+    import signal
+    import subprocess
+    cmd = cmd or [sys.executable, '-u', os.path.abspath(__file__)] + list(argv)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=None if r == 0 else sys.stderr,
+                                      start_new_session=True))
+    rc = 0
+    failed = None
+    while True:
+        alive = 0
+        for r, p in enumerate(procs):
+            code = p.poll()
+            if code is None:
+                alive += 1
+            elif code != 0 and failed is None:
+                failed, rc = r, code
+        if failed is not None or alive == 0:
+            break
+        time.sleep(poll_s)
+    if failed is not None:
+        print(f'[bench] rank {failed} exited with {rc}; stopping the other ranks', file=sys.stderr, flush=True)
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except OSError:
+                    pass
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+        rc = rc if rc > 0 else 1  # a signal death (negative) still fails the launcher
+    return rc
+
+
 def main():
     faulthandler.enable()  # a crash prints the Python stack of every thread
     args = parse()
     if args.cpu_worker:
         cpu_worker(*args.cpu_worker)
         return
+    if (args.gpus or 1) > 1 and 'WORLD_SIZE' not in os.environ:
+        # the driver's `python bench.py --gpus N`: be the launcher of N ranks (before any HIP call)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    env_world = int(os.environ.get('WORLD_SIZE', '1'))
+    if args.gpus is not None and args.gpus != env_world:  # before the CPU worker or any HIP call
+        raise SystemExit(f'bench.py: --gpus {args.gpus} but the process group has {env_world} ranks')
     cpu_s = 0.0 if args.no_cpu_baseline else args.cpu_baseline_seconds
     worker = None
     if int(os.environ.get('WORLD_SIZE', '1')) == 1 and cpu_s > 0 and not args.pmc_bracket:
@@ -948,6 +1022,7 @@ def main():
     rdist.init_from_env()
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
+    assert args.gpus is None or args.gpus == world
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if os.environ.get('RSYS_DIST_BACKEND') == 'gloo':  # rehearsal: ranks share the box's GPUs
         local %= max(torch.cuda.device_count(), 1)
@@ -959,8 +1034,7 @@ def main():
     out = run_workload(args, args.config, args.dtype, args.zipf, args.hard_negatives, rank, world, dev,
                        cpu_s, peaks)
     if args.pmc_bracket:
-        if dist.is_initialized():
-            dist.destroy_process_group()
+        _teardown()
         return
     extras = {}
     order = [args.config]
@@ -1040,7 +1114,22 @@ def main():
         # stdout carries ONE compact line the driver parses (round 4's 23 KB line was not parsed)
         print(json.dumps({'bench_detail': out}), file=sys.stderr, flush=True)
         print(json.dumps(compact_line(out)), flush=True)
+    _teardown()
+
+
+def _teardown():
+    """Every captured graph (they hold RCCL kernels of the communicator at N > 1) is released and
+    the device drained before the process group goes: ncclCommDestroy waits for the graphs that
+    still use the communicator (round 5, gpurun_out/r5_b_rccl.log: a hang at exit otherwise)."""
+    import gc
+    gc.collect()
+    if torch.cuda.is_initialized():
+        torch.cuda.synchronize()
     if dist.is_initialized():
+        if dist.get_world_size() > 1:
+            dist.barrier()
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
         dist.destroy_process_group()
 
 

@@ -416,9 +416,10 @@ extern "C" int rs_gemm_add_layernorm(int M, int N, int K, const float* A, int ld
   hipStream_t st = as_stream(stream);
   // bf16 mode, B-row calls (the pruned last encoder layer, M = 4,096): the fused bf16 kernel takes
   // them too (round 5: one launch instead of the small-M fp32 GEMM + rs_add_layernorm_fwd)
-  const bool small_bf16 = (flags & RS_GEMM_BF16) && M >= 16 && M % 16 == 0 && N == 64 && K % 64 == 0 &&
-                          lda % 4 == 0 && ldw % 4 == 0 && aligned16(A) && aligned16(W) &&
-                          !getenv_flag("RSYS_SMALL_LN_UNFUSED");
+  // K in {64, 256}: the bf16 instances' kc = K / 64 in {1, 4} (other FFN widths take the GEMM +
+  // rs_add_layernorm_fwd below)
+  const bool small_bf16 = (flags & RS_GEMM_BF16) && M >= 16 && M % 16 == 0 && N == 64 &&
+                          (K == 64 || K == 256) && lda % 4 == 0 && ldw % 4 == 0 && aligned16(A) && aligned16(W);
   if ((rowgemm_ln_supported(M, N, K, A, lda) || small_bf16) && !getenv_flag("RSYS_UNFUSED_LN")) {
     StreamArgs sa{};
     sa.M = M; sa.N = N; sa.K = K; sa.alpha = 1.f; sa.beta = 0.f; sa.A = A; sa.lda = lda;

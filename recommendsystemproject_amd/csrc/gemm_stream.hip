@@ -1125,6 +1125,8 @@ int rowgemm_ln_launch(const StreamArgs& s, hipStream_t st) {
     RS_LNB(1, 0) RS_LNB(1, 1) RS_LNB(1, 16) RS_LNB(1, 17) RS_LNB(4, 0) RS_LNB(4, 1) RS_LNB(4, 16) RS_LNB(4, 17)
 #undef RS_LNB
   }
+  // no instance: an error, never a silent return with h / y unwritten (round-6 advisor finding)
+  RS_CHECK_ARG(kt == 4 || kt == 16, "rowgemm_ln: no instance for N=%d K=%d (K/16 must be 4 or 16)", s.N, s.K);
   if (s.M % 16 != 0 || s.K != kt * 16) {  // guarded generic instances
     if (kt == 4) rowgemm_kernel<4, 4, true><<<bx, 512, lds, st>>>(s);
     else rowgemm_kernel<4, 16, true><<<bx, 512, lds, st>>>(s);
@@ -1133,6 +1135,7 @@ int rowgemm_ln_launch(const StreamArgs& s, hipStream_t st) {
   if (kt == KTV && ekey == EV) rowgemm_kernel<4, KTV, true, 1, EV><<<bx, 512, lds, st>>>(s);
     RS_LN(4, 0) else RS_LN(4, 1) else RS_LN(4, 16) else RS_LN(4, 17)
     else RS_LN(16, 0) else RS_LN(16, 1) else RS_LN(16, 16) else RS_LN(16, 17)
+    else { set_error("rowgemm_ln: no instance for K=%d epilogue %d", s.K, ekey); return -1; }
 #undef RS_LN
   }
   RS_CHECK_LAUNCH("rowgemm_ln");

@@ -231,8 +231,11 @@ __global__ __launch_bounds__(1024) void reduce_jobs_kernel(RedJobs js) {
   }
 }
 
-bool g_defer = false;
-std::vector<RedJob> g_jobs;
+// Per host thread: a deferred_reduce scope (ops.py) is opened and flushed on the thread that runs
+// the encoder's backward (an autograd device thread), and only that thread's reductions queue
+// into it; a call from any other thread (another device's autograd worker) launches as usual.
+thread_local bool g_defer = false;
+thread_local std::vector<RedJob> g_jobs;
 
 int launch_jobs(const RedJob* jobs, int n, hipStream_t st) {
   for (int a = 0; a < n; a += kMaxJobs) {

@@ -26,7 +26,7 @@ from torch.autograd.function import once_differentiable
 
 from . import _hip, ops, precision, streams
 from . import dist as _dp
-from .flat import SEG_MEAN, SEG_ONE, SEG_SUM, flat_of, grad_of, lookup_table
+from .flat import SEG_MEAN, SEG_ONE, SEG_SUM, _dp_active, flat_of, grad_of, lookup_table
 
 
 def _seg(**kw):
@@ -130,8 +130,10 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
                          agreed=getattr(s, 'agreed', None))
         if c is not None:
             calls[i] = c
-            if pool and mode is not None and args is None:
-                # the gather stages this call's hot rows (runs of equal sorted keys) into LDS
+            if pool and mode is not None and args is None and getattr(c, 'a2a', None) is None and not _dp_active():
+                # the gather stages this call's hot rows (runs of equal sorted keys) into LDS; only
+                # for a single-process call, whose sorted keys are the table's global row ids (a
+                # data-parallel exchange's keys can be slot indices)
                 s.hot_keys, s.hot_n = c.keys.data_ptr(), c.n
         if args is not None and flat_of(t) is lt.flat:
             if lazy is not None and lazy != args:
@@ -405,16 +407,9 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key, params=()):
         if p > 0:
             ops.dropout_bwd(dx, p, key, 0)
     lin = proc.feature_projection[0]
-    # dx is final here (the dropout backward above ran in place before this point). Under the
-    # encoder's deferred reductions the projection's weight gradient and the flush of every
-    # reduction queued so far run on a side stream beside dcat and the tables' gradients below
-    # (ops.deferred_side; joined at the end of the encoder backward)
-    with ops.deferred_side(dx, cat) as forked:
-        if forked:
-            ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
-    if not forked:
-        with _WgradBranch(dx, cat):
-            ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
+    # dx is final here (the dropout backward above ran in place before this point)
+    with _WgradBranch(dx, cat):
+        ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
     dcat = ops.linear_bwd_input(dx, lin.weight)
     for s, t in zip(segs, tables):
         s.grad = grad_of(t).data_ptr()

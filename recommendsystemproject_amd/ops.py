@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import threading
 
 import numpy as np
 import torch
@@ -25,16 +26,23 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-_DEFER_KEEP = []  # deferred_reduce: the workspaces of this scope, alive until its flush is queued
-_DEFER_SIDE = []  # deferred_reduce: the side streams of this scope's early flushes (deferred_side)
-_SIDE_STREAMS = {}
+class _DeferState(threading.local):
+    """deferred_reduce's scope state, per host thread like the library's queue (csrc/reduce.hip
+    g_defer / g_jobs are thread_local): a scope opened on one thread (the autograd device thread
+    running the encoder backward) neither sees nor keeps another thread's workspaces."""
+
+    def __init__(self):
+        self.keep = []  # the workspaces of each open scope, alive until its flush is queued
+
+
+_DEFER = _DeferState()
 
 
 def ws(nbytes: int, device) -> torch.Tensor:
     """Workspace from the caching allocator (capture-safe)."""
     t = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
-    if _DEFER_KEEP:
-        _DEFER_KEEP[-1].append(t)  # a queued reduction reads it at the flush
+    if _DEFER.keep:
+        _DEFER.keep[-1].append(t)  # a queued reduction reads it at the flush
     return t
 
 
@@ -42,12 +50,13 @@ def ws(nbytes: int, device) -> torch.Tensor:
 def deferred_reduce(on=True):
     """The parameter-gradient reductions queued inside run as ONE launch at the end of the scope
     (rs_reduce_defer / rs_reduce_flush, round 5): nothing inside may read those gradients. Off
-    (plain pass-through) when `on` is false, in a nested scope, or with RSYS_DEFER_REDUCE=0."""
-    if not on or _DEFER_KEEP or os.environ.get('RSYS_DEFER_REDUCE', '1') == '0':
+    (plain pass-through) when `on` is false, in a nested scope, or with RSYS_DEFER_REDUCE=0. The
+    scope belongs to the calling host thread (library-side queue and this side's workspaces are
+    thread-local): reductions issued by other threads meanwhile are not deferred."""
+    if not on or _DEFER.keep or os.environ.get('RSYS_DEFER_REDUCE', '1') == '0':
         yield
         return
-    _DEFER_KEEP.append([])
-    _DEFER_SIDE.append([])
+    _DEFER.keep.append([])
     call('rs_reduce_defer', 1)
     try:
         yield
@@ -56,41 +65,7 @@ def deferred_reduce(on=True):
         try:
             call('rs_reduce_flush', stream())
         finally:
-            # the early flushes' side streams joined before the workspaces they read are released
-            cur = torch.cuda.current_stream() if _DEFER_SIDE[-1] else None
-            for sd in _DEFER_SIDE.pop():
-                cur.wait_stream(sd)
-            _DEFER_KEEP.pop()
-
-
-@contextlib.contextmanager
-def deferred_side(*tensors):
-    """Inside a deferred_reduce scope: the body runs on a side stream forked from the current one,
-    and the reductions queued so far (plus the body's) are flushed there at its end -- beside the
-    rest of the scope, which must not read those gradients; the scope's end joins it back
-    (round 5: the encoder's flush and input-projection weight gradient beside the sequence tables'
-    gradients). `tensors`: made on the current stream and read by the body. Yields whether it
-    forked (plain pass-through outside a scope, from a side stream, with RSYS_TOWER_STREAMS=0, the
-    bench's serial instrumented pass, and unless RSYS_FLUSH_SIDE=1). Opt-in: measured at C2 (bf16,
-    replayed graph) 1.27 -> 1.356 ms per step -- the graph's extra branch took the hardware queue
-    the item tower's backward chain runs on, which then waited behind the sequence tables'
-    gradient kernels; C3 fp32 0.759 -> 0.755."""
-    from . import streams
-    if (not _DEFER_SIDE or os.environ.get('RSYS_FLUSH_SIDE', '0') != '1' or not torch.cuda.is_available()
-            or os.environ.get('RSYS_TOWER_STREAMS', '1') == '0' or not streams.can_fork()):
-        yield False
-        return
-    main = torch.cuda.current_stream()
-    side = _SIDE_STREAMS.get(main.device)
-    if side is None:
-        side = _SIDE_STREAMS[main.device] = streams.side_stream(main.device)
-    side.wait_stream(main)
-    for t in tensors:
-        t.record_stream(side)
-    _DEFER_SIDE[-1].append(side)
-    with torch.cuda.stream(side):
-        yield True
-        call('rs_reduce_flush', stream())
+            _DEFER.keep.pop()
 
 
 def gemm(A, B, C, M, N, K, *, transA, transB, lda, ldb, ldc, alpha=1.0, beta=0.0, epi=0,

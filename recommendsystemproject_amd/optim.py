@@ -100,11 +100,15 @@ class _DeviceClip:
                       self.ticket.data_ptr(), float(max_norm), self.norm.data_ptr(), self.coef.data_ptr(),
                       counter.data_ptr() if counter is not None else None, ops.stream())
             return
-        if not batches or os.environ.get('RSYS_OPT_FUSE', '1') == '0':
+        # the dense partials ride in the first sorted launch only when there is a dense region:
+        # that launch adds its dense workgroups for n > 0 only, and rs_grad_sqnorm writes the
+        # n = 0 partial (0) that rs_clip_coef* then sums
+        fuse_dense = n > 0 and os.environ.get('RSYS_OPT_FUSE', '1') != '0'
+        if not batches or not fuse_dense:
             _hip.call('rs_grad_sqnorm', g.data_ptr(), n, float(scale), ws.data_ptr(), ops.stream())
         for j, batch in enumerate(batches):
             arr = (_hip.SortedCall * len(batch))(*[sc for sc, _ in batch])
-            if j == 0 and os.environ.get('RSYS_OPT_FUSE', '1') != '0':
+            if j == 0 and fuse_dense:
                 _hip.call('rs_sorted_sqnorm_batch_dense', C.addressof(arr), len(batch), float(scale),
                           ws.data_ptr() + 8 * (nd + batch[0][1] * ns), g.data_ptr(), n, ws.data_ptr(), ops.stream())
             else:

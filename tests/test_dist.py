@@ -742,18 +742,27 @@ def test_dp_overlap_buckets_gloo_cpu():
 
 
 @pytest.mark.gpu
-def test_bench_two_ranks_gloo_one_gpu(tmp_path):
+@pytest.mark.parametrize('launcher', ['self', 'torchrun'])
+def test_bench_two_ranks_gloo_one_gpu(tmp_path, launcher):
     """bench.py's N > 1 path (one JSON line from rank 0, bucketed all-reduce started in the
     backward, max-over-ranks timing), two gloo ranks sharing the GPU: eager steps (host-staged
-    gloo collectives cannot be captured; RCCL runs capture them)."""
+    gloo collectives cannot be captured; RCCL runs capture them). 'self': the driver's plain
+    `python bench.py --gpus 2` (bench.launch_ranks starts the ranks); 'torchrun': under
+    torch.distributed.run."""
     import json
     import subprocess
     import sys
     port = _free_port()
     env = dict(os.environ, RSYS_DIST_BACKEND='gloo', MASTER_ADDR='127.0.0.1')
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'bench.py'),
-           '--gpus', '2', '--steps', '3', '--warmup', '2', '--config', 'c2', '--no-cpu-baseline', '--extra=']
+    for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_PORT'):
+        env.pop(k, None)
+    args = [os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--steps', '3', '--warmup', '2', '--config', 'c2',
+            '--no-cpu-baseline', '--extra=']
+    if launcher == 'torchrun':
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+               '--master-addr', '127.0.0.1', '--master-port', str(port)] + args
+    else:
+        cmd = [sys.executable] + args
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]

@@ -474,3 +474,42 @@ def test_c5_capped_matches_oracle():
     for k in ('user_tower.seq_encoder.feature_embedder.embeddings.hist_item_ids.weight',
               'item_tower.embeddings.item_id_enc.weight', 'item_tower.mlp.mlp.0.weight'):
         _assert_adam_close(k, sd[k].cpu() - ref.S[k].detach(), lr=1e-3, steps=2)
+
+
+@pytest.mark.timeout(600)
+def test_c5_configured_batch_matches_oracle():
+    """C5 at its configured batch in the parity precision: B = 4096, L = 200, N = 10 hard
+    negatives from a device catalog, fp32, the tables capped to 10M rows (the bench's CPU leg runs
+    the oracle at exactly this size; 100M rows with the oracle's dense Adam state exceed the box's
+    host memory). One step: the loss within 1e-4 of the oracle's and three updated weight tensors
+    (the history table, the item-id table, the item tower's first Linear)."""
+    cfg = cap_vocab(cfg_of('c5'), 10_000_000)
+    B, N = 4096, 10
+    shapes = {k: s for k, s, _ in model_state_shapes(cfg)}
+    state = synth.make_state(shapes, seed=55)
+    model, maps = build(cfg, state)
+    assert len(ensure_flat(model).lazy) == 2
+    lr = float(cfg['train']['learning_rate'])
+    opt = Adam(model.parameters(), lr=lr)
+    catalog, V = _catalog(cfg)
+    g = torch.Generator().manual_seed(5)
+    b = synth.make_batch(cfg, B, seed=56, edge_cases=True)
+    assert b['user_tower']['sequence']['hist_item_ids'].shape[1] == 200
+    neg = torch.randint(1, V, (B, N), generator=g)
+    got = _c5_step(model, opt, cfg, b, catalog, neg.to(DEV))
+    torch.cuda.synchronize()
+    cat_sparse = catalog.sparse[neg.to(DEV).reshape(-1)].long().cpu().reshape(B, N, -1)
+    cat_seq = {k: v[neg.to(DEV).reshape(-1)].long().cpu().reshape(B, N, -1) for k, v in catalog.sequence.items()}
+    sd = {k: v.cpu() for k, v in model.state_dict().items()
+          if k in ('user_tower.seq_encoder.feature_embedder.embeddings.hist_item_ids.weight',
+                   'item_tower.embeddings.item_id_enc.weight', 'item_tower.mlp.mlp.0.weight')}
+    del model, opt, catalog
+    ref = OracleTrainer(cfg, state, lr=lr)
+    del state
+    rb = synth.batch_to_torch(b)
+    rb['hard_negatives'] = [{'sparse': cat_sparse[:, n], 'sequence': {k: v[:, n] for k, v in cat_seq.items()}}
+                            for n in range(N)]
+    want = float(ref.step(rb, maps, temperature=float(cfg['train']['temperature'])))
+    assert abs(got - want) < 1e-4, (got, want)
+    for k, w in sd.items():
+        _assert_adam_close(k, w - ref.S[k].detach(), lr=lr, steps=1)
