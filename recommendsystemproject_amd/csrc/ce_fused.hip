@@ -71,7 +71,6 @@ struct CeArgs {
   int ldS;
   const __bf16* strb;   // bf16 backward: the streamed rows pre-rounded to bf16 (the same bits the
                         // staging rounds to), half the bytes per tile: twice the tiles per batch
-  int* cnt;             // fwd: the finish kernel's ticket, zeroed here by workgroup (0, 0) (nullable)
 };
 
 __device__ __forceinline__ bf16x8 cvt8(const floatx4& a, const floatx4& b) {
@@ -482,7 +481,6 @@ __device__ __forceinline__ void ce_tile_body(const CeArgs& a, const int split, C
 template <int D, int MODE, bool F32>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(2))) void ce_tile_kernel(CeArgs a) {
   __shared__ __attribute__((aligned(16))) CeLds<D, F32> lds;
-  if (MODE == 0 && a.cnt && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.cnt = 0;
   ce_tile_body<D, MODE, F32>(a, blockIdx.y, lds);
 }
 
@@ -514,7 +512,7 @@ __device__ __forceinline__ void ce_finish_row(const float* __restrict__ part_m, 
                                               const float* __restrict__ diag, int NS, const float* __restrict__ U,
                                               const float* __restrict__ Hn, int64_t hs_row, int64_t hs_slot, int B,
                                               int N, int D, float invT, float* __restrict__ lse,
-                                              float* __restrict__ row_loss, int i, int lane, bool sc1);
+                                              float* __restrict__ row_loss, int i, int lane);
 
 __global__ __launch_bounds__(256) void ce_finish_fwd_kernel(const float* __restrict__ part_m,
                                                             const float* __restrict__ part_s,
@@ -525,13 +523,12 @@ __global__ __launch_bounds__(256) void ce_finish_fwd_kernel(const float* __restr
                                                             int N, int D, float invT,
                                                             float* __restrict__ lse,
                                                             float* __restrict__ row_loss,
-                                                            int* __restrict__ cnt, float* __restrict__ loss,
-                                                            float loss_scale, const float* __restrict__ I,
+                                                            const float* __restrict__ I,
                                                             __bf16* __restrict__ outb) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + wave;
   if (i < B) ce_finish_row(part_m, part_s, diag, NS, U, Hn, hs_row, hs_slot, B, N, D, invT, lse, row_loss, i,
-                           lane, cnt != nullptr);
+                           lane);
   // rows i of U and I rounded to bf16 for the backward's streamed operands (outb: [2][B][D]; D even) -- the
   // backward's rounding launch folded into this short one
   if (outb && i < B)
@@ -542,36 +539,13 @@ __global__ __launch_bounds__(256) void ce_finish_fwd_kernel(const float* __restr
       *reinterpret_cast<bf16x2*>(outb + (int64_t)i * D + c) = bf16x2{(__bf16)u.x, (__bf16)u.y};
       *reinterpret_cast<bf16x2*>(outb + ((int64_t)B + i) * D + c) = bf16x2{(__bf16)v.x, (__bf16)v.y};
     }
-  if (!cnt) return;
-  // the mean over the rows by the last workgroup to finish (fused rs_sum, round 5): every wave's
-  // row_loss store is agent-scope and drained before the workgroup's one ticket (the fence-free
-  // hand-off of MI355X_MICROARCH.md); the last adder reads them with agent-scope loads and sums
-  // in a fixed order (deterministic), then re-arms the ticket
-  __shared__ int s_last;
-  __shared__ double red[4];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  double acc = 0.0;
-  for (int r = threadIdx.x; r < B; r += 256)
-    acc += (double)__hip_atomic_load(row_loss + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  acc = wave_sum(acc);
-  if (lane == 0) red[wave] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    *loss = (float)((red[0] + red[1] + red[2] + red[3]) * (double)loss_scale);
-    *cnt = 0;
-  }
 }
 
 __device__ __forceinline__ void ce_finish_row(const float* __restrict__ part_m, const float* __restrict__ part_s,
                                               const float* __restrict__ diag, int NS, const float* __restrict__ U,
                                               const float* __restrict__ Hn, int64_t hs_row, int64_t hs_slot, int B,
                                               int N, int D, float invT, float* __restrict__ lse,
-                                              float* __restrict__ row_loss, int i, int lane, bool sc1) {
+                                              float* __restrict__ row_loss, int i, int lane) {
   float hl = -INFINITY;  // lane n < N: hard-negative logit n
   for (int n = 0; n < N; ++n) {
     const float* hp = Hn + (int64_t)i * hs_row + (int64_t)n * hs_slot;
@@ -590,8 +564,7 @@ __device__ __forceinline__ void ce_finish_row(const float* __restrict__ part_m, 
   if (lane == 0) {
     const float l = m + logf(s);
     lse[i] = l;
-    if (sc1) __hip_atomic_store(row_loss + i, l - diag[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else row_loss[i] = l - diag[i];
+    row_loss[i] = l - diag[i];
   }
 }
 
@@ -705,22 +678,15 @@ int ce_fused_fwd(const float* U, const float* I, const float* Hn, int64_t h_row_
   a.S = S; a.ldS = (int)rs_inbatch_ce_s_ld(B);
   a.split_rows = cdiv(cdiv(B, NS), kTile) * kTile;
   a.part_m = ws; a.part_s = ws + (int64_t)NS * B; a.diag = ws + (int64_t)2 * NS * B;
-  // the finish kernel's ticket, after diag (rs_inbatch_ce_fused_ws_bytes: the backward's larger
-  // workspace leaves room); zeroed by the tile kernel's first workgroup, re-armed by the last adder
-  // RSYS_CE_SUM_FUSED=1: the mean by the finish kernel's last workgroup (round 5) -- measured
-  // slower: ce_finish_fwd 5 -> 19.5 us against rs_sum's 4.8 (1,024 workgroups' tickets on one
-  // counter), C3 fp32 0.816 vs 0.813, so the separate launch stays the default
-  const bool fused_sum = getenv_flag("RSYS_CE_SUM_FUSED");
-  a.cnt = fused_sum ? reinterpret_cast<int*>(ws + (int64_t)2 * NS * B + B) : nullptr;
+  // the mean over the rows: rs_sum's own launch (round 5 measured the finish kernel's last-arriver
+  // sum slower: 1,024 workgroups' tickets on one counter, 5 -> 19.5 us)
   const int NSr = cdiv(B, a.split_rows);
   launch_tiles<0, F32>(a, D, NSr, st);
   RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_fwd tiles" : "rs_inbatch_ce_fused_fwd tiles");
   const HStrideArgs hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
   ce_finish_fwd_kernel<<<cdiv(B, 4), 256, 0, st>>>(a.part_m, a.part_s, a.diag, NSr, U, Hn, hs.row, hs.slot, B,
-                                                   N, D, a.invT, lse, row_loss, a.cnt, loss, 1.f / (float)B,
-                                                   I, F32 ? nullptr : uib);
+                                                   N, D, a.invT, lse, row_loss, I, F32 ? nullptr : uib);
   RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_fwd finish" : "rs_inbatch_ce_fused_fwd finish");
-  if (fused_sum) return 0;
   return rs_sum(row_loss, B, 1.f / (float)B, loss, stream);
 }
 
@@ -752,9 +718,8 @@ int ce_fused_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_
   const dim3 grid(cdiv(B, kOwnW * kWaves), NSr, 2);
   if constexpr (!F32) {
     // bf16: U and I rounded once (one small launch), so every workgroup streams half the bytes
-    // and stages twice the tiles per batch with the same registers (RSYS_CE_STREAM_F32=1: the
-    // fp32 rows, rounded as staged)
-    if (!getenv_flag("RSYS_CE_STREAM_F32")) {
+    // and stages twice the tiles per batch with the same registers
+    {
       // the forward's copies when it wrote them (rs_inbatch_ce_fused_fwd_uib), else one launch here
       const __bf16* Ub = uib;
       if (!uib) {
@@ -778,18 +743,19 @@ int ce_fused_bwd(const float* U, const float* I, const float* Hn, int64_t h_row_
       }
       return 0;
     }
+  } else {  // fp32: the fp32 rows streamed as they are
+    if (D == 128) ce_bwd_pair_kernel<128, true><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
+    else ce_bwd_pair_kernel<64, true><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
+    RS_CHECK_LAUNCH("rs_inbatch_ce_fused_f32_bwd tiles");
+    ce_reduce_kernel<<<(int)cdiv(2 * n / 4, 256), 256, 0, st>>>(ws, NSr, n, dU, dI, I, U, grad_out, B, a.invT);
+    RS_CHECK_LAUNCH("rs_inbatch_ce_fused_f32_bwd reduce");
+    if (N) {
+      const HStrideArgs hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
+      ce_hard_bwd_kernel<<<cdiv(B, 4), 256, 0, st>>>(U, Hn, hs.row, hs.slot, B, N, D, a.invT, lse, grad_out, dhl);
+      RS_CHECK_LAUNCH("rs_inbatch_ce_fused_f32_bwd hard");
+    }
+    return 0;
   }
-  if (D == 128) ce_bwd_pair_kernel<128, F32><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
-  else ce_bwd_pair_kernel<64, F32><<<grid, 64 * kWaves, 0, st>>>(aU, aI);
-  RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_bwd tiles" : "rs_inbatch_ce_fused_bwd tiles");
-  ce_reduce_kernel<<<(int)cdiv(2 * n / 4, 256), 256, 0, st>>>(ws, NSr, n, dU, dI, I, U, grad_out, B, a.invT);
-  RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_bwd reduce" : "rs_inbatch_ce_fused_bwd reduce");
-  if (N) {
-    const HStrideArgs hs{h_row_stride > 0 ? h_row_stride : (int64_t)N * D, h_slot_stride > 0 ? h_slot_stride : D};
-    ce_hard_bwd_kernel<<<cdiv(B, 4), 256, 0, st>>>(U, Hn, hs.row, hs.slot, B, N, D, a.invT, lse, grad_out, dhl);
-    RS_CHECK_LAUNCH(F32 ? "rs_inbatch_ce_fused_f32_bwd hard" : "rs_inbatch_ce_fused_bwd hard");
-  }
-  return 0;
 }
 
 }  // namespace

@@ -281,17 +281,7 @@ extern "C" int rs_reduce_flush(void* stream) {
   if (jobs.empty()) return 0;
   // the long jobs' workgroups (most partials each) dispatched first, the short ones fill the tail
   // (each job's sums are independent of where it sits in the grid)
-  if (!rs::getenv_flag("RSYS_DEFER_FIFO"))
-    std::stable_sort(jobs.begin(), jobs.end(), [](const rs::RedJob& x, const rs::RedJob& y) { return x.P > y.P; });
-  static const bool dbg = rs::getenv_flag("RSYS_DEFER_DEBUG");
-  if (dbg) {
-    int64_t bytes = 0;
-    for (const auto& j : jobs) {
-      fprintf(stderr, "rs_reduce_flush job P=%d N=%d ranges=%d\n", j.P, j.N, j.nr);
-      bytes += (int64_t)(j.P + 1) * j.N * 4;
-    }
-    fprintf(stderr, "rs_reduce_flush %zu jobs, %.2f MB\n", jobs.size(), bytes / 1e6);
-  }
+  std::stable_sort(jobs.begin(), jobs.end(), [](const rs::RedJob& x, const rs::RedJob& y) { return x.P > y.P; });
   return rs::launch_jobs(jobs.data(), (int)jobs.size(), rs::as_stream(stream));
 }
 
