@@ -37,8 +37,6 @@ constexpr int64_t kSmallTableBytes = 48 * 1024;
 
 constexpr int kRowsPerLane = 4;            // forward sparse rows per lane on token-sized launches
 constexpr int kBagBatch = 16;              // bag ids (and rows) loaded per batch
-constexpr int kBagBatchNt = 4;             // the same for rows of large tables (non-temporal loads)
-constexpr int64_t kNtTableBytes = 64ll << 20;  // tables from this size: rows read once, nt loads
 constexpr int kLazyBagBatch = 8;           // the same with exp_avg / exp_avg_sq rows beside them
 // forward: a table of at most this size whose workgroup reads at least as many row bytes as the
 // table holds is staged whole into LDS first (every row of such a table is hot: the genre / age /
@@ -95,7 +93,6 @@ struct SegLaunch {
   int16_t slots[kMaxSeg];  // bwd: its row slots per workgroup (private [V][D] LDS images)
   int slot_lds;            // bwd: dynamic LDS bytes of the slot kernel
   uint8_t rpt[kMaxSeg];    // fwd sparse segments: rows per lane (kRowsPerLane on token-sized launches)
-  uint8_t nt[kMaxSeg];     // fwd: rows of a large table -- non-temporal loads, shorter bag batches
   uint8_t hot[kMaxSeg];    // fwd: pooled lookups with their hot rows staged in LDS (gather_pool_hot)
   int16_t tblocks[kMaxSeg];
   int tblock_start[kMaxSeg + 1];
@@ -129,14 +126,13 @@ __device__ __forceinline__ bool id_ok(int64_t id, int64_t vocab, int* err) {
   return true;
 }
 
-template <bool VEC, bool NT = false>
+template <bool VEC>
 __device__ __forceinline__ void load_row(const float* p, float* v) {
   if (VEC) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v t = NT ? __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p)) : *reinterpret_cast<const f4v*>(p);
-    v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
   } else {
-    v[0] = NT ? __builtin_nontemporal_load(p) : p[0];
+    v[0] = p[0];
   }
 }
 
@@ -173,14 +169,11 @@ __device__ __forceinline__ void lazy_replay(const LazyLaunch& z, int2 last, int 
 
 // Pooled bag: the (un-normalised) sum or max of positions [lbeg, lend) of row `row`'s bag.
 // LAZY: the rows read through the catch-up.
-// NT (rows of a large table, read once per step): non-temporal row loads and 4 rows in flight per
-// lane group instead of 16, bags not split (tools/gather_sweep.hip, C3's history shape from HBM,
-// 8 rotating id sets: 16 rows split 4 ways, default policy, 4.7 TB/s; 4 rows unsplit nt 5.5 TB/s)
-template <bool VEC, bool LAZY = false, bool NT = false>
+template <bool VEC, bool LAZY = false>
 __device__ __forceinline__ void pool_acc(const SegLaunch& a, const rs_feature_seg_t& sg, int row,
                                          int c, int lbeg, int lend, float* acc) {
   constexpr int W = VEC ? 4 : 1;
-  constexpr int NB = LAZY ? kLazyBagBatch : (NT ? kBagBatchNt : kBagBatch);
+  constexpr int NB = LAZY ? kLazyBagBatch : kBagBatch;
   const int64_t* ids = sg.idx + (int64_t)row * sg.idx_stride;
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = sg.pool_mode == RS_POOL_MAX ? -INFINITY : 0.f;
@@ -204,7 +197,7 @@ __device__ __forceinline__ void pool_acc(const SegLaunch& a, const rs_feature_se
       bad |= u < nb && !valid;
       ok[u] = u < nb && valid;
       const int64_t r = ok[u] ? raw[u] : 0;
-      load_row<VEC, NT && !LAZY>(sg.table + r * sg.dim + c, v[u]);
+      load_row<VEC>(sg.table + r * sg.dim + c, v[u]);
       if constexpr (LAZY) {
         lst[u] = reinterpret_cast<const int2*>(sg.lazy_last)[r];
         load_row<VEC>(sg.table + r * sg.dim + c + a.lz.moff, mv[u]);
@@ -232,7 +225,7 @@ __device__ __forceinline__ void pool_acc(const SegLaunch& a, const rs_feature_se
   if (bad && a.err) atomicOr(a.err, 1);
 }
 
-template <bool VEC, bool LAZY = false, bool NT = false>
+template <bool VEC, bool LAZY = false>
 __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int row, int chunk) {
   constexpr int W = VEC ? 4 : 1;
   const int c = chunk * W;
@@ -242,7 +235,7 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
     const int64_t id = sg.idx[(int64_t)row * sg.idx_stride];
     if (id_ok(id, sg.vocab, a.err)) {
       const float* pr = sg.table + id * sg.dim + c;
-      load_row<VEC, NT && !LAZY>(pr, acc);
+      load_row<VEC>(pr, acc);
       if constexpr (LAZY) {
         float mv[4], vv[4];
         const int2 l = reinterpret_cast<const int2*>(sg.lazy_last)[id];
@@ -252,7 +245,7 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
       }
     }
   } else if (sg.kind == RS_SEG_POOL) {
-    pool_acc<VEC, LAZY, NT>(a, sg, row, c, 0, sg.bag, acc);
+    pool_acc<VEC, LAZY>(a, sg, row, c, 0, sg.bag, acc);
     if (sg.pool_mode == RS_POOL_MEAN) {
       const float n = (float)sg.bag;
 #pragma unroll
@@ -279,7 +272,7 @@ __device__ void gather_seg(const SegLaunch& a, const rs_feature_seg_t& sg, int r
 // workgroups of one float4 per lane, each a serial id -> row -> store chain). The workgroup owns
 // rows [lb R rpb, (lb + 1) R rpb); all R ids are loaded, then all R rows, then the R stores, so a
 // lane has R independent chains in flight. Same values as gather_seg (bad ids: zeros + err flag).
-template <int R, bool LAZY = false, bool NT = false>
+template <int R, bool LAZY = false>
 __device__ void gather_sparse_rows(const SegLaunch& a, const rs_feature_seg_t& sg, int rpb, int lb,
                                    int r, int chunk) {
   const int c = chunk * 4;
@@ -301,7 +294,7 @@ __device__ void gather_sparse_rows(const SegLaunch& a, const rs_feature_seg_t& s
     okk[k] = ok;
     bad |= row < a.rows && !ok;
     const float* pr = sg.table + (ok ? id[k] : 0) * sg.dim + c;
-    load_row<true, NT && !LAZY>(pr, v[k]);
+    load_row<true>(pr, v[k]);
     if constexpr (LAZY) {
       lst[k] = reinterpret_cast<const int2*>(sg.lazy_last)[ok ? id[k] : 0];
       load_row<true>(pr + a.lz.moff, mv[k]);
@@ -330,7 +323,7 @@ __device__ void gather_sparse_rows(const SegLaunch& a, const rs_feature_seg_t& s
 // Pooled bag split over S row groups (small batches: more loads in flight per bag). Row group
 // g = r * S + p sums positions [p * per, (p + 1) * per) of bag r; the S partial sums are added
 // in p order through LDS by group p = 0.
-template <bool VEC, bool LAZY = false, bool NT = false>
+template <bool VEC, bool LAZY = false>
 __device__ void gather_pool_split(const SegLaunch& a, const rs_feature_seg_t& sg, int s, int lb) {
   constexpr int W = VEC ? 4 : 1;
   __shared__ float4 red[256];
@@ -343,7 +336,7 @@ __device__ void gather_pool_split(const SegLaunch& a, const rs_feature_seg_t& sg
   const int lbeg = p * per < sg.bag ? p * per : sg.bag;
   const int lend = lbeg + per < sg.bag ? lbeg + per : sg.bag;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if (active) pool_acc<VEC, LAZY, NT>(a, sg, row, chunk * W, lbeg, lend, acc);
+  if (active) pool_acc<VEC, LAZY>(a, sg, row, chunk * W, lbeg, lend, acc);
   red[threadIdx.x] = make_float4(acc[0], acc[1], acc[2], acc[3]);
   __syncthreads();
   if (!active || p != 0) return;
@@ -538,8 +531,7 @@ __global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
     sg.table = reinterpret_cast<const float*>(stage_lds);
   }
   if (a.split[s] > 1) {  // uniform per workgroup: the barrier inside is reached by every thread
-    if (a.vec[s] && a.nt[s]) gather_pool_split<true, false, true>(a, sg, s, lb);
-    else if (a.vec[s]) gather_pool_split<true>(a, sg, s, lb);
+    if (a.vec[s]) gather_pool_split<true>(a, sg, s, lb);
     else gather_pool_split<false>(a, sg, s, lb);
     return;
   }
@@ -547,14 +539,12 @@ __global__ __launch_bounds__(256) void gather_fwd_kernel(SegLaunch a) {
   const int r = threadIdx.x / C, chunk = threadIdx.x % C;
   if (r >= a.rpb[s]) return;
   if (a.rpt[s] == kRowsPerLane) {  // plan: sparse, vec only
-    if (a.nt[s]) gather_sparse_rows<kRowsPerLane, false, true>(a, sg, a.rpb[s], lb, r, chunk);
-    else gather_sparse_rows<kRowsPerLane>(a, sg, a.rpb[s], lb, r, chunk);
+    gather_sparse_rows<kRowsPerLane>(a, sg, a.rpb[s], lb, r, chunk);
     return;
   }
   const int row = lb * a.rpb[s] + r;
   if (row >= a.rows) return;
-  if (a.vec[s] && a.nt[s]) gather_seg<true, false, true>(a, sg, row, chunk);
-  else if (a.vec[s]) gather_seg<true>(a, sg, row, chunk);
+  if (a.vec[s]) gather_seg<true>(a, sg, row, chunk);
   else gather_seg<false>(a, sg, row, chunk);
 }
 
@@ -677,8 +667,6 @@ __device__ __forceinline__ void gather_bwd_body(const SegLaunch& a, int bid) {
   else scatter_seg<false>(a, sg, row, chunk, nullptr, lbeg, lend);
 }
 
-__global__ __launch_bounds__(256) void gather_bwd_kernel(SegLaunch a) { gather_bwd_body(a, blockIdx.x); }
-
 __device__ __forceinline__ void gather_bwd_small_body(const SegLaunch& a, int bid, float* lds) {
   int s = 0;
   while (s + 1 < a.nseg && bid >= a.sblock_start[s + 1]) ++s;
@@ -702,11 +690,6 @@ __device__ __forceinline__ void gather_bwd_small_body(const SegLaunch& a, int bi
     const float v = lds[e];
     if (v != 0.f) atomicAdd(sg.grad + e, v);
   }
-}
-
-__global__ __launch_bounds__(256) void gather_bwd_small_kernel(SegLaunch a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  gather_bwd_small_body(a, blockIdx.x, lds);
 }
 
 // dense segment s (Linear(1, D) of one input column) by one 256-thread workgroup: dW[c] +=
@@ -1169,71 +1152,6 @@ __global__ __launch_bounds__(kReduceWaves * 64) void reduce_partials_kernel(SegL
   }
 }
 
-// Linear(1, D) backward: dW[c] += sum_b dout[b,c]*x[b]; db[c] += sum_b dout[b,c].
-// One 1024-thread workgroup per dense segment: 1024/D row lanes, 8 rows in flight per lane,
-// then a fixed-order LDS reduction (deterministic).
-// One workgroup per dense segment (Linear(1, D) of one input column): dW[c] += sum_r dout[r][c] x[r],
-// db[c] += sum_r dout[r][c]. Row-lanes keep 16 rows' loads in flight; the row-lanes of a column
-// meet by wave shuffles, then across waves in a fixed LDS order (round 5: C2's D = 8 column was
-// 11.9 us -- four load round trips and a 128-long serial LDS sum per column)
-__global__ __launch_bounds__(1024) void dense_bwd_kernel(SegLaunch a) {
-  const int s = blockIdx.x;
-  const rs_feature_seg_t& sg = a.segs[s];
-  if (sg.kind != RS_SEG_DENSE) return;
-  __shared__ float red_w[1024], red_b[1024];
-  const int D = sg.dim;
-  const int lanes = 1024 / D;  // D <= 256
-  const int c = threadIdx.x % D, rl = threadIdx.x / D;
-  constexpr int U = 16;
-  float aw = 0.f, ab = 0.f;
-  if (rl < lanes) {
-    int row = rl;
-    for (; row + (U - 1) * lanes < a.rows; row += U * lanes) {
-      float gv[U], xv[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        gv[u] = a.dout[(int64_t)(row + u * lanes) * a.ldo + sg.out_col + c];
-        xv[u] = sg.x[(int64_t)(row + u * lanes) * sg.idx_stride];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        aw += gv[u] * xv[u];
-        ab += gv[u];
-      }
-    }
-    for (; row < a.rows; row += lanes) {
-      const float gv = a.dout[(int64_t)row * a.ldo + sg.out_col + c];
-      aw += gv * sg.x[(int64_t)row * sg.idx_stride];
-      ab += gv;
-    }
-  }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int np;  // partials per column in red_*[i * D + c]
-  if (D < 64 && 64 % D == 0) {
-    // the 64 / D row-lanes of a column inside one wave: butterfly (every lane ends with the sum)
-    for (int off = D; off < 64; off <<= 1) {
-      aw += __shfl_xor(aw, off, 64);
-      ab += __shfl_xor(ab, off, 64);
-    }
-    if (lane < D) {
-      red_w[w * D + c] = aw;
-      red_b[w * D + c] = ab;
-    }
-    np = 16;
-  } else {
-    red_w[threadIdx.x] = aw;
-    red_b[threadIdx.x] = ab;
-    np = lanes;
-  }
-  __syncthreads();
-  if (threadIdx.x < D) {
-    float sw = 0.f, sb = 0.f;
-    for (int i = 0; i < np; ++i) { sw += red_w[i * D + c]; sb += red_b[i * D + c]; }
-    sg.grad[c] += sw;
-    sg.grad_bias[c] += sb;
-  }
-}
-
 // Ranged table-gradient plan of one segment (0 ranges: the atomic scatter). Sparse ids and sum /
 // mean bags of a table of 48 KB - 4 MB (smaller ones: the slot kernel), D in {16, 32, 64, 128,
 // 256} (D/4 lanes per lookup divide a wave into <= 16 groups); ranges of 64 KB; chunks of >= 2 x
@@ -1309,11 +1227,9 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     // Split long sum/mean bags over S row groups while the launch is short of ~8 waves per SIMD
     // and every group keeps >= 8 positions (C3: B = 4096, L = 50, D = 128 -> S = 4).
     int S = 1;
-    // opt-in (RSYS_GATHER_NT=1): faster from HBM in isolation (tools/gather_sweep.hip), slower in
-    // the step (C3 fp32 0.037 -> 0.043 ms): there the catch-up has just brought the rows on chip,
-    // and rows not kept in the Infinity Cache cost the optimizer's later read of them
-    const bool nt = !bwd && vec && table_kind && g.vocab * g.dim * 4 >= kNtTableBytes && getenv_flag("RSYS_GATHER_NT");
-    if (g.kind == RS_SEG_POOL && g.pool_mode != RS_POOL_MAX && !a.small[s] && !nt) {
+    // (round 5 measured non-temporal row loads for large tables slower in the step, C3 fp32 0.037
+    // -> 0.043 ms: the catch-up has just brought the rows on chip)
+    if (g.kind == RS_SEG_POOL && g.pool_mode != RS_POOL_MAX && !a.small[s]) {
       while (2 * S * C <= 256 && (g.bag + 2 * S - 1) / (2 * S) >= 8 &&
              (int64_t)rows * C * S < 8192 * 64)
         S *= 2;
@@ -1323,9 +1239,8 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
     a.rpt[s] = (!bwd && vec && g.kind == RS_SEG_SPARSE && (int64_t)rows * C >= (int64_t)2048 * 256)
                    ? kRowsPerLane : 1;
     a.rpb[s] = 256 / (C * S);
-    a.nt[s] = nt;
     a.hot[s] = !bwd && vec && g.kind == RS_SEG_POOL && g.pool_mode != RS_POOL_MAX && g.hot_keys &&
-               g.hot_n >= 2 * kHotQ && !nt && !g.lazy_last && g.dim <= 256 && getenv_flag("RSYS_HOT_ROWS");
+               g.hot_n >= 2 * kHotQ && !g.lazy_last && g.dim <= 256 && getenv_flag("RSYS_HOT_ROWS");
     if (a.hot[s]) {
       const int hb = kHotMax * g.dim * 4;
       if (hb > a.stage_lds) a.stage_lds = hb;
@@ -1410,7 +1325,6 @@ int plan(SegLaunch& a, const rs_feature_seg_t* segs_host, int nseg, int rows, in
                                    std::min<int64_t>(1024, cdiv(rows, kOhWaves * 128)));
     nb = std::max<int64_t>(1, nb);
     int64_t rpw = cdiv(cdiv(rows, nb * kOhWaves), per_wave_min) * per_wave_min;
-    if (const char* e = getenv("RSYS_OH_RPW")) rpw = std::max<int64_t>(per_wave_min, atoi(e) / per_wave_min * per_wave_min);  // tuning only
     nb = std::max<int64_t>(1, cdiv(rows, rpw * kOhWaves));
     a.oh_rpw[s] = (int)rpw;
     a.tblocks[s] = (int16_t)nb;  // the partial count (pchunks)
@@ -1556,19 +1470,10 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
   hipStream_t st = as_stream(stream);
   int ndense = 0;
   for (int s = 0; s < nseg; ++s) ndense += segs_host[s].kind == RS_SEG_DENSE;
-  const bool split = getenv_flag("RSYS_GATHER_BWD_SPLIT");  // A/B: three launches
-  if (!split && a.block_start[nseg] + a.sblock_start[nseg] + ndense > 0) {
+  if (a.block_start[nseg] + a.sblock_start[nseg] + ndense > 0) {
     gather_bwd_fused_kernel<<<a.sblock_start[nseg] + ndense + a.block_start[nseg], 256,
                               std::max(a.small_lds, 512 * 4), st>>>(a, a.sblock_start[nseg], ndense);
     RS_CHECK_LAUNCH("rs_gather_bwd");
-  }
-  if (split && a.block_start[nseg] > 0) {
-    gather_bwd_kernel<<<a.block_start[nseg], 256, 0, st>>>(a);
-    RS_CHECK_LAUNCH("rs_gather_bwd");
-  }
-  if (split && a.sblock_start[nseg] > 0) {
-    gather_bwd_small_kernel<<<a.sblock_start[nseg], 256, a.small_lds, st>>>(a);
-    RS_CHECK_LAUNCH("rs_gather_bwd small");
   }
   if (a.rblock_start[nseg] > 0) {
     gather_bwd_range_kernel<<<a.rblock_start[nseg], kRangeThreads, a.range_lds, st>>>(a);
@@ -1607,10 +1512,6 @@ extern "C" int rs_gather_bwd(const rs_feature_seg_t* segs, int nseg, int rows, c
       if (a.pchunks[s]) nel = std::max<int64_t>(nel, segs_host[s].vocab * segs_host[s].dim / 4 + 1);
     reduce_partials_kernel<<<(int)std::min<int64_t>(cdiv(nel, 64), 1024), kReduceWaves * 64, 0, st>>>(a);
     RS_CHECK_LAUNCH("rs_gather_bwd partials");
-  }
-  if (split && ndense) {
-    dense_bwd_kernel<<<nseg, 1024, 0, st>>>(a);
-    RS_CHECK_LAUNCH("rs_gather_bwd dense");
   }
   return 0;
 }

@@ -778,11 +778,7 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(StreamArgs a, int rows_
 int wgrad_blocks(int Kr) {
   // row splits: 512 measured best at C2 (256 -> 0.101, 384 -> 0.091, 512 -> 0.083, 768 -> 0.082,
   // 1024 -> 0.099 ms per step of rs_wgrad_bf16)
-  static const int cap = [] {
-    const char* e = getenv("RSYS_WGRAD_CAP");  // A/B knob: the row-split cap
-    const int v = e ? atoi(e) : 0;
-    return v >= 16 && v <= 2048 ? v : 512;
-  }();
+  constexpr int cap = 512;
   int nb = Kr / 64;  // >= 64 rows per workgroup; short K (the MLP's B = 4096) still fills 64 CUs
   if (nb > cap) nb = cap;
   if (nb < 1) nb = 1;

@@ -229,118 +229,6 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter_kernel(
   }
 }
 
-// ---------------------------------------------------------------- single-launch passes (round 4)
-// Every pass's global digit totals come from one histogram launch over the pass-0 keys (a digit's
-// total does not depend on the order), and each pass is then ONE launch: a tile takes the next
-// tile index from a counter (so every lower tile is already running), ranks its keys in the tile
-// (rank_round, as above), publishes its per-digit counts, and finds the count of each digit in
-// all lower tiles by decoupled look-back (status word per (tile, digit): FLAG_AGG + the tile's own
-// count as soon as it is known, FLAG_PRE + the inclusive prefix once the look-back is done).
-// 1 + passes launches (+ one memset) instead of 3 x passes: C3's 204,800-lookup history call went
-// through 9 dependent launches. Same stable order, same bits.
-constexpr uint64_t kFlagAgg = 1ull << 62, kFlagPre = 2ull << 62, kFlagMask = 3ull << 62;
-
-__global__ __launch_bounds__(kSortThreads) void sort_hist_all_kernel(
-    const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab, int64_t n,
-    SortPlan plan, int* __restrict__ tot) {
-  __shared__ int h[4][kMaxRadix];
-  for (int t = threadIdx.x; t < 4 * kMaxRadix; t += kSortThreads) (&h[0][0])[t] = 0;
-  __syncthreads();
-  for (int64_t e = (int64_t)blockIdx.x * kSortThreads + threadIdx.x; e < n; e += (int64_t)gridDim.x * kSortThreads) {
-    const uint32_t k = raw_key(ids, id_bytes, bag, stride, vocab, e);
-    for (int q = 0; q < plan.passes; ++q) atomicAdd(&h[q][(k >> plan.shift[q]) & ((1 << plan.dbits[q]) - 1)], 1);
-  }
-  __syncthreads();
-  for (int q = 0; q < plan.passes; ++q) {
-    const int radix = 1 << plan.dbits[q];
-    for (int t = threadIdx.x; t < radix; t += kSortThreads)
-      if (h[q][t]) atomicAdd(&tot[q * kMaxRadix + t], h[q][t]);
-  }
-}
-
-__global__ __launch_bounds__(kSortThreads) void sort_onesweep_kernel(
-    const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab,
-    const uint32_t* __restrict__ ksrc, const uint32_t* __restrict__ vsrc, int64_t n, int shift,
-    int dbits, const int* __restrict__ tot, unsigned long long* __restrict__ status, int* __restrict__ counter,
-    uint32_t* __restrict__ kdst, uint32_t* __restrict__ vdst) {
-  __shared__ RankLds<kSortThreads> lds;
-  __shared__ int gbase[kMaxRadix];
-  __shared__ int s_tile;
-  const int radix = 1 << dbits;
-  rank_reset(lds, radix);
-  if (threadIdx.x == 0) s_tile = atomicAdd(counter, 1);
-  // global base of each digit: keys of smaller digits
-  if (threadIdx.x < 64) {
-    int carry = 0;
-    const int lane = threadIdx.x;
-    for (int d0 = 0; d0 < radix; d0 += 64) {
-      const int x = d0 + lane < radix ? tot[d0 + lane] : 0;
-      int y = x;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(y, o, 64);
-        if (lane >= o) y += t;
-      }
-      if (d0 + lane < radix) gbase[d0 + lane] = carry + y - x;
-      carry += __shfl(y, 63, 64);
-    }
-  }
-  __syncthreads();
-  const int tile = s_tile;
-  const int64_t base = (int64_t)tile * kSortTile;
-  uint32_t key[kSortRounds], val[kSortRounds];
-  int lp[kSortRounds];
-#pragma unroll
-  for (int r = 0; r < kSortRounds; ++r) {
-    const int64_t e = base + r * kSortThreads + threadIdx.x;
-    key[r] = kSentinel;
-    val[r] = 0;
-    if (e < n) {
-      key[r] = ksrc ? ksrc[e] : raw_key(ids, id_bytes, bag, stride, vocab, e);
-      val[r] = vsrc ? vsrc[e] : (uint32_t)e;
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < kSortRounds; ++r) {
-    const int64_t e = base + r * kSortThreads + threadIdx.x;
-    const uint32_t d = (key[r] >> shift) & (radix - 1);
-    lp[r] = rank_round(lds, d, e < n, dbits, radix);
-  }
-  // lds.run[d] = this tile's count of digit d: publish it, then look back over the lower tiles
-  unsigned long long* my = status + (int64_t)tile * kMaxRadix;
-  for (int d = threadIdx.x; d < radix; d += kSortThreads)
-    __hip_atomic_store(my + d, kFlagAgg | (unsigned long long)lds.run[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int d = threadIdx.x; d < radix; d += kSortThreads) {
-    unsigned long long excl = 0;
-    for (int j = tile - 1; j >= 0;) {
-      const unsigned long long w =
-          __hip_atomic_load(status + (int64_t)j * kMaxRadix + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long f = w & kFlagMask;
-      if (f == 0) {  // tile j has not published yet (it is running: it took its index earlier)
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      excl += w & ~kFlagMask;
-      if (f == kFlagPre) break;
-      --j;
-    }
-    __hip_atomic_store(my + d, kFlagPre | (excl + (unsigned long long)lds.run[d]), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    gbase[d] += (int)excl;
-  }
-  __syncthreads();
-  // rank_round's positions count from the tile's start of each digit (lds.pre per round)
-#pragma unroll
-  for (int r = 0; r < kSortRounds; ++r) {
-    const int64_t e = base + r * kSortThreads + threadIdx.x;
-    if (e < n) {
-      const uint32_t d = (key[r] >> shift) & (radix - 1);
-      const int64_t pos = (int64_t)gbase[d] + lp[r];
-      kdst[pos] = key[r];
-      vdst[pos] = val[r];
-    }
-  }
-}
-
 // ---------------------------------------------------------------- one-tile sort (n <= 4096)
 // One workgroup, the keys in registers (4 per thread) and exchanged through LDS between the
 // radix passes. (Measured and rejected: a bitonic sort of key/index pairs -- 39 us with an LDS
@@ -454,148 +342,6 @@ __global__ __launch_bounds__(kTileThreads) void sort_tile_kernel(
     if (e < n) {
       kout[e] = key[r];
       vout[e] = val[r];
-    }
-  }
-}
-
-// ---------------------------------------------------------------- big-tile passes (round 5)
-// Calls above kRankMax lookups (C3's 204,800-id history call): tiles of 4,096 keys, one 1,024-thread
-// workgroup each, TWO launches per pass instead of three:
-//   sort_bhist_kernel    per-tile digit counts -> hist[digit][tile];
-//   sort_bscatter_kernel every tile computes its digits' global bases itself from hist (the keys of
-//                        smaller digits, plus this digit's keys in earlier tiles: ntiles loads per
-//                        digit, 50 at C3), ranks its keys wave-major as sort_tile_kernel does, puts
-//                        them into tile order (by digit) through LDS and stores them from there, so
-//                        a digit's keys leave the tile as one contiguous run (coalesced stores).
-// Stable (tile order, then wave-major key order within a tile): the same keys and values as the
-// 1,024-key tiles. Opt-in (RSYS_SORT_BIG_TILES=1): measured slower in the C3 step (history call
-// 3 x (6.5 + 14.4) us against 3 x (hist + scan + scatter) ~ 55 us: the wave-major ranking of 4,096
-// keys on one workgroup costs more than the launch it saves).
-__global__ __launch_bounds__(kTileThreads) void sort_bhist_kernel(
-    const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab,
-    const uint32_t* __restrict__ src, int64_t n, int shift, int dbits, int* __restrict__ hist) {
-  __shared__ int h[kMaxRadix];
-  const int radix = 1 << dbits;
-  for (int t = threadIdx.x; t < radix; t += kTileThreads) h[t] = 0;
-  __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kTileMax;
-#pragma unroll
-  for (int r = 0; r < kTileMax / kTileThreads; ++r) {
-    const int64_t e = base + r * kTileThreads + threadIdx.x;
-    if (e < n) {
-      const uint32_t k = src ? src[e] : raw_key(ids, id_bytes, bag, stride, vocab, e);
-      atomicAdd(&h[(k >> shift) & (radix - 1)], 1);
-    }
-  }
-  __syncthreads();
-  for (int t = threadIdx.x; t < radix; t += kTileThreads) hist[(int64_t)t * gridDim.x + blockIdx.x] = h[t];
-}
-
-__global__ __launch_bounds__(kTileThreads) void sort_bscatter_kernel(
-    const void* __restrict__ ids, int id_bytes, int bag, int64_t stride, int64_t vocab,
-    const uint32_t* __restrict__ ksrc, const uint32_t* __restrict__ vsrc, int64_t n, int shift, int dbits,
-    const int* __restrict__ hist, uint32_t* __restrict__ kdst, uint32_t* __restrict__ vdst) {
-  __shared__ uint16_t cnt[kTileWaves][kMaxRadix];  // per wave: running, then exclusive, digit counts
-  __shared__ int tbase[kMaxRadix];                  // the tile's exclusive digit scan
-  __shared__ int gbase[kMaxRadix];                  // global start of the tile's run of each digit
-  __shared__ int wsum[kTileWaves], wsum2[kTileWaves];
-  __shared__ uint32_t xk[kTileMax], xv[kTileMax];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  const int radix = 1 << dbits;
-  const int tile = blockIdx.x, ntiles = gridDim.x;
-  const int64_t base = (int64_t)tile * kTileMax;
-  const int nt = (int)(n - base < kTileMax ? n - base : kTileMax);
-  uint32_t key[kSortRounds], val[kSortRounds];
-#pragma unroll
-  for (int r = 0; r < kSortRounds; ++r) {
-    const int e = w * kTileKeys + r * 64 + lane;
-    key[r] = kSentinel;
-    val[r] = 0;
-    if (e < nt) {
-      key[r] = ksrc ? ksrc[base + e] : raw_key(ids, id_bytes, bag, stride, vocab, base + e);
-      val[r] = vsrc ? vsrc[base + e] : (uint32_t)(base + e);
-    }
-  }
-  // this digit's keys in earlier tiles and in all tiles (thread d)
-  int before = 0, total = 0;
-  if ((int)threadIdx.x < radix) {
-    const int* hd = hist + (int64_t)threadIdx.x * ntiles;
-    for (int t = 0; t < ntiles; ++t) {
-      const int c = hd[t];
-      before += t < tile ? c : 0;
-      total += c;
-    }
-  }
-  for (int t = threadIdx.x; t < kTileWaves * radix; t += kTileThreads) cnt[t / radix][t % radix] = 0;
-  __syncthreads();
-  int pin[kSortRounds];
-#pragma unroll
-  for (int r = 0; r < kSortRounds; ++r) {
-    const bool valid = w * kTileKeys + r * 64 + lane < nt;
-    const uint32_t d = (key[r] >> shift) & (radix - 1);
-    uint64_t peers = __ballot(valid);
-    for (int b = 0; b < dbits; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const uint64_t bb = __ballot(bit);
-      peers &= bit ? bb : ~bb;
-    }
-    const int lrank = __popcll(peers & lt);
-    const int old = valid ? (int)cnt[w][d] : 0;
-    __builtin_amdgcn_wave_barrier();
-    if (valid && lrank == 0) cnt[w][d] = (uint16_t)(old + __popcll(peers));
-    __builtin_amdgcn_wave_barrier();
-    pin[r] = old + lrank;
-  }
-  __syncthreads();
-  // per digit: exclusive offsets over the waves; the tile's digit counts and the global totals
-  // scanned over the digits (two inclusive scans: lanes, then the waves' sums)
-  int tot = 0;
-  if ((int)threadIdx.x < radix) {
-#pragma unroll
-    for (int ww = 0; ww < kTileWaves; ++ww) {
-      const int c = cnt[ww][threadIdx.x];
-      cnt[ww][threadIdx.x] = (uint16_t)tot;
-      tot += c;
-    }
-  }
-  int y = tot, g = total;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t1 = __shfl_up(y, o, 64), t2 = __shfl_up(g, o, 64);
-    if (lane >= o) { y += t1; g += t2; }
-  }
-  if (lane == 63) { wsum[w] = y; wsum2[w] = g; }
-  __syncthreads();
-  if ((int)threadIdx.x < radix) {
-    int pre = 0, pre2 = 0;
-    for (int ww = 0; ww < w; ++ww) { pre += wsum[ww]; pre2 += wsum2[ww]; }
-    tbase[threadIdx.x] = pre + y - tot;
-    gbase[threadIdx.x] = pre2 + g - total + before;
-  }
-  __syncthreads();
-  // keys into tile order (by digit) through LDS
-#pragma unroll
-  for (int r = 0; r < kSortRounds; ++r) {
-    const bool valid = w * kTileKeys + r * 64 + lane < nt;
-    if (valid) {
-      const uint32_t d = (key[r] >> shift) & (radix - 1);
-      const int pl = tbase[d] + (int)cnt[w][d] + pin[r];
-      xk[pl] = key[r];
-      xv[pl] = val[r];
-    }
-  }
-  __syncthreads();
-  // store from tile order: position j of the tile holds a key of digit d at tile offset j - tbase[d]
-#pragma unroll
-  for (int r = 0; r < kSortRounds; ++r) {
-    const int j = r * kTileThreads + (int)threadIdx.x;
-    if (j < nt) {
-      const uint32_t k = xk[j];
-      const uint32_t d = (k >> shift) & (radix - 1);
-      const int64_t pos = (int64_t)gbase[d] + (j - tbase[d]);
-      kdst[pos] = k;
-      vdst[pos] = xv[j];
     }
   }
 }
@@ -1418,7 +1164,7 @@ __global__ __launch_bounds__(256) void segsum_kernel(SegArgs a) {
 // Both fix levels in one launch (round 5): every wave runs level 1 for its block, the workgroups
 // hand their block partials and flags to the last one to finish (agent-scope stores, one ticket),
 // which runs level 2 for every block. Saves a launch per call (~4.5 us each on this box, three
-// calls on C3's critical path); RSYS_SEGSUM_TWO_FIX=1 keeps the two launches.
+// calls on C3's critical path).
 struct FixLds {
   int s_last;
   int tails[256];
@@ -1489,38 +1235,17 @@ __global__ __launch_bounds__(256) void segsum_fix_batch_kernel(SegBatch b) {
   segsum_fix_body<NV>(b.c[k], blockIdx.x - b.fblk0[k], b.fblk0[k + 1] - b.fblk0[k], L);
 }
 
-template <int NV>
-__global__ __launch_bounds__(256) void segsum_fix_blocks_kernel(SegArgs a) {
-  fix_block<NV>(a, blockIdx.x * 4 + (threadIdx.x >> 6));
-}
-
-template <int NV>
-__global__ __launch_bounds__(256) void segsum_fix_runs_kernel(SegArgs a) {
-  fix_run<NV>(a, blockIdx.x * 4 + (threadIdx.x >> 6));
-}
-
 AdamConst make_hyper(float b1, float b2, float eps, float wd) {
   AdamConst h;
   h.one_m_b1 = 1.f - b1; h.b2 = b2; h.one_m_b2 = 1.f - b2; h.eps = eps; h.wd = wd;
   return h;
 }
 
-// opt-in (RSYS_SORT_ONESWEEP=1): the single-launch passes with decoupled look-back measured slower
-// than the histogram + scatter launches at C3 (rs_lookup_sort 0.094 -> 0.115 ms per step)
-bool sort_onesweep() {
-  static const bool v = getenv_flag("RSYS_SORT_ONESWEEP");
-  return v;
-}
-
-// workspace: ping-pong keys + vals, then the multi-launch path's [radix][tiles] histogram and digit
-// totals, or the single-launch path's status words [passes][tiles][radix] (u64), tile counters and
-// per-pass digit totals
+// workspace: ping-pong keys + vals, then the [radix][tiles] histogram and digit totals
 int64_t sort_ws_bytes(int64_t n, int64_t vocab) {
   if (n <= kRankMax) return (int64_t)cdiv(n, kRankBlock) * n * 4 + 256;  // the counting sort's partials
   const SortPlan p = make_plan(n, vocab);
-  const int64_t multi = ((int64_t)kMaxRadix * p.ntiles + kMaxRadix) * 4;
-  const int64_t one = (int64_t)p.passes * p.ntiles * kMaxRadix * 8 + 64 + (int64_t)4 * kMaxRadix * 4;
-  return 2 * n * 4 + (multi > one ? multi : one) + 256;
+  return 2 * n * 4 + ((int64_t)kMaxRadix * p.ntiles + kMaxRadix) * 4 + 256;
 }
 
 }  // namespace
@@ -1540,10 +1265,9 @@ extern "C" int rs_lookup_sort(const void* ids, int id_bytes, int rows, int bag, 
   if (n == 0) return 0;
   hipStream_t st = as_stream(stream);
   const SortPlan p = make_plan(n, vocab);
-  // opt-in (RSYS_SORT_RANK=1): the counting sort (its partials in ws) -- measured no faster than the
-  // one-tile radix sort (two launches of 10.4 + 6.6 us against one of ~18 us: the ~4.5 us launch
-  // floor of this box eats the gain)
-  if (n <= kRankMax && ws && (getenv_flag("RSYS_SORT_RANK") || n > kTileMax)) {
+  // past one tile's keys, up to kRankMax: the counting sort (its partials in ws); round 5 measured it
+  // no faster than the one-tile radix sort below kTileMax (10.4 + 6.6 us against ~18 us)
+  if (n <= kRankMax && ws && n > kTileMax) {
     const int nb = (int)cdiv(n, kRankBlock);
     rank_partial_kernel<<<dim3(nb, nb), kRankBlock, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, (int)n,
                                                               static_cast<int*>(ws));
@@ -1561,48 +1285,7 @@ extern "C" int rs_lookup_sort(const void* ids, int id_bytes, int rows, int bag, 
   RS_CHECK_ARG(ws, "rs_lookup_sort: workspace needed for %lld lookups", (long long)n);
   uint32_t* tk = static_cast<uint32_t*>(ws);
   uint32_t* tv = tk + n;
-  if (sort_onesweep()) {
-    // status words (8-byte aligned after the ping-pong buffers), tile counters, digit totals
-    const int64_t off = ((2 * n * 4 + 7) / 8) * 8;
-    unsigned long long* status = reinterpret_cast<unsigned long long*>(static_cast<char*>(ws) + off);
-    const int64_t nstatus = (int64_t)p.passes * p.ntiles * kMaxRadix;
-    int* counters = reinterpret_cast<int*>(status + nstatus);
-    int* tot = counters + 16;
-    RS_RET_IF((int)hipMemsetAsync(status, 0, nstatus * 8 + 64 + (int64_t)4 * kMaxRadix * 4, st));
-    const int hb = (int)std::min<int64_t>(cdiv(n, kSortThreads), 256);
-    sort_hist_all_kernel<<<hb, kSortThreads, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, n, p, tot);
-    RS_CHECK_LAUNCH("rs_lookup_sort hist");
-    for (int q = 0; q < p.passes; ++q) {
-      const bool to_out = ((p.passes - 1 - q) & 1) == 0;
-      uint32_t* kd = to_out ? keys : tk;
-      uint32_t* vd = to_out ? vals : tv;
-      const uint32_t* ks = q == 0 ? nullptr : (to_out ? tk : keys);
-      const uint32_t* vs = q == 0 ? nullptr : (to_out ? tv : vals);
-      sort_onesweep_kernel<<<p.ntiles, kSortThreads, 0, st>>>(
-          ids, id_bytes, bag, row_stride, vocab, ks, vs, n, p.shift[q], p.dbits[q], tot + q * kMaxRadix,
-          status + (int64_t)q * p.ntiles * kMaxRadix, counters + q, kd, vd);
-      RS_CHECK_LAUNCH("rs_lookup_sort pass");
-    }
-    return 0;
-  }
   int* hist = reinterpret_cast<int*>(tv + n);
-  if (getenv_flag("RSYS_SORT_BIG_TILES")) {  // opt-in: 4,096-key tiles, two launches per pass
-    const int nt4 = (int)cdiv(n, kTileMax);
-    for (int q = 0; q < p.passes; ++q) {
-      const bool to_out = ((p.passes - 1 - q) & 1) == 0;
-      uint32_t* kd = to_out ? keys : tk;
-      uint32_t* vd = to_out ? vals : tv;
-      const uint32_t* ks = q == 0 ? nullptr : (to_out ? tk : keys);
-      const uint32_t* vs = q == 0 ? nullptr : (to_out ? tv : vals);
-      sort_bhist_kernel<<<nt4, kTileThreads, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, ks, n, p.shift[q],
-                                                      p.dbits[q], hist);
-      RS_CHECK_LAUNCH("rs_lookup_sort bhist");
-      sort_bscatter_kernel<<<nt4, kTileThreads, 0, st>>>(ids, id_bytes, bag, row_stride, vocab, ks, vs, n,
-                                                         p.shift[q], p.dbits[q], hist, kd, vd);
-      RS_CHECK_LAUNCH("rs_lookup_sort bscatter");
-    }
-    return 0;
-  }
   int* tot = hist + (int64_t)kMaxRadix * p.ntiles;
   // ping-pong so that the last pass lands in (keys, vals)
   for (int q = 0; q < p.passes; ++q) {
@@ -1842,19 +1525,11 @@ extern "C" int rs_segsum(const uint32_t* keys, const uint32_t* vals, int64_t n, 
   RS_CHECK_ARG(D % 4 == 0 && ldo % 4 == 0 && aligned16(dout) && aligned16(grad),
                "rs_segsum: D, ldo multiples of 4 and 16-byte aligned dout / grad required");
   const int bgrid = cdiv(cdiv(a.nchunks, kFixBlock), 4);
-  const bool two_fix = getenv_flag("RSYS_SEGSUM_TWO_FIX");
 #define RS_SEGSUM(NV, G)                                               \
   segsum_kernel<NV, G><<<grid, 256, 0, st>>>(a);                       \
   RS_CHECK_LAUNCH("rs_segsum");                                        \
-  if (two_fix) {                                                       \
-    segsum_fix_blocks_kernel<NV><<<bgrid, 256, 0, st>>>(a);            \
-    RS_CHECK_LAUNCH("rs_segsum blocks");                               \
-    segsum_fix_runs_kernel<NV><<<bgrid, 256, 0, st>>>(a);              \
-    RS_CHECK_LAUNCH("rs_segsum runs");                                 \
-  } else {                                                             \
-    segsum_fix_kernel<NV><<<bgrid, 256, 0, st>>>(a);                   \
-    RS_CHECK_LAUNCH("rs_segsum fix");                                  \
-  }
+  segsum_fix_kernel<NV><<<bgrid, 256, 0, st>>>(a);                     \
+  RS_CHECK_LAUNCH("rs_segsum fix");
   if (D <= 16) { RS_SEGSUM(1, 4) }
   else if (D <= 32) { RS_SEGSUM(1, 8) }
   else if (D <= 64) { RS_SEGSUM(1, 16) }

@@ -102,7 +102,7 @@ struct TwArgs {
   const int64_t* e_key;
   int e_site;
   Fin fin;  // EPI_STATS / EPI_BWD
-  unsigned long long* dbg;  // profiling only: per-workgroup phase timestamps (RSYS_TOWER_DBG)
+  unsigned long long* dbg;  // profiling only: per-workgroup phase timestamps (rs_tower_debug_buffer)
 };
 
 template <typename T>
@@ -1018,33 +1018,22 @@ int launch_tm(const TwArgs& a, int nblocks, hipStream_t st, const char* name) {
 #undef RS_TW_LAUNCH
 }
 
-int tower_tm_override() {
-  static const int v = [] {
-    const char* e = getenv("RSYS_TOWER_TM");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 // Row tile per launch (round 4): 64 rows when that grid fills the chip (193..256 workgroups, or
 // >= 512), else 32 (B = 4096 gives 64 row tiles: a 128-column Linear was 128 workgroups on 256 CUs); the final
 // Linear (whole rows per workgroup for F.normalize, no statistics hand-off) goes to 16 rows when
 // 32 still leave CUs idle. Measured (tools/tower_phases.py, C3 user tower): the 128-column
 // forward 22 -> 17 us, the final Linear 14 -> 6 us, the 128-column backward 19 -> 17 us; 32-row
 // tiles on grids that were already >= 256 workgroups were slower (their last arriver merges twice
-// the tiles). RSYS_TOWER_TM=16/32/64 forces one (A/B).
+// the tiles).
 template <typename T, int TN, int PRO, int EPI>
 int launch(const TwArgs& a, int nblocks, hipStream_t st, const char* name) {
   auto wgs = [&](int tm) { return (int64_t)nblocks * (cdiv(a.G * cdiv(a.Bg, tm), 8) * 8); };
-  int tm = tower_tm_override();
-  if (tm != 16 && tm != 32 && tm != 64) {
-    // 64 rows fill the chip once (193..256 workgroups) or at two and more per CU; between, a
-    // 64-row grid runs a second partial wave of workgroups (C3's 320-workgroup first-layer
-    // backward: 40 us at 64 rows, 25 us at 32)
-    const int64_t w64 = wgs(64);
-    tm = (w64 > 192 && w64 <= 256) || w64 >= 512 ? 64 : 32;
-    if (EPI == EPI_L2 && wgs(32) < 256) tm = 16;
-  }
+  // 64 rows fill the chip once (193..256 workgroups) or at two and more per CU; between, a 64-row
+  // grid runs a second partial wave of workgroups (C3's 320-workgroup first-layer backward: 40 us
+  // at 64 rows, 25 us at 32)
+  const int64_t w64 = wgs(64);
+  int tm = (w64 > 192 && w64 <= 256) || w64 >= 512 ? 64 : 32;
+  if (EPI == EPI_L2 && wgs(32) < 256) tm = 16;
   if constexpr (EPI == EPI_L2) {
     if (tm == 16) return launch_tm<T, 16, TN, PRO, EPI>(a, nblocks, st, name);
   }

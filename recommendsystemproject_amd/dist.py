@@ -380,9 +380,7 @@ class overlap:
     def __init__(self, model):
         f = flat_of(next(model.parameters())) if is_active() else None
         self.gb = getattr(f, 'dp_buckets', None) if f is not None else None
-        if os.environ.get('RSYS_DP_OVERLAP', '1') == '0':
-            self.gb = None
-        elif (self.gb is not None and dist.get_backend() != 'nccl' and torch.cuda.is_available()
+        if (self.gb is not None and dist.get_backend() != 'nccl' and torch.cuda.is_available()
               and torch.cuda.is_current_stream_capturing()):
             self.gb = None  # host-staged collectives (gloo) cannot be captured
 

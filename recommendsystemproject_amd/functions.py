@@ -145,25 +145,23 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
     order = list(groups.values())
     # no fork from a side stream (the item tower's, or the user tower's own): a fork of a fork
     # breaks hipGraph capture on this ROCm (streams.py)
-    fork = (len(order) > 1 and os.environ.get('RSYS_TOWER_STREAMS', '1') != '0' and
-            os.environ.get('RSYS_LOOKUP_STREAMS', '1') != '0' and torch.cuda.is_available() and streams.can_fork())
+    fork = (len(order) > 1 and os.environ.get('RSYS_TOWER_STREAMS', '1') != '0' and torch.cuda.is_available() and
+            streams.can_fork())
     if not fork:
         for idxs in order:
             for i in idxs:
                 one(i)
         return calls, lazy
-    # the largest table's work stays on the current stream, the others fork (onto the stream
-    # TwoTowerModel prefers -- the item tower's, ahead of its tower -- or a stream per table)
+    # the largest table's work stays on the current stream, the others fork (a stream per table)
     order.sort(key=lambda idxs: -sum(int(segs[i].vocab) for i in idxs))
     main = torch.cuda.current_stream()
     sides = []
-    pref = streams.preferred_lookup_stream()
     for k, idxs in enumerate(order):
         if k == 0:
             for i in idxs:
                 one(i)
             continue
-        st = pref if pref is not None and pref.device == main.device else _call_stream(main, k)
+        st = _call_stream(main, k)
         st.wait_stream(main)
         with torch.cuda.stream(st):
             for i in idxs:
@@ -207,12 +205,10 @@ def _grad_tables(segs, calls, dout, tables, rows, params=()):
     if rest:
         rest = _sorted_ordinary(rest, rows, dout)
     if rest:
-        _gather_bwd_split(rest, rows, dout)
+        ops.gather_bwd(rest, rows, dout)
     _dp.note_writer(params, written=True)
     # calls of different tables of one row width share one launch pair (rs_segsum_batch, up to 4
-    # a launch); a table's calls keep their order (each its own launch after the first);
-    # RSYS_SEGSUM_BATCH=0: one rs_segsum per call
-    batch_on = os.environ.get('RSYS_SEGSUM_BATCH', '1') != '0'
+    # a launch); a table's calls keep their order (each its own launch after the first)
     pending = []
 
     def flush():
@@ -224,7 +220,7 @@ def _grad_tables(segs, calls, dout, tables, rows, params=()):
     for t, c, ptr in big:
         if ptr is None:  # max-pooled: its per-lookup gradient rows are already the call's dseg
             continue
-        args = t.segsum_call(c, ptr, dout.stride(0)) if batch_on else None
+        args = t.segsum_call(c, ptr, dout.stride(0))
         if args is None:
             flush()
             t.segsum(c, ptr, dout.stride(0))
@@ -274,38 +270,6 @@ def _sorted_ordinary(segs, rows, dout):
         _hip.call('rs_segsum', keys.data_ptr(), vals.data_ptr(), n, bag, mode, sg.pad_idx, ptr,
                   dout.stride(0), sg.dim, sg.grad, 1, ws.data_ptr(), ops.stream())
     return rest
-
-
-_HEAVY_LOOKUPS = 65536
-
-
-def _gather_bwd_split(segs, rows, dout):
-    """rs_gather_bwd of a gather's ordinary segments. Token-sized segments (>= 64K lookups: C2's
-    per-token history tables, 204,800 ids into 3,500 x 32 and 614,400 tag ids into 30 x 8) each
-    take a latency-bound kernel that leaves most of the chip idle, and one launch runs its kernels
-    back to back: the heavy segments after the first go to side streams, forked from the current
-    one and joined back before the caller reports its gradients. Opt-in (RSYS_GRAD_STREAMS=1;
-    never with RSYS_TOWER_STREAMS=0, the bench's serial instrumented pass): measured at C2 (bf16,
-    replayed graphs) 1.40 -> 1.48 ms per step, like the weight-gradient branches (_WgradBranch):
-    on this ROCm the replayed graph pays more for the extra cross-queue waits than the two
-    latency-bound kernels gain by overlapping."""
-    heavy = [sg for sg in segs if sg.kind in (_hip.RS_SEG_SPARSE, _hip.RS_SEG_POOL) and
-             rows * (sg.bag if sg.kind == _hip.RS_SEG_POOL else 1) >= _HEAVY_LOOKUPS]
-    if (len(heavy) < 2 or os.environ.get('RSYS_GRAD_STREAMS', '0') != '1' or
-            os.environ.get('RSYS_TOWER_STREAMS', '1') == '0' or not dout.is_cuda or not streams.can_fork()):
-        ops.gather_bwd(segs, rows, dout)
-        return
-    main = torch.cuda.current_stream()
-    side = [_call_stream(main, 8 + k) for k in range(len(heavy) - 1)]
-    moved = {id(sg) for sg in heavy[1:]}
-    for st, sg in zip(side, heavy[1:]):
-        st.wait_stream(main)
-        dout.record_stream(st)
-        with torch.cuda.stream(st):
-            ops.gather_bwd([sg], rows, dout)
-    ops.gather_bwd([sg for sg in segs if id(sg) not in moved], rows, dout)
-    for st in side:
-        main.wait_stream(st)
 
 
 def _max_as_single(c, s, dout):
@@ -408,13 +372,10 @@ def seq_input_bwd(proc, saved, dx, B, L, p, key, params=()):
             ops.dropout_bwd(dx, p, key, 0)
     lin = proc.feature_projection[0]
     # dx is final here (the dropout backward above ran in place before this point)
-    with _WgradBranch(dx, cat):
-        ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
+    ops.linear_bwd_weight(dx, cat, grad_of(lin.weight), db=grad_of(lin.bias))
     dcat = ops.linear_bwd_input(dx, lin.weight)
     for s, t in zip(segs, tables):
         s.grad = grad_of(t).data_ptr()
-    # the encoder's weight gradients (side stream) are in before the op reports its gradients
-    _WgradBranch.join()
     _grad_tables(segs, calls, dcat, tables, B * L, params)
 
 
@@ -442,74 +403,12 @@ class SeqFeaturesFn(torch.autograd.Function):
     @once_differentiable
     def backward(ctx, dx):
         dx = dx.contiguous().view(ctx.B * ctx.L, -1).clone()  # consumed in place below
-        try:
-            seq_input_bwd(ctx.proc, ctx.saved, dx, ctx.B, ctx.L, ctx.p, ctx.key, ctx.params)
-        finally:
-            _WgradBranch.join()
+        seq_input_bwd(ctx.proc, ctx.saved, dx, ctx.B, ctx.L, ctx.p, ctx.key, ctx.params)
         ctx.saved = ctx.params = None
         return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
 
 # ================================================================================ encoder layer
-class _WgradBranch:
-    """The encoder backward's weight gradients on a side stream (round 4): a layer's dW / db
-    kernels only read activations and the layer's output gradient, and nothing on the input-
-    gradient chain reads what they write (the flat gradient), so they run beside the chain
-    instead of in it -- forked from the current stream once their inputs are queued, joined back
-    before the op reports its gradients (seq_input_bwd). The fork / join is captured into the
-    step's hipGraph as parallel branches. Opt-in (RSYS_WGRAD_STREAM=1; never with
-    RSYS_TOWER_STREAMS=0, the bench's serial instrumented pass): measured at C2 (bf16, replayed
-    graphs) 1.425 -> 1.46 ms per step -- the branches' cross-queue waits cost more than the
-    overlap gains, the weight-gradient kernels being full-chip launches themselves."""
-
-    _streams = {}
-
-    def __init__(self, *tensors):
-        self.on = (os.environ.get('RSYS_WGRAD_STREAM', '0') == '1' and
-                   os.environ.get('RSYS_TOWER_STREAMS', '1') != '0' and
-                   all(t.is_cuda for t in tensors) and not any(_is_fake(t) for t in tensors) and
-                   streams.can_fork())
-        self.tensors = tensors
-
-    def __enter__(self):
-        if not self.on:
-            return self
-        main = torch.cuda.current_stream()
-        side = self._streams.get(main.device)
-        if side is None:
-            side = self._streams[main.device] = streams.side_stream(main.device)
-        side.wait_stream(main)
-        for t in self.tensors:  # made on the main stream, read on the side one
-            t.record_stream(side)
-        _WgradBranch._pending[main.device] = side
-        self._ctx = torch.cuda.stream(side)
-        self._ctx.__enter__()
-        return self
-
-    def __exit__(self, *exc):
-        if self.on:
-            self._ctx.__exit__(*exc)
-
-    _pending = {}
-
-    @classmethod
-    def join(cls):
-        """The current stream waits for the weight gradients forked so far."""
-        if not cls._pending:
-            return
-        main = torch.cuda.current_stream()
-        side = cls._pending.pop(main.device, None)
-        if side is not None:
-            main.wait_stream(side)
-
-    @classmethod
-    def assert_joined(cls):
-        """The optimizer reads the flat gradient: no forked weight-gradient branch may be pending."""
-        if cls._pending:
-            cls._pending.clear()
-            raise RuntimeError('rsys: an encoder weight-gradient branch was forked and never joined')
-
-
 def _is_fake(t):
     from torch._subclasses.fake_tensor import FakeTensor
     return isinstance(t, FakeTensor)
@@ -592,10 +491,9 @@ def _post_attn_bwd(lyr, saved, dx2, p, key, site):
             m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias), h1, lyr.norm1.weight, m1, r1,
             g(lyr.norm1.weight), g(lyr.norm1.bias), p, key, site + 1, site + 3)
         ln1_done = True
-        with _WgradBranch(x1, f1[1], dff):
-            ops.ffn_wgrad_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, f1[1], dff, p,
-                               g(lyr.linear1.weight), g(lyr.linear1.bias), g(lyr.linear2.weight),
-                               g(lyr.linear2.bias))
+        ops.ffn_wgrad_bf16(x1, lyr.linear1.weight, lyr.linear1.bias, lyr.linear2.weight, f1[1], dff, p,
+                           g(lyr.linear1.weight), g(lyr.linear1.bias), g(lyr.linear2.weight),
+                           g(lyr.linear2.bias))
     else:
         dff = torch.empty_like(dx2) if p > 0 else None
         dh2 = ops.layernorm_bwd(h2, dx2, lyr.norm2.weight, m2, r2, g(lyr.norm2.weight), g(lyr.norm2.bias),
@@ -614,12 +512,7 @@ def _post_attn_bwd(lyr, saved, dx2, p, key, site):
                                 da=dsa, p=p, key=key, site=site + 1)
     if dsa is None:  # p == 0: dsa IS dh1 (read here before the in-proj backward accumulates into it)
         dsa = dh1
-        # the in-proj backward then accumulates into dh1 on the main stream: this weight gradient
-        # reads it first, on the main stream too
-        ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
-    else:
-        with _WgradBranch(dsa, att):
-            ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
+    ops.linear_bwd_weight(dsa, att, g(sa_mod.out_proj.weight), db=g(sa_mod.out_proj.bias))
     datt = ops.linear_bwd_input(dsa, sa_mod.out_proj.weight)
     return dh1, datt
 
@@ -628,11 +521,10 @@ def _in_proj_bwd(lyr, x, dqkv, dx=None):
     """in_proj weight gradient and dx (+)= dqkv W_in."""
     g = grad_of
     sa_mod = lyr.self_attn
-    with _WgradBranch(dqkv, x):
-        if dqkv.dtype == torch.bfloat16:  # bf16 dqkv (RS_ATTN_QKV_BF16): bf16-MFMA weight gradient
-            ops.wgrad_bf16(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
-        else:
-            ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
+    if dqkv.dtype == torch.bfloat16:  # bf16 dqkv (RS_ATTN_QKV_BF16): bf16-MFMA weight gradient
+        ops.wgrad_bf16(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
+    else:
+        ops.linear_bwd_weight(dqkv, x, g(sa_mod.in_proj_weight), db=g(sa_mod.in_proj_bias))
     if dx is None:
         return ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight)
     return ops.linear_bwd_input(dqkv, sa_mod.in_proj_weight, out=dx, beta=1.0)  # dx = dh1 + dqkv Win
@@ -722,32 +614,26 @@ class SeqEncoderFn(torch.autograd.Function):
         n = len(ctx.layers)
         # the encoder's weight / LayerNorm / positional gradient reductions queued and run as one
         # launch at the end (ops.deferred_reduce): not under data parallelism (the bucket's
-        # all-reduce starts inside seq_input_bwd) nor with the weight gradients on a side stream
+        # all-reduce starts inside seq_input_bwd)
         from .flat import _dp_active
-        defer = not _dp_active() and os.environ.get('RSYS_WGRAD_STREAM', '0') != '1'
-        try:
-            with ops.deferred_reduce(defer):
-                if ctx.prune:
-                    # the fused bf16 FFN backward only reads the output gradient; the fp32 path's
-                    # norm2 backward runs in place over it (autograd's buffer: give it a copy)
-                    ls = ctx.layer_saved[n - 1]
-                    d_last = dout if isinstance(ls[8], tuple) else dout.clone()
-                    dx = layer_bwd_last(ctx.layers[n - 1], ls, d_last, ctx.key_pad,
-                                        ctx.last, B, L, d, H, p, key, _layer_site(n - 1))
-                    n -= 1
-                else:
-                    dx = torch.zeros(B * L, d, device=dout.device, dtype=torch.float32)
-                    seg = _seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=ctx.last.data_ptr(),
-                               grad=dx.data_ptr())
-                    ops.gather_bwd([seg], B, dout)
-                for i in reversed(range(n)):
-                    dx = layer_bwd(ctx.layers[i], ctx.layer_saved[i], dx, ctx.key_pad, B, L, d, H, p, key,
-                                   _layer_site(i))
-                seq_input_bwd(proc, ctx.in_saved, dx, B, L, p, key, ctx.params)
-        finally:
-            # structural join of any weight-gradient branch this backward forked (seq_input_bwd
-            # joins on its normal path; an exception or a path that never reaches it joins here)
-            _WgradBranch.join()
+        with ops.deferred_reduce(not _dp_active()):
+            if ctx.prune:
+                # the fused bf16 FFN backward only reads the output gradient; the fp32 path's
+                # norm2 backward runs in place over it (autograd's buffer: give it a copy)
+                ls = ctx.layer_saved[n - 1]
+                d_last = dout if isinstance(ls[8], tuple) else dout.clone()
+                dx = layer_bwd_last(ctx.layers[n - 1], ls, d_last, ctx.key_pad,
+                                    ctx.last, B, L, d, H, p, key, _layer_site(n - 1))
+                n -= 1
+            else:
+                dx = torch.zeros(B * L, d, device=dout.device, dtype=torch.float32)
+                seg = _seg(kind=_hip.RS_SEG_LASTVALID, dim=d, out_col=0, bag=L, idx=ctx.last.data_ptr(),
+                           grad=dx.data_ptr())
+                ops.gather_bwd([seg], B, dout)
+            for i in reversed(range(n)):
+                dx = layer_bwd(ctx.layers[i], ctx.layer_saved[i], dx, ctx.key_pad, B, L, d, H, p, key,
+                               _layer_site(i))
+            seq_input_bwd(proc, ctx.in_saved, dx, B, L, p, key, ctx.params)
         ctx.layer_saved = ctx.in_saved = ctx.params = None
         return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
@@ -982,9 +868,7 @@ def tower_chain_supported(feature_bn, mlp, x, G) -> bool:
     """The fused chain (csrc/tower.hip) covers training mode with batch statistics: feature_bn and
     every hidden BatchNorm with a momentum, inputs of width <= 512, hidden widths <= 256, an output
     of width <= 128, all multiples of 4. Eval mode (running statistics) and other shapes take the
-    per-op path (BatchNormFn + MLPFn). RSYS_TOWER_CHAIN=0 forces the per-op path (A/B)."""
-    if os.environ.get('RSYS_TOWER_CHAIN', '1') == '0':
-        return False
+    per-op path (BatchNormFn + MLPFn)."""
     if not (feature_bn.training and mlp.training) or x.dim() != 2:
         return False
     seq = mlp.mlp

@@ -297,7 +297,7 @@ def _zbits_words(B, L, d, H, p, flags):
     """uint16 words of rs_attn_fwd's saved dropout keep bits (include/rsys_hip.h): the bf16 MFMA
     path with L <= 64 and p > 0 (the dispatch condition of attention.hip), else 0."""
     if not (p > 0 and flags & _hip.RS_GEMM_BF16 and d // H == 16 and L <= 64 and B * H * L * L < 2 ** 32
-            and not os.environ.get('RSYS_ATTN_VALU') and not os.environ.get('RSYS_ATTN_NO_ZBITS')):
+            and not os.environ.get('RSYS_ATTN_VALU')):
         return 0
     return B * H * ((L + 15) // 16) * 64
 
@@ -378,8 +378,6 @@ def linear_add_layernorm_rows(x, W, bias, table, rows, bag, gamma, beta, eps=1e-
     take the shape (the caller gathers the rows instead)."""
     M, K = x.shape
     N = W.shape[0]
-    if os.environ.get('RSYS_LN_ROWS') == '0':  # A/B: the gathered copy (round 4's path)
-        return None
     if not (precision.gemm_flags() & _hip.RS_GEMM_BF16) or M % 16 or N != 64 or K not in (64, 256) or \
             x.stride(0) % 4 or W.stride(0) % 4 or rows.dtype != torch.int64 or not table.is_contiguous():
         return None

@@ -93,8 +93,7 @@ class _DeviceClip:
         # region's in the first of those launches
         items = [(_sorted_call(t, c, i, g=g, owner=owner), k) for k, (t, c, owner, i) in enumerate(work)]
         batches = _sorted_batches(items)
-        if (not work and prepare is None and os.environ.get('RSYS_OPT_FUSE', '1') != '0'
-                and os.environ.get('RSYS_SQNORM_CLIP_FUSED', '1') != '0'):
+        if not work and prepare is None:
             # no lazy tables: the partials and the coefficient in one launch (same bits)
             _hip.call('rs_grad_sqnorm_clip_step', g.data_ptr(), n, float(scale), ws.data_ptr(),
                       self.ticket.data_ptr(), float(max_norm), self.norm.data_ptr(), self.coef.data_ptr(),
@@ -103,7 +102,7 @@ class _DeviceClip:
         # the dense partials ride in the first sorted launch only when there is a dense region:
         # that launch adds its dense workgroups for n > 0 only, and rs_grad_sqnorm writes the
         # n = 0 partial (0) that rs_clip_coef* then sums
-        fuse_dense = n > 0 and os.environ.get('RSYS_OPT_FUSE', '1') != '0'
+        fuse_dense = n > 0
         if not batches or not fuse_dense:
             _hip.call('rs_grad_sqnorm', g.data_ptr(), n, float(scale), ws.data_ptr(), ops.stream())
         for j, batch in enumerate(batches):
@@ -227,8 +226,6 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        from .functions import _WgradBranch
-        _WgradBranch.assert_joined()
         for group in self.param_groups:
             b1, b2 = group['betas']
             f = self._group_flat(group)
@@ -239,7 +236,6 @@ class Adam(torch.optim.Optimizer):
                 lr, eps, wd = float(group['lr']), float(group['eps']), float(group['weight_decay'])
                 coef = None
                 counted = prepared = False
-                fuse = os.environ.get('RSYS_OPT_FUSE', '1') != '0'
                 if f.lazy and st['step'] >= CONSTS_CAP - 1:
                     raise RuntimeError(f'lazy Adam: more than {CONSTS_CAP - 2} steps; raise optim.CONSTS_CAP')
                 if clip_max_norm is not None and clip_max_norm > 0:
@@ -248,7 +244,7 @@ class Adam(torch.optim.Optimizer):
                     # the device step count (and the lazy tables' step constants) advanced by the
                     # clip coefficient's own launch (no rs_counter_add / rs_adam_prepare launch)
                     counted = not f.lazy
-                    prepared = bool(f.lazy) and fuse
+                    prepared = bool(f.lazy)
                     self._clip.compute(f.grad, f.dense_numel, clip_max_norm, self.grad_scale, f.lazy,
                                        counter=st['step_dev'] if counted else None,
                                        prepare=(st['step_dev'], st['consts'], CONSTS_CAP, lr, b1, b2)
@@ -262,7 +258,7 @@ class Adam(torch.optim.Optimizer):
                     _hip.call('rs_counter_add', st['step_dev'].data_ptr(), 1, ops.stream())
                 dense_args = (f.data.data_ptr(), f.grad.data_ptr(), st['m'].data_ptr(), st['v'].data_ptr(),
                               f.dense_numel)
-                dense_done = not (f.lazy and fuse)
+                dense_done = not f.lazy
                 if dense_done:
                     _hip.call('rs_adam_step', *dense_args, lr, float(b1), float(b2), eps, wd, 0,
                               st['step_dev'].data_ptr(), float(self.grad_scale), coef, 0, ops.stream())

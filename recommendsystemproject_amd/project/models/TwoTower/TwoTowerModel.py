@@ -86,38 +86,23 @@ class TwoTowerModel(nn.Module):
             return user_emb, item_emb, hard_neg_emb
         # fork: the item tower (and its hard-negative pass) on the side stream, the user tower on
         # the current one; join before the loss. Autograd runs each tower's backward on the stream
-        # its forward used, so the backward overlaps the same way. RSYS_LOOKUPS_ON_SIDE=1 (opt-in)
-        # issues the user tower first and forks the lookup chains of its smaller large tables (C3's
-        # user ids: sort + catch-up, ~27 us) onto the side stream ahead of the item tower; measured
-        # slower (round 5: C3 fp32 0.78 -> 0.82, C2 1.33 -> 1.35 ms per step, two repetitions
-        # each); the reversed creation order also moves the item tower's backward ahead of the
-        # user tower's in the autograd queue.
+        # its forward used, so the backward overlaps the same way. (Round 5 measured the user
+        # tower's smaller lookup chains forked onto the side stream ahead of the item tower
+        # slower: C3 fp32 0.78 -> 0.82, C2 1.33 -> 1.35 ms per step.)
         main = torch.cuda.current_stream(dev)
         streams.set_root(main)  # collectives issued on the side streams run here (streams.on_root)
         side.wait_stream(main)
         ustream = self._user_stream(dev)
-        # (data parallel keeps round 4's order: with the item tower created last, its backward is
-        # issued first, and its bucket's all-reduce, issued from the root stream (streams.on_root),
-        # would hold the whole user-tower backward behind it)
-        on_side = (ustream is None and not rdist.is_active() and
-                   os.environ.get('RSYS_LOOKUPS_ON_SIDE') == '1')
-        if not on_side:
-            with torch.cuda.stream(side):
-                item_emb, hard_neg_emb = self._item_side(batch_data)
+        with torch.cuda.stream(side):
+            item_emb, hard_neg_emb = self._item_side(batch_data)
         if ustream is not None:
             ustream.wait_stream(main)
             with torch.cuda.stream(ustream):
                 user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
             main.wait_stream(ustream)
             user_emb.record_stream(main)
-        elif on_side:
-            with streams.prefer_lookup_stream(side):
-                user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
         else:
             user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
-        if on_side:
-            with torch.cuda.stream(side):
-                item_emb, hard_neg_emb = self._item_side(batch_data)
         main.wait_stream(side)
         outs = [t for t in (item_emb, hard_neg_emb) if t is not None]
         for t in outs:

@@ -25,7 +25,6 @@ import torch
 
 _FORKED = set()  # stream identities of the side streams created here
 _ROOT = {}       # device index -> the stream the current step's forward ran on (its fork origin)
-_LOOKUP = []     # innermost last: the stream the large tables' extra lookup chains fork onto
 
 
 def _key(s):
@@ -73,19 +72,3 @@ def on_root(sync=True):
         yield
     if sync:
         cur.wait_stream(root)
-
-
-@contextlib.contextmanager
-def prefer_lookup_stream(s):
-    """While active, the per-table lookup chains that functions._lookup_lazy forks (every large
-    table of a call but the largest) go to side stream `s` instead of a stream of their own
-    (TwoTowerModel: the item tower's stream, ahead of the item tower, whose queue has slack)."""
-    _LOOKUP.append(s)
-    try:
-        yield
-    finally:
-        _LOOKUP.pop()
-
-
-def preferred_lookup_stream():
-    return _LOOKUP[-1] if _LOOKUP else None
