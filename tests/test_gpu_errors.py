@@ -125,31 +125,48 @@ def _clone_batch(b):
     return {k: _clone_batch(v) for k, v in b.items()} if isinstance(b, dict) else b
 
 
-def test_rccl_captured_step_row_sharded_world_size_one(monkeypatch):
+def test_rccl_captured_step_row_sharded_world_size_one():
     """bench.py's N > 1 step exactly as the driver's RCCL scaling run executes it, on one GPU: the
     'nccl' backend at world_size 1 with the exchange forced on and every lookup table row-sharded
     (RSYS_SHARD_ROWS=1: the single-id / per-token lookups through the all-to-all row exchange,
     pooled bags through all-gather + reduce-scatter), forward + backward with the bucketed
     all-reduces started inside it + the shard exchange + clip + Adam captured into ONE hipGraph
     (thread_local capture, as bench.py) and replayed for 3 steps on new batches. Deterministic
-    mode; the weights after the replays equal an eager run of the same 5 steps bitwise."""
+    mode; the weights after the replays equal an eager run of the same 5 steps bitwise.
+    Runs in a fresh process of its own, as bench.py's ranks do: round 6's full-suite run once
+    aborted inside this test after ~130 other tests had run in the same process (a native
+    thread's abort, no GPU fault; the same test passed alone and the driver's bench ranks are
+    fresh processes), and an abort must fail this test, not end the suite."""
+    import subprocess
+    import sys
+    code = ('import sys; sys.path[:0] = [%r, %r, %r]; import test_gpu_errors as t; t._rccl_captured_body()'
+            % (ROOT, os.path.join(ROOT, 'tests'), os.path.join(ROOT, 'tests', 'golden')))
+    env = dict(os.environ, RSYS_LAZY_ROWS='1', RSYS_SHARD_ROWS='1', MASTER_ADDR='127.0.0.1',
+               MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, '-u', '-c', code], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=180)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert '[rccl-captured] bitwise equal' in out and '[rccl-captured] torn down' in out, out[-4000:]
+
+
+def _rccl_captured_body():
+    """The body of test_rccl_captured_step_row_sharded_world_size_one, in its own process
+    (RSYS_LAZY_ROWS, RSYS_SHARD_ROWS and the rendezvous set by the parent)."""
     import faulthandler
     import sys
     from recommendsystemproject_amd import ops
+    import recommendsystemproject_amd.flat as flat
 
     def stage(msg):
         print(f'[rccl-captured] {msg}', file=sys.stderr, flush=True)
-    faulthandler.dump_traceback_later(100, exit=True)  # a hang prints every thread's stack and ends
-    monkeypatch.setenv('RSYS_LAZY_ROWS', '1')
-    monkeypatch.setenv('RSYS_SHARD_ROWS', '1')
-    monkeypatch.setenv('MASTER_ADDR', '127.0.0.1')
-    monkeypatch.setenv('MASTER_PORT', str(_free_port()))
+    faulthandler.enable()
+    faulthandler.dump_traceback_later(150, exit=True)  # a hang prints every thread's stack and ends
     dist.init_process_group('nccl', rank=0, world_size=1, device_id=DEV)
     torch.use_deterministic_algorithms(True, warn_only=True)
+    rdist.is_active = lambda: True
+    flat._dp_active = lambda: True
     try:
-        monkeypatch.setattr(rdist, 'is_active', lambda: True)
-        import recommendsystemproject_amd.flat as flat
-        monkeypatch.setattr(flat, '_dp_active', lambda: True)
         _, cfg = _model()
         b = _batches(cfg, 5)
         losses = {}
@@ -197,3 +214,4 @@ def test_rccl_captured_step_row_sharded_world_size_one(monkeypatch):
         gc.collect()
         torch.cuda.synchronize()
         dist.destroy_process_group()
+    stage('torn down')

@@ -6,6 +6,7 @@
 #   launch2: `python bench.py --gpus 2` (gloo, one GPU: the self-launcher)
 #   c3     : C3 fp32 + C2 bf16 lines without CPU legs
 #   prof   : rocprofv3 --kernel-trace --stats of the default C2 bench (+ C3 fp32 extra)
+#   ab     : env A/B (tools/gpu_ab_env.sh "$AB" "$AB_CFGS")
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-a}
@@ -30,6 +31,7 @@ print('c3 fp32', d['ms_per_step'], 'c2 bf16', d['extra']['c2_bf16']['ms_per_step
     prof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
           timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r6_${TAG}_prof -o run -- \
             python3 bench.py --no-cpu-baseline --extra c3:fp32 --prof-markers > gpurun_out/r6_${TAG}_prof.log 2>&1; rc=$? ;;
+    ab) REPS=${REPS:-2} timeout -k 10 900 bash tools/gpu_ab_env.sh "$AB" "${AB_CFGS:-c3:fp32 c2:bf16}"; rc=$? ;;
     *) echo "unknown stage $s"; rc=2 ;;
   esac
   [ $rc -eq 0 ] || { echo "[gpu_r6] stage $s failed rc=$rc"; exit $rc; }
