@@ -614,6 +614,12 @@ typedef struct rs_sorted_call {
 int rs_sorted_adam_batch(const rs_sorted_call_t* calls, int ncalls, const int64_t* step,
                          const float* consts, float beta1, float beta2, float eps, float weight_decay,
                          float scale, const float* coef, void* stream);
+/* rs_sorted_catchup of up to 8 sorted calls (of one row-width class) in one launch (round 6):
+ * each call's distinct rows brought to the optimizer step (g, owner unused). Replaces back-to-back
+ * forward catch-ups of several large tables (GenericTower.py:150-157: the tower's lookups). */
+int rs_sorted_catchup_batch(const rs_sorted_call_t* calls, int ncalls, const int64_t* step,
+                            const float* consts, float beta1, float beta2, float eps, float weight_decay,
+                            void* stream);
 /* The same two batches with the flat buffer's dense region [0, n) in the same launch (round 5):
  * rs_grad_sqnorm's partials of g (rs_sqnorm_parts(n) of them) into ws_dense, and rs_adam_step's
  * update of p, g, m, v (step constants from *step, lr) -- the same partitions, the same bits as the

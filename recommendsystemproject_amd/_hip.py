@@ -75,6 +75,7 @@ SIGNATURES = {
     'rs_colsum': (i32, [vp, i32, i32, i32, f32, f32, vp, vp, vp]),
     'rs_gather_fwd': (i32, [vp, i32, i32, vp, i32, vp, vp]),
     'rs_sorted_adam_batch': (i32, [vp, i32, vp, vp, f32, f32, f32, f32, f32, vp, vp]),
+    'rs_sorted_catchup_batch': (i32, [vp, i32, vp, vp, f32, f32, f32, f32, vp]),
     'rs_sorted_sqnorm_batch': (i32, [vp, i32, f32, vp, vp]),
     'rs_copy_many': (i32, [i32, vp, vp, vp, vp]),
     'rs_nan_check_many': (i32, [i32, vp, vp, vp, vp, vp]),

@@ -1409,9 +1409,10 @@ static int sorted_rows_batch(int op, const rs_sorted_call_t* calls, int ncalls, 
   int wg = 0;
   for (int c = 0; c < ncalls; ++c) {
     const rs_sorted_call_t& k = calls[c];
-    RS_CHECK_ARG(k.keys && k.g && k.D >= 1 && k.n >= 0 && lanes_per_row(k.D) == G,
+    RS_CHECK_ARG(k.keys && (k.g || op == kCatchup) && k.D >= 1 && k.n >= 0 && lanes_per_row(k.D) == G,
                  "rs_sorted_*_batch: call %d: bad args or another row width class than call 0", c);
-    RS_CHECK_ARG(op != kAdam || (k.p && k.m && k.v && k.last), "rs_sorted_adam_batch: call %d: null state", c);
+    RS_CHECK_ARG((op != kAdam && op != kCatchup) || (k.p && k.m && k.v && k.last),
+                 "rs_sorted_adam_batch / rs_sorted_catchup_batch: call %d: null state", c);
     RowArgs& a = b.a[c];
     a.keys = k.keys; a.n = k.n; a.D = k.D; a.p = k.p; a.g = k.g; a.m = k.m; a.v = k.v; a.last = k.last;
     a.owner = k.owner; a.call = k.call; a.step = step;
@@ -1432,12 +1433,24 @@ static int sorted_rows_batch(int op, const rs_sorted_call_t* calls, int ncalls, 
   }
   if (op == kAdam) {
     RS_BATCH(kAdam)
+  } else if (op == kCatchup) {
+    RS_BATCH(kCatchup)
   } else {
     RS_BATCH(kSqnorm)
   }
 #undef RS_BATCH
   RS_CHECK_LAUNCH("rs_sorted_rows_batch");
   return 0;
+}
+
+// The forward catch-up of several sorted calls (tables) in one launch (round 6: C3's user side ran the
+// history table's and the user-id table's catch-ups as two launches back to back on one queue)
+extern "C" int rs_sorted_catchup_batch(const rs_sorted_call_t* calls, int ncalls, const int64_t* step,
+                                       const float* consts, float beta1, float beta2, float eps,
+                                       float weight_decay, void* stream) {
+  RS_CHECK_ARG(step && consts, "rs_sorted_catchup_batch: null pointer");
+  return sorted_rows_batch(kCatchup, calls, ncalls, step, consts, beta1, beta2, eps, weight_decay, 1.f, nullptr,
+                           nullptr, as_stream(stream));
 }
 
 extern "C" int rs_sorted_adam_batch(const rs_sorted_call_t* calls, int ncalls, const int64_t* step,

@@ -77,7 +77,7 @@ class LookupCall:
 
     __slots__ = ('keys', 'vals', 'ws', 'n', 'rows', 'bag', 'pad', 'mode', 'ids_ptr',
                  'id_bytes', 'row_stride', 'keep', 'dseg', 'local_rows', 'own_rows', 'prescale', 'a2a',
-                 'agreed')
+                 'agreed', 'catchup_due')
 
     def __init__(self, keys, vals, n, rows, bag, pad, mode, ids_ptr, id_bytes, row_stride, keep, ws=None):
         self.keys, self.vals, self.n, self.rows, self.bag = keys, vals, n, rows, bag
@@ -90,6 +90,7 @@ class LookupCall:
         self.prescale = None  # ragged mean bags: 1 / this rank's bag length (union summed as SUM)
         self.a2a = None  # all-to-all row-sharded call: the requester side (A2ARequest)
         self.agreed = None  # data parallel: (rows, bag, ragged) over the ranks (dist.agree_batch)
+        self.catchup_due = False  # lookup(defer_catchup=True): its sorted catch-up is the caller's (catchup_batch)
 
 
 # rs_segsum modes: one id per gradient row, mean bag, sum bag (max pooling: atomic scatter)
@@ -162,7 +163,7 @@ class LazyTable:
                           id_bytes, row_stride, keep, ws)
 
     def lookup(self, ids_ptr, rows, bag, row_stride, pad, mode, id_bytes=8, keep=None, record=True,
-               read_through=False, agreed=None):
+               read_through=False, agreed=None, defer_catchup=False):
         """Forward hook: bring the call's rows to the current optimizer step before they are
         gathered and, when the step will train on this lookup (`record`), list it for the step
         with its ids sorted by row. Default: sort, then rs_sorted_catchup over the distinct rows.
@@ -180,6 +181,9 @@ class LazyTable:
         if opt is None or rows * bag == 0 or (c is not None and read_through):
             return c
         hyper = (opt['step_dev'].data_ptr(), opt['consts'].data_ptr(), *opt['hyper'], _stream())
+        if c is not None and defer_catchup:
+            c.catchup_due = True  # issued with the other tables' by catchup_batch
+            return c
         if c is not None:
             _hip.call('rs_sorted_catchup', c.keys.data_ptr(), c.n, self.D, self.ptr(self.flat.data),
                       self.ptr(opt['m']), self.ptr(opt['v']), self.last.data_ptr(), *hyper)
@@ -711,15 +715,48 @@ def gather_shards(local, t):
 
 
 def lookup_table(weight, ids_ptr, rows, bag, row_stride, pad, mode, keep=None, record=True, read_through=False,
-                 agreed=None):
+                 agreed=None, defer_catchup=False):
     """Forward-side hook of the custom ops for a table lookup: a LookupCall for large
     (lazy-Adam) tables (None for ordinary ones, and for a lookup no backward follows: `record`
-    False, the rows are only brought current)."""
+    False, the rows are only brought current). `defer_catchup`: a recorded call's sorted catch-up
+    is left to the caller (catchup_batch, the call's catchup_due set)."""
     t = getattr(weight, '_rs_lazy', None)
     if t is None or flat_of(weight) is not t.flat:
         return None
     return t.lookup(ids_ptr, rows, bag, row_stride, pad, mode, keep=keep, record=record, read_through=read_through,
-                    agreed=agreed)
+                    agreed=agreed, defer_catchup=defer_catchup)
+
+
+def catchup_batch(items):
+    """The deferred forward catch-ups of [(LazyTable, LookupCall)] (calls with catchup_due) as
+    rs_sorted_catchup_batch launches: up to 8 calls of one row-width class, one flat buffer and
+    DISTINCT tables a launch (two calls of one table touch the same rows: the later one runs in a later launch,
+    after the earlier one's rows are current), in the given order."""
+    from .optim import _row_class
+    todo = [(t, c) for t, c in items if c is not None and c.catchup_due]
+    while todo:
+        batch, rest, tables, cls = [], [], set(), None
+        for t, c in todo:
+            k = (_row_class(t.D), id(t.flat))  # one optimizer state per launch
+            if len(batch) < 8 and id(t) not in tables and (cls is None or k == cls):
+                batch.append((t, c))
+                tables.add(id(t))
+                cls = k
+            else:
+                rest.append((t, c))
+        opt = batch[0][0].flat.lazy_opt
+        arr = (_hip.SortedCall * len(batch))()
+        for j, (t, c) in enumerate(batch):
+            sc = arr[j]
+            sc.keys, sc.n, sc.D, sc.call = c.keys.data_ptr(), c.n, t.D, 0
+            sc.p, sc.g = t.ptr(t.flat.data), None
+            sc.m, sc.v = t.ptr(opt['m']), t.ptr(opt['v'])
+            sc.last, sc.owner = t.last.data_ptr(), None
+            c.catchup_due = False
+        import ctypes
+        _hip.call('rs_sorted_catchup_batch', ctypes.addressof(arr), len(batch), opt['step_dev'].data_ptr(),
+                  opt['consts'].data_ptr(), *opt['hyper'], _stream())
+        todo = rest
 
 
 def grad_of(p):

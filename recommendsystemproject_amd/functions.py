@@ -26,7 +26,7 @@ from torch.autograd.function import once_differentiable
 
 from . import _hip, ops, precision, streams
 from . import dist as _dp
-from .flat import SEG_MEAN, SEG_ONE, SEG_SUM, _dp_active, flat_of, grad_of, lookup_table
+from .flat import SEG_MEAN, SEG_ONE, SEG_SUM, _dp_active, catchup_batch, flat_of, grad_of, lookup_table
 
 
 def _seg(**kw):
@@ -115,6 +115,8 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
                 continue
             groups.setdefault(id(t), []).append(i)
 
+    batched = os.environ.get('RSYS_CATCHUP_BATCH', '1') != '0'
+
     def one(i):
         nonlocal lazy
         s, t = segs[i], tables[i]
@@ -127,7 +129,7 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
         args = lt.read_through_args() if record and mode is not None and _read_through() else None
         c = lookup_table(t, s.idx, rows, bag, s.idx_stride, None if s.pad_idx < 0 else s.pad_idx,
                          -1 if mode is None else mode, keep=keep, record=record, read_through=args is not None,
-                         agreed=getattr(s, 'agreed', None))
+                         agreed=getattr(s, 'agreed', None), defer_catchup=batched)
         if c is not None:
             calls[i] = c
             if pool and mode is not None and args is None and getattr(c, 'a2a', None) is None and not _dp_active():
@@ -143,6 +145,18 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
         return c
 
     order = list(groups.values())
+    if batched:
+        # every table's sort on the current stream, then the catch-ups of all of them in one launch
+        # (rs_sorted_catchup_batch; a table's later calls in later launches)
+        order.sort(key=lambda idxs: -sum(int(segs[i].vocab) for i in idxs))
+        done = []
+        for idxs in order:
+            for i in idxs:
+                c = one(i)
+                if c is not None and c.catchup_due:
+                    done.append((tables[i]._rs_lazy, c))
+        catchup_batch(done)
+        return calls, lazy
     # no fork from a side stream (the item tower's, or the user tower's own): a fork of a fork
     # breaks hipGraph capture on this ROCm (streams.py)
     fork = (len(order) > 1 and os.environ.get('RSYS_TOWER_STREAMS', '1') != '0' and torch.cuda.is_available() and
