@@ -24,7 +24,7 @@ import os
 import torch
 from torch.autograd.function import once_differentiable
 
-from . import _hip, ops, precision, streams
+from . import _hip, ops, precision
 from . import dist as _dp
 from .flat import SEG_MEAN, SEG_ONE, SEG_SUM, _dp_active, catchup_batch, flat_of, grad_of, lookup_table
 
@@ -64,24 +64,6 @@ def _read_through():
     return os.environ.get('RSYS_READ_THROUGH', '0') == '1'
 
 
-_CALL_STREAMS = {}
-
-
-def _skey(s):
-    """A stream's identity (torch.cuda.Stream, or the generic torch.Stream dynamo hands out)."""
-    h = getattr(s, 'cuda_stream', None)
-    return h if h is not None else ('id', getattr(s, 'stream_id', id(s)), getattr(s, 'device_index', None))
-
-
-def _call_stream(parent, k):
-    """The k-th side stream of `parent` for the per-table lookup work of one gather."""
-    key = (parent.device.index, _skey(parent), k)
-    st = _CALL_STREAMS.get(key)
-    if st is None:
-        st = _CALL_STREAMS[key] = streams.side_stream(parent.device)
-    return st
-
-
 def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
     """Large (lazy-Adam) tables, flat.py: bring this call's rows to the current optimizer step
     before the gather reads them -- or, recorded lookups, have the gather read them through the
@@ -93,13 +75,9 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
     A row-sharded table (flat.py module doc) is looked up here: its segment is replaced by one
     reading this rank's rows as the exchange returned them (the all-to-all's row buckets, or
     the reduce-scatter's pooled bags), kept alive through `keep`.
-    The sort + catch-up of different tables are independent chains of small, latency-bound
-    kernels (C3: the user-id table's 35 us beside the history table's 200 us): the second and later
-    tables run on side streams forked from and joined back into the current one (a table's own
-    calls stay in order on one stream: their catch-ups touch the same rows). RSYS_TOWER_STREAMS=0
-    keeps everything on the current stream. (Measured: inside the replayed hipGraph the forked
-    chain still runs on the forking stream's queue; sending it to the item tower's stream instead
-    queued it behind that tower and made the C3 step slower, 0.718 -> 0.75 ms.)"""
+    Every table's sort runs first, then one batched catch-up of all the calls (round 6; before,
+    the second and later tables' sort + catch-up chains were forked onto side streams, which inside
+    the replayed hipGraph still ran on the forking stream's queue)."""
     calls = {}
     lazy = None
     groups = {}  # table -> segment indices, first-seen order
@@ -115,8 +93,6 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
                 continue
             groups.setdefault(id(t), []).append(i)
 
-    batched = os.environ.get('RSYS_CATCHUP_BATCH', '1') != '0'
-
     def one(i):
         nonlocal lazy
         s, t = segs[i], tables[i]
@@ -129,7 +105,7 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
         args = lt.read_through_args() if record and mode is not None and _read_through() else None
         c = lookup_table(t, s.idx, rows, bag, s.idx_stride, None if s.pad_idx < 0 else s.pad_idx,
                          -1 if mode is None else mode, keep=keep, record=record, read_through=args is not None,
-                         agreed=getattr(s, 'agreed', None), defer_catchup=batched)
+                         agreed=getattr(s, 'agreed', None), defer_catchup=True)
         if c is not None:
             calls[i] = c
             if pool and mode is not None and args is None and getattr(c, 'a2a', None) is None and not _dp_active():
@@ -144,50 +120,18 @@ def _lookup_lazy(segs, tables, rows, keep=None, record=True, err=None):
             s.lazy_last = lt.last.data_ptr()
         return c
 
-    order = list(groups.values())
-    if batched:
-        # every table's sort on the current stream, then the catch-ups of all of them in one launch
-        # (rs_sorted_catchup_batch; a table's later calls in later launches)
-        order.sort(key=lambda idxs: -sum(int(segs[i].vocab) for i in idxs))
-        done = []
-        for idxs in order:
-            for i in idxs:
-                c = one(i)
-                if c is not None and c.catchup_due:
-                    done.append((tables[i]._rs_lazy, c))
-        catchup_batch(done)
-        return calls, lazy
-    # no fork from a side stream (the item tower's, or the user tower's own): a fork of a fork
-    # breaks hipGraph capture on this ROCm (streams.py)
-    fork = (len(order) > 1 and os.environ.get('RSYS_TOWER_STREAMS', '1') != '0' and torch.cuda.is_available() and
-            streams.can_fork())
-    if not fork:
-        for idxs in order:
-            for i in idxs:
-                one(i)
-        return calls, lazy
-    # the largest table's work stays on the current stream, the others fork (a stream per table)
-    order.sort(key=lambda idxs: -sum(int(segs[i].vocab) for i in idxs))
-    main = torch.cuda.current_stream()
-    sides = []
-    for k, idxs in enumerate(order):
-        if k == 0:
-            for i in idxs:
-                one(i)
-            continue
-        st = _call_stream(main, k)
-        st.wait_stream(main)
-        with torch.cuda.stream(st):
-            for i in idxs:
-                c = one(i)
-                if c is not None:  # made on the side stream, read on the main one until the step ends
-                    for x in (c.keys, c.vals, c.ws):
-                        if isinstance(x, torch.Tensor):
-                            x.record_stream(main)
-        if st not in sides:
-            sides.append(st)
-    for st in sides:
-        main.wait_stream(st)
+    # every table's sort on the current stream, then the catch-ups of all of them in one launch
+    # (rs_sorted_catchup_batch; a table's later calls in later launches). Round 6: C3 fp32
+    # 0.722 -> 0.711 ms per step against a sort + catch-up chain per table (the second and later
+    # tables forked onto side streams, which inside the replayed graph ran on the same queue)
+    order = sorted(groups.values(), key=lambda idxs: -sum(int(segs[i].vocab) for i in idxs))
+    done = []
+    for idxs in order:
+        for i in idxs:
+            c = one(i)
+            if c is not None and c.catchup_due:
+                done.append((tables[i]._rs_lazy, c))
+    catchup_batch(done)
     return calls, lazy
 
 

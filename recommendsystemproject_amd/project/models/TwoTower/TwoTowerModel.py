@@ -93,10 +93,10 @@ class TwoTowerModel(nn.Module):
         streams.set_root(main)  # collectives issued on the side streams run here (streams.on_root)
         side.wait_stream(main)
         ustream = self._user_stream(dev)
-        item_last = ustream is None and not rdist.is_active() and os.environ.get('RSYS_ITEM_LAST') == '1'
-        if not item_last:
-            with torch.cuda.stream(side):
-                item_emb, hard_neg_emb = self._item_side(batch_data)
+        # (round 6 measured the item tower created after the user tower -- its backward then issued
+        # first, beside the user tower's -- slower: C2 1.244 -> 1.251-1.266, C3 fp32 0.711 -> 0.723)
+        with torch.cuda.stream(side):
+            item_emb, hard_neg_emb = self._item_side(batch_data)
         if ustream is not None:
             ustream.wait_stream(main)
             with torch.cuda.stream(ustream):
@@ -105,9 +105,6 @@ class TwoTowerModel(nn.Module):
             user_emb.record_stream(main)
         else:
             user_emb = self.user_tower(batch_data['user_tower'], self.user_feature_mapping)
-        if item_last:
-            with torch.cuda.stream(side):
-                item_emb, hard_neg_emb = self._item_side(batch_data)
         main.wait_stream(side)
         outs = [t for t in (item_emb, hard_neg_emb) if t is not None]
         for t in outs:
