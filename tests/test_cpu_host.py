@@ -160,3 +160,45 @@ def test_custom_ops_registered_with_fake_impls():
         loss, ticket = torch.ops.rsys.inbatch_softmax_loss(U, I, torch.empty(64, dtype=torch.int64), None, 0.15,
                                                           True)
         assert loss.shape == () and ticket.dtype == torch.int64
+
+
+def test_catchup_batch_grouping(monkeypatch):
+    """flat.catchup_batch: up to 8 calls a launch, one row-width class and one flat buffer per
+    launch, and never two calls of one table in a launch (their catch-ups touch the same rows: the
+    later call goes in a later launch, in order)."""
+    import torch
+    from recommendsystemproject_amd import _hip, flat
+
+    class FakeFlat:
+        def __init__(self):
+            z = torch.zeros(4)
+            self.data = z
+            self.lazy_opt = {'m': z, 'v': z, 'step_dev': z, 'consts': z, 'hyper': (0.9, 0.999, 1e-8, 0.0)}
+
+    class FakeTable:
+        def __init__(self, D, fl):
+            self.D, self.flat, self.last = D, fl, torch.zeros(2, dtype=torch.int32)
+
+        def ptr(self, t):
+            return t.data_ptr()
+
+    class FakeCall:
+        def __init__(self):
+            self.keys, self.n, self.catchup_due = torch.zeros(3, dtype=torch.int32), 3, True
+
+    f1, f2 = FakeFlat(), FakeFlat()
+    a, b, c, d = FakeTable(128, f1), FakeTable(100, f1), FakeTable(16, f1), FakeTable(128, f2)
+    items = [(a, FakeCall()), (b, FakeCall()), (a, FakeCall()), (c, FakeCall()), (d, FakeCall()), (b, FakeCall())]
+    launched = []
+
+    def fake_call(name, arr_ptr, n, *rest):
+        arr = (_hip.SortedCall * n).from_address(arr_ptr)
+        launched.append([next(t for t, cl in items if cl.keys.data_ptr() == arr[j].keys) for j in range(n)])
+        return 0
+    monkeypatch.setattr(_hip, 'call', fake_call)
+    monkeypatch.setattr(flat, '_stream', lambda: None)
+    flat.catchup_batch(items)
+    assert all(not cl.catchup_due for _, cl in items)
+    names = {id(a): 'a', id(b): 'b', id(c): 'c', id(d): 'd'}
+    got = [[names[id(t)] for t in g] for g in launched]
+    assert got == [['a', 'b'], ['a', 'b'], ['c'], ['d']], got

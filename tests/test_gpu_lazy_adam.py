@@ -356,3 +356,56 @@ def test_pack_ids_and_rows():
     y = torch.empty(300, 16, device=DEV)
     _hip.call('rs_pack_rows', x.data_ptr() + 4 * 7, 50, 300, 16, y.data_ptr(), ops.stream())
     assert torch.equal(y, x[:, 7:23])
+
+
+def test_sorted_catchup_batch_bitwise():
+    """rs_sorted_catchup_batch (round 6: a gather's tables caught up in one launch) against one
+    rs_sorted_catchup per call: two tables of different widths in one row class (D = 128, 100)
+    and a third call on the first table in a second launch, rows several steps stale -- the same
+    parameters, moments and `last` bit for bit."""
+    V, cap, pad = 5000, 64, 3
+    gen = torch.Generator().manual_seed(11)
+    S = ops.stream()
+    hyper = (B1, B2, EPS, 0.0)
+    step = torch.zeros((), dtype=torch.int64, device=DEV)
+    consts = torch.zeros(cap, 2, device=DEV)
+    consts.view(torch.int32)[0, 0] = cap
+    for _ in range(6):
+        _hip.call('rs_adam_prepare', step.data_ptr(), consts.data_ptr(), cap, LR, B1, B2, S)
+    state = {}
+    for name, D in (('a', 128), ('b', 100)):
+        p = torch.randn(V, D, generator=gen).to(DEV)
+        m = (0.01 * torch.randn(V, D, generator=gen)).to(DEV)
+        v = (0.001 * torch.rand(V, D, generator=gen)).to(DEV)
+        last = torch.randint(0, 5, (V, 1), generator=gen, dtype=torch.int32).repeat(1, 2).to(DEV)
+        state[name] = (D, p, m, v, last)
+    calls = []
+    for name in ('a', 'b', 'a'):
+        ids = torch.randint(0, V, (700,), generator=gen)
+        ids[:4] = pad
+        keys, _ = _sort(ids.to(DEV), V)
+        calls.append((name, keys, ids.numel()))
+    copies = {k: (D, p.clone(), m.clone(), v.clone(), last.clone()) for k, (D, p, m, v, last) in state.items()}
+    for name, keys, n in calls:  # one launch per call
+        D, p, m, v, last = copies[name]
+        _hip.call('rs_sorted_catchup', keys.data_ptr(), n, D, p.data_ptr(), m.data_ptr(), v.data_ptr(),
+                  last.data_ptr(), step.data_ptr(), consts.data_ptr(), *hyper, S)
+
+    def launch(group):
+        arr = (_hip.SortedCall * len(group))()
+        for j, (name, keys, n) in enumerate(group):
+            D, p, m, v, last = state[name]
+            sc = arr[j]
+            sc.keys, sc.n, sc.D, sc.call = keys.data_ptr(), n, D, 0
+            sc.p, sc.g, sc.m, sc.v, sc.last, sc.owner = p.data_ptr(), None, m.data_ptr(), v.data_ptr(), \
+                last.data_ptr(), None
+        import ctypes
+        _hip.call('rs_sorted_catchup_batch', ctypes.addressof(arr), len(group), step.data_ptr(),
+                  consts.data_ptr(), *hyper, S)
+    launch(calls[:2])   # tables a and b together
+    launch(calls[2:])   # a's second call after
+    torch.cuda.synchronize()
+    for name in state:
+        for x, y in zip(state[name][1:], copies[name][1:]):
+            assert torch.equal(x, y), name
+    assert int(state['a'][4][:, 1].max().item()) == 6
