@@ -410,8 +410,10 @@ LAZY_ROW_BYTES = {
 LAZY_ROW_BYTES['rs_sorted_adam_batch_dense'] = LAZY_ROW_BYTES['rs_sorted_adam_batch']
 LAZY_ROW_BYTES['rs_sorted_sqnorm_batch_dense'] = LAZY_ROW_BYTES['rs_sorted_sqnorm_batch']
 DENSE_BYTES_PER_PARAM = {'rs_adam_step': 28.0, 'rs_sorted_adam_batch_dense': 28.0, 'rs_sorted_sqnorm_batch_dense': 4.0}
-LAZY_ENTRIES = ('rs_lookup_sort', 'rs_sorted_catchup', 'rs_segsum', 'rs_sorted_sqnorm_batch', 'rs_sorted_adam_batch',
-                'rs_sorted_sqnorm_batch_dense', 'rs_sorted_adam_batch_dense')
+LAZY_ROW_BYTES['rs_sorted_catchup_batch'] = LAZY_ROW_BYTES['rs_sorted_catchup']  # round 6: one launch per gather
+LAZY_ENTRIES = ('rs_lookup_sort', 'rs_sorted_catchup', 'rs_sorted_catchup_batch', 'rs_segsum',
+                'rs_segsum_batch', 'rs_sorted_sqnorm_batch', 'rs_sorted_adam_batch', 'rs_sorted_sqnorm_batch_dense',
+                'rs_sorted_adam_batch_dense')
 
 
 def optimizer_roofline(summ, rows, flat_numel, dense_numel, ms_step, args, B, name, dtype, zipf, hard_negatives):
@@ -746,17 +748,18 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
     # catchup_gather: the lazy tables' forward unit -- the catch-up that brings a call's distinct rows
     # current, then the gather that reads them (priced by their own algorithmic bytes, both kernels'
     # event time)
-    groups = {'rs_gather_fwd': ('rs_gather_fwd', 'rs_gather_fwd_lazy'), 'table_grad': ('rs_gather_bwd', 'rs_segsum'),
-              'catchup_gather': ('rs_sorted_catchup', 'rs_gather_fwd', 'rs_gather_fwd_lazy')}
-    if lazy_rows:
-        summ = dict(summ)
-        if 'rs_sorted_catchup' in summ:  # priced per distinct row (LAZY_ROW_BYTES), as optimizer_roofline
-            summ['rs_sorted_catchup'] = dict(summ['rs_sorted_catchup'],
-                                             bytes=LAZY_ROW_BYTES['rs_sorted_catchup'](lazy_rows))
+    groups = {'rs_gather_fwd': ('rs_gather_fwd', 'rs_gather_fwd_lazy'),
+              'table_grad': ('rs_gather_bwd', 'rs_segsum', 'rs_segsum_batch'),
+              'catchup_gather': ('catchup', 'rs_gather_fwd', 'rs_gather_fwd_lazy')}
+    gs = dict(summ)  # the groups' entries, with the forward catch-up merged
+    cu = [gs[k] for k in ('rs_sorted_catchup', 'rs_sorted_catchup_batch') if k in gs]
+    if cu and lazy_rows:  # the forward catch-up (one launch per gather since round 6), priced per
+        # distinct row (LAZY_ROW_BYTES), as optimizer_roofline
+        gs['catchup'] = {'ms': sum(x['ms'] for x in cu), 'bytes': LAZY_ROW_BYTES['rs_sorted_catchup'](lazy_rows)}
     for k, members in groups.items():
-        if k == 'catchup_gather' and 'rs_sorted_catchup' not in summ:
+        if k == 'catchup_gather' and 'catchup' not in gs:
             continue
-        ms = [summ[m] for m in members if m in summ]
+        ms = [gs[m] for m in members if m in gs]
         g = {'ms': sum(x['ms'] for x in ms), 'bytes': sum(x['bytes'] for x in ms)}
         if g['ms'] > 0:
             gbs = g['bytes'] / (g['ms'] * 1e-3) / 1e9
@@ -772,7 +775,7 @@ def run_workload(args, name, dtype, zipf, hard_negatives, rank, world, dev, cpu_
                 # modelled with every distinct row (batches - 1) steps stale, the bench's cycle
                 el_steps = sum(D * r for D, _, r in lazy_rows) / 3 * max(args.batches - 1, 0)
                 valu_ms = el_steps * 34.0 / 64 / (1024 * 2.4e9) * 1e3
-                ms_c = summ['rs_sorted_catchup']['ms'] / 3
+                ms_c = gs['catchup']['ms'] / 3
                 gather_roof[k]['catchup_valu_model'] = {
                     'element_steps_per_step': round(el_steps), 'valu_bound_ms': round(valu_ms, 4),
                     'catchup_ms_per_step': round(ms_c, 4), 'frac': round(valu_ms / ms_c, 4) if ms_c > 0 else None,

@@ -102,6 +102,13 @@ def _tower_wgrad_work(a):
     return fl, by
 
 
+def _segsum_batch_work(a):
+    import ctypes as C
+    from . import _hip
+    arr, D = C.cast(a[0], C.POINTER(_hip.SegsumCall)), a[2]
+    return 0.0, sum(arr[i].n * D * 4.0 + arr[i].n / arr[i].bag * D * 4.0 + arr[i].n * 4.0 for i in range(a[1]))
+
+
 def _adam_work(a):
     n = a[4]
     return 12.0 * n, 28.0 * n
@@ -207,6 +214,7 @@ WORK = {
     # ids) like the scatter it replaces; the per-row catch-up / Adam / sqnorm work depends on the
     # device-side distinct-row count and is timed only
     'rs_lookup_sort': lambda a: (0.0, a[2] * a[3] * (a[1] + 8.0)),
+    'rs_segsum_batch': _segsum_batch_work,
     'rs_segsum': lambda a: (0.0, a[2] * a[8] * 4.0 + a[2] / a[3] * a[8] * 4.0 + a[2] * 4.0),
 }
 
