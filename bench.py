@@ -70,7 +70,7 @@ def parse():
                     help='ranks (one process per GPU). Without torchrun\'s WORLD_SIZE, N > 1 makes this '
                          'process a launcher of N rank processes (launch_ranks); under torchrun it must '
                          'equal WORLD_SIZE')
-    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--steps', type=int, default=100)  # 100 x 1.24 ms at C2: averages out the box's step-to-step noise
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--config', default='c2')
     ap.add_argument('--batch', type=int, default=None, help='per-GPU batch (default: config)')
