@@ -26,3 +26,48 @@ def _release_device_memory():
     if torch.cuda.is_initialized():
         gc.collect()
         torch.cuda.empty_cache()
+
+
+# Heartbeat for long tests (the C5 configured-batch oracle test runs its CPU oracle for minutes
+# with its output captured): a daemon thread reports, every 60 s of one test, the test's id and
+# elapsed time on the terminal and in gpurun_out/pytest_heartbeat.txt, so a run watched for
+# silence is not taken for a hung one.
+import threading  # noqa: E402
+import time  # noqa: E402
+
+_HB = {'test': None, 't0': 0.0, 'tr': None}
+
+
+def _heartbeat():
+    path = os.path.join(ROOT, 'gpurun_out', 'pytest_heartbeat.txt')
+    while True:
+        time.sleep(60)
+        test, t0 = _HB['test'], _HB['t0']
+        if test is None or time.time() - t0 < 55:
+            continue
+        msg = f'[heartbeat] {test} running {time.time() - t0:.0f} s'
+        try:
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            with open(path, 'a') as f:
+                f.write(msg + '\n')
+        except OSError:
+            pass
+        tr = _HB['tr']
+        if tr is not None:
+            try:
+                tr.write_line(msg)
+            except Exception:  # the reporter is not thread-safe; the file carries the beat
+                pass
+
+
+def pytest_sessionstart(session):
+    _HB['tr'] = session.config.pluginmanager.get_plugin('terminalreporter')
+    threading.Thread(target=_heartbeat, name='pytest-heartbeat', daemon=True).start()
+
+
+def pytest_runtest_logstart(nodeid, location):
+    _HB['test'], _HB['t0'] = nodeid, time.time()
+
+
+def pytest_runtest_logfinish(nodeid, location):
+    _HB['test'] = None
